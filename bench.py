@@ -1,0 +1,206 @@
+#!/usr/bin/env python
+"""Headline benchmark: buyers encoded+retrieved/sec @ k=100 over a 1M x 384 catalog
+(BASELINE.json metric, configs[2]) on MI355X, with the HBM/MFMA roofline of the dominant
+kernel and the CPU baseline beside it.
+
+One step = one pass of the hot path over one batch of synthetic buyers, inputs resident in
+HBM before the timed region:
+  Mode B buyer encode (gather the 20 history rows of each buyer from the resident item
+  table + weighted average + F.normalize; EmbeddingEncoder.encode_buyer with the item rows
+  gathered instead of re-encoded)  ->  query re-normalisation (VectorDatabase.retrieve_batch)
+  ->  exact inner-product top-k (fused HIP scan + top-k).
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): the catalog is
+row-sharded over the ranks (north_star / SURVEY 8(e)); each rank encodes its own buyers,
+queries are all-gathered over RCCL, every rank scans its shard for all queries, per-shard
+top-k lists go back to the buyer's owner with one all-to-all and are merged there.  Per-rank
+work (buyers x catalog rows scanned) is constant in N: "scaling": "weak".
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "two-tower-model-v2_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from twotower import _lib, kernels  # noqa: E402
+
+F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X dense f32 MFMA (MI355X_MICROARCH.md)
+HBM_PEAK_GBPS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--catalog", type=int, default=1_000_000)
+    p.add_argument("--buyers", type=int, default=10_000, help="buyers per rank per step")
+    p.add_argument("--hist", type=int, default=20)
+    p.add_argument("--k", type=int, default=100)
+    p.add_argument("--dim", type=int, default=384)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-single", type=int, default=32)
+    p.add_argument("--cpu-batch", type=int, default=512)
+    return p.parse_args()
+
+
+def event_mix(gen, shape, device):
+    u = torch.rand(shape, generator=gen, device=device)
+    w = torch.ones(shape, device=device)
+    w[u > 0.75] = 5.0
+    w[u > 0.92] = 10.0
+    return w
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if a.gpus != world:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    N, E, B, S, K = a.catalog, a.dim, a.buyers, a.hist, a.k
+    ep = _lib.padded_dim(E)
+    # ---- synthetic inputs (identical catalog on every rank; buyers differ per rank)
+    g = torch.Generator(device=dev).manual_seed(2)
+    table = torch.zeros((N, ep), device=dev)
+    table[:, :E] = torch.randn((N, E), generator=g, device=dev)
+    kernels.l2norm_rows(table, E, _lib.TT_NORM_MAX_EPS, out=table)  # ItemTower outputs (F.normalize)
+    lo, hi = rank * N // world, (rank + 1) * N // world
+    shard = torch.empty((hi - lo, ep), device=dev)
+    kernels.l2norm_rows(table[lo:hi], E, _lib.TT_NORM_ADD_EPS, out=shard)  # build_index
+    gb = torch.Generator(device=dev).manual_seed(3 + rank)
+    hist = torch.randint(0, N, (B, S), generator=gb, device=dev, dtype=torch.int64)
+    w = event_mix(gb, (B, S), dev)
+
+    q = torch.empty((B, ep), device=dev)
+    qall = torch.empty((world * B, ep), device=dev) if world > 1 else q
+    nq = world * B
+    ws = torch.empty(kernels.scan_workspace_bytes(hi - lo, E, nq, K), dtype=torch.uint8, device=dev)
+    s_shard = torch.empty((nq, K), device=dev)
+    i_shard = torch.empty((nq, K), dtype=torch.int64, device=dev)
+    if world > 1:
+        s_recv = torch.empty((world, B, K), device=dev)
+        i_recv = torch.empty((world, B, K), dtype=torch.int64, device=dev)
+    L = _lib.lib()
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        kernels.gather_weighted_avg_l2(table, E, hist, w, out=q)
+        kernels.l2norm_rows(q, E, _lib.TT_NORM_ADD_EPS, out=q)
+        if world > 1:
+            dist.all_gather_into_tensor(qall, q)
+        e0, e1 = (ev if ev else (None, None))
+        _lib.check(L.tt_scan_topk_f32_timed(
+            shard.data_ptr(), hi - lo, E, shard.stride(0), lo,
+            qall.data_ptr(), nq, qall.stride(0), K, s_shard.data_ptr(), i_shard.data_ptr(),
+            ws.data_ptr(), ws.numel(), stream.cuda_stream,
+            e0.cuda_event if e0 is not None else None, e1.cuda_event if e1 is not None else None),
+            "scan")
+        if world > 1:
+            dist.all_to_all_single(s_recv.view(world * B, K), s_shard)
+            dist.all_to_all_single(i_recv.view(world * B, K), i_shard)
+            return kernels.merge_topk(s_recv, i_recv, K)
+        return s_shard, i_shard
+
+    for _ in range(a.warmup):
+        step()
+    evs = []
+    for _ in range(a.steps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)  # materialise the hipEvent handles; the ABI re-records them
+        e1.record(stream)
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        out = step(evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    dt = t1 - t0
+    scan_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps
+    if world > 1:
+        t = torch.tensor([dt, scan_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt, scan_ms = t.tolist()
+    ms_per_step = dt / a.steps * 1e3
+    value = world * B / (dt / a.steps)
+
+    # dominant kernel: k_scan_topk_f32, per launch: nq queries x (hi-lo) rows x E
+    rows = hi - lo
+    flops = 2.0 * nq * rows * E
+    alg_bytes = 4.0 * rows * ep + 4.0 * nq * ep + nq * K * 8.0 * 1.0  # catalog once, queries, lists
+    achieved_tf = flops / (scan_ms * 1e-3) / 1e12
+    result = {
+        "metric": "buyers encoded+retrieved/sec @ k=100, 1M x 384 catalog",
+        "value": value,
+        "unit": "buyers/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (random-normal item embeddings, uniform 20-event histories, event mix 0.75/0.17/0.08)",
+        "config": {
+            "workload": "configs[2]: 1M x 384 catalog, 10k buyers/rank x 20 events, weighted-avg, "
+                        "Mode B (history rows gathered), k=100",
+            "catalog_rows": N, "dim": E, "buyers_per_rank": B, "history": S, "k": K,
+            "parallelism": f"catalog row-shard x{world}" + (" + RCCL all-gather(queries) / all-to-all(top-k)" if world > 1 else ""),
+        },
+        "roofline": {
+            "kernel": "k_scan_topk_f32",
+            "bound": "mfma",
+            "achieved": achieved_tf,
+            "peak": F32_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved_tf / F32_MFMA_PEAK_TFLOPS,
+            "traffic": None,
+            "scan_ms": scan_ms,
+            "flops_per_launch": flops,
+            "algorithmic_bytes_per_launch": alg_bytes,
+            "achieved_hbm_gbps": alg_bytes / (scan_ms * 1e-3) / 1e9,
+        },
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        sys.path.insert(0, ROOT)
+        from oracle import cpu_baseline
+
+        del ws
+        torch.cuda.empty_cache()
+        hist_np = hist.cpu().numpy()
+        w_np = w.cpu().numpy()
+        table_np = table[:, :E].cpu().numpy()
+        cat_np = shard[:, :E].cpu().numpy()
+        result["cpu_baseline"] = cpu_baseline.run(table_np, cat_np, hist_np, w_np, K,
+                                                  single_buyers=a.cpu_single,
+                                                  batch_buyers=a.cpu_batch)
+        result["cpu_baseline"]["gpu_over_cpu_single"] = value / result["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,122 @@
+/*
+ * twotower_hip.h -- C ABI of libtwotower_hip.so, the MI355X (gfx950) hot path of the
+ * two-tower retrieval stack.
+ *
+ * The reference (HeikalPro/two-tower-model-v2) has no FFI of its own: its hot path is
+ * Python that calls third-party numerics (faiss-cpu IndexFlatIP, sentence-transformers,
+ * torch).  Every entry point below replaces one of those numeric calls; the reference
+ * interface each replaces is cited (file:line under the reference root).  The Python
+ * mirror of the reference classes (two-tower-model-v2_amd/twotower/) binds these with
+ * ctypes; INTEGRATION.md shows the binding a maintainer of the reference would add.
+ *
+ * Conventions
+ *   - All pointers are DEVICE pointers (hipMalloc / torch CUDA tensors), caller-owned,
+ *     row-major, float32 unless stated.  `ld_*` = leading dimension (elements per row).
+ *   - Every call is asynchronous on `stream` (a hipStream_t passed as void*); no call
+ *     allocates device memory or synchronises.  Scratch comes from a caller workspace
+ *     whose size is queried first.
+ *   - Return value: TT_OK (0) or a negative TT_ERR_* code; tt_last_error() returns a
+ *     thread-local message for the last failing call on the calling thread.
+ *   - Numerics: every kernel follows a CANONICAL float32 evaluation order that the CPU
+ *     oracle (oracle/tt_oracle.c) restates, so GPU and oracle agree bit-for-bit where
+ *     the doc says "bit-exact".  See DESIGN.md "Canonical numerics".
+ */
+#ifndef TWOTOWER_HIP_H
+#define TWOTOWER_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TT_OK 0
+#define TT_ERR_INVALID (-1)     /* bad argument (shape, k, null pointer)              */
+#define TT_ERR_LAUNCH (-2)      /* HIP launch / runtime error                         */
+#define TT_ERR_UNSUPPORTED (-3) /* configuration outside what the kernels implement   */
+#define TT_ERR_WORKSPACE (-4)   /* workspace too small                                */
+
+#define TT_NORM_ADD_EPS 0 /* x / (||x|| + 1e-8)      vector_db.py:44-45,152-153,189-190 */
+#define TT_NORM_MAX_EPS 1 /* x / max(||x||, 1e-12)   F.normalize: item_tower.py:209,
+                                                     buyer_tower.py:66,99                */
+
+/* Library version (major*10000 + minor*100 + patch) and last error (thread-local). */
+int tt_version(void);
+const char* tt_last_error(void);
+
+/* ---------------------------------------------------------------------------------
+ * Row L2 normalisation.  ||x|| is numpy's np.linalg.norm(axis=1) on float32, i.e.
+ * sqrtf(pairwise_sum(x*x)) with numpy's 8-way-unrolled pairwise tree (bit-exact).
+ *   mode TT_NORM_ADD_EPS replaces  VectorDatabase.build_index  src/inference/vector_db.py:43-45
+ *                        and the query re-normalisation in retrieve / retrieve_batch
+ *                        vector_db.py:151-153, 188-190.
+ *   mode TT_NORM_MAX_EPS replaces  F.normalize(p=2, dim=1)  src/models/item_tower.py:209,
+ *                        src/models/buyer_tower.py:66,99.
+ * Also writes an optional bf16 copy (y_bf16 may be NULL; ld = ld_y).  In-place (x == y) is allowed.
+ * --------------------------------------------------------------------------------- */
+int tt_l2norm_rows_f32(const float* x, int64_t n, int32_t d, int64_t ld_x, float* y,
+                       int64_t ld_y, uint16_t* y_bf16, int32_t mode, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Exact inner-product top-k over a row-major catalog shard.
+ * Replaces faiss.IndexFlatIP.search  (src/inference/vector_db.py:160 retrieve,
+ * vector_db.py:197 retrieve_batch).  Scores are float32 dot products evaluated in the
+ * canonical fma order (bit-exact vs the oracle); results sorted by score descending,
+ * ties broken by LOWER global row (row_base + local row).  NaN scores are never
+ * returned; if fewer than k finite scores exist the tail is (-inf, -1).
+ *   db       [n, ld_db]  normalised catalog shard (ld_db >= d, multiple of 4, and the
+ *                        padding columns d..ld_db-1 must be zero)
+ *   q        [nq, ld_q]  normalised queries (ld_q >= d; same zero padding)
+ *   out_*    [nq, k]     k <= n is the caller's job (reference clamps, vector_db.py:159,196)
+ * workspace: size from tt_scan_workspace_bytes (same n, d, nq, k).
+ * --------------------------------------------------------------------------------- */
+int32_t tt_padded_dim(int32_t d); /* row length the scan reads: 64,128,256,384,512,768; -1 if d > 768 */
+int tt_scan_workspace_bytes(int64_t n, int32_t d, int32_t nq, int32_t k, int64_t* bytes);
+int tt_scan_topk_f32(const float* db, int64_t n, int32_t d, int64_t ld_db, int64_t row_base,
+                     const float* q, int32_t nq, int64_t ld_q, int32_t k, float* out_score,
+                     int64_t* out_idx, void* workspace, int64_t workspace_bytes,
+                     void* stream);
+
+/* Same as tt_scan_topk_f32, and records ev_start / ev_stop (hipEvent_t, may be NULL) on
+ * `stream` immediately around the scan kernel (not the slab merge), so a benchmark can time
+ * the dominant kernel alone. */
+int tt_scan_topk_f32_timed(const float* db, int64_t n, int32_t d, int64_t ld_db,
+                           int64_t row_base, const float* q, int32_t nq, int64_t ld_q, int32_t k,
+                           float* out_score, int64_t* out_idx, void* workspace,
+                           int64_t workspace_bytes, void* stream, void* ev_start,
+                           void* ev_stop);
+
+/* Merge n_lists per-shard top-k lists [n_lists, nq, k_in] (each sorted, global row ids)
+ * into [nq, k]; same ordering rule.  Used after the RCCL all-gather of per-shard top-k
+ * (multi-GPU row sharding). */
+int tt_topk_merge_f32(const float* in_score, const int64_t* in_idx, int32_t n_lists,
+                      int32_t nq, int32_t k_in, int32_t k, float* out_score,
+                      int64_t* out_idx, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Buyer tower.
+ * tt_weighted_avg_l2_f32   replaces BuyerTower.weighted_average  src/models/buyer_tower.py:43-68
+ *   items [b, s, d], w [b, s] -> out [b, ld_out]:  w/(sum w + 1e-8), sum_s x*w, F.normalize.
+ * tt_gather_weighted_avg_l2_f32  same, with the history rows gathered from a resident
+ *   item-embedding table by index (Mode B of EmbeddingEncoder.encode_buyer,
+ *   src/inference/encoder.py:286-303): hist [b, s] int64 row ids into table [n_table, ld_table];
+ *   an id < 0 marks padding (weight must be 0 there).
+ * tt_attn_agg_l2_f32       replaces BuyerTower.attention_aggregation buyer_tower.py:70-101:
+ *   a = W2.relu(W1.x + b1) + b2 ; softmax_s(a*w) ; sum_s alpha*x ; F.normalize.
+ *   W1 [h, d] (nn.Linear weight layout), b1 [h], W2 [h] (Linear(h,1).weight), b2 [1].
+ * --------------------------------------------------------------------------------- */
+int tt_weighted_avg_l2_f32(const float* items, int64_t b, int32_t s, int32_t d,
+                           const float* w, float* out, int64_t ld_out, void* stream);
+int tt_gather_weighted_avg_l2_f32(const float* table, int64_t n_table, int64_t ld_table,
+                                  int32_t d, const int64_t* hist, const float* w,
+                                  int64_t b, int32_t s, float* out, int64_t ld_out,
+                                  void* stream);
+int tt_attn_agg_l2_f32(const float* items, int64_t b, int32_t s, int32_t d, const float* w,
+                       const float* W1, const float* b1, int32_t h, const float* W2,
+                       const float* b2, float* out, int64_t ld_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TWOTOWER_HIP_H */

@@ -1,0 +1,84 @@
+"""CPU baseline for bench.py (TEST/MEASUREMENT INFRASTRUCTURE -- never the product).
+
+A CPU port of the reference's hot path for BASELINE.json configs[2] (Mode B buyer encode +
+exact top-k), run on the host cores of the GPU box:
+  buyer encode   BuyerTower.weighted_average   src/models/buyer_tower.py:58-66  (torch CPU)
+  query norm     VectorDatabase.retrieve      src/inference/vector_db.py:151-153 (numpy)
+  exact top-k    faiss IndexFlatIP.search     vector_db.py:160 -- faiss-cpu is absent on
+                 this image, so the port is its algorithm: BLAS sgemm of the scores
+                 (torch CPU matmul) + per-query top-k selection.
+Two variants:
+  (i)  reference-faithful: one buyer at a time, nq = 1, as /retrieve (server.py:241-244)
+       and Evaluator (metrics.py:425-429) call it;
+  (ii) batched: retrieve_batch over query blocks (vector_db.py:171-209; no caller in the repo).
+If ``import faiss`` works on the host, the faiss IndexFlatIP itself is timed instead
+(kind "reference").
+"""
+from __future__ import annotations
+
+import os
+import time
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+def _encode(table: torch.Tensor, hist: np.ndarray, w: np.ndarray) -> np.ndarray:
+    x = table[torch.from_numpy(hist)]                      # [b, s, d] gathered history
+    wt = torch.from_numpy(w).unsqueeze(-1)
+    nw = wt / (wt.sum(dim=1, keepdim=True) + 1e-8)
+    return F.normalize((x * nw).sum(dim=1), p=2, dim=1).numpy()
+
+
+def _norm(q: np.ndarray) -> np.ndarray:
+    return (q / (np.linalg.norm(q, axis=1, keepdims=True) + 1e-8)).astype(np.float32)
+
+
+def run(table_np: np.ndarray, catalog_np: np.ndarray, hist: np.ndarray, w: np.ndarray, k: int,
+        single_buyers: int = 16, batch_buyers: int = 256, threads: int | None = None) -> dict:
+    threads = threads or int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    table = torch.from_numpy(table_np)
+    cat = torch.from_numpy(catalog_np)
+    try:
+        import faiss  # noqa: F401
+        index = faiss.IndexFlatIP(catalog_np.shape[1])
+        index.add(catalog_np)
+        search = lambda q, kk: index.search(q, kk)  # noqa: E731
+        kind = "reference"
+    except Exception:
+        def search(q, kk):
+            s = torch.from_numpy(q) @ cat.T
+            v, i = torch.topk(s, kk, dim=1)
+            return v.numpy(), i.numpy()
+        kind = "port"
+
+    # warm-up (one buyer each way)
+    search(_norm(_encode(table, hist[:1], w[:1])), k)
+
+    # (i) reference-faithful: encode_buyer + retrieve per buyer, nq = 1
+    t0 = time.perf_counter()
+    for b in range(single_buyers):
+        q = _norm(_encode(table, hist[b:b + 1], w[b:b + 1]))
+        search(q, k)
+    t_single = time.perf_counter() - t0
+
+    # (ii) batched retrieve_batch in blocks of 64 queries
+    nb = batch_buyers
+    t0 = time.perf_counter()
+    q = _norm(_encode(table, hist[:nb], w[:nb]))
+    for a in range(0, nb, 64):
+        search(q[a:a + 64], k)
+    t_batch = time.perf_counter() - t0
+    return {
+        "value": single_buyers / t_single,
+        "unit": "buyers/s",
+        "cores": threads,
+        "kind": kind,
+        "sample": (f"(i) {single_buyers} buyers one at a time (nq=1) and (ii) {nb} buyers "
+                   f"batched 64/query-block, Mode B weighted-avg encode, exact top-{k} over "
+                   f"{catalog_np.shape[0]}x{catalog_np.shape[1]} f32, torch-CPU sgemm+topk"),
+        "batched_value": nb / t_batch,
+        "seconds": t_single + t_batch,
+    }

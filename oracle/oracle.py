@@ -1,0 +1,164 @@
+"""CPU oracle for the two-tower hot path -- TEST INFRASTRUCTURE, never the product.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module.  It wraps oracle/tt_oracle.c (canonical float32 restatement, bit-exact with the HIP
+kernels) and adds float64 restatements of the reference semantics:
+
+* ``flatip_search_f64``  faiss.IndexFlatIP.search as used by VectorDatabase.retrieve /
+  retrieve_batch (reference src/inference/vector_db.py:159-160, 196-197): exact inner
+  product, k clamped by the caller, descending scores.  faiss-cpu (>=1.7.4,
+  requirements.txt:26) is not installed offline; this restates its published semantics.
+* ``vector_db_normalize``  the reference's own numpy expression (vector_db.py:44-45):
+  ``x / (np.linalg.norm(x, axis=1, keepdims=True) + 1e-8)`` -- executed with numpy itself.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "_build", "libtt_oracle.so")
+_lib = None
+
+_f32p = ctypes.POINTER(ctypes.c_float)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _SO
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = ctypes.CDLL(_SO)
+        L.tto_norm.restype = ctypes.c_float
+        L.tto_norm.argtypes = [_f32p, _i64]
+        L.tto_dot.restype = ctypes.c_float
+        L.tto_dot.argtypes = [_f32p, _f32p, _i32]
+        L.tto_l2norm_rows.restype = None
+        L.tto_l2norm_rows.argtypes = [_f32p, _i64, _i32, _i64, _f32p, _i64, _i32]
+        L.tto_scan_topk.restype = None
+        L.tto_scan_topk.argtypes = [_f32p, _i64, _i32, _i64, _i64, _f32p, _i32, _i64, _i32,
+                                    _f32p, _i64p]
+        L.tto_weighted_avg_l2.restype = None
+        L.tto_weighted_avg_l2.argtypes = [_f32p, _f32p, _i64, _i64p, _i64, _i32, _i32, _f32p,
+                                          _f32p, _i64]
+        L.tto_attn_agg_l2.restype = None
+        L.tto_attn_agg_l2.argtypes = [_f32p, _i64, _i32, _i32, _f32p, _f32p, _f32p, _i32,
+                                      _f32p, _f32p, _f32p, _i64]
+        _lib = L
+    return _lib
+
+
+def _fp(a):
+    return a.ctypes.data_as(_f32p) if a is not None else None
+
+
+def _c32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+# --------------------------------------------------------------------------- canonical f32
+def l2norm_rows(x: np.ndarray, mode: int) -> np.ndarray:
+    """mode 0: x/(||x||+1e-8) (vector_db.py:44-45); mode 1: F.normalize (item_tower.py:209)."""
+    x = _c32(x)
+    n, d = x.shape
+    y = np.empty_like(x)
+    lib().tto_l2norm_rows(_fp(x), n, d, d, _fp(y), d, mode)
+    return y
+
+
+def dot(x: np.ndarray, q: np.ndarray) -> float:
+    x, q = _c32(x), _c32(q)
+    return float(lib().tto_dot(_fp(x), _fp(q), x.shape[0]))
+
+
+def scan_topk(db: np.ndarray, q: np.ndarray, k: int, row_base: int = 0):
+    """Canonical-f32 exact top-k; bit-exact reference for tt_scan_topk_f32."""
+    db, q = _c32(db), _c32(q)
+    n, d = db.shape
+    nq = q.shape[0]
+    s = np.empty((nq, k), np.float32)
+    i = np.empty((nq, k), np.int64)
+    lib().tto_scan_topk(_fp(db), n, d, d, row_base, _fp(q), nq, d, k, _fp(s),
+                        i.ctypes.data_as(_i64p))
+    return s, i
+
+
+def weighted_avg_l2(items: np.ndarray, w: np.ndarray) -> np.ndarray:
+    items, w = _c32(items), _c32(w)
+    b, s, d = items.shape
+    out = np.empty((b, d), np.float32)
+    lib().tto_weighted_avg_l2(_fp(items), None, 0, None, b, s, d, _fp(w), _fp(out), d)
+    return out
+
+
+def gather_weighted_avg_l2(table: np.ndarray, hist: np.ndarray, w: np.ndarray) -> np.ndarray:
+    table, w = _c32(table), _c32(w)
+    hist = np.ascontiguousarray(hist, dtype=np.int64)
+    b, s = hist.shape
+    d = table.shape[1]
+    out = np.empty((b, d), np.float32)
+    lib().tto_weighted_avg_l2(None, _fp(table), d, hist.ctypes.data_as(_i64p), b, s, d, _fp(w),
+                              _fp(out), d)
+    return out
+
+
+def attn_agg_l2(items, w, W1, b1, W2, b2) -> np.ndarray:
+    items, w, W1, b1, W2, b2 = map(_c32, (items, w, W1, b1, W2, b2))
+    b, s, d = items.shape
+    h = W1.shape[0]
+    out = np.empty((b, d), np.float32)
+    lib().tto_attn_agg_l2(_fp(items), b, s, d, _fp(w), _fp(W1), _fp(b1), h,
+                          _fp(W2.reshape(-1)), _fp(b2.reshape(-1)), _fp(out), d)
+    return out
+
+
+# --------------------------------------------------------------------------- reference f64
+def vector_db_normalize(x: np.ndarray) -> np.ndarray:
+    """The reference's expression, vector_db.py:44-45 / 152-153 / 189-190, run by numpy."""
+    norms = np.linalg.norm(x, axis=1, keepdims=True)
+    return (x / (norms + 1e-8)).astype(np.float32)
+
+
+def flatip_search_f64(db: np.ndarray, q: np.ndarray, k: int):
+    """fp64 restatement of IndexFlatIP.search: scores desc, ties -> lower row."""
+    s = np.asarray(q, np.float64) @ np.asarray(db, np.float64).T
+    order = np.lexsort((np.broadcast_to(np.arange(db.shape[0]), s.shape), -s), axis=1)[:, :k]
+    return np.take_along_axis(s, order, 1), order.astype(np.int64)
+
+
+def topk_parity_f64(gpu_s, gpu_i, db, q, k, score_tol=1e-5, gap=1e-6):
+    """SURVEY.md H0 parity rule (ii) against the fp64 oracle.  Returns list of problems."""
+    ref_s, ref_i = flatip_search_f64(db, q, k)
+    full = np.asarray(q, np.float64) @ np.asarray(db, np.float64).T
+    problems = []
+    for qi in range(q.shape[0]):
+        got = full[qi, gpu_i[qi]]
+        if np.max(np.abs(gpu_s[qi].astype(np.float64) - got)) > score_tol:
+            problems.append((qi, "score"))
+            continue
+        # ids must match at every rank whose fp64 gap to neighbours exceeds `gap`
+        rs = ref_s[qi]
+        kth = rs[-1]
+        nxt = np.sort(full[qi])[::-1][k] if full.shape[1] > k else -np.inf
+        for r in range(k):
+            lo = rs[r + 1] if r + 1 < k else nxt
+            hi = rs[r - 1] if r > 0 else np.inf
+            if hi - rs[r] > gap and rs[r] - lo > gap and gpu_i[qi, r] != ref_i[qi, r]:
+                problems.append((qi, f"id@{r}"))
+                break
+        # set equality outside the near-tie band at the k/k+1 boundary
+        sure = set(ref_i[qi][rs > kth + gap].tolist())
+        if not sure.issubset(set(gpu_i[qi].tolist())):
+            problems.append((qi, "set"))
+    return problems

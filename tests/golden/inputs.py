@@ -1,0 +1,159 @@
+"""Deterministic inputs for the golden fixtures (seeded numpy PCG64 streams).
+
+Both tests/golden/make_golden.py (reference side) and the tests regenerate inputs here;
+the fixtures store a sha256 of the inputs so a drifting generator is detected.
+"""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+
+EVENT_MIX = (np.array([1.0, 5.0, 10.0], np.float32), np.array([0.75, 0.17, 0.08]))
+
+
+def sha(*arrays) -> str:
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def event_weights(rng, shape):
+    vals, p = EVENT_MIX
+    return vals[rng.choice(3, size=shape, p=p)].astype(np.float32)
+
+
+# ----------------------------------------------------------------------------- buyer tower
+BUYER_CASES = {
+    "wavg_reftest": dict(method="weighted_avg", E=384, B=2, S=5, seed=11, w="reftest"),
+    "wavg_b8_s20": dict(method="weighted_avg", E=384, B=8, S=20, seed=12),
+    "wavg_s100": dict(method="weighted_avg", E=384, B=4, S=100, seed=13),
+    "wavg_s1": dict(method="weighted_avg", E=384, B=3, S=1, seed=14),
+    "wavg_pad": dict(method="weighted_avg", E=384, B=4, S=20, seed=15, pad=8),
+    "wavg_zero_w": dict(method="weighted_avg", E=384, B=2, S=5, seed=16, w="zero"),
+    "wavg_e768": dict(method="weighted_avg", E=768, B=4, S=20, seed=17),
+    "wavg_scaled": dict(method="weighted_avg", E=384, B=4, S=20, seed=18, scale=1000.0),
+    "wavg_e100": dict(method="weighted_avg", E=100, B=3, S=7, seed=19),
+    "attn_reftest": dict(method="attention", E=384, B=2, S=5, seed=21, w="reftest"),
+    "attn_b8_s20": dict(method="attention", E=384, B=8, S=20, seed=22),
+    "attn_pad": dict(method="attention", E=384, B=4, S=20, seed=23, pad=8),
+    "attn_e768": dict(method="attention", E=768, B=3, S=20, seed=24),
+    "attn_s100": dict(method="attention", E=384, B=2, S=100, seed=25),
+}
+
+
+def buyer_inputs(spec):
+    rng = np.random.default_rng(spec["seed"])
+    B, S, E = spec["B"], spec["S"], spec["E"]
+    items = rng.standard_normal((B, S, E), dtype=np.float32)
+    if "scale" in spec:
+        items *= np.float32(spec["scale"])
+    if spec.get("w") == "reftest":  # reference tests/test_buyer_tower.py:25
+        w = np.array([[1.0, 5.0, 10.0, 1.0, 1.0], [1.0, 1.0, 5.0, 5.0, 1.0]], np.float32)
+    elif spec.get("w") == "zero":
+        w = np.zeros((B, S), np.float32)
+    else:
+        w = event_weights(rng, (B, S))
+    if spec.get("pad"):
+        p = spec["pad"]
+        items[:, S - p:, :] = 0.0
+        w[:, S - p:] = 0.0
+    return items, w
+
+
+def attn_weights(spec):
+    rng = np.random.default_rng(1000 + spec["seed"])
+    E, H = spec["E"], spec.get("H", 128)
+    a, b = 1.0 / np.sqrt(E), 1.0 / np.sqrt(H)
+    W1 = rng.uniform(-a, a, (H, E)).astype(np.float32)
+    b1 = rng.uniform(-a, a, (H,)).astype(np.float32)
+    W2 = rng.uniform(-b, b, (1, H)).astype(np.float32)
+    b2 = rng.uniform(-b, b, (1,)).astype(np.float32)
+    return W1, b1, W2, b2
+
+
+# ----------------------------------------------------------------------------- InfoNCE
+INFONCE_CASES = {
+    "b8_e384": dict(B=8, E=384, N=4, tau=0.07, seed=31),
+    "b64_e768": dict(B=64, E=768, N=4, tau=0.07, seed=32),
+    "b32_e384_t05": dict(B=32, E=384, N=4, tau=0.5, seed=33),
+}
+
+
+def _unit(x):
+    return (x / np.linalg.norm(x, axis=-1, keepdims=True)).astype(np.float32)
+
+
+def infonce_inputs(spec):
+    rng = np.random.default_rng(spec["seed"])
+    B, E, N = spec["B"], spec["E"], spec["N"]
+    return (_unit(rng.standard_normal((B, E), dtype=np.float32)),
+            _unit(rng.standard_normal((B, E), dtype=np.float32)),
+            _unit(rng.standard_normal((B, N, E), dtype=np.float32)))
+
+
+# ----------------------------------------------------------------------------- item head
+BRANDS = ["Acme", "Dubai Gold", "Lazurde", "Damas", "Tiffany"]
+CATEGORIES = ["rings", "necklaces", "bracelets", "engine-oil"]
+
+
+def item_text_embeddings():
+    rng = np.random.default_rng(41)
+    return rng.standard_normal((16, 384), dtype=np.float32) * np.float32(0.3)
+
+
+def item_head_weights(use_cat: bool):
+    """Seeded ItemTower head parameters (names as in the reference module, item_tower.py:58-63,
+    84-97).  Embedding row 0 (<UNK>, padding_idx) stays zero as nn.Embedding initialises it."""
+    rng = np.random.default_rng(42 if use_cat else 43)
+    din = 384 + (128 if use_cat else 0)
+    w = {
+        "projection.0.weight": rng.uniform(-1, 1, (256, din)) / np.sqrt(din),
+        "projection.0.bias": rng.uniform(-1, 1, (256,)) / np.sqrt(din),
+        "projection.3.weight": rng.uniform(-1, 1, (384, 256)) / 16.0,
+        "projection.3.bias": rng.uniform(-1, 1, (384,)) / 16.0,
+    }
+    if use_cat:
+        for name, n in (("brand_embedding.weight", len(BRANDS) + 1),
+                        ("category_embedding.weight", len(CATEGORIES) + 1)):
+            e = rng.standard_normal((n, 64))
+            e[0] = 0.0
+            w[name] = e
+    return {k: v.astype(np.float32) for k, v in w.items()}
+
+
+def item_batch():
+    texts = [f"p#{i}" for i in range(12)]
+    brands = ["Acme", "Damas", None, "Unknown", "Tiffany", "Lazurde", "", "Dubai Gold", "Acme",
+              "Damas", None, "Tiffany"]
+    cats = ["rings", None, "necklaces", "bracelets", "engine-oil", "nope", "rings", "",
+            "bracelets", "rings", "necklaces", None]
+    return texts, brands, cats
+
+
+# ----------------------------------------------------------------------------- flat IP
+FLATIP_CASES = {
+    "n1_k10": dict(N=1, Q=4, k=10, seed=51),
+    "n99_k100": dict(N=99, Q=16, k=100, seed=52),
+    "n100_k100": dict(N=100, Q=16, k=100, seed=53),
+    "n101_k100": dict(N=101, Q=16, k=100, seed=54),
+    "n4096_k1": dict(N=4096, Q=16, k=1, seed=55),
+    "n4096_k10": dict(N=4096, Q=16, k=10, seed=56),
+    "n4096_k100": dict(N=4096, Q=16, k=100, seed=57),
+    "n4096_k1000": dict(N=4096, Q=8, k=1000, seed=58),
+    "dups_k100": dict(N=600, Q=8, k=100, seed=59, dups=True),
+    "e768_k100": dict(N=2000, Q=8, k=100, seed=60, E=768),
+}
+
+
+def flatip_inputs(spec):
+    rng = np.random.default_rng(spec["seed"])
+    E = spec.get("E", 384)
+    x = rng.standard_normal((spec["N"], E), dtype=np.float32)
+    if spec.get("dups"):
+        # every row appears 3 times (exact ties at every score) -> tie order by row index
+        base = x[: spec["N"] // 3]
+        x = np.concatenate([base, base, base])[: spec["N"]].copy()
+    q = rng.standard_normal((spec["Q"], E), dtype=np.float32)
+    return x, q

@@ -1,0 +1,83 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol the header
+declares, and rejects bad arguments before touching the device."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "twotower_hip.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(tt_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def L():
+    from twotower import _lib
+
+    if not os.path.exists(_lib.LIB_PATH):
+        _lib.build()
+    return _lib.lib()
+
+
+def test_header_declares_expected_entry_points():
+    fns = header_functions()
+    for name in ("tt_scan_topk_f32", "tt_topk_merge_f32", "tt_l2norm_rows_f32",
+                 "tt_weighted_avg_l2_f32", "tt_gather_weighted_avg_l2_f32", "tt_attn_agg_l2_f32",
+                 "tt_scan_workspace_bytes", "tt_padded_dim", "tt_last_error", "tt_version"):
+        assert name in fns
+
+
+def test_library_exports_every_header_symbol(L):
+    from twotower import _lib
+
+    for name in header_functions():
+        assert hasattr(L, name), f"{name} declared in include/twotower_hip.h but not exported"
+        assert name in _lib.SIGNATURES, f"{name} has no ctypes signature in _lib.py"
+
+
+def test_version_and_padded_dim(L):
+    assert L.tt_version() >= 100
+    assert [L.tt_padded_dim(d) for d in (1, 64, 65, 100, 384, 385, 768, 769)] == \
+        [64, 64, 128, 128, 384, 512, 768, -1]
+
+
+def test_invalid_arguments_rejected_without_device(L):
+    from twotower._lib import check
+
+    rc = L.tt_scan_topk_f32(None, 0, 384, 384, 0, None, 1, 384, 10, None, None, None, 0, None)
+    assert rc == -1 and b"empty catalog" in L.tt_last_error()
+    rc = L.tt_scan_topk_f32(None, 100, 384, 384, 0, None, 1, 384, 101, None, None, None, 0, None)
+    assert rc == -1 and b"k <= n" in L.tt_last_error()
+    rc = L.tt_scan_topk_f32(None, 100, 900, 900, 0, None, 1, 900, 10, None, None, None, 0, None)
+    assert rc == -3
+    rc = L.tt_l2norm_rows_f32(None, 10, 384, 100, None, 384, None, 0, None)
+    assert rc == -1
+    rc = L.tt_weighted_avg_l2_f32(None, 4, 0, 384, None, None, 384, None)
+    assert rc == -1
+    with pytest.raises(RuntimeError, match="status -1"):
+        check(L.tt_l2norm_rows_f32(None, 1, 384, 100, None, 384, None, 0, None), "norm")
+    b = ctypes.c_int64(0)
+    assert L.tt_scan_workspace_bytes(1_000_000, 384, 10_000, 100, ctypes.byref(b)) == 0
+    assert b.value > 10_000 * 100 * 8
+
+
+def test_product_path_has_no_cpu_fallback():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import numpy as np
+    from twotower import BuyerTower, HipUnavailable, VectorDatabase
+
+    db = VectorDatabase(384)
+    with pytest.raises(HipUnavailable):
+        db.build_index(np.ones((4, 384), np.float32), ["a", "b", "c", "d"])
+    bt = BuyerTower(384, "weighted_avg")
+    with pytest.raises(HipUnavailable):
+        bt(torch.ones(1, 3, 384), torch.ones(1, 3))

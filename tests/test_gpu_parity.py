@@ -1,0 +1,258 @@
+"""Parity of the HIP kernels (through the C ABI) with the CPU oracle and the reference
+fixtures.  Bar: bit-exact for ids and for scores / normalised rows where the
+oracle restates the kernel's canonical order; stated tolerances elsewhere."""
+import numpy as np
+import pytest
+import torch
+
+import inputs as gi
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def K():
+    from twotower import kernels
+
+    return kernels
+
+
+def dev_rows(x, ep=None):
+    from twotower import _lib
+
+    x = np.ascontiguousarray(x, np.float32)
+    ep = ep or _lib.padded_dim(x.shape[1])
+    t = torch.zeros((x.shape[0], ep), dtype=torch.float32, device="cuda")
+    t[:, : x.shape[1]] = torch.from_numpy(x).cuda()
+    return t
+
+
+# ------------------------------------------------------------------ normalisation
+@pytest.mark.parametrize("d", [1, 7, 64, 100, 128, 200, 257, 384, 768, 1000, 1536])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_l2norm_bit_exact(K, oracle_mod, d, mode):
+    rng = np.random.default_rng(d + 7 * mode)
+    x = (rng.standard_normal((257, d)) * rng.uniform(1e-3, 1e3, (257, 1))).astype(np.float32)
+    x[5] = 0.0  # zero row: mode 0 -> 0/(0+1e-8) = 0, mode 1 -> 0/1e-12 = 0
+    xt = torch.from_numpy(x).cuda()
+    ld = d + 3
+    out = torch.full((257, ld), 7.0, device="cuda")
+    K.l2norm_rows(xt, d, mode, out=out)
+    got = out.cpu().numpy()
+    assert np.array_equal(got[:, :d], oracle_mod.l2norm_rows(x, mode))
+    assert np.all(got[:, d:] == 0)  # padding invariant
+    if mode == 0:
+        assert np.array_equal(got[:, :d], oracle_mod.vector_db_normalize(x))
+
+
+def test_l2norm_bf16_copy(K):
+    x = torch.randn(100, 384, device="cuda")
+    out = torch.empty_like(x)
+    ob = torch.empty((100, 384), dtype=torch.bfloat16, device="cuda")
+    K.l2norm_rows(x, 384, 0, out=out, out_bf16=ob)
+    assert torch.equal(ob, out.to(torch.bfloat16))
+
+
+# ------------------------------------------------------------------ scan + top-k
+SCAN_CASES = [
+    # n, d, nq, k
+    (1, 384, 3, 1),
+    (33, 64, 3, 1),
+    (100, 384, 16, 100),
+    (101, 384, 16, 100),
+    (1000, 384, 5, 10),
+    (4096, 384, 16, 100),
+    (4096, 384, 70, 128),
+    (3000, 100, 7, 50),
+    (5000, 768, 8, 100),
+    (20000, 384, 130, 100),
+    (70000, 384, 2, 100),
+    (200000, 384, 1, 100),
+    (4096, 384, 8, 129),
+    (4096, 384, 8, 1000),
+    (2048, 256, 17, 1024),
+]
+
+
+@pytest.mark.parametrize("n,d,nq,k", SCAN_CASES)
+def test_scan_bit_exact_vs_oracle(K, oracle_mod, n, d, nq, k):
+    rng = np.random.default_rng(n * 31 + d + k)
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
+    q = oracle_mod.l2norm_rows(rng.standard_normal((nq, d)).astype(np.float32), 0)
+    s, i = K.scan_topk(dev_rows(x), n, d, dev_rows(q), k)
+    s, i = s.cpu().numpy(), i.cpu().numpy()
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    assert np.array_equal(i, ri)
+    assert np.array_equal(s, rs)
+
+
+def test_scan_ties_and_duplicates(K, oracle_mod):
+    rng = np.random.default_rng(9)
+    base = oracle_mod.l2norm_rows(rng.standard_normal((700, 384)).astype(np.float32), 0)
+    x = np.concatenate([base] * 5)  # every score appears 5x; the lower row must win
+    q = np.concatenate([base[:8], np.zeros((2, 384), np.float32)])  # zero query: all scores 0
+    s, i = K.scan_topk(dev_rows(x), x.shape[0], 384, dev_rows(q), 128)
+    rs, ri = oracle_mod.scan_topk(x, q, 128)
+    assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
+    assert np.array_equal(ri[-1], np.arange(128))  # all-equal scores -> rows 0..127
+
+
+def test_scan_nan_rows_never_returned(K, oracle_mod):
+    rng = np.random.default_rng(10)
+    x = oracle_mod.l2norm_rows(rng.standard_normal((300, 384)).astype(np.float32), 0)
+    x[[3, 50, 299]] = np.nan
+    q = oracle_mod.l2norm_rows(rng.standard_normal((4, 384)).astype(np.float32), 0)
+    s, i = K.scan_topk(dev_rows(x), 300, 384, dev_rows(q), 299)
+    rs, ri = oracle_mod.scan_topk(x, q, 299)
+    assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
+    assert not np.isin(i.cpu().numpy()[:, :297], [3, 50, 299]).any()
+    assert np.all(i.cpu().numpy()[:, 297:] == -1)
+
+
+def test_scan_row_base_and_merge_equal_single_shard(K, oracle_mod):
+    rng = np.random.default_rng(11)
+    n, d, nq, k = 50000, 384, 40, 100
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
+    q = dev_rows(oracle_mod.l2norm_rows(rng.standard_normal((nq, d)).astype(np.float32), 0))
+    cuts = [0, 7000, 19000, 33333, n]
+    parts = [K.scan_topk(dev_rows(x[a:b]), b - a, d, q, k, row_base=a)
+             for a, b in zip(cuts[:-1], cuts[1:])]
+    ms, mi = K.merge_topk(torch.stack([p[0] for p in parts]), torch.stack([p[1] for p in parts]), k)
+    fs, fi = K.scan_topk(dev_rows(x), n, d, q, k)
+    assert torch.equal(mi, fi) and torch.equal(ms, fs)
+
+
+@pytest.mark.parametrize("case", list(gi.FLATIP_CASES))
+def test_vector_db_matches_reference_fixture(golden, oracle_mod, case):
+    """Full reference API path: build_index -> retrieve_batch / retrieve vs the f64
+    restatement of faiss IndexFlatIP over the reference's numpy-normalised catalog."""
+    from twotower import VectorDatabase
+
+    g = golden("flatip.npz")
+    spec = gi.FLATIP_CASES[case]
+    x, q = gi.flatip_inputs(spec)
+    E = x.shape[1]
+    ids = [f"p{j}" for j in range(x.shape[0])]
+    vdb = VectorDatabase(E)
+    vdb.build_index(x, ids)
+    xn = vdb.index.xb[:, :E].cpu().numpy()
+    assert gi.sha(np.ascontiguousarray(xn)) == bytes(g[case + "__xn_sha"]).decode()
+    res = vdb.retrieve_batch(q, k=spec["k"])
+    ref_i, ref_s = g[case + "__i"], g[case + "__s64"]
+    k = ref_i.shape[1]
+    got_i = np.array([[int(pid[1:]) for pid, _ in r] for r in res])
+    got_s = np.array([[sc for _, sc in r] for r in res])
+    assert got_i.shape == (q.shape[0], k)
+    np.testing.assert_allclose(got_s, ref_s, rtol=0, atol=1e-5)
+    assert oracle_mod.topk_parity_f64(got_s.astype(np.float32), got_i, xn, g[case + "__qn"], k) == []
+    one = vdb.retrieve(q[0], k=spec["k"])
+    assert one == res[0]
+
+
+def test_vector_db_errors_and_clamp():
+    from twotower import VectorDatabase
+
+    vdb = VectorDatabase(384)
+    with pytest.raises(ValueError, match="Index not built"):
+        vdb.retrieve(np.ones(384, np.float32))
+    with pytest.raises(ValueError, match="Embedding dimension mismatch: expected 384, got 128"):
+        vdb.build_index(np.ones((3, 128), np.float32), ["a", "b", "c"])
+    vdb.build_index(np.eye(5, 384, dtype=np.float32), list("abcde"))
+    r = vdb.retrieve(np.eye(5, 384, dtype=np.float32)[2], k=50)
+    assert len(r) == 5 and r[0] == ("c", pytest.approx(1.0, abs=1e-6))
+
+
+def test_vector_db_save_load_roundtrip(tmp_path):
+    from twotower import VectorDatabase
+
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((500, 384)).astype(np.float32)
+    ids = [f"prod_{i}" for i in range(500)]
+    a = VectorDatabase(384)
+    a.build_index(x, ids)
+    a.save_index(str(tmp_path / "i.faiss"), str(tmp_path / "ids.npy"), str(tmp_path / "m.json"))
+    b = VectorDatabase(384)
+    b.load_index(str(tmp_path / "i.faiss"), str(tmp_path / "ids.npy"), str(tmp_path / "m.json"))
+    assert torch.equal(a.index.xb, b.index.xb) and b.product_ids == ids
+    q = rng.standard_normal((5, 384)).astype(np.float32)
+    assert a.retrieve_batch(q, 20) == b.retrieve_batch(q, 20)
+
+
+# ------------------------------------------------------------------ buyer tower
+@pytest.mark.parametrize("case", [c for c, s in gi.BUYER_CASES.items()
+                                  if s["method"] == "weighted_avg"])
+def test_weighted_avg_bit_exact_and_vs_reference(K, oracle_mod, golden, case):
+    spec = gi.BUYER_CASES[case]
+    items, w = gi.buyer_inputs(spec)
+    got = K.weighted_avg_l2(torch.from_numpy(items).cuda(), torch.from_numpy(w).cuda()).cpu().numpy()
+    assert np.array_equal(got, oracle_mod.weighted_avg_l2(items, w))
+    np.testing.assert_allclose(got, golden("buyer.npz")[case], rtol=0, atol=1e-6)
+
+
+def test_gather_weighted_avg_bit_exact(K, oracle_mod):
+    rng = np.random.default_rng(12)
+    table = oracle_mod.l2norm_rows(rng.standard_normal((5000, 384)).astype(np.float32), 1)
+    hist = rng.integers(0, 5000, (300, 20))
+    hist[:, 15:] = -1
+    w = gi.event_weights(rng, (300, 20))
+    w[:, 15:] = 0
+    out = K.gather_weighted_avg_l2(dev_rows(table), 384, torch.from_numpy(hist).cuda(),
+                                   torch.from_numpy(w).cuda()).cpu().numpy()
+    assert np.array_equal(out[:, :384], oracle_mod.gather_weighted_avg_l2(table, hist, w))
+
+
+@pytest.mark.parametrize("case", [c for c, s in gi.BUYER_CASES.items()
+                                  if s["method"] == "attention"])
+def test_attention_vs_oracle_and_reference(K, oracle_mod, golden, case):
+    spec = gi.BUYER_CASES[case]
+    items, w = gi.buyer_inputs(spec)
+    W1, b1, W2, b2 = gi.attn_weights(spec)
+    t = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    got = K.attn_agg_l2(t(items), t(w), t(W1), t(b1), t(W2), t(b2)).cpu().numpy()
+    # expf on the device and in libm may differ by an ulp: tolerance, not bit-exact
+    np.testing.assert_allclose(got, oracle_mod.attn_agg_l2(items, w, W1, b1, W2, b2),
+                               rtol=0, atol=1e-6)
+    np.testing.assert_allclose(got, golden("buyer.npz")[case], rtol=0, atol=2e-6)
+
+
+def test_buyer_tower_module_drop_in(golden):
+    """The reference's own unit test (tests/test_buyer_tower.py) run against our module."""
+    from twotower import BuyerTower
+
+    for method in ("weighted_avg", "attention"):
+        bt = BuyerTower(384, method).eval()
+        items = torch.randn(2, 5, 384)
+        weights = torch.tensor([[1.0, 5.0, 10.0, 1.0, 1.0], [1.0, 1.0, 5.0, 5.0, 1.0]])
+        with torch.no_grad():
+            y = bt(items, weights)
+        assert y.shape == (2, 384) and y.device.type == "cpu"
+        assert torch.allclose(y.norm(dim=1), torch.ones(2), atol=1e-5)
+    with pytest.raises(ValueError, match="Unknown aggregation method: mean"):
+        BuyerTower(384, "mean")
+
+
+# ------------------------------------------------------------------ full-size properties
+@pytest.mark.slow
+def test_scan_full_size_properties(K, oracle_mod):
+    """BASELINE config[2] size (1M x 384, k=100): sortedness, exact recomputed scores for the
+    returned rows, and completeness against an fp64 GPU GEMV for a query subset."""
+    n, d, nq, k = 1_000_000, 384, 64, 100
+    g = torch.Generator(device="cuda").manual_seed(2)
+    x = torch.randn((n, d), generator=g, device="cuda")
+    K.l2norm_rows(x, d, 0, out=x)
+    q = torch.randn((nq, d), generator=g, device="cuda")
+    K.l2norm_rows(q, d, 0, out=q)
+    s, i = K.scan_topk(x, n, d, q, k)
+    assert torch.all(s[:, :-1] >= s[:, 1:])
+    assert torch.all((i >= 0) & (i < n))
+    assert all(len(set(r)) == k for r in i.cpu().numpy().tolist())
+    xs = x[i.reshape(-1)].cpu().numpy().reshape(nq, k, d)
+    qs = q.cpu().numpy()
+    for a in range(0, nq, 8):
+        for b in range(0, k, 9):
+            assert oracle_mod.dot(xs[a, b], qs[a]) == s[a, b].item()
+    full = (q[:8].double() @ x.double().T)
+    kth = s[:8, -1].double()
+    missing = (full > kth[:, None] + 1e-6)
+    missing.scatter_(1, i[:8], False)
+    assert not missing.any()

@@ -1,0 +1,200 @@
+// tt_common.hpp -- shared device/host helpers for libtwotower_hip.so (gfx950 only).
+//
+// Canonical float32 numerics shared by every kernel (restated on the CPU in
+// oracle/tt_oracle.c; DESIGN.md "Canonical numerics"):
+//   * pairwise_sumsq: numpy's float32 pairwise sum of x*x (loops_utils.h pairwise_sum:
+//     n<8 sequential, n<=128 eight interleaved accumulators, else split at
+//     n/2 - (n/2)%8).  np.linalg.norm(axis=1) == sqrtf(pairwise_sumsq) bit-for-bit.
+//   * dot (scan score): fmaf chain, d = 16t + 4g + i visited in (t, i, g) order --
+//     exactly what a chain of v_mfma_f32_16x16x4_f32 computes when lane-group g holds
+//     dims 16t+4g..16t+4g+3 (see tt_scan.hip).
+//   * top-k order: score descending, ties -> lower row; NaN never selected.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/twotower_hip.h"
+
+namespace tt {
+
+// ----------------------------------------------------------------------------- errors
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+int check_launch(const char* what);
+
+#define TT_REQUIRE(cond, msg)                                                     \
+  do {                                                                            \
+    if (!(cond)) return ::tt::fail(TT_ERR_INVALID, std::string(__func__) + ": " + (msg)); \
+  } while (0)
+
+// ----------------------------------------------------------------------------- device utils
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Orders LDS traffic between lanes of ONE wave (no workgroup barrier: waves of a block
+// run independent control flow in the scan kernel).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Monotone map float -> uint32 (larger float -> larger key).  -0 is folded to +0 so that
+// equal scores compare equal; NaN maps to 0 (below every finite value and -inf).
+__device__ __forceinline__ uint32_t float_key(float f) {
+  if (f != f) return 0u;
+  f = f + 0.0f;  // -0 -> +0 under round-to-nearest
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key_float(uint32_t k) {
+  uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  return __uint_as_float(u);
+}
+// 64-bit sort key: high word = score key, low word = ~row (lower row wins a tie).
+__device__ __forceinline__ uint64_t make_key(float score, uint32_t row) {
+  return ((uint64_t)float_key(score) << 32) | (uint64_t)(0xffffffffu - row);
+}
+__device__ __forceinline__ float key_score(uint64_t k) { return key_float((uint32_t)(k >> 32)); }
+__device__ __forceinline__ uint32_t key_row(uint64_t k) { return 0xffffffffu - (uint32_t)k; }
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  lo = __shfl_xor(lo, m, 64);
+  hi = __shfl_xor(hi, m, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// numpy pairwise float32 sum of v[i]*v[i] (i < n, stride 1), sequential in ONE lane.
+// Recursion is unrolled into an explicit post-order walk (depth <= 24).
+__device__ __forceinline__ float pw_leaf_sumsq(const float* a, int n) {
+  if (n < 8) {
+    float res = 0.0f;
+    for (int i = 0; i < n; ++i) res = res + __fmul_rn(a[i], a[i]);
+    return res;
+  }
+  float r0 = __fmul_rn(a[0], a[0]), r1 = __fmul_rn(a[1], a[1]);
+  float r2 = __fmul_rn(a[2], a[2]), r3 = __fmul_rn(a[3], a[3]);
+  float r4 = __fmul_rn(a[4], a[4]), r5 = __fmul_rn(a[5], a[5]);
+  float r6 = __fmul_rn(a[6], a[6]), r7 = __fmul_rn(a[7], a[7]);
+  int i = 8;
+  for (; i < n - (n % 8); i += 8) {
+    r0 = r0 + __fmul_rn(a[i + 0], a[i + 0]);
+    r1 = r1 + __fmul_rn(a[i + 1], a[i + 1]);
+    r2 = r2 + __fmul_rn(a[i + 2], a[i + 2]);
+    r3 = r3 + __fmul_rn(a[i + 3], a[i + 3]);
+    r4 = r4 + __fmul_rn(a[i + 4], a[i + 4]);
+    r5 = r5 + __fmul_rn(a[i + 5], a[i + 5]);
+    r6 = r6 + __fmul_rn(a[i + 6], a[i + 6]);
+    r7 = r7 + __fmul_rn(a[i + 7], a[i + 7]);
+  }
+  float res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < n; ++i) res = res + __fmul_rn(a[i], a[i]);
+  return res;
+}
+
+__device__ __forceinline__ float pw_sumsq_serial(const float* a, int n) {
+  if (n <= 128) return pw_leaf_sumsq(a, n);
+  // explicit stack: entries are (start, len) to expand, or len == -1 meaning "combine".
+  int st_s[48], st_n[48];
+  float val[24];
+  int sp = 0, vp = 0;
+  st_s[sp] = 0; st_n[sp] = n; ++sp;
+  while (sp > 0) {
+    --sp;
+    const int s = st_s[sp], len = st_n[sp];
+    if (len < 0) {
+      const float b = val[--vp];
+      const float a0 = val[--vp];
+      val[vp++] = a0 + b;
+    } else if (len <= 128) {
+      val[vp++] = pw_leaf_sumsq(a + s, len);
+    } else {
+      int n2 = len / 2;
+      n2 -= n2 % 8;
+      st_s[sp] = 0; st_n[sp] = -1; ++sp;           // combine after both halves
+      st_s[sp] = s + n2; st_n[sp] = len - n2; ++sp;  // right half (processed second)
+      st_s[sp] = s; st_n[sp] = n2; ++sp;             // left half (processed first)
+    }
+  }
+  return val[0];
+}
+
+// Wave-parallel version for a row held in LDS: valid when numpy's recursion tree is a
+// perfect binary tree of depth D <= 3 (true for d = 384, 768 and most d <= 1024).  Leaf
+// b (of 2^D) is found by walking the split rule; lane 8b+j owns accumulator r_j of leaf b.
+// Returns the sum in every lane.  `depth` < 0 means "not perfect": caller uses the serial path.
+__host__ __device__ inline int pw_perfect_depth(int n) {
+  // returns D if the split tree is perfect with D <= 3, else -1
+  int lens[8] = {n, 0, 0, 0, 0, 0, 0, 0};
+  int cnt = 1;
+  for (int D = 0; D <= 3; ++D) {
+    bool all_leaf = true, any_leaf = false;
+    for (int i = 0; i < cnt; ++i) {
+      if (lens[i] <= 128) any_leaf = true; else all_leaf = false;
+    }
+    if (all_leaf) return D;
+    if (any_leaf || D == 3) return -1;
+    int nl[8];
+    for (int i = 0; i < cnt; ++i) {
+      int n2 = lens[i] / 2;
+      n2 -= n2 % 8;
+      nl[2 * i] = n2;
+      nl[2 * i + 1] = lens[i] - n2;
+    }
+    cnt *= 2;
+    for (int i = 0; i < cnt; ++i) lens[i] = nl[i];
+  }
+  return -1;
+}
+
+__device__ __forceinline__ float pw_sumsq_wave(const float* row, int n, int depth, int lane) {
+  const int leaf = lane >> 3, j = lane & 7;
+  float r = 0.0f;
+  int s = 0, len = n;
+  const bool active = leaf < (1 << depth);
+  if (active) {
+    for (int lvl = depth - 1; lvl >= 0; --lvl) {
+      int n2 = len / 2;
+      n2 -= n2 % 8;
+      if ((leaf >> lvl) & 1) { s += n2; len -= n2; } else { len = n2; }
+    }
+  }
+  const float* a = row + s;
+  const bool small = len < 8;
+  if (active && !small) {
+    r = __fmul_rn(a[j], a[j]);
+    for (int i = 8 + j; i < len - (len % 8); i += 8) r = r + __fmul_rn(a[i], a[i]);
+  }
+  // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)): the xor butterfly reproduces it (each + commutes)
+  r = r + __shfl_xor(r, 1, 64);
+  r = r + __shfl_xor(r, 2, 64);
+  r = r + __shfl_xor(r, 4, 64);
+  if (active) {
+    if (small) {
+      r = 0.0f;
+      for (int i = 0; i < len; ++i) r = r + __fmul_rn(a[i], a[i]);
+    } else {
+      for (int i = len - (len % 8); i < len; ++i) r = r + __fmul_rn(a[i], a[i]);
+    }
+  }
+  // inter-leaf tree: pw(left) + pw(right), perfect tree -> butterfly over leaf groups
+  for (int lvl = 0; lvl < depth; ++lvl) r = r + __shfl_xor(r, 8 << lvl, 64);
+  return __shfl(r, 0, 64);
+}
+
+// F.normalize / vector_db denominators (canonical: IEEE sqrt + IEEE div, no fast math)
+__device__ __forceinline__ float norm_denom(float sumsq, int mode) {
+  const float nrm = sqrtf(sumsq);  // correctly rounded (__fsqrt_rn lowers to the 1-ulp v_sqrt_f32)
+  return mode == TT_NORM_ADD_EPS ? nrm + 1e-8f : fmaxf(nrm, 1e-12f);
+}
+
+__device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+}  // namespace tt

@@ -1,0 +1,105 @@
+"""Loader for libtwotower_hip.so (the C ABI declared in include/twotower_hip.h).
+
+The library is built in-tree (two-tower-model-v2_amd/lib/) by csrc/Makefile and bound with
+ctypes.  ``import torch`` happens first so the library's libamdhip64.so.7 dependency
+resolves to the HIP runtime torch already loaded.  There is no CPU fallback:
+if the library is missing or no HIP device is visible, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+
+import torch  # noqa: F401  (must precede the dlopen, see module docstring)
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libtwotower_hip.so")
+CSRC = os.path.join(_PKG_ROOT, "csrc")
+
+TT_OK = 0
+TT_NORM_ADD_EPS = 0
+TT_NORM_MAX_EPS = 1
+
+_lock = threading.Lock()
+_lib = None
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+
+# name -> (restype, argtypes); mirrors include/twotower_hip.h
+SIGNATURES = {
+    "tt_version": (ctypes.c_int, []),
+    "tt_last_error": (ctypes.c_char_p, []),
+    "tt_padded_dim": (_i32, [_i32]),
+    "tt_l2norm_rows_f32": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _i64, _vp, _i32, _vp]),
+    "tt_scan_workspace_bytes": (ctypes.c_int, [_i64, _i32, _i32, _i32, ctypes.POINTER(_i64)]),
+    "tt_scan_topk_f32": (ctypes.c_int, [_vp, _i64, _i32, _i64, _i64, _vp, _i32, _i64, _i32, _vp,
+                                        _vp, _vp, _i64, _vp]),
+    "tt_scan_topk_f32_timed": (ctypes.c_int, [_vp, _i64, _i32, _i64, _i64, _vp, _i32, _i64, _i32,
+                                              _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
+    "tt_topk_merge_f32": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp]),
+    "tt_weighted_avg_l2_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _i64, _vp]),
+    "tt_gather_weighted_avg_l2_f32": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _i64,
+                                                     _i32, _vp, _i64, _vp]),
+    "tt_attn_agg_l2_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp,
+                                          _vp, _i64, _vp]),
+}
+
+
+class HipUnavailable(RuntimeError):
+    """Raised when the HIP library or a HIP device is missing (no silent fallback)."""
+
+
+def build(verbose: bool = False) -> str:
+    """Compile csrc/ for gfx950 into lib/libtwotower_hip.so (hipcc cross-compiles on CPU)."""
+    subprocess.run(["make", "-C", CSRC] + ([] if verbose else ["-s"]), check=True)
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise HipUnavailable(
+                    f"{LIB_PATH} not built; run `make -C {CSRC}` (or __graft_entry__.build())")
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != TT_OK:
+        msg = lib().tt_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (status {rc}): {msg}")
+
+
+def require_device(t: "torch.Tensor", name: str) -> None:
+    if not t.is_cuda:
+        raise HipUnavailable(f"{name} must be a HIP device tensor (got {t.device})")
+
+
+def device() -> "torch.device":
+    if not torch.cuda.is_available():
+        raise HipUnavailable("no HIP device visible: the two-tower hot path runs only on MI355X")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def padded_dim(d: int) -> int:
+    ep = lib().tt_padded_dim(int(d))
+    if ep < 0:
+        raise RuntimeError(f"embedding dim {d} unsupported by the scan kernel (max 768)")
+    return ep

@@ -1,0 +1,143 @@
+"""Tensor-level wrappers over the C ABI (include/twotower_hip.h).
+
+Every function takes/returns HIP device tensors, launches on torch's current stream and
+never synchronises.  Shapes and dtypes are validated here so that a bad call raises a
+Python exception instead of reaching a kernel with inconsistent sizes.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import check, lib, require_device, stream_ptr
+
+_f32 = torch.float32
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _check_2d(t, name, dtype=_f32):
+    require_device(t, name)
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"{name} must be 2-D with unit column stride, got {tuple(t.shape)}")
+
+
+def alloc_rows(n: int, d: int, device=None) -> torch.Tensor:
+    """[n, tt_padded_dim(d)] zero-initialised float32 (the scan's row layout)."""
+    ep = _lib.padded_dim(d)
+    return torch.zeros((n, ep), dtype=_f32, device=device or _lib.device())
+
+
+def l2norm_rows(x: torch.Tensor, d: int, mode: int, out: torch.Tensor = None,
+                out_bf16: torch.Tensor = None) -> torch.Tensor:
+    """Row-normalise the first d columns of x; padding columns of out are zeroed."""
+    _check_2d(x, "x")
+    if out is None:
+        out = torch.empty_like(x)
+    _check_2d(out, "out")
+    if out.shape[0] != x.shape[0] or out.shape[1] < d or x.shape[1] < d:
+        raise ValueError("l2norm_rows: shape mismatch")
+    if out_bf16 is not None:
+        if out_bf16.shape != out.shape or out_bf16.dtype != torch.bfloat16:
+            raise ValueError("out_bf16 must be bf16 with out's shape")
+    check(lib().tt_l2norm_rows_f32(_ptr(x), x.shape[0], d, x.stride(0), _ptr(out), out.stride(0),
+                                   _ptr(out_bf16), mode, stream_ptr()), "tt_l2norm_rows_f32")
+    return out
+
+
+def scan_workspace_bytes(n: int, d: int, nq: int, k: int) -> int:
+    b = ctypes.c_int64(0)
+    check(lib().tt_scan_workspace_bytes(n, d, nq, k, ctypes.byref(b)), "tt_scan_workspace_bytes")
+    return b.value
+
+
+def scan_topk(db: torch.Tensor, n: int, d: int, q: torch.Tensor, k: int, row_base: int = 0,
+              workspace: torch.Tensor = None, out=None):
+    """Exact top-k of q @ db[:n].T -> (scores [nq,k] f32, rows [nq,k] int64 = row_base + row)."""
+    _check_2d(db, "db")
+    _check_2d(q, "q")
+    nq = q.shape[0]
+    if not (1 <= k <= n <= db.shape[0]):
+        raise ValueError(f"scan_topk: need 1 <= k ({k}) <= n ({n}) <= rows ({db.shape[0]})")
+    if out is None:
+        out = (torch.empty((nq, k), dtype=_f32, device=q.device),
+               torch.empty((nq, k), dtype=torch.int64, device=q.device))
+    if nq == 0:
+        return out
+    need = scan_workspace_bytes(n, d, nq, k)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=q.device)
+    check(lib().tt_scan_topk_f32(_ptr(db), n, d, db.stride(0), row_base, _ptr(q), nq, q.stride(0),
+                                 k, _ptr(out[0]), _ptr(out[1]), _ptr(workspace), workspace.numel(),
+                                 stream_ptr()), "tt_scan_topk_f32")
+    return out
+
+
+def merge_topk(scores: torch.Tensor, idx: torch.Tensor, k: int):
+    """[L, nq, k_in] per-shard sorted lists (global ids) -> [nq, k]."""
+    require_device(scores, "scores")
+    if scores.dim() != 3 or idx.shape != scores.shape or idx.dtype != torch.int64:
+        raise ValueError("merge_topk: expected [L, nq, k_in] f32 scores and int64 ids")
+    scores, idx = scores.contiguous(), idx.contiguous()
+    L, nq, k_in = scores.shape
+    out_s = torch.empty((nq, k), dtype=_f32, device=scores.device)
+    out_i = torch.empty((nq, k), dtype=torch.int64, device=scores.device)
+    check(lib().tt_topk_merge_f32(_ptr(scores), _ptr(idx), L, nq, k_in, k, _ptr(out_s),
+                                  _ptr(out_i), stream_ptr()), "tt_topk_merge_f32")
+    return out_s, out_i
+
+
+def weighted_avg_l2(items: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None):
+    require_device(items, "item_embeddings")
+    if items.dim() != 3 or w.shape != items.shape[:2]:
+        raise ValueError("weighted_avg_l2: items [B,S,E] and weights [B,S] required")
+    items = items.contiguous().to(_f32)
+    w = w.contiguous().to(_f32)
+    b, s, d = items.shape
+    if out is None:
+        out = torch.empty((b, d), dtype=_f32, device=items.device)
+    check(lib().tt_weighted_avg_l2_f32(_ptr(items), b, s, d, _ptr(w), _ptr(out), out.stride(0),
+                                       stream_ptr()), "tt_weighted_avg_l2_f32")
+    return out
+
+
+def gather_weighted_avg_l2(table: torch.Tensor, d: int, hist: torch.Tensor, w: torch.Tensor,
+                           out: torch.Tensor = None):
+    """Mode B buyer encode: rows table[hist[b, s]] aggregated with weights w[b, s]."""
+    _check_2d(table, "table")
+    require_device(hist, "hist")
+    if hist.dtype != torch.int64 or hist.dim() != 2 or w.shape != hist.shape:
+        raise ValueError("gather_weighted_avg_l2: hist [B,S] int64 and w [B,S] required")
+    hist = hist.contiguous()
+    w = w.contiguous().to(_f32)
+    b, s = hist.shape
+    if out is None:
+        out = torch.empty((b, table.shape[1]), dtype=_f32, device=table.device)
+    check(lib().tt_gather_weighted_avg_l2_f32(_ptr(table), table.shape[0], table.stride(0), d,
+                                              _ptr(hist), _ptr(w), b, s, _ptr(out),
+                                              out.stride(0), stream_ptr()),
+          "tt_gather_weighted_avg_l2_f32")
+    return out
+
+
+def attn_agg_l2(items, w, W1, b1, W2, b2, out=None):
+    require_device(items, "item_embeddings")
+    if items.dim() != 3 or w.shape != items.shape[:2]:
+        raise ValueError("attn_agg_l2: items [B,S,E] and weights [B,S] required")
+    items = items.contiguous().to(_f32)
+    w = w.contiguous().to(_f32)
+    W1, b1, W2, b2 = (t.detach().contiguous().to(_f32) for t in (W1, b1, W2, b2))
+    b, s, d = items.shape
+    h = W1.shape[0]
+    if out is None:
+        out = torch.empty((b, d), dtype=_f32, device=items.device)
+    check(lib().tt_attn_agg_l2_f32(_ptr(items), b, s, d, _ptr(w), _ptr(W1), _ptr(b1), h, _ptr(W2),
+                                   _ptr(b2), _ptr(out), out.stride(0), stream_ptr()),
+          "tt_attn_agg_l2_f32")
+    return out

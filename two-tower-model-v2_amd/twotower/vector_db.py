@@ -1,0 +1,235 @@
+"""VectorDatabase on MI355X: drop-in for the reference's FAISS-backed class.
+
+Reference: src/inference/vector_db.py (class VectorDatabase :10).  Same constructor,
+methods, attributes, return types and error messages; the faiss.IndexFlatIP it wraps
+(:48, :54, :160, :197) is replaced by ``FlatIPIndex``, a device-resident catalog whose
+search is the fused HIP scan + top-k kernel (csrc/tt_scan.hip).
+
+Numerics: build_index normalises rows on the GPU with numpy's exact float32 algorithm
+(bit-identical to the reference's ``embeddings / (norms + 1e-8)``, :44-45); queries get the
+same treatment (:152-153, :189-190); scores are exact float32 inner products (canonical
+fma order), sorted descending, ties to the lower row.
+"""
+from __future__ import annotations
+
+import json
+import struct
+from pathlib import Path
+from typing import List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib, kernels
+
+
+class FlatIPIndex:
+    """Device-resident exact inner-product index (the faiss.IndexFlatIP surface used by the
+    reference: ``d``, ``ntotal``, ``add``, ``search``).
+
+    Layout in HBM: ``xb`` = [capacity, tt_padded_dim(d)] float32, row-major, zero padded,
+    rows L2-normalised by ``add`` exactly as the reference does before ``index.add``.
+    """
+
+    def __init__(self, d: int, device=None):
+        self.d = int(d)
+        self.ep = _lib.padded_dim(self.d)
+        self.device = device or _lib.device()
+        self.xb = torch.zeros((0, self.ep), dtype=torch.float32, device=self.device)
+        self.ntotal = 0
+        self._ws = None
+
+    # faiss-style add of ALREADY-normalised float32 rows (host or device)
+    def add(self, x) -> None:
+        x = torch.as_tensor(x, dtype=torch.float32)
+        if x.dim() != 2 or x.shape[1] != self.d:
+            raise ValueError(f"add: expected [n, {self.d}] float32")
+        rows = torch.zeros((x.shape[0], self.ep), dtype=torch.float32, device=self.device)
+        rows[:, : self.d].copy_(x, non_blocking=False)
+        self.xb = torch.cat([self.xb[: self.ntotal], rows]) if self.ntotal else rows
+        self.ntotal = self.xb.shape[0]
+
+    def add_normalized_from(self, x) -> None:
+        """Copy raw rows to the device and normalise there (x / (||x|| + 1e-8))."""
+        x = torch.as_tensor(x)
+        if x.dim() != 2 or x.shape[1] != self.d:
+            raise ValueError(f"add: expected [n, {self.d}]")
+        raw = torch.zeros((x.shape[0], self.ep), dtype=torch.float32, device=self.device)
+        raw[:, : self.d].copy_(x.to(torch.float32))
+        kernels.l2norm_rows(raw, self.d, _lib.TT_NORM_ADD_EPS, out=raw)
+        self.xb = torch.cat([self.xb[: self.ntotal], raw]) if self.ntotal else raw
+        self.ntotal = self.xb.shape[0]
+
+    def search_device(self, q: torch.Tensor, k: int):
+        """q: [nq, ep] normalised device rows -> (scores [nq,k], labels [nq,k]) on device."""
+        if k < 1:
+            raise RuntimeError("Error: 'k > 0' failed")  # faiss' own assertion text
+        need = kernels.scan_workspace_bytes(self.ntotal, self.d, q.shape[0], k)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return kernels.scan_topk(self.xb, self.ntotal, self.d, q, k, workspace=self._ws)
+
+    def search(self, x: np.ndarray, k: int):
+        """faiss signature: float32 [nq, d] host queries -> (D [nq,k] f32, I [nq,k] i64) host."""
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        q = torch.zeros((x.shape[0], self.ep), dtype=torch.float32, device=self.device)
+        q[:, : self.d].copy_(torch.from_numpy(x))
+        s, i = self.search_device(q, k)
+        return s.cpu().numpy(), i.cpu().numpy()
+
+    def reconstruct(self, i: int) -> np.ndarray:
+        return self.xb[i, : self.d].cpu().numpy()
+
+
+# ------------------------------------------------------------------ index file format
+# Best-effort faiss IndexFlatIP layout (fourcc "IxFI", header, codes).  The real faiss
+# reader is absent offline, so compatibility with faiss.read_index is UNPINNED;
+# our own load_index reads exactly what save_index writes.
+_FOURCC = b"IxFI"
+
+
+def write_flat_ip(index: FlatIPIndex, path: str) -> None:
+    xb = index.xb[: index.ntotal, : index.d].contiguous().cpu().numpy().astype("<f4")
+    with open(path, "wb") as f:
+        f.write(_FOURCC)
+        f.write(struct.pack("<iqqqBi", index.d, index.ntotal, 1 << 20, 1 << 20, 1, 0))
+        f.write(struct.pack("<Q", xb.size))
+        f.write(xb.tobytes())
+
+
+def read_flat_ip(path: str, device=None) -> FlatIPIndex:
+    with open(path, "rb") as f:
+        if f.read(4) != _FOURCC:
+            raise RuntimeError(f"{path}: not an IndexFlatIP file")
+        d, ntotal, _, _, _, _ = struct.unpack("<iqqqBi", f.read(struct.calcsize("<iqqqBi")))
+        (size,) = struct.unpack("<Q", f.read(8))
+        xb = np.frombuffer(f.read(size * 4), dtype="<f4").reshape(ntotal, d)
+    index = FlatIPIndex(d, device)
+    index.add(xb)
+    return index
+
+
+class VectorDatabase:
+    """Mirror of reference ``VectorDatabase`` (src/inference/vector_db.py:10-233)."""
+
+    def __init__(self, embedding_dim: int = 384):
+        self.embedding_dim = embedding_dim
+        self.index: Optional[FlatIPIndex] = None
+        self.product_ids = None
+        self.id_to_index = None
+        self.index_to_id = None
+
+    def build_index(self, embeddings: np.ndarray, product_ids: List[str]):
+        """reference :25-61"""
+        n_products, dim = embeddings.shape
+        if dim != self.embedding_dim:
+            raise ValueError(
+                f"Embedding dimension mismatch: expected {self.embedding_dim}, got {dim}")
+        index = FlatIPIndex(self.embedding_dim)
+        # reference normalises in the input dtype (:44-45) then casts to f32 (:51); for the
+        # float32 inputs the pipeline produces this is the GPU numpy-exact normalisation.
+        if np.asarray(embeddings).dtype == np.float32:
+            index.add_normalized_from(torch.from_numpy(np.ascontiguousarray(embeddings)))
+        else:
+            norms = np.linalg.norm(embeddings, axis=1, keepdims=True)
+            index.add((embeddings / (norms + 1e-8)).astype(np.float32))
+        self.index = index
+        self.product_ids = product_ids
+        self.id_to_index = {pid: idx for idx, pid in enumerate(product_ids)}
+        self.index_to_id = {idx: pid for idx, pid in enumerate(product_ids)}
+        print(f"Built FAISS index with {n_products} products")
+
+    def load_index(self, index_path: str, product_ids_path: Optional[str] = None,
+                   mapping_path: Optional[str] = None):
+        """reference :63-98"""
+        self.index = read_flat_ip(index_path)
+        if product_ids_path:
+            product_ids_array = np.load(product_ids_path, allow_pickle=False)
+            self.product_ids = product_ids_array.tolist()
+        else:
+            n_products = self.index.ntotal
+            self.product_ids = [f"product_{i}" for i in range(n_products)]
+        if mapping_path and Path(mapping_path).exists():
+            with open(mapping_path, "r", encoding="utf-8") as f:
+                self.id_to_index = json.load(f)
+            self.index_to_id = {v: k for k, v in self.id_to_index.items()}
+        else:
+            self.id_to_index = {pid: idx for idx, pid in enumerate(self.product_ids)}
+            self.index_to_id = {idx: pid for idx, pid in enumerate(self.product_ids)}
+        print(f"Loaded FAISS index with {len(self.product_ids)} products")
+
+    def save_index(self, index_path: str, product_ids_path: Optional[str] = None,
+                   mapping_path: Optional[str] = None):
+        """reference :100-128"""
+        if self.index is None:
+            raise ValueError("Index not built. Call build_index() first.")
+        write_flat_ip(self.index, index_path)
+        if product_ids_path:
+            np.save(product_ids_path, np.array(self.product_ids))
+        if mapping_path and self.id_to_index:
+            with open(mapping_path, "w", encoding="utf-8") as f:
+                json.dump(self.id_to_index, f, ensure_ascii=False, indent=2)
+        print(f"Saved FAISS index to {index_path}")
+
+    # -------------------------------------------------------------- device fast path
+    def normalize_queries(self, q: torch.Tensor) -> torch.Tensor:
+        """Device queries [nq, >=d] -> [nq, ep] rows q/(||q||+1e-8) (reference :152-153)."""
+        out = torch.empty((q.shape[0], self.index.ep), dtype=torch.float32, device=q.device)
+        return kernels.l2norm_rows(q, self.embedding_dim, _lib.TT_NORM_ADD_EPS, out=out)
+
+    def search(self, query_embeddings: torch.Tensor, k: int = 10, normalized: bool = False):
+        """Device-level retrieve_batch: returns (scores [nq,k], rows [nq,k]) device tensors.
+        ``normalized=True`` skips the q/(||q||+1e-8) step (rows already [nq, ep], padded)."""
+        if self.index is None:
+            raise ValueError("Index not built. Call build_index() or load_index() first.")
+        k = min(k, self.index.ntotal)
+        q = query_embeddings if normalized else self.normalize_queries(query_embeddings)
+        return self.index.search_device(q, k)
+
+    def _search_host(self, query_embeddings: np.ndarray, k: int):
+        x = np.ascontiguousarray(query_embeddings)
+        if x.dtype != np.float32:
+            # reference normalises in the input dtype, then casts (:189-193): do the same
+            norms = np.linalg.norm(x, axis=1, keepdims=True)
+            x = (x / (norms + 1e-8)).astype(np.float32)
+            normalized = True
+        else:
+            normalized = False
+        q = torch.zeros((x.shape[0], self.index.ep), dtype=torch.float32, device=self.index.device)
+        q[:, : self.embedding_dim].copy_(torch.from_numpy(x))
+        s, i = self.search(q, k, normalized=normalized)
+        return s.cpu().numpy(), i.cpu().numpy()
+
+    def _to_results(self, scores: np.ndarray, indices: np.ndarray):
+        out = []
+        n = len(self.product_ids)
+        for query_scores, query_indices in zip(scores, indices):
+            res = []
+            for idx, score in zip(query_indices, query_scores):
+                if idx < n:  # reference :165 (note: -1 would pass, as in the reference)
+                    res.append((self.product_ids[idx], float(score)))
+            out.append(res)
+        return out
+
+    def retrieve(self, query_embedding: np.ndarray, k: int = 10) -> List[Tuple[str, float]]:
+        """reference :130-169"""
+        if self.index is None:
+            raise ValueError("Index not built. Call build_index() or load_index() first.")
+        if query_embedding.ndim == 1:
+            query_embedding = query_embedding.reshape(1, -1)
+        return self._to_results(*self._search_host(query_embedding, k))[0]
+
+    def retrieve_batch(self, query_embeddings: np.ndarray,
+                       k: int = 10) -> List[List[Tuple[str, float]]]:
+        """reference :171-209"""
+        if self.index is None:
+            raise ValueError("Index not built. Call build_index() or load_index() first.")
+        return self._to_results(*self._search_host(query_embeddings, k))
+
+    def get_embedding(self, product_id: str) -> Optional[np.ndarray]:
+        """reference :211-231 (always None there: FAISS cannot reconstruct in that code)."""
+        if self.index is None or self.id_to_index is None:
+            return None
+        if product_id not in self.id_to_index:
+            return None
+        return None
