@@ -22,6 +22,8 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 3 --warmup 1 ${BENCH_ARGS:-} ;;
+    pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 2 --warmup 1 ${BENCH_ARGS:-}
+           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 2 --warmup 1 ${BENCH_ARGS:-} ;;
   esac
 done
 echo "session done"
