@@ -32,7 +32,8 @@ import torch.distributed as dist  # noqa: E402
 
 from twotower import _lib, kernels  # noqa: E402
 
-F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X dense f32 MFMA (MI355X_MICROARCH.md)
+F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X dense f32 MFMA (MI355X_MICROARCH.md)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity)
 HBM_PEAK_GBPS = 8000.0
 
 
@@ -46,6 +47,9 @@ def parse():
     p.add_argument("--hist", type=int, default=20)
     p.add_argument("--k", type=int, default=100)
     p.add_argument("--dim", type=int, default=384)
+    p.add_argument("--method", choices=["bf16", "f32"], default="bf16",
+                   help="bf16: bf16 MFMA filter + exact f32 re-rank; f32: exact f32 MFMA scan "
+                        "(identical results)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-single", type=int, default=32)
     p.add_argument("--cpu-batch", type=int, default=512)
@@ -81,7 +85,10 @@ def main():
     kernels.l2norm_rows(table, E, _lib.TT_NORM_MAX_EPS, out=table)  # ItemTower outputs (F.normalize)
     lo, hi = rank * N // world, (rank + 1) * N // world
     shard = torch.empty((hi - lo, ep), device=dev)
-    kernels.l2norm_rows(table[lo:hi], E, _lib.TT_NORM_ADD_EPS, out=shard)  # build_index
+    shard16 = torch.empty((hi - lo, ep), device=dev, dtype=torch.bfloat16)
+    kernels.l2norm_rows(table[lo:hi], E, _lib.TT_NORM_ADD_EPS, out=shard, out_bf16=shard16)
+    xmax = float(torch.linalg.vector_norm(shard, dim=1).max())  # build-time statistic
+    eps = kernels.filter_eps(ep, xmax)
     gb = torch.Generator(device=dev).manual_seed(3 + rank)
     hist = torch.randint(0, N, (B, S), generator=gb, device=dev, dtype=torch.int64)
     w = event_mix(gb, (B, S), dev)
@@ -89,7 +96,9 @@ def main():
     q = torch.empty((B, ep), device=dev)
     qall = torch.empty((world * B, ep), device=dev) if world > 1 else q
     nq = world * B
-    ws = torch.empty(kernels.scan_workspace_bytes(hi - lo, E, nq, K), dtype=torch.uint8, device=dev)
+    ws_bytes = (kernels.filter_workspace_bytes(hi - lo, E, nq, K) if a.method == "bf16"
+                else kernels.scan_workspace_bytes(hi - lo, E, nq, K))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     s_shard = torch.empty((nq, K), device=dev)
     i_shard = torch.empty((nq, K), dtype=torch.int64, device=dev)
     if world > 1:
@@ -103,13 +112,21 @@ def main():
         kernels.l2norm_rows(q, E, _lib.TT_NORM_ADD_EPS, out=q)
         if world > 1:
             dist.all_gather_into_tensor(qall, q)
-        e0, e1 = (ev if ev else (None, None))
-        _lib.check(L.tt_scan_topk_f32_timed(
-            shard.data_ptr(), hi - lo, E, shard.stride(0), lo,
-            qall.data_ptr(), nq, qall.stride(0), K, s_shard.data_ptr(), i_shard.data_ptr(),
-            ws.data_ptr(), ws.numel(), stream.cuda_stream,
-            e0.cuda_event if e0 is not None else None, e1.cuda_event if e1 is not None else None),
-            "scan")
+        e0, e1, p0, p1 = (ev if ev else (None, None, None, None))
+        if p0 is not None:
+            p0.record(stream)
+        if a.method == "bf16":
+            kernels.scan_topk_bf16(shard, shard16, hi - lo, E, qall, K, eps, row_base=lo,
+                                   workspace=ws, out=(s_shard, i_shard), events=(e0, e1))
+        else:
+            _lib.check(L.tt_scan_topk_f32_timed(
+                shard.data_ptr(), hi - lo, E, shard.stride(0), lo,
+                qall.data_ptr(), nq, qall.stride(0), K, s_shard.data_ptr(), i_shard.data_ptr(),
+                ws.data_ptr(), ws.numel(), stream.cuda_stream,
+                e0.cuda_event if e0 is not None else None,
+                e1.cuda_event if e1 is not None else None), "scan")
+        if p1 is not None:
+            p1.record(stream)
         if world > 1:
             dist.all_to_all_single(s_recv.view(world * B, K), s_shard)
             dist.all_to_all_single(i_recv.view(world * B, K), i_shard)
@@ -120,10 +137,10 @@ def main():
         step()
     evs = []
     for _ in range(a.steps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)  # materialise the hipEvent handles; the ABI re-records them
-        e1.record(stream)
-        evs.append((e0, e1))
+        ev = tuple(torch.cuda.Event(enable_timing=True) for _ in range(4))
+        for e in ev:
+            e.record(stream)  # materialise the hipEvent handles; the ABI re-records them
+        evs.append(ev)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -136,19 +153,33 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     dt = t1 - t0
-    scan_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps
+    scan_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / a.steps
+    search_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / a.steps
     if world > 1:
-        t = torch.tensor([dt, scan_ms], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt, scan_ms, search_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt, scan_ms = t.tolist()
+        dt, scan_ms, search_ms = t.tolist()
+    fallback = (kernels.filter_fallback_count(ws, hi - lo, E, nq, K) if a.method == "bf16"
+                else 0)
     ms_per_step = dt / a.steps * 1e3
     value = world * B / (dt / a.steps)
 
-    # dominant kernel: k_scan_topk_f32, per launch: nq queries x (hi-lo) rows x E
+    # dominant kernel, per launch: nq queries x (hi-lo) rows x E multiply-adds
+    #   bf16: k_filter_bf16 over the full shard (bf16 catalog image read once = 2*rows*ep B)
+    #   f32:  k_scan_topk_f32 (f32 catalog read once = 4*rows*ep B)
     rows = hi - lo
     flops = 2.0 * nq * rows * E
-    alg_bytes = 4.0 * rows * ep + 4.0 * nq * ep + nq * K * 8.0 * 1.0  # catalog once, queries, lists
+    elem = 2.0 if a.method == "bf16" else 4.0
+    alg_bytes = elem * rows * ep + 4.0 * nq * ep
     achieved_tf = flops / (scan_ms * 1e-3) / 1e12
+    kname = "k_filter_bf16" if a.method == "bf16" else "k_scan_topk_f32"
+    peak = BF16_MFMA_PEAK_TFLOPS if a.method == "bf16" else F32_MFMA_PEAK_TFLOPS
+    traffic = None
+    tj = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tj):
+        tk = json.load(open(tj)).get("kernels", {}).get(kname)
+        if tk and tk.get("config", "").startswith(f"{N // 1000000}M x {E}"):
+            traffic = tk["fetch_bytes"] + tk["write_bytes"]
     result = {
         "metric": "buyers encoded+retrieved/sec @ k=100, 1M x 384 catalog",
         "value": value,
@@ -160,7 +191,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "bf16 filter + f32 exact scores" if a.method == "bf16" else "f32",
         "data": "synthetic (random-normal item embeddings, uniform 20-event histories, event mix 0.75/0.17/0.08)",
         "config": {
             "workload": "configs[2]: 1M x 384 catalog, 10k buyers/rank x 20 events, weighted-avg, "
@@ -169,14 +200,16 @@ def main():
             "parallelism": f"catalog row-shard x{world}" + (" + RCCL all-gather(queries) / all-to-all(top-k)" if world > 1 else ""),
         },
         "roofline": {
-            "kernel": "k_scan_topk_f32",
+            "kernel": kname,
             "bound": "mfma",
             "achieved": achieved_tf,
-            "peak": F32_MFMA_PEAK_TFLOPS,
+            "peak": peak,
             "unit": "TFLOP/s",
-            "frac": achieved_tf / F32_MFMA_PEAK_TFLOPS,
-            "traffic": None,
-            "scan_ms": scan_ms,
+            "frac": achieved_tf / peak,
+            "traffic": traffic,
+            "kernel_ms": scan_ms,
+            "search_ms": search_ms,
+            "fallback_queries_last_step": fallback,
             "flops_per_launch": flops,
             "algorithmic_bytes_per_launch": alg_bytes,
             "achieved_hbm_gbps": alg_bytes / (scan_ms * 1e-3) / 1e9,

@@ -86,6 +86,36 @@ int tt_scan_topk_f32_timed(const float* db, int64_t n, int32_t d, int64_t ld_db,
                            int64_t workspace_bytes, void* stream, void* ev_start,
                            void* ev_stop);
 
+/* Exact scan of the queries listed on the device: slots 0 .. *qsel_n-1 read query qsel[slot]
+ * and write row qsel[slot] of out_*.  Blocks beyond *qsel_n exit at once, so it can be
+ * enqueued unconditionally as the fallback of tt_scan_topk_bf16f32 (no host sync). */
+int tt_scan_topk_f32_select(const float* db, int64_t n, int32_t d, int64_t ld_db,
+                            int64_t row_base, const float* q, int32_t nq, int64_t ld_q,
+                            int32_t k, const int32_t* qsel, const int32_t* qsel_n,
+                            float* out_score, int64_t* out_idx, void* workspace,
+                            int64_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Same results as tt_scan_topk_f32 (bit-identical: canonical f32 scores, same order), found
+ * through a bf16 MFMA filter over db_bf16 (the bf16 image of db, e.g. from tt_l2norm_rows_f32)
+ * followed by an exact f32 re-rank of the candidates whose bf16 score lies within 2*eps of the
+ * bf16 k-th best.  eps must bound |bf16 score - f32 score| for every (row, query):
+ *   eps >= ((2^-8 + 2^-18) + 3*d_pad*2^-24) * max||x|| * max||q||.
+ * Queries whose candidate lists overflow are re-scanned exactly in a fallback launch.
+ * k <= 128 (larger k: tt_scan_topk_f32).  Workspace: tt_filter_workspace_bytes.
+ * ev_start/ev_stop (may be NULL) are recorded around the full-catalog filter kernel (the
+ * dominant kernel; the sample levels, selection and re-rank are outside the bracket).
+ * --------------------------------------------------------------------------------- */
+int tt_filter_workspace_bytes(int64_t n, int32_t d, int32_t nq, int32_t k, int64_t* bytes);
+/* Byte offset (in the workspace) of the int32 count of queries the last call served through
+ * the exact fallback -- a diagnostic, read after the stream is synchronised. */
+int tt_filter_fallback_offset(int64_t n, int32_t d, int32_t nq, int32_t k, int64_t* offset);
+int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n, int32_t d,
+                         int64_t ld_db, int64_t row_base, const float* q, int32_t nq,
+                         int64_t ld_q, int32_t k, float eps, float* out_score, int64_t* out_idx,
+                         void* workspace, int64_t workspace_bytes, void* stream,
+                         void* ev_start, void* ev_stop);
+
 /* Merge n_lists per-shard top-k lists [n_lists, nq, k_in] (each sorted, global row ids)
  * into [nq, k]; same ordering rule.  Used after the RCCL all-gather of per-shard top-k
  * (multi-GPU row sharding). */

@@ -86,6 +86,82 @@ def test_scan_bit_exact_vs_oracle(K, oracle_mod, n, d, nq, k):
     assert np.array_equal(s, rs)
 
 
+BF16_CASES = [c for c in SCAN_CASES if c[3] <= 128] + [
+    (2049, 384, 5, 128),     # two filter levels, k at the filter's maximum
+    (300000, 384, 40, 100),  # four filter levels
+    (60000, 768, 33, 100),   # E = 768 (one query block per wave)
+    (20000, 384, 300, 100),  # several query tiles
+    (40000, 512, 9, 64),
+]
+
+
+@pytest.mark.parametrize("n,d,nq,k", BF16_CASES)
+def test_bf16_filter_bit_exact_vs_oracle(K, oracle_mod, n, d, nq, k):
+    """bf16 MFMA filter + exact f32 re-rank == canonical f32 top-k, bit for bit."""
+    from twotower import _lib
+
+    rng = np.random.default_rng(n * 17 + d + k)
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
+    q = oracle_mod.l2norm_rows(rng.standard_normal((nq, d)).astype(np.float32), 0)
+    db = dev_rows(x)
+    db16 = db.to(torch.bfloat16)
+    eps = K.filter_eps(_lib.padded_dim(d))
+    s, i = K.scan_topk_bf16(db, db16, n, d, dev_rows(q), k, eps)
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    assert np.array_equal(i.cpu().numpy(), ri)
+    assert np.array_equal(s.cpu().numpy(), rs)
+
+
+def test_bf16_filter_no_fallback_on_iid_data(K):
+    """The optimistic threshold must hold on iid data: no query may need the exact fallback
+    (a performance property: fallbacks are correct but slow)."""
+    from twotower import _lib
+
+    n, d, nq, k = 400000, 384, 300, 100
+    g = torch.Generator(device="cuda").manual_seed(5)
+    db = torch.randn((n, d), generator=g, device="cuda")
+    K.l2norm_rows(db, d, 0, out=db)
+    q = torch.randn((nq, d), generator=g, device="cuda")
+    K.l2norm_rows(q, d, 0, out=q)
+    ws = torch.empty(K.filter_workspace_bytes(n, d, nq, k), dtype=torch.uint8, device="cuda")
+    K.scan_topk_bf16(db, db.to(torch.bfloat16), n, d, q, k, K.filter_eps(_lib.padded_dim(d)),
+                     workspace=ws)
+    torch.cuda.synchronize()
+    assert K.filter_fallback_count(ws, n, d, nq, k) == 0
+
+
+@pytest.mark.parametrize("eps", [0.5, 4.0])
+def test_bf16_filter_fallback_is_exact(K, oracle_mod, eps):
+    """A loose bound overflows the candidate lists: every query then takes the exact
+    fallback launch, and the results must not change."""
+    rng = np.random.default_rng(77)
+    n, d, nq, k = 30000, 384, 20, 100
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
+    q = oracle_mod.l2norm_rows(rng.standard_normal((nq, d)).astype(np.float32), 0)
+    db = dev_rows(x)
+    ws = torch.empty(K.filter_workspace_bytes(n, d, nq, k), dtype=torch.uint8, device="cuda")
+    s, i = K.scan_topk_bf16(db, db.to(torch.bfloat16), n, d, dev_rows(q), k, eps, workspace=ws)
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
+    assert K.filter_fallback_count(ws, n, d, nq, k) == nq  # every query took the fallback
+
+
+def test_bf16_filter_clusters_and_ties(K, oracle_mod):
+    """Near-duplicate clusters (band overflow) and exact duplicates (ties on both scores)."""
+    rng = np.random.default_rng(78)
+    base = oracle_mod.l2norm_rows(rng.standard_normal((400, 384)).astype(np.float32), 0)
+    noise = rng.standard_normal((12000, 384)).astype(np.float32) * 1e-4
+    x = oracle_mod.l2norm_rows(np.repeat(base, 30, axis=0) + noise, 0)
+    x[:1200] = np.repeat(base[:40], 30, axis=0)  # exact duplicates
+    q = np.concatenate([base[:6], oracle_mod.l2norm_rows(
+        rng.standard_normal((6, 384)).astype(np.float32), 0), np.zeros((1, 384), np.float32)])
+    db = dev_rows(x)
+    s, i = K.scan_topk_bf16(db, db.to(torch.bfloat16), x.shape[0], 384, dev_rows(q), 128,
+                            K.filter_eps(384))
+    rs, ri = oracle_mod.scan_topk(x, q, 128)
+    assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
+
+
 def test_scan_ties_and_duplicates(K, oracle_mod):
     rng = np.random.default_rng(9)
     base = oracle_mod.l2norm_rows(rng.standard_normal((700, 384)).astype(np.float32), 0)

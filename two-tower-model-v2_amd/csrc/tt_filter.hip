@@ -1,0 +1,820 @@
+// tt_filter.hip -- exact top-k via a bf16 MFMA filter + exact float32 re-rank (gfx950).
+//
+// Same contract as tt_scan_topk_f32 (replaces faiss.IndexFlatIP.search,
+// src/inference/vector_db.py:160,197): results are the top-k by the CANONICAL float32 score
+// (tt_common.hpp), ties to the lower row -- bit-identical to the f32 scan.  The bf16 pass
+// only decides WHICH rows need an exact score:
+//
+//   a(r) = bf16(x_r) . bf16(q) accumulated in f32 by v_mfma_f32_16x16x32_bf16.
+//   |a(r) - s(r)| <= eps  with  eps = (2u+u^2)|x||q| + 3*E*2^-24 |x||q|,  u = 2^-9
+//   (bf16 round-to-nearest on both operands, Cauchy-Schwarz; the last term covers the f32
+//   accumulation of a and of the canonical score s).  The caller passes eps.
+//
+// Pipeline per call (all on the stream, no host sync, DESIGN.md "Scan v2"):
+//   1. levels L = coarse..fine over nested strided row samples (stride 16^L, last = 1).
+//      k_filter_bf16 appends every sample row with a >= theta_q to per-(query, slab)
+//      candidate lists; k_select sorts a query's candidates and sets theta for the next
+//      level = k-th best a of this sample (a lower bound of the k-th best a of any superset).
+//      The last level filters with theta = T - 2*eps, and k_select keeps the band
+//      a >= A_k - 2*eps, where A_k = k-th best a over the whole catalog.  Every row of the
+//      exact top-k has a >= s - eps >= s_k - eps >= A_k - 2*eps, so the band contains it.
+//   2. k_rerank computes the canonical f32 score of every band row (gathered from the f32
+//      catalog), sorts (score desc, row asc) and writes the top-k.
+//   3. A query whose candidate lists overflow is flagged, appended to a device-side list, and
+//      served by the exact f32 scan kernel (tt_scan.hip) in a fallback launch whose blocks
+//      exit immediately when the list is empty.
+#include "tt_common.hpp"
+
+namespace tt {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int FL_WAVES = 4;
+constexpr int FL_CAP = 256;     // entries per (query, slab) list
+constexpr int SEL_CAP = 4096;   // candidates per query a level may produce
+constexpr int BAND_CAP = 1024;  // rows per query in the final band
+constexpr int FL_KMAX = 128;
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f32_to_bf16_rne(lo) | ((uint32_t)f32_to_bf16_rne(hi) << 16);
+}
+
+// XCD-aware block id: blocks b and b+8 run on the same XCD (observed placement, speed only).
+// Give every XCD a contiguous range of logical ids so that its co-resident blocks share slabs.
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+  const int q = nblk / 8, r = nblk % 8, x = bid % 8, local = bid / 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + local;
+}
+
+// --------------------------------------------------------------------------- filter
+// Block: FL_WAVES waves over the same slab rows; wave w owns QB*16 queries (B fragments of
+// v_mfma_f32_16x16x32_bf16 in VGPRs).  A fragments (16 rows x 32 dims) are streamed straight
+// from HBM: lane l loads 16 B of row (l&15) at dims 32s + 8(l>>4).
+template <int EP, int QB>
+__global__ __launch_bounds__(64 * FL_WAVES, 2) void k_filter_dense(
+    const uint16_t* __restrict__ xb, int64_t n, int64_t ld, const float* __restrict__ q,
+    int nq, int64_t ldq, const float* __restrict__ theta, int64_t stride, int64_t n_sample,
+    int rows_per_slab, int n_slabs, int n_qt, uint64_t* __restrict__ lists,
+    int* __restrict__ counts) {
+  constexpr int KS = EP / 32;  // k-steps
+  constexpr int QPW = 16 * QB;
+  __shared__ int cnt[FL_WAVES][QPW];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, g = lane >> 4;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int slab = lb / n_qt, qt = lb % n_qt;
+  const int qbase = qt * (FL_WAVES * QPW) + w * QPW;
+
+  bf16x8 qf[QB][KS];
+  float th[QB];
+  bool qv[QB];
+#pragma unroll
+  for (int b = 0; b < QB; ++b) {
+    const int qi = qbase + 16 * b + col;
+    qv[b] = qi < nq;
+    th[b] = qv[b] ? theta[qi] : __builtin_huge_valf();
+    const float* qp = q + (int64_t)(qv[b] ? qi : 0) * ldq + 8 * g;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const f32x4 v0 = *(const f32x4*)(qp + 32 * s);
+      const f32x4 v1 = *(const f32x4*)(qp + 32 * s + 4);
+      u32x4 u = {pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]), pack_bf16x2(v1[0], v1[1]),
+                 pack_bf16x2(v1[2], v1[3])};
+      qf[b][s] = __builtin_bit_cast(bf16x8, u);
+    }
+  }
+  if (lane < QPW) cnt[w][lane] = 0;
+  wave_sync();
+
+  const int64_t j0 = (int64_t)slab * rows_per_slab;
+  const int64_t j1 = (j0 + rows_per_slab < n_sample) ? j0 + rows_per_slab : n_sample;
+  if (j0 < j1) {
+    auto row_ptr = [&](int64_t jb) {
+      int64_t j = jb + col;
+      j = j < j1 ? j : j1 - 1;
+      return (const u32x4*)(xb + j * stride * ld) + g;  // 16 B = 8 bf16 at dims 8g..
+    };
+    // EP <= 512: the next 16-row block's A fragments are loaded before this block's MFMAs
+    // (one block in flight per wave); EP = 768 has no VGPRs for that and relies on the
+    // second wave per SIMD to cover the load latency.
+    constexpr bool PREFETCH = EP <= 512;
+    u32x4 cur[KS], nxt[PREFETCH ? KS : 1];
+    {
+      const u32x4* p = row_ptr(j0);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) cur[s] = p[4 * s];
+    }
+    for (int64_t jb = j0; jb < j1; jb += 16) {
+      const bool more = jb + 16 < j1;
+      if constexpr (PREFETCH) {
+        if (more) {
+          const u32x4* p = row_ptr(jb + 16);
+#pragma unroll
+          for (int s = 0; s < KS; ++s) nxt[s] = p[4 * s];
+        }
+      }
+      f32x4 acc[QB];
+#pragma unroll
+      for (int b = 0; b < QB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const bf16x8 a = __builtin_bit_cast(bf16x8, cur[s]);
+#pragma unroll
+        for (int b = 0; b < QB; ++b)
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[b][s], acc[b], 0, 0, 0);
+      }
+      // lane holds a(row jb + 4g + jj, query qbase + 16b + col)
+      uint32_t pass = 0;
+#pragma unroll
+      for (int b = 0; b < QB; ++b)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const bool ok = (jb + 4 * g + jj < j1) && (acc[b][jj] >= th[b]);
+          pass |= ok ? (1u << (4 * b + jj)) : 0u;
+        }
+      if (__ballot(pass != 0) != 0ull) {
+#pragma unroll
+        for (int b = 0; b < QB; ++b) {
+          const int qi = qbase + 16 * b + col;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) {
+            if (pass & (1u << (4 * b + jj))) {
+              const int slot = atomicAdd(&cnt[w][16 * b + col], 1);
+              if (slot < FL_CAP) {
+                const int64_t r = (jb + 4 * g + jj) * stride;
+                lists[((int64_t)qi * n_slabs + slab) * FL_CAP + slot] =
+                    make_key(acc[b][jj], (uint32_t)r);
+              }
+            }
+          }
+        }
+      }
+      if (more) {
+        if constexpr (PREFETCH) {
+#pragma unroll
+          for (int s = 0; s < KS; ++s) cur[s] = nxt[s];
+        } else {
+          const u32x4* p = row_ptr(jb + 16);
+#pragma unroll
+          for (int s = 0; s < KS; ++s) cur[s] = p[4 * s];
+        }
+      }
+    }
+  }
+  wave_sync();
+  if (lane < QPW) {
+    const int qi = qbase + lane;
+    if (qi < nq) counts[(int64_t)qi * n_slabs + slab] = cnt[w][lane];
+  }
+}
+
+
+// --------------------------------------------------------------------------- ring filter
+// The streaming filter for every level except the coarsest.  One 512-thread block (8 waves,
+// one block per CU) owns 8*QPW queries and a slab of sample rows.  Catalog tiles of TR rows
+// are DMA'd HBM -> LDS by all waves (global_load_lds_dwordx4, 1 KiB per wave-instruction)
+// into a 4-slot ring, PD = 3 tiles ahead, waited with a counted vmcnt and a raw s_barrier
+// (cdna_hip_programming.md section 5 "Pipelining across barriers").  Each wave reads the
+// A fragments of a tile with ds_read_b128 (16-B chunks XOR-swizzled by row on the DMA SOURCE
+// address, read with the same XOR: conflict-free) and runs RB x QB x KS MFMAs.  Candidates
+// (a >= theta) go to an LDS pool that is flushed to the per-(query, slab) lists in HBM only
+// when half full and at the end, so global stores almost never sit in the vmcnt queue in
+// front of the ring's DMA.
+template <int EP> struct RingCfg;
+template <> struct RingCfg<64> { static constexpr int TR = 64, QB = 2; };
+template <> struct RingCfg<128> { static constexpr int TR = 32, QB = 2; };
+template <> struct RingCfg<256> { static constexpr int TR = 32, QB = 2; };
+template <> struct RingCfg<384> { static constexpr int TR = 32, QB = 2; };
+template <> struct RingCfg<512> { static constexpr int TR = 16, QB = 1; };
+template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
+
+constexpr int RG_WAVES = 8, RG_PD = 3, RG_SLOTS = RG_PD + 1;
+constexpr int RG_POOL = 4096, RG_FLUSH = 2048;
+constexpr uint32_t RG_OVF = 1u << 30;  // marks a (query, slab) list whose entries were dropped
+
+template <int EP>
+constexpr int ring_qpb() { return RG_WAVES * 16 * RingCfg<EP>::QB; }
+template <int EP>
+constexpr int ring_smem() {
+  return RG_SLOTS * RingCfg<EP>::TR * EP * 2 + RG_POOL * 12 + ring_qpb<EP>() * 4 + 16;
+}
+
+// LDS ops of the ring kernel's append path, in inline asm: the compiler cannot prove they do
+// not alias the in-flight global_load_lds and would otherwise precede each with vmcnt(0),
+// draining the ring whenever a candidate is found.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ uint32_t lds_add_rtn(uint32_t addr, uint32_t v) {
+  uint32_t r;
+  asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(r) : "v"(addr), "v"(v) : "memory");
+  return r;
+}
+__device__ __forceinline__ void lds_or(uint32_t addr, uint32_t v) {
+  asm volatile("ds_or_b32 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_write64(uint32_t addr, uint64_t v) {
+  asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_write32(uint32_t addr, uint32_t v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void lds_barrier() {
+  // LDS traffic retired + workgroup barrier, WITHOUT the vmcnt(0) that __syncthreads() adds
+  // while a global_load_lds is in flight (it would drain the ring)
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int EP>
+__global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
+    const uint16_t* __restrict__ xb, int64_t ld, const float* __restrict__ q, int nq,
+    int64_t ldq, const float* __restrict__ theta, int64_t stride, int64_t n_sample,
+    int rows_per_slab, int n_slabs, int n_qt, uint64_t* __restrict__ lists,
+    int* __restrict__ counts) {
+  constexpr int TR = RingCfg<EP>::TR, QB = RingCfg<EP>::QB;
+  constexpr int KS = EP / 32, QPW = 16 * QB, QPB = RG_WAVES * QPW;
+  constexpr int CPR = EP / 8;  // 16-B chunks per row
+  constexpr int TILE_B = TR * EP * 2;
+  constexpr int PIECES = TILE_B / 1024, PPW = PIECES / RG_WAVES;
+  constexpr int FM = (CPR >= 16 ? 16 : CPR) - 1;
+  constexpr int RB = TR / 16;
+  static_assert(PIECES % RG_WAVES == 0, "tile must split into whole 1-KiB pieces per wave");
+  __shared__ __attribute__((aligned(16))) char smem[ring_smem<EP>()];
+  char* ring = smem;
+  uint64_t* pool_key = (uint64_t*)(smem + RG_SLOTS * TILE_B);
+  uint32_t* pool_meta = (uint32_t*)(pool_key + RG_POOL);
+  int* qcnt = (int*)(pool_meta + RG_POOL);
+  int* pool_n = qcnt + QPB;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int slab = lb / n_qt, qt = lb % n_qt;
+  const int qbase = qt * QPB + w * QPW;
+
+  bf16x8 qf[QB][KS];
+  float th[QB];
+#pragma unroll
+  for (int b = 0; b < QB; ++b) {
+    const int qi = qbase + 16 * b + col;
+    const bool v = qi < nq;
+    th[b] = v ? theta[qi] : __builtin_huge_valf();
+    const float* qp = q + (int64_t)(v ? qi : 0) * ldq + 8 * g;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const f32x4 v0 = *(const f32x4*)(qp + 32 * s);
+      const f32x4 v1 = *(const f32x4*)(qp + 32 * s + 4);
+      u32x4 u = {pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]), pack_bf16x2(v1[0], v1[1]),
+                 pack_bf16x2(v1[2], v1[3])};
+      qf[b][s] = __builtin_bit_cast(bf16x8, u);
+    }
+  }
+  for (int i = tid; i < QPB; i += 64 * RG_WAVES) qcnt[i] = 0;
+  if (tid == 0) *pool_n = 0;
+
+  const int64_t j0 = (int64_t)slab * rows_per_slab;
+  const int64_t j1 = (j0 + rows_per_slab < n_sample) ? j0 + rows_per_slab : n_sample;
+  const int n_tiles = j0 < j1 ? (int)((j1 - j0 + TR - 1) / TR) : 0;
+
+  // DMA of tile t into ring slot t % RG_SLOTS: piece p of the tile = LDS bytes [1024p, +1024),
+  // lane i writes 16-B chunk P = 64p + i = (row r, position pos); its source is chunk
+  // pos ^ (r & FM) of that row, so row r's logical chunk c lives at position c ^ (r & FM).
+  // Per lane the (row, column byte) of each piece is loop-invariant.
+  const int64_t row_bytes = stride * ld * 2;
+  int dr[PPW], dcol[PPW];
+#pragma unroll
+  for (int pp = 0; pp < PPW; ++pp) {
+    const int P = (w + RG_WAVES * pp) * 64 + lane;
+    dr[pp] = P / CPR;
+    dcol[pp] = 16 * ((P % CPR) ^ (dr[pp] & FM));
+  }
+  auto issue = [&](int t) {
+    char* slot = ring + (t % RG_SLOTS) * TILE_B;
+    const int64_t jt = j0 + (int64_t)t * TR;
+    const bool clamp = jt + TR > j1;  // wave-uniform: only the slab's last tile
+#pragma unroll
+    for (int pp = 0; pp < PPW; ++pp) {
+      int64_t j = jt + dr[pp];
+      if (clamp) j = j < j1 ? j : j1 - 1;
+      const char* src = (const char*)xb + j * row_bytes + dcol[pp];
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(
+                                           slot + (w + RG_WAVES * pp) * 1024),
+                                       16, 0, 0);
+    }
+  };
+  auto flush = [&](int n) {
+    for (int i = tid; i < n; i += 64 * RG_WAVES) {
+      const uint32_t m = pool_meta[i];
+      const int qi = qt * QPB + (int)(m >> 16);
+      lists[((int64_t)qi * n_slabs + slab) * FL_CAP + (m & 0xffff)] = pool_key[i];
+    }
+  };
+  // A-fragment read offsets: row r = 16rb + col, chunk c = 4s + g = 16(u) .. with s = 4u + v,
+  // so c ^ f = 4(s ^ h) + (g ^ (f & 3)) with f = r & FM, h = f >> 2  ->  the lane-dependent
+  // part depends on v only; u becomes an immediate (+256u bytes).
+  int lrd[RB][4];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    const int r = 16 * rb + col, f = r & FM, h = f >> 2;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) lrd[rb][v] = 16 * (r * CPR + (g ^ (f & 3))) + 64 * (v ^ h);
+  }
+
+  for (int t = 0; t < RG_PD && t < n_tiles; ++t) issue(t);
+  lds_barrier();  // counters initialised
+
+  for (int t = 0; t < n_tiles; ++t) {
+    const int younger = (n_tiles - 1 - t) < (RG_PD - 1) ? (n_tiles - 1 - t) : (RG_PD - 1);
+    if (younger >= 2) wait_vm<2 * PPW>();
+    else if (younger == 1) wait_vm<PPW>();
+    else wait_vm<0>();
+    lds_barrier();  // tile t landed for every wave; every wave finished step t-1
+    const int pn = *pool_n;
+    if (pn >= RG_FLUSH) {
+      flush(pn < RG_POOL ? pn : RG_POOL);
+      lds_barrier();
+      if (tid == 0) *pool_n = 0;
+      lds_barrier();
+    }
+    if (t + RG_PD < n_tiles) issue(t + RG_PD);
+
+    const char* slot = ring + (t % RG_SLOTS) * TILE_B;
+    f32x4 acc[RB][QB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int b = 0; b < QB; ++b) acc[rb][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        const u32x4 av = *(const u32x4*)(slot + lrd[rb][s & 3] + 256 * (s >> 2));
+        const bf16x8 a = __builtin_bit_cast(bf16x8, av);
+#pragma unroll
+        for (int b = 0; b < QB; ++b)
+          acc[rb][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[b][s], acc[rb][b], 0, 0, 0);
+      }
+    }
+    // fast reject: per query block the max of this lane's RB*4 scores against theta
+    bool any = false;
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      float m = acc[0][b][0];
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) m = fmaxf(m, acc[rb][b][jj]);
+      any = any || (m >= th[b]);
+    }
+    if (__ballot(any) == 0ull) continue;
+    // lane holds a(row j0 + t*TR + 16rb + 4g + jj, query qbase + 16b + col)
+    const int64_t jt = j0 + (int64_t)t * TR;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int b = 0; b < QB; ++b)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          if ((acc[rb][b][jj] >= th[b]) && (jt + 16 * rb + 4 * g + jj < j1)) {
+            const int ql = w * QPW + 16 * b + col;
+            const uint32_t slot_i = lds_add_rtn(lds_addr(&qcnt[ql]), 1u);
+            if ((slot_i & ~RG_OVF) < (uint32_t)FL_CAP) {
+              const uint32_t pi = lds_add_rtn(lds_addr(pool_n), 1u);
+              if (pi < (uint32_t)RG_POOL) {
+                const int64_t r = (jt + 16 * rb + 4 * g + jj) * stride;
+                lds_write64(lds_addr(&pool_key[pi]), make_key(acc[rb][b][jj], (uint32_t)r));
+                lds_write32(lds_addr(&pool_meta[pi]), ((uint32_t)ql << 16) | (slot_i & 0xffff));
+              } else {
+                lds_or(lds_addr(&qcnt[ql]), RG_OVF);
+              }
+            }
+          }
+        }
+  }
+  wait_vm<0>();
+  lds_barrier();
+  const int pn = *pool_n;
+  flush(pn < RG_POOL ? pn : RG_POOL);
+  for (int i = tid; i < QPB; i += 64 * RG_WAVES) {
+    const int qi = qt * QPB + i;
+    if (qi < nq) {
+      const uint32_t c = (uint32_t)qcnt[i];
+      counts[(int64_t)qi * n_slabs + slab] = (c & RG_OVF) ? FL_CAP + 1 : (int)c;
+    }
+  }
+}
+
+// --------------------------------------------------------------------------- select
+__device__ void block_sort_desc(uint64_t* buf, int n_pow2) {
+  for (int size = 2; size <= n_pow2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int i = threadIdx.x; i < n_pow2 / 2; i += blockDim.x) {
+        const int lo = 2 * stride * (i / stride) + (i % stride);
+        const int hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const uint64_t a = buf[lo], b = buf[hi];
+        if ((a < b) == up) {
+          buf[lo] = b;
+          buf[hi] = a;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ int pow2_at_least(int v) {
+  int p = 2;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+__device__ void flag_query(int qid, int* flags, int* qsel, int* qsel_n) {
+  if (atomicExch(&flags[qid], 1) == 0) {
+    const int pos = atomicAdd(qsel_n, 1);
+    qsel[pos] = qid;
+  }
+}
+
+// mode 0 (sample level): theta_out[q] = aref[q] = a_J, the J-th best a of the sample (its
+//   candidates are a superset of the sample's top J because theta <= a_J of a subset).
+// mode 1 (full catalog): A_k = k-th best a.  The level was filtered with theta = aref - eps2;
+//   that captures every row with a >= A_k - eps2 iff aref <= A_k: checked here, else the
+//   query is flagged for the exact fallback.  band[q] = candidates with a >= A_k - eps2.
+__global__ __launch_bounds__(256) void k_select(const uint64_t* __restrict__ lists,
+                                                const int* __restrict__ counts, int n_slabs,
+                                                int k, int J, float eps2, int mode,
+                                                float* __restrict__ theta_out,
+                                                float* __restrict__ aref,
+                                                uint64_t* __restrict__ band, int* band_n,
+                                                int* flags, int* qsel, int* qsel_n) {
+  __shared__ uint64_t buf[SEL_CAP];
+  __shared__ int total, bad;
+  const int qid = blockIdx.x;
+  if (threadIdx.x == 0) { total = 0; bad = flags[qid]; }
+  __syncthreads();
+  if (bad) {
+    if (threadIdx.x == 0 && mode == 0) theta_out[qid] = __builtin_huge_valf();
+    return;
+  }
+  const int* qc = counts + (int64_t)qid * n_slabs;
+  for (int s = threadIdx.x; s < n_slabs; s += blockDim.x) {
+    const int c = qc[s];
+    if (c > FL_CAP) bad = 1;  // benign race: every writer stores 1
+    else atomicAdd(&total, c);
+  }
+  __syncthreads();
+  if (!bad && total > SEL_CAP) bad = 1;
+  __syncthreads();
+  if (bad) {
+    if (threadIdx.x == 0) {
+      flag_query(qid, flags, qsel, qsel_n);
+      if (mode == 0) theta_out[qid] = __builtin_huge_valf();
+    }
+    return;
+  }
+  // gather: slab lists are contiguous per query -> walk (slab, slot) pairs
+  __shared__ int fill;
+  if (threadIdx.x == 0) fill = 0;
+  __syncthreads();
+  const uint64_t* ql = lists + (int64_t)qid * n_slabs * FL_CAP;
+  for (int64_t e = threadIdx.x; e < (int64_t)n_slabs * FL_CAP; e += blockDim.x) {
+    const int s = (int)(e / FL_CAP), i = (int)(e % FL_CAP);
+    if (i < qc[s]) buf[atomicAdd(&fill, 1)] = ql[e];
+  }
+  __syncthreads();
+  const int nb = total;
+  const int np = pow2_at_least(nb);
+  for (int i = nb + threadIdx.x; i < np; i += blockDim.x) buf[i] = 0ull;
+  block_sort_desc(buf, np);
+  if (mode == 0) {
+    const float aj = nb >= J ? key_float((uint32_t)(buf[J - 1] >> 32)) : -__builtin_huge_valf();
+    if (threadIdx.x == 0) {
+      theta_out[qid] = aj;
+      aref[qid] = aj;
+    }
+    return;
+  }
+  const float ak = nb >= k ? key_float((uint32_t)(buf[k - 1] >> 32)) : -__builtin_huge_valf();
+  if (!(ak >= aref[qid])) {  // optimistic threshold did not hold (or fewer than k rows)
+    if (threadIdx.x == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
+  // band = prefix of the sorted list with a >= ak - eps2 (NaN never enters the lists)
+  const float thr = ak - eps2;
+  __shared__ int bn;
+  if (threadIdx.x == 0) bn = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+    const float a = key_float((uint32_t)(buf[i] >> 32));
+    const bool in = a >= thr;
+    const bool next_in = (i + 1 < nb) && key_float((uint32_t)(buf[i + 1] >> 32)) >= thr;
+    if (in && !next_in) bn = i + 1;
+  }
+  __syncthreads();
+  const int nband = bn;
+  if (nband > BAND_CAP) {
+    if (threadIdx.x == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
+  for (int i = threadIdx.x; i < nband; i += blockDim.x) band[(int64_t)qid * BAND_CAP + i] = buf[i];
+  if (threadIdx.x == 0) band_n[qid] = nband;
+}
+
+// --------------------------------------------------------------------------- rerank
+template <int EP>
+__global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, int64_t ld,
+                                                const float* __restrict__ q, int64_t ldq,
+                                                const uint64_t* __restrict__ band,
+                                                const int* __restrict__ band_n,
+                                                const int* __restrict__ flags, int k,
+                                                int64_t row_base, float* __restrict__ out_s,
+                                                int64_t* __restrict__ out_i) {
+  __shared__ uint64_t buf[BAND_CAP];
+  __shared__ __attribute__((aligned(16))) float qs[EP];
+  const int qid = blockIdx.x;
+  if (flags[qid]) return;  // served by the exact fallback
+  const int nb = band_n[qid];
+  for (int i = threadIdx.x; i < EP; i += blockDim.x) qs[i] = q[(int64_t)qid * ldq + i];
+  __syncthreads();
+  for (int e = threadIdx.x; e < nb; e += blockDim.x) {
+    const uint32_t r = key_row(band[(int64_t)qid * BAND_CAP + e]);
+    const f32x4* xr = (const f32x4*)(db + (int64_t)r * ld);
+    float acc = 0.0f;
+#pragma unroll 4
+    for (int t = 0; t < EP / 16; ++t) {
+      const f32x4 x0 = xr[4 * t + 0], x1 = xr[4 * t + 1], x2 = xr[4 * t + 2], x3 = xr[4 * t + 3];
+      const float* qt = qs + 16 * t;
+      // canonical order: for i: for g: d = 16t + 4g + i
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc = fmaf(x0[i], qt[0 + i], acc);
+        acc = fmaf(x1[i], qt[4 + i], acc);
+        acc = fmaf(x2[i], qt[8 + i], acc);
+        acc = fmaf(x3[i], qt[12 + i], acc);
+      }
+    }
+    buf[e] = acc != acc ? 0ull : make_key(acc, r);
+  }
+  const int np = pow2_at_least(nb);
+  for (int i = nb + threadIdx.x; i < np; i += blockDim.x) buf[i] = 0ull;
+  block_sort_desc(buf, np);
+  for (int i = threadIdx.x; i < k; i += blockDim.x) {
+    float s = -__builtin_huge_valf();
+    int64_t ix = -1;
+    if (i < nb && buf[i] != 0ull) {
+      s = key_score(buf[i]);
+      ix = row_base + (int64_t)key_row(buf[i]);
+    }
+    out_s[(int64_t)qid * k + i] = s;
+    out_i[(int64_t)qid * k + i] = ix;
+  }
+}
+
+__global__ void k_fill_f32(float* x, int n, float v) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = v;
+}
+__global__ void k_add_f32(float* x, int n, float v) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = x[i] + v;
+}
+
+// --------------------------------------------------------------------------- host
+struct Level {
+  int64_t stride, n_sample;
+  int rows_per_slab, n_slabs, n_qt;
+  bool dense;
+};
+
+struct FilterPlan {
+  int n_levels, max_slabs, J;
+  Level lv[8];
+};
+
+// Levels over nested strided samples (stride 16^i, coarsest first).  The coarsest has
+// <= SEL_CAP/2 rows and is scored densely (every row a candidate); the others stream through
+// the ring kernel.  J = rows of a sample level's top list that feed the next threshold: the
+// full catalog has ~16*J rows above a_J(stride-16 sample), comfortably >= k.
+static FilterPlan plan_filter(int64_t n, int nq, int k, int ep) {
+  FilterPlan p;
+  // ~16*J full-catalog rows lie above a_J(stride-16 sample); J = k/8 + 12 keeps that count
+  // >= k with ~3.5 sigma margin on iid scores (fewer only under heavy clustering -> fallback)
+  p.J = (k + 7) / 8 + 12;
+  if (p.J > k) p.J = k;
+  int64_t strides[8];
+  int nl = 0;
+  int64_t s = 1;
+  while ((n + s - 1) / s > SEL_CAP / 2 && nl < 7) {
+    strides[nl++] = s;
+    s *= 16;
+  }
+  strides[nl++] = s;
+  p.n_levels = nl;
+  p.max_slabs = 1;
+  const int dense_qpb = FL_WAVES * 16 * (ep <= 384 ? 2 : 1);
+  int ring_qpb_v = RG_WAVES * 16 * (ep <= 384 ? 2 : 1);
+  for (int i = 0; i < nl; ++i) {
+    Level& L = p.lv[i];
+    L.stride = strides[nl - 1 - i];
+    L.n_sample = (n + L.stride - 1) / L.stride;
+    L.dense = i == 0;
+    const int qpb = L.dense ? dense_qpb : ring_qpb_v;
+    L.n_qt = (nq + qpb - 1) / qpb;
+    int64_t sl;
+    if (L.dense) {
+      sl = (L.n_sample + FL_CAP / 2 - 1) / (FL_CAP / 2);  // every row is a candidate
+    } else {
+      // >= ~3 blocks per CU in flight over the level; slabs >= 8 tiles long
+      sl = (768 + L.n_qt - 1) / L.n_qt;
+      const int64_t max_by_rows = (L.n_sample + 255) / 256;
+      if (sl > max_by_rows) sl = max_by_rows;
+    }
+    if (sl < 1) sl = 1;
+    int64_t r = (L.n_sample + sl - 1) / sl;
+    r = (r + 63) / 64 * 64;
+    L.rows_per_slab = (int)r;
+    L.n_slabs = (int)((L.n_sample + r - 1) / r);
+    if (L.n_slabs > p.max_slabs) p.max_slabs = L.n_slabs;
+  }
+  return p;
+}
+
+struct FilterWs {
+  uint64_t* lists;
+  int* counts;
+  float* theta;
+  float* aref;
+  uint64_t* band;
+  int* band_n;
+  int* flags;  // flags[nq], qsel[nq], qsel_n[1] are contiguous (one memset)
+  int* qsel;
+  int* qsel_n;
+  void* scan_ws;
+  int64_t scan_ws_bytes;
+  int64_t total;
+};
+
+static int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
+
+static FilterWs carve(void* base, const FilterPlan& p, int64_t n, int d, int nq, int k) {
+  FilterWs w;
+  // base == nullptr: size / offset query -> pointers are offsets from a fake 4 KiB base
+  char* c = base ? (char*)base : (char*)4096;
+  int64_t off = 0;
+  auto take = [&](int64_t bytes) {
+    char* r = c + off;
+    off += align256(bytes);
+    return r;
+  };
+  w.lists = (uint64_t*)take((int64_t)nq * p.max_slabs * FL_CAP * 8);
+  w.counts = (int*)take((int64_t)nq * p.max_slabs * 4);
+  w.theta = (float*)take((int64_t)nq * 4);
+  w.aref = (float*)take((int64_t)nq * 4);
+  w.band = (uint64_t*)take((int64_t)nq * BAND_CAP * 8);
+  w.band_n = (int*)take((int64_t)nq * 4);
+  int* fl = (int*)take(((int64_t)2 * nq + 1) * 4);
+  w.flags = fl;
+  w.qsel = fl + nq;
+  w.qsel_n = fl + 2 * nq;
+  int64_t sb = 0;
+  tt_scan_workspace_bytes(n, d, nq, k, &sb);
+  w.scan_ws_bytes = sb;
+  w.scan_ws = take(sb);
+  w.total = off;
+  return w;
+}
+
+template <int EP>
+static void launch_level(const Level& L, const uint16_t* xb, int64_t n, int64_t ld,
+                         const float* q, int nq, int64_t ldq, const FilterWs& w,
+                         hipStream_t st) {
+  const int nblk = L.n_qt * L.n_slabs;
+  if (L.dense) {
+    constexpr int QB = EP <= 384 ? 2 : 1;
+    hipLaunchKernelGGL((k_filter_dense<EP, QB>), dim3(nblk), dim3(64 * FL_WAVES), 0, st, xb, n,
+                       ld, q, nq, ldq, w.theta, L.stride, L.n_sample, L.rows_per_slab,
+                       L.n_slabs, L.n_qt, w.lists, w.counts);
+  } else {
+    hipLaunchKernelGGL((k_filter_ring<EP>), dim3(nblk), dim3(64 * RG_WAVES), 0, st, xb, ld, q,
+                       nq, ldq, w.theta, L.stride, L.n_sample, L.rows_per_slab, L.n_slabs,
+                       L.n_qt, w.lists, w.counts);
+  }
+}
+
+}  // namespace tt
+
+using namespace tt;
+
+// implemented in tt_scan.hip: exact f32 scan restricted to a device-side query list
+extern "C" int tt_scan_topk_f32_select(const float* db, int64_t n, int32_t d, int64_t ld_db,
+                                       int64_t row_base, const float* q, int32_t nq,
+                                       int64_t ld_q, int32_t k, const int32_t* qsel,
+                                       const int32_t* qsel_n, float* out_score,
+                                       int64_t* out_idx, void* workspace,
+                                       int64_t workspace_bytes, void* stream);
+
+extern "C" int tt_filter_workspace_bytes(int64_t n, int32_t d, int32_t nq, int32_t k,
+                                         int64_t* bytes) {
+  TT_REQUIRE(bytes != nullptr, "bytes == NULL");
+  TT_REQUIRE(n >= 1 && nq >= 1 && k >= 1, "n, nq, k must be >= 1");
+  const int ep = tt_padded_dim(d);
+  TT_REQUIRE(ep > 0, "d > 768");
+  const FilterPlan p = plan_filter(n, nq, k, ep);
+  *bytes = carve(nullptr, p, n, d, nq, k).total;
+  return TT_OK;
+}
+
+extern "C" int tt_filter_fallback_offset(int64_t n, int32_t d, int32_t nq, int32_t k,
+                                         int64_t* offset) {
+  TT_REQUIRE(offset != nullptr && n >= 1 && nq >= 1 && k >= 1, "bad arguments");
+  const int ep = tt_padded_dim(d);
+  TT_REQUIRE(ep > 0, "d > 768");
+  const FilterPlan p = plan_filter(n, nq, k, ep);
+  const FilterWs w = carve(nullptr, p, n, d, nq, k);
+  *offset = (int64_t)((char*)w.qsel_n - (char*)4096);
+  return TT_OK;
+}
+
+extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n,
+                                    int32_t d, int64_t ld_db, int64_t row_base, const float* q,
+                                    int32_t nq, int64_t ld_q, int32_t k, float eps,
+                                    float* out_score, int64_t* out_idx, void* workspace,
+                                    int64_t workspace_bytes, void* stream, void* ev_start,
+                                    void* ev_stop) {
+  TT_REQUIRE(n >= 1 && n <= 0x7fffffffLL, "need 1 <= n < 2^31");
+  TT_REQUIRE(nq >= 0, "nq < 0");
+  TT_REQUIRE(k >= 1 && k <= n, "need 1 <= k <= n");
+  TT_REQUIRE(eps >= 0.0f, "eps < 0");
+  if (nq == 0) return TT_OK;
+  if (k > FL_KMAX) return fail(TT_ERR_UNSUPPORTED, "tt_scan_topk_bf16f32: k > 128");
+  const int ep = tt_padded_dim(d);
+  if (ep < 0) return fail(TT_ERR_UNSUPPORTED, "tt_scan_topk_bf16f32: d > 768");
+  TT_REQUIRE(ld_db >= ep && ld_q >= ep && ld_db % 8 == 0 && ld_q % 4 == 0,
+             "ld must be >= tt_padded_dim(d), ld_db % 8 == 0 (zero padded)");
+  TT_REQUIRE(((uintptr_t)db % 16) == 0 && ((uintptr_t)db_bf16 % 16) == 0 &&
+                 ((uintptr_t)q % 16) == 0, "pointers must be 16-B aligned");
+  const FilterPlan p = plan_filter(n, nq, k, ep);
+  const FilterWs w = carve(workspace, p, n, d, nq, k);
+  if (workspace == nullptr || workspace_bytes < w.total)
+    return fail(TT_ERR_WORKSPACE, "tt_scan_topk_bf16f32: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(w.flags, 0, ((size_t)2 * nq + 1) * 4, st) != hipSuccess)
+    return fail(TT_ERR_LAUNCH, "hipMemsetAsync(flags)");
+  const float eps2 = 2.0f * eps;
+  const unsigned fill_grid = (unsigned)((nq + 255) / 256);
+  hipLaunchKernelGGL(k_fill_f32, dim3(fill_grid), dim3(256), 0, st, w.theta, nq,
+                     -__builtin_huge_valf());
+  hipLaunchKernelGGL(k_fill_f32, dim3(fill_grid), dim3(256), 0, st, w.aref, nq,
+                     -__builtin_huge_valf());
+  for (int li = 0; li < p.n_levels; ++li) {
+    const Level& L = p.lv[li];
+    const bool last = li == p.n_levels - 1;
+    if (last && li > 0)  // full-catalog level: theta = a_J(stride-16 sample) - 2 eps
+      hipLaunchKernelGGL(k_add_f32, dim3(fill_grid), dim3(256), 0, st, w.theta, nq, -eps2);
+    if (last && ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
+      return fail(TT_ERR_LAUNCH, "hipEventRecord(start)");
+    switch (ep) {
+      case 64: launch_level<64>(L, db_bf16, n, ld_db, q, nq, ld_q, w, st); break;
+      case 128: launch_level<128>(L, db_bf16, n, ld_db, q, nq, ld_q, w, st); break;
+      case 256: launch_level<256>(L, db_bf16, n, ld_db, q, nq, ld_q, w, st); break;
+      case 384: launch_level<384>(L, db_bf16, n, ld_db, q, nq, ld_q, w, st); break;
+      case 512: launch_level<512>(L, db_bf16, n, ld_db, q, nq, ld_q, w, st); break;
+      case 768: launch_level<768>(L, db_bf16, n, ld_db, q, nq, ld_q, w, st); break;
+      default: return fail(TT_ERR_UNSUPPORTED, "bad padded dim");
+    }
+    int rc = check_launch("k_filter");
+    if (rc) return rc;
+    if (last && ev_stop && hipEventRecord((hipEvent_t)ev_stop, st) != hipSuccess)
+      return fail(TT_ERR_LAUNCH, "hipEventRecord(stop)");
+    hipLaunchKernelGGL(k_select, dim3(nq), dim3(256), 0, st, w.lists, w.counts, L.n_slabs, k,
+                       p.J, eps2, last ? 1 : 0, w.theta, w.aref, w.band, w.band_n, w.flags,
+                       w.qsel, w.qsel_n);
+    rc = check_launch("k_select");
+    if (rc) return rc;
+  }
+  switch (ep) {
+#define TT_RR(E)                                                                              \
+  case E:                                                                                     \
+    hipLaunchKernelGGL(k_rerank<E>, dim3(nq), dim3(256), 0, st, db, ld_db, q, ld_q, w.band,   \
+                       w.band_n, w.flags, k, row_base, out_score, out_idx);                   \
+    break;
+    TT_RR(64) TT_RR(128) TT_RR(256) TT_RR(384) TT_RR(512) TT_RR(768)
+#undef TT_RR
+  }
+  int rc = check_launch("k_rerank");
+  if (rc) return rc;
+  // exact fallback for flagged queries (blocks exit at once when none is flagged)
+  return tt_scan_topk_f32_select(db, n, d, ld_db, row_base, q, nq, ld_q, k, w.qsel, w.qsel_n,
+                                 out_score, out_idx, w.scan_ws, w.scan_ws_bytes, stream);
+}

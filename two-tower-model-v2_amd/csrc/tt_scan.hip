@@ -142,19 +142,23 @@ template <int EP, class Cfg>
 __global__ __launch_bounds__(64 * Cfg::kWaves, ((EP <= 384 && Cfg::kWaves > 1) ? 2 : 1)) void k_scan_topk_f32(
     const float* __restrict__ db, int64_t n, int64_t ld_db, const float* __restrict__ q,
     int nq, int64_t ld_q, int k, int rows_per_slab, int n_slabs,
-    float* __restrict__ ws_score, int* __restrict__ ws_row, int* __restrict__ ws_cnt) {
+    float* __restrict__ ws_score, int* __restrict__ ws_row, int* __restrict__ ws_cnt,
+    const int* __restrict__ qsel, const int* __restrict__ qsel_n) {
   constexpr int SC_QPB = Cfg::kQPB, SC_CAND = Cfg::kCand;
   __shared__ typename Cfg::Smem sm;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ql = lane & 15, g = lane >> 4;
   const int qt = blockIdx.x, slab = blockIdx.y;
+  if (qsel) nq = *qsel_n;  // fallback mode: slots 0..nq-1 map to queries qsel[slot]
+  if (qt * SC_QPB >= nq) return;
   const int qi = qt * SC_QPB + w * SC_QPW + ql;
   const bool qvalid = qi < nq;
 
   // query fragment: dims 16t + 4g .. +3 of query qi
   f32x4 qf[EP / 16];
   {
-    const float* qp = q + (int64_t)(qvalid ? qi : 0) * ld_q + 4 * g;
+    const int qrow = qvalid ? (qsel ? qsel[qi] : qi) : 0;
+    const float* qp = q + (int64_t)qrow * ld_q + 4 * g;
 #pragma unroll
     for (int t = 0; t < EP / 16; ++t) {
       f32x4 v = *(const f32x4*)(qp + 16 * t);
@@ -279,11 +283,14 @@ __global__ __launch_bounds__(256) void k_merge_lists(const float* __restrict__ i
                                                      int n_lists, int64_t list_stride_q,
                                                      int64_t list_stride_l, int k_in, int k,
                                                      int64_t row_base, float* out_s,
-                                                     int64_t* out_i) {
+                                                     int64_t* out_i, const int* qsel,
+                                                     const int* qsel_n) {
   __shared__ uint64_t buf[MG_CAP];
   __shared__ int bcnt;
   __shared__ uint32_t th_key;
   const int qid = blockIdx.x;
+  if (qsel && qid >= *qsel_n) return;
+  const int64_t orow = qsel ? qsel[qid] : qid;
   const float* qs = in_s + (int64_t)qid * list_stride_q;
   const IdxT* qix = in_i + (int64_t)qid * list_stride_q;
   const int* qc = in_c ? in_c + (int64_t)qid * n_lists : nullptr;
@@ -346,8 +353,8 @@ __global__ __launch_bounds__(256) void k_merge_lists(const float* __restrict__ i
       s = key_score(buf[i]);
       ix = row_base + (int64_t)key_row(buf[i]);
     }
-    out_s[(int64_t)qid * k + i] = s;
-    out_i[(int64_t)qid * k + i] = ix;
+    out_s[orow * k + i] = s;
+    out_i[orow * k + i] = ix;
   }
 }
 
@@ -402,12 +409,11 @@ extern "C" int tt_scan_workspace_bytes(int64_t n, int32_t d, int32_t nq, int32_t
   return TT_OK;
 }
 
-extern "C" int tt_scan_topk_f32_timed(const float* db, int64_t n, int32_t d, int64_t ld_db,
-                                      int64_t row_base, const float* q, int32_t nq,
-                                      int64_t ld_q, int32_t k, float* out_score,
-                                      int64_t* out_idx, void* workspace,
-                                      int64_t workspace_bytes, void* stream, void* ev_start,
-                                      void* ev_stop) {
+static int scan_f32_impl(const float* db, int64_t n, int32_t d, int64_t ld_db,
+                         int64_t row_base, const float* q, int32_t nq, int64_t ld_q, int32_t k,
+                         const int32_t* qsel, const int32_t* qsel_n, float* out_score,
+                         int64_t* out_idx, void* workspace, int64_t workspace_bytes,
+                         void* stream, void* ev_start, void* ev_stop) {
   TT_REQUIRE(n >= 1, "empty catalog");
   TT_REQUIRE(n <= 0x7fffffffLL, "shard rows must fit int32");
   TT_REQUIRE(nq >= 0, "nq < 0");
@@ -435,10 +441,12 @@ extern "C" int tt_scan_topk_f32_timed(const float* db, int64_t n, int32_t d, int
   case E:                                                                                    \
     if (wide)                                                                                \
       hipLaunchKernelGGL((k_scan_topk_f32<E, CfgWide>), grid, block, 0, st, db, n, ld_db, q, \
-                         nq, ld_q, k, p.rows_per_slab, p.n_slabs, ws_s, ws_r, ws_c);         \
+                         nq, ld_q, k, p.rows_per_slab, p.n_slabs, ws_s, ws_r, ws_c, qsel,    \
+                         qsel_n);                                                            \
     else                                                                                     \
       hipLaunchKernelGGL((k_scan_topk_f32<E, CfgNarrow>), grid, block, 0, st, db, n, ld_db,  \
-                         q, nq, ld_q, k, p.rows_per_slab, p.n_slabs, ws_s, ws_r, ws_c);      \
+                         q, nq, ld_q, k, p.rows_per_slab, p.n_slabs, ws_s, ws_r, ws_c, qsel, \
+                         qsel_n);                                                            \
     break;
   if (ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "tt_scan_topk_f32_timed: hipEventRecord(start) failed");
@@ -459,16 +467,39 @@ extern "C" int tt_scan_topk_f32_timed(const float* db, int64_t n, int32_t d, int
     return fail(TT_ERR_LAUNCH, "tt_scan_topk_f32_timed: hipEventRecord(stop) failed");
   hipLaunchKernelGGL(k_merge_lists<int>, dim3(nq), dim3(256), 0, st, ws_s, ws_r, ws_c,
                      p.n_slabs, (int64_t)p.n_slabs * k, (int64_t)k, k, k, row_base, out_score,
-                     out_idx);
+                     out_idx, qsel, qsel_n);
   return check_launch("k_merge_lists");
+}
+
+extern "C" int tt_scan_topk_f32_timed(const float* db, int64_t n, int32_t d, int64_t ld_db,
+                                      int64_t row_base, const float* q, int32_t nq,
+                                      int64_t ld_q, int32_t k, float* out_score,
+                                      int64_t* out_idx, void* workspace,
+                                      int64_t workspace_bytes, void* stream, void* ev_start,
+                                      void* ev_stop) {
+  return scan_f32_impl(db, n, d, ld_db, row_base, q, nq, ld_q, k, nullptr, nullptr, out_score,
+                       out_idx, workspace, workspace_bytes, stream, ev_start, ev_stop);
 }
 
 extern "C" int tt_scan_topk_f32(const float* db, int64_t n, int32_t d, int64_t ld_db,
                                 int64_t row_base, const float* q, int32_t nq, int64_t ld_q,
                                 int32_t k, float* out_score, int64_t* out_idx, void* workspace,
                                 int64_t workspace_bytes, void* stream) {
-  return tt_scan_topk_f32_timed(db, n, d, ld_db, row_base, q, nq, ld_q, k, out_score, out_idx,
-                                workspace, workspace_bytes, stream, nullptr, nullptr);
+  return scan_f32_impl(db, n, d, ld_db, row_base, q, nq, ld_q, k, nullptr, nullptr, out_score,
+                       out_idx, workspace, workspace_bytes, stream, nullptr, nullptr);
+}
+
+// Exact scan of the queries listed on the device (qsel[0 .. *qsel_n)); outputs go to the
+// listed rows of out_*.  Launched for nq slots; blocks beyond *qsel_n exit immediately.
+extern "C" int tt_scan_topk_f32_select(const float* db, int64_t n, int32_t d, int64_t ld_db,
+                                       int64_t row_base, const float* q, int32_t nq,
+                                       int64_t ld_q, int32_t k, const int32_t* qsel,
+                                       const int32_t* qsel_n, float* out_score,
+                                       int64_t* out_idx, void* workspace,
+                                       int64_t workspace_bytes, void* stream) {
+  TT_REQUIRE(qsel != nullptr && qsel_n != nullptr, "qsel / qsel_n must be device pointers");
+  return scan_f32_impl(db, n, d, ld_db, row_base, q, nq, ld_q, k, qsel, qsel_n, out_score,
+                       out_idx, workspace, workspace_bytes, stream, nullptr, nullptr);
 }
 
 extern "C" int tt_topk_merge_f32(const float* in_score, const int64_t* in_idx, int32_t n_lists,
@@ -480,6 +511,7 @@ extern "C" int tt_topk_merge_f32(const float* in_score, const int64_t* in_idx, i
   // layout [n_lists][nq][k_in]: list stride nq*k_in, query stride k_in
   hipLaunchKernelGGL(k_merge_lists<int64_t>, dim3(nq), dim3(256), 0, (hipStream_t)stream,
                      in_score, in_idx, (const int*)nullptr, n_lists, (int64_t)k_in,
-                     (int64_t)nq * k_in, k_in, k, (int64_t)0, out_score, out_idx);
+                     (int64_t)nq * k_in, k_in, k, (int64_t)0, out_score, out_idx,
+                     (const int*)nullptr, (const int*)nullptr);
   return check_launch("tt_topk_merge_f32");
 }

@@ -79,6 +79,59 @@ def scan_topk(db: torch.Tensor, n: int, d: int, q: torch.Tensor, k: int, row_bas
     return out
 
 
+FILTER_KMAX = 128
+
+
+def filter_eps(ep: int, xmax: float = 1.00001, qmax: float = 1.00001) -> float:
+    """Bound on |bf16 score - canonical f32 score| (include/twotower_hip.h)."""
+    return ((2.0 ** -8 + 2.0 ** -18) + 3.0 * ep * 2.0 ** -24) * xmax * qmax * 1.001
+
+
+def filter_workspace_bytes(n: int, d: int, nq: int, k: int) -> int:
+    b = ctypes.c_int64(0)
+    check(lib().tt_filter_workspace_bytes(n, d, nq, k, ctypes.byref(b)),
+          "tt_filter_workspace_bytes")
+    return b.value
+
+
+def filter_fallback_count(workspace: torch.Tensor, n: int, d: int, nq: int, k: int) -> int:
+    """Queries of the last scan_topk_bf16 call (with this workspace) that took the exact
+    fallback.  Diagnostic: synchronises."""
+    off = ctypes.c_int64(0)
+    check(lib().tt_filter_fallback_offset(n, d, nq, k, ctypes.byref(off)),
+          "tt_filter_fallback_offset")
+    return int(workspace[off.value:off.value + 4].view(torch.int32).item())
+
+
+def scan_topk_bf16(db: torch.Tensor, db16: torch.Tensor, n: int, d: int, q: torch.Tensor,
+                   k: int, eps: float, row_base: int = 0, workspace: torch.Tensor = None,
+                   out=None, events=(None, None)):
+    """Exact top-k (bit-identical to scan_topk) via the bf16 filter + f32 re-rank (k <= 128)."""
+    _check_2d(db, "db")
+    _check_2d(db16, "db16", torch.bfloat16)
+    _check_2d(q, "q")
+    if db16.shape[0] < n or db16.stride(0) != db.stride(0):
+        raise ValueError("db16 must be the bf16 image of db (same rows and leading dim)")
+    nq = q.shape[0]
+    if not (1 <= k <= min(n, FILTER_KMAX)) or n > db.shape[0]:
+        raise ValueError(f"scan_topk_bf16: need 1 <= k ({k}) <= min(n, 128), n <= rows")
+    if out is None:
+        out = (torch.empty((nq, k), dtype=_f32, device=q.device),
+               torch.empty((nq, k), dtype=torch.int64, device=q.device))
+    if nq == 0:
+        return out
+    need = filter_workspace_bytes(n, d, nq, k)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=q.device)
+    e0, e1 = events
+    check(lib().tt_scan_topk_bf16f32(
+        _ptr(db), _ptr(db16), n, d, db.stride(0), row_base, _ptr(q), nq, q.stride(0), k,
+        ctypes.c_float(eps), _ptr(out[0]), _ptr(out[1]), _ptr(workspace), workspace.numel(),
+        stream_ptr(), e0.cuda_event if e0 is not None else None,
+        e1.cuda_event if e1 is not None else None), "tt_scan_topk_bf16f32")
+    return out
+
+
 def merge_topk(scores: torch.Tensor, idx: torch.Tensor, k: int):
     """[L, nq, k_in] per-shard sorted lists (global ids) -> [nq, k]."""
     require_device(scores, "scores")

@@ -36,8 +36,19 @@ class FlatIPIndex:
         self.ep = _lib.padded_dim(self.d)
         self.device = device or _lib.device()
         self.xb = torch.zeros((0, self.ep), dtype=torch.float32, device=self.device)
+        self.xb16 = torch.zeros((0, self.ep), dtype=torch.bfloat16, device=self.device)
+        self.xmax = 0.0  # max row norm: scales the bf16 filter's error bound
         self.ntotal = 0
         self._ws = None
+
+    def _append(self, rows: torch.Tensor, rows16: torch.Tensor) -> None:
+        if self.ntotal:
+            rows = torch.cat([self.xb[: self.ntotal], rows])
+            rows16 = torch.cat([self.xb16[: self.ntotal], rows16])
+        self.xb, self.xb16 = rows, rows16
+        self.ntotal = rows.shape[0]
+        if self.ntotal:  # one-time build statistic
+            self.xmax = float(torch.linalg.vector_norm(self.xb, dim=1).nan_to_num(0.0).max())
 
     # faiss-style add of ALREADY-normalised float32 rows (host or device)
     def add(self, x) -> None:
@@ -46,8 +57,7 @@ class FlatIPIndex:
             raise ValueError(f"add: expected [n, {self.d}] float32")
         rows = torch.zeros((x.shape[0], self.ep), dtype=torch.float32, device=self.device)
         rows[:, : self.d].copy_(x, non_blocking=False)
-        self.xb = torch.cat([self.xb[: self.ntotal], rows]) if self.ntotal else rows
-        self.ntotal = self.xb.shape[0]
+        self._append(rows, rows.to(torch.bfloat16))
 
     def add_normalized_from(self, x) -> None:
         """Copy raw rows to the device and normalise there (x / (||x|| + 1e-8))."""
@@ -56,17 +66,28 @@ class FlatIPIndex:
             raise ValueError(f"add: expected [n, {self.d}]")
         raw = torch.zeros((x.shape[0], self.ep), dtype=torch.float32, device=self.device)
         raw[:, : self.d].copy_(x.to(torch.float32))
-        kernels.l2norm_rows(raw, self.d, _lib.TT_NORM_ADD_EPS, out=raw)
-        self.xb = torch.cat([self.xb[: self.ntotal], raw]) if self.ntotal else raw
-        self.ntotal = self.xb.shape[0]
+        raw16 = torch.empty((x.shape[0], self.ep), dtype=torch.bfloat16, device=self.device)
+        kernels.l2norm_rows(raw, self.d, _lib.TT_NORM_ADD_EPS, out=raw, out_bf16=raw16)
+        self._append(raw, raw16)
 
-    def search_device(self, q: torch.Tensor, k: int):
-        """q: [nq, ep] normalised device rows -> (scores [nq,k], labels [nq,k]) on device."""
+    def search_device(self, q: torch.Tensor, k: int, method: str = "auto", qmax: float = 1.00001):
+        """q: [nq, ep] normalised device rows -> (scores [nq,k], labels [nq,k]) on device.
+
+        method "auto": bf16 filter + exact f32 re-rank for k <= 128, else the f32 scan;
+        "f32" / "bf16" force one.  Both give bit-identical results."""
         if k < 1:
             raise RuntimeError("Error: 'k > 0' failed")  # faiss' own assertion text
-        need = kernels.scan_workspace_bytes(self.ntotal, self.d, q.shape[0], k)
+        use_bf16 = method == "bf16" or (method == "auto" and k <= kernels.FILTER_KMAX)
+        if use_bf16:
+            need = kernels.filter_workspace_bytes(self.ntotal, self.d, q.shape[0], k)
+        else:
+            need = kernels.scan_workspace_bytes(self.ntotal, self.d, q.shape[0], k)
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        if use_bf16:
+            eps = kernels.filter_eps(self.ep, max(self.xmax, 1e-30), qmax)
+            return kernels.scan_topk_bf16(self.xb, self.xb16, self.ntotal, self.d, q, k, eps,
+                                          workspace=self._ws)
         return kernels.scan_topk(self.xb, self.ntotal, self.d, q, k, workspace=self._ws)
 
     def search(self, x: np.ndarray, k: int):
