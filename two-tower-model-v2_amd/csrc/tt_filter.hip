@@ -25,6 +25,8 @@
 //      exit immediately when the list is empty.
 #include "tt_common.hpp"
 
+#include <type_traits>
+
 namespace tt {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -189,8 +191,20 @@ template <> struct RingCfg<384> { static constexpr int TR = 32, QB = 2; };
 template <> struct RingCfg<512> { static constexpr int TR = 16, QB = 1; };
 template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 
+// Experiment switches (timing-only builds, results WRONG when set): tools/exp_filter.sh
+#ifndef TT_EXP_NODMA
+#define TT_EXP_NODMA 0  // skip the DMA issue/wait: MFMA + selection on stale LDS
+#endif
+#ifndef TT_EXP_NOSEL
+#define TT_EXP_NOSEL 0  // skip candidate selection
+#endif
+#ifndef TT_EXP_NOBAR
+#define TT_EXP_NOBAR 0  // skip the per-step barrier
+#endif
 constexpr int RG_WAVES = 8, RG_PD = 3, RG_SLOTS = RG_PD + 1;
-constexpr int RG_POOL = 4096, RG_FLUSH = 2048;
+constexpr int RG_POOL = 4096;                  // pool entries per block
+constexpr int RG_WPOOL = RG_POOL / RG_WAVES;   // ... per wave (wave-private region)
+constexpr int RG_WFLUSH = RG_WPOOL / 2;
 constexpr uint32_t RG_OVF = 1u << 30;  // marks a (query, slab) list whose entries were dropped
 
 template <int EP>
@@ -226,6 +240,29 @@ template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+// A-fragment reads issued by hand so that their lgkmcnt waits are counted: the compiler's own
+// schedule drains lgkmcnt(0) after every pair of reads (serialising LDS latency into the MFMA
+// stream).  lds_wait_tie<N> waits until at most N LDS operations are outstanding and ties the
+// fragment registers through the wait, so no consumer can be scheduled above it.
+template <int N, typename F, int I = 0>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, F, I + 1>(static_cast<F&&>(f));
+  }
+}
+template <int OFF>
+__device__ __forceinline__ u32x4 lds_read128(uint32_t addr) {
+  u32x4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+  return r;
+}
+template <int N>
+__device__ __forceinline__ void lds_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N));
+}
+__device__ __forceinline__ void reg_tie(u32x4& r) { asm volatile("" : "+v"(r)); }
+
 __device__ __forceinline__ void lds_barrier() {
   // LDS traffic retired + workgroup barrier, WITHOUT the vmcnt(0) that __syncthreads() adds
   // while a global_load_lds is in flight (it would drain the ring)
@@ -251,7 +288,6 @@ __global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
   uint64_t* pool_key = (uint64_t*)(smem + RG_SLOTS * TILE_B);
   uint32_t* pool_meta = (uint32_t*)(pool_key + RG_POOL);
   int* qcnt = (int*)(pool_meta + RG_POOL);
-  int* pool_n = qcnt + QPB;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -278,7 +314,6 @@ __global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
     }
   }
   for (int i = tid; i < QPB; i += 64 * RG_WAVES) qcnt[i] = 0;
-  if (tid == 0) *pool_n = 0;
 
   const int64_t j0 = (int64_t)slab * rows_per_slab;
   const int64_t j1 = (j0 + rows_per_slab < n_sample) ? j0 + rows_per_slab : n_sample;
@@ -311,12 +346,22 @@ __global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
                                        16, 0, 0);
     }
   };
-  auto flush = [&](int n) {
-    for (int i = tid; i < n; i += 64 * RG_WAVES) {
-      const uint32_t m = pool_meta[i];
-      const int qi = qt * QPB + (int)(m >> 16);
-      lists[((int64_t)qi * n_slabs + slab) * FL_CAP + (m & 0xffff)] = pool_key[i];
+  // Candidate pool: each wave owns RG_WPOOL entries and the counters of its own queries, so
+  // appends need no atomics and no cross-wave synchronisation; the pool position `wn` is a
+  // wave-uniform (scalar) count.  Flush (rare): per-(query, slab) list slots are assigned by
+  // LDS atomics on the wave's own counters.  In-order LDS within a wave orders everything.
+  uint64_t* wkey = pool_key + w * RG_WPOOL;
+  uint32_t* wmeta = pool_meta + w * RG_WPOOL;
+  uint32_t wn = 0;
+  auto flush = [&]() {
+    const int n = wn < (uint32_t)RG_WPOOL ? (int)wn : RG_WPOOL;
+    for (int i = lane; i < n; i += 64) {
+      const uint32_t ql = wmeta[i];
+      const uint32_t slot_i = lds_add_rtn(lds_addr(&qcnt[ql]), 1u) & ~RG_OVF;
+      if (slot_i < (uint32_t)FL_CAP)
+        lists[((int64_t)(qt * QPB + (int)ql) * n_slabs + slab) * FL_CAP + slot_i] = wkey[i];
     }
+    wn = 0;
   };
   // A-fragment read offsets: row r = 16rb + col, chunk c = 4s + g = 16(u) .. with s = 4u + v,
   // so c ^ f = 4(s ^ h) + (g ^ (f & 3)) with f = r & FM, h = f >> 2  ->  the lane-dependent
@@ -329,86 +374,155 @@ __global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
     for (int v = 0; v < 4; ++v) lrd[rb][v] = 16 * (r * CPR + (g ^ (f & 3))) + 64 * (v ^ h);
   }
 
-  for (int t = 0; t < RG_PD && t < n_tiles; ++t) issue(t);
-  lds_barrier();  // counters initialised
-
-  for (int t = 0; t < n_tiles; ++t) {
-    const int younger = (n_tiles - 1 - t) < (RG_PD - 1) ? (n_tiles - 1 - t) : (RG_PD - 1);
+  // Fast reject of a finished tile (lane: RB*4 scores per query block): per-block maxima.
+  // NaN scores (the t = 0 placeholder, NaN rows) never pass a >= test.
+  auto tile_max = [&](const f32x4 (&sc)[RB][QB], float (&mx)[QB]) {
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      float m = sc[0][b][0];
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) m = fmaxf(m, sc[rb][b][jj]);
+      mx[b] = m;
+    }
+  };
+  // Append the passing scores of tile t (lane: rows jt + 16rb + 4g + jj, query 16b + col).
+  // One v_cmp + scalar branch per candidate slot; lanes of a non-empty slot write at
+  // wn + (passing lanes below).  An entry past the wave's pool marks its query overflowed
+  // (-> exact fallback).  Rows past the slab end (its last tile only) are masked to -inf first.
+  auto append = [&](f32x4 (&sc)[RB][QB], const float (&mx)[QB], int t) {
+    const int64_t jt = j0 + (int64_t)t * TR;
+    if (jt + TR > j1) {
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          if (jt + 16 * rb + 4 * g + jj >= j1)
+#pragma unroll
+            for (int b = 0; b < QB; ++b) sc[rb][b][jj] = -__builtin_huge_valf();
+    }
+    const uint32_t rlane = (uint32_t)((jt + 4 * g) * stride);
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      if (__ballot(mx[b] >= th[b]) == 0ull) continue;
+      const uint32_t ql = (uint32_t)(w * QPW + 16 * b + col);
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const float v = sc[rb][b][jj];
+          const uint64_t bm = __ballot(v >= th[b]);
+          if (bm != 0ull) {
+            const uint32_t pos =
+                wn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+            if (v >= th[b]) {
+              if (pos < (uint32_t)RG_WPOOL) {
+                const uint32_t u = __float_as_uint(v + 0.0f);  // not NaN: it passed
+                const uint32_t key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+                const uint32_t r = rlane + (uint32_t)((16 * rb + jj) * stride);
+                lds_write64(lds_addr(&wkey[pos]), ((uint64_t)key << 32) | (uint64_t)(~r));
+                lds_write32(lds_addr(&wmeta[pos]), ql);
+              } else {
+                lds_or(lds_addr(&qcnt[ql]), RG_OVF);
+              }
+            }
+            wn += (uint32_t)__popcll(bm);
+          }
+        }
+    }
+  };
+  // wait until only `younger` tiles issued after the awaited one are still in flight
+  auto wait_tiles = [&](int younger) {
+    if (TT_EXP_NODMA) return;
     if (younger >= 2) wait_vm<2 * PPW>();
     else if (younger == 1) wait_vm<PPW>();
     else wait_vm<0>();
-    lds_barrier();  // tile t landed for every wave; every wave finished step t-1
-    const int pn = *pool_n;
-    if (pn >= RG_FLUSH) {
-      flush(pn < RG_POOL ? pn : RG_POOL);
-      lds_barrier();
-      if (tid == 0) *pool_n = 0;
-      lds_barrier();
-    }
-    if (t + RG_PD < n_tiles) issue(t + RG_PD);
+  };
 
+  // Step t: issue tile t+PD; MFMAs of tile t; selection of tile t-1 (its VALU fills the
+  // MFMA issue gaps); wait for tile t+1 and barrier.  The barrier therefore sits behind a
+  // full step of in-flight MFMAs, and the slot the next issue overwrites (tile t-1's) was
+  // last read before it.
+  for (int t = 0; t < RG_PD && t < n_tiles; ++t) issue(t);
+  wait_tiles(n_tiles - 1 < RG_PD - 1 ? n_tiles - 1 : RG_PD - 1);
+  lds_barrier();  // tile 0 landed; counters initialised
+  const float qnan = __builtin_nanf("");
+  f32x4 accp[RB][QB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int b = 0; b < QB; ++b) accp[rb][b] = f32x4{qnan, qnan, qnan, qnan};
+
+  // A fragments are read FD k-steps ahead of their MFMAs into a static register ring, so the
+  // compiler's counted lgkmcnt waits cover the LDS latency instead of draining every pair.
+  constexpr int FD = 3;
+  for (int t = 0; t < n_tiles; ++t) {
+    if (!TT_EXP_NODMA && t + RG_PD < n_tiles) issue(t + RG_PD);
     const char* slot = ring + (t % RG_SLOTS) * TILE_B;
+    uint32_t ra[RB][4];  // per-lane fragment addresses of k-steps s = 4m + (0..3)
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ra[rb][i] = lds_addr(slot) + lrd[rb][i];
+    u32x4 fr[FD + 1][RB];
+    auto read_step = [&](auto sc_) {
+      constexpr int S = decltype(sc_)::value;
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) fr[S % (FD + 1)][rb] = lds_read128<256 * (S >> 2)>(ra[rb][S & 3]);
+    };
+    static_for<FD>([&](auto s_) { read_step(s_); });
     f32x4 acc[RB][QB];
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int b = 0; b < QB; ++b) acc[rb][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float mx[QB];
+    static_for<KS>([&](auto s_) {
+      constexpr int s = decltype(s_)::value;
+      if constexpr (s + FD < KS) read_step(std::integral_constant<int, s + FD>{});
+      // reads of steps s+1 .. min(s+FD, KS-1) may stay in flight
+      constexpr int younger = (s + FD < KS ? FD : KS - 1 - s) * RB;
+      lds_wait<younger>();
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
+      for (int rb = 0; rb < RB; ++rb) reg_tie(fr[s % (FD + 1)][rb]);
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) {
-        const u32x4 av = *(const u32x4*)(slot + lrd[rb][s & 3] + 256 * (s >> 2));
-        const bf16x8 a = __builtin_bit_cast(bf16x8, av);
+        const bf16x8 a = __builtin_bit_cast(bf16x8, fr[s % (FD + 1)][rb]);
 #pragma unroll
         for (int b = 0; b < QB; ++b)
           acc[rb][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[b][s], acc[rb][b], 0, 0, 0);
       }
+      if constexpr (s == KS / 2) tile_max(accp, mx);  // VALU between this tile's MFMAs
+    });
+    if (!TT_EXP_NOSEL) append(accp, mx, t - 1);
+    if (TT_EXP_NOSEL && mx[0] >= th[0]) asm volatile("" ::: "memory");
+    if (t + 1 < n_tiles) {
+      const int younger = (n_tiles - 2 - t) < (RG_PD - 1) ? (n_tiles - 2 - t) : (RG_PD - 1);
+      wait_tiles(younger);
     }
-    // fast reject: per query block the max of this lane's RB*4 scores against theta
-    bool any = false;
-#pragma unroll
-    for (int b = 0; b < QB; ++b) {
-      float m = acc[0][b][0];
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) m = fmaxf(m, acc[rb][b][jj]);
-      any = any || (m >= th[b]);
-    }
-    if (__ballot(any) == 0ull) continue;
-    // lane holds a(row j0 + t*TR + 16rb + 4g + jj, query qbase + 16b + col)
-    const int64_t jt = j0 + (int64_t)t * TR;
+    if (!TT_EXP_NOBAR) lds_barrier();
+    if (wn >= (uint32_t)RG_WFLUSH) flush();
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-      for (int b = 0; b < QB; ++b)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          if ((acc[rb][b][jj] >= th[b]) && (jt + 16 * rb + 4 * g + jj < j1)) {
-            const int ql = w * QPW + 16 * b + col;
-            const uint32_t slot_i = lds_add_rtn(lds_addr(&qcnt[ql]), 1u);
-            if ((slot_i & ~RG_OVF) < (uint32_t)FL_CAP) {
-              const uint32_t pi = lds_add_rtn(lds_addr(pool_n), 1u);
-              if (pi < (uint32_t)RG_POOL) {
-                const int64_t r = (jt + 16 * rb + 4 * g + jj) * stride;
-                lds_write64(lds_addr(&pool_key[pi]), make_key(acc[rb][b][jj], (uint32_t)r));
-                lds_write32(lds_addr(&pool_meta[pi]), ((uint32_t)ql << 16) | (slot_i & 0xffff));
-              } else {
-                lds_or(lds_addr(&qcnt[ql]), RG_OVF);
-              }
-            }
-          }
-        }
+      for (int b = 0; b < QB; ++b) accp[rb][b] = acc[rb][b];
+  }
+  if (n_tiles > 0 && !TT_EXP_NOSEL) {
+    float mx[QB];
+    tile_max(accp, mx);
+    append(accp, mx, n_tiles - 1);
   }
   wait_vm<0>();
-  lds_barrier();
-  const int pn = *pool_n;
-  flush(pn < RG_POOL ? pn : RG_POOL);
-  for (int i = tid; i < QPB; i += 64 * RG_WAVES) {
-    const int qi = qt * QPB + i;
+  flush();
+  lds_wait<0>();
+  for (int i = lane; i < QPW; i += 64) {
+    const int qi = qbase + i;
     if (qi < nq) {
-      const uint32_t c = (uint32_t)qcnt[i];
-      counts[(int64_t)qi * n_slabs + slab] = (c & RG_OVF) ? FL_CAP + 1 : (int)c;
+      const uint32_t c = (uint32_t)qcnt[w * QPW + i];
+      counts[(int64_t)qi * n_slabs + slab] =
+          (c & RG_OVF) || c > (uint32_t)FL_CAP ? FL_CAP + 1 : (int)c;
     }
   }
 }

@@ -15,7 +15,7 @@ import threading
 import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libtwotower_hip.so")
+LIB_PATH = os.environ.get("TWOTOWER_HIP_LIB") or os.path.join(_PKG_ROOT, "lib", "libtwotower_hip.so")
 CSRC = os.path.join(_PKG_ROOT, "csrc")
 
 TT_OK = 0
