@@ -87,8 +87,7 @@ def main():
     shard = torch.empty((hi - lo, ep), device=dev)
     shard16 = torch.empty((hi - lo, ep), device=dev, dtype=torch.bfloat16)
     kernels.l2norm_rows(table[lo:hi], E, _lib.TT_NORM_ADD_EPS, out=shard, out_bf16=shard16)
-    xmax = float(torch.linalg.vector_norm(shard, dim=1).max())  # build-time statistic
-    eps = kernels.filter_eps(ep, xmax)
+    bounds = kernels.bf16_image_bounds(shard, shard16, E).tolist()  # build-time statistic
     gb = torch.Generator(device=dev).manual_seed(3 + rank)
     hist = torch.randint(0, N, (B, S), generator=gb, device=dev, dtype=torch.int64)
     w = event_mix(gb, (B, S), dev)
@@ -116,7 +115,7 @@ def main():
         if p0 is not None:
             p0.record(stream)
         if a.method == "bf16":
-            kernels.scan_topk_bf16(shard, shard16, hi - lo, E, qall, K, eps, row_base=lo,
+            kernels.scan_topk_bf16(shard, shard16, hi - lo, E, qall, K, bounds, row_base=lo,
                                    workspace=ws, out=(s_shard, i_shard), events=(e0, e1))
         else:
             _lib.check(L.tt_scan_topk_f32_timed(

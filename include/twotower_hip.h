@@ -98,10 +98,12 @@ int tt_scan_topk_f32_select(const float* db, int64_t n, int32_t d, int64_t ld_db
 /* ---------------------------------------------------------------------------------
  * Same results as tt_scan_topk_f32 (bit-identical: canonical f32 scores, same order), found
  * through a bf16 MFMA filter over db_bf16 (the bf16 image of db, e.g. from tt_l2norm_rows_f32)
- * followed by an exact f32 re-rank of the candidates whose bf16 score lies within 2*eps of the
- * bf16 k-th best.  eps must bound |bf16 score - f32 score| for every (row, query):
- *   eps >= ((2^-8 + 2^-18) + 3*d_pad*2^-24) * max||x|| * max||q||.
- * Queries whose candidate lists overflow are re-scanned exactly in a fallback launch.
+ * followed by an exact f32 re-rank of the candidates whose bf16 score lies within 2*eps_q of
+ * the bf16 k-th best.  eps_q bounds |bf16 score - f32 score| for query q over every row; it
+ * is derived on the device from x_norm_max >= max_r ||x_r|| and
+ * x_resid_max >= max_r ||x_r - db_bf16_r|| (both from tt_bf16_image_bounds; larger values
+ * stay exact but filter less).  Queries whose candidate lists overflow, or whose optimistic
+ * sample threshold fails, are re-scanned exactly in a fallback launch.
  * k <= 128 (larger k: tt_scan_topk_f32).  Workspace: tt_filter_workspace_bytes.
  * ev_start/ev_stop (may be NULL) are recorded around the full-catalog filter kernel (the
  * dominant kernel; the sample levels, selection and re-rank are outside the bracket).
@@ -112,9 +114,17 @@ int tt_filter_workspace_bytes(int64_t n, int32_t d, int32_t nq, int32_t k, int64
 int tt_filter_fallback_offset(int64_t n, int32_t d, int32_t nq, int32_t k, int64_t* offset);
 int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n, int32_t d,
                          int64_t ld_db, int64_t row_base, const float* q, int32_t nq,
-                         int64_t ld_q, int32_t k, float eps, float* out_score, int64_t* out_idx,
+                         int64_t ld_q, int32_t k, float x_norm_max, float x_resid_max,
+                         float* out_score, int64_t* out_idx,
                          void* workspace, int64_t workspace_bytes, void* stream,
                          void* ev_start, void* ev_stop);
+
+/* Bounds of a catalog shard and its bf16 image for tt_scan_topk_bf16f32: max-combines
+ * (atomically, so successive add() batches accumulate; the caller zero-fills out2 once)
+ * out2[0] >= max_r ||x_r|| and out2[1] >= max_r ||x_r - x_bf16_r||  (out2: 2 device floats).
+ * NaN rows are skipped. */
+int tt_bf16_image_bounds(const float* x, const uint16_t* x_bf16, int64_t n, int32_t d,
+                         int64_t ld, float* out2, void* stream);
 
 /* Merge n_lists per-shard top-k lists [n_lists, nq, k_in] (each sorted, global row ids)
  * into [nq, k]; same ordering rule.  Used after the RCCL all-gather of per-shard top-k

@@ -95,6 +95,27 @@ BF16_CASES = [c for c in SCAN_CASES if c[3] <= 128] + [
 ]
 
 
+def bounds(K, db, db16, d):
+    return K.bf16_image_bounds(db, db16, d).tolist()
+
+
+def test_bf16_image_bounds_vs_torch(K):
+    """tt_bf16_image_bounds: upper bounds, tight to ~1e-6, NaN rows skipped."""
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.randn((5000, 384), generator=g, device="cuda") * 3
+    x[17] = float("nan")
+    x16 = x.to(torch.bfloat16)
+    X, R = K.bf16_image_bounds(x, x16, 384).tolist()
+    ok = ~torch.isnan(x).any(dim=1)
+    nx = torch.linalg.vector_norm(x[ok].double(), dim=1).max().item()
+    nr = torch.linalg.vector_norm((x[ok].double() - x16[ok].double()), dim=1).max().item()
+    assert nx <= X <= nx * (1 + 1e-4) and nr <= R <= nr * (1 + 1e-4)
+    out2 = torch.zeros(2, device="cuda")  # max-combine across batches
+    K.bf16_image_bounds(x[:2500], x16[:2500], 384, out2=out2)
+    K.bf16_image_bounds(x[2500:], x16[2500:], 384, out2=out2)
+    assert out2.tolist() == [X, R]
+
+
 @pytest.mark.parametrize("n,d,nq,k", BF16_CASES)
 def test_bf16_filter_bit_exact_vs_oracle(K, oracle_mod, n, d, nq, k):
     """bf16 MFMA filter + exact f32 re-rank == canonical f32 top-k, bit for bit."""
@@ -105,11 +126,29 @@ def test_bf16_filter_bit_exact_vs_oracle(K, oracle_mod, n, d, nq, k):
     q = oracle_mod.l2norm_rows(rng.standard_normal((nq, d)).astype(np.float32), 0)
     db = dev_rows(x)
     db16 = db.to(torch.bfloat16)
-    eps = K.filter_eps(_lib.padded_dim(d))
-    s, i = K.scan_topk_bf16(db, db16, n, d, dev_rows(q), k, eps)
+    s, i = K.scan_topk_bf16(db, db16, n, d, dev_rows(q), k, bounds(K, db, db16, d))
     rs, ri = oracle_mod.scan_topk(x, q, k)
     assert np.array_equal(i.cpu().numpy(), ri)
     assert np.array_equal(s.cpu().numpy(), rs)
+
+
+def test_bf16_filter_exact_under_biased_rounding(K, oracle_mod):
+    """Every catalog/query component sits just past a bf16 rounding midpoint, so all products
+    round the same way (the case a worst-case-u bound of 2^-8 misses): still bit-exact."""
+    rng = np.random.default_rng(79)
+    n, d, nq, k = 50000, 384, 24, 100
+
+    def biased(a):
+        u = a.astype(np.float32).view(np.uint32)
+        return ((u & np.uint32(0xFFFF0000)) | np.uint32(0x8001)).view(np.float32)
+
+    x = biased(rng.standard_normal((n, d)).astype(np.float32) / np.sqrt(d))
+    q = biased(rng.standard_normal((nq, d)).astype(np.float32) / np.sqrt(d))
+    db = dev_rows(x)
+    db16 = db.to(torch.bfloat16)
+    s, i = K.scan_topk_bf16(db, db16, n, d, dev_rows(q), k, bounds(K, db, db16, d))
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
 
 
 def test_bf16_filter_no_fallback_on_iid_data(K):
@@ -124,14 +163,14 @@ def test_bf16_filter_no_fallback_on_iid_data(K):
     q = torch.randn((nq, d), generator=g, device="cuda")
     K.l2norm_rows(q, d, 0, out=q)
     ws = torch.empty(K.filter_workspace_bytes(n, d, nq, k), dtype=torch.uint8, device="cuda")
-    K.scan_topk_bf16(db, db.to(torch.bfloat16), n, d, q, k, K.filter_eps(_lib.padded_dim(d)),
-                     workspace=ws)
+    db16 = db.to(torch.bfloat16)
+    K.scan_topk_bf16(db, db16, n, d, q, k, bounds(K, db, db16, d), workspace=ws)
     torch.cuda.synchronize()
     assert K.filter_fallback_count(ws, n, d, nq, k) == 0
 
 
-@pytest.mark.parametrize("eps", [0.5, 4.0])
-def test_bf16_filter_fallback_is_exact(K, oracle_mod, eps):
+@pytest.mark.parametrize("resid", [0.5, 4.0])
+def test_bf16_filter_fallback_is_exact(K, oracle_mod, resid):
     """A loose bound overflows the candidate lists: every query then takes the exact
     fallback launch, and the results must not change."""
     rng = np.random.default_rng(77)
@@ -140,7 +179,8 @@ def test_bf16_filter_fallback_is_exact(K, oracle_mod, eps):
     q = oracle_mod.l2norm_rows(rng.standard_normal((nq, d)).astype(np.float32), 0)
     db = dev_rows(x)
     ws = torch.empty(K.filter_workspace_bytes(n, d, nq, k), dtype=torch.uint8, device="cuda")
-    s, i = K.scan_topk_bf16(db, db.to(torch.bfloat16), n, d, dev_rows(q), k, eps, workspace=ws)
+    s, i = K.scan_topk_bf16(db, db.to(torch.bfloat16), n, d, dev_rows(q), k, (1.0, resid),
+                            workspace=ws)
     rs, ri = oracle_mod.scan_topk(x, q, k)
     assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
     assert K.filter_fallback_count(ws, n, d, nq, k) == nq  # every query took the fallback
@@ -156,8 +196,8 @@ def test_bf16_filter_clusters_and_ties(K, oracle_mod):
     q = np.concatenate([base[:6], oracle_mod.l2norm_rows(
         rng.standard_normal((6, 384)).astype(np.float32), 0), np.zeros((1, 384), np.float32)])
     db = dev_rows(x)
-    s, i = K.scan_topk_bf16(db, db.to(torch.bfloat16), x.shape[0], 384, dev_rows(q), 128,
-                            K.filter_eps(384))
+    db16 = db.to(torch.bfloat16)
+    s, i = K.scan_topk_bf16(db, db16, x.shape[0], 384, dev_rows(q), 128, bounds(K, db, db16, 384))
     rs, ri = oracle_mod.scan_topk(x, q, 128)
     assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
 

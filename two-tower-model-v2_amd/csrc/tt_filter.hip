@@ -6,9 +6,14 @@
 // only decides WHICH rows need an exact score:
 //
 //   a(r) = bf16(x_r) . bf16(q) accumulated in f32 by v_mfma_f32_16x16x32_bf16.
-//   |a(r) - s(r)| <= eps  with  eps = (2u+u^2)|x||q| + 3*E*2^-24 |x||q|,  u = 2^-9
-//   (bf16 round-to-nearest on both operands, Cauchy-Schwarz; the last term covers the f32
-//   accumulation of a and of the canonical score s).  The caller passes eps.
+//   |a(r) - s(r)| <= eps_q, computed per query by k_query_eps from the catalog bounds
+//   X >= max||x_r||, R >= max||x_r - bf16(x_r)|| (tt_bf16_image_bounds):
+//     x.q - x~.q~ = (x - x~).q + x~.(q - q~)          (Cauchy-Schwarz on both terms)
+//     eps_q = R|q| + (X+R)|q - q~| + 2E 2^-24 (X+R)|q~| + E 2^-24 X|q|      (x 1.001)
+//   The last two terms bound the f32 accumulation of a (any order, 2 roundings per add
+//   allowed) and of the canonical fma chain s over E = padded-dim terms.  Using the measured
+//   rounding residuals instead of the worst case u = 2^-8 per operand keeps eps ~2x tighter
+//   for real data while staying a bound.
 //
 // Pipeline per call (all on the stream, no host sync, DESIGN.md "Scan v2"):
 //   1. levels L = coarse..fine over nested strided row samples (stride 16^L, last = 1).
@@ -567,7 +572,8 @@ __device__ void flag_query(int qid, int* flags, int* qsel, int* qsel_n) {
 //   query is flagged for the exact fallback.  band[q] = candidates with a >= A_k - eps2.
 __global__ __launch_bounds__(256) void k_select(const uint64_t* __restrict__ lists,
                                                 const int* __restrict__ counts, int n_slabs,
-                                                int k, int J, float eps2, int mode,
+                                                int k, int J, const float* __restrict__ eps2,
+                                                int mode,
                                                 float* __restrict__ theta_out,
                                                 float* __restrict__ aref,
                                                 uint64_t* __restrict__ band, int* band_n,
@@ -625,7 +631,7 @@ __global__ __launch_bounds__(256) void k_select(const uint64_t* __restrict__ lis
     return;
   }
   // band = prefix of the sorted list with a >= ak - eps2 (NaN never enters the lists)
-  const float thr = ak - eps2;
+  const float thr = ak - eps2[qid];
   __shared__ int bn;
   if (threadIdx.x == 0) bn = 0;
   __syncthreads();
@@ -699,9 +705,40 @@ __global__ void k_fill_f32(float* x, int n, float v) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] = v;
 }
-__global__ void k_add_f32(float* x, int n, float v) {
+
+// Per-query error bound eps2[q] = 2 eps_q (see the header).  One wave per query.
+template <int EP>
+__global__ __launch_bounds__(256) void k_query_eps(const float* __restrict__ q, int nq,
+                                                   int64_t ldq, float X, float R,
+                                                   float* __restrict__ eps2) {
+  const int qi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (qi >= nq) return;
+  const float* qr = q + (int64_t)qi * ldq;
+  float sq = 0.0f, st = 0.0f, sr = 0.0f;
+  for (int i = lane; i < EP; i += 64) {
+    const float v = qr[i], vt = __uint_as_float((uint32_t)f32_to_bf16_rne(v) << 16);
+    sq = fmaf(v, v, sq);
+    st = fmaf(vt, vt, st);
+    sr = fmaf(v - vt, v - vt, sr);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    sq += __shfl_xor(sq, o, 64);
+    st += __shfl_xor(st, o, 64);
+    sr += __shfl_xor(sr, o, 64);
+  }
+  if (lane == 0) {
+    const float grow = 1.0f + (float)(EP + 2) * 1.1920929e-07f, up = 1.0f + 2.4e-7f;
+    const float nq_ = sqrtf(sq * grow) * up, nt = sqrtf(st * grow) * up, nr = sqrtf(sr * grow) * up;
+    const float g = (float)EP * 5.9604645e-08f * 1.01f;  // E 2^-24 (first order + slack)
+    const float e = R * nq_ + (X + R) * nr + 2.0f * g * (X + R) * nt + g * X * nq_;
+    const float r = 2.0f * e * 1.001f;
+    eps2[qi] = r == r ? r : __builtin_huge_valf();  // a NaN query: widest band (never returned)
+  }
+}
+
+__global__ void k_sub_arr(float* x, const float* y, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) x[i] = x[i] + v;
+  if (i < n) x[i] = x[i] - y[i];
 }
 
 // --------------------------------------------------------------------------- host
@@ -769,6 +806,7 @@ struct FilterWs {
   int* counts;
   float* theta;
   float* aref;
+  float* eps2;
   uint64_t* band;
   int* band_n;
   int* flags;  // flags[nq], qsel[nq], qsel_n[1] are contiguous (one memset)
@@ -795,6 +833,7 @@ static FilterWs carve(void* base, const FilterPlan& p, int64_t n, int d, int nq,
   w.counts = (int*)take((int64_t)nq * p.max_slabs * 4);
   w.theta = (float*)take((int64_t)nq * 4);
   w.aref = (float*)take((int64_t)nq * 4);
+  w.eps2 = (float*)take((int64_t)nq * 4);
   w.band = (uint64_t*)take((int64_t)nq * BAND_CAP * 8);
   w.band_n = (int*)take((int64_t)nq * 4);
   int* fl = (int*)take(((int64_t)2 * nq + 1) * 4);
@@ -862,14 +901,15 @@ extern "C" int tt_filter_fallback_offset(int64_t n, int32_t d, int32_t nq, int32
 
 extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n,
                                     int32_t d, int64_t ld_db, int64_t row_base, const float* q,
-                                    int32_t nq, int64_t ld_q, int32_t k, float eps,
-                                    float* out_score, int64_t* out_idx, void* workspace,
+                                    int32_t nq, int64_t ld_q, int32_t k, float x_norm_max,
+                                    float x_resid_max, float* out_score, int64_t* out_idx, void* workspace,
                                     int64_t workspace_bytes, void* stream, void* ev_start,
                                     void* ev_stop) {
   TT_REQUIRE(n >= 1 && n <= 0x7fffffffLL, "need 1 <= n < 2^31");
   TT_REQUIRE(nq >= 0, "nq < 0");
   TT_REQUIRE(k >= 1 && k <= n, "need 1 <= k <= n");
-  TT_REQUIRE(eps >= 0.0f, "eps < 0");
+  TT_REQUIRE(x_norm_max >= 0.0f && x_resid_max >= 0.0f,
+             "x_norm_max / x_resid_max must be >= 0 (tt_bf16_image_bounds)");
   if (nq == 0) return TT_OK;
   if (k > FL_KMAX) return fail(TT_ERR_UNSUPPORTED, "tt_scan_topk_bf16f32: k > 128");
   const int ep = tt_padded_dim(d);
@@ -885,17 +925,26 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(w.flags, 0, ((size_t)2 * nq + 1) * 4, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "hipMemsetAsync(flags)");
-  const float eps2 = 2.0f * eps;
   const unsigned fill_grid = (unsigned)((nq + 255) / 256);
   hipLaunchKernelGGL(k_fill_f32, dim3(fill_grid), dim3(256), 0, st, w.theta, nq,
                      -__builtin_huge_valf());
   hipLaunchKernelGGL(k_fill_f32, dim3(fill_grid), dim3(256), 0, st, w.aref, nq,
                      -__builtin_huge_valf());
+  const unsigned eps_grid = (unsigned)((nq + 3) / 4);
+  switch (ep) {
+#define TT_QE(E)                                                                              \
+  case E:                                                                                     \
+    hipLaunchKernelGGL(k_query_eps<E>, dim3(eps_grid), dim3(256), 0, st, q, nq, ld_q,         \
+                       x_norm_max, x_resid_max, w.eps2);                                      \
+    break;
+    TT_QE(64) TT_QE(128) TT_QE(256) TT_QE(384) TT_QE(512) TT_QE(768)
+#undef TT_QE
+  }
   for (int li = 0; li < p.n_levels; ++li) {
     const Level& L = p.lv[li];
     const bool last = li == p.n_levels - 1;
     if (last && li > 0)  // full-catalog level: theta = a_J(stride-16 sample) - 2 eps
-      hipLaunchKernelGGL(k_add_f32, dim3(fill_grid), dim3(256), 0, st, w.theta, nq, -eps2);
+      hipLaunchKernelGGL(k_sub_arr, dim3(fill_grid), dim3(256), 0, st, w.theta, w.eps2, nq);
     if (last && ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
       return fail(TT_ERR_LAUNCH, "hipEventRecord(start)");
     switch (ep) {
@@ -912,7 +961,7 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
     if (last && ev_stop && hipEventRecord((hipEvent_t)ev_stop, st) != hipSuccess)
       return fail(TT_ERR_LAUNCH, "hipEventRecord(stop)");
     hipLaunchKernelGGL(k_select, dim3(nq), dim3(256), 0, st, w.lists, w.counts, L.n_slabs, k,
-                       p.J, eps2, last ? 1 : 0, w.theta, w.aref, w.band, w.band_n, w.flags,
+                       p.J, w.eps2, last ? 1 : 0, w.theta, w.aref, w.band, w.band_n, w.flags,
                        w.qsel, w.qsel_n);
     rc = check_launch("k_select");
     if (rc) return rc;

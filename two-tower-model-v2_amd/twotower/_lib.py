@@ -47,8 +47,9 @@ SIGNATURES = {
     "tt_filter_fallback_offset": (ctypes.c_int, [_i64, _i32, _i32, _i32,
                                                  ctypes.POINTER(_i64)]),
     "tt_scan_topk_bf16f32": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _i64, _vp, _i32, _i64,
-                                            _i32, ctypes.c_float, _vp, _vp, _vp, _i64, _vp, _vp,
-                                            _vp]),
+                                            _i32, ctypes.c_float, ctypes.c_float, _vp, _vp, _vp,
+                                            _i64, _vp, _vp, _vp]),
+    "tt_bf16_image_bounds": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _vp, _vp]),
     "tt_topk_merge_f32": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp]),
     "tt_weighted_avg_l2_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _i64, _vp]),
     "tt_gather_weighted_avg_l2_f32": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _i64,

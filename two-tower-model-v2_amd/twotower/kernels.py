@@ -82,9 +82,19 @@ def scan_topk(db: torch.Tensor, n: int, d: int, q: torch.Tensor, k: int, row_bas
 FILTER_KMAX = 128
 
 
-def filter_eps(ep: int, xmax: float = 1.00001, qmax: float = 1.00001) -> float:
-    """Bound on |bf16 score - canonical f32 score| (include/twotower_hip.h)."""
-    return ((2.0 ** -8 + 2.0 ** -18) + 3.0 * ep * 2.0 ** -24) * xmax * qmax * 1.001
+def bf16_image_bounds(x: torch.Tensor, x16: torch.Tensor, d: int, out2: torch.Tensor = None):
+    """Max-combine (max ||x_r||, max ||x_r - x16_r||) upper bounds into out2 (device [2] f32).
+
+    These catalog bounds set the bf16 filter's per-query error bound (tt_scan_topk_bf16f32)."""
+    _check_2d(x, "x")
+    _check_2d(x16, "x16", torch.bfloat16)
+    if x16.shape != x.shape or x16.stride(0) != x.stride(0):
+        raise ValueError("x16 must be the bf16 image of x (same shape and leading dim)")
+    if out2 is None:
+        out2 = torch.zeros(2, dtype=_f32, device=x.device)
+    check(lib().tt_bf16_image_bounds(_ptr(x), _ptr(x16), x.shape[0], d, x.stride(0), _ptr(out2),
+                                     stream_ptr()), "tt_bf16_image_bounds")
+    return out2
 
 
 def filter_workspace_bytes(n: int, d: int, nq: int, k: int) -> int:
@@ -104,9 +114,12 @@ def filter_fallback_count(workspace: torch.Tensor, n: int, d: int, nq: int, k: i
 
 
 def scan_topk_bf16(db: torch.Tensor, db16: torch.Tensor, n: int, d: int, q: torch.Tensor,
-                   k: int, eps: float, row_base: int = 0, workspace: torch.Tensor = None,
+                   k: int, bounds, row_base: int = 0, workspace: torch.Tensor = None,
                    out=None, events=(None, None)):
-    """Exact top-k (bit-identical to scan_topk) via the bf16 filter + f32 re-rank (k <= 128)."""
+    """Exact top-k (bit-identical to scan_topk) via the bf16 filter + f32 re-rank (k <= 128).
+
+    bounds = (x_norm_max, x_resid_max) host floats, e.g. bf16_image_bounds(...).tolist()."""
+    x_norm_max, x_resid_max = (float(v) for v in bounds)
     _check_2d(db, "db")
     _check_2d(db16, "db16", torch.bfloat16)
     _check_2d(q, "q")
@@ -126,7 +139,7 @@ def scan_topk_bf16(db: torch.Tensor, db16: torch.Tensor, n: int, d: int, q: torc
     e0, e1 = events
     check(lib().tt_scan_topk_bf16f32(
         _ptr(db), _ptr(db16), n, d, db.stride(0), row_base, _ptr(q), nq, q.stride(0), k,
-        ctypes.c_float(eps), _ptr(out[0]), _ptr(out[1]), _ptr(workspace), workspace.numel(),
+        ctypes.c_float(x_norm_max), ctypes.c_float(x_resid_max), _ptr(out[0]), _ptr(out[1]), _ptr(workspace), workspace.numel(),
         stream_ptr(), e0.cuda_event if e0 is not None else None,
         e1.cuda_event if e1 is not None else None), "tt_scan_topk_bf16f32")
     return out

@@ -37,18 +37,21 @@ class FlatIPIndex:
         self.device = device or _lib.device()
         self.xb = torch.zeros((0, self.ep), dtype=torch.float32, device=self.device)
         self.xb16 = torch.zeros((0, self.ep), dtype=torch.bfloat16, device=self.device)
-        self.xmax = 0.0  # max row norm: scales the bf16 filter's error bound
+        # (max ||x_r||, max ||x_r - bf16(x_r)||): the bf16 filter's error-bound inputs
+        self._bounds_dev = torch.zeros(2, dtype=torch.float32, device=self.device)
+        self.bounds = (0.0, 0.0)
         self.ntotal = 0
         self._ws = None
 
     def _append(self, rows: torch.Tensor, rows16: torch.Tensor) -> None:
+        if rows.shape[0]:  # build-time statistic over the new rows (max-combined)
+            kernels.bf16_image_bounds(rows, rows16, self.d, out2=self._bounds_dev)
+            self.bounds = tuple(self._bounds_dev.tolist())
         if self.ntotal:
             rows = torch.cat([self.xb[: self.ntotal], rows])
             rows16 = torch.cat([self.xb16[: self.ntotal], rows16])
         self.xb, self.xb16 = rows, rows16
         self.ntotal = rows.shape[0]
-        if self.ntotal:  # one-time build statistic
-            self.xmax = float(torch.linalg.vector_norm(self.xb, dim=1).nan_to_num(0.0).max())
 
     # faiss-style add of ALREADY-normalised float32 rows (host or device)
     def add(self, x) -> None:
@@ -70,7 +73,7 @@ class FlatIPIndex:
         kernels.l2norm_rows(raw, self.d, _lib.TT_NORM_ADD_EPS, out=raw, out_bf16=raw16)
         self._append(raw, raw16)
 
-    def search_device(self, q: torch.Tensor, k: int, method: str = "auto", qmax: float = 1.00001):
+    def search_device(self, q: torch.Tensor, k: int, method: str = "auto"):
         """q: [nq, ep] normalised device rows -> (scores [nq,k], labels [nq,k]) on device.
 
         method "auto": bf16 filter + exact f32 re-rank for k <= 128, else the f32 scan;
@@ -85,9 +88,8 @@ class FlatIPIndex:
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
         if use_bf16:
-            eps = kernels.filter_eps(self.ep, max(self.xmax, 1e-30), qmax)
-            return kernels.scan_topk_bf16(self.xb, self.xb16, self.ntotal, self.d, q, k, eps,
-                                          workspace=self._ws)
+            return kernels.scan_topk_bf16(self.xb, self.xb16, self.ntotal, self.d, q, k,
+                                          self.bounds, workspace=self._ws)
         return kernels.scan_topk(self.xb, self.ntotal, self.d, q, k, workspace=self._ws)
 
     def search(self, x: np.ndarray, k: int):
