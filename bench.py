@@ -31,6 +31,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from twotower import _lib, kernels  # noqa: E402
+from twotower.sharded import TopkExchange, shard_range  # noqa: E402
 
 F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X dense f32 MFMA (MI355X_MICROARCH.md)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity)
@@ -51,8 +52,8 @@ def parse():
                    help="bf16: bf16 MFMA filter + exact f32 re-rank; f32: exact f32 MFMA scan "
                         "(identical results)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-single", type=int, default=32)
-    p.add_argument("--cpu-batch", type=int, default=512)
+    p.add_argument("--cpu-single", type=int, default=128)
+    p.add_argument("--cpu-batch", type=int, default=2048)
     return p.parse_args()
 
 
@@ -83,7 +84,7 @@ def main():
     table = torch.zeros((N, ep), device=dev)
     table[:, :E] = torch.randn((N, E), generator=g, device=dev)
     kernels.l2norm_rows(table, E, _lib.TT_NORM_MAX_EPS, out=table)  # ItemTower outputs (F.normalize)
-    lo, hi = rank * N // world, (rank + 1) * N // world
+    lo, hi = shard_range(N, rank, world)
     shard = torch.empty((hi - lo, ep), device=dev)
     shard16 = torch.empty((hi - lo, ep), device=dev, dtype=torch.bfloat16)
     kernels.l2norm_rows(table[lo:hi], E, _lib.TT_NORM_ADD_EPS, out=shard, out_bf16=shard16)
@@ -93,24 +94,17 @@ def main():
     w = event_mix(gb, (B, S), dev)
 
     q = torch.empty((B, ep), device=dev)
-    qall = torch.empty((world * B, ep), device=dev) if world > 1 else q
+    ex = TopkExchange(B, ep, K, device=dev)  # all-gather queries / all-to-all top-k (RCCL)
     nq = world * B
     ws_bytes = (kernels.filter_workspace_bytes(hi - lo, E, nq, K) if a.method == "bf16"
                 else kernels.scan_workspace_bytes(hi - lo, E, nq, K))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     s_shard = torch.empty((nq, K), device=dev)
     i_shard = torch.empty((nq, K), dtype=torch.int64, device=dev)
-    if world > 1:
-        s_recv = torch.empty((world, B, K), device=dev)
-        i_recv = torch.empty((world, B, K), dtype=torch.int64, device=dev)
     L = _lib.lib()
     stream = torch.cuda.current_stream()
 
-    def step(ev=None):
-        kernels.gather_weighted_avg_l2(table, E, hist, w, out=q)
-        kernels.l2norm_rows(q, E, _lib.TT_NORM_ADD_EPS, out=q)
-        if world > 1:
-            dist.all_gather_into_tensor(qall, q)
+    def local_search(qall, ev):
         e0, e1, p0, p1 = (ev if ev else (None, None, None, None))
         if p0 is not None:
             p0.record(stream)
@@ -126,11 +120,12 @@ def main():
                 e1.cuda_event if e1 is not None else None), "scan")
         if p1 is not None:
             p1.record(stream)
-        if world > 1:
-            dist.all_to_all_single(s_recv.view(world * B, K), s_shard)
-            dist.all_to_all_single(i_recv.view(world * B, K), i_shard)
-            return kernels.merge_topk(s_recv, i_recv, K)
         return s_shard, i_shard
+
+    def step(ev=None):
+        kernels.gather_weighted_avg_l2(table, E, hist, w, out=q)  # Mode B buyer encode
+        kernels.l2norm_rows(q, E, _lib.TT_NORM_ADD_EPS, out=q)    # retrieve_batch :189-190
+        return ex.search(q, lambda qall: local_search(qall, ev), kernels.merge_topk)
 
     for _ in range(a.warmup):
         step()
@@ -171,7 +166,7 @@ def main():
     elem = 2.0 if a.method == "bf16" else 4.0
     alg_bytes = elem * rows * ep + 4.0 * nq * ep
     achieved_tf = flops / (scan_ms * 1e-3) / 1e12
-    kname = "k_filter_bf16" if a.method == "bf16" else "k_scan_topk_f32"
+    kname = f"k_filter_ring<{ep}, true>" if a.method == "bf16" else "k_scan_topk_f32"
     peak = BF16_MFMA_PEAK_TFLOPS if a.method == "bf16" else F32_MFMA_PEAK_TFLOPS
     traffic = None
     tj = os.path.join(ROOT, "profiles", "traffic.json")

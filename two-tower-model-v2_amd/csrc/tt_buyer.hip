@@ -34,7 +34,11 @@ __device__ __forceinline__ void normalize_store(float* row_s, int d, int depth, 
   for (int e = lane; e < d; e += 64) out[e] = __fdiv_rn(row_s[e], den);
 }
 
-// items: dense [b][s][d] (gather == false) or table rows selected by hist (gather == true)
+// items: dense [b][s][d] (gather == false) or table rows selected by hist (gather == true).
+// One wave per buyer; lane owns elements e = lane + 64 i.  The s history rows are walked in
+// order (canonical accumulation order), 64 at a time: lane j of a chunk computes that row's
+// normalised weight and id once, and __shfl broadcasts them, so the loop body is only the
+// row loads (all i of a row issued together, coalesced 256-B wave loads) and the FMAs.
 template <bool GATHER>
 __global__ __launch_bounds__(256) void k_weighted_avg_l2(const float* __restrict__ src,
                                                          int64_t ld_src, int64_t n_table,
@@ -42,6 +46,7 @@ __global__ __launch_bounds__(256) void k_weighted_avg_l2(const float* __restrict
                                                          const float* __restrict__ w, int64_t b,
                                                          int s, int d, float* __restrict__ out,
                                                          int64_t ld_out, int depth) {
+  constexpr int PER = BY_MAXD / 64;
   __shared__ float buf[4][BY_MAXD];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float* row_s = buf[wv];
@@ -50,20 +55,41 @@ __global__ __launch_bounds__(256) void k_weighted_avg_l2(const float* __restrict
     float wsum = 0.0f;
     for (int j = 0; j < s; ++j) wsum = wsum + wb[j];
     wsum = wsum + 1e-8f;
-    for (int e = lane; e < d; e += 64) {
-      float acc = 0.0f;
-      for (int j = 0; j < s; ++j) {
-        const float nw = __fdiv_rn(wb[j], wsum);
-        float x;
+    float acc[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) acc[i] = 0.0f;
+    for (int j0 = 0; j0 < s; j0 += 64) {
+      const int jn = s - j0 < 64 ? s - j0 : 64;
+      float my_nw = 0.0f;
+      int64_t my_r = -1;
+      if (lane < jn) {
+        my_nw = __fdiv_rn(wb[j0 + lane], wsum);
         if (GATHER) {
-          const int64_t r = hist[bi * s + j];
-          x = (r >= 0 && r < n_table) ? src[r * ld_src + e] : 0.0f;
+          const int64_t r = hist[bi * s + j0 + lane];
+          my_r = (r >= 0 && r < n_table) ? r : -1;
         } else {
-          x = src[(bi * s + j) * (int64_t)d + e];
+          my_r = bi * s + j0 + lane;
         }
-        acc = acc + __fmul_rn(x, nw);
       }
-      row_s[e] = acc;
+      for (int jj = 0; jj < jn; ++jj) {
+        const float nw = __shfl(my_nw, jj, 64);
+        const int64_t r = (int64_t)(((uint64_t)(uint32_t)__shfl((int)(my_r >> 32), jj, 64) << 32) |
+                                    (uint32_t)__shfl((int)my_r, jj, 64));
+        const float* xr = GATHER ? src + r * ld_src : src + r * (int64_t)d;
+        float x[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+          const int e = lane + 64 * i;
+          x[i] = (r >= 0 && e < d) ? xr[e] : 0.0f;
+        }
+#pragma unroll
+        for (int i = 0; i < PER; ++i) acc[i] = acc[i] + __fmul_rn(x[i], nw);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = lane + 64 * i;
+      if (e < d) row_s[e] = acc[i];
     }
     wave_sync();
     normalize_store(row_s, d, depth, lane, out + bi * ld_out);

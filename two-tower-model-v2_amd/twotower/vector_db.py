@@ -31,8 +31,9 @@ class FlatIPIndex:
     rows L2-normalised by ``add`` exactly as the reference does before ``index.add``.
     """
 
-    def __init__(self, d: int, device=None):
+    def __init__(self, d: int, device=None, row_base: int = 0):
         self.d = int(d)
+        self.row_base = int(row_base)  # global id of local row 0 (catalog row shard)
         self.ep = _lib.padded_dim(self.d)
         self.device = device or _lib.device()
         self.xb = torch.zeros((0, self.ep), dtype=torch.float32, device=self.device)
@@ -89,8 +90,10 @@ class FlatIPIndex:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
         if use_bf16:
             return kernels.scan_topk_bf16(self.xb, self.xb16, self.ntotal, self.d, q, k,
-                                          self.bounds, workspace=self._ws)
-        return kernels.scan_topk(self.xb, self.ntotal, self.d, q, k, workspace=self._ws)
+                                          self.bounds, row_base=self.row_base,
+                                          workspace=self._ws)
+        return kernels.scan_topk(self.xb, self.ntotal, self.d, q, k, row_base=self.row_base,
+                                 workspace=self._ws)
 
     def search(self, x: np.ndarray, k: int):
         """faiss signature: float32 [nq, d] host queries -> (D [nq,k] f32, I [nq,k] i64) host."""
