@@ -155,6 +155,77 @@ int tt_attn_agg_l2_f32(const float* items, int64_t b, int32_t s, int32_t d, cons
                        const float* W1, const float* b1, int32_t h, const float* W2,
                        const float* b2, float* out, int64_t ld_out, void* stream);
 
+/* ---------------------------------------------------------------------------------
+ * Item tower (tt_encoder.hip).
+ *
+ * The text encoder of ItemTower.encode_text (src/models/item_tower.py:100-124, which calls
+ * SentenceTransformer("paraphrase-multilingual-MiniLM-L12-v2").encode: BertModel + mean
+ * pooling, normalize_embeddings=False) over PACKED token sequences: ids[T] holds the n_seq
+ * sequences back to back, cu_seqlens[n_seq+1] their offsets (every length >= 1, <= max_len).
+ * Weights follow the Hugging Face BertModel state dict (nn.Linear [out, in] layout); Q, K, V
+ * are concatenated row-wise into wqkv [3H, H] / bqkv [3H].  prec TT_PREC_F32 runs every GEMM
+ * on v_mfma_f32_16x16x4_f32 (the parity path); TT_PREC_BF16 runs them on
+ * v_mfma_f32_16x16x32_bf16 with f32 accumulation, f32 residual stream, LayerNorm, softmax and
+ * pooling (the *_bf16 weight copies must be set).  out_pooled [n_seq, ld_out] f32.
+ * --------------------------------------------------------------------------------- */
+#define TT_PREC_F32 0
+#define TT_PREC_BF16 1
+#define TT_ACT_NONE 0
+#define TT_ACT_GELU 1 /* exact erf GELU (hidden_act="gelu") */
+#define TT_ACT_RELU 2
+
+typedef struct tt_bert_layer {
+  const float *wqkv, *bqkv;   /* [3H, H], [3H]   attention.self.{query,key,value} */
+  const float *wo, *bo;       /* [H, H], [H]     attention.output.dense          */
+  const float *ln1_g, *ln1_b; /* [H]             attention.output.LayerNorm      */
+  const float *w1, *b1;       /* [I, H], [I]     intermediate.dense              */
+  const float *w2, *b2;       /* [H, I], [H]     output.dense                    */
+  const float *ln2_g, *ln2_b; /* [H]             output.LayerNorm                */
+  const uint16_t *wqkv_bf16, *wo_bf16, *w1_bf16, *w2_bf16; /* bf16 images (TT_PREC_BF16) */
+} tt_bert_layer;
+
+typedef struct tt_bert_model {
+  int32_t vocab, hidden, heads, intermediate, layers, max_positions;
+  float ln_eps;
+  const float* word_emb;  /* [vocab, H] embeddings.word_embeddings     */
+  const float* pos_emb;   /* [max_positions, H]                       */
+  const float* type_emb;  /* [>=1, H] token_type_embeddings (row 0)   */
+  const float *emb_ln_g, *emb_ln_b;
+  const tt_bert_layer* layer; /* HOST array [layers] of device pointers */
+} tt_bert_model;
+
+int tt_bert_workspace_bytes(int64_t T, int32_t H, int32_t I, int32_t prec, int64_t* bytes);
+int tt_bert_encode(const tt_bert_model* model, const int32_t* ids, const int32_t* cu_seqlens,
+                   int32_t n_seq, int64_t T, int32_t max_len, int32_t prec, float* out_pooled,
+                   int64_t ld_out, void* workspace, int64_t workspace_bytes, void* stream);
+
+/* Building blocks of tt_bert_encode and of the projection head (ItemTower.projection,
+ * item_tower.py:58-63: Linear -> ReLU -> Dropout(eval) -> Linear; then tt_l2norm_rows_f32
+ * with TT_NORM_MAX_EPS for F.normalize, :209).
+ * tt_gemm_*: C[M,N] = act(A[M,K] . W[N,K]^T + bias) + residual, f32 out (+ optional bf16
+ *   copy C_bf16); N % 128 == 0; K % 32 (f32) / K % 64 (bf16) == 0; bias/residual may be NULL. */
+int tt_gemm_f32(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias,
+                const float* residual, int64_t ldr, float* C, int64_t ldc, uint16_t* C_bf16,
+                int64_t ldc16, int32_t M, int32_t N, int32_t K, int32_t act, void* stream);
+int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
+                 const float* bias, const float* residual, int64_t ldr, float* C, int64_t ldc,
+                 uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N, int32_t K, int32_t act,
+                 void* stream);
+/* torch.nn.LayerNorm over rows of width H <= 1024 (BertLayer LayerNorms). */
+int tt_layernorm_f32(const float* x, int64_t ldx, const float* gamma, const float* beta,
+                     float eps, float* y, int64_t ldy, uint16_t* y_bf16, int64_t ldy16,
+                     int64_t rows, int32_t H, void* stream);
+/* BertSelfAttention over packed sequences: qkv [T, 3H] -> out [T, H] (head dim 32 or 64). */
+int tt_attention_varlen_f32(const float* qkv, int64_t ld_qkv, const int32_t* cu_seqlens,
+                            int32_t n_seq, int32_t max_len, int32_t H, int32_t heads,
+                            float* out, int64_t ld_out, uint16_t* out_bf16, void* stream);
+/* ItemTower.forward concat (item_tower.py:126-172,198): [pooled | brand_table[brand_ids] |
+ * cat_table[cat_ids]]; a NULL table/ids or an id < 0 gives zeros (missing lists). */
+int tt_item_concat(const float* pooled, int64_t ld_pooled, int32_t Ht, const int32_t* brand_ids,
+                   const float* brand_table, const int32_t* cat_ids, const float* cat_table,
+                   int32_t C, int64_t b, float* out, int64_t ld_out, uint16_t* out_bf16,
+                   void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,221 @@
+"""Item-tower HIP kernels (csrc/tt_encoder.hip) vs float32 references, through the C ABI.
+
+Tolerances: the f32 path (f32 MFMA) differs from torch/oracle only by summation order
+(~1e-6 relative per GEMM); the bf16 path rounds GEMM operands to bf16 (8-bit mantissa) and
+is checked against the f32 reference with a bf16-sized tolerance.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import make_bert_golden as mbg
+import inputs as gi
+
+pytestmark = pytest.mark.gpu
+
+
+def _gemm(A, W, bias=None, res=None, act=0, prec="f32", want16=False):
+    from twotower import _lib
+
+    L = _lib.lib()
+    M, K = A.shape
+    N = W.shape[0]
+    C = torch.empty((M, N), device="cuda")
+    C16 = torch.empty((M, N), device="cuda", dtype=torch.bfloat16) if want16 else None
+    if prec == "f32":
+        fn, a, w = L.tt_gemm_f32, A, W
+    else:
+        fn, a, w = L.tt_gemm_bf16, A.to(torch.bfloat16), W.to(torch.bfloat16)
+    _lib.check(fn(a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0),
+                  bias.data_ptr() if bias is not None else None,
+                  res.data_ptr() if res is not None else None, res.stride(0) if res is not None else 0,
+                  C.data_ptr(), C.stride(0), C16.data_ptr() if want16 else None,
+                  C16.stride(0) if want16 else 0, M, N, K, act, _lib.stream_ptr()), "gemm")
+    return C, C16
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 128, 32), (77, 256, 512), (300, 1152, 384),
+                                   (1000, 384, 1536), (4097, 1536, 384)])
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_gemm_f32_vs_torch(M, N, K, act):
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + act)
+    A = torch.randn((M, K), generator=g, device="cuda")
+    W = torch.randn((N, K), generator=g, device="cuda") / K ** 0.5
+    b = torch.randn(N, generator=g, device="cuda")
+    R = torch.randn((M, N), generator=g, device="cuda")
+    C, C16 = _gemm(A, W, b, R, act, "f32", want16=True)
+    ref = (A.double() @ W.double().T) + b.double()
+    ref = {0: ref, 1: F.gelu(ref), 2: torch.relu(ref)}[act] + R.double()
+    torch.testing.assert_close(C.double(), ref, rtol=1e-5, atol=2e-5)
+    assert torch.equal(C16, C.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("M,N,K", [(5, 128, 64), (300, 1152, 384), (2049, 384, 1536)])
+def test_gemm_bf16_vs_torch(M, N, K):
+    g = torch.Generator(device="cuda").manual_seed(M * 3 + N + K)
+    A = torch.randn((M, K), generator=g, device="cuda")
+    W = torch.randn((N, K), generator=g, device="cuda") / K ** 0.5
+    b = torch.randn(N, generator=g, device="cuda")
+    C, _ = _gemm(A, W, b, None, 1, "bf16")
+    ref = F.gelu(A.to(torch.bfloat16).double() @ W.to(torch.bfloat16).double().T + b.double())
+    torch.testing.assert_close(C.double(), ref, rtol=1e-4, atol=1e-4)  # exact products, f32 sums
+
+
+def test_gemm_rejects_unsupported_shapes():
+    from twotower import _lib
+
+    A = torch.zeros((4, 48), device="cuda")
+    W = torch.zeros((100, 48), device="cuda")
+    C = torch.zeros((4, 100), device="cuda")
+    rc = _lib.lib().tt_gemm_f32(A.data_ptr(), 48, W.data_ptr(), 48, None, None, 0, C.data_ptr(),
+                                100, None, 0, 4, 100, 48, 0, _lib.stream_ptr())
+    assert rc == -3
+
+
+def test_layernorm_vs_torch():
+    from twotower import _lib
+
+    x = torch.randn((1001, 384), device="cuda") * 3 + 1
+    gm, bt = torch.randn(384, device="cuda"), torch.randn(384, device="cuda")
+    y = torch.empty_like(x)
+    _lib.check(_lib.lib().tt_layernorm_f32(x.data_ptr(), 384, gm.data_ptr(), bt.data_ptr(), 1e-12,
+                                           y.data_ptr(), 384, None, 0, 1001, 384,
+                                           _lib.stream_ptr()), "ln")
+    torch.testing.assert_close(y, F.layer_norm(x, (384,), gm, bt, 1e-12), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("lens", [[1], [7, 64, 128], [3, 200, 1, 512, 33]])
+def test_attention_varlen_vs_torch(lens):
+    from twotower import _lib
+
+    H, nh = 384, 12
+    T = sum(lens)
+    qkv = torch.randn((T, 3 * H), device="cuda")
+    cu = torch.tensor(np.concatenate([[0], np.cumsum(lens)]), dtype=torch.int32, device="cuda")
+    out = torch.empty((T, H), device="cuda")
+    _lib.check(_lib.lib().tt_attention_varlen_f32(qkv.data_ptr(), 3 * H, cu.data_ptr(), len(lens),
+                                                  max(lens), H, nh, out.data_ptr(), H, None,
+                                                  _lib.stream_ptr()), "attn")
+    ref = torch.empty_like(out)
+    c = cu.tolist()
+    for i in range(len(lens)):
+        a, b = c[i], c[i + 1]
+        q, k, v = (qkv[a:b, j * H:(j + 1) * H].view(b - a, nh, 32).transpose(0, 1) for j in range(3))
+        ref[a:b] = (torch.softmax(q @ k.transpose(1, 2) / 32 ** 0.5, -1) @ v).transpose(0, 1).reshape(b - a, H)
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+
+
+def _encoder(prec, cfg=mbg.CFG, seed=mbg.SEED):
+    from twotower.item_tower import BertEncoder, random_bert_state_dict
+
+    sd = random_bert_state_dict(cfg, seed)
+    return BertEncoder(sd, cfg, prec=prec), sd
+
+
+def test_encoder_f32_vs_transformers_fixture(golden):
+    g = golden("bert.npz")
+    enc, _ = _encoder("f32")
+    ids = torch.from_numpy(g["ids"]).cuda()
+    cu = torch.from_numpy(g["cu_seqlens"]).cuda()
+    y = enc.encode_packed(ids, cu, int(np.diff(g["cu_seqlens"]).max()))
+    np.testing.assert_allclose(y.cpu().numpy(), g["pooled"], rtol=0, atol=5e-5)
+
+
+def test_encoder_bf16_close_to_f32(golden):
+    g = golden("bert.npz")
+    ids = torch.from_numpy(g["ids"]).cuda()
+    cu = torch.from_numpy(g["cu_seqlens"]).cuda()
+    mx = int(np.diff(g["cu_seqlens"]).max())
+    y16 = _encoder("bf16")[0].encode_packed(ids, cu, mx).cpu()
+    ref = torch.from_numpy(g["pooled"])
+    cos = F.cosine_similarity(y16, ref, dim=1)
+    assert cos.min() > 0.999, cos
+    assert (y16 - ref).abs().max() < 0.05 * ref.abs().max()
+
+
+def test_encoder_f32_vs_oracle_large_batch():
+    """256 ragged sequences (L in [16, 128]) -- the configs[1] encode batch -- vs the oracle."""
+    from oracle import bert_ref
+
+    cfg = dict(mbg.CFG, layers=2)
+    enc, sd = _encoder("f32", cfg, seed=21)
+    rng = np.random.default_rng(5)
+    seqs = [rng.integers(0, cfg["vocab"], rng.integers(16, 129)).tolist() for _ in range(256)]
+    y = enc.encode_ids(seqs).cpu()
+    cu = np.concatenate([[0], np.cumsum([len(s) for s in seqs])])
+    ref = bert_ref.bert_mean_pool(sd, cfg, torch.tensor([t for s in seqs for t in s]), cu)
+    np.testing.assert_allclose(y.numpy(), ref.numpy(), rtol=0, atol=3e-5)
+
+
+@pytest.mark.parametrize("use_cat", [False, True])
+def test_item_head_vs_reference_fixture(golden, use_cat):
+    """ItemTower.forward on the device (concat, projection GEMMs, F.normalize) with the same
+    stand-in text encoder the fixture was made with."""
+    from twotower.item_tower import ItemTower
+
+    emb = gi.item_text_embeddings()
+
+    class Stub:
+        def get_sentence_embedding_dimension(self):
+            return 384
+
+        def encode(self, texts, **kw):
+            return torch.from_numpy(emb[[int(t.split("#")[1]) for t in texts]])
+
+    g = golden("item_head.npz")
+    it = ItemTower(use_categorical_features=use_cat, text_encoder=Stub())
+    if use_cat:
+        it.initialize_categorical_embeddings(gi.BRANDS, gi.CATEGORIES)
+    with torch.no_grad():
+        for k, v in gi.item_head_weights(use_cat).items():
+            dict(it.named_parameters())[k].copy_(torch.from_numpy(v))
+    texts, brands, cats = gi.item_batch()
+    y = it(texts, brands if use_cat else None, cats if use_cat else None)
+    assert y.is_cuda
+    tag = "cat" if use_cat else "nocat"
+    np.testing.assert_allclose(y.cpu().numpy(), g[f"{tag}__out"], rtol=0, atol=2e-6)
+    yb = it.encode_batch(texts, brands if use_cat else None, cats if use_cat else None, 5)
+    np.testing.assert_allclose(yb, g[f"{tag}__out"], rtol=0, atol=2e-6)
+
+
+def test_item_tower_uninitialised_categorical_raises_like_reference():
+    from twotower.item_tower import ItemTower
+
+    class Stub:
+        def get_sentence_embedding_dimension(self):
+            return 384
+
+        def encode(self, texts, **kw):
+            return torch.zeros((len(texts), 384))
+
+    it = ItemTower(use_categorical_features=True, text_encoder=Stub())
+    with pytest.raises(RuntimeError, match="cannot be multiplied"):
+        it(["a", "b"], ["x", "y"], ["c", "d"])
+
+
+def test_item_tower_end_to_end_vs_oracle():
+    """Texts -> HashTokenizer -> HIP encoder -> head  ==  oracle encoder -> oracle head."""
+    from oracle import bert_ref
+    from twotower.item_tower import HashTokenizer, ItemTower, random_bert_state_dict
+
+    cfg = dict(mbg.CFG, layers=3)
+    sd = random_bert_state_dict(cfg, 9)
+    it = ItemTower(use_categorical_features=True, encoder_state_dict=sd, encoder_cfg=cfg,
+                   prec="f32")
+    it.initialize_categorical_embeddings(gi.BRANDS, gi.CATEGORIES)
+    texts = ["خاتم ذهب عيار 21", "", "necklace gold 18k Damas", "   ", "زيت محرك 5W-30"]
+    brands = ["Damas", None, "Acme", "Unknown", "Lazurde"]
+    cats = ["rings", "necklaces", None, "bracelets", "engine-oil"]
+    y = it(texts, brands, cats).cpu()
+    tok = HashTokenizer(cfg["vocab"])
+    seqs = tok([t if t and t.strip() else " " for t in texts])
+    cu = np.concatenate([[0], np.cumsum([len(s) for s in seqs])])
+    te = bert_ref.bert_mean_pool(sd, cfg, torch.tensor([t for s in seqs for t in s]), cu)
+    head = {k: v.detach().cpu() for k, v in it.state_dict().items()}
+    bid = [it.brand_vocab.get(b, 0) if b else 0 for b in brands]
+    cid = [it.category_vocab.get(c, 0) if c else 0 for c in cats]
+    ref = bert_ref.item_head(te, head, bid, cid)
+    np.testing.assert_allclose(y.numpy(), ref.numpy(), rtol=0, atol=5e-5)

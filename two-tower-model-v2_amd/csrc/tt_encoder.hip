@@ -1,0 +1,589 @@
+// tt_encoder.hip -- item-tower text encoder (MiniLM-class BERT) + projection head (gfx950).
+//
+// Replaces (reference file:line):
+//   ItemTower.encode_text -> SentenceTransformer.encode   src/models/item_tower.py:100-124
+//     (BertModel forward + mean pooling over the attention mask, normalize_embeddings=False)
+//   ItemTower.encode_categorical + forward                item_tower.py:126-211
+//     (concat [text | brand | category] -> Linear -> ReLU -> (Dropout: eval) -> Linear ->
+//      F.normalize)
+//
+// Sequences are PACKED (varlen): the T = sum(L_i) real tokens of a batch are rows of one
+// [T, H] activation matrix and cu_seqlens[n_seq+1] delimits them.  The reference pads each
+// length-sorted batch of 32 to its longest text; padded keys are masked out of attention and
+// padded rows out of the mean pool, so packing computes the same function with no work on
+// padding.
+//
+// Kernels (one layer = 4 GEMMs + attention + 2 LayerNorms):
+//   k_gemm<T>    C[M,N] = A[M,K] . W[N,K]^T (+bias, GELU/ReLU, +residual), f32 out (+bf16 copy).
+//                128x128 block tile, 4 waves of 64x64, MFMA v_mfma_f32_16x16x4_f32 (T = float:
+//                the parity path) or v_mfma_f32_16x16x32_bf16 (T = bf16: the fast path, f32
+//                accumulate).  Tiles stream HBM/L2 -> LDS with global_load_lds_dwordx4 (no VGPR
+//                round trip), double-buffered; XOR-swizzled 16-B chunks make the ds_read_b128
+//                fragment reads conflict-free.  Both element types use 128-B LDS rows
+//                (BK = 32 f32 / 64 bf16), so the data path is shared.
+//   k_layernorm  wave per row (H <= 1024), two-pass mean/variance, optional bf16 copy.
+//   k_embed_ln   word + token-type + position embeddings -> LayerNorm (BertEmbeddings).
+//   k_attn       block per (sequence, head): K/V of the head in LDS, one thread per query
+//                row, two passes (row max, then exp-weighted sum), f32.
+//   k_mean_pool  block per sequence (sentence-transformers Pooling, mean mode).
+#include "tt_common.hpp"
+
+namespace tt {
+
+typedef __bf16 bf16x8e __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+enum { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2 };
+
+constexpr int GM_BM = 128, GM_BN = 128;
+constexpr int GM_TILE_B = GM_BM * 128;  // one operand tile: 128 rows x 128 B
+constexpr int GM_STAGE_B = 2 * GM_TILE_B;
+
+template <typename T>
+struct GemmElt;
+template <>
+struct GemmElt<float> {
+  static constexpr int BK = 32;  // elements per 128-B LDS row
+};
+template <>
+struct GemmElt<uint16_t> {
+  static constexpr int BK = 64;
+};
+
+__device__ __forceinline__ void enc_lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+template <int N>
+__device__ __forceinline__ void enc_wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+
+// XCD-aware tile order: consecutive logical tiles (same A rows, all N tiles) on one XCD.
+__device__ __forceinline__ int enc_xcd_remap(int bid, int nblk) {
+  const int q = nblk / 8, r = nblk % 8, x = bid % 8, local = bid / 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + local;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_t lda,
+                                                 const T* __restrict__ W, int64_t ldw,
+                                                 const float* __restrict__ bias,
+                                                 const float* __restrict__ res, int64_t ldr,
+                                                 float* __restrict__ C, int64_t ldc,
+                                                 uint16_t* __restrict__ C16, int64_t ldc16,
+                                                 int M, int N, int K, int act) {
+  constexpr int BK = GemmElt<T>::BK;
+  constexpr int EPC = 16 / sizeof(T);  // elements per 16-B chunk
+  __shared__ __attribute__((aligned(16))) char smem[2 * GM_STAGE_B];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int n_tn = N / GM_BN;
+  const int lb = enc_xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = lb / n_tn, tn = lb % n_tn;
+  const int m0 = tm * GM_BM, n0 = tn * GM_BN;
+
+  // DMA mapping: piece p (0..15) of a tile = LDS bytes [1024p, +1024) = rows 8p..8p+7;
+  // lane i -> row 8p + (i >> 3), physical chunk i & 7, logical chunk (i & 7) ^ ((row >> 1) & 7).
+  // Wave w issues pieces w, w+4, w+8, w+12 of each operand.
+  int64_t a_off[4], w_off[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int p = w + 4 * j;
+    const int row = 8 * p + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    int am = m0 + row;
+    am = am < M ? am : M - 1;
+    a_off[j] = (int64_t)am * lda + c * EPC;
+    w_off[j] = (int64_t)(n0 + row) * ldw + c * EPC;
+  }
+  auto issue = [&](int kt) {
+    char* st = smem + (kt & 1) * GM_STAGE_B;
+    const int64_t k0 = (int64_t)kt * BK;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = w + 4 * j;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(A + a_off[j] + k0),
+          (__attribute__((address_space(3))) void*)(st + 1024 * p), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(W + w_off[j] + k0),
+          (__attribute__((address_space(3))) void*)(st + GM_TILE_B + 1024 * p), 16, 0, 0);
+    }
+  };
+
+  // fragment read offsets (bytes within a tile): row r = 64*wm + 16 i + (l & 15) (A) or
+  // 64*wn + 16 j + (l & 15) (W); logical chunk c = 4 s + (l >> 4), s = read step 0..1.
+  const int g = lane >> 4, rl = lane & 15;
+  int fa[4][2], fb[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ra = 64 * wm + 16 * i + rl, rb = 64 * wn + 16 * i + rl;
+      const int c = 4 * s + g;
+      fa[i][s] = ra * 128 + 16 * (c ^ ((ra >> 1) & 7));
+      fb[i][s] = GM_TILE_B + rb * 128 + 16 * (c ^ ((rb >> 1) & 7));
+    }
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  issue(0);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) {
+      issue(kt + 1);
+      enc_wait_vm<8>();
+    } else {
+      enc_wait_vm<0>();
+    }
+    enc_lds_barrier();
+    const char* st = smem + (kt & 1) * GM_STAGE_B;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      u32x4 av[4], bv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        av[i] = *(const u32x4*)(st + fa[i][s]);
+        bv[i] = *(const u32x4*)(st + fb[i][s]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if constexpr (sizeof(T) == 4) {
+            const f32x4 a = __builtin_bit_cast(f32x4, av[i]), b = __builtin_bit_cast(f32x4, bv[j]);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u], acc[i][j], 0, 0, 0);
+          } else {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8e, av[i]), __builtin_bit_cast(bf16x8e, bv[j]),
+                acc[i][j], 0, 0, 0);
+          }
+        }
+    }
+    enc_lds_barrier();
+  }
+
+  // epilogue: lane holds C[16 i + 4 g + v][16 j + rl]
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + 64 * wn + 16 * j + rl;
+    const float bn = bias ? bias[n] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int m = m0 + 64 * wm + 16 * i + 4 * g + v;
+        if (m >= M) continue;
+        float y = acc[i][j][v] + bn;
+        if (act == ACT_GELU) y = gelu_erf(y);
+        else if (act == ACT_RELU) y = y > 0.0f ? y : 0.0f;
+        if (res) y = y + res[(int64_t)m * ldr + n];
+        C[(int64_t)m * ldc + n] = y;
+        if (C16) C16[(int64_t)m * ldc16 + n] = f32_to_bf16_rne(y);
+      }
+  }
+}
+
+// LayerNorm over rows of width H (<= 1024): wave per row.  torch.nn.LayerNorm semantics
+// (biased variance, (x - mean) / sqrt(var + eps) * gamma + beta).
+__global__ __launch_bounds__(256) void k_layernorm(const float* __restrict__ x, int64_t ldx,
+                                                   const float* __restrict__ gamma,
+                                                   const float* __restrict__ beta, float eps,
+                                                   float* __restrict__ y, int64_t ldy,
+                                                   uint16_t* __restrict__ y16, int64_t ldy16,
+                                                   int64_t rows, int H) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + w; r < rows; r += (int64_t)gridDim.x * 4) {
+    const float* xr = x + r * ldx;
+    float v[16];
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = lane + 64 * i;
+      v[i] = e < H ? xr[e] : 0.0f;
+      s += v[i];
+    }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    const float mean = s / (float)H;
+    float q = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = lane + 64 * i;
+      const float d = e < H ? v[i] - mean : 0.0f;
+      q = fmaf(d, d, q);
+    }
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    const float rstd = 1.0f / sqrtf(q / (float)H + eps);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = lane + 64 * i;
+      if (e < H) {
+        const float o = (v[i] - mean) * rstd * gamma[e] + beta[e];
+        y[r * ldy + e] = o;
+        if (y16) y16[r * ldy16 + e] = f32_to_bf16_rne(o);
+      }
+    }
+  }
+}
+
+// BertEmbeddings: (word[id] + token_type[0]) + position[t - start] -> LayerNorm.
+__global__ __launch_bounds__(256) void k_embed_ln(const int32_t* __restrict__ ids,
+                                                  const int32_t* __restrict__ cu, int n_seq,
+                                                  int64_t T, const float* __restrict__ word,
+                                                  int vocab, const float* __restrict__ pos,
+                                                  const float* __restrict__ type0,
+                                                  const float* __restrict__ gamma,
+                                                  const float* __restrict__ beta, float eps,
+                                                  float* __restrict__ y, uint16_t* __restrict__ y16,
+                                                  int H) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < T; t += (int64_t)gridDim.x * 4) {
+    int lo = 0, hi = n_seq;  // sequence: cu[lo] <= t < cu[lo+1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (cu[mid] <= t) lo = mid;
+      else hi = mid;
+    }
+    const int p = (int)(t - cu[lo]);
+    int id = ids[t];
+    id = (id >= 0 && id < vocab) ? id : 0;
+    const float* wr = word + (int64_t)id * H;
+    const float* pr = pos + (int64_t)p * H;
+    float v[16];
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = lane + 64 * i;
+      v[i] = e < H ? (wr[e] + type0[e]) + pr[e] : 0.0f;
+      s += v[i];
+    }
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    const float mean = s / (float)H;
+    float q = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = lane + 64 * i;
+      const float d = e < H ? v[i] - mean : 0.0f;
+      q = fmaf(d, d, q);
+    }
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    const float rstd = 1.0f / sqrtf(q / (float)H + eps);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = lane + 64 * i;
+      if (e < H) {
+        const float o = (v[i] - mean) * rstd * gamma[e] + beta[e];
+        y[t * H + e] = o;
+        if (y16) y16[t * H + e] = f32_to_bf16_rne(o);
+      }
+    }
+  }
+}
+
+// Multi-head self-attention over packed sequences.  qkv: [T, 3H] (Q | K | V, head h at
+// columns h*DH within each third).  Block per (sequence, head); K and V of the head live in
+// LDS; thread = query row.  softmax(q.k / sqrt(DH)) . v, keys restricted to the sequence.
+template <int DH>
+__global__ __launch_bounds__(128) void k_attn(const float* __restrict__ qkv, int64_t ldq,
+                                              const int32_t* __restrict__ cu, int H, int heads,
+                                              float scale, float* __restrict__ out,
+                                              int64_t ldo, uint16_t* __restrict__ out16) {
+  extern __shared__ float kv[];  // [L][DH] keys then [L][DH] values
+  const int sq = blockIdx.x / heads, h = blockIdx.x % heads;
+  const int t0 = cu[sq], L = cu[sq + 1] - t0;
+  float* ks = kv;
+  float* vs = kv + (int64_t)L * DH;
+  for (int e = threadIdx.x; e < L * DH; e += blockDim.x) {
+    const int j = e / DH, c = e % DH;
+    const float* row = qkv + (int64_t)(t0 + j) * ldq;
+    ks[e] = row[H + h * DH + c];
+    vs[e] = row[2 * H + h * DH + c];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < L; i += blockDim.x) {
+    const float* qr = qkv + (int64_t)(t0 + i) * ldq + h * DH;
+    float q[DH];
+#pragma unroll
+    for (int c = 0; c < DH; ++c) q[c] = qr[c];
+    float m = -__builtin_huge_valf();
+    for (int j = 0; j < L; ++j) {
+      const float* kr = ks + j * DH;
+      float s = 0.0f;
+#pragma unroll
+      for (int c = 0; c < DH; ++c) s = fmaf(q[c], kr[c], s);
+      m = fmaxf(m, s * scale);
+    }
+    float acc[DH];
+#pragma unroll
+    for (int c = 0; c < DH; ++c) acc[c] = 0.0f;
+    float l = 0.0f;
+    for (int j = 0; j < L; ++j) {
+      const float* kr = ks + j * DH;
+      float s = 0.0f;
+#pragma unroll
+      for (int c = 0; c < DH; ++c) s = fmaf(q[c], kr[c], s);
+      const float p = expf(s * scale - m);
+      l += p;
+      const float* vr = vs + j * DH;
+#pragma unroll
+      for (int c = 0; c < DH; ++c) acc[c] = fmaf(p, vr[c], acc[c]);
+    }
+    const float inv = 1.0f / l;
+    float* orow = out + (int64_t)(t0 + i) * ldo + h * DH;
+#pragma unroll
+    for (int c = 0; c < DH; ++c) {
+      const float o = acc[c] * inv;
+      orow[c] = o;
+      if (out16) out16[(int64_t)(t0 + i) * ldo + h * DH + c] = f32_to_bf16_rne(o);
+    }
+  }
+}
+
+// Mean pooling over each packed sequence: sum_t h[t] / max(L, 1e-9)  (ST Pooling, mean).
+__global__ __launch_bounds__(256) void k_mean_pool(const float* __restrict__ x, int64_t ldx,
+                                                   const int32_t* __restrict__ cu, int H,
+                                                   float* __restrict__ out, int64_t ldo) {
+  const int sq = blockIdx.x;
+  const int t0 = cu[sq], t1 = cu[sq + 1];
+  const float cnt = fmaxf((float)(t1 - t0), 1e-9f);
+  for (int e = threadIdx.x; e < H; e += blockDim.x) {
+    float s = 0.0f;
+    for (int t = t0; t < t1; ++t) s += x[(int64_t)t * ldx + e];
+    out[(int64_t)sq * ldo + e] = s / cnt;
+  }
+}
+
+// [pooled (Ht) | brand_table[bid] (C) | cat_table[cid] (C)] -> f32 rows (+bf16 copy);
+// a null table (or negative id) contributes zeros (item_tower.py:158-159,168-169).
+__global__ __launch_bounds__(256) void k_item_concat(const float* __restrict__ pooled,
+                                                     int64_t ldp, int Ht,
+                                                     const int32_t* __restrict__ bid,
+                                                     const float* __restrict__ btab,
+                                                     const int32_t* __restrict__ cid,
+                                                     const float* __restrict__ ctab, int C,
+                                                     float* __restrict__ out, int64_t ldo,
+                                                     uint16_t* __restrict__ out16, int width) {
+  const int r = blockIdx.x;
+  for (int e = threadIdx.x; e < width; e += blockDim.x) {
+    float v = 0.0f;
+    if (e < Ht) v = pooled[(int64_t)r * ldp + e];
+    else if (e < Ht + C) v = (btab && bid && bid[r] >= 0) ? btab[(int64_t)bid[r] * C + (e - Ht)] : 0.0f;
+    else if (e < Ht + 2 * C) v = (ctab && cid && cid[r] >= 0) ? ctab[(int64_t)cid[r] * C + (e - Ht - C)] : 0.0f;
+    out[(int64_t)r * ldo + e] = v;
+    if (out16) out16[(int64_t)r * ldo + e] = f32_to_bf16_rne(v);
+  }
+}
+
+}  // namespace tt
+
+using namespace tt;
+
+// ------------------------------------------------------------------------------- C ABI
+extern "C" int tt_gemm_f32(const float* A, int64_t lda, const float* W, int64_t ldw,
+                           const float* bias, const float* residual, int64_t ldr, float* C,
+                           int64_t ldc, uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N,
+                           int32_t K, int32_t act, void* stream) {
+  TT_REQUIRE(M >= 0 && N >= 0 && K >= 0, "negative size");
+  if (M == 0 || N == 0) return TT_OK;
+  if (N % GM_BN != 0 || K % GemmElt<float>::BK != 0)
+    return fail(TT_ERR_UNSUPPORTED, "tt_gemm_f32: need N % 128 == 0 and K % 32 == 0");
+  TT_REQUIRE(A && W && C, "null pointer");
+  TT_REQUIRE(lda % 4 == 0 && ldw % 4 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0,
+             "A/W must be 16-B aligned with lda, ldw % 4 == 0");
+  TT_REQUIRE(act >= 0 && act <= 2, "bad activation");
+  const int nblk = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
+  hipLaunchKernelGGL(k_gemm<float>, dim3(nblk), dim3(256), 0, (hipStream_t)stream, A, lda, W, ldw,
+                     bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
+  return check_launch("tt_gemm_f32");
+}
+
+extern "C" int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
+                            const float* bias, const float* residual, int64_t ldr, float* C,
+                            int64_t ldc, uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N,
+                            int32_t K, int32_t act, void* stream) {
+  TT_REQUIRE(M >= 0 && N >= 0 && K >= 0, "negative size");
+  if (M == 0 || N == 0) return TT_OK;
+  if (N % GM_BN != 0 || K % GemmElt<uint16_t>::BK != 0)
+    return fail(TT_ERR_UNSUPPORTED, "tt_gemm_bf16: need N % 128 == 0 and K % 64 == 0");
+  TT_REQUIRE(A && W && C, "null pointer");
+  TT_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0,
+             "A/W must be 16-B aligned with lda, ldw % 8 == 0");
+  TT_REQUIRE(act >= 0 && act <= 2, "bad activation");
+  const int nblk = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
+  hipLaunchKernelGGL(k_gemm<uint16_t>, dim3(nblk), dim3(256), 0, (hipStream_t)stream, A, lda, W,
+                     ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
+  return check_launch("tt_gemm_bf16");
+}
+
+extern "C" int tt_layernorm_f32(const float* x, int64_t ldx, const float* gamma,
+                                const float* beta, float eps, float* y, int64_t ldy,
+                                uint16_t* y_bf16, int64_t ldy16, int64_t rows, int32_t H,
+                                void* stream) {
+  TT_REQUIRE(rows >= 0 && H >= 1 && H <= 1024, "need rows >= 0, 1 <= H <= 1024");
+  if (rows == 0) return TT_OK;
+  TT_REQUIRE(x && gamma && beta && y, "null pointer");
+  const int64_t b = (rows + 3) / 4;
+  hipLaunchKernelGGL(k_layernorm, dim3((unsigned)(b < 8192 ? b : 8192)), dim3(256), 0,
+                     (hipStream_t)stream, x, ldx, gamma, beta, eps, y, ldy, y_bf16, ldy16, rows, H);
+  return check_launch("tt_layernorm_f32");
+}
+
+extern "C" int tt_attention_varlen_f32(const float* qkv, int64_t ld_qkv, const int32_t* cu_seqlens,
+                                       int32_t n_seq, int32_t max_len, int32_t H, int32_t heads,
+                                       float* out, int64_t ld_out, uint16_t* out_bf16,
+                                       void* stream) {
+  TT_REQUIRE(n_seq >= 0 && heads >= 1 && H % heads == 0, "bad n_seq / heads");
+  if (n_seq == 0) return TT_OK;
+  const int dh = H / heads;
+  TT_REQUIRE(max_len >= 1 && max_len <= 512, "max_len must be in [1, 512]");
+  TT_REQUIRE(qkv && cu_seqlens && out, "null pointer");
+  const size_t smem = (size_t)2 * max_len * dh * sizeof(float);
+  if (smem > 160 * 1024) return fail(TT_ERR_UNSUPPORTED, "attention K/V exceed LDS");
+  const float scale = 1.0f / sqrtf((float)dh);
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)(n_seq * heads));
+  if (smem > 64 * 1024) {
+    const void* fn = dh == 32 ? (const void*)k_attn<32> : (const void*)k_attn<64>;
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess)
+      return fail(TT_ERR_LAUNCH, "hipFuncSetAttribute(max dynamic LDS)");
+  }
+  switch (dh) {
+    case 32:
+      hipLaunchKernelGGL(k_attn<32>, grid, dim3(128), smem, st, qkv, ld_qkv, cu_seqlens, H, heads,
+                         scale, out, ld_out, out_bf16);
+      break;
+    case 64:
+      hipLaunchKernelGGL(k_attn<64>, grid, dim3(128), smem, st, qkv, ld_qkv, cu_seqlens, H, heads,
+                         scale, out, ld_out, out_bf16);
+      break;
+    default:
+      return fail(TT_ERR_UNSUPPORTED, "attention head dim must be 32 or 64");
+  }
+  return check_launch("tt_attention_varlen_f32");
+}
+
+namespace {
+size_t align_up(size_t b) { return (b + 255) / 256 * 256; }
+struct EncWs {
+  float *x, *qkv, *ctx, *y, *ff;
+  uint16_t *x16, *ctx16, *ff16;
+  size_t total;
+};
+EncWs enc_carve(char* base, int64_t T, int H, int I, bool bf16) {
+  EncWs w{};
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* p = base ? base + off : nullptr;
+    off += align_up(bytes);
+    return p;
+  };
+  w.x = (float*)take((size_t)T * H * 4);
+  w.qkv = (float*)take((size_t)T * 3 * H * 4);
+  w.ctx = (float*)take((size_t)T * H * 4);
+  w.y = (float*)take((size_t)T * H * 4);
+  w.ff = (float*)take((size_t)T * I * 4);
+  if (bf16) {
+    w.x16 = (uint16_t*)take((size_t)T * H * 2);
+    w.ctx16 = (uint16_t*)take((size_t)T * H * 2);
+    w.ff16 = (uint16_t*)take((size_t)T * I * 2);
+  }
+  w.total = off;
+  return w;
+}
+}  // namespace
+
+extern "C" int tt_bert_workspace_bytes(int64_t T, int32_t H, int32_t I, int32_t prec,
+                                       int64_t* bytes) {
+  TT_REQUIRE(bytes && T >= 0 && H > 0 && I > 0, "bad arguments");
+  *bytes = (int64_t)enc_carve(nullptr, T, H, I, prec == TT_PREC_BF16).total;
+  return TT_OK;
+}
+
+extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const int32_t* cu_seqlens,
+                              int32_t n_seq, int64_t T, int32_t max_len, int32_t prec,
+                              float* out_pooled, int64_t ld_out, void* workspace,
+                              int64_t workspace_bytes, void* stream) {
+  TT_REQUIRE(m != nullptr, "model == NULL");
+  TT_REQUIRE(prec == TT_PREC_F32 || prec == TT_PREC_BF16, "bad precision");
+  TT_REQUIRE(n_seq >= 0 && T >= n_seq, "need T >= n_seq >= 0 (no empty sequences)");
+  if (n_seq == 0) return TT_OK;
+  const int H = m->hidden, I = m->intermediate, NL = m->layers;
+  TT_REQUIRE(H > 0 && H <= 1024 && I > 0 && NL >= 0 && m->heads > 0, "bad model dims");
+  TT_REQUIRE(max_len <= m->max_positions, "max_len > max_position_embeddings");
+  const bool bf = prec == TT_PREC_BF16;
+  EncWs w = enc_carve((char*)workspace, T, H, I, bf);
+  if (!workspace || workspace_bytes < (int64_t)w.total)
+    return fail(TT_ERR_WORKSPACE, "tt_bert_encode: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  {
+    const int64_t b = (T + 3) / 4;
+    hipLaunchKernelGGL(k_embed_ln, dim3((unsigned)(b < 16384 ? b : 16384)), dim3(256), 0, st, ids,
+                       cu_seqlens, n_seq, T, m->word_emb, m->vocab, m->pos_emb, m->type_emb,
+                       m->emb_ln_g, m->emb_ln_b, m->ln_eps, w.x, bf ? w.x16 : nullptr, H);
+    int rc = check_launch("k_embed_ln");
+    if (rc) return rc;
+  }
+  for (int l = 0; l < NL; ++l) {
+    const tt_bert_layer& L = m->layer[l];
+    int rc;
+    // Q|K|V = x Wqkv^T + b
+    rc = bf ? tt_gemm_bf16(w.x16, H, L.wqkv_bf16, H, L.bqkv, nullptr, 0, w.qkv, 3 * H, nullptr, 0,
+                           (int)T, 3 * H, H, ACT_NONE, stream)
+            : tt_gemm_f32(w.x, H, L.wqkv, H, L.bqkv, nullptr, 0, w.qkv, 3 * H, nullptr, 0, (int)T,
+                          3 * H, H, ACT_NONE, stream);
+    if (rc) return rc;
+    rc = tt_attention_varlen_f32(w.qkv, 3 * H, cu_seqlens, n_seq, max_len, H, m->heads, w.ctx, H,
+                                 bf ? w.ctx16 : nullptr, stream);
+    if (rc) return rc;
+    // y = ctx Wo^T + bo + x ; x = LN(y)
+    rc = bf ? tt_gemm_bf16(w.ctx16, H, L.wo_bf16, H, L.bo, w.x, H, w.y, H, nullptr, 0, (int)T, H, H,
+                           ACT_NONE, stream)
+            : tt_gemm_f32(w.ctx, H, L.wo, H, L.bo, w.x, H, w.y, H, nullptr, 0, (int)T, H, H,
+                          ACT_NONE, stream);
+    if (rc) return rc;
+    rc = tt_layernorm_f32(w.y, H, L.ln1_g, L.ln1_b, m->ln_eps, w.x, H, bf ? w.x16 : nullptr, H, T,
+                          H, stream);
+    if (rc) return rc;
+    // ff = GELU(x W1^T + b1) ; y = ff W2^T + b2 + x ; x = LN(y)
+    rc = bf ? tt_gemm_bf16(w.x16, H, L.w1_bf16, H, L.b1, nullptr, 0, w.ff, I, w.ff16, I, (int)T, I,
+                           H, ACT_GELU, stream)
+            : tt_gemm_f32(w.x, H, L.w1, H, L.b1, nullptr, 0, w.ff, I, nullptr, 0, (int)T, I, H,
+                          ACT_GELU, stream);
+    if (rc) return rc;
+    rc = bf ? tt_gemm_bf16(w.ff16, I, L.w2_bf16, I, L.b2, w.x, H, w.y, H, nullptr, 0, (int)T, H, I,
+                           ACT_NONE, stream)
+            : tt_gemm_f32(w.ff, I, L.w2, I, L.b2, w.x, H, w.y, H, nullptr, 0, (int)T, H, I, ACT_NONE,
+                          stream);
+    if (rc) return rc;
+    rc = tt_layernorm_f32(w.y, H, L.ln2_g, L.ln2_b, m->ln_eps, w.x, H, bf ? w.x16 : nullptr, H, T,
+                          H, stream);
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(k_mean_pool, dim3((unsigned)n_seq), dim3(256), 0, st, w.x, (int64_t)H,
+                     cu_seqlens, H, out_pooled, ld_out);
+  return check_launch("k_mean_pool");
+}
+
+extern "C" int tt_item_concat(const float* pooled, int64_t ld_pooled, int32_t Ht,
+                              const int32_t* brand_ids, const float* brand_table,
+                              const int32_t* cat_ids, const float* cat_table, int32_t C, int64_t b,
+                              float* out, int64_t ld_out, uint16_t* out_bf16, void* stream) {
+  TT_REQUIRE(b >= 0 && Ht > 0 && C >= 0, "bad sizes");
+  if (b == 0) return TT_OK;
+  TT_REQUIRE(pooled && out && ld_out >= Ht + 2 * C, "null pointer or ld_out too small");
+  hipLaunchKernelGGL(k_item_concat, dim3((unsigned)b), dim3(256), 0, (hipStream_t)stream, pooled,
+                     ld_pooled, Ht, brand_ids, brand_table, cat_ids, cat_table, C, out, ld_out,
+                     out_bf16, Ht + 2 * C);
+  return check_launch("tt_item_concat");
+}

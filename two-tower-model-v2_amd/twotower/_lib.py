@@ -29,6 +29,26 @@ _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64
 _i32 = ctypes.c_int32
 
+TT_PREC_F32 = 0
+TT_PREC_BF16 = 1
+TT_ACT_NONE, TT_ACT_GELU, TT_ACT_RELU = 0, 1, 2
+
+
+class BertLayer(ctypes.Structure):
+    """tt_bert_layer (include/twotower_hip.h): device pointers of one BertLayer."""
+    _fields_ = [(n, _vp) for n in (
+        "wqkv", "bqkv", "wo", "bo", "ln1_g", "ln1_b", "w1", "b1", "w2", "b2", "ln2_g", "ln2_b",
+        "wqkv_bf16", "wo_bf16", "w1_bf16", "w2_bf16")]
+
+
+class BertModel(ctypes.Structure):
+    """tt_bert_model (include/twotower_hip.h)."""
+    _fields_ = [("vocab", _i32), ("hidden", _i32), ("heads", _i32), ("intermediate", _i32),
+                ("layers", _i32), ("max_positions", _i32), ("ln_eps", ctypes.c_float),
+                ("word_emb", _vp), ("pos_emb", _vp), ("type_emb", _vp), ("emb_ln_g", _vp),
+                ("emb_ln_b", _vp), ("layer", ctypes.POINTER(BertLayer))]
+
+
 # name -> (restype, argtypes); mirrors include/twotower_hip.h
 SIGNATURES = {
     "tt_version": (ctypes.c_int, []),
@@ -56,6 +76,19 @@ SIGNATURES = {
                                                      _i32, _vp, _i64, _vp]),
     "tt_attn_agg_l2_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp,
                                           _vp, _i64, _vp]),
+    "tt_bert_workspace_bytes": (ctypes.c_int, [_i64, _i32, _i32, _i32, ctypes.POINTER(_i64)]),
+    "tt_bert_encode": (ctypes.c_int, [ctypes.POINTER(BertModel), _vp, _vp, _i32, _i64, _i32, _i32,
+                                      _vp, _i64, _vp, _i64, _vp]),
+    "tt_gemm_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64,
+                                   _i32, _i32, _i32, _i32, _vp]),
+    "tt_gemm_bf16": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64,
+                                    _i32, _i32, _i32, _i32, _vp]),
+    "tt_layernorm_f32": (ctypes.c_int, [_vp, _i64, _vp, _vp, ctypes.c_float, _vp, _i64, _vp, _i64,
+                                        _i64, _i32, _vp]),
+    "tt_attention_varlen_f32": (ctypes.c_int, [_vp, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _i64,
+                                               _vp, _vp]),
+    "tt_item_concat": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _i64, _vp, _i64,
+                                      _vp, _vp]),
 }
 
 
