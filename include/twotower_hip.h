@@ -215,7 +215,13 @@ int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
 int tt_layernorm_f32(const float* x, int64_t ldx, const float* gamma, const float* beta,
                      float eps, float* y, int64_t ldy, uint16_t* y_bf16, int64_t ldy16,
                      int64_t rows, int32_t H, void* stream);
-/* BertSelfAttention over packed sequences: qkv [T, 3H] -> out [T, H] (head dim 32 or 64). */
+/* BertSelfAttention over packed sequences: qkv [T, 3H] -> out [T, H].
+ * tt_attention_varlen: MFMA kernel, head dim 32, prec TT_PREC_F32 (f32 MFMA) or TT_PREC_BF16
+ *   (bf16 K/Q/V/P operands, f32 accumulation and softmax).
+ * tt_attention_varlen_f32: scalar f32 kernel, head dim 32 or 64 (reference restatement). */
+int tt_attention_varlen(const float* qkv, int64_t ld_qkv, const int32_t* cu_seqlens,
+                        int32_t n_seq, int32_t max_len, int32_t H, int32_t heads, int32_t prec,
+                        float* out, int64_t ld_out, uint16_t* out_bf16, void* stream);
 int tt_attention_varlen_f32(const float* qkv, int64_t ld_qkv, const int32_t* cu_seqlens,
                             int32_t n_seq, int32_t max_len, int32_t H, int32_t heads,
                             float* out, int64_t ld_out, uint16_t* out_bf16, void* stream);

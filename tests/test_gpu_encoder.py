@@ -87,8 +87,9 @@ def test_layernorm_vs_torch():
     torch.testing.assert_close(y, F.layer_norm(x, (384,), gm, bt, 1e-12), rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("lens", [[1], [7, 64, 128], [3, 200, 1, 512, 33]])
-def test_attention_varlen_vs_torch(lens):
+@pytest.mark.parametrize("lens", [[1], [7, 64, 128], [3, 200, 1, 512, 33], [31, 32, 33, 17]])
+@pytest.mark.parametrize("kind", ["scalar", "mfma_f32", "mfma_bf16"])
+def test_attention_varlen_vs_torch(lens, kind):
     from twotower import _lib
 
     H, nh = 384, 12
@@ -96,16 +97,25 @@ def test_attention_varlen_vs_torch(lens):
     qkv = torch.randn((T, 3 * H), device="cuda")
     cu = torch.tensor(np.concatenate([[0], np.cumsum(lens)]), dtype=torch.int32, device="cuda")
     out = torch.empty((T, H), device="cuda")
-    _lib.check(_lib.lib().tt_attention_varlen_f32(qkv.data_ptr(), 3 * H, cu.data_ptr(), len(lens),
-                                                  max(lens), H, nh, out.data_ptr(), H, None,
-                                                  _lib.stream_ptr()), "attn")
+    out16 = torch.empty((T, H), device="cuda", dtype=torch.bfloat16)
+    L = _lib.lib()
+    if kind == "scalar":
+        rc = L.tt_attention_varlen_f32(qkv.data_ptr(), 3 * H, cu.data_ptr(), len(lens), max(lens),
+                                       H, nh, out.data_ptr(), H, out16.data_ptr(), _lib.stream_ptr())
+    else:
+        rc = L.tt_attention_varlen(qkv.data_ptr(), 3 * H, cu.data_ptr(), len(lens), max(lens), H, nh,
+                                   _lib.TT_PREC_BF16 if kind == "mfma_bf16" else _lib.TT_PREC_F32,
+                                   out.data_ptr(), H, out16.data_ptr(), _lib.stream_ptr())
+    _lib.check(rc, "attn")
+    assert torch.equal(out16, out.to(torch.bfloat16))
     ref = torch.empty_like(out)
     c = cu.tolist()
     for i in range(len(lens)):
         a, b = c[i], c[i + 1]
         q, k, v = (qkv[a:b, j * H:(j + 1) * H].view(b - a, nh, 32).transpose(0, 1) for j in range(3))
         ref[a:b] = (torch.softmax(q @ k.transpose(1, 2) / 32 ** 0.5, -1) @ v).transpose(0, 1).reshape(b - a, H)
-    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+    tol = 2e-2 if kind == "mfma_bf16" else 1e-5  # bf16 operands: 8-bit mantissa
+    torch.testing.assert_close(out, ref, rtol=tol, atol=tol)
 
 
 def _encoder(prec, cfg=mbg.CFG, seed=mbg.SEED):

@@ -1,0 +1,73 @@
+"""Item-tower encode throughput (configs[1]: batches of 256 texts, L ~ U[16, 128]).
+
+    python tools/bench_encoder.py [--prec bf16|f32] [--batches 20] [--batch 256]
+
+Synthetic "Arabic-like" token ids (Zipf over a 30k-id sub-range, <s>=0 / </s>=2), seeded
+MiniLM-L12 weights.  Prints one JSON line: texts/s, ms per batch, achieved TFLOP/s.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "two-tower-model-v2_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from twotower.item_tower import MINILM_L12, BertEncoder, pack_sequences, random_bert_state_dict  # noqa: E402
+
+
+def synth_batch(rng, B, lo=16, hi=128, fixed=None):
+    seqs = []
+    for _ in range(B):
+        L = fixed or int(rng.integers(lo, hi + 1))
+        body = 3 + (rng.zipf(1.1, size=L - 2) % 30000)
+        seqs.append([0] + body.tolist() + [2])
+    return seqs
+
+
+def flops(seqs, cfg):
+    H, I, nl = cfg["hidden"], cfg["intermediate"], cfg["layers"]
+    f = 0
+    for s in seqs:
+        L = len(s)
+        f += nl * (2 * L * H * (3 * H + H + 2 * I) + 4 * L * L * H)
+    return f
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--prec", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--batches", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--fixed-len", type=int, default=None)
+    a = ap.parse_args()
+    cfg = MINILM_L12
+    enc = BertEncoder(random_bert_state_dict(cfg, 0), cfg, prec=a.prec)
+    rng = np.random.default_rng(1)
+    batches = [pack_sequences(synth_batch(rng, a.batch, fixed=a.fixed_len)) for _ in range(4)]
+    seqs0 = [synth_batch(np.random.default_rng(1), a.batch, fixed=a.fixed_len)]
+    out = torch.empty((a.batch, cfg["hidden"]), device="cuda")
+    for ids, cu, mx in batches:  # warmup
+        enc.encode_packed(ids, cu, mx, out=out)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.batches):
+        ids, cu, mx = batches[i % len(batches)]
+        enc.encode_packed(ids, cu, mx, out=out)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    rng = np.random.default_rng(1)
+    fl = np.mean([flops(synth_batch(rng, a.batch, fixed=a.fixed_len), cfg) for _ in range(4)])
+    ms = dt / a.batches * 1e3
+    print(json.dumps({"prec": a.prec, "batch": a.batch, "ms_per_batch": ms,
+                      "texts_per_s": a.batch / (ms * 1e-3),
+                      "tflops": fl / (ms * 1e-3) / 1e12,
+                      "tokens_per_batch": int(batches[0][0].numel())}))
+
+
+if __name__ == "__main__":
+    main()

@@ -350,6 +350,160 @@ __global__ __launch_bounds__(128) void k_attn(const float* __restrict__ qkv, int
   }
 }
 
+// MFMA attention for head dim 32: block (4 waves) per (sequence, head), wave per 16-query tile.
+// Computes S^T = K Q^T (keys x queries) so that, in the MFMA C layout, lane (g = l >> 4,
+// q = l & 15) holds the scores of query q for keys 4g..4g+3 of each 16-key block -- exactly
+// the B-operand layout of the next product O^T = V^T P^T.  The probabilities never leave
+// registers; softmax statistics are per column (query) = a lane, reduced over g with two
+// cross-lane xors.  Keys stream in chunks of 32 with online (rescaled) softmax.
+//   BF = true : v_mfma_f32_16x16x32_bf16 (K, Q, V, P in bf16, f32 accumulate/softmax).
+//   BF = false: v_mfma_f32_16x16x4_f32 (everything f32: the parity path).
+// LDS: K [Lk][32] (rows padded to 144 B f32 / 80 B bf16) and V^T [32][vst] (vst = 128k + 4 f32
+// / 128k + 8 bf16 elements): both fragment reads are bank-conflict-free.
+template <bool BF>
+__global__ __launch_bounds__(256) void k_attn32_mfma(const float* __restrict__ qkv, int64_t ldq,
+                                                     const int32_t* __restrict__ cu, int H,
+                                                     int heads, float scale,
+                                                     float* __restrict__ out, int64_t ldo,
+                                                     uint16_t* __restrict__ out16) {
+  constexpr int DH = 32;
+  constexpr int ES = BF ? 2 : 4;
+  constexpr int KROW = DH * ES + 16;
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, ql = lane & 15;
+  const int sq = blockIdx.x / heads, h = blockIdx.x % heads;
+  const int t0 = cu[sq], L = cu[sq + 1] - t0;
+  const int Lk = (L + 31) & ~31;
+  const int vst = ((Lk + 127) & ~127) + (BF ? 8 : 4);
+  char* Ks = sm;
+  char* Vt = sm + (size_t)Lk * KROW;
+  for (int e = tid; e < Lk * DH; e += 256) {
+    const int j = e / DH, c = e % DH;
+    float kv = 0.0f, vv = 0.0f;
+    if (j < L) {
+      const float* row = qkv + (int64_t)(t0 + j) * ldq + h * DH + c;
+      kv = row[H];
+      vv = row[2 * H];
+    }
+    if (BF) {
+      *(uint16_t*)(Ks + j * KROW + c * 2) = f32_to_bf16_rne(kv);
+      *(uint16_t*)(Vt + ((size_t)c * vst + j) * 2) = f32_to_bf16_rne(vv);
+    } else {
+      *(float*)(Ks + j * KROW + c * 4) = kv;
+      *(float*)(Vt + ((size_t)c * vst + j) * 4) = vv;
+    }
+  }
+  __syncthreads();
+  for (int q0 = 16 * w; q0 < L; q0 += 64) {
+    const int qr = q0 + ql < L ? q0 + ql : L - 1;
+    const float* qp = qkv + (int64_t)(t0 + qr) * ldq + h * DH;
+    f32x4 qa = *(const f32x4*)(qp + 4 * g), qb = *(const f32x4*)(qp + 16 + 4 * g);
+    bf16x8e qf;
+    if (BF) {  // slots 8g + j <-> dims 8g + j
+      const f32x4 x0 = *(const f32x4*)(qp + 8 * g), x1 = *(const f32x4*)(qp + 8 * g + 4);
+      u32x4 u = {(uint32_t)f32_to_bf16_rne(x0[0]) | ((uint32_t)f32_to_bf16_rne(x0[1]) << 16),
+                 (uint32_t)f32_to_bf16_rne(x0[2]) | ((uint32_t)f32_to_bf16_rne(x0[3]) << 16),
+                 (uint32_t)f32_to_bf16_rne(x1[0]) | ((uint32_t)f32_to_bf16_rne(x1[1]) << 16),
+                 (uint32_t)f32_to_bf16_rne(x1[2]) | ((uint32_t)f32_to_bf16_rne(x1[3]) << 16)};
+      qf = __builtin_bit_cast(bf16x8e, u);
+    }
+    float m = -__builtin_huge_valf(), lsum = 0.0f;
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    for (int kc = 0; kc < Lk; kc += 32) {
+      f32x4 sc[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const char* kr = Ks + (kc + 16 * b + ql) * KROW;
+        f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        if (BF) {
+          const u32x4 kf = *(const u32x4*)(kr + 16 * g);
+          z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8e, kf), qf, z, 0, 0, 0);
+        } else {  // slot g <-> dim 4g + u (u < 4), 16 + 4g + (u - 4) (u >= 4)
+          const f32x4 ka = *(const f32x4*)(kr + 16 * g), kb = *(const f32x4*)(kr + 64 + 16 * g);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) z = __builtin_amdgcn_mfma_f32_16x16x4f32(ka[u], qa[u], z, 0, 0, 0);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) z = __builtin_amdgcn_mfma_f32_16x16x4f32(kb[u], qb[u], z, 0, 0, 0);
+        }
+        // z[v] = score(key kc + 16b + 4g + v, query q0 + ql)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int key = kc + 16 * b + 4 * g + v;
+          z[v] = key < L ? z[v] * scale : -__builtin_huge_valf();
+        }
+        sc[b] = z;
+      }
+      float cm = fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
+                       fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
+      cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+      const float mn = fmaxf(m, cm);
+      const float corr = expf(m - mn);
+      m = mn;
+      float ps = 0.0f;
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          sc[b][v] = expf(sc[b][v] - mn);
+          ps += sc[b][v];
+        }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      lsum = lsum * corr + ps;
+#pragma unroll
+      for (int db = 0; db < 2; ++db) acc[db] = acc[db] * corr;
+      if (BF) {  // P^T slots: j < 4 <-> key kc + 4g + j, j >= 4 <-> kc + 16 + 4g + (j - 4)
+        u32x4 pu = {(uint32_t)f32_to_bf16_rne(sc[0][0]) | ((uint32_t)f32_to_bf16_rne(sc[0][1]) << 16),
+                    (uint32_t)f32_to_bf16_rne(sc[0][2]) | ((uint32_t)f32_to_bf16_rne(sc[0][3]) << 16),
+                    (uint32_t)f32_to_bf16_rne(sc[1][0]) | ((uint32_t)f32_to_bf16_rne(sc[1][1]) << 16),
+                    (uint32_t)f32_to_bf16_rne(sc[1][2]) | ((uint32_t)f32_to_bf16_rne(sc[1][3]) << 16)};
+        const bf16x8e pf = __builtin_bit_cast(bf16x8e, pu);
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          const char* vr = Vt + ((size_t)(16 * db + ql) * vst + kc + 4 * g) * 2;
+          const uint64_t lo = *(const uint64_t*)vr, hi = *(const uint64_t*)(vr + 32);
+          u32x4 vu = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+          acc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8e, vu), pf,
+                                                            acc[db], 0, 0, 0);
+        }
+      } else {  // per 16-key block b and v: slot g <-> key kc + 16b + 4g + v
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const f32x4 vv = *(const f32x4*)(Vt + ((size_t)(16 * db + ql) * vst + kc + 16 * b + 4 * g) * 4);
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+              acc[db] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[v], sc[b][v], acc[db], 0, 0, 0);
+          }
+      }
+    }
+    // acc[db][v] = O^T[dim 16 db + 4 g + v][query q0 + ql]
+    if (q0 + ql < L) {
+      const float inv = 1.0f / lsum;
+      float* orow = out + (int64_t)(t0 + q0 + ql) * ldo + h * DH;
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const f32x4 o = acc[db] * inv;
+        *(f32x4*)(orow + 16 * db + 4 * g) = o;
+        if (out16) {
+          uint16_t* o16 = out16 + (int64_t)(t0 + q0 + ql) * ldo + h * DH + 16 * db + 4 * g;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) o16[v] = f32_to_bf16_rne(o[v]);
+        }
+      }
+    }
+  }
+}
+
+size_t attn32_smem(int max_len, bool bf) {
+  const int Lk = (max_len + 31) & ~31;
+  const int vst = ((Lk + 127) & ~127) + (bf ? 8 : 4);
+  return (size_t)Lk * (32 * (bf ? 2 : 4) + 16) + (size_t)32 * vst * (bf ? 2 : 4);
+}
+
 // Mean pooling over each packed sequence: sum_t h[t] / max(L, 1e-9)  (ST Pooling, mean).
 __global__ __launch_bounds__(256) void k_mean_pool(const float* __restrict__ x, int64_t ldx,
                                                    const int32_t* __restrict__ cu, int H,
@@ -437,6 +591,36 @@ extern "C" int tt_layernorm_f32(const float* x, int64_t ldx, const float* gamma,
   hipLaunchKernelGGL(k_layernorm, dim3((unsigned)(b < 8192 ? b : 8192)), dim3(256), 0,
                      (hipStream_t)stream, x, ldx, gamma, beta, eps, y, ldy, y_bf16, ldy16, rows, H);
   return check_launch("tt_layernorm_f32");
+}
+
+extern "C" int tt_attention_varlen(const float* qkv, int64_t ld_qkv, const int32_t* cu_seqlens,
+                                   int32_t n_seq, int32_t max_len, int32_t H, int32_t heads,
+                                   int32_t prec, float* out, int64_t ld_out, uint16_t* out_bf16,
+                                   void* stream) {
+  TT_REQUIRE(n_seq >= 0 && heads >= 1 && H % heads == 0, "bad n_seq / heads");
+  TT_REQUIRE(prec == TT_PREC_F32 || prec == TT_PREC_BF16, "bad precision");
+  if (n_seq == 0) return TT_OK;
+  TT_REQUIRE(max_len >= 1 && max_len <= 512, "max_len must be in [1, 512]");
+  TT_REQUIRE(qkv && cu_seqlens && out, "null pointer");
+  TT_REQUIRE(ld_qkv % 4 == 0 && ld_out % 4 == 0 && H % 4 == 0 && ((uintptr_t)qkv % 16) == 0 &&
+                 ((uintptr_t)out % 16) == 0, "qkv/out must be 16-B aligned rows");
+  if (H / heads != 32)
+    return fail(TT_ERR_UNSUPPORTED, "tt_attention_varlen: MFMA path needs head dim 32");
+  const bool bf = prec == TT_PREC_BF16;
+  const size_t smem = attn32_smem(max_len, bf);
+  const void* fn = bf ? (const void*)k_attn32_mfma<true> : (const void*)k_attn32_mfma<false>;
+  if (smem > 64 * 1024 &&
+      hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess)
+    return fail(TT_ERR_LAUNCH, "hipFuncSetAttribute(max dynamic LDS)");
+  const float scale = 1.0f / sqrtf(32.0f);
+  const dim3 grid((unsigned)(n_seq * heads));
+  if (bf)
+    hipLaunchKernelGGL(k_attn32_mfma<true>, grid, dim3(256), smem, (hipStream_t)stream, qkv,
+                       ld_qkv, cu_seqlens, H, heads, scale, out, ld_out, out_bf16);
+  else
+    hipLaunchKernelGGL(k_attn32_mfma<false>, grid, dim3(256), smem, (hipStream_t)stream, qkv,
+                       ld_qkv, cu_seqlens, H, heads, scale, out, ld_out, out_bf16);
+  return check_launch("tt_attention_varlen");
 }
 
 extern "C" int tt_attention_varlen_f32(const float* qkv, int64_t ld_qkv, const int32_t* cu_seqlens,
@@ -543,8 +727,12 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
             : tt_gemm_f32(w.x, H, L.wqkv, H, L.bqkv, nullptr, 0, w.qkv, 3 * H, nullptr, 0, (int)T,
                           3 * H, H, ACT_NONE, stream);
     if (rc) return rc;
-    rc = tt_attention_varlen_f32(w.qkv, 3 * H, cu_seqlens, n_seq, max_len, H, m->heads, w.ctx, H,
-                                 bf ? w.ctx16 : nullptr, stream);
+    if (H / m->heads == 32)
+      rc = tt_attention_varlen(w.qkv, 3 * H, cu_seqlens, n_seq, max_len, H, m->heads, prec, w.ctx,
+                               H, bf ? w.ctx16 : nullptr, stream);
+    else
+      rc = tt_attention_varlen_f32(w.qkv, 3 * H, cu_seqlens, n_seq, max_len, H, m->heads, w.ctx,
+                                   H, bf ? w.ctx16 : nullptr, stream);
     if (rc) return rc;
     // y = ctx Wo^T + bo + x ; x = LN(y)
     rc = bf ? tt_gemm_bf16(w.ctx16, H, L.wo_bf16, H, L.bo, w.x, H, w.y, H, nullptr, 0, (int)T, H, H,

@@ -85,6 +85,8 @@ SIGNATURES = {
                                     _i32, _i32, _i32, _i32, _vp]),
     "tt_layernorm_f32": (ctypes.c_int, [_vp, _i64, _vp, _vp, ctypes.c_float, _vp, _i64, _vp, _i64,
                                         _i64, _i32, _vp]),
+    "tt_attention_varlen": (ctypes.c_int, [_vp, _i64, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i64,
+                                           _vp, _vp]),
     "tt_attention_varlen_f32": (ctypes.c_int, [_vp, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _i64,
                                                _vp, _vp]),
     "tt_item_concat": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _i64, _vp, _i64,
