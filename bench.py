@@ -54,6 +54,10 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-single", type=int, default=128)
     p.add_argument("--cpu-batch", type=int, default=2048)
+    p.add_argument("--mode-a-buyers", type=int, default=256,
+                   help="Mode A sample per rank (history texts re-encoded); 0 disables")
+    p.add_argument("--mode-a-prec", choices=["bf16", "f32"], default="bf16")
+    p.add_argument("--mode-a-steps", type=int, default=3)
     return p.parse_args()
 
 
@@ -63,6 +67,83 @@ def event_mix(gen, shape, device):
     w[u > 0.75] = 5.0
     w[u > 0.92] = 10.0
     return w
+
+
+def synth_text_ids(rng, n, vocab, lo=16, hi=128):
+    """Synthetic 'Arabic-like' token sequences: <s>=0, Zipf(1.1) ids over a 30k sub-range,
+    </s>=2; lengths ~ U[lo, hi] (SURVEY.md section 8(d), configs[1])."""
+    out = []
+    for _ in range(n):
+        L = int(rng.integers(lo, hi + 1))
+        out.append([0] + (3 + (rng.zipf(1.1, size=L - 2) % 30000) % (vocab - 3)).tolist() + [2])
+    return out
+
+
+def mode_a(a, dev, world, rank, search_local, k, E):
+    """Mode A: EmbeddingEncoder.encode_buyer as written (src/inference/encoder.py:286-303):
+    each buyer's S history texts are re-encoded by the item tower (MiniLM encoder on HIP,
+    projection head, F.normalize), then weighted-averaged and searched."""
+    from twotower.item_tower import MINILM_L12, BertEncoder, ItemTower, pack_sequences, \
+        random_bert_state_dict
+
+    B, S = a.mode_a_buyers, a.hist
+    cfg = MINILM_L12
+    sd = random_bert_state_dict(cfg, 0)
+    enc = BertEncoder(sd, cfg, device=dev, prec=a.mode_a_prec)
+
+    class _Dim:
+        def get_sentence_embedding_dimension(self):
+            return cfg["hidden"]
+
+    torch.manual_seed(0)
+    it = ItemTower(text_encoder=_Dim())
+    it.initialize_categorical_embeddings([f"brand{i}" for i in range(50)],
+                                         [f"cat{i}" for i in range(20)])
+    it.to(dev).eval()
+    rng = np.random.default_rng(100 + rank)
+    seqs = synth_text_ids(rng, B * S, cfg["vocab"])
+    ids, cu, mx = pack_sequences(seqs, dev)
+    bid = rng.integers(0, 51, B * S).tolist()
+    cid = rng.integers(0, 21, B * S).tolist()
+    w = event_mix(torch.Generator(device=dev).manual_seed(7 + rank), (B, S), dev)
+    pooled = torch.empty((B * S, cfg["hidden"]), device=dev)
+    ex = TopkExchange(B, _lib.padded_dim(E), k, device=dev)
+
+    def step():
+        enc.encode_packed(ids, cu, mx, out=pooled)
+        items = it.head(pooled, bid, cid, use_cat=True)            # [B*S, E] unit rows
+        q = kernels.weighted_avg_l2(items.view(B, S, E), w)         # BuyerTower.forward
+        qn = torch.zeros((B, _lib.padded_dim(E)), device=dev)
+        kernels.l2norm_rows(q, E, _lib.TT_NORM_ADD_EPS, out=qn)      # retrieve :152-153
+        return ex.search(qn, search_local, kernels.merge_topk)
+
+    step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.mode_a_steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = (time.perf_counter() - t0) / a.mode_a_steps
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    tokens = int(ids.numel())
+    res = {"value": world * B / dt, "unit": "buyers/s", "ms_per_step": dt * 1e3,
+           "buyers_per_rank": B, "texts_per_step_per_rank": B * S,
+           "tokens_per_step_per_rank": tokens, "encoder_prec": a.mode_a_prec,
+           "texts_per_s": world * B * S / dt,
+           "model": "MiniLM-L12 architecture (12L/384h/12 heads/FFN 1536, vocab 250037), "
+                    "seeded random weights; synthetic token ids, L ~ U[16,128]"}
+    cpu_inputs = (sd, cfg, {k2: v.detach().cpu() for k2, v in it.state_dict().items()},
+                  [seqs[b * S:(b + 1) * S] for b in range(4)],
+                  [bid[b * S:(b + 1) * S] for b in range(4)],
+                  [cid[b * S:(b + 1) * S] for b in range(4)], w[:4].cpu().numpy())
+    return res, cpu_inputs
 
 
 def main():
@@ -209,6 +290,16 @@ def main():
             "achieved_hbm_gbps": alg_bytes / (scan_ms * 1e-3) / 1e9,
         },
     }
+    def local_search_k(qall):  # Mode A search (its own query count; workspace per call)
+        if a.method == "bf16":
+            return kernels.scan_topk_bf16(shard, shard16, hi - lo, E, qall, K, bounds,
+                                          row_base=lo)
+        return kernels.scan_topk(shard, hi - lo, E, qall, K, row_base=lo)
+
+    cpu_a = None
+    if a.mode_a_buyers > 0:
+        result["mode_a"], cpu_a = mode_a(a, dev, world, rank, lambda qall: local_search_k(qall),
+                                         K, E)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         sys.path.insert(0, ROOT)
         from oracle import cpu_baseline
@@ -223,6 +314,12 @@ def main():
                                                   single_buyers=a.cpu_single,
                                                   batch_buyers=a.cpu_batch)
         result["cpu_baseline"]["gpu_over_cpu_single"] = value / result["cpu_baseline"]["value"]
+        if cpu_a is not None:
+            sd_, cfg_, head_, seqs_, bid_, cid_, w_ = cpu_a
+            result["mode_a"]["cpu_baseline"] = cpu_baseline.run_mode_a(
+                sd_, cfg_, head_, seqs_, bid_, cid_, w_, cat_np, K, n_buyers=3)
+            result["mode_a"]["gpu_over_cpu_single"] = (
+                result["mode_a"]["value"] / result["mode_a"]["cpu_baseline"]["value"])
     if rank == 0:
         print(json.dumps(result))
     if world > 1:

@@ -13,6 +13,11 @@ Two variants:
   (ii) batched: retrieve_batch over query blocks (vector_db.py:171-209; no caller in the repo).
 If ``import faiss`` works on the host, the faiss IndexFlatIP itself is timed instead
 (kind "reference").
+
+``run_mode_a`` times Mode A (EmbeddingEncoder.encode_buyer as written, encoder.py:286-303:
+the history texts are re-encoded by the item tower) one buyer at a time: the torch-CPU
+restatement of the MiniLM encoder (oracle/bert_ref.py) + projection head + weighted average +
+nq = 1 exact search.
 """
 from __future__ import annotations
 
@@ -82,3 +87,37 @@ def run(table_np: np.ndarray, catalog_np: np.ndarray, hist: np.ndarray, w: np.nd
         "batched_value": nb / t_batch,
         "seconds": t_single + t_batch,
     }
+
+
+def run_mode_a(sd, cfg, head_sd, seqs_per_buyer, brand_ids, cat_ids, w, catalog_np, k,
+               n_buyers: int = 2, threads: int | None = None) -> dict:
+    """Mode A per buyer: encode S history texts (bert_ref, torch CPU f32) -> head ->
+    weighted average -> F.normalize -> q/(||q||+1e-8) -> exact top-k (nq = 1)."""
+    from . import bert_ref
+
+    threads = threads or int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    cat = torch.from_numpy(catalog_np)
+
+    def one(b):
+        seqs = seqs_per_buyer[b]
+        cu = np.concatenate([[0], np.cumsum([len(x) for x in seqs])])
+        with torch.no_grad():
+            te = bert_ref.bert_mean_pool(sd, cfg, torch.tensor([t for x in seqs for t in x]), cu)
+            items = bert_ref.item_head(te, head_sd, brand_ids[b], cat_ids[b])
+        wt = torch.from_numpy(w[b:b + 1]).unsqueeze(-1)
+        nw = wt / (wt.sum(dim=1, keepdim=True) + 1e-8)
+        q = _norm(F.normalize((items.unsqueeze(0) * nw).sum(dim=1), p=2, dim=1).numpy())
+        torch.topk(torch.from_numpy(q) @ cat.T, k, dim=1)
+
+    one(0)  # warm-up
+    t0 = time.perf_counter()
+    for b in range(n_buyers):
+        one(b)
+    dt = time.perf_counter() - t0
+    n_texts = sum(len(seqs_per_buyer[b]) for b in range(n_buyers))
+    return {"value": n_buyers / dt, "unit": "buyers/s", "cores": threads, "kind": "port",
+            "sample": f"{n_buyers} buyers one at a time, {n_texts} history texts re-encoded by "
+                      f"a torch-CPU f32 MiniLM-L12 restatement + head + exact top-{k} "
+                      f"(nq=1) over {catalog_np.shape[0]} rows",
+            "seconds": dt}
