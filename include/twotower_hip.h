@@ -203,7 +203,7 @@ int tt_bert_encode(const tt_bert_model* model, const int32_t* ids, const int32_t
  * item_tower.py:58-63: Linear -> ReLU -> Dropout(eval) -> Linear; then tt_l2norm_rows_f32
  * with TT_NORM_MAX_EPS for F.normalize, :209).
  * tt_gemm_*: C[M,N] = act(A[M,K] . W[N,K]^T + bias) + residual, f32 out (+ optional bf16
- *   copy C_bf16); N % 128 == 0; K % 32 (f32) / K % 64 (bf16) == 0; bias/residual may be NULL. */
+ *   copy C_bf16); K % 32 (f32) / K % 64 (bf16) == 0, any M, N; bias/residual may be NULL. */
 int tt_gemm_f32(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias,
                 const float* residual, int64_t ldr, float* C, int64_t ldc, uint16_t* C_bf16,
                 int64_t ldc16, int32_t M, int32_t N, int32_t K, int32_t act, void* stream);
@@ -231,6 +231,22 @@ int tt_item_concat(const float* pooled, int64_t ld_pooled, int32_t Ht, const int
                    const float* brand_table, const int32_t* cat_ids, const float* cat_table,
                    int32_t C, int64_t b, float* out, int64_t ld_out, uint16_t* out_bf16,
                    void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * InfoNCE loss with in-batch negatives (tt_loss.hip), forward and backward in one call.
+ * Replaces InfoNCELoss.forward (src/training/losses.py:20-79) + its autograd backward.
+ * b [B, E] (ldb), p [B, E] (ldp), n [B, N, E] (row stride ldn_row, item stride ldn_item),
+ * N <= 64, E % 32 == 0 (f32) / % 64 == 0 (bf16).  loss: ONE device float (mean over rows).
+ * grad_b [B, E], grad_p [B, E], grad_n [B, N, E] (contiguous) are d loss / d input; pass
+ * NULL for all three to skip the backward.  prec selects f32 or bf16 MFMA for the three
+ * B x B x E GEMMs (softmax and the rest in f32).  Workspace: tt_infonce_workspace_bytes.
+ * --------------------------------------------------------------------------------- */
+int tt_infonce_workspace_bytes(int32_t B, int32_t N, int32_t E, int32_t prec,
+                               int32_t with_grads, int64_t* bytes);
+int tt_infonce_f32(const float* b, int64_t ldb, const float* p, int64_t ldp, const float* n,
+                   int64_t ldn_row, int64_t ldn_item, int32_t B, int32_t N, int32_t E,
+                   float temperature, int32_t prec, float* loss, float* grad_b, float* grad_p,
+                   float* grad_n, void* workspace, int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -108,3 +108,21 @@ def test_hash_tokenizer_deterministic():
     assert a == tok(["hello world", " ", "a b c d e f g h i j"])
     assert a[0][0] == 0 and a[0][-1] == 2 and len(a[2]) == 8 and a[1] == [0, 2]
     assert all(3 <= t < 1000 for s in a for t in s[1:-1])
+
+
+@pytest.mark.parametrize("case", list(gi.INFONCE_CASES))
+def test_infonce_oracle_vs_reference_fixture(golden, case):
+    from oracle import losses_ref
+
+    g = golden("infonce.npz")
+    spec = gi.INFONCE_CASES[case]
+    b, p, n = (torch.from_numpy(a).requires_grad_(True) for a in gi.infonce_inputs(spec))
+    loss = losses_ref.infonce(b, p, n, spec["tau"])
+    loss.backward()
+    assert abs(loss.item() - g[case + "__loss"][0]) < 1e-6
+    if case + "__gb" in g:
+        for t, k in ((b, "gb"), (p, "gp"), (n, "gn")):
+            np.testing.assert_allclose(t.grad.numpy(), g[f"{case}__{k}"], rtol=0, atol=1e-7)
+    else:
+        gn = [t.grad.norm().item() for t in (b, p, n)]
+        np.testing.assert_allclose(gn, g[case + "__gnorm"], rtol=1e-5)

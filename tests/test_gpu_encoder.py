@@ -64,6 +64,18 @@ def test_gemm_bf16_vs_torch(M, N, K):
     torch.testing.assert_close(C.double(), ref, rtol=1e-4, atol=1e-4)  # exact products, f32 sums
 
 
+@pytest.mark.parametrize("M,N,K", [(8, 8, 384), (513, 517, 768), (3, 100, 64)])
+def test_gemm_ragged_n(M, N, K):
+    g = torch.Generator(device="cuda").manual_seed(N)
+    A = torch.randn((M, K), generator=g, device="cuda")
+    W = torch.randn((N, K), generator=g, device="cuda")
+    C, _ = _gemm(A, W)
+    torch.testing.assert_close(C.double(), A.double() @ W.double().T, rtol=1e-5, atol=1e-4)
+    C, _ = _gemm(A, W, prec="bf16")
+    ref = A.to(torch.bfloat16).double() @ W.to(torch.bfloat16).double().T
+    torch.testing.assert_close(C.double(), ref, rtol=1e-4, atol=1e-3)
+
+
 def test_gemm_rejects_unsupported_shapes():
     from twotower import _lib
 

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
-  const int n_tn = N / GM_BN;
+  const int n_tn = (N + GM_BN - 1) / GM_BN;
   const int lb = enc_xcd_remap(blockIdx.x, gridDim.x);
   const int tm = lb / n_tn, tn = lb % n_tn;
   const int m0 = tm * GM_BM, n0 = tn * GM_BN;
@@ -98,8 +98,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_
     const int c = (lane & 7) ^ ((row >> 1) & 7);
     int am = m0 + row;
     am = am < M ? am : M - 1;
+    int wn_ = n0 + row;
+    wn_ = wn_ < N ? wn_ : N - 1;  // rows past N: clamped loads, masked stores
     a_off[j] = (int64_t)am * lda + c * EPC;
-    w_off[j] = (int64_t)(n0 + row) * ldw + c * EPC;
+    w_off[j] = (int64_t)wn_ * ldw + c * EPC;
   }
   auto issue = [&](int kt) {
     char* st = smem + (kt & 1) * GM_STAGE_B;
@@ -178,6 +180,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int n = n0 + 64 * wn + 16 * j + rl;
+    if (n >= N) continue;
     const float bn = bias ? bias[n] : 0.0f;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -550,13 +553,13 @@ extern "C" int tt_gemm_f32(const float* A, int64_t lda, const float* W, int64_t 
                            int32_t K, int32_t act, void* stream) {
   TT_REQUIRE(M >= 0 && N >= 0 && K >= 0, "negative size");
   if (M == 0 || N == 0) return TT_OK;
-  if (N % GM_BN != 0 || K % GemmElt<float>::BK != 0)
-    return fail(TT_ERR_UNSUPPORTED, "tt_gemm_f32: need N % 128 == 0 and K % 32 == 0");
+  if (K % GemmElt<float>::BK != 0)
+    return fail(TT_ERR_UNSUPPORTED, "tt_gemm_f32: need K % 32 == 0");
   TT_REQUIRE(A && W && C, "null pointer");
   TT_REQUIRE(lda % 4 == 0 && ldw % 4 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0,
              "A/W must be 16-B aligned with lda, ldw % 4 == 0");
   TT_REQUIRE(act >= 0 && act <= 2, "bad activation");
-  const int nblk = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
+  const int nblk = ((M + GM_BM - 1) / GM_BM) * ((N + GM_BN - 1) / GM_BN);
   hipLaunchKernelGGL(k_gemm<float>, dim3(nblk), dim3(256), 0, (hipStream_t)stream, A, lda, W, ldw,
                      bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
   return check_launch("tt_gemm_f32");
@@ -568,13 +571,13 @@ extern "C" int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, i
                             int32_t K, int32_t act, void* stream) {
   TT_REQUIRE(M >= 0 && N >= 0 && K >= 0, "negative size");
   if (M == 0 || N == 0) return TT_OK;
-  if (N % GM_BN != 0 || K % GemmElt<uint16_t>::BK != 0)
-    return fail(TT_ERR_UNSUPPORTED, "tt_gemm_bf16: need N % 128 == 0 and K % 64 == 0");
+  if (K % GemmElt<uint16_t>::BK != 0)
+    return fail(TT_ERR_UNSUPPORTED, "tt_gemm_bf16: need K % 64 == 0");
   TT_REQUIRE(A && W && C, "null pointer");
   TT_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0,
              "A/W must be 16-B aligned with lda, ldw % 8 == 0");
   TT_REQUIRE(act >= 0 && act <= 2, "bad activation");
-  const int nblk = ((M + GM_BM - 1) / GM_BM) * (N / GM_BN);
+  const int nblk = ((M + GM_BM - 1) / GM_BM) * ((N + GM_BN - 1) / GM_BN);
   hipLaunchKernelGGL(k_gemm<uint16_t>, dim3(nblk), dim3(256), 0, (hipStream_t)stream, A, lda, W,
                      ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
   return check_launch("tt_gemm_bf16");

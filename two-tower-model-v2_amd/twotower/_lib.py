@@ -89,6 +89,10 @@ SIGNATURES = {
                                            _vp, _vp]),
     "tt_attention_varlen_f32": (ctypes.c_int, [_vp, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _i64,
                                                _vp, _vp]),
+    "tt_infonce_workspace_bytes": (ctypes.c_int, [_i32, _i32, _i32, _i32, _i32,
+                                                  ctypes.POINTER(_i64)]),
+    "tt_infonce_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32,
+                                      ctypes.c_float, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "tt_item_concat": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _i64, _vp, _i64,
                                       _vp, _vp]),
 }
