@@ -206,6 +206,12 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #ifndef TT_EXP_NOBAR
 #define TT_EXP_NOBAR 0  // skip the per-step barrier
 #endif
+#ifndef TT_EXP_NOWRITE
+#define TT_EXP_NOWRITE 0  // selection control flow without the LDS pool writes
+#endif
+#ifndef TT_EXP_MAXONLY
+#define TT_EXP_MAXONLY 0  // per-block max + ballot only (no per-slot scan)
+#endif
 constexpr int RG_WAVES = 8, RG_PD = 3, RG_SLOTS = RG_PD + 1;
 constexpr int RG_POOL = 4096;                  // pool entries per block
 constexpr int RG_WPOOL = RG_POOL / RG_WAVES;   // ... per wave (wave-private region)
@@ -331,22 +337,30 @@ __global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
   // pos ^ (r & FM) of that row, so row r's logical chunk c lives at position c ^ (r & FM).
   // Per lane the (row, column byte) of each piece is loop-invariant.
   const int64_t row_bytes = stride * ld * 2;
-  int dr[PPW], dcol[PPW];
+  const char* src0[PPW];  // lane's source of piece pp in tile 0 (full tiles: + t * tile_bytes)
 #pragma unroll
   for (int pp = 0; pp < PPW; ++pp) {
     const int P = (w + RG_WAVES * pp) * 64 + lane;
-    dr[pp] = P / CPR;
-    dcol[pp] = 16 * ((P % CPR) ^ (dr[pp] & FM));
+    const int r = P / CPR;
+    src0[pp] = (const char*)xb + (j0 + r) * row_bytes + 16 * ((P % CPR) ^ (r & FM));
   }
-  auto issue = [&](int t) {
+  const int64_t tile_bytes = row_bytes * TR;
+  auto issue = [&](int t) __attribute__((always_inline)) {
     char* slot = ring + (t % RG_SLOTS) * TILE_B;
     const int64_t jt = j0 + (int64_t)t * TR;
     const bool clamp = jt + TR > j1;  // wave-uniform: only the slab's last tile
 #pragma unroll
     for (int pp = 0; pp < PPW; ++pp) {
-      int64_t j = jt + dr[pp];
-      if (clamp) j = j < j1 ? j : j1 - 1;
-      const char* src = (const char*)xb + j * row_bytes + dcol[pp];
+      const char* src;
+      if (!clamp) {
+        src = src0[pp] + (int64_t)t * tile_bytes;
+      } else {  // recompute the lane's (row, column) of piece pp: rare path, no live registers
+        const int P = (w + RG_WAVES * pp) * 64 + lane;
+        const int r = P / CPR;
+        int64_t j = jt + r;
+        j = j < j1 ? j : j1 - 1;
+        src = (const char*)xb + j * row_bytes + 16 * ((P % CPR) ^ (r & FM));
+      }
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(
                                            slot + (w + RG_WAVES * pp) * 1024),
@@ -360,7 +374,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
   uint64_t* wkey = pool_key + w * RG_WPOOL;
   uint32_t* wmeta = pool_meta + w * RG_WPOOL;
   uint32_t wn = 0;
-  auto flush = [&]() {
+  auto flush = [&]() __attribute__((always_inline)) {
     const int n = wn < (uint32_t)RG_WPOOL ? (int)wn : RG_WPOOL;
     for (int i = lane; i < n; i += 64) {
       const uint32_t ql = wmeta[i];
@@ -383,7 +397,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
 
   // Fast reject of a finished tile (lane: RB*4 scores per query block): per-block maxima.
   // NaN scores (the t = 0 placeholder, NaN rows) never pass a >= test.
-  auto tile_max = [&](const f32x4 (&sc)[RB][QB], float (&mx)[QB]) {
+  auto tile_max = [&](const f32x4 (&sc)[RB][QB], float (&mx)[QB]) __attribute__((always_inline)) {
 #pragma unroll
     for (int b = 0; b < QB; ++b) {
       float m = sc[0][b][0];
@@ -398,7 +412,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
   // One v_cmp + scalar branch per candidate slot; lanes of a non-empty slot write at
   // wn + (passing lanes below).  An entry past the wave's pool marks its query overflowed
   // (-> exact fallback).  Rows past the slab end (its last tile only) are masked to -inf first.
-  auto append = [&](f32x4 (&sc)[RB][QB], const float (&mx)[QB], int t) {
+  auto append = [&](f32x4 (&sc)[RB][QB], const float (&mx)[QB], int t) __attribute__((always_inline)) {
     const int64_t jt = j0 + (int64_t)t * TR;
     if (jt + TR > j1) {
 #pragma unroll
@@ -413,6 +427,10 @@ __global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
 #pragma unroll
     for (int b = 0; b < QB; ++b) {
       if (__ballot(mx[b] >= th[b]) == 0ull) continue;
+      if (TT_EXP_MAXONLY) {
+        asm volatile("" ::: "memory");
+        continue;
+      }
       const uint32_t ql = (uint32_t)(w * QPW + 16 * b + col);
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb)
@@ -424,7 +442,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
             const uint32_t pos =
                 wn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
                                                __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
-            if (v >= th[b]) {
+            if (!TT_EXP_NOWRITE && v >= th[b]) {
               if (pos < (uint32_t)RG_WPOOL) {
                 const uint32_t u = __float_as_uint(v + 0.0f);  // not NaN: it passed
                 const uint32_t key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -441,17 +459,24 @@ __global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
     }
   };
   // wait until only `younger` tiles issued after the awaited one are still in flight
-  auto wait_tiles = [&](int younger) {
+  auto wait_tiles = [&](int younger) __attribute__((always_inline)) {
     if (TT_EXP_NODMA) return;
     if (younger >= 2) wait_vm<2 * PPW>();
     else if (younger == 1) wait_vm<PPW>();
     else wait_vm<0>();
   };
 
-  // Step t: issue tile t+PD; MFMAs of tile t; selection of tile t-1 (its VALU fills the
-  // MFMA issue gaps); wait for tile t+1 and barrier.  The barrier therefore sits behind a
-  // full step of in-flight MFMAs, and the slot the next issue overwrites (tile t-1's) was
-  // last read before it.
+  // Continuous MFMA stream over the slab: A fragments are read FD k-steps ahead into a
+  // static register ring that runs ACROSS tile boundaries (the first FD steps of tile t+1
+  // are read during the last FD steps of tile t), with hand-counted lgkmcnt waits.  Once per
+  // tile, at step S_MID (before the first cross-tile read), every wave waits for its DMA
+  // pieces of tile t+1, the block barriers (tile t+1 visible; every wave done with tile t-1),
+  // and the slot of tile t-1 is refilled with tile t+PD.  The selection of tile t-1 (per-block
+  // max mid-tile, then the candidate scan) runs between tile t's MFMAs.
+  // FD + 1 divides KS (the ring index is s % (FD + 1)); 2 steps ahead where registers are tight
+  constexpr int FD = (EP >= 384 && KS % 3 == 0) ? 2 : (KS >= 4 ? 3 : 1);
+  constexpr int S_MID = (KS - FD) / 2;
+  static_assert(KS % (FD + 1) == 0 && S_MID < KS - FD, "fragment ring layout");
   for (int t = 0; t < RG_PD && t < n_tiles; ++t) issue(t);
   wait_tiles(n_tiles - 1 < RG_PD - 1 ? n_tiles - 1 : RG_PD - 1);
   lds_barrier();  // tile 0 landed; counters initialised
@@ -462,36 +487,39 @@ __global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
 #pragma unroll
     for (int b = 0; b < QB; ++b) accp[rb][b] = f32x4{qnan, qnan, qnan, qnan};
 
-  // A fragments are read FD k-steps ahead of their MFMAs into a static register ring, so the
-  // compiler's counted lgkmcnt waits cover the LDS latency instead of draining every pair.
-  constexpr int FD = 3;
-  for (int t = 0; t < n_tiles; ++t) {
-    if (!TT_EXP_NODMA && t + RG_PD < n_tiles) issue(t + RG_PD);
-    const char* slot = ring + (t % RG_SLOTS) * TILE_B;
-    uint32_t ra[RB][4];  // per-lane fragment addresses of k-steps s = 4m + (0..3)
+  // fragment address = lrd (lane part) + slot base (wave-uniform)
+  const uint32_t ring_base = lds_addr(ring);
+  u32x4 fr[FD + 1][RB];
+  auto read_step = [&](uint32_t slot_base, auto sc_) __attribute__((always_inline)) {
+    constexpr int S = decltype(sc_)::value;
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) ra[rb][i] = lds_addr(slot) + lrd[rb][i];
-    u32x4 fr[FD + 1][RB];
-    auto read_step = [&](auto sc_) {
-      constexpr int S = decltype(sc_)::value;
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb) fr[S % (FD + 1)][rb] = lds_read128<256 * (S >> 2)>(ra[rb][S & 3]);
-    };
-    static_for<FD>([&](auto s_) { read_step(s_); });
+      fr[S % (FD + 1)][rb] = lds_read128<256 * (S >> 2)>(slot_base + lrd[rb][S & 3]);
+  };
+  if (n_tiles > 0) static_for<FD>([&](auto s_) __attribute__((always_inline)) { read_step(ring_base, s_); });
+  for (int t = 0; t < n_tiles; ++t) {
+    const bool has_next = t + 1 < n_tiles;
+    const uint32_t sb = ring_base + (uint32_t)((t % RG_SLOTS) * TILE_B);
+    const uint32_t sbn = ring_base + (uint32_t)(((t + 1) % RG_SLOTS) * TILE_B);
     f32x4 acc[RB][QB];
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int b = 0; b < QB; ++b) acc[rb][b] = f32x4{0.f, 0.f, 0.f, 0.f};
     float mx[QB];
-    static_for<KS>([&](auto s_) {
+    static_for<KS>([&](auto s_) __attribute__((always_inline)) {
       constexpr int s = decltype(s_)::value;
-      if constexpr (s + FD < KS) read_step(std::integral_constant<int, s + FD>{});
-      // reads of steps s+1 .. min(s+FD, KS-1) may stay in flight
-      constexpr int younger = (s + FD < KS ? FD : KS - 1 - s) * RB;
-      lds_wait<younger>();
+      if constexpr (s + FD < KS) {
+        read_step(sb, std::integral_constant<int, s + FD>{});
+        lds_wait<FD * RB>();
+      } else {
+        if (has_next) {
+          read_step(sbn, std::integral_constant<int, s + FD - KS>{});
+          lds_wait<FD * RB>();
+        } else {
+          lds_wait<(KS - 1 - s) * RB>();
+        }
+      }
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) reg_tie(fr[s % (FD + 1)][rb]);
 #pragma unroll
@@ -501,15 +529,24 @@ __global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
         for (int b = 0; b < QB; ++b)
           acc[rb][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[b][s], acc[rb][b], 0, 0, 0);
       }
-      if constexpr (s == KS / 2) tile_max(accp, mx);  // VALU between this tile's MFMAs
+      if constexpr (s == 0) tile_max(accp, mx);  // VALU between this tile's MFMAs
+      if constexpr (s == S_MID) {
+        if (has_next) {
+          if (t + 2 < n_tiles) wait_vm<PPW>();
+          else wait_vm<0>();
+        }
+        if (!TT_EXP_NOBAR) asm volatile("s_barrier" ::: "memory");
+        if (!TT_EXP_NODMA && t + RG_PD < n_tiles) issue(t + RG_PD);
+      }
+      if constexpr (s == (KS > 1 ? 1 : 0)) {  // early: tile t-1's scores die before the peak
+        if (!TT_EXP_NOSEL) append(accp, mx, t - 1);
+        if (TT_EXP_NOSEL) {
+#pragma unroll
+          for (int b = 0; b < QB; ++b)
+            if (mx[b] >= th[b]) asm volatile("" ::: "memory");
+        }
+      }
     });
-    if (!TT_EXP_NOSEL) append(accp, mx, t - 1);
-    if (TT_EXP_NOSEL && mx[0] >= th[0]) asm volatile("" ::: "memory");
-    if (t + 1 < n_tiles) {
-      const int younger = (n_tiles - 2 - t) < (RG_PD - 1) ? (n_tiles - 2 - t) : (RG_PD - 1);
-      wait_tiles(younger);
-    }
-    if (!TT_EXP_NOBAR) lds_barrier();
     if (wn >= (uint32_t)RG_WFLUSH) flush();
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
@@ -759,6 +796,40 @@ struct FilterPlan {
 // <= SEL_CAP/2 rows and is scored densely (every row a candidate); the others stream through
 // the ring kernel.  J = rows of a sample level's top list that feed the next threshold: the
 // full catalog has ~16*J rows above a_J(stride-16 sample), comfortably >= k.
+static int device_cus() {
+  static const int cus = [] {
+    int d = 0, v = 0;
+    if (hipGetDevice(&d) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && v > 0)
+      return v;
+    return 256;  // MI355X
+  }();
+  return cus;
+}
+
+// Slab count of a ring level: the kernel runs one 512-thread block per CU (148 KB LDS), so
+// the n_qt * slabs blocks execute in ceil(blocks / CUs) equal rounds.  Minimise
+// rounds * (rows per slab + per-slab overhead ~ 3 tiles), slabs <= 64 (list memory and
+// k_select work grow with the slab count), slabs >= 1 tile-row chunk of 256 rows.
+static int64_t ring_slabs(int n_qt, int64_t n_sample) {
+  const int ncu = device_cus();
+  int64_t sl_max = n_sample / 256;
+  if (sl_max > 64) sl_max = 64;
+  if (sl_max < 1) sl_max = 1;
+  int64_t best = 1;
+  double best_cost = 1e300;
+  for (int64_t sl = 1; sl <= sl_max; ++sl) {
+    const int64_t rounds = ((int64_t)n_qt * sl + ncu - 1) / ncu;
+    const int64_t rows = ((n_sample + sl - 1) / sl + 63) / 64 * 64;
+    const double cost = (double)rounds * (double)(rows + 96);
+    if (cost < best_cost * 0.999) {
+      best_cost = cost;
+      best = sl;
+    }
+  }
+  return best;
+}
+
 static FilterPlan plan_filter(int64_t n, int nq, int k, int ep) {
   FilterPlan p;
   // ~16*J full-catalog rows lie above a_J(stride-16 sample); J = k/8 + 12 keeps that count
@@ -788,10 +859,7 @@ static FilterPlan plan_filter(int64_t n, int nq, int k, int ep) {
     if (L.dense) {
       sl = (L.n_sample + FL_CAP / 2 - 1) / (FL_CAP / 2);  // every row is a candidate
     } else {
-      // >= ~3 blocks per CU in flight over the level; slabs >= 8 tiles long
-      sl = (768 + L.n_qt - 1) / L.n_qt;
-      const int64_t max_by_rows = (L.n_sample + 255) / 256;
-      if (sl > max_by_rows) sl = max_by_rows;
+      sl = ring_slabs(L.n_qt, L.n_sample);
     }
     if (sl < 1) sl = 1;
     int64_t r = (L.n_sample + sl - 1) / sl;
