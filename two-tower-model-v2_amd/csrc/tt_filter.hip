@@ -690,6 +690,124 @@ __global__ __launch_bounds__(256) void k_select(const uint64_t* __restrict__ lis
   if (threadIdx.x == 0) band_n[qid] = nband;
 }
 
+// Wave-per-query selection (replaces the block sort): the candidate keys of a query are
+// gathered into a wave-private LDS buffer, the R-th largest score (R = J or k) is found by a
+// 32-step bitwise search on the orderable score bits (count of keys >= candidate, reduced
+// across the wave), and -- full level -- the band a >= A_k - eps2 is compacted with
+// ballot/mbcnt (unordered: k_rerank sorts by the exact score).  Same outputs as k_select.
+constexpr int SW_CAP = 2048;  // candidates per query (more: the query takes the exact fallback)
+__global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict__ lists,
+                                                     const int* __restrict__ counts, int n_slabs,
+                                                     int k, int J, const float* __restrict__ eps2,
+                                                     int mode, float* __restrict__ theta_out,
+                                                     float* __restrict__ aref,
+                                                     uint64_t* __restrict__ band,
+                                                     int* __restrict__ band_n,
+                                                     int* __restrict__ flags, int* qsel,
+                                                     int* qsel_n, int nq) {
+  __shared__ uint64_t buf[4][SW_CAP];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int qid = blockIdx.x * 4 + w;
+  if (qid >= nq) return;  // the whole wave (no block-level barriers below)
+  uint64_t* kb = buf[w];
+  if (flags[qid]) {
+    if (lane == 0 && mode == 0) theta_out[qid] = __builtin_huge_valf();
+    return;
+  }
+  const int* qc = counts + (int64_t)qid * n_slabs;
+  const uint64_t* ql = lists + (int64_t)qid * n_slabs * FL_CAP;
+  // slab counts -> offsets (wave scan, 64 slabs per pass)
+  int total = 0;
+  bool bad = false;
+  for (int s0 = 0; s0 < n_slabs; s0 += 64) {
+    int c = s0 + lane < n_slabs ? qc[s0 + lane] : 0;
+    bad = bad || __ballot(c > FL_CAP) != 0ull;
+    int incl = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      incl += lane >= o ? y : 0;
+    }
+    total += __shfl(incl, 63, 64);
+  }
+  if (bad || total > SW_CAP) {
+    if (lane == 0) {
+      flag_query(qid, flags, qsel, qsel_n);
+      if (mode == 0) theta_out[qid] = __builtin_huge_valf();
+    }
+    return;
+  }
+  int off = 0;
+  for (int s = 0; s < n_slabs; ++s) {
+    const int c = qc[s];
+    for (int i = lane; i < c; i += 64) kb[off + i] = ql[(int64_t)s * FL_CAP + i];
+    off += c;
+  }
+  wave_sync();
+  const int R = mode == 0 ? J : k;
+  if (total < R) {  // fewer than R candidates: a_J = -inf (sample) / cannot certify (full)
+    if (lane == 0) {
+      if (mode == 0) {
+        theta_out[qid] = -__builtin_huge_valf();
+        aref[qid] = -__builtin_huge_valf();
+      } else {
+        flag_query(qid, flags, qsel, qsel_n);
+      }
+    }
+    return;
+  }
+  constexpr int PER = SW_CAP / 64;
+  const int ni = (total + 63) / 64;
+  uint32_t hv[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int j = lane + 64 * i;
+    hv[i] = (i < ni && j < total) ? (uint32_t)(kb[j] >> 32) : 0u;  // 0 = below every key
+  }
+  uint32_t T = 0;
+  for (int bit = 31; bit >= 0; --bit) {
+    const uint32_t cand = T | (1u << bit);
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      if (i < ni) cnt += hv[i] >= cand ? 1 : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if (cnt >= R) T = cand;
+  }
+  const float A = key_float(T);
+  if (mode == 0) {
+    if (lane == 0) {
+      theta_out[qid] = A;
+      aref[qid] = A;
+    }
+    return;
+  }
+  if (!(A >= aref[qid])) {  // the optimistic threshold did not hold
+    if (lane == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
+  const float thr = A - eps2[qid];
+  int nb = 0;
+  uint64_t* qb = band + (int64_t)qid * BAND_CAP;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    if (i < ni) {
+      const int j = lane + 64 * i;
+      const bool in = j < total && key_float(hv[i]) >= thr;
+      const uint64_t bm = __ballot(in);
+      const int pos = nb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+      if (in && pos < BAND_CAP) qb[pos] = kb[j];
+      nb += __popcll(bm);
+    }
+  }
+  if (lane == 0) {
+    if (nb > BAND_CAP) flag_query(qid, flags, qsel, qsel_n);
+    else band_n[qid] = nb;
+  }
+}
+
 // --------------------------------------------------------------------------- rerank
 template <int EP>
 __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, int64_t ld,
@@ -1031,10 +1149,10 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
     if (rc) return rc;
     if (last && ev_stop && hipEventRecord((hipEvent_t)ev_stop, st) != hipSuccess)
       return fail(TT_ERR_LAUNCH, "hipEventRecord(stop)");
-    hipLaunchKernelGGL(k_select, dim3(nq), dim3(256), 0, st, w.lists, w.counts, L.n_slabs, k,
-                       p.J, w.eps2, last ? 1 : 0, w.theta, w.aref, w.band, w.band_n, w.flags,
-                       w.qsel, w.qsel_n);
-    rc = check_launch("k_select");
+    hipLaunchKernelGGL(k_select_wave, dim3((nq + 3) / 4), dim3(256), 0, st, w.lists, w.counts,
+                       L.n_slabs, k, p.J, w.eps2, last ? 1 : 0, w.theta, w.aref, w.band, w.band_n,
+                       w.flags, w.qsel, w.qsel_n, nq);
+    rc = check_launch("k_select_wave");
     if (rc) return rc;
   }
   switch (ep) {
