@@ -212,7 +212,7 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #ifndef TT_EXP_MAXONLY
 #define TT_EXP_MAXONLY 0  // per-block max + ballot only (no per-slot scan)
 #endif
-constexpr int RG_WAVES = 8, RG_PD = 3, RG_SLOTS = RG_PD + 1;
+constexpr int RG_WAVES = 8, RG_PD = 3, RG_SLOTS = RG_PD + 1;  // 3 tiles in flight
 constexpr int RG_POOL = 4096;                  // pool entries per block
 constexpr int RG_WPOOL = RG_POOL / RG_WAVES;   // ... per wave (wave-private region)
 constexpr int RG_WFLUSH = RG_WPOOL / 2;
@@ -337,23 +337,26 @@ __global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
   // pos ^ (r & FM) of that row, so row r's logical chunk c lives at position c ^ (r & FM).
   // Per lane the (row, column byte) of each piece is loop-invariant.
   const int64_t row_bytes = stride * ld * 2;
-  const char* src0[PPW];  // lane's source of piece pp in tile 0 (full tiles: + t * tile_bytes)
+  // source = wave-uniform tile base (SGPRs) + the lane's 32-bit offset within the tile
+  uint32_t voff[PPW];
 #pragma unroll
   for (int pp = 0; pp < PPW; ++pp) {
     const int P = (w + RG_WAVES * pp) * 64 + lane;
     const int r = P / CPR;
-    src0[pp] = (const char*)xb + (j0 + r) * row_bytes + 16 * ((P % CPR) ^ (r & FM));
+    voff[pp] = (uint32_t)(r * row_bytes) + 16u * (uint32_t)((P % CPR) ^ (r & FM));
   }
   const int64_t tile_bytes = row_bytes * TR;
+  const char* slab_base = (const char*)xb + j0 * row_bytes;
   auto issue = [&](int t) __attribute__((always_inline)) {
     char* slot = ring + (t % RG_SLOTS) * TILE_B;
     const int64_t jt = j0 + (int64_t)t * TR;
     const bool clamp = jt + TR > j1;  // wave-uniform: only the slab's last tile
+    const char* tb = slab_base + (int64_t)t * tile_bytes;
 #pragma unroll
     for (int pp = 0; pp < PPW; ++pp) {
       const char* src;
       if (!clamp) {
-        src = src0[pp] + (int64_t)t * tile_bytes;
+        src = tb + voff[pp];
       } else {  // recompute the lane's (row, column) of piece pp: rare path, no live registers
         const int P = (w + RG_WAVES * pp) * 64 + lane;
         const int r = P / CPR;
@@ -387,7 +390,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
   // A-fragment read offsets: row r = 16rb + col, chunk c = 4s + g = 16(u) .. with s = 4u + v,
   // so c ^ f = 4(s ^ h) + (g ^ (f & 3)) with f = r & FM, h = f >> 2  ->  the lane-dependent
   // part depends on v only; u becomes an immediate (+256u bytes).
-  int lrd[RB][4];
+  uint32_t lrd[RB][4];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
     const int r = 16 * rb + col, f = r & FM, h = f >> 2;
@@ -461,7 +464,8 @@ __global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
   // wait until only `younger` tiles issued after the awaited one are still in flight
   auto wait_tiles = [&](int younger) __attribute__((always_inline)) {
     if (TT_EXP_NODMA) return;
-    if (younger >= 2) wait_vm<2 * PPW>();
+    if (younger >= 3) wait_vm<3 * PPW>();
+    else if (younger == 2) wait_vm<2 * PPW>();
     else if (younger == 1) wait_vm<PPW>();
     else wait_vm<0>();
   };
@@ -487,71 +491,91 @@ __global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
 #pragma unroll
     for (int b = 0; b < QB; ++b) accp[rb][b] = f32x4{qnan, qnan, qnan, qnan};
 
-  // fragment address = lrd (lane part) + slot base (wave-uniform)
-  const uint32_t ring_base = lds_addr(ring);
+  // Fragment addresses: the tile loop is unrolled by RG_SLOTS so the slot of every tile is a
+  // compile-time constant: slots 0-2 address from lrd, slots 3-4 from lrd + 3 TILE_B, and the
+  // slot and k-step offsets are ds_read immediates (no address arithmetic in the loop).
+  static_assert(RG_SLOTS <= 6 && 2 * TILE_B + 256 * (KS / 4) < 65536, "ds_read offset range");
+  uint32_t lrd2[RB][4];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lrd[rb][i] += lds_addr(ring);
+      lrd2[rb][i] = lrd[rb][i] + 3 * TILE_B;
+    }
   u32x4 fr[FD + 1][RB];
-  auto read_step = [&](uint32_t slot_base, auto sc_) __attribute__((always_inline)) {
-    constexpr int S = decltype(sc_)::value;
+  auto read_step = [&](auto slot_, auto sc_) __attribute__((always_inline)) {
+    constexpr int SL = decltype(slot_)::value, S = decltype(sc_)::value;
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
-      fr[S % (FD + 1)][rb] = lds_read128<256 * (S >> 2)>(slot_base + lrd[rb][S & 3]);
+      fr[S % (FD + 1)][rb] = lds_read128<(SL % 3) * TILE_B + 256 * (S >> 2)>(
+          SL >= 3 ? lrd2[rb][S & 3] : lrd[rb][S & 3]);
   };
-  if (n_tiles > 0) static_for<FD>([&](auto s_) __attribute__((always_inline)) { read_step(ring_base, s_); });
-  for (int t = 0; t < n_tiles; ++t) {
-    const bool has_next = t + 1 < n_tiles;
-    const uint32_t sb = ring_base + (uint32_t)((t % RG_SLOTS) * TILE_B);
-    const uint32_t sbn = ring_base + (uint32_t)(((t + 1) % RG_SLOTS) * TILE_B);
-    f32x4 acc[RB][QB];
+  if (n_tiles > 0)
+    static_for<FD>([&](auto s_) __attribute__((always_inline)) {
+      read_step(std::integral_constant<int, 0>{}, s_);
+    });
+  for (int t0 = 0; t0 < n_tiles; t0 += RG_SLOTS) {
+    static_for<RG_SLOTS>([&](auto u_) __attribute__((always_inline)) {
+      constexpr int U = decltype(u_)::value;  // t % RG_SLOTS
+      const int t = t0 + U;
+      if (t < n_tiles) {
+        const bool has_next = t + 1 < n_tiles;
+        f32x4 acc[RB][QB];
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb)
+        for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-      for (int b = 0; b < QB; ++b) acc[rb][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float mx[QB];
-    static_for<KS>([&](auto s_) __attribute__((always_inline)) {
-      constexpr int s = decltype(s_)::value;
-      if constexpr (s + FD < KS) {
-        read_step(sb, std::integral_constant<int, s + FD>{});
-        lds_wait<FD * RB>();
-      } else {
-        if (has_next) {
-          read_step(sbn, std::integral_constant<int, s + FD - KS>{});
-          lds_wait<FD * RB>();
-        } else {
-          lds_wait<(KS - 1 - s) * RB>();
-        }
-      }
+          for (int b = 0; b < QB; ++b) acc[rb][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+        float mx[QB];
+        static_for<KS>([&](auto s_) __attribute__((always_inline)) {
+          constexpr int s = decltype(s_)::value;
+          if constexpr (s + FD < KS) {
+            read_step(std::integral_constant<int, U>{}, std::integral_constant<int, s + FD>{});
+            lds_wait<FD * RB>();
+          } else {
+            if (has_next) {
+              read_step(std::integral_constant<int, (U + 1) % RG_SLOTS>{},
+                        std::integral_constant<int, s + FD - KS>{});
+              lds_wait<FD * RB>();
+            } else {
+              lds_wait<(KS - 1 - s) * RB>();
+            }
+          }
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb) reg_tie(fr[s % (FD + 1)][rb]);
+          for (int rb = 0; rb < RB; ++rb) reg_tie(fr[s % (FD + 1)][rb]);
 #pragma unroll
-      for (int rb = 0; rb < RB; ++rb) {
-        const bf16x8 a = __builtin_bit_cast(bf16x8, fr[s % (FD + 1)][rb]);
+          for (int rb = 0; rb < RB; ++rb) {
+            const bf16x8 a = __builtin_bit_cast(bf16x8, fr[s % (FD + 1)][rb]);
 #pragma unroll
-        for (int b = 0; b < QB; ++b)
-          acc[rb][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[b][s], acc[rb][b], 0, 0, 0);
-      }
-      if constexpr (s == 0) tile_max(accp, mx);  // VALU between this tile's MFMAs
-      if constexpr (s == S_MID) {
-        if (has_next) {
-          if (t + 2 < n_tiles) wait_vm<PPW>();
-          else wait_vm<0>();
-        }
-        if (!TT_EXP_NOBAR) asm volatile("s_barrier" ::: "memory");
-        if (!TT_EXP_NODMA && t + RG_PD < n_tiles) issue(t + RG_PD);
-      }
-      if constexpr (s == (KS > 1 ? 1 : 0)) {  // early: tile t-1's scores die before the peak
-        if (!TT_EXP_NOSEL) append(accp, mx, t - 1);
-        if (TT_EXP_NOSEL) {
+            for (int b = 0; b < QB; ++b)
+              acc[rb][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[b][s], acc[rb][b], 0, 0, 0);
+          }
+          if constexpr (s == 0) tile_max(accp, mx);  // VALU between this tile's MFMAs
+          if constexpr (s == S_MID) {
+            if (has_next) {
+              // tiles issued after t+1 and still in flight: t+2 .. t+PD-1
+              const int younger = n_tiles - 2 - t < RG_PD - 2 ? n_tiles - 2 - t : RG_PD - 2;
+              wait_tiles(younger);
+            }
+            if (!TT_EXP_NOBAR) asm volatile("s_barrier" ::: "memory");
+            if (!TT_EXP_NODMA && t + RG_PD < n_tiles) issue(t + RG_PD);
+          }
+          if constexpr (s == (KS > 1 ? 1 : 0)) {  // early: tile t-1's scores die before the peak
+            if (!TT_EXP_NOSEL) append(accp, mx, t - 1);
+            if (TT_EXP_NOSEL) {
 #pragma unroll
-          for (int b = 0; b < QB; ++b)
-            if (mx[b] >= th[b]) asm volatile("" ::: "memory");
-        }
+              for (int b = 0; b < QB; ++b)
+                if (mx[b] >= th[b]) asm volatile("" ::: "memory");
+            }
+          }
+        });
+        if (wn >= (uint32_t)RG_WFLUSH) flush();
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+          for (int b = 0; b < QB; ++b) accp[rb][b] = acc[rb][b];
       }
     });
-    if (wn >= (uint32_t)RG_WFLUSH) flush();
-#pragma unroll
-    for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-      for (int b = 0; b < QB; ++b) accp[rb][b] = acc[rb][b];
   }
   if (n_tiles > 0 && !TT_EXP_NOSEL) {
     float mx[QB];
