@@ -248,6 +248,46 @@ int tt_infonce_f32(const float* b, int64_t ldb, const float* p, int64_t ldp, con
                    float temperature, int32_t prec, float* loss, float* grad_b, float* grad_p,
                    float* grad_n, void* workspace, int64_t workspace_bytes, void* stream);
 
+/* Round-to-nearest-even bf16 copy of an f32 matrix (GEMM operands of the bf16 paths). */
+int tt_f32_to_bf16(const float* x, int64_t ldx, int32_t rows, int32_t cols, uint16_t* y,
+                   int64_t ldy, void* stream);
+
+/* ---------------------------------------------------------------------------------
+ * Training-step pieces (tt_train.hip) for configs[4]: InfoNCE on the item-tower head and the
+ * buyer-tower attention MLP (src/training/trainer.py:74-243; text encoder frozen,
+ * item_tower.py:40-42), GEMMs via tt_gemm_*.
+ * --------------------------------------------------------------------------------- */
+/* F.normalize backward: dy = (dz - z (z.dz)) / ||y|| (||y|| > 1e-12), else dz / 1e-12. */
+int tt_l2norm_backward_f32(const float* y, int64_t ldy, const float* z, int64_t ldz,
+                           const float* dz, int64_t lddz, int64_t n, int32_t d, float* dy,
+                           int64_t lddy, void* stream);
+/* x [rows, cols] -> t [cols, ldt] (t[c][r] = x[r][c]; columns rows..ldt-1 zero). */
+int tt_transpose_f32(const float* x, int64_t ldx, int32_t rows, int32_t cols, float* t,
+                     int32_t ldt, void* stream);
+/* out[c] (+)= sum_r x[r][c]  (bias gradients). */
+int tt_col_sum_f32(const float* x, int64_t ldx, int64_t rows, int32_t cols, float* out,
+                   int32_t accumulate, void* stream);
+/* dh[i] = 0 where h[i] <= 0 (ReLU backward, in place). */
+int tt_relu_backward_f32(float* dh, const float* h, int64_t n, void* stream);
+/* BuyerTower.attention_aggregation after H = relu(x W1^T + b1) (buyer_tower.py:85-99):
+ * a = H.W2 + b2, c = a*w, alpha = softmax_S(c), o = sum alpha x, z = F.normalize(o).
+ * H [B*S, Hd], x [B, S, E], w [B, S]; saves alpha [B, S], onorm [B]. S <= 128, E <= 1024. */
+int tt_attn_pool_fwd_f32(const float* H, int32_t Hd, const float* W2, float b2, const float* w,
+                         const float* x, int64_t B, int32_t S, int32_t E, float* alpha,
+                         float* onorm, float* z, int64_t ldz, void* stream);
+/* Its backward: dW2 [Hd], db2 [1], dH [B*S, Hd] (ReLU mask not applied); da_ws [B*S] scratch. */
+int tt_attn_pool_bwd_f32(const float* dz, int64_t lddz, const float* z, int64_t ldz,
+                         const float* onorm, const float* alpha, const float* w, const float* x,
+                         int64_t B, int32_t S, int32_t E, const float* H, const float* W2,
+                         int32_t Hd, float* dW2, float* db2, float* dH, float* da_ws,
+                         void* stream);
+/* nn.Embedding(padding_idx=0) backward: table_grad[ids[r]] += g[r] (ids <= 0 skipped). */
+int tt_embedding_backward_f32(const float* g, int64_t ldg, const int32_t* ids, int64_t n,
+                              int32_t C, float* table_grad, void* stream);
+/* torch.optim.Adam step (weight_decay 0): step is the 1-based step count after increment. */
+int tt_adam_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                float beta2, float eps, int32_t step, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

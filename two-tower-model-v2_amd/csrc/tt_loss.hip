@@ -284,3 +284,15 @@ extern "C" int tt_infonce_f32(const float* b, int64_t ldb, const float* p, int64
                      grad_b, (int64_t)E, grad_p, (int64_t)E, grad_n, (int64_t)N * E, (int64_t)E);
   return check_launch("k_infonce_grads");
 }
+
+extern "C" int tt_f32_to_bf16(const float* x, int64_t ldx, int32_t rows, int32_t cols, uint16_t* y,
+                              int64_t ldy, void* stream) {
+  TT_REQUIRE(rows >= 0 && cols >= 0, "bad sizes");
+  if (rows == 0 || cols == 0) return TT_OK;
+  TT_REQUIRE(x && y, "null pointer");
+  const int64_t n = (int64_t)rows * cols;
+  const unsigned g = (unsigned)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192);
+  hipLaunchKernelGGL(k_to_bf16, dim3(g), dim3(256), 0, (hipStream_t)stream, x, ldx, rows, cols, y,
+                     ldy);
+  return check_launch("tt_f32_to_bf16");
+}

@@ -93,6 +93,19 @@ SIGNATURES = {
                                                   ctypes.POINTER(_i64)]),
     "tt_infonce_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32,
                                       ctypes.c_float, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "tt_l2norm_backward_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _vp,
+                                              _i64, _vp]),
+    "tt_transpose_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i32, _vp]),
+    "tt_col_sum_f32": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _i32, _vp]),
+    "tt_relu_backward_f32": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
+    "tt_attn_pool_fwd_f32": (ctypes.c_int, [_vp, _i32, _vp, ctypes.c_float, _vp, _vp, _i64, _i32,
+                                            _i32, _vp, _vp, _vp, _i64, _vp]),
+    "tt_attn_pool_bwd_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _i32,
+                                            _i32, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp]),
+    "tt_embedding_backward_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i32, _vp, _vp]),
+    "tt_adam_f32": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float,
+                                   ctypes.c_float, ctypes.c_float, _i32, _vp]),
+    "tt_f32_to_bf16": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp]),
     "tt_item_concat": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _i64, _vp, _i64,
                                       _vp, _vp]),
 }
