@@ -198,7 +198,7 @@ def test_item_head_vs_reference_fixture(golden, use_cat):
     y = it(texts, brands if use_cat else None, cats if use_cat else None)
     assert y.is_cuda
     tag = "cat" if use_cat else "nocat"
-    np.testing.assert_allclose(y.cpu().numpy(), g[f"{tag}__out"], rtol=0, atol=2e-6)
+    np.testing.assert_allclose(y.detach().cpu().numpy(), g[f"{tag}__out"], rtol=0, atol=2e-6)
     yb = it.encode_batch(texts, brands if use_cat else None, cats if use_cat else None, 5)
     np.testing.assert_allclose(yb, g[f"{tag}__out"], rtol=0, atol=2e-6)
 
@@ -231,7 +231,7 @@ def test_item_tower_end_to_end_vs_oracle():
     texts = ["خاتم ذهب عيار 21", "", "necklace gold 18k Damas", "   ", "زيت محرك 5W-30"]
     brands = ["Damas", None, "Acme", "Unknown", "Lazurde"]
     cats = ["rings", "necklaces", None, "bracelets", "engine-oil"]
-    y = it(texts, brands, cats).cpu()
+    y = it(texts, brands, cats).detach().cpu()
     tok = HashTokenizer(cfg["vocab"])
     seqs = tok([t if t and t.strip() else " " for t in texts])
     cu = np.concatenate([[0], np.cumsum([len(s) for s in seqs])])

@@ -133,3 +133,53 @@ def test_train_step_bf16_loss_decreases():
     step = TwoTowerTrainStep(it, bt, lr=1e-3, prec="bf16")
     losses = [step.step(items, w, pos, neg).item() for _ in range(20)]
     assert losses[-1] < losses[0] and all(np.isfinite(losses))
+
+
+def test_modules_train_under_torch_autograd():
+    """The mirrored modules are drop-ins for the reference's own training loop:
+    forward_simplified -> InfoNCELoss -> loss.backward() -> torch.optim.Adam, gradients by the
+    HIP backward kernels (autograd_ops), equal to the CPU reference's."""
+    from twotower.losses import InfoNCELoss
+    from twotower.two_tower import TwoTowerModel
+
+    B, N, S, E, tau = 6, 4, 5, 384, 0.07
+    it, bt = _setup(E, True, seed=5)
+    emb = torch.from_numpy(np.random.default_rng(2).standard_normal((16, 384)).astype(np.float32))
+
+    class Stub:
+        def get_sentence_embedding_dimension(self):
+            return 384
+
+        def encode(self, texts, **kw):
+            return emb[[int(t.split("#")[1]) for t in texts]]
+
+    rng = np.random.default_rng(6)
+    items = torch.from_numpy(rng.standard_normal((B, S, E)).astype(np.float32))
+    w = torch.from_numpy(rng.integers(1, 11, (B, S)).astype(np.float32))
+    pos_i = rng.integers(0, 16, B)
+    neg_i = rng.integers(0, 16, (B, N))
+    pb = [gi.BRANDS[i % 5] if i % 3 else None for i in range(B)]
+    nb = [[gi.BRANDS[(i + j) % 5] for j in range(N)] for i in range(B)]
+    ids = lambda names: torch.tensor([it.brand_vocab.get(x, 0) if x else 0 for x in names],  # noqa
+                                     dtype=torch.int32)
+    ref_loss, ref_g, _ = _reference_step(
+        it, bt, items, w, emb[pos_i], emb[neg_i], ids(pb), torch.zeros(B, dtype=torch.int32),
+        ids([x for l in nb for x in l]).view(B, N), torch.zeros((B, N), dtype=torch.int32),
+        tau, 1e-3)
+    it.text_encoder = Stub()
+    model = TwoTowerModel(it, bt).cuda()
+    model.item_tower.eval()
+    out = model.forward_simplified(items.cuda(), w.cuda(), [f"p#{i}" for i in pos_i],
+                                   [[f"p#{j}" for j in row] for row in neg_i], pb, None, nb, None)
+    loss = InfoNCELoss(tau)(out["buyer_embeddings"], out["positive_embeddings"],
+                            out["negative_embeddings"])
+    loss.backward()
+    assert abs(loss.item() - ref_loss) < 1e-5 * max(1, abs(ref_loss))
+    got = {"proj0.w": it.projection[0].weight.grad, "proj3.b": it.projection[3].bias.grad,
+           "att0.w": bt.attention[0].weight.grad, "att2.b": bt.attention[2].bias.grad,
+           "brand": it.brand_embedding.weight.grad, "cat": it.category_embedding.weight.grad}
+    for k, g in got.items():
+        v = ref_g[k]
+        scale = v.abs().max().item() + 1e-12
+        assert (g.cpu().reshape(v.shape) - v).abs().max().item() <= 1e-4 * scale + 1e-6, k
+    torch.optim.Adam(model.parameters(), lr=1e-3).step()  # torch's own optimizer on top

@@ -48,13 +48,16 @@ class BuyerTower(nn.Module):
     def attention_aggregation(self, item_embeddings: torch.Tensor,
                               weights: torch.Tensor) -> torch.Tensor:
         """reference :70-101 -> tt_attn_agg_l2_f32"""
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError(
-                "BuyerTower attention backward is not implemented on the HIP path yet; "
-                "call under torch.no_grad() (inference) -- training lands with the config-5 step")
         home = item_embeddings.device
         l0, l2 = self.attention[0], self.attention[2]
         dev = _lib.device()
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            from .autograd_ops import AttnAggFn  # training: HIP forward + backward
+
+            out = AttnAggFn.apply(self._on_device(item_embeddings), self._on_device(weights),
+                                  l0.weight.to(dev), l0.bias.to(dev), l2.weight.to(dev),
+                                  l2.bias.to(dev))
+            return out.to(home)
         out = kernels.attn_agg_l2(self._on_device(item_embeddings), self._on_device(weights),
                                   l0.weight.to(dev), l0.bias.to(dev), l2.weight.to(dev),
                                   l2.bias.to(dev))

@@ -305,6 +305,18 @@ class ItemTower(nn.Module):
         dev = text_emb.device
         B, Ht = text_emb.shape
         C = self.categorical_embedding_dim if use_cat else 0
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            from .autograd_ops import ItemHeadFn  # training: HIP forward + backward
+
+            l0, l3 = self.projection[0], self.projection[3]
+            ids = lambda v: (torch.tensor(v, dtype=torch.int32, device=dev)  # noqa: E731
+                             if v is not None else None)
+            bt = self.brand_embedding.weight.to(dev) if use_cat else None
+            ct = self.category_embedding.weight.to(dev) if use_cat else None
+            return ItemHeadFn.apply(text_emb, ids(brand_ids) if use_cat else None,
+                                    ids(cat_ids) if use_cat else None, bt, ct,
+                                    l0.weight.to(dev), l0.bias.to(dev), l3.weight.to(dev),
+                                    l3.bias.to(dev))
         width = Ht + 2 * C
         l0, l3 = self.projection[0], self.projection[3]
         x = torch.empty((B, width), dtype=torch.float32, device=dev)

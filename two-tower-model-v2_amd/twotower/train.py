@@ -27,6 +27,62 @@ def _p(t):
     return t.data_ptr() if t is not None else None
 
 
+class GemmOps:
+    """GEMM-shaped pieces of the backward passes on the HIP kernels (f32 or bf16 MFMA)."""
+
+    def __init__(self, prec: str = "f32", device=None):
+        if prec not in ("f32", "bf16"):
+            raise ValueError("prec must be 'f32' or 'bf16'")
+        self.prec = prec
+        self.dev = device or _lib.device()
+
+    def gemm(self, A, W, bias=None, act=0, res=None):
+        """C = act(A W^T + bias) (+ res): A [M,K], W [N,K] f32 device (K % 32 / 64 == 0)."""
+        M, K = A.shape
+        N = W.shape[0]
+        C = torch.empty((M, N), dtype=torch.float32, device=self.dev)
+        if self.prec == "bf16":
+            A16 = torch.empty((M, K), dtype=torch.bfloat16, device=self.dev)
+            W16 = torch.empty((N, K), dtype=torch.bfloat16, device=self.dev)
+            check(lib().tt_f32_to_bf16(A.data_ptr(), A.stride(0), M, K, A16.data_ptr(), K,
+                                       stream_ptr()), "bf16 A")
+            check(lib().tt_f32_to_bf16(W.data_ptr(), W.stride(0), N, K, W16.data_ptr(), K,
+                                       stream_ptr()), "bf16 W")
+            check(lib().tt_gemm_bf16(A16.data_ptr(), K, W16.data_ptr(), K, _p(bias), _p(res),
+                                     res.stride(0) if res is not None else 0, C.data_ptr(), N,
+                                     None, 0, M, N, K, act, stream_ptr()), "gemm_bf16")
+        else:
+            check(lib().tt_gemm_f32(A.data_ptr(), A.stride(0), W.data_ptr(), W.stride(0),
+                                    _p(bias), _p(res), res.stride(0) if res is not None else 0,
+                                    C.data_ptr(), N, None, 0, M, N, K, act, stream_ptr()),
+                  "gemm_f32")
+        return C
+
+    def kpad(self, k: int) -> int:
+        q = 64 if self.prec == "bf16" else 32
+        return (k + q - 1) // q * q
+
+    def T(self, x, ld=None):
+        """x [r, c] -> [c, ld] with zero columns r..ld-1 (ld = K padding of the GEMM)."""
+        r, c = x.shape
+        ld = ld or self.kpad(r)
+        t = torch.empty((c, ld), dtype=torch.float32, device=self.dev)
+        check(lib().tt_transpose_f32(x.data_ptr(), x.stride(0), r, c, t.data_ptr(), ld,
+                                     stream_ptr()), "transpose")
+        return t
+
+    def dW(self, dY, X):
+        """dY^T X : [N, M] x [M, K] -> [N, K] (dY [M, N], X [M, K])."""
+        ldk = self.kpad(dY.shape[0])
+        return self.gemm(self.T(dY, ldk), self.T(X, ldk))
+
+    def colsum(self, x):
+        out = torch.empty(x.shape[1], dtype=torch.float32, device=self.dev)
+        check(lib().tt_col_sum_f32(x.data_ptr(), x.stride(0), x.shape[0], x.shape[1],
+                                   out.data_ptr(), 0, stream_ptr()), "col_sum")
+        return out
+
+
 class TwoTowerTrainStep:
     """One optimizer step of the item head + buyer attention under InfoNCE (Adam)."""
 
@@ -39,6 +95,7 @@ class TwoTowerTrainStep:
         self.it, self.bt = item_tower, buyer_tower
         self.tau, self.lr, self.betas, self.eps, self.prec = temperature, lr, betas, eps, prec
         self.dev = _lib.device()
+        self.ops = GemmOps(prec, self.dev)
         self.it.to(self.dev)
         self.bt.to(self.dev)
         self.params = self._params()
@@ -61,52 +118,20 @@ class TwoTowerTrainStep:
                 raise ValueError("parameters must be contiguous")
         return {k: v.data for k, v in p.items()}
 
-    # ------------------------------------------------------------------ GEMM helpers
     def _gemm(self, A, W, bias=None, act=0, res=None):
-        """C = act(A W^T + bias) (+ res): A [M,K], W [N,K] f32 device, K padded by caller."""
-        M, K = A.shape
-        N = W.shape[0]
-        C = torch.empty((M, N), dtype=torch.float32, device=self.dev)
-        if self.prec == "bf16":
-            A16 = torch.empty((M, K), dtype=torch.bfloat16, device=self.dev)
-            W16 = torch.empty((N, K), dtype=torch.bfloat16, device=self.dev)
-            check(lib().tt_f32_to_bf16(A.data_ptr(), A.stride(0), M, K, A16.data_ptr(), K,
-                                       stream_ptr()), "bf16 A")
-            check(lib().tt_f32_to_bf16(W.data_ptr(), W.stride(0), N, K, W16.data_ptr(), K,
-                                       stream_ptr()), "bf16 W")
-            check(lib().tt_gemm_bf16(A16.data_ptr(), K, W16.data_ptr(), K, _p(bias), _p(res),
-                                     res.stride(0) if res is not None else 0, C.data_ptr(), N,
-                                     None, 0, M, N, K, act, stream_ptr()), "gemm_bf16")
-        else:
-            check(lib().tt_gemm_f32(A.data_ptr(), A.stride(0), W.data_ptr(), W.stride(0),
-                                    _p(bias), _p(res), res.stride(0) if res is not None else 0,
-                                    C.data_ptr(), N, None, 0, M, N, K, act, stream_ptr()),
-                  "gemm_f32")
-        return C
+        return self.ops.gemm(A, W, bias, act, res)
 
-    def _kpad(self, k: int) -> int:
-        q = 64 if self.prec == "bf16" else 32
-        return (k + q - 1) // q * q
+    def _kpad(self, k):
+        return self.ops.kpad(k)
 
     def _T(self, x, ld=None):
-        """x [r, c] -> [c, ld] with zero columns r..ld-1 (ld = K padding of the GEMM)."""
-        r, c = x.shape
-        ld = ld or self._kpad(r)
-        t = torch.empty((c, ld), dtype=torch.float32, device=self.dev)
-        check(lib().tt_transpose_f32(x.data_ptr(), x.stride(0), r, c, t.data_ptr(), ld,
-                                     stream_ptr()), "transpose")
-        return t
+        return self.ops.T(x, ld)
 
     def _dW(self, dY, X):
-        """dY^T X : [N, M] x [M, K] -> [N, K] (dY [M, N], X [M, K])."""
-        ldk = self._kpad(dY.shape[0])
-        return self._gemm(self._T(dY, ldk), self._T(X, ldk))
+        return self.ops.dW(dY, X)
 
     def _colsum(self, x):
-        out = torch.empty(x.shape[1], dtype=torch.float32, device=self.dev)
-        check(lib().tt_col_sum_f32(x.data_ptr(), x.stride(0), x.shape[0], x.shape[1],
-                                   out.data_ptr(), 0, stream_ptr()), "col_sum")
-        return out
+        return self.ops.colsum(x)
 
     # ------------------------------------------------------------------ the step
     def forward_backward(self, buyer_items, weights, pos_text, neg_text, pos_brand=None,

@@ -56,6 +56,8 @@ class FlatIPIndex:
 
     # faiss-style add of ALREADY-normalised float32 rows (host or device)
     def add(self, x) -> None:
+        if isinstance(x, np.ndarray) and not x.flags.writeable:
+            x = np.array(x)  # torch refuses read-only numpy buffers (e.g. np.load mmap)
         x = torch.as_tensor(x, dtype=torch.float32)
         if x.dim() != 2 or x.shape[1] != self.d:
             raise ValueError(f"add: expected [n, {self.d}] float32")
