@@ -222,6 +222,10 @@ int tt_layernorm_f32(const float* x, int64_t ldx, const float* gamma, const floa
 int tt_attention_varlen(const float* qkv, int64_t ld_qkv, const int32_t* cu_seqlens,
                         int32_t n_seq, int32_t max_len, int32_t H, int32_t heads, int32_t prec,
                         float* out, int64_t ld_out, uint16_t* out_bf16, void* stream);
+/* Same (bf16 operands) reading a bf16 qkv [T, 3H]; out and/or out_bf16 may be NULL. */
+int tt_attention_varlen_bf16(const uint16_t* qkv, int64_t ld_qkv, const int32_t* cu_seqlens,
+                             int32_t n_seq, int32_t max_len, int32_t H, int32_t heads,
+                             float* out, int64_t ld_out, uint16_t* out_bf16, void* stream);
 int tt_attention_varlen_f32(const float* qkv, int64_t ld_qkv, const int32_t* cu_seqlens,
                             int32_t n_seq, int32_t max_len, int32_t H, int32_t heads,
                             float* out, int64_t ld_out, uint16_t* out_bf16, void* stream);

@@ -241,3 +241,39 @@ def test_item_tower_end_to_end_vs_oracle():
     cid = [it.category_vocab.get(c, 0) if c else 0 for c in cats]
     ref = bert_ref.item_head(te, head, bid, cid)
     np.testing.assert_allclose(y.numpy(), ref.numpy(), rtol=0, atol=5e-5)
+
+
+def test_attention_bf16_input_matches_f32_input():
+    """tt_attention_varlen_bf16 (bf16 qkv) == tt_attention_varlen(prec bf16) on the rounded
+    input: the latter rounds q/k/v to bf16 itself, so the results are bit-identical."""
+    from twotower import _lib
+
+    lens = [5, 77, 128, 1]
+    H, nh, T = 384, 12, sum(lens)
+    qkv = torch.randn((T, 3 * H), device="cuda")
+    q16 = qkv.to(torch.bfloat16)
+    cu = torch.tensor(np.concatenate([[0], np.cumsum(lens)]), dtype=torch.int32, device="cuda")
+    a = torch.empty((T, H), device="cuda")
+    b16 = torch.empty((T, H), device="cuda", dtype=torch.bfloat16)
+    L = _lib.lib()
+    _lib.check(L.tt_attention_varlen(qkv.data_ptr(), 3 * H, cu.data_ptr(), 4, 128, H, nh,
+                                     _lib.TT_PREC_BF16, a.data_ptr(), H, None, _lib.stream_ptr()), "a")
+    _lib.check(L.tt_attention_varlen_bf16(q16.data_ptr(), 3 * H, cu.data_ptr(), 4, 128, H, nh,
+                                          None, H, b16.data_ptr(), _lib.stream_ptr()), "b")
+    assert torch.equal(b16, a.to(torch.bfloat16))
+
+
+def test_gemm_bf16_only_output_and_misaligned_bias():
+    g = torch.Generator(device="cuda").manual_seed(1)
+    A = torch.randn((300, 384), generator=g, device="cuda")
+    W = torch.randn((1152, 384), generator=g, device="cuda")
+    b = torch.randn(1153, generator=g, device="cuda")[1:]  # 4-B aligned only: scalar epilogue
+    C, C16 = _gemm(A, W, b, None, 1, "bf16", want16=True)
+    from twotower import _lib
+
+    only16 = torch.empty((300, 1152), device="cuda", dtype=torch.bfloat16)
+    a16, w16 = A.to(torch.bfloat16), W.to(torch.bfloat16)
+    _lib.check(_lib.lib().tt_gemm_bf16(a16.data_ptr(), 384, w16.data_ptr(), 384, b.data_ptr(), None,
+                                       0, None, 1152, only16.data_ptr(), 1152, 300, 1152, 384, 1,
+                                       _lib.stream_ptr()), "gemm")
+    assert torch.equal(only16, C16)

@@ -1,0 +1,54 @@
+"""Microbenchmark of tt_gemm_bf16 / tt_gemm_f32 at the encoder's shapes.
+
+    python tools/bench_gemm.py [--prec bf16] [--M 18340]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "two-tower-model-v2_amd"))
+
+import torch  # noqa: E402
+
+from twotower import _lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--prec", default="bf16")
+    ap.add_argument("--M", type=int, default=18340)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    L = _lib.lib()
+    dt = torch.bfloat16 if a.prec == "bf16" else torch.float32
+    fn = L.tt_gemm_bf16 if a.prec == "bf16" else L.tt_gemm_f32
+    out = {}
+    for (N, K, act, res) in [(1152, 384, 0, False), (384, 384, 0, True), (1536, 384, 1, False),
+                             (384, 1536, 0, True)]:
+        A = torch.randn(a.M, K, device="cuda").to(dt)
+        W = torch.randn(N, K, device="cuda").to(dt)
+        b = torch.randn(N, device="cuda")
+        R = torch.randn(a.M, N, device="cuda") if res else None
+        C = torch.empty(a.M, N, device="cuda")
+
+        def run():
+            _lib.check(fn(A.data_ptr(), K, W.data_ptr(), K, b.data_ptr(),
+                          R.data_ptr() if res else None, N, C.data_ptr(), N, None, 0, a.M, N, K,
+                          act, _lib.stream_ptr()), "gemm")
+        for _ in range(3):
+            run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / a.iters
+        out[f"N{N}_K{K}"] = {"us": round(ms * 1e3, 1), "tflops": round(2 * a.M * N * K / ms / 1e9, 1)}
+    print(json.dumps({"prec": a.prec, "M": a.M, **out}))
+
+
+if __name__ == "__main__":
+    main()

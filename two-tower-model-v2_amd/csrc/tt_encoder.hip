@@ -176,25 +176,59 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_
     enc_lds_barrier();
   }
 
-  // epilogue: lane holds C[16 i + 4 g + v][16 j + rl]
+  // Epilogue staged through LDS (the stages are free after the last barrier): each wave
+  // parks its raw 64x64 accumulator tile (row stride 68 floats: conflict-free writes), then
+  // reads it back row-contiguous so bias, residual and the stores are coalesced 16-B (f32) /
+  // 8-B (bf16) accesses.  C or C16 may be NULL (write only the copy the consumer needs).
+  float* tile = (float*)(smem + w * (32 * 68 * 4));  // two halves of 32 rows per wave
+  static_assert(4 * 32 * 68 * 4 <= 2 * GM_STAGE_B, "epilogue tile fits the stage buffers");
+  const bool vec = (N % 4) == 0 && (ldc % 4) == 0 && (!res || (ldr % 4) == 0) &&
+                   (!C16 || (ldc16 % 4) == 0) && ((uintptr_t)bias % 16) == 0 &&
+                   ((uintptr_t)res % 16) == 0 && ((uintptr_t)C % 16) == 0 &&
+                   ((uintptr_t)C16 % 8) == 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + 64 * wn + 16 * j + rl;
-    if (n >= N) continue;
-    const float bn = bias ? bias[n] : 0.0f;
+  for (int half = 0; half < 2; ++half) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int m = m0 + 64 * wm + 16 * i + 4 * g + v;
-        if (m >= M) continue;
-        float y = acc[i][j][v] + bn;
-        if (act == ACT_GELU) y = gelu_erf(y);
-        else if (act == ACT_RELU) y = y > 0.0f ? y : 0.0f;
-        if (res) y = y + res[(int64_t)m * ldr + n];
-        C[(int64_t)m * ldc + n] = y;
-        if (C16) C16[(int64_t)m * ldc16 + n] = f32_to_bf16_rne(y);
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          tile[(16 * ii + 4 * g + v) * 68 + 16 * j + rl] = acc[2 * half + ii][j][v];
+    wave_sync();
+#pragma unroll 4
+    for (int it = 0; it < 8; ++it) {
+      const int idx = it * 64 + lane, row = idx >> 4, c4 = idx & 15;
+      const int m = m0 + 64 * wm + 32 * half + row, n = n0 + 64 * wn + 4 * c4;
+      if (m >= M || n >= N) continue;
+      const f32x4 a4 = *(const f32x4*)(tile + row * 68 + 4 * c4);
+      if (vec) {
+        f32x4 y = a4;
+        if (bias) y = y + *(const f32x4*)(bias + n);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (act == ACT_GELU) y[u] = gelu_erf(y[u]);
+          else if (act == ACT_RELU) y[u] = y[u] > 0.0f ? y[u] : 0.0f;
+        }
+        if (res) y = y + *(const f32x4*)(res + (int64_t)m * ldr + n);
+        if (C) *(f32x4*)(C + (int64_t)m * ldc + n) = y;
+        if (C16) {
+          const uint2 pk = {(uint32_t)f32_to_bf16_rne(y[0]) | ((uint32_t)f32_to_bf16_rne(y[1]) << 16),
+                            (uint32_t)f32_to_bf16_rne(y[2]) | ((uint32_t)f32_to_bf16_rne(y[3]) << 16)};
+          *(uint2*)(C16 + (int64_t)m * ldc16 + n) = pk;
+        }
+      } else {
+        for (int u = 0; u < 4 && n + u < N; ++u) {
+          float y = a4[u] + (bias ? bias[n + u] : 0.0f);
+          if (act == ACT_GELU) y = gelu_erf(y);
+          else if (act == ACT_RELU) y = y > 0.0f ? y : 0.0f;
+          if (res) y = y + res[(int64_t)m * ldr + n + u];
+          if (C) C[(int64_t)m * ldc + n + u] = y;
+          if (C16) C16[(int64_t)m * ldc16 + n + u] = f32_to_bf16_rne(y);
+        }
       }
+    }
+    wave_sync();
   }
 }
 
@@ -363,8 +397,8 @@ __global__ __launch_bounds__(128) void k_attn(const float* __restrict__ qkv, int
 //   BF = false: v_mfma_f32_16x16x4_f32 (everything f32: the parity path).
 // LDS: K [Lk][32] (rows padded to 144 B f32 / 80 B bf16) and V^T [32][vst] (vst = 128k + 4 f32
 // / 128k + 8 bf16 elements): both fragment reads are bank-conflict-free.
-template <bool BF>
-__global__ __launch_bounds__(256) void k_attn32_mfma(const float* __restrict__ qkv, int64_t ldq,
+template <bool BF, typename TI>
+__global__ __launch_bounds__(256) void k_attn32_mfma(const TI* __restrict__ qkv, int64_t ldq,
                                                      const int32_t* __restrict__ cu, int H,
                                                      int heads, float scale,
                                                      float* __restrict__ out, int64_t ldo,
@@ -384,8 +418,18 @@ __global__ __launch_bounds__(256) void k_attn32_mfma(const float* __restrict__ q
   for (int e = tid; e < Lk * DH; e += 256) {
     const int j = e / DH, c = e % DH;
     float kv = 0.0f, vv = 0.0f;
-    if (j < L) {
-      const float* row = qkv + (int64_t)(t0 + j) * ldq + h * DH + c;
+    if constexpr (sizeof(TI) == 2) {  // bf16 input (BF only): copy the bits
+      uint16_t kb = 0, vb = 0;
+      if (j < L) {
+        const TI* row = qkv + (int64_t)(t0 + j) * ldq + h * DH + c;
+        kb = row[H];
+        vb = row[2 * H];
+      }
+      *(uint16_t*)(Ks + j * KROW + c * 2) = kb;
+      *(uint16_t*)(Vt + ((size_t)c * vst + j) * 2) = vb;
+      continue;
+    } else if (j < L) {
+      const TI* row = qkv + (int64_t)(t0 + j) * ldq + h * DH + c;
       kv = row[H];
       vv = row[2 * H];
     }
@@ -400,10 +444,15 @@ __global__ __launch_bounds__(256) void k_attn32_mfma(const float* __restrict__ q
   __syncthreads();
   for (int q0 = 16 * w; q0 < L; q0 += 64) {
     const int qr = q0 + ql < L ? q0 + ql : L - 1;
-    const float* qp = qkv + (int64_t)(t0 + qr) * ldq + h * DH;
-    f32x4 qa = *(const f32x4*)(qp + 4 * g), qb = *(const f32x4*)(qp + 16 + 4 * g);
+    const TI* qp = qkv + (int64_t)(t0 + qr) * ldq + h * DH;
+    f32x4 qa = {0.f, 0.f, 0.f, 0.f}, qb = {0.f, 0.f, 0.f, 0.f};
     bf16x8e qf;
-    if (BF) {  // slots 8g + j <-> dims 8g + j
+    if constexpr (sizeof(TI) == 2) {  // slots 8g + j <-> dims 8g + j, bits copied
+      qf = __builtin_bit_cast(bf16x8e, *(const u32x4*)(qp + 8 * g));
+    } else if (!BF) {
+      qa = *(const f32x4*)(qp + 4 * g);
+      qb = *(const f32x4*)(qp + 16 + 4 * g);
+    } else {  // slots 8g + j <-> dims 8g + j
       const f32x4 x0 = *(const f32x4*)(qp + 8 * g), x1 = *(const f32x4*)(qp + 8 * g + 4);
       u32x4 u = {(uint32_t)f32_to_bf16_rne(x0[0]) | ((uint32_t)f32_to_bf16_rne(x0[1]) << 16),
                  (uint32_t)f32_to_bf16_rne(x0[2]) | ((uint32_t)f32_to_bf16_rne(x0[3]) << 16),
@@ -486,11 +535,10 @@ __global__ __launch_bounds__(256) void k_attn32_mfma(const float* __restrict__ q
     // acc[db][v] = O^T[dim 16 db + 4 g + v][query q0 + ql]
     if (q0 + ql < L) {
       const float inv = 1.0f / lsum;
-      float* orow = out + (int64_t)(t0 + q0 + ql) * ldo + h * DH;
 #pragma unroll
       for (int db = 0; db < 2; ++db) {
         const f32x4 o = acc[db] * inv;
-        *(f32x4*)(orow + 16 * db + 4 * g) = o;
+        if (out) *(f32x4*)(out + (int64_t)(t0 + q0 + ql) * ldo + h * DH + 16 * db + 4 * g) = o;
         if (out16) {
           uint16_t* o16 = out16 + (int64_t)(t0 + q0 + ql) * ldo + h * DH + 16 * db + 4 * g;
 #pragma unroll
@@ -555,7 +603,7 @@ extern "C" int tt_gemm_f32(const float* A, int64_t lda, const float* W, int64_t 
   if (M == 0 || N == 0) return TT_OK;
   if (K % GemmElt<float>::BK != 0)
     return fail(TT_ERR_UNSUPPORTED, "tt_gemm_f32: need K % 32 == 0");
-  TT_REQUIRE(A && W && C, "null pointer");
+  TT_REQUIRE(A && W && (C || C_bf16), "null pointer");
   TT_REQUIRE(lda % 4 == 0 && ldw % 4 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0,
              "A/W must be 16-B aligned with lda, ldw % 4 == 0");
   TT_REQUIRE(act >= 0 && act <= 2, "bad activation");
@@ -573,7 +621,7 @@ extern "C" int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, i
   if (M == 0 || N == 0) return TT_OK;
   if (K % GemmElt<uint16_t>::BK != 0)
     return fail(TT_ERR_UNSUPPORTED, "tt_gemm_bf16: need K % 64 == 0");
-  TT_REQUIRE(A && W && C, "null pointer");
+  TT_REQUIRE(A && W && (C || C_bf16), "null pointer");
   TT_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0,
              "A/W must be 16-B aligned with lda, ldw % 8 == 0");
   TT_REQUIRE(act >= 0 && act <= 2, "bad activation");
@@ -611,19 +659,42 @@ extern "C" int tt_attention_varlen(const float* qkv, int64_t ld_qkv, const int32
     return fail(TT_ERR_UNSUPPORTED, "tt_attention_varlen: MFMA path needs head dim 32");
   const bool bf = prec == TT_PREC_BF16;
   const size_t smem = attn32_smem(max_len, bf);
-  const void* fn = bf ? (const void*)k_attn32_mfma<true> : (const void*)k_attn32_mfma<false>;
+  const void* fn = bf ? (const void*)k_attn32_mfma<true, float> : (const void*)k_attn32_mfma<false, float>;
   if (smem > 64 * 1024 &&
       hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "hipFuncSetAttribute(max dynamic LDS)");
   const float scale = 1.0f / sqrtf(32.0f);
   const dim3 grid((unsigned)(n_seq * heads));
   if (bf)
-    hipLaunchKernelGGL(k_attn32_mfma<true>, grid, dim3(256), smem, (hipStream_t)stream, qkv,
+    hipLaunchKernelGGL((k_attn32_mfma<true, float>), grid, dim3(256), smem, (hipStream_t)stream, qkv,
                        ld_qkv, cu_seqlens, H, heads, scale, out, ld_out, out_bf16);
   else
-    hipLaunchKernelGGL(k_attn32_mfma<false>, grid, dim3(256), smem, (hipStream_t)stream, qkv,
+    hipLaunchKernelGGL((k_attn32_mfma<false, float>), grid, dim3(256), smem, (hipStream_t)stream, qkv,
                        ld_qkv, cu_seqlens, H, heads, scale, out, ld_out, out_bf16);
   return check_launch("tt_attention_varlen");
+}
+
+extern "C" int tt_attention_varlen_bf16(const uint16_t* qkv, int64_t ld_qkv,
+                                        const int32_t* cu_seqlens, int32_t n_seq,
+                                        int32_t max_len, int32_t H, int32_t heads, float* out,
+                                        int64_t ld_out, uint16_t* out_bf16, void* stream) {
+  TT_REQUIRE(n_seq >= 0 && heads >= 1 && H % heads == 0, "bad n_seq / heads");
+  if (n_seq == 0) return TT_OK;
+  TT_REQUIRE(max_len >= 1 && max_len <= 512, "max_len must be in [1, 512]");
+  TT_REQUIRE(qkv && cu_seqlens && (out || out_bf16), "null pointer");
+  TT_REQUIRE(ld_qkv % 8 == 0 && ld_out % 4 == 0 && H % 8 == 0 && ((uintptr_t)qkv % 16) == 0,
+             "qkv must be 16-B aligned rows");
+  if (H / heads != 32)
+    return fail(TT_ERR_UNSUPPORTED, "tt_attention_varlen_bf16: head dim must be 32");
+  const size_t smem = attn32_smem(max_len, true);
+  const void* fn = (const void*)k_attn32_mfma<true, uint16_t>;
+  if (smem > 64 * 1024 &&
+      hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess)
+    return fail(TT_ERR_LAUNCH, "hipFuncSetAttribute(max dynamic LDS)");
+  hipLaunchKernelGGL((k_attn32_mfma<true, uint16_t>), dim3((unsigned)(n_seq * heads)), dim3(256),
+                     smem, (hipStream_t)stream, qkv, ld_qkv, cu_seqlens, H, heads,
+                     1.0f / sqrtf(32.0f), out, ld_out, out_bf16);
+  return check_launch("tt_attention_varlen_bf16");
 }
 
 extern "C" int tt_attention_varlen_f32(const float* qkv, int64_t ld_qkv, const int32_t* cu_seqlens,
@@ -664,7 +735,7 @@ namespace {
 size_t align_up(size_t b) { return (b + 255) / 256 * 256; }
 struct EncWs {
   float *x, *qkv, *ctx, *y, *ff;
-  uint16_t *x16, *ctx16, *ff16;
+  uint16_t *x16, *ctx16, *ff16, *qkv16;
   size_t total;
 };
 EncWs enc_carve(char* base, int64_t T, int H, int I, bool bf16) {
@@ -675,15 +746,19 @@ EncWs enc_carve(char* base, int64_t T, int H, int I, bool bf16) {
     off += align_up(bytes);
     return p;
   };
+  // f32 path: x, qkv, ctx, y, ff (f32).  bf16 path: x, y (f32 residual stream / LayerNorm)
+  // and bf16 copies only where the consumer is a bf16 GEMM or the bf16 attention.
   w.x = (float*)take((size_t)T * H * 4);
-  w.qkv = (float*)take((size_t)T * 3 * H * 4);
-  w.ctx = (float*)take((size_t)T * H * 4);
   w.y = (float*)take((size_t)T * H * 4);
-  w.ff = (float*)take((size_t)T * I * 4);
   if (bf16) {
     w.x16 = (uint16_t*)take((size_t)T * H * 2);
+    w.qkv16 = (uint16_t*)take((size_t)T * 3 * H * 2);
     w.ctx16 = (uint16_t*)take((size_t)T * H * 2);
     w.ff16 = (uint16_t*)take((size_t)T * I * 2);
+  } else {
+    w.qkv = (float*)take((size_t)T * 3 * H * 4);
+    w.ctx = (float*)take((size_t)T * H * 4);
+    w.ff = (float*)take((size_t)T * I * 4);
   }
   w.total = off;
   return w;
@@ -725,17 +800,22 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
     const tt_bert_layer& L = m->layer[l];
     int rc;
     // Q|K|V = x Wqkv^T + b
-    rc = bf ? tt_gemm_bf16(w.x16, H, L.wqkv_bf16, H, L.bqkv, nullptr, 0, w.qkv, 3 * H, nullptr, 0,
-                           (int)T, 3 * H, H, ACT_NONE, stream)
+    rc = bf ? tt_gemm_bf16(w.x16, H, L.wqkv_bf16, H, L.bqkv, nullptr, 0, nullptr, 3 * H, w.qkv16,
+                           3 * H, (int)T, 3 * H, H, ACT_NONE, stream)
             : tt_gemm_f32(w.x, H, L.wqkv, H, L.bqkv, nullptr, 0, w.qkv, 3 * H, nullptr, 0, (int)T,
                           3 * H, H, ACT_NONE, stream);
     if (rc) return rc;
-    if (H / m->heads == 32)
+    if (bf && H / m->heads == 32)
+      rc = tt_attention_varlen_bf16(w.qkv16, 3 * H, cu_seqlens, n_seq, max_len, H, m->heads,
+                                    nullptr, H, w.ctx16, stream);
+    else if (bf)
+      return fail(TT_ERR_UNSUPPORTED, "tt_bert_encode: bf16 path needs head dim 32");
+    else if (H / m->heads == 32)
       rc = tt_attention_varlen(w.qkv, 3 * H, cu_seqlens, n_seq, max_len, H, m->heads, prec, w.ctx,
-                               H, bf ? w.ctx16 : nullptr, stream);
+                               H, nullptr, stream);
     else
       rc = tt_attention_varlen_f32(w.qkv, 3 * H, cu_seqlens, n_seq, max_len, H, m->heads, w.ctx,
-                                   H, bf ? w.ctx16 : nullptr, stream);
+                                   H, nullptr, stream);
     if (rc) return rc;
     // y = ctx Wo^T + bo + x ; x = LN(y)
     rc = bf ? tt_gemm_bf16(w.ctx16, H, L.wo_bf16, H, L.bo, w.x, H, w.y, H, nullptr, 0, (int)T, H, H,
@@ -747,8 +827,8 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
                           H, stream);
     if (rc) return rc;
     // ff = GELU(x W1^T + b1) ; y = ff W2^T + b2 + x ; x = LN(y)
-    rc = bf ? tt_gemm_bf16(w.x16, H, L.w1_bf16, H, L.b1, nullptr, 0, w.ff, I, w.ff16, I, (int)T, I,
-                           H, ACT_GELU, stream)
+    rc = bf ? tt_gemm_bf16(w.x16, H, L.w1_bf16, H, L.b1, nullptr, 0, nullptr, I, w.ff16, I, (int)T,
+                           I, H, ACT_GELU, stream)
             : tt_gemm_f32(w.x, H, L.w1, H, L.b1, nullptr, 0, w.ff, I, nullptr, 0, (int)T, I, H,
                           ACT_GELU, stream);
     if (rc) return rc;

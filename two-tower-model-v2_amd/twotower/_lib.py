@@ -87,6 +87,8 @@ SIGNATURES = {
                                         _i64, _i32, _vp]),
     "tt_attention_varlen": (ctypes.c_int, [_vp, _i64, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i64,
                                            _vp, _vp]),
+    "tt_attention_varlen_bf16": (ctypes.c_int, [_vp, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _i64,
+                                                _vp, _vp]),
     "tt_attention_varlen_f32": (ctypes.c_int, [_vp, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _i64,
                                                _vp, _vp]),
     "tt_infonce_workspace_bytes": (ctypes.c_int, [_i32, _i32, _i32, _i32, _i32,
