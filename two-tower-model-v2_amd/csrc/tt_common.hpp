@@ -197,4 +197,24 @@ __device__ __forceinline__ uint16_t f32_to_bf16_rne(float f) {
   return (uint16_t)(u >> 16);
 }
 
+
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+// Hand-issued LDS reads with counted waits (the compiler drains lgkmcnt(0) before every use
+// of its own reads).  lds_wait<N> waits until at most N LDS operations are outstanding;
+// reg_tie pins a consumer below the wait that made its register valid.
+template <int OFF>
+__device__ __forceinline__ u32x4_t lds_read128(uint32_t addr) {
+  u32x4_t r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+  return r;
+}
+template <int N>
+__device__ __forceinline__ void lds_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N));
+}
+__device__ __forceinline__ void reg_tie(u32x4_t& r) { asm volatile("" : "+v"(r)); }
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
 }  // namespace tt

@@ -148,27 +148,37 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_
       enc_wait_vm<0>();
     }
     enc_lds_barrier();
-    const char* st = smem + (kt & 1) * GM_STAGE_B;
+    // all 16 fragment reads of the stage issued up front; counted waits per read step
+    const uint32_t sb = lds_addr(smem) + (uint32_t)((kt & 1) * GM_STAGE_B);
+    u32x4 av[2][4], bv[2][4];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      u32x4 av[4], bv[4];
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        av[i] = *(const u32x4*)(st + fa[i][s]);
-        bv[i] = *(const u32x4*)(st + fb[i][s]);
+        av[s][i] = lds_read128<0>(sb + fa[i][s]);
+        bv[s][i] = lds_read128<0>(sb + fb[i][s]);
+      }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (s == 0) lds_wait<8>();
+      else lds_wait<0>();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        reg_tie(av[s][i]);
+        reg_tie(bv[s][i]);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if constexpr (sizeof(T) == 4) {
-            const f32x4 a = __builtin_bit_cast(f32x4, av[i]), b = __builtin_bit_cast(f32x4, bv[j]);
+            const f32x4 a = __builtin_bit_cast(f32x4, av[s][i]), b = __builtin_bit_cast(f32x4, bv[s][j]);
 #pragma unroll
             for (int u = 0; u < 4; ++u)
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u], acc[i][j], 0, 0, 0);
           } else {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                __builtin_bit_cast(bf16x8e, av[i]), __builtin_bit_cast(bf16x8e, bv[j]),
+                __builtin_bit_cast(bf16x8e, av[s][i]), __builtin_bit_cast(bf16x8e, bv[s][j]),
                 acc[i][j], 0, 0, 0);
           }
         }

@@ -228,9 +228,6 @@ constexpr int ring_smem() {
 // LDS ops of the ring kernel's append path, in inline asm: the compiler cannot prove they do
 // not alias the in-flight global_load_lds and would otherwise precede each with vmcnt(0),
 // draining the ring whenever a candidate is found.
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
 __device__ __forceinline__ uint32_t lds_add_rtn(uint32_t addr, uint32_t v) {
   uint32_t r;
   asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
@@ -262,17 +259,7 @@ __device__ __forceinline__ void static_for(F&& f) {
     static_for<N, F, I + 1>(static_cast<F&&>(f));
   }
 }
-template <int OFF>
-__device__ __forceinline__ u32x4 lds_read128(uint32_t addr) {
-  u32x4 r;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
-  return r;
-}
-template <int N>
-__device__ __forceinline__ void lds_wait() {
-  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N));
-}
-__device__ __forceinline__ void reg_tie(u32x4& r) { asm volatile("" : "+v"(r)); }
+
 
 __device__ __forceinline__ void lds_barrier() {
   // LDS traffic retired + workgroup barrier, WITHOUT the vmcnt(0) that __syncthreads() adds
