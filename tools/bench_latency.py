@@ -1,0 +1,61 @@
+"""Search latency vs batch size (the /retrieve path calls with one buyer at a time).
+
+    python tools/bench_latency.py [--catalog 1000000]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "two-tower-model-v2_amd"))
+
+import torch  # noqa: E402
+
+from twotower import _lib, kernels  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--catalog", type=int, default=1_000_000)
+    ap.add_argument("--dim", type=int, default=384)
+    ap.add_argument("--k", type=int, default=100)
+    a = ap.parse_args()
+    N, E, K = a.catalog, a.dim, a.k
+    ep = _lib.padded_dim(E)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    db = torch.zeros((N, ep), device="cuda")
+    db[:, :E] = torch.randn((N, E), generator=g, device="cuda")
+    db16 = torch.empty((N, ep), device="cuda", dtype=torch.bfloat16)
+    kernels.l2norm_rows(db, E, 0, out=db, out_bf16=db16)
+    bounds = kernels.bf16_image_bounds(db, db16, E).tolist()
+    res = {}
+    for nq in (1, 8, 32, 128, 1024):
+        q = torch.zeros((nq, ep), device="cuda")
+        q[:, :E] = torch.randn((nq, E), generator=g, device="cuda")
+        kernels.l2norm_rows(q, E, 0, out=q)
+        row = {}
+        for method in ("f32", "bf16"):
+            if method == "bf16":
+                ws = torch.empty(kernels.filter_workspace_bytes(N, E, nq, K), dtype=torch.uint8,
+                                 device="cuda")
+                fn = lambda: kernels.scan_topk_bf16(db, db16, N, E, q, K, bounds, workspace=ws)  # noqa
+            else:
+                ws = torch.empty(kernels.scan_workspace_bytes(N, E, nq, K), dtype=torch.uint8,
+                                 device="cuda")
+                fn = lambda: kernels.scan_topk(db, N, E, q, K, workspace=ws)  # noqa
+            for _ in range(3):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            row[method] = round(e0.elapsed_time(e1) / 10, 3)
+        res[nq] = row
+    print(json.dumps({"catalog": N, "dim": E, "k": K, "ms_per_search": res}))
+
+
+if __name__ == "__main__":
+    main()
