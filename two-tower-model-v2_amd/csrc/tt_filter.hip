@@ -192,7 +192,10 @@ template <int EP> struct RingCfg;
 template <> struct RingCfg<64> { static constexpr int TR = 64, QB = 2; };
 template <> struct RingCfg<128> { static constexpr int TR = 32, QB = 2; };
 template <> struct RingCfg<256> { static constexpr int TR = 32, QB = 2; };
-template <> struct RingCfg<384> { static constexpr int TR = 32, QB = 2; };
+#ifndef TT_RING_HALF
+#define TT_RING_HALF 0  // 4-wave blocks, 2 per CU (independent lockstep groups per CU)
+#endif
+template <> struct RingCfg<384> { static constexpr int TR = TT_RING_HALF ? 16 : 32, QB = 2; };
 template <> struct RingCfg<512> { static constexpr int TR = 16, QB = 1; };
 template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 
@@ -212,8 +215,9 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #ifndef TT_EXP_MAXONLY
 #define TT_EXP_MAXONLY 0  // per-block max + ballot only (no per-slot scan)
 #endif
-constexpr int RG_WAVES = 8, RG_PD = 3, RG_SLOTS = RG_PD + 1;  // 3 tiles in flight
-constexpr int RG_POOL = 4096;                  // pool entries per block
+constexpr int RG_WAVES = TT_RING_HALF ? 4 : 8, RG_PD = 3, RG_SLOTS = RG_PD + 1;  // 3 in flight
+constexpr int RG_POOL = 512 * RG_WAVES;        // pool entries per block
+constexpr int RG_BLOCKS_PER_CU = TT_RING_HALF ? 2 : 1;
 constexpr int RG_WPOOL = RG_POOL / RG_WAVES;   // ... per wave (wave-private region)
 constexpr int RG_WFLUSH = RG_WPOOL / 2;
 constexpr uint32_t RG_OVF = 1u << 30;  // marks a (query, slab) list whose entries were dropped
@@ -270,7 +274,7 @@ __device__ __forceinline__ void lds_barrier() {
 // FULL: the full-catalog (last) level -- a separate instantiation of the same code so that
 // profiles attribute the dominant launch on its own (bench.py's roofline kernel).
 template <int EP, bool FULL>
-__global__ __launch_bounds__(64 * RG_WAVES, 1) void k_filter_ring(
+__global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring(
     const uint16_t* __restrict__ xb, int64_t ld, const float* __restrict__ q, int nq,
     int64_t ldq, const float* __restrict__ theta, int64_t stride, int64_t n_sample,
     int rows_per_slab, int n_slabs, int n_qt, uint64_t* __restrict__ lists,
@@ -941,7 +945,7 @@ static int device_cus() {
 // rounds * (rows per slab + per-slab overhead ~ 3 tiles), slabs <= 64 (list memory and
 // k_select work grow with the slab count), slabs >= 1 tile-row chunk of 256 rows.
 static int64_t ring_slabs(int n_qt, int64_t n_sample) {
-  const int ncu = device_cus();
+  const int ncu = device_cus() * RG_BLOCKS_PER_CU;  // concurrent blocks
   int64_t sl_max = n_sample / 256;
   if (sl_max > 64) sl_max = 64;
   if (sl_max < 1) sl_max = 1;
