@@ -119,6 +119,36 @@ int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n, in
                          void* workspace, int64_t workspace_bytes, void* stream,
                          void* ev_start, void* ev_stop);
 
+/* ---------------------------------------------------------------------------------
+ * Row-sharded (multi-GPU) form of tt_scan_topk_bf16f32: three stages with two tiny
+ * collectives in between.  Each rank calls, on its shard (same nq
+ * queries on every rank, row_base = first global row of the shard):
+ *   1. tt_sharded_filter_begin   sample levels; theta[nq] f32 at workspace + *theta_offset
+ *      -> caller: all-reduce MAX over ranks (in place)
+ *   2. tt_sharded_filter_full    full level with theta_q = max_s a_J - 2 eps_q (the union's
+ *      sample statistic: each shard keeps only rows that can be in the GLOBAL top-k);
+ *      gcount[nq] int32 at workspace + *count_offset = #candidates >= max_s a_J
+ *      -> caller: all-reduce SUM over ranks (in place)
+ *   3. tt_sharded_filter_finish  queries with sum < k fall back to the exact scan on every
+ *      rank; the rest re-rank their shard's candidates exactly; out = this shard's part of
+ *      the global top-k (padded with (-inf, -1)), to be merged with tt_topk_merge_f32.
+ * Each shard re-ranks only rows that can be in the global top-k, so the exact work summed
+ * over ranks stays that of one search over the whole catalog.  Same workspace size as
+ * tt_filter_workspace_bytes(n_shard, d, nq, k).
+ * --------------------------------------------------------------------------------- */
+int tt_sharded_filter_begin(const uint16_t* db_bf16, int64_t n, int32_t d, int64_t ld_db,
+                            const float* q, int32_t nq, int64_t ld_q, int32_t k,
+                            float x_norm_max, float x_resid_max, void* workspace,
+                            int64_t workspace_bytes, void* stream, int64_t* theta_offset);
+int tt_sharded_filter_full(const uint16_t* db_bf16, int64_t n, int32_t d, int64_t ld_db,
+                           const float* q, int32_t nq, int64_t ld_q, int32_t k, void* workspace,
+                           int64_t workspace_bytes, void* stream, void* ev_start, void* ev_stop,
+                           int64_t* count_offset);
+int tt_sharded_filter_finish(const float* db, const uint16_t* db_bf16, int64_t n, int32_t d,
+                             int64_t ld_db, int64_t row_base, const float* q, int32_t nq,
+                             int64_t ld_q, int32_t k, float* out_score, int64_t* out_idx,
+                             void* workspace, int64_t workspace_bytes, void* stream);
+
 /* Bounds of a catalog shard and its bf16 image for tt_scan_topk_bf16f32: max-combines
  * (atomically, so successive add() batches accumulate; the caller zero-fills out2 once)
  * out2[0] >= max_r ||x_r|| and out2[1] >= max_r ||x_r - x_bf16_r||  (out2: 2 device floats).

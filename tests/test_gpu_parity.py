@@ -372,3 +372,64 @@ def test_scan_full_size_properties(K, oracle_mod):
     missing = (full > kth[:, None] + 1e-6)
     missing.scatter_(1, i[:8], False)
     assert not missing.any()
+
+
+@pytest.mark.parametrize("W,n,nq,k", [(2, 300000, 64, 100), (8, 1000000, 40, 100),
+                                      (3, 5000, 17, 64), (4, 2000, 9, 10)])
+def test_sharded_filter_protocol_bit_exact(K, oracle_mod, W, n, nq, k):
+    """tt_sharded_filter_* on W row shards of one catalog (the collectives done by hand on
+    one GPU) + merge == the single-catalog exact top-k, bit for bit."""
+    from twotower.sharded import shard_range
+
+    rng = np.random.default_rng(W * 1000 + nq)
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, 384)).astype(np.float32), 0)
+    x[n // 2: n // 2 + 50] = x[:50]  # duplicates across shards
+    q = oracle_mod.l2norm_rows(rng.standard_normal((nq, 384)).astype(np.float32), 0)
+    qd = dev_rows(q)
+    shards = []
+    for r in range(W):
+        lo, hi = shard_range(n, r, W)
+        db = dev_rows(x[lo:hi])
+        db16 = db.to(torch.bfloat16)
+        shards.append((lo, hi, db, db16, bounds(K, db, db16, 384)))
+    # run the three stages on every shard, reducing between them like the collectives would
+    import ctypes
+    from twotower import _lib
+
+    L, st = _lib.lib(), _lib.stream_ptr()
+    wss, offs = [], []
+    for lo, hi, db, db16, bd in shards:
+        ws = torch.empty(K.filter_workspace_bytes(hi - lo, 384, nq, k), dtype=torch.uint8,
+                         device="cuda")
+        off = ctypes.c_int64(0)
+        _lib.check(L.tt_sharded_filter_begin(db16.data_ptr(), hi - lo, 384, db16.stride(0),
+                                             qd.data_ptr(), nq, qd.stride(0), k,
+                                             ctypes.c_float(bd[0]), ctypes.c_float(bd[1]),
+                                             ws.data_ptr(), ws.numel(), st, ctypes.byref(off)), "b")
+        wss.append(ws)
+        offs.append(off.value)
+    th = torch.stack([ws[o:o + 4 * nq].view(torch.float32) for ws, o in zip(wss, offs)]).amax(0)
+    for ws, o in zip(wss, offs):
+        ws[o:o + 4 * nq].view(torch.float32).copy_(th)
+    coffs = []
+    for (lo, hi, db, db16, bd), ws in zip(shards, wss):
+        off = ctypes.c_int64(0)
+        _lib.check(L.tt_sharded_filter_full(db16.data_ptr(), hi - lo, 384, db16.stride(0),
+                                            qd.data_ptr(), nq, qd.stride(0), k, ws.data_ptr(),
+                                            ws.numel(), st, None, None, ctypes.byref(off)), "f")
+        coffs.append(off.value)
+    cnt = torch.stack([ws[o:o + 4 * nq].view(torch.int32) for ws, o in zip(wss, coffs)]).sum(0)
+    outs_s, outs_i = [], []
+    for (lo, hi, db, db16, bd), ws, o in zip(shards, wss, coffs):
+        ws[o:o + 4 * nq].view(torch.int32).copy_(cnt.to(torch.int32))
+        s = torch.empty((nq, k), device="cuda")
+        i = torch.empty((nq, k), device="cuda", dtype=torch.int64)
+        _lib.check(L.tt_sharded_filter_finish(db.data_ptr(), db16.data_ptr(), hi - lo, 384,
+                                              db.stride(0), lo, qd.data_ptr(), nq, qd.stride(0), k,
+                                              s.data_ptr(), i.data_ptr(), ws.data_ptr(), ws.numel(),
+                                              st), "fin")
+        outs_s.append(s)
+        outs_i.append(i)
+    ms, mi = K.merge_topk(torch.stack(outs_s), torch.stack(outs_i), k)
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    assert np.array_equal(mi.cpu().numpy(), ri) and np.array_equal(ms.cpu().numpy(), rs)

@@ -719,7 +719,8 @@ __global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict_
                                                      uint64_t* __restrict__ band,
                                                      int* __restrict__ band_n,
                                                      int* __restrict__ flags, int* qsel,
-                                                     int* qsel_n, int nq) {
+                                                     int* qsel_n, int nq,
+                                                     int* __restrict__ gcount) {
   __shared__ uint64_t buf[4][SW_CAP];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int qid = blockIdx.x * 4 + w;
@@ -759,6 +760,28 @@ __global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict_
     off += c;
   }
   wave_sync();
+  if (mode == 2) {  // sharded full level: every candidate is band; report #(a >= aref)
+    const float ar = aref[qid];
+    int cnt = 0, nb = 0;
+    uint64_t* qb = band + (int64_t)qid * BAND_CAP;
+    for (int j0 = 0; j0 < total; j0 += 64) {
+      const int j = j0 + lane;
+      const bool in = j < total;
+      const uint64_t key = in ? kb[j] : 0ull;
+      cnt += __popcll(__ballot(in && key_float((uint32_t)(key >> 32)) >= ar));
+      const uint64_t bm = __ballot(in);
+      const int pos = nb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+      if (in && pos < BAND_CAP) qb[pos] = key;
+      nb += __popcll(bm);
+    }
+    if (lane == 0) {
+      gcount[qid] = cnt;
+      if (nb > BAND_CAP) flag_query(qid, flags, qsel, qsel_n);  // this shard: exact fallback
+      else band_n[qid] = nb;
+    }
+    return;
+  }
   const int R = mode == 0 ? J : k;
   if (total < R) {  // fewer than R candidates: a_J = -inf (sample) / cannot certify (full)
     if (lane == 0) {
@@ -823,6 +846,15 @@ __global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict_
   }
 }
 
+// sharded: a query whose candidates above max_s a_J number fewer than k over all shards
+// (gcount all-reduced by the caller) did not certify its threshold -> exact fallback on
+// every shard (the decision is identical on all ranks).
+__global__ void k_flag_by_count(const int* __restrict__ gcount, int nq, int k, int* flags,
+                                int* qsel, int* qsel_n) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < nq && !flags[q] && gcount[q] < k) flag_query(q, flags, qsel, qsel_n);
+}
+
 // --------------------------------------------------------------------------- rerank
 template <int EP>
 __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, int64_t ld,
@@ -873,6 +905,10 @@ __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, in
   }
 }
 
+__global__ void k_fill_i32(int* x, int n, int v) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = v;
+}
 __global__ void k_fill_f32(float* x, int n, float v) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] = v;
@@ -1010,6 +1046,7 @@ struct FilterWs {
   float* theta;
   float* aref;
   float* eps2;
+  int* gcount;
   uint64_t* band;
   int* band_n;
   int* flags;  // flags[nq], qsel[nq], qsel_n[1] are contiguous (one memset)
@@ -1037,6 +1074,7 @@ static FilterWs carve(void* base, const FilterPlan& p, int64_t n, int d, int nq,
   w.theta = (float*)take((int64_t)nq * 4);
   w.aref = (float*)take((int64_t)nq * 4);
   w.eps2 = (float*)take((int64_t)nq * 4);
+  w.gcount = (int*)take((int64_t)nq * 4);
   w.band = (uint64_t*)take((int64_t)nq * BAND_CAP * 8);
   w.band_n = (int*)take((int64_t)nq * 4);
   int* fl = (int*)take(((int64_t)2 * nq + 1) * 4);
@@ -1103,31 +1141,35 @@ extern "C" int tt_filter_fallback_offset(int64_t n, int32_t d, int32_t nq, int32
   return TT_OK;
 }
 
-extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n,
-                                    int32_t d, int64_t ld_db, int64_t row_base, const float* q,
-                                    int32_t nq, int64_t ld_q, int32_t k, float x_norm_max,
-                                    float x_resid_max, float* out_score, int64_t* out_idx, void* workspace,
-                                    int64_t workspace_bytes, void* stream, void* ev_start,
-                                    void* ev_stop) {
+namespace {
+// Shared prologue of the single-shard call and the sharded stages: validation, plan, carve.
+int filter_setup(const float* db, const uint16_t* db_bf16, int64_t n, int32_t d, int64_t ld_db,
+                 const float* q, int32_t nq, int64_t ld_q, int32_t k, void* workspace,
+                 int64_t workspace_bytes, int* ep_out, FilterPlan* p, FilterWs* w) {
   TT_REQUIRE(n >= 1 && n <= 0x7fffffffLL, "need 1 <= n < 2^31");
-  TT_REQUIRE(nq >= 0, "nq < 0");
+  TT_REQUIRE(nq >= 1, "nq < 1");
   TT_REQUIRE(k >= 1 && k <= n, "need 1 <= k <= n");
-  TT_REQUIRE(x_norm_max >= 0.0f && x_resid_max >= 0.0f,
-             "x_norm_max / x_resid_max must be >= 0 (tt_bf16_image_bounds)");
-  if (nq == 0) return TT_OK;
-  if (k > FL_KMAX) return fail(TT_ERR_UNSUPPORTED, "tt_scan_topk_bf16f32: k > 128");
+  if (k > FL_KMAX) return fail(TT_ERR_UNSUPPORTED, "bf16 filter: k > 128");
   const int ep = tt_padded_dim(d);
-  if (ep < 0) return fail(TT_ERR_UNSUPPORTED, "tt_scan_topk_bf16f32: d > 768");
+  if (ep < 0) return fail(TT_ERR_UNSUPPORTED, "bf16 filter: d > 768");
   TT_REQUIRE(ld_db >= ep && ld_q >= ep && ld_db % 8 == 0 && ld_q % 4 == 0,
              "ld must be >= tt_padded_dim(d), ld_db % 8 == 0 (zero padded)");
-  TT_REQUIRE(((uintptr_t)db % 16) == 0 && ((uintptr_t)db_bf16 % 16) == 0 &&
+  TT_REQUIRE((db == nullptr || ((uintptr_t)db % 16) == 0) && ((uintptr_t)db_bf16 % 16) == 0 &&
                  ((uintptr_t)q % 16) == 0, "pointers must be 16-B aligned");
-  const FilterPlan p = plan_filter(n, nq, k, ep);
-  const FilterWs w = carve(workspace, p, n, d, nq, k);
-  if (workspace == nullptr || workspace_bytes < w.total)
-    return fail(TT_ERR_WORKSPACE, "tt_scan_topk_bf16f32: workspace too small");
-  hipStream_t st = (hipStream_t)stream;
-  if (hipMemsetAsync(w.flags, 0, ((size_t)2 * nq + 1) * 4, st) != hipSuccess)
+  *p = plan_filter(n, nq, k, ep);
+  *w = carve(workspace, *p, n, d, nq, k);
+  if (workspace == nullptr || workspace_bytes < w->total)
+    return fail(TT_ERR_WORKSPACE, "bf16 filter: workspace too small");
+  *ep_out = ep;
+  return TT_OK;
+}
+
+int filter_init(const FilterWs& w, const float* q, int nq, int64_t ld_q, int ep, float x_norm_max,
+                float x_resid_max, hipStream_t st) {
+  TT_REQUIRE(x_norm_max >= 0.0f && x_resid_max >= 0.0f,
+             "x_norm_max / x_resid_max must be >= 0 (tt_bf16_image_bounds)");
+  if (hipMemsetAsync(w.flags, 0, ((size_t)2 * nq + 1) * 4, st) != hipSuccess ||
+      hipMemsetAsync(w.gcount, 0, (size_t)nq * 4, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "hipMemsetAsync(flags)");
   const unsigned fill_grid = (unsigned)((nq + 255) / 256);
   hipLaunchKernelGGL(k_fill_f32, dim3(fill_grid), dim3(256), 0, st, w.theta, nq,
@@ -1144,32 +1186,50 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
     TT_QE(64) TT_QE(128) TT_QE(256) TT_QE(384) TT_QE(512) TT_QE(768)
 #undef TT_QE
   }
-  for (int li = 0; li < p.n_levels; ++li) {
-    const Level& L = p.lv[li];
-    const bool last = li == p.n_levels - 1;
-    if (last && li > 0)  // full-catalog level: theta = a_J(stride-16 sample) - 2 eps
-      hipLaunchKernelGGL(k_sub_arr, dim3(fill_grid), dim3(256), 0, st, w.theta, w.eps2, nq);
-    if (last && ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
-      return fail(TT_ERR_LAUNCH, "hipEventRecord(start)");
-    switch (ep) {
-      case 64: launch_level<64>(L, db_bf16, n, ld_db, q, nq, ld_q, w, st); break;
-      case 128: launch_level<128>(L, db_bf16, n, ld_db, q, nq, ld_q, w, st); break;
-      case 256: launch_level<256>(L, db_bf16, n, ld_db, q, nq, ld_q, w, st); break;
-      case 384: launch_level<384>(L, db_bf16, n, ld_db, q, nq, ld_q, w, st); break;
-      case 512: launch_level<512>(L, db_bf16, n, ld_db, q, nq, ld_q, w, st); break;
-      case 768: launch_level<768>(L, db_bf16, n, ld_db, q, nq, ld_q, w, st); break;
-      default: return fail(TT_ERR_UNSUPPORTED, "bad padded dim");
-    }
-    int rc = check_launch("k_filter");
-    if (rc) return rc;
-    if (last && ev_stop && hipEventRecord((hipEvent_t)ev_stop, st) != hipSuccess)
-      return fail(TT_ERR_LAUNCH, "hipEventRecord(stop)");
-    hipLaunchKernelGGL(k_select_wave, dim3((nq + 3) / 4), dim3(256), 0, st, w.lists, w.counts,
-                       L.n_slabs, k, p.J, w.eps2, last ? 1 : 0, w.theta, w.aref, w.band, w.band_n,
-                       w.flags, w.qsel, w.qsel_n, nq);
-    rc = check_launch("k_select_wave");
-    if (rc) return rc;
+  return check_launch("filter_init");
+}
+
+// level li (+ its selection in `mode`); events around the full-catalog level
+int filter_level(const FilterPlan& p, const FilterWs& w, int li, int mode, const uint16_t* db16,
+                 int64_t n, int64_t ld_db, const float* q, int nq, int64_t ld_q, int k, int ep,
+                 hipStream_t st, void* ev_start, void* ev_stop) {
+  const Level& L = p.lv[li];
+  const bool last = li == p.n_levels - 1;
+  if (last && ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
+    return fail(TT_ERR_LAUNCH, "hipEventRecord(start)");
+  switch (ep) {
+    case 64: launch_level<64>(L, db16, n, ld_db, q, nq, ld_q, w, st); break;
+    case 128: launch_level<128>(L, db16, n, ld_db, q, nq, ld_q, w, st); break;
+    case 256: launch_level<256>(L, db16, n, ld_db, q, nq, ld_q, w, st); break;
+    case 384: launch_level<384>(L, db16, n, ld_db, q, nq, ld_q, w, st); break;
+    case 512: launch_level<512>(L, db16, n, ld_db, q, nq, ld_q, w, st); break;
+    case 768: launch_level<768>(L, db16, n, ld_db, q, nq, ld_q, w, st); break;
+    default: return fail(TT_ERR_UNSUPPORTED, "bad padded dim");
   }
+  int rc = check_launch("k_filter");
+  if (rc) return rc;
+  if (last && ev_stop && hipEventRecord((hipEvent_t)ev_stop, st) != hipSuccess)
+    return fail(TT_ERR_LAUNCH, "hipEventRecord(stop)");
+  hipLaunchKernelGGL(k_select_wave, dim3((nq + 3) / 4), dim3(256), 0, st, w.lists, w.counts,
+                     L.n_slabs, k, p.J, w.eps2, mode, w.theta, w.aref, w.band, w.band_n, w.flags,
+                     w.qsel, w.qsel_n, nq, w.gcount);
+  return check_launch("k_select_wave");
+}
+
+// the full level's threshold: aref = theta (a_J of the last sample, global max when sharded),
+// theta = aref - 2 eps
+int full_threshold(const FilterWs& w, int nq, hipStream_t st) {
+  const unsigned g = (unsigned)((nq + 255) / 256);
+  if (hipMemcpyAsync(w.aref, w.theta, (size_t)nq * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return fail(TT_ERR_LAUNCH, "hipMemcpyAsync(aref)");
+  hipLaunchKernelGGL(k_sub_arr, dim3(g), dim3(256), 0, st, w.theta, w.eps2, nq);
+  return check_launch("k_sub_arr");
+}
+
+int filter_finish(const FilterWs& w, const float* db, int64_t n, int32_t d, int64_t ld_db,
+                  int64_t row_base, const float* q, int nq, int64_t ld_q, int k, int ep,
+                  float* out_score, int64_t* out_idx, hipStream_t st) {
+  TT_REQUIRE(db != nullptr && out_score && out_idx, "null pointer");
   switch (ep) {
 #define TT_RR(E)                                                                              \
   case E:                                                                                     \
@@ -1183,5 +1243,107 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
   if (rc) return rc;
   // exact fallback for flagged queries (blocks exit at once when none is flagged)
   return tt_scan_topk_f32_select(db, n, d, ld_db, row_base, q, nq, ld_q, k, w.qsel, w.qsel_n,
-                                 out_score, out_idx, w.scan_ws, w.scan_ws_bytes, stream);
+                                 out_score, out_idx, w.scan_ws, w.scan_ws_bytes, st);
+}
+}  // namespace
+
+extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n,
+                                    int32_t d, int64_t ld_db, int64_t row_base, const float* q,
+                                    int32_t nq, int64_t ld_q, int32_t k, float x_norm_max,
+                                    float x_resid_max, float* out_score, int64_t* out_idx,
+                                    void* workspace, int64_t workspace_bytes, void* stream,
+                                    void* ev_start, void* ev_stop) {
+  TT_REQUIRE(nq >= 0, "nq < 0");
+  if (nq == 0) return TT_OK;
+  int ep;
+  FilterPlan p;
+  FilterWs w;
+  int rc = filter_setup(db, db_bf16, n, d, ld_db, q, nq, ld_q, k, workspace, workspace_bytes, &ep,
+                        &p, &w);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if ((rc = filter_init(w, q, nq, ld_q, ep, x_norm_max, x_resid_max, st))) return rc;
+  for (int li = 0; li < p.n_levels; ++li) {
+    const bool last = li == p.n_levels - 1;
+    if (last && li > 0 && (rc = full_threshold(w, nq, st))) return rc;
+    if ((rc = filter_level(p, w, li, last ? 1 : 0, db_bf16, n, ld_db, q, nq, ld_q, k, ep, st,
+                           ev_start, ev_stop)))
+      return rc;
+  }
+  return filter_finish(w, db, n, d, ld_db, row_base, q, nq, ld_q, k, ep, out_score, out_idx, st);
+}
+
+// ------------------------------------------------------------------ sharded (multi-GPU)
+extern "C" int tt_sharded_filter_begin(const uint16_t* db_bf16, int64_t n, int32_t d,
+                                       int64_t ld_db, const float* q, int32_t nq, int64_t ld_q,
+                                       int32_t k, float x_norm_max, float x_resid_max,
+                                       void* workspace, int64_t workspace_bytes, void* stream,
+                                       int64_t* theta_offset) {
+  TT_REQUIRE(theta_offset != nullptr, "theta_offset == NULL");
+  int ep;
+  FilterPlan p;
+  FilterWs w;
+  int rc = filter_setup(nullptr, db_bf16, n, d, ld_db, q, nq, ld_q, k, workspace, workspace_bytes,
+                        &ep, &p, &w);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if ((rc = filter_init(w, q, nq, ld_q, ep, x_norm_max, x_resid_max, st))) return rc;
+  for (int li = 0; li + 1 < p.n_levels; ++li)
+    if ((rc = filter_level(p, w, li, 0, db_bf16, n, ld_db, q, nq, ld_q, k, ep, st, nullptr,
+                           nullptr)))
+      return rc;
+  *theta_offset = (int64_t)((char*)w.theta - (char*)workspace);
+  return TT_OK;
+}
+
+extern "C" int tt_sharded_filter_full(const uint16_t* db_bf16, int64_t n, int32_t d,
+                                      int64_t ld_db, const float* q, int32_t nq, int64_t ld_q,
+                                      int32_t k, void* workspace, int64_t workspace_bytes,
+                                      void* stream, void* ev_start, void* ev_stop,
+                                      int64_t* count_offset) {
+  TT_REQUIRE(count_offset != nullptr, "count_offset == NULL");
+  int ep;
+  FilterPlan p;
+  FilterWs w;
+  int rc = filter_setup(nullptr, db_bf16, n, d, ld_db, q, nq, ld_q, k, workspace, workspace_bytes,
+                        &ep, &p, &w);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  const int li = p.n_levels - 1;
+  if (li == 0) {
+    // a shard of <= 2048 rows has no sample level: exact local top-k (mode 1) and a count
+    // that always certifies
+    if ((rc = filter_level(p, w, li, 1, db_bf16, n, ld_db, q, nq, ld_q, k, ep, st, ev_start,
+                           ev_stop)))
+      return rc;
+    hipLaunchKernelGGL(k_fill_i32, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, w.gcount,
+                       nq, 0x3fffffff);
+  } else {
+    if ((rc = full_threshold(w, nq, st))) return rc;
+    if ((rc = filter_level(p, w, li, 2, db_bf16, n, ld_db, q, nq, ld_q, k, ep, st, ev_start,
+                           ev_stop)))
+      return rc;
+  }
+  *count_offset = (int64_t)((char*)w.gcount - (char*)workspace);
+  return check_launch("tt_sharded_filter_full");
+}
+
+extern "C" int tt_sharded_filter_finish(const float* db, const uint16_t* db_bf16, int64_t n,
+                                        int32_t d, int64_t ld_db, int64_t row_base,
+                                        const float* q, int32_t nq, int64_t ld_q, int32_t k,
+                                        float* out_score, int64_t* out_idx, void* workspace,
+                                        int64_t workspace_bytes, void* stream) {
+  int ep;
+  FilterPlan p;
+  FilterWs w;
+  int rc = filter_setup(db, db_bf16, n, d, ld_db, q, nq, ld_q, k, workspace, workspace_bytes, &ep,
+                        &p, &w);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (p.n_levels > 1) {
+    hipLaunchKernelGGL(k_flag_by_count, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st,
+                       w.gcount, nq, k, w.flags, w.qsel, w.qsel_n);
+    if ((rc = check_launch("k_flag_by_count"))) return rc;
+  }
+  return filter_finish(w, db, n, d, ld_db, row_base, q, nq, ld_q, k, ep, out_score, out_idx, st);
 }

@@ -69,6 +69,13 @@ SIGNATURES = {
     "tt_scan_topk_bf16f32": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _i64, _vp, _i32, _i64,
                                             _i32, ctypes.c_float, ctypes.c_float, _vp, _vp, _vp,
                                             _i64, _vp, _vp, _vp]),
+    "tt_sharded_filter_begin": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _i64, _i32,
+                                               ctypes.c_float, ctypes.c_float, _vp, _i64, _vp,
+                                               ctypes.POINTER(_i64)]),
+    "tt_sharded_filter_full": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _i64, _i32, _vp,
+                                              _i64, _vp, _vp, _vp, ctypes.POINTER(_i64)]),
+    "tt_sharded_filter_finish": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _i64, _vp, _i32,
+                                                _i64, _i32, _vp, _vp, _vp, _i64, _vp]),
     "tt_bf16_image_bounds": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _vp, _vp]),
     "tt_topk_merge_f32": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp]),
     "tt_weighted_avg_l2_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _i64, _vp]),

@@ -145,6 +145,51 @@ def scan_topk_bf16(db: torch.Tensor, db16: torch.Tensor, n: int, d: int, q: torc
     return out
 
 
+def scan_topk_bf16_sharded(db: torch.Tensor, db16: torch.Tensor, n: int, d: int,
+                           q: torch.Tensor, k: int, bounds, row_base: int, allreduce_max,
+                           allreduce_sum, workspace: torch.Tensor = None, out=None,
+                           events=(None, None)):
+    """This shard's part of the GLOBAL exact top-k (tt_sharded_filter_*, include/twotower_hip.h).
+
+    allreduce_max(t) / allreduce_sum(t) reduce a device tensor in place over the shards
+    (e.g. torch.distributed.all_reduce with ReduceOp.MAX / SUM); every shard passes the same
+    queries.  Merge the shards' outputs with merge_topk."""
+    _check_2d(db, "db")
+    _check_2d(db16, "db16", torch.bfloat16)
+    _check_2d(q, "q")
+    nq = q.shape[0]
+    if not (1 <= k <= min(n, FILTER_KMAX)) or n > db.shape[0]:
+        raise ValueError(f"scan_topk_bf16_sharded: need 1 <= k ({k}) <= min(n, 128)")
+    if out is None:
+        out = (torch.empty((nq, k), dtype=_f32, device=q.device),
+               torch.empty((nq, k), dtype=torch.int64, device=q.device))
+    if nq == 0:
+        return out
+    need = filter_workspace_bytes(n, d, nq, k)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=q.device)
+    x_norm_max, x_resid_max = (float(v) for v in bounds)
+    L, st = lib(), stream_ptr()
+    off = ctypes.c_int64(0)
+    check(L.tt_sharded_filter_begin(_ptr(db16), n, d, db16.stride(0), _ptr(q), nq, q.stride(0), k,
+                                    ctypes.c_float(x_norm_max), ctypes.c_float(x_resid_max),
+                                    _ptr(workspace), workspace.numel(), st, ctypes.byref(off)),
+          "tt_sharded_filter_begin")
+    allreduce_max(workspace[off.value:off.value + 4 * nq].view(_f32))
+    e0, e1 = events
+    check(L.tt_sharded_filter_full(_ptr(db16), n, d, db16.stride(0), _ptr(q), nq, q.stride(0), k,
+                                   _ptr(workspace), workspace.numel(), st,
+                                   e0.cuda_event if e0 is not None else None,
+                                   e1.cuda_event if e1 is not None else None, ctypes.byref(off)),
+          "tt_sharded_filter_full")
+    allreduce_sum(workspace[off.value:off.value + 4 * nq].view(torch.int32))
+    check(L.tt_sharded_filter_finish(_ptr(db), _ptr(db16), n, d, db.stride(0), row_base, _ptr(q),
+                                     nq, q.stride(0), k, _ptr(out[0]), _ptr(out[1]),
+                                     _ptr(workspace), workspace.numel(), st),
+          "tt_sharded_filter_finish")
+    return out
+
+
 def merge_topk(scores: torch.Tensor, idx: torch.Tensor, k: int):
     """[L, nq, k_in] per-shard sorted lists (global ids) -> [nq, k]."""
     require_device(scores, "scores")
