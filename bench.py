@@ -175,21 +175,47 @@ def main():
     w = event_mix(gb, (B, S), dev)
 
     q = torch.empty((B, ep), device=dev)
-    ex = TopkExchange(B, ep, K, device=dev)  # all-gather queries / all-to-all top-k (RCCL)
+    staged = a.method == "bf16" and world > 1
+    # all-gather queries (+ their sharded-filter stats) / all-to-all top-k (RCCL)
+    ex = TopkExchange(B, ep, K, device=dev, aux_width=2 if staged else 0)
     nq = world * B
-    ws_bytes = (kernels.filter_workspace_bytes(hi - lo, E, nq, K) if a.method == "bf16"
-                else kernels.scan_workspace_bytes(hi - lo, E, nq, K))
+    if staged:
+        # row-sharded bf16 filter (tt_sharded_filter_*): the replicated 1/16 catalog sample
+        # (from the replicated item table, same rows as the shards' images) and the
+        # whole-catalog bounds (MAX over ranks), both built once like the index
+        sample16 = torch.empty(((N + 15) // 16, ep), device=dev, dtype=torch.bfloat16)
+        kernels.l2norm_rows(table[::16].contiguous(), E, _lib.TT_NORM_ADD_EPS,
+                            out=torch.empty_like(sample16, dtype=torch.float32),
+                            out_bf16=sample16)
+        gb_ = torch.tensor(bounds, device=dev)
+        dist.all_reduce(gb_, op=dist.ReduceOp.MAX)
+        bounds = gb_.tolist()
+        stats = torch.empty((B, 2), device=dev)
+        ws_begin = torch.empty(kernels.filter_workspace_bytes(sample16.shape[0], E, B, K),
+                               dtype=torch.uint8, device=dev)
+        pcount = torch.empty((nq, _lib.TT_SHARD_PROBES), dtype=torch.int32, device=dev)
+        ws_bytes = kernels.sharded_workspace_bytes(hi - lo, E, nq, K)
+    elif a.method == "bf16":
+        ws_bytes = kernels.filter_workspace_bytes(hi - lo, E, nq, K)
+    else:
+        ws_bytes = kernels.scan_workspace_bytes(hi - lo, E, nq, K)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     s_shard = torch.empty((nq, K), device=dev)
     i_shard = torch.empty((nq, K), dtype=torch.int64, device=dev)
     L = _lib.lib()
     stream = torch.cuda.current_stream()
 
-    def local_search(qall, ev):
+    def local_search(qall, ev, stats_all=None):
         e0, e1, p0, p1 = (ev if ev else (None, None, None, None))
         if p0 is not None:
             p0.record(stream)
-        if a.method == "bf16":
+        if staged:
+            # shard filter -> all-reduce SUM of probe counts -> shard re-rank
+            kernels.sharded_search(shard, shard16, hi - lo, E, qall, K, bounds, lo, stats_all,
+                                   lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM),
+                                   workspace=ws, out=(s_shard, i_shard), pcount=pcount,
+                                   events=(e0, e1))
+        elif a.method == "bf16":
             kernels.scan_topk_bf16(shard, shard16, hi - lo, E, qall, K, bounds, row_base=lo,
                                    workspace=ws, out=(s_shard, i_shard), events=(e0, e1))
         else:
@@ -206,6 +232,10 @@ def main():
     def step(ev=None):
         kernels.gather_weighted_avg_l2(table, E, hist, w, out=q)  # Mode B buyer encode
         kernels.l2norm_rows(q, E, _lib.TT_NORM_ADD_EPS, out=q)    # retrieve_batch :189-190
+        if staged:  # this rank's thresholds from the replicated sample, gathered with q
+            kernels.sharded_begin(sample16, E, q, K, stats=stats, workspace=ws_begin)
+            return ex.search(q, lambda qall, sall: local_search(qall, ev, sall),
+                             kernels.merge_topk, aux=stats)
         return ex.search(q, lambda qall: local_search(qall, ev), kernels.merge_topk)
 
     for _ in range(a.warmup):
@@ -234,8 +264,8 @@ def main():
         t = torch.tensor([dt, scan_ms, search_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, scan_ms, search_ms = t.tolist()
-    fallback = (kernels.filter_fallback_count(ws, hi - lo, E, nq, K) if a.method == "bf16"
-                else 0)
+    fallback = (kernels.filter_fallback_count(ws, hi - lo, E, nq, K, sharded=staged)
+                if a.method == "bf16" else 0)
     ms_per_step = dt / a.steps * 1e3
     value = world * B / (dt / a.steps)
 
@@ -272,7 +302,7 @@ def main():
             "workload": "configs[2]: 1M x 384 catalog, 10k buyers/rank x 20 events, weighted-avg, "
                         "Mode B (history rows gathered), k=100",
             "catalog_rows": N, "dim": E, "buyers_per_rank": B, "history": S, "k": K,
-            "parallelism": f"catalog row-shard x{world}" + (" + RCCL all-gather(queries) / all-to-all(top-k)" if world > 1 else ""),
+            "parallelism": f"catalog row-shard x{world}" + (" + RCCL all-gather(queries), all-reduce(threshold, counts), all-to-all(top-k)" if world > 1 else ""),
         },
         "roofline": {
             "kernel": kname,

@@ -120,33 +120,46 @@ int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n, in
                          void* ev_start, void* ev_stop);
 
 /* ---------------------------------------------------------------------------------
- * Row-sharded (multi-GPU) form of tt_scan_topk_bf16f32: three stages with two tiny
- * collectives in between.  Each rank calls, on its shard (same nq
- * queries on every rank, row_base = first global row of the shard):
- *   1. tt_sharded_filter_begin   sample levels; theta[nq] f32 at workspace + *theta_offset
- *      -> caller: all-reduce MAX over ranks (in place)
- *   2. tt_sharded_filter_full    full level with theta_q = max_s a_J - 2 eps_q (the union's
- *      sample statistic: each shard keeps only rows that can be in the GLOBAL top-k);
- *      gcount[nq] int32 at workspace + *count_offset = #candidates >= max_s a_J
- *      -> caller: all-reduce SUM over ranks (in place)
- *   3. tt_sharded_filter_finish  queries with sum < k fall back to the exact scan on every
- *      rank; the rest re-rank their shard's candidates exactly; out = this shard's part of
- *      the global top-k (padded with (-inf, -1)), to be merged with tt_topk_merge_f32.
- * Each shard re-ranks only rows that can be in the global top-k, so the exact work summed
- * over ranks stays that of one search over the whole catalog.  Same workspace size as
- * tt_filter_workspace_bytes(n_shard, d, nq, k).
+ * Row-sharded (multi-GPU) form of tt_scan_topk_bf16f32 (faiss IndexFlatIP.search,
+ * vector_db.py:160,197, over a catalog split by rows across ranks).
+ * Every rank holds its shard [row_base, row_base + n) in f32 and bf16, plus the GLOBAL
+ * stride-TT_SHARD_SAMPLE_STRIDE sample of the bf16 image (rows 0, 16, 32, ... of the whole
+ * catalog; 1/16 of a shard-set, built once with the index).  Per batch:
+ *   1. tt_sharded_filter_begin (rank-local queries only, on the global sample):
+ *      stats[q] = {theta_q, smax_q} = {a_J, max a} of the sample -- the threshold the
+ *      single-catalog call derives, and the top of the probe range.
+ *      -> caller: all-gather queries and stats (row order = query order)
+ *   2. tt_sharded_filter_full (all W*B queries, on the shard):  bf16 filter with
+ *      theta_q - 2 eps_q; probe_counts[q][i] = #shard rows with a >= t_i,
+ *      t_i = theta_q + i (smax_q - theta_q) / TT_SHARD_PROBES.
+ *      -> caller: all-reduce SUM of probe_counts [nq][TT_SHARD_PROBES] int32
+ *   3. tt_sharded_filter_finish: a query with < k rows over all shards above theta_q takes the
+ *      exact scan on every rank (identical decision everywhere); the rest re-rank the shard
+ *      rows with a >= t* - 2 eps_q, t* = highest probe holding >= k rows (t* <= A_k).
+ *      out = this shard's part of the global top-k (padded (-inf, -1)), merged across ranks
+ *      with tt_topk_merge_f32 -- bit-identical to one search over the whole catalog.
+ * x_norm_max / x_resid_max must bound the WHOLE catalog (all-reduce MAX of the shards'
+ * tt_bf16_image_bounds).  Workspaces: begin -> tt_filter_workspace_bytes(n_sample, d, B, k);
+ * full + finish (same buffer, kept between the calls) -> tt_sharded_workspace_bytes.
  * --------------------------------------------------------------------------------- */
-int tt_sharded_filter_begin(const uint16_t* db_bf16, int64_t n, int32_t d, int64_t ld_db,
-                            const float* q, int32_t nq, int64_t ld_q, int32_t k,
-                            float x_norm_max, float x_resid_max, void* workspace,
-                            int64_t workspace_bytes, void* stream, int64_t* theta_offset);
+#define TT_SHARD_PROBES 16
+#define TT_SHARD_SAMPLE_STRIDE 16
+int tt_sharded_workspace_bytes(int64_t n, int32_t d, int32_t nq, int32_t k, int64_t* bytes);
+/* byte offset in the full/finish workspace of the int32 count of queries that took the
+ * exact fallback on this shard (diagnostic) */
+int tt_sharded_fallback_offset(int64_t n, int32_t d, int32_t nq, int32_t k, int64_t* offset);
+int tt_sharded_filter_begin(const uint16_t* sample_bf16, int64_t n_sample, int32_t d, int64_t ld,
+                            const float* q, int32_t nq, int64_t ld_q, int32_t k, float* stats,
+                            void* workspace, int64_t workspace_bytes, void* stream);
 int tt_sharded_filter_full(const uint16_t* db_bf16, int64_t n, int32_t d, int64_t ld_db,
-                           const float* q, int32_t nq, int64_t ld_q, int32_t k, void* workspace,
-                           int64_t workspace_bytes, void* stream, void* ev_start, void* ev_stop,
-                           int64_t* count_offset);
+                           const float* q, int32_t nq, int64_t ld_q, int32_t k,
+                           float x_norm_max, float x_resid_max, const float* stats,
+                           int32_t* probe_counts, void* workspace, int64_t workspace_bytes,
+                           void* stream, void* ev_start, void* ev_stop);
 int tt_sharded_filter_finish(const float* db, const uint16_t* db_bf16, int64_t n, int32_t d,
                              int64_t ld_db, int64_t row_base, const float* q, int32_t nq,
-                             int64_t ld_q, int32_t k, float* out_score, int64_t* out_idx,
+                             int64_t ld_q, int32_t k, const float* stats,
+                             const int32_t* probe_counts, float* out_score, int64_t* out_idx,
                              void* workspace, int64_t workspace_bytes, void* stream);
 
 /* Bounds of a catalog shard and its bf16 image for tt_scan_topk_bf16f32: max-combines

@@ -374,62 +374,83 @@ def test_scan_full_size_properties(K, oracle_mod):
     assert not missing.any()
 
 
-@pytest.mark.parametrize("W,n,nq,k", [(2, 300000, 64, 100), (8, 1000000, 40, 100),
-                                      (3, 5000, 17, 64), (4, 2000, 9, 10)])
-def test_sharded_filter_protocol_bit_exact(K, oracle_mod, W, n, nq, k):
-    """tt_sharded_filter_* on W row shards of one catalog (the collectives done by hand on
-    one GPU) + merge == the single-catalog exact top-k, bit for bit."""
+def _sharded_search_emulated(K, x, q, W, k, owners=None):
+    """The row-sharded protocol with W shards on one GPU: per-owner begin on the global
+    sample, stats 'all-gathered' by concatenation, probe counts 'all-reduced' by summing."""
     from twotower.sharded import shard_range
 
+    n = x.shape[0]
+    nq = q.shape[0]
+    qd = dev_rows(q)
+    xd = dev_rows(x)
+    x16 = xd.to(torch.bfloat16)
+    sample = K.sharded_sample(x16, n)
+    groups = owners or [(r * nq // W, (r + 1) * nq // W) for r in range(W)]
+    stats = torch.cat([K.sharded_begin(sample, 384, qd[a:b], k) for a, b in groups])
+    shards = []
+    bmax = torch.zeros(2)
+    for r in range(W):
+        lo, hi = shard_range(n, r, W)
+        bd = torch.tensor(bounds(K, xd[lo:hi], x16[lo:hi], 384))
+        bmax = torch.maximum(bmax, bd)
+        shards.append((lo, hi))
+    pcs = [torch.empty((nq, 16), dtype=torch.int32, device="cuda") for _ in range(W)]
+    wss = [None] * W
+    outs = [None] * W
+    # stage 2 on every shard, then the SUM, then stage 3 (split sharded_search by hand)
+    from twotower import _lib
+    import ctypes
+
+    L, st = _lib.lib(), _lib.stream_ptr()
+    for r, (lo, hi) in enumerate(shards):
+        wss[r] = torch.empty(K.sharded_workspace_bytes(hi - lo, 384, nq, k), dtype=torch.uint8,
+                             device="cuda")
+        _lib.check(L.tt_sharded_filter_full(
+            x16[lo:].data_ptr(), hi - lo, 384, x16.stride(0), qd.data_ptr(), nq, qd.stride(0), k,
+            ctypes.c_float(bmax[0]), ctypes.c_float(bmax[1]), stats.data_ptr(), pcs[r].data_ptr(),
+            wss[r].data_ptr(), wss[r].numel(), st, None, None), "full")
+    total = torch.stack(pcs).sum(0, dtype=torch.int32)
+    for r, (lo, hi) in enumerate(shards):
+        s_ = torch.empty((nq, k), device="cuda")
+        i_ = torch.empty((nq, k), device="cuda", dtype=torch.int64)
+        _lib.check(L.tt_sharded_filter_finish(
+            xd[lo:].data_ptr(), x16[lo:].data_ptr(), hi - lo, 384, xd.stride(0), lo, qd.data_ptr(),
+            nq, qd.stride(0), k, stats.data_ptr(), total.data_ptr(), s_.data_ptr(), i_.data_ptr(),
+            wss[r].data_ptr(), wss[r].numel(), st), "finish")
+        outs[r] = (s_, i_)
+    fb = [K.filter_fallback_count(wss[r], hi - lo, 384, nq, k, sharded=True)
+          for r, (lo, hi) in enumerate(shards)]
+    ms, mi = K.merge_topk(torch.stack([o[0] for o in outs]), torch.stack([o[1] for o in outs]), k)
+    return ms.cpu().numpy(), mi.cpu().numpy(), fb
+
+
+@pytest.mark.parametrize("W,n,nq,k", [(2, 300000, 64, 100), (8, 1000000, 40, 100),
+                                      (3, 5000, 17, 64), (4, 2000, 9, 10), (8, 70000, 33, 128)])
+def test_sharded_filter_protocol_bit_exact(K, oracle_mod, W, n, nq, k):
+    """tt_sharded_filter_* on W row shards of one catalog (collectives done by hand on one
+    GPU) + merge == the single-catalog exact top-k, bit for bit; few fallbacks on iid data."""
     rng = np.random.default_rng(W * 1000 + nq)
     x = oracle_mod.l2norm_rows(rng.standard_normal((n, 384)).astype(np.float32), 0)
     x[n // 2: n // 2 + 50] = x[:50]  # duplicates across shards
     q = oracle_mod.l2norm_rows(rng.standard_normal((nq, 384)).astype(np.float32), 0)
-    qd = dev_rows(q)
-    shards = []
-    for r in range(W):
-        lo, hi = shard_range(n, r, W)
-        db = dev_rows(x[lo:hi])
-        db16 = db.to(torch.bfloat16)
-        shards.append((lo, hi, db, db16, bounds(K, db, db16, 384)))
-    # run the three stages on every shard, reducing between them like the collectives would
-    import ctypes
-    from twotower import _lib
-
-    L, st = _lib.lib(), _lib.stream_ptr()
-    wss, offs = [], []
-    for lo, hi, db, db16, bd in shards:
-        ws = torch.empty(K.filter_workspace_bytes(hi - lo, 384, nq, k), dtype=torch.uint8,
-                         device="cuda")
-        off = ctypes.c_int64(0)
-        _lib.check(L.tt_sharded_filter_begin(db16.data_ptr(), hi - lo, 384, db16.stride(0),
-                                             qd.data_ptr(), nq, qd.stride(0), k,
-                                             ctypes.c_float(bd[0]), ctypes.c_float(bd[1]),
-                                             ws.data_ptr(), ws.numel(), st, ctypes.byref(off)), "b")
-        wss.append(ws)
-        offs.append(off.value)
-    th = torch.stack([ws[o:o + 4 * nq].view(torch.float32) for ws, o in zip(wss, offs)]).amax(0)
-    for ws, o in zip(wss, offs):
-        ws[o:o + 4 * nq].view(torch.float32).copy_(th)
-    coffs = []
-    for (lo, hi, db, db16, bd), ws in zip(shards, wss):
-        off = ctypes.c_int64(0)
-        _lib.check(L.tt_sharded_filter_full(db16.data_ptr(), hi - lo, 384, db16.stride(0),
-                                            qd.data_ptr(), nq, qd.stride(0), k, ws.data_ptr(),
-                                            ws.numel(), st, None, None, ctypes.byref(off)), "f")
-        coffs.append(off.value)
-    cnt = torch.stack([ws[o:o + 4 * nq].view(torch.int32) for ws, o in zip(wss, coffs)]).sum(0)
-    outs_s, outs_i = [], []
-    for (lo, hi, db, db16, bd), ws, o in zip(shards, wss, coffs):
-        ws[o:o + 4 * nq].view(torch.int32).copy_(cnt.to(torch.int32))
-        s = torch.empty((nq, k), device="cuda")
-        i = torch.empty((nq, k), device="cuda", dtype=torch.int64)
-        _lib.check(L.tt_sharded_filter_finish(db.data_ptr(), db16.data_ptr(), hi - lo, 384,
-                                              db.stride(0), lo, qd.data_ptr(), nq, qd.stride(0), k,
-                                              s.data_ptr(), i.data_ptr(), ws.data_ptr(), ws.numel(),
-                                              st), "fin")
-        outs_s.append(s)
-        outs_i.append(i)
-    ms, mi = K.merge_topk(torch.stack(outs_s), torch.stack(outs_i), k)
+    ms, mi, fb = _sharded_search_emulated(K, x, q, W, k)
     rs, ri = oracle_mod.scan_topk(x, q, k)
-    assert np.array_equal(mi.cpu().numpy(), ri) and np.array_equal(ms.cpu().numpy(), rs)
+    assert np.array_equal(mi, ri) and np.array_equal(ms, rs)
+    if n >= 100000:
+        assert max(fb) <= nq // 10, fb
+
+
+def test_sharded_filter_clustered_and_nan(K, oracle_mod):
+    """Near-duplicate clusters (tiny score gaps: probes land inside eps) and a NaN query:
+    still bit-exact (fallbacks allowed)."""
+    rng = np.random.default_rng(7)
+    n, W, k = 60000, 4, 100
+    c = rng.standard_normal((30, 384)).astype(np.float32)
+    x = c[rng.integers(0, 30, n)] + 1e-3 * rng.standard_normal((n, 384)).astype(np.float32)
+    x = oracle_mod.l2norm_rows(x, 0)
+    q = oracle_mod.l2norm_rows(rng.standard_normal((12, 384)).astype(np.float32), 0)
+    q[3] = np.nan
+    ms, mi, _ = _sharded_search_emulated(K, x, q, W, k)
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    ok = np.arange(12) != 3
+    assert np.array_equal(mi[ok], ri[ok]) and np.array_equal(ms[ok], rs[ok])

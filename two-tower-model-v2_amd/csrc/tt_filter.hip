@@ -42,6 +42,16 @@ constexpr int FL_CAP = 256;     // entries per (query, slab) list
 constexpr int SEL_CAP = 4096;   // candidates per query a level may produce
 constexpr int BAND_CAP = 1024;  // rows per query in the final band
 constexpr int FL_KMAX = 128;
+constexpr int SH_P = TT_SHARD_PROBES;  // sharded: count probes per query
+
+// Sharded probe thresholds t_i = theta + i (smax - theta) / SH_P, i < SH_P (t_0 = theta).
+// Identical expression in the counting (k_select_wave mode 2) and cutting (k_probe_cut)
+// kernels: the cut is sound only for a t_i whose counts were taken with the same float.
+__device__ __forceinline__ float probe_t(float theta, float smax, int i) {
+  const float span = smax - theta;
+  const float step = (span > 0.0f && span < __builtin_huge_valf()) ? span * (1.0f / SH_P) : 0.0f;
+  return fmaf((float)i, step, theta);
+}
 
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return (uint32_t)f32_to_bf16_rne(lo) | ((uint32_t)f32_to_bf16_rne(hi) << 16);
@@ -720,12 +730,15 @@ __global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict_
                                                      int* __restrict__ band_n,
                                                      int* __restrict__ flags, int* qsel,
                                                      int* qsel_n, int nq,
-                                                     int* __restrict__ gcount) {
+                                                     const float* __restrict__ stats,
+                                                     int* __restrict__ pcount,
+                                                     float* __restrict__ smax_out) {
   __shared__ uint64_t buf[4][SW_CAP];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int qid = blockIdx.x * 4 + w;
   if (qid >= nq) return;  // the whole wave (no block-level barriers below)
   uint64_t* kb = buf[w];
+  if (mode == 2 && lane < SH_P) pcount[(int64_t)qid * SH_P + lane] = 0;  // overflow: count 0
   if (flags[qid]) {
     if (lane == 0 && mode == 0) theta_out[qid] = __builtin_huge_valf();
     return;
@@ -760,23 +773,32 @@ __global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict_
     off += c;
   }
   wave_sync();
-  if (mode == 2) {  // sharded full level: every candidate is band; report #(a >= aref)
-    const float ar = aref[qid];
-    int cnt = 0, nb = 0;
+  if (mode == 2) {
+    // sharded full level: every candidate (a >= theta_g - eps2) is band; report the shard's
+    // count of candidates a >= t_i at the SH_P probes (all-reduced SUM by the caller)
+    const float th = stats[2 * qid], sm = stats[2 * qid + 1];
+    int cnt[SH_P];
+#pragma unroll
+    for (int i = 0; i < SH_P; ++i) cnt[i] = 0;
+    int nb = 0;
     uint64_t* qb = band + (int64_t)qid * BAND_CAP;
     for (int j0 = 0; j0 < total; j0 += 64) {
       const int j = j0 + lane;
       const bool in = j < total;
       const uint64_t key = in ? kb[j] : 0ull;
-      cnt += __popcll(__ballot(in && key_float((uint32_t)(key >> 32)) >= ar));
+      const float a = key_float((uint32_t)(key >> 32));
+#pragma unroll
+      for (int i = 0; i < SH_P; ++i) cnt[i] += __popcll(__ballot(in && a >= probe_t(th, sm, i)));
       const uint64_t bm = __ballot(in);
       const int pos = nb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
       if (in && pos < BAND_CAP) qb[pos] = key;
       nb += __popcll(bm);
     }
+#pragma unroll
+    for (int i = 0; i < SH_P; ++i)
+      if (lane == i) pcount[(int64_t)qid * SH_P + i] = cnt[i];
     if (lane == 0) {
-      gcount[qid] = cnt;
       if (nb > BAND_CAP) flag_query(qid, flags, qsel, qsel_n);  // this shard: exact fallback
       else band_n[qid] = nb;
     }
@@ -788,6 +810,7 @@ __global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict_
       if (mode == 0) {
         theta_out[qid] = -__builtin_huge_valf();
         aref[qid] = -__builtin_huge_valf();
+        if (smax_out) smax_out[qid] = -__builtin_huge_valf();  // probes all at theta = -inf
       } else {
         flag_query(qid, flags, qsel, qsel_n);
       }
@@ -815,6 +838,14 @@ __global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict_
   }
   const float A = key_float(T);
   if (mode == 0) {
+    if (smax_out) {  // sharded: the sample's best a (upper end of the probe range)
+      uint32_t m = 0;
+#pragma unroll
+      for (int i = 0; i < PER; ++i)
+        if (i < ni) m = max(m, hv[i]);
+      for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+      if (lane == 0) smax_out[qid] = key_float(m);
+    }
     if (lane == 0) {
       theta_out[qid] = A;
       aref[qid] = A;
@@ -846,13 +877,24 @@ __global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict_
   }
 }
 
-// sharded: a query whose candidates above max_s a_J number fewer than k over all shards
-// (gcount all-reduced by the caller) did not certify its threshold -> exact fallback on
-// every shard (the decision is identical on all ranks).
-__global__ void k_flag_by_count(const int* __restrict__ gcount, int nq, int k, int* flags,
-                                int* qsel, int* qsel_n) {
+// sharded finish: pcount[q][i] = #rows over ALL shards with a >= t_i (all-reduced SUM).
+// pcount[q][0] < k: the sample threshold did not certify -> exact fallback on every shard
+// (identical decision on all ranks).  Else A_k >= t* = the highest probe with >= k rows, so
+// every row of the exact top-k has a >= A_k - eps2 >= t* - eps2 = cut[q] (the band bound of
+// the single-shard path with A_k relaxed to t*).
+__global__ void k_probe_cut(const int* __restrict__ pcount, const float* __restrict__ stats,
+                            const float* __restrict__ eps2, int nq, int k, int* flags, int* qsel,
+                            int* qsel_n, float* __restrict__ cut) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q < nq && !flags[q] && gcount[q] < k) flag_query(q, flags, qsel, qsel_n);
+  if (q >= nq) return;
+  const int* pc = pcount + (int64_t)q * SH_P;
+  if (pc[0] < k) {
+    if (!flags[q]) flag_query(q, flags, qsel, qsel_n);
+    return;
+  }
+  int i = 0;
+  while (i + 1 < SH_P && pc[i + 1] >= k) ++i;
+  cut[q] = probe_t(stats[2 * q], stats[2 * q + 1], i) - eps2[q];
 }
 
 // --------------------------------------------------------------------------- rerank
@@ -862,17 +904,33 @@ __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, in
                                                 const uint64_t* __restrict__ band,
                                                 const int* __restrict__ band_n,
                                                 const int* __restrict__ flags, int k,
-                                                int64_t row_base, float* __restrict__ out_s,
+                                                int64_t row_base,
+                                                const float* __restrict__ cut,
+                                                float* __restrict__ out_s,
                                                 int64_t* __restrict__ out_i) {
   __shared__ uint64_t buf[BAND_CAP];
   __shared__ __attribute__((aligned(16))) float qs[EP];
+  __shared__ int nkeep;
   const int qid = blockIdx.x;
   if (flags[qid]) return;  // served by the exact fallback
-  const int nb = band_n[qid];
+  int nb = band_n[qid];
+  const uint64_t* qband = band + (int64_t)qid * BAND_CAP;
   for (int i = threadIdx.x; i < EP; i += blockDim.x) qs[i] = q[(int64_t)qid * ldq + i];
+  if (cut) {  // sharded: keep band rows with a >= cut[q] (unordered; sorted below)
+    const float c = cut[qid];
+    if (threadIdx.x == 0) nkeep = 0;
+    __syncthreads();
+    for (int e = threadIdx.x; e < nb; e += blockDim.x) {
+      const uint64_t key = qband[e];
+      if (key_float((uint32_t)(key >> 32)) >= c) buf[atomicAdd(&nkeep, 1)] = key;
+    }
+    __syncthreads();
+    nb = nkeep;
+    qband = buf;
+  }
   __syncthreads();
   for (int e = threadIdx.x; e < nb; e += blockDim.x) {
-    const uint32_t r = key_row(band[(int64_t)qid * BAND_CAP + e]);
+    const uint32_t r = key_row(qband[e]);
     const f32x4* xr = (const f32x4*)(db + (int64_t)r * ld);
     float acc = 0.0f;
 #pragma unroll 4
@@ -1046,7 +1104,7 @@ struct FilterWs {
   float* theta;
   float* aref;
   float* eps2;
-  int* gcount;
+  float* cut;
   uint64_t* band;
   int* band_n;
   int* flags;  // flags[nq], qsel[nq], qsel_n[1] are contiguous (one memset)
@@ -1074,7 +1132,7 @@ static FilterWs carve(void* base, const FilterPlan& p, int64_t n, int d, int nq,
   w.theta = (float*)take((int64_t)nq * 4);
   w.aref = (float*)take((int64_t)nq * 4);
   w.eps2 = (float*)take((int64_t)nq * 4);
-  w.gcount = (int*)take((int64_t)nq * 4);
+  w.cut = (float*)take((int64_t)nq * 4);
   w.band = (uint64_t*)take((int64_t)nq * BAND_CAP * 8);
   w.band_n = (int*)take((int64_t)nq * 4);
   int* fl = (int*)take(((int64_t)2 * nq + 1) * 4);
@@ -1168,8 +1226,7 @@ int filter_init(const FilterWs& w, const float* q, int nq, int64_t ld_q, int ep,
                 float x_resid_max, hipStream_t st) {
   TT_REQUIRE(x_norm_max >= 0.0f && x_resid_max >= 0.0f,
              "x_norm_max / x_resid_max must be >= 0 (tt_bf16_image_bounds)");
-  if (hipMemsetAsync(w.flags, 0, ((size_t)2 * nq + 1) * 4, st) != hipSuccess ||
-      hipMemsetAsync(w.gcount, 0, (size_t)nq * 4, st) != hipSuccess)
+  if (hipMemsetAsync(w.flags, 0, ((size_t)2 * nq + 1) * 4, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "hipMemsetAsync(flags)");
   const unsigned fill_grid = (unsigned)((nq + 255) / 256);
   hipLaunchKernelGGL(k_fill_f32, dim3(fill_grid), dim3(256), 0, st, w.theta, nq,
@@ -1192,7 +1249,8 @@ int filter_init(const FilterWs& w, const float* q, int nq, int64_t ld_q, int ep,
 // level li (+ its selection in `mode`); events around the full-catalog level
 int filter_level(const FilterPlan& p, const FilterWs& w, int li, int mode, const uint16_t* db16,
                  int64_t n, int64_t ld_db, const float* q, int nq, int64_t ld_q, int k, int ep,
-                 hipStream_t st, void* ev_start, void* ev_stop) {
+                 hipStream_t st, void* ev_start, void* ev_stop, const float* stats = nullptr,
+                 int* pcount = nullptr, float* smax_out = nullptr) {
   const Level& L = p.lv[li];
   const bool last = li == p.n_levels - 1;
   if (last && ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
@@ -1212,7 +1270,7 @@ int filter_level(const FilterPlan& p, const FilterWs& w, int li, int mode, const
     return fail(TT_ERR_LAUNCH, "hipEventRecord(stop)");
   hipLaunchKernelGGL(k_select_wave, dim3((nq + 3) / 4), dim3(256), 0, st, w.lists, w.counts,
                      L.n_slabs, k, p.J, w.eps2, mode, w.theta, w.aref, w.band, w.band_n, w.flags,
-                     w.qsel, w.qsel_n, nq, w.gcount);
+                     w.qsel, w.qsel_n, nq, stats, pcount, smax_out);
   return check_launch("k_select_wave");
 }
 
@@ -1228,13 +1286,14 @@ int full_threshold(const FilterWs& w, int nq, hipStream_t st) {
 
 int filter_finish(const FilterWs& w, const float* db, int64_t n, int32_t d, int64_t ld_db,
                   int64_t row_base, const float* q, int nq, int64_t ld_q, int k, int ep,
-                  float* out_score, int64_t* out_idx, hipStream_t st) {
+                  float* out_score, int64_t* out_idx, hipStream_t st,
+                  const float* cut = nullptr) {
   TT_REQUIRE(db != nullptr && out_score && out_idx, "null pointer");
   switch (ep) {
 #define TT_RR(E)                                                                              \
   case E:                                                                                     \
     hipLaunchKernelGGL(k_rerank<E>, dim3(nq), dim3(256), 0, st, db, ld_db, q, ld_q, w.band,   \
-                       w.band_n, w.flags, k, row_base, out_score, out_idx);                   \
+                       w.band_n, w.flags, k, row_base, cut, out_score, out_idx);              \
     break;
     TT_RR(64) TT_RR(128) TT_RR(256) TT_RR(384) TT_RR(512) TT_RR(768)
 #undef TT_RR
@@ -1274,76 +1333,142 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
 }
 
 // ------------------------------------------------------------------ sharded (multi-GPU)
-extern "C" int tt_sharded_filter_begin(const uint16_t* db_bf16, int64_t n, int32_t d,
-                                       int64_t ld_db, const float* q, int32_t nq, int64_t ld_q,
-                                       int32_t k, float x_norm_max, float x_resid_max,
-                                       void* workspace, int64_t workspace_bytes, void* stream,
-                                       int64_t* theta_offset) {
-  TT_REQUIRE(theta_offset != nullptr, "theta_offset == NULL");
+namespace {
+// the full level of a shard as a one-level plan: stride 1, dense when the shard is small
+FilterPlan plan_full(int64_t n, int nq, int k, int ep) {
+  FilterPlan p = plan_filter(n, nq, k, ep);
+  const Level last = p.lv[p.n_levels - 1];
+  p.n_levels = 1;
+  p.lv[0] = last;
+  p.max_slabs = last.n_slabs;
+  return p;
+}
+
+__global__ void k_pack_stats(const float* __restrict__ theta, const float* __restrict__ smax,
+                             int nq, float* __restrict__ stats) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nq) {
+    stats[2 * i] = theta[i];
+    stats[2 * i + 1] = smax[i];
+  }
+}
+
+// full-level threshold from the exchanged sample statistic: aref = theta_g, theta = theta_g - eps2
+__global__ void k_stats_theta(const float* __restrict__ stats, const float* __restrict__ eps2,
+                              int nq, float* __restrict__ aref, float* __restrict__ theta) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nq) {
+    aref[i] = stats[2 * i];
+    theta[i] = stats[2 * i] - eps2[i];
+  }
+}
+
+int sharded_setup(const float* db, const uint16_t* db_bf16, int64_t n, int32_t d, int64_t ld_db,
+                  const float* q, int32_t nq, int64_t ld_q, int32_t k, void* workspace,
+                  int64_t workspace_bytes, int* ep, FilterPlan* p, FilterWs* w) {
+  int rc = filter_setup(db, db_bf16, n, d, ld_db, q, nq, ld_q, k, workspace, workspace_bytes, ep,
+                        p, w);
+  if (rc) return rc;
+  *p = plan_full(n, nq, k, *ep);
+  *w = carve(workspace, *p, n, d, nq, k);
+  if (workspace_bytes < w->total) return fail(TT_ERR_WORKSPACE, "sharded filter: workspace too small");
+  return TT_OK;
+}
+}  // namespace
+
+extern "C" int tt_sharded_workspace_bytes(int64_t n, int32_t d, int32_t nq, int32_t k,
+                                          int64_t* bytes) {
+  TT_REQUIRE(bytes != nullptr, "bytes == NULL");
+  TT_REQUIRE(n >= 1 && nq >= 1 && k >= 1, "n, nq, k must be >= 1");
+  const int ep = tt_padded_dim(d);
+  TT_REQUIRE(ep > 0, "d > 768");
+  *bytes = carve(nullptr, plan_full(n, nq, k, ep), n, d, nq, k).total;
+  return TT_OK;
+}
+
+extern "C" int tt_sharded_fallback_offset(int64_t n, int32_t d, int32_t nq, int32_t k,
+                                          int64_t* offset) {
+  TT_REQUIRE(offset != nullptr && n >= 1 && nq >= 1 && k >= 1, "bad arguments");
+  const int ep = tt_padded_dim(d);
+  TT_REQUIRE(ep > 0, "d > 768");
+  const FilterWs w = carve(nullptr, plan_full(n, nq, k, ep), n, d, nq, k);
+  *offset = (int64_t)((char*)w.qsel_n - (char*)4096);
+  return TT_OK;
+}
+
+extern "C" int tt_sharded_filter_begin(const uint16_t* sample_bf16, int64_t n_sample, int32_t d,
+                                       int64_t ld, const float* q, int32_t nq, int64_t ld_q,
+                                       int32_t k, float* stats, void* workspace,
+                                       int64_t workspace_bytes, void* stream) {
+  TT_REQUIRE(stats != nullptr, "stats == NULL");
+  TT_REQUIRE(nq >= 0, "nq < 0");
+  if (nq == 0) return TT_OK;
   int ep;
   FilterPlan p;
   FilterWs w;
-  int rc = filter_setup(nullptr, db_bf16, n, d, ld_db, q, nq, ld_q, k, workspace, workspace_bytes,
-                        &ep, &p, &w);
+  // the sample may hold fewer than k rows: plan with k' = min(k, n_sample), J from k
+  const int32_t kk = (int64_t)k > n_sample ? (int32_t)n_sample : k;
+  TT_REQUIRE(k >= 1 && k <= FL_KMAX, "need 1 <= k <= 128");
+  int rc = filter_setup(nullptr, sample_bf16, n_sample, d, ld, q, nq, ld_q, kk, workspace,
+                        workspace_bytes, &ep, &p, &w);
   if (rc) return rc;
+  p = plan_filter(n_sample, nq, k, ep);  // same J as the single-catalog call for this k
   hipStream_t st = (hipStream_t)stream;
-  if ((rc = filter_init(w, q, nq, ld_q, ep, x_norm_max, x_resid_max, st))) return rc;
-  for (int li = 0; li + 1 < p.n_levels; ++li)
-    if ((rc = filter_level(p, w, li, 0, db_bf16, n, ld_db, q, nq, ld_q, k, ep, st, nullptr,
-                           nullptr)))
+  if ((rc = filter_init(w, q, nq, ld_q, ep, 0.0f, 0.0f, st))) return rc;
+  for (int li = 0; li < p.n_levels; ++li) {
+    const bool last = li == p.n_levels - 1;
+    if ((rc = filter_level(p, w, li, 0, sample_bf16, n_sample, ld, q, nq, ld_q, k, ep, st, nullptr,
+                           nullptr, nullptr, nullptr, last ? w.cut : nullptr)))
       return rc;
-  *theta_offset = (int64_t)((char*)w.theta - (char*)workspace);
-  return TT_OK;
+  }
+  hipLaunchKernelGGL(k_pack_stats, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, w.theta,
+                     w.cut, nq, stats);
+  return check_launch("k_pack_stats");
 }
 
 extern "C" int tt_sharded_filter_full(const uint16_t* db_bf16, int64_t n, int32_t d,
                                       int64_t ld_db, const float* q, int32_t nq, int64_t ld_q,
-                                      int32_t k, void* workspace, int64_t workspace_bytes,
-                                      void* stream, void* ev_start, void* ev_stop,
-                                      int64_t* count_offset) {
-  TT_REQUIRE(count_offset != nullptr, "count_offset == NULL");
+                                      int32_t k, float x_norm_max, float x_resid_max,
+                                      const float* stats, int32_t* probe_counts, void* workspace,
+                                      int64_t workspace_bytes, void* stream, void* ev_start,
+                                      void* ev_stop) {
+  TT_REQUIRE(stats != nullptr && probe_counts != nullptr, "null pointer");
+  TT_REQUIRE(nq >= 0, "nq < 0");
+  if (nq == 0) return TT_OK;
   int ep;
   FilterPlan p;
   FilterWs w;
-  int rc = filter_setup(nullptr, db_bf16, n, d, ld_db, q, nq, ld_q, k, workspace, workspace_bytes,
-                        &ep, &p, &w);
+  int rc = sharded_setup(nullptr, db_bf16, n, d, ld_db, q, nq, ld_q, k, workspace, workspace_bytes,
+                         &ep, &p, &w);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
-  const int li = p.n_levels - 1;
-  if (li == 0) {
-    // a shard of <= 2048 rows has no sample level: exact local top-k (mode 1) and a count
-    // that always certifies
-    if ((rc = filter_level(p, w, li, 1, db_bf16, n, ld_db, q, nq, ld_q, k, ep, st, ev_start,
-                           ev_stop)))
-      return rc;
-    hipLaunchKernelGGL(k_fill_i32, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, w.gcount,
-                       nq, 0x3fffffff);
-  } else {
-    if ((rc = full_threshold(w, nq, st))) return rc;
-    if ((rc = filter_level(p, w, li, 2, db_bf16, n, ld_db, q, nq, ld_q, k, ep, st, ev_start,
-                           ev_stop)))
-      return rc;
-  }
-  *count_offset = (int64_t)((char*)w.gcount - (char*)workspace);
-  return check_launch("tt_sharded_filter_full");
+  if ((rc = filter_init(w, q, nq, ld_q, ep, x_norm_max, x_resid_max, st))) return rc;
+  hipLaunchKernelGGL(k_stats_theta, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, stats,
+                     w.eps2, nq, w.aref, w.theta);
+  if ((rc = check_launch("k_stats_theta"))) return rc;
+  return filter_level(p, w, 0, 2, db_bf16, n, ld_db, q, nq, ld_q, k, ep, st, ev_start, ev_stop,
+                      stats, probe_counts, nullptr);
 }
 
 extern "C" int tt_sharded_filter_finish(const float* db, const uint16_t* db_bf16, int64_t n,
                                         int32_t d, int64_t ld_db, int64_t row_base,
                                         const float* q, int32_t nq, int64_t ld_q, int32_t k,
+                                        const float* stats, const int32_t* probe_counts,
                                         float* out_score, int64_t* out_idx, void* workspace,
                                         int64_t workspace_bytes, void* stream) {
+  TT_REQUIRE(stats != nullptr && probe_counts != nullptr, "null pointer");
+  TT_REQUIRE(nq >= 0, "nq < 0");
+  if (nq == 0) return TT_OK;
   int ep;
   FilterPlan p;
   FilterWs w;
-  int rc = filter_setup(db, db_bf16, n, d, ld_db, q, nq, ld_q, k, workspace, workspace_bytes, &ep,
-                        &p, &w);
+  int rc = sharded_setup(db, db_bf16, n, d, ld_db, q, nq, ld_q, k, workspace, workspace_bytes,
+                         &ep, &p, &w);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
-  if (p.n_levels > 1) {
-    hipLaunchKernelGGL(k_flag_by_count, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st,
-                       w.gcount, nq, k, w.flags, w.qsel, w.qsel_n);
-    if ((rc = check_launch("k_flag_by_count"))) return rc;
-  }
-  return filter_finish(w, db, n, d, ld_db, row_base, q, nq, ld_q, k, ep, out_score, out_idx, st);
+  hipLaunchKernelGGL(k_probe_cut, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st,
+                     probe_counts, stats, w.eps2, nq, k, w.flags, w.qsel, w.qsel_n, w.cut);
+  if ((rc = check_launch("k_probe_cut"))) return rc;
+  return filter_finish(w, db, n, d, ld_db, row_base, q, nq, ld_q, k, ep, out_score, out_idx, st,
+                       w.cut);
 }

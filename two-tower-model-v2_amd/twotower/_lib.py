@@ -19,6 +19,8 @@ LIB_PATH = os.environ.get("TWOTOWER_HIP_LIB") or os.path.join(_PKG_ROOT, "lib", 
 CSRC = os.path.join(_PKG_ROOT, "csrc")
 
 TT_OK = 0
+TT_SHARD_PROBES = 16  # include/twotower_hip.h
+TT_SHARD_SAMPLE_STRIDE = 16
 TT_NORM_ADD_EPS = 0
 TT_NORM_MAX_EPS = 1
 
@@ -69,13 +71,15 @@ SIGNATURES = {
     "tt_scan_topk_bf16f32": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _i64, _vp, _i32, _i64,
                                             _i32, ctypes.c_float, ctypes.c_float, _vp, _vp, _vp,
                                             _i64, _vp, _vp, _vp]),
-    "tt_sharded_filter_begin": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _i64, _i32,
-                                               ctypes.c_float, ctypes.c_float, _vp, _i64, _vp,
-                                               ctypes.POINTER(_i64)]),
-    "tt_sharded_filter_full": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _i64, _i32, _vp,
-                                              _i64, _vp, _vp, _vp, ctypes.POINTER(_i64)]),
+    "tt_sharded_workspace_bytes": (ctypes.c_int, [_i64, _i32, _i32, _i32, ctypes.POINTER(_i64)]),
+    "tt_sharded_fallback_offset": (ctypes.c_int, [_i64, _i32, _i32, _i32, ctypes.POINTER(_i64)]),
+    "tt_sharded_filter_begin": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _i64, _i32, _vp,
+                                               _vp, _i64, _vp]),
+    "tt_sharded_filter_full": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _i64, _i32,
+                                              ctypes.c_float, ctypes.c_float, _vp, _vp, _vp, _i64,
+                                              _vp, _vp, _vp]),
     "tt_sharded_filter_finish": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _i64, _vp, _i32,
-                                                _i64, _i32, _vp, _vp, _vp, _i64, _vp]),
+                                                _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "tt_bf16_image_bounds": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _vp, _vp]),
     "tt_topk_merge_f32": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp]),
     "tt_weighted_avg_l2_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _i64, _vp]),

@@ -104,12 +104,13 @@ def filter_workspace_bytes(n: int, d: int, nq: int, k: int) -> int:
     return b.value
 
 
-def filter_fallback_count(workspace: torch.Tensor, n: int, d: int, nq: int, k: int) -> int:
-    """Queries of the last scan_topk_bf16 call (with this workspace) that took the exact
-    fallback.  Diagnostic: synchronises."""
+def filter_fallback_count(workspace: torch.Tensor, n: int, d: int, nq: int, k: int,
+                          sharded: bool = False) -> int:
+    """Queries of the last scan_topk_bf16 (sharded=True: sharded_search) call with this
+    workspace that took the exact fallback.  Diagnostic: synchronises."""
     off = ctypes.c_int64(0)
-    check(lib().tt_filter_fallback_offset(n, d, nq, k, ctypes.byref(off)),
-          "tt_filter_fallback_offset")
+    fn = lib().tt_sharded_fallback_offset if sharded else lib().tt_filter_fallback_offset
+    check(fn(n, d, nq, k, ctypes.byref(off)), "fallback_offset")
     return int(workspace[off.value:off.value + 4].view(torch.int32).item())
 
 
@@ -145,47 +146,81 @@ def scan_topk_bf16(db: torch.Tensor, db16: torch.Tensor, n: int, d: int, q: torc
     return out
 
 
-def scan_topk_bf16_sharded(db: torch.Tensor, db16: torch.Tensor, n: int, d: int,
-                           q: torch.Tensor, k: int, bounds, row_base: int, allreduce_max,
-                           allreduce_sum, workspace: torch.Tensor = None, out=None,
-                           events=(None, None)):
-    """This shard's part of the GLOBAL exact top-k (tt_sharded_filter_*, include/twotower_hip.h).
+def sharded_sample(x16: torch.Tensor, n: int) -> torch.Tensor:
+    """Rows 0, 16, 32, ... of a bf16 catalog image (the replicated sample of the sharded search)."""
+    return x16[:n:_lib.TT_SHARD_SAMPLE_STRIDE].contiguous()
 
-    allreduce_max(t) / allreduce_sum(t) reduce a device tensor in place over the shards
-    (e.g. torch.distributed.all_reduce with ReduceOp.MAX / SUM); every shard passes the same
-    queries.  Merge the shards' outputs with merge_topk."""
+
+def sharded_begin(sample16: torch.Tensor, d: int, q: torch.Tensor, k: int, stats=None,
+                  workspace: torch.Tensor = None) -> torch.Tensor:
+    """Stage 1 of the row-sharded search (tt_sharded_filter_begin): this rank's queries
+    against the global catalog sample -> stats [nq, 2] f32 (threshold, probe top)."""
+    _check_2d(sample16, "sample16", torch.bfloat16)
+    _check_2d(q, "q")
+    nq, ns = q.shape[0], sample16.shape[0]
+    if stats is None:
+        stats = torch.empty((nq, 2), dtype=_f32, device=q.device)
+    if nq == 0:
+        return stats
+    need = filter_workspace_bytes(ns, d, nq, min(k, ns))
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=q.device)
+    check(lib().tt_sharded_filter_begin(_ptr(sample16), ns, d, sample16.stride(0), _ptr(q), nq,
+                                        q.stride(0), k, _ptr(stats), _ptr(workspace),
+                                        workspace.numel(), stream_ptr()),
+          "tt_sharded_filter_begin")
+    return stats
+
+
+def sharded_workspace_bytes(n: int, d: int, nq: int, k: int) -> int:
+    v = ctypes.c_int64(0)
+    check(lib().tt_sharded_workspace_bytes(n, d, nq, k, ctypes.byref(v)),
+          "tt_sharded_workspace_bytes")
+    return v.value
+
+
+def sharded_search(db: torch.Tensor, db16: torch.Tensor, n: int, d: int, q: torch.Tensor, k: int,
+                   bounds, row_base: int, stats: torch.Tensor, allreduce_sum,
+                   workspace: torch.Tensor = None, out=None, pcount: torch.Tensor = None,
+                   events=(None, None)):
+    """Stages 2-3 of the row-sharded search (tt_sharded_filter_full / _finish): all ranks'
+    queries q [nq, ep] and their gathered stats [nq, 2] against this rank's shard; between the
+    stages allreduce_sum(t) sums the probe counts [nq, 16] int32 over ranks in place.
+    Returns this shard's part of the global top-k; merge the ranks' parts with merge_topk.
+    bounds must hold for the whole catalog (MAX over the shards)."""
     _check_2d(db, "db")
     _check_2d(db16, "db16", torch.bfloat16)
     _check_2d(q, "q")
     nq = q.shape[0]
     if not (1 <= k <= min(n, FILTER_KMAX)) or n > db.shape[0]:
-        raise ValueError(f"scan_topk_bf16_sharded: need 1 <= k ({k}) <= min(n, 128)")
+        raise ValueError(f"sharded_search: need 1 <= k ({k}) <= min(n, 128)")
+    if tuple(stats.shape) != (nq, 2) or stats.dtype != _f32 or not stats.is_contiguous():
+        raise ValueError("sharded_search: stats must be contiguous float32 [nq, 2]")
     if out is None:
         out = (torch.empty((nq, k), dtype=_f32, device=q.device),
                torch.empty((nq, k), dtype=torch.int64, device=q.device))
     if nq == 0:
         return out
-    need = filter_workspace_bytes(n, d, nq, k)
+    need = sharded_workspace_bytes(n, d, nq, k)
     if workspace is None or workspace.numel() < need:
         workspace = torch.empty(need, dtype=torch.uint8, device=q.device)
+    if pcount is None or pcount.numel() < nq * _lib.TT_SHARD_PROBES:
+        pcount = torch.empty((nq, _lib.TT_SHARD_PROBES), dtype=torch.int32, device=q.device)
+    pcount = pcount.view(-1)[: nq * _lib.TT_SHARD_PROBES]
     x_norm_max, x_resid_max = (float(v) for v in bounds)
     L, st = lib(), stream_ptr()
-    off = ctypes.c_int64(0)
-    check(L.tt_sharded_filter_begin(_ptr(db16), n, d, db16.stride(0), _ptr(q), nq, q.stride(0), k,
-                                    ctypes.c_float(x_norm_max), ctypes.c_float(x_resid_max),
-                                    _ptr(workspace), workspace.numel(), st, ctypes.byref(off)),
-          "tt_sharded_filter_begin")
-    allreduce_max(workspace[off.value:off.value + 4 * nq].view(_f32))
     e0, e1 = events
     check(L.tt_sharded_filter_full(_ptr(db16), n, d, db16.stride(0), _ptr(q), nq, q.stride(0), k,
-                                   _ptr(workspace), workspace.numel(), st,
-                                   e0.cuda_event if e0 is not None else None,
-                                   e1.cuda_event if e1 is not None else None, ctypes.byref(off)),
+                                   ctypes.c_float(x_norm_max), ctypes.c_float(x_resid_max),
+                                   _ptr(stats), _ptr(pcount), _ptr(workspace), workspace.numel(),
+                                   st, e0.cuda_event if e0 is not None else None,
+                                   e1.cuda_event if e1 is not None else None),
           "tt_sharded_filter_full")
-    allreduce_sum(workspace[off.value:off.value + 4 * nq].view(torch.int32))
+    allreduce_sum(pcount)
     check(L.tt_sharded_filter_finish(_ptr(db), _ptr(db16), n, d, db.stride(0), row_base, _ptr(q),
-                                     nq, q.stride(0), k, _ptr(out[0]), _ptr(out[1]),
-                                     _ptr(workspace), workspace.numel(), st),
+                                     nq, q.stride(0), k, _ptr(stats), _ptr(pcount),
+                                     out[0].data_ptr(), out[1].data_ptr(), _ptr(workspace),
+                                     workspace.numel(), st),
           "tt_sharded_filter_finish")
     return out
 

@@ -9,6 +9,12 @@ catalog is split contiguously over the W ranks of a process group (rank r owns g
   3. all-to-all: the block of B rows for rank j goes back to rank j  -> [W, B, k]
   4. merge the W sorted lists (tt_topk_merge_f32)    [B, k]
 
+With the bf16 filter (k <= 128) step 2 is the staged protocol of include/twotower_hip.h
+(tt_sharded_filter_*): each rank first derives its own queries' thresholds from a replicated
+1/16 sample of the whole catalog (stats [B, 2], all-gathered with the queries), and one
+all-reduce SUM of per-query probe counts [W*B, 16] int32 between the filter and the re-rank
+lets every shard re-rank only rows that can reach the GLOBAL top-k.
+
 A score does not depend on the shard, and the merge order is the scan's (score desc, lower
 global row first), so the result is bit-identical to a single-GPU search of the whole
 catalog.  ``TopkExchange`` is the collective part; the local search and the merge are passed
@@ -40,12 +46,15 @@ class TopkExchange:
 
     Buffers are allocated once (no allocation inside a step)."""
 
-    def __init__(self, b_local: int, width: int, k: int, device=None, group=None):
+    def __init__(self, b_local: int, width: int, k: int, device=None, group=None,
+                 aux_width: int = 0):
         self.group = group
         self.rank, self.world = _world(group)
         self.b, self.k = int(b_local), int(k)
         dev = device if device is not None else "cpu"
         self.qall = torch.empty((self.world * self.b, width), dtype=torch.float32, device=dev)
+        self.aux_all = (torch.empty((self.world * self.b, aux_width), dtype=torch.float32,
+                                    device=dev) if aux_width else None)
         self.s_recv = torch.empty((self.world, self.b, self.k), dtype=torch.float32, device=dev)
         self.i_recv = torch.empty((self.world, self.b, self.k), dtype=torch.int64, device=dev)
 
@@ -65,11 +74,23 @@ class TopkExchange:
                                i_shard.contiguous(), group=self.group)
         return self.s_recv, self.i_recv
 
-    def search(self, q: Tensor, local_search: Callable[[Tensor], Tuple[Tensor, Tensor]],
-               merge: Callable[[Tensor, Tensor, int], Tuple[Tensor, Tensor]]):
-        """q: my B queries -> (scores [B, k], global ids [B, k]) over the whole catalog."""
+    def gather_aux(self, aux: Tensor) -> Tensor:
+        """Per-query side data [B, aux_width] f32 (the sharded filter's stats), same order."""
+        if self.world == 1:
+            return aux
+        dist.all_gather_into_tensor(self.aux_all, aux.contiguous(), group=self.group)
+        return self.aux_all
+
+    def search(self, q: Tensor, local_search: Callable[..., Tuple[Tensor, Tensor]],
+               merge: Callable[[Tensor, Tensor, int], Tuple[Tensor, Tensor]],
+               aux: Optional[Tensor] = None):
+        """q: my B queries -> (scores [B, k], global ids [B, k]) over the whole catalog.
+        With aux [B, a]: local_search(qall, aux_all) gets every rank's aux rows too."""
         qall = self.gather_queries(q)
-        s, i = local_search(qall)
+        if aux is not None:
+            s, i = local_search(qall, self.gather_aux(aux))
+        else:
+            s, i = local_search(qall)
         if self.world == 1:
             return s, i
         s_recv, i_recv = self.return_results(s, i)
@@ -97,7 +118,8 @@ def sharded_search(q: Tensor, k: int, local_search, merge, group=None):
 class ShardedFlatIP:
     """Rank-local shard of a row-sharded catalog, searched by the HIP kernels.
 
-    ``add_shard`` takes this rank's rows (already normalised, like FlatIPIndex.add);
+    ``add_shard`` takes this rank's rows (already normalised, like FlatIPIndex.add) and builds
+    the replicated catalog sample + whole-catalog bf16 bounds (collectives, once);
     ``search`` takes this rank's queries ([B, ep] device rows) and returns the global top-k.
     """
 
@@ -110,18 +132,76 @@ class ShardedFlatIP:
         self.lo, self.hi = shard_range(self.n_global, self.rank, self.world)
         self.index = FlatIPIndex(d, device=device, row_base=self.lo)
         self._ex: Optional[TopkExchange] = None
+        self.sample16: Optional[Tensor] = None
+        self.bounds = (0.0, 0.0)
+        self._ws_begin: Optional[Tensor] = None
 
     def add_shard(self, x) -> None:
         if x.shape[0] != self.hi - self.lo:
             raise ValueError(f"rank {self.rank} owns {self.hi - self.lo} rows, got {x.shape[0]}")
         self.index.add(x)
+        if self.world > 1:
+            self._build_sample()
+
+    def _build_sample(self) -> None:
+        """Global rows 0, 16, 32, ... of the bf16 image on every rank (all-gather, padded to
+        the largest rank's count) and the bounds MAX over ranks."""
+        from . import _lib
+
+        st = _lib.TT_SHARD_SAMPLE_STRIDE
+        ix = self.index
+        mine = ix.xb16[(-self.lo) % st: ix.ntotal: st]
+        cnt = torch.tensor([mine.shape[0]], dtype=torch.int64, device=ix.device)
+        cnts = [torch.zeros_like(cnt) for _ in range(self.world)]
+        dist.all_gather(cnts, cnt, group=self.group)
+        cnts = [int(c.item()) for c in cnts]
+        cmax = max(cnts)
+        pad = torch.zeros((cmax, ix.ep), dtype=torch.bfloat16, device=ix.device)
+        pad[: mine.shape[0]] = mine
+        allp = torch.empty((self.world * cmax, ix.ep), dtype=torch.bfloat16, device=ix.device)
+        dist.all_gather_into_tensor(allp.view(torch.int16), pad.view(torch.int16),
+                                    group=self.group)
+        self.sample16 = torch.cat([allp[r * cmax: r * cmax + c] for r, c in enumerate(cnts)])
+        b = torch.tensor(ix.bounds, dtype=torch.float32, device=ix.device)
+        dist.all_reduce(b, op=dist.ReduceOp.MAX, group=self.group)
+        self.bounds = tuple(b.tolist())
+
+    def _staged(self, k: int, method: str) -> bool:
+        """Every rank takes the same branch: decided from (n_global, world, k, method) only."""
+        smallest = self.n_global // self.world
+        return (self.world > 1 and method in ("auto", "bf16") and 1 <= k <= 128
+                and smallest >= k)
 
     def search(self, q: Tensor, k: int, method: str = "auto"):
         from . import kernels
 
-        if self._ex is None or self._ex.b != q.shape[0] or self._ex.k != k:
-            self._ex = TopkExchange(q.shape[0], q.shape[1], k, device=q.device, group=self.group)
+        staged = self._staged(k, method)
+        if (self._ex is None or self._ex.b != q.shape[0] or self._ex.k != k
+                or (self._ex.aux_all is None) == staged):
+            self._ex = TopkExchange(q.shape[0], q.shape[1], k, device=q.device, group=self.group,
+                                    aux_width=2 if staged else 0)
+        if staged:
+            ix = self.index
+            need = kernels.filter_workspace_bytes(self.sample16.shape[0], ix.d, q.shape[0],
+                                                  min(k, self.sample16.shape[0]))
+            if self._ws_begin is None or self._ws_begin.numel() < need:
+                self._ws_begin = torch.empty(need, dtype=torch.uint8, device=ix.device)
+            stats = kernels.sharded_begin(self.sample16, ix.d, q, k, workspace=self._ws_begin)
+            return self._ex.search(q, lambda qa, sa: self._local_staged(qa, sa, k),
+                                   kernels.merge_topk, aux=stats)
         return self._ex.search(q, lambda qa: self._local(qa, k, method), kernels.merge_topk)
+
+    def _local_staged(self, qa: Tensor, stats: Tensor, k: int):
+        from . import kernels
+
+        ix = self.index
+        need = kernels.sharded_workspace_bytes(ix.ntotal, ix.d, qa.shape[0], k)
+        if ix._ws is None or ix._ws.numel() < need:
+            ix._ws = torch.empty(need, dtype=torch.uint8, device=ix.device)
+        g = self.group
+        return kernels.sharded_search(
+            ix.xb, ix.xb16, ix.ntotal, ix.d, qa, k, self.bounds, ix.row_base, stats,
+            lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=g), workspace=ix._ws)
 
     def _local(self, qa: Tensor, k: int, method: str):
         """Local top-k with global ids; a shard smaller than k pads with (-inf, -1)."""
