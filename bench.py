@@ -48,6 +48,8 @@ def parse():
     p.add_argument("--hist", type=int, default=20)
     p.add_argument("--k", type=int, default=100)
     p.add_argument("--dim", type=int, default=384)
+    p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                   help="gloo: rehearse N ranks on one GPU (functional check, not a measurement)")
     p.add_argument("--method", choices=["bf16", "f32"], default="bf16",
                    help="bf16: bf16 MFMA filter + exact f32 re-rank; f32: exact f32 MFMA scan "
                         "(identical results)")
@@ -153,10 +155,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", 0))
     if a.gpus != world:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    if a.backend == "gloo":  # rehearsal: ranks may share the visible GPU(s)
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     N, E, B, S, K = a.catalog, a.dim, a.buyers, a.hist, a.k
     ep = _lib.padded_dim(E)
@@ -281,7 +288,7 @@ def main():
     peak = BF16_MFMA_PEAK_TFLOPS if a.method == "bf16" else F32_MFMA_PEAK_TFLOPS
     traffic = None
     tj = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tj):
+    if os.path.exists(tj) and world == 1:  # PMC pass is of the 1-GPU launch shape
         tk = json.load(open(tj)).get("kernels", {}).get(kname)
         if tk and tk.get("config", "").startswith(f"{N // 1000000}M x {E}"):
             traffic = tk["fetch_bytes"] + tk["write_bytes"]
@@ -302,7 +309,8 @@ def main():
             "workload": "configs[2]: 1M x 384 catalog, 10k buyers/rank x 20 events, weighted-avg, "
                         "Mode B (history rows gathered), k=100",
             "catalog_rows": N, "dim": E, "buyers_per_rank": B, "history": S, "k": K,
-            "parallelism": f"catalog row-shard x{world}" + (" + RCCL all-gather(queries), all-reduce(threshold, counts), all-to-all(top-k)" if world > 1 else ""),
+            "backend": a.backend if world > 1 else None,
+            "parallelism": f"catalog row-shard x{world}" + ((" + RCCL all-gather(queries, filter stats), all-reduce(probe counts), all-to-all(top-k)" if staged else " + RCCL all-gather(queries), all-to-all(top-k)") if world > 1 else ""),
         },
         "roofline": {
             "kernel": kname,

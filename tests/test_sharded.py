@@ -118,3 +118,44 @@ def test_exchange_single_process_is_passthrough():
     q = torch.randn(4, 8)
     s, i = ex.search(q, lambda qa: (qa[:, :3], torch.zeros(4, 3, dtype=torch.int64)), None)
     assert torch.equal(s, q[:, :3])
+
+
+def _aux_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from twotower.sharded import TopkExchange
+
+        B, k = 5, 3
+        q = torch.arange(B * 4, dtype=torch.float32).view(B, 4) + 100 * rank
+        aux = torch.stack([q[:, 0], -q[:, 0]], 1)  # per-query stats travel with the query
+        seen = {}
+
+        def local(qall, aux_all):
+            seen["ok"] = bool(torch.equal(aux_all[:, 0], qall[:, 0])
+                              and torch.equal(aux_all[:, 1], -qall[:, 0]))
+            # the staged filter's probe-count exchange: SUM over ranks in place
+            pc = torch.full((qall.shape[0], 16), rank + 1, dtype=torch.int32)
+            dist.all_reduce(pc, op=dist.ReduceOp.SUM)
+            seen["sum"] = int(pc[0, 0])
+            s = qall[:, :k].clone()
+            i = torch.arange(qall.shape[0] * k, dtype=torch.int64).view(-1, k)
+            return s, i
+
+        ex = TopkExchange(B, 4, k, aux_width=2)
+        ex.search(q, local, lambda s, i, kk: (s[rank], i[rank]), aux=aux)
+        np.save(os.path.join(out_dir, f"aux{rank}.npy"),
+                np.array([seen["ok"], seen["sum"]], dtype=np.int64))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_gathers_aux_rows_with_queries(tmp_path):
+    """The sharded filter's stats [B, 2] are all-gathered in query order next to the queries
+    (TopkExchange aux), and the probe counts SUM over ranks."""
+    world = 3
+    mp.start_processes(_aux_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="fork")
+    for r in range(world):
+        ok, tot = np.load(tmp_path / f"aux{r}.npy")
+        assert ok == 1 and tot == sum(range(1, world + 1))

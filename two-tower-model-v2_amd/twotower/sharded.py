@@ -159,7 +159,7 @@ class ShardedFlatIP:
         pad = torch.zeros((cmax, ix.ep), dtype=torch.bfloat16, device=ix.device)
         pad[: mine.shape[0]] = mine
         allp = torch.empty((self.world * cmax, ix.ep), dtype=torch.bfloat16, device=ix.device)
-        dist.all_gather_into_tensor(allp.view(torch.int16), pad.view(torch.int16),
+        dist.all_gather_into_tensor(allp.view(torch.int32), pad.view(torch.int32),
                                     group=self.group)
         self.sample16 = torch.cat([allp[r * cmax: r * cmax + c] for r, c in enumerate(cnts)])
         b = torch.tensor(ix.bounds, dtype=torch.float32, device=ix.device)
