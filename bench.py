@@ -35,7 +35,6 @@ from twotower.sharded import TopkExchange, shard_range  # noqa: E402
 
 F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X dense f32 MFMA (MI355X_MICROARCH.md)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity)
-I8_MFMA_PEAK_TOPS = 5000.0      # MI355X dense int8 MFMA: 2x bf16 per clock (MI355X_MICROARCH.md)
 HBM_PEAK_GBPS = 8000.0
 
 
@@ -51,7 +50,7 @@ def parse():
     p.add_argument("--dim", type=int, default=384)
     p.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                    help="gloo: rehearse N ranks on one GPU (functional check, not a measurement)")
-    p.add_argument("--method", choices=["bf16", "i8", "f32"], default="bf16",
+    p.add_argument("--method", choices=["bf16", "f32"], default="bf16",
                    help="bf16: bf16 MFMA filter + exact f32 re-rank; f32: exact f32 MFMA scan "
                         "(identical results)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -178,7 +177,6 @@ def main():
     shard16 = torch.empty((hi - lo, ep), device=dev, dtype=torch.bfloat16)
     kernels.l2norm_rows(table[lo:hi], E, _lib.TT_NORM_ADD_EPS, out=shard, out_bf16=shard16)
     bounds = kernels.bf16_image_bounds(shard, shard16, E).tolist()  # build-time statistic
-    img8 = kernels.i8_image(shard, E) if a.method == "i8" else None
     gb = torch.Generator(device=dev).manual_seed(3 + rank)
     hist = torch.randint(0, N, (B, S), generator=gb, device=dev, dtype=torch.int64)
     w = event_mix(gb, (B, S), dev)
@@ -204,7 +202,7 @@ def main():
                                dtype=torch.uint8, device=dev)
         pcount = torch.empty((nq, _lib.TT_SHARD_PROBES), dtype=torch.int32, device=dev)
         ws_bytes = kernels.sharded_workspace_bytes(hi - lo, E, nq, K)
-    elif a.method in ("bf16", "i8"):
+    elif a.method == "bf16":
         ws_bytes = kernels.filter_workspace_bytes(hi - lo, E, nq, K)
     else:
         ws_bytes = kernels.scan_workspace_bytes(hi - lo, E, nq, K)
@@ -224,9 +222,6 @@ def main():
                                    lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM),
                                    workspace=ws, out=(s_shard, i_shard), pcount=pcount,
                                    events=(e0, e1))
-        elif a.method == "i8":
-            kernels.scan_topk_i8(shard, img8, hi - lo, E, qall, K, row_base=lo, workspace=ws,
-                                 out=(s_shard, i_shard), events=(e0, e1))
         elif a.method == "bf16":
             kernels.scan_topk_bf16(shard, shard16, hi - lo, E, qall, K, bounds, row_base=lo,
                                    workspace=ws, out=(s_shard, i_shard), events=(e0, e1))
@@ -277,7 +272,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, scan_ms, search_ms = t.tolist()
     fallback = (kernels.filter_fallback_count(ws, hi - lo, E, nq, K, sharded=staged)
-                if a.method in ("bf16", "i8") else 0)
+                if a.method == "bf16" else 0)
     ms_per_step = dt / a.steps * 1e3
     value = world * B / (dt / a.steps)
 
@@ -286,13 +281,11 @@ def main():
     #   f32:  k_scan_topk_f32 (f32 catalog read once = 4*rows*ep B)
     rows = hi - lo
     flops = 2.0 * nq * rows * E
-    elem = {"bf16": 2.0, "i8": 1.0}.get(a.method, 4.0)
+    elem = 2.0 if a.method == "bf16" else 4.0
     alg_bytes = elem * rows * ep + 4.0 * nq * ep
     achieved_tf = flops / (scan_ms * 1e-3) / 1e12
-    kname = {"bf16": f"k_filter_ring<{ep}, true, false>",
-             "i8": f"k_filter_ring<{ep}, true, true>"}.get(a.method, "k_scan_topk_f32")
-    peak = {"bf16": BF16_MFMA_PEAK_TFLOPS, "i8": I8_MFMA_PEAK_TOPS}.get(a.method,
-                                                                       F32_MFMA_PEAK_TFLOPS)
+    kname = f"k_filter_ring<{ep}, true>" if a.method == "bf16" else "k_scan_topk_f32"
+    peak = BF16_MFMA_PEAK_TFLOPS if a.method == "bf16" else F32_MFMA_PEAK_TFLOPS
     traffic = None
     tj = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tj) and world == 1:  # PMC pass is of the 1-GPU launch shape
@@ -310,8 +303,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": {"bf16": "bf16 filter + f32 exact scores",
-                  "i8": "int8 filter + f32 exact scores"}.get(a.method, "f32"),
+        "dtype": "bf16 filter + f32 exact scores" if a.method == "bf16" else "f32",
         "data": "synthetic (random-normal item embeddings, uniform 20-event histories, event mix 0.75/0.17/0.08)",
         "config": {
             "workload": "configs[2]: 1M x 384 catalog, 10k buyers/rank x 20 events, weighted-avg, "
@@ -325,7 +317,7 @@ def main():
             "bound": "mfma",
             "achieved": achieved_tf,
             "peak": peak,
-            "unit": "TOP/s" if a.method == "i8" else "TFLOP/s",
+            "unit": "TFLOP/s",
             "frac": achieved_tf / peak,
             "traffic": traffic,
             "kernel_ms": scan_ms,

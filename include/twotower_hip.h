@@ -120,30 +120,6 @@ int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n, in
                          void* ev_start, void* ev_stop);
 
 /* ---------------------------------------------------------------------------------
- * int8 filter + exact float32 re-rank: the same contract and results as
- * tt_scan_topk_bf16f32 / tt_scan_topk_f32 (faiss IndexFlatIP.search, vector_db.py:160,197),
- * with the filter on an int8 image of the catalog (v_mfma_i32_16x16x64_i8: twice the bf16
- * MFMA rate, half the image bytes).  Image: x ~ c o n, per-dimension scales c[ep] (0 on
- * padding), n int8 [n, ld_i8] bytes zero padded.  Per query: q' = c o q, t = max|q'|/127,
- * m = rne(q'/t); a(r) = fl(float(n_r . m) * t); |a - s| <= eps_q from the MEASURED bounds
- * X >= max||x||, R >= max||x - c o n||, N >= max||n|| (tt_quantize_i8_rows), so every
- * result stays exact whatever c is.  Needs tt_padded_dim(d) >= 128; k <= 128.
- * Workspace: tt_filter_workspace_bytes.
- * --------------------------------------------------------------------------------- */
-/* out[i] = max(out[i], max_r |x_ri|) for i < d (caller zero-fills out[d] once) */
-int tt_absmax_cols_f32(const float* x, int64_t n, int32_t d, int64_t ld, float* out,
-                       void* stream);
-/* out = rne(x / colscale) clamped to +-127 (0 where colscale == 0 or x is NaN), padding = 0;
- * max-combines out3 = {X, R, N} (caller zero-fills once; NaN rows skipped) */
-int tt_quantize_i8_rows(const float* x, int64_t n, int32_t d, int64_t ld, const float* colscale,
-                        int8_t* out, int64_t ld_out, float* out3, void* stream);
-int tt_scan_topk_i8f32(const float* db, const int8_t* db_i8, int64_t n, int32_t d, int64_t ld_db,
-                       int64_t ld_i8, int64_t row_base, const float* q, int32_t nq, int64_t ld_q,
-                       int32_t k, const float* colscale, float x_norm_max, float x_resid_max,
-                       float n_norm_max, float* out_score, int64_t* out_idx, void* workspace,
-                       int64_t workspace_bytes, void* stream, void* ev_start, void* ev_stop);
-
-/* ---------------------------------------------------------------------------------
  * Row-sharded (multi-GPU) form of tt_scan_topk_bf16f32 (faiss IndexFlatIP.search,
  * vector_db.py:160,197, over a catalog split by rows across ranks).
  * Every rank holds its shard [row_base, row_base + n) in f32 and bf16, plus the GLOBAL

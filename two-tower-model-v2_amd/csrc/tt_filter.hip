@@ -57,26 +57,6 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return (uint32_t)f32_to_bf16_rne(lo) | ((uint32_t)f32_to_bf16_rne(hi) << 16);
 }
 
-typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
-
-// int8 filter (tt_scan_topk_i8f32): a(r) = fl(float(n_r . m_q) * t_q), the i32 dot of the
-// int8 row and query images (exact: |dot| <= 768 * 127^2 < 2^24) times the query scale.
-// fl(d * t) is non-decreasing in the integer d, so "a >= theta" is "dot >= D" with
-// D = min{d : fl(d * t) >= theta}; the filters compare raw i32 accumulators against D.
-// D >= INT_MIN + 1 always, so INT_MIN marks "no row" (placeholders, rows past a slab end).
-__device__ __forceinline__ int i8_threshold(float theta, float tq) {
-  constexpr int LO = -2147483647, HI = 2147483647;
-  if (!(theta == theta) || !(tq == tq)) return HI;  // NaN threshold / NaN query: nothing passes
-  if (tq == 0.0f) return 0.0f >= theta ? LO : HI;   // zero query: every a is 0
-  if (theta == -__builtin_huge_valf()) return LO;
-  const double x = (double)theta / (double)tq;
-  if (x > 3.0e7) return HI;   // above any |dot| (< 2^24)
-  if (x < -3.0e7) return LO;
-  int d = (int)floor(x) - 3;
-  while (!((float)d * tq >= theta)) ++d;  // a few steps: (float)d * tq is within 1 ulp of d*tq
-  return d < LO ? LO : d;
-}
-
 // XCD-aware block id: blocks b and b+8 run on the same XCD (observed placement, speed only).
 // Give every XCD a contiguous range of logical ids so that its co-resident blocks share slabs.
 __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
@@ -84,59 +64,17 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + local;
 }
 
-// 16-B query fragments of k-step s (lane g-group): bf16 packed from the f32 query, or the
-// int8 query image's bytes [64 s + 16 g, +16)
-template <int EP, int KS, bool I8>
-__device__ __forceinline__ void load_query_frags(const void* q, int64_t ldq, int qi, int g,
-                                                 u32x4 (&qf)[KS]) {
-  if constexpr (I8) {
-    const char* qp = (const char*)q + (int64_t)qi * ldq + 16 * g;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) qf[s] = *(const u32x4*)(qp + 64 * s);
-  } else {
-    const float* qp = (const float*)q + (int64_t)qi * ldq + 8 * g;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const f32x4 v0 = *(const f32x4*)(qp + 32 * s);
-      const f32x4 v1 = *(const f32x4*)(qp + 32 * s + 4);
-      qf[s] = u32x4{pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]),
-                    pack_bf16x2(v1[0], v1[1]), pack_bf16x2(v1[2], v1[3])};
-    }
-  }
-}
-
-template <bool I8, typename A4>
-__device__ __forceinline__ A4 mfma_step(const u32x4& a, const u32x4& b, const A4& c) {
-  if constexpr (I8)
-    return __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, a),
-                                                 __builtin_bit_cast(i32x4, b), c, 0, 0, 0);
-  else
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
-                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
-}
-
-template <bool I8, typename V>
-__device__ __forceinline__ float score_of(V v, float tq) {
-  if constexpr (I8) return (float)v * tq;
-  else return v + 0.0f;
-}
-
 // --------------------------------------------------------------------------- filter
 // Block: FL_WAVES waves over the same slab rows; wave w owns QB*16 queries (B fragments of
 // v_mfma_f32_16x16x32_bf16 in VGPRs).  A fragments (16 rows x 32 dims) are streamed straight
 // from HBM: lane l loads 16 B of row (l&15) at dims 32s + 8(l>>4).
-// I8: int8 row / query images (q = the int8 query image, ldq in bytes, tq = query scales),
-// v_mfma_i32_16x16x64_i8; the same 16-B-per-lane fragment loads cover 16 dims instead of 8.
-template <int EP, int QB, bool I8>
+template <int EP, int QB>
 __global__ __launch_bounds__(64 * FL_WAVES, 2) void k_filter_dense(
-    const void* __restrict__ xb, int64_t n, int64_t ld, const void* __restrict__ q,
-    int nq, int64_t ldq, const float* __restrict__ tq, const float* __restrict__ theta,
-    int64_t stride, int64_t n_sample, int rows_per_slab, int n_slabs, int n_qt,
-    uint64_t* __restrict__ lists, int* __restrict__ counts) {
-  using S = typename std::conditional<I8, int, float>::type;
-  using A4 = typename std::conditional<I8, i32x4, f32x4>::type;
-  constexpr int ES = I8 ? 1 : 2;
-  constexpr int KS = EP * ES / 64;  // k-steps of 64 B
+    const uint16_t* __restrict__ xb, int64_t n, int64_t ld, const float* __restrict__ q,
+    int nq, int64_t ldq, const float* __restrict__ theta, int64_t stride, int64_t n_sample,
+    int rows_per_slab, int n_slabs, int n_qt, uint64_t* __restrict__ lists,
+    int* __restrict__ counts) {
+  constexpr int KS = EP / 32;  // k-steps
   constexpr int QPW = 16 * QB;
   __shared__ int cnt[FL_WAVES][QPW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -145,20 +83,22 @@ __global__ __launch_bounds__(64 * FL_WAVES, 2) void k_filter_dense(
   const int slab = lb / n_qt, qt = lb % n_qt;
   const int qbase = qt * (FL_WAVES * QPW) + w * QPW;
 
-  u32x4 qf[QB][KS];
-  S th[QB];
-  float tqv[QB];
+  bf16x8 qf[QB][KS];
+  float th[QB];
   bool qv[QB];
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
     const int qi = qbase + 16 * b + col;
     qv[b] = qi < nq;
-    load_query_frags<EP, KS, I8>(q, ldq, qv[b] ? qi : 0, g, qf[b]);
-    if constexpr (I8) {
-      tqv[b] = qv[b] ? tq[qi] : 0.0f;
-      th[b] = qv[b] ? i8_threshold(theta[qi], tqv[b]) : 2147483647;
-    } else {
-      th[b] = qv[b] ? theta[qi] : __builtin_huge_valf();
+    th[b] = qv[b] ? theta[qi] : __builtin_huge_valf();
+    const float* qp = q + (int64_t)(qv[b] ? qi : 0) * ldq + 8 * g;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const f32x4 v0 = *(const f32x4*)(qp + 32 * s);
+      const f32x4 v1 = *(const f32x4*)(qp + 32 * s + 4);
+      u32x4 u = {pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]), pack_bf16x2(v1[0], v1[1]),
+                 pack_bf16x2(v1[2], v1[3])};
+      qf[b][s] = __builtin_bit_cast(bf16x8, u);
     }
   }
   if (lane < QPW) cnt[w][lane] = 0;
@@ -170,7 +110,7 @@ __global__ __launch_bounds__(64 * FL_WAVES, 2) void k_filter_dense(
     auto row_ptr = [&](int64_t jb) {
       int64_t j = jb + col;
       j = j < j1 ? j : j1 - 1;
-      return (const u32x4*)((const char*)xb + j * stride * ld * ES) + g;  // 16 B at byte 16g
+      return (const u32x4*)(xb + j * stride * ld) + g;  // 16 B = 8 bf16 at dims 8g..
     };
     // EP <= 512: the next 16-row block's A fragments are loaded before this block's MFMAs
     // (one block in flight per wave); EP = 768 has no VGPRs for that and relies on the
@@ -191,13 +131,16 @@ __global__ __launch_bounds__(64 * FL_WAVES, 2) void k_filter_dense(
           for (int s = 0; s < KS; ++s) nxt[s] = p[4 * s];
         }
       }
-      A4 acc[QB];
+      f32x4 acc[QB];
 #pragma unroll
-      for (int b = 0; b < QB; ++b) acc[b] = A4{0, 0, 0, 0};
+      for (int b = 0; b < QB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
+      for (int s = 0; s < KS; ++s) {
+        const bf16x8 a = __builtin_bit_cast(bf16x8, cur[s]);
 #pragma unroll
-        for (int b = 0; b < QB; ++b) acc[b] = mfma_step<I8>(cur[s], qf[b][s], acc[b]);
+        for (int b = 0; b < QB; ++b)
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[b][s], acc[b], 0, 0, 0);
+      }
       // lane holds a(row jb + 4g + jj, query qbase + 16b + col)
       uint32_t pass = 0;
 #pragma unroll
@@ -218,7 +161,7 @@ __global__ __launch_bounds__(64 * FL_WAVES, 2) void k_filter_dense(
               if (slot < FL_CAP) {
                 const int64_t r = (jb + 4 * g + jj) * stride;
                 lists[((int64_t)qi * n_slabs + slab) * FL_CAP + slot] =
-                    make_key(score_of<I8>(acc[b][jj], tqv[b]), (uint32_t)r);
+                    make_key(acc[b][jj], (uint32_t)r);
               }
             }
           }
@@ -255,26 +198,16 @@ __global__ __launch_bounds__(64 * FL_WAVES, 2) void k_filter_dense(
 // (a >= theta) go to an LDS pool that is flushed to the per-(query, slab) lists in HBM only
 // when half full and at the end, so global stores almost never sit in the vmcnt queue in
 // front of the ring's DMA.
-template <int EP, bool I8 = false> struct RingCfg;
+template <int EP> struct RingCfg;
 template <> struct RingCfg<64> { static constexpr int TR = 64, QB = 2; };
 template <> struct RingCfg<128> { static constexpr int TR = 32, QB = 2; };
 template <> struct RingCfg<256> { static constexpr int TR = 32, QB = 2; };
 #ifndef TT_RING_HALF
 #define TT_RING_HALF 0  // 4-wave blocks, 2 per CU (independent lockstep groups per CU)
 #endif
-#ifndef TT_I8_TR384
-#define TT_I8_TR384 64  // int8 rows are half as wide: twice the rows per tile for the same bytes
-#endif
 template <> struct RingCfg<384> { static constexpr int TR = TT_RING_HALF ? 16 : 32, QB = 2; };
 template <> struct RingCfg<512> { static constexpr int TR = 16, QB = 1; };
 template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
-// int8: the row bytes of bf16 EP/2 -> same tile bytes with twice the rows where registers allow
-template <> struct RingCfg<64, true> { static constexpr int TR = 64, QB = 2; };
-template <> struct RingCfg<128, true> { static constexpr int TR = 64, QB = 2; };
-template <> struct RingCfg<256, true> { static constexpr int TR = 32, QB = 2; };
-template <> struct RingCfg<384, true> { static constexpr int TR = TT_I8_TR384, QB = 2; };
-template <> struct RingCfg<512, true> { static constexpr int TR = 32, QB = 1; };
-template <> struct RingCfg<768, true> { static constexpr int TR = 32, QB = 1; };
 
 // Experiment switches (timing-only builds, results WRONG when set): tools/exp_filter.sh
 #ifndef TT_EXP_NODMA
@@ -299,16 +232,12 @@ constexpr int RG_WPOOL = RG_POOL / RG_WAVES;   // ... per wave (wave-private reg
 constexpr int RG_WFLUSH = RG_WPOOL / 2;
 constexpr uint32_t RG_OVF = 1u << 30;  // marks a (query, slab) list whose entries were dropped
 
-template <int EP, bool I8 = false>
-constexpr int ring_qpb() { return RG_WAVES * 16 * RingCfg<EP, I8>::QB; }
-template <int EP, bool I8 = false>
+template <int EP>
+constexpr int ring_qpb() { return RG_WAVES * 16 * RingCfg<EP>::QB; }
+template <int EP>
 constexpr int ring_smem() {
-  return RG_SLOTS * RingCfg<EP, I8>::TR * EP * (I8 ? 1 : 2) + RG_POOL * 12 + ring_qpb<EP, I8>() * 4 +
-         16;
+  return RG_SLOTS * RingCfg<EP>::TR * EP * 2 + RG_POOL * 12 + ring_qpb<EP>() * 4 + 16;
 }
-// XOR swizzle mask of the 16-B chunks of a row: the largest power of two <= 16 dividing the
-// chunk count, minus one (the swizzled position stays inside the row)
-constexpr int ring_fm(int cpr) { return (cpr % 16 == 0 ? 16 : cpr % 8 == 0 ? 8 : 4) - 1; }
 
 // LDS ops of the ring kernel's append path, in inline asm: the compiler cannot prove they do
 // not alias the in-flight global_load_lds and would otherwise precede each with vmcnt(0),
@@ -354,25 +283,21 @@ __device__ __forceinline__ void lds_barrier() {
 
 // FULL: the full-catalog (last) level -- a separate instantiation of the same code so that
 // profiles attribute the dominant launch on its own (bench.py's roofline kernel).
-// I8: the int8 images (see k_filter_dense); ld / ldq in bytes.
-template <int EP, bool FULL, bool I8>
+template <int EP, bool FULL>
 __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring(
-    const void* __restrict__ xb, int64_t ld, const void* __restrict__ q, int nq,
-    int64_t ldq, const float* __restrict__ tq, const float* __restrict__ theta, int64_t stride,
-    int64_t n_sample, int rows_per_slab, int n_slabs, int n_qt, uint64_t* __restrict__ lists,
+    const uint16_t* __restrict__ xb, int64_t ld, const float* __restrict__ q, int nq,
+    int64_t ldq, const float* __restrict__ theta, int64_t stride, int64_t n_sample,
+    int rows_per_slab, int n_slabs, int n_qt, uint64_t* __restrict__ lists,
     int* __restrict__ counts) {
-  using S = typename std::conditional<I8, int, float>::type;
-  using A4 = typename std::conditional<I8, i32x4, f32x4>::type;
-  constexpr int ES = I8 ? 1 : 2;
-  constexpr int TR = RingCfg<EP, I8>::TR, QB = RingCfg<EP, I8>::QB;
-  constexpr int KS = EP * ES / 64, QPW = 16 * QB, QPB = RG_WAVES * QPW;
-  constexpr int CPR = EP * ES / 16;  // 16-B chunks per row
-  constexpr int TILE_B = TR * EP * ES;
+  constexpr int TR = RingCfg<EP>::TR, QB = RingCfg<EP>::QB;
+  constexpr int KS = EP / 32, QPW = 16 * QB, QPB = RG_WAVES * QPW;
+  constexpr int CPR = EP / 8;  // 16-B chunks per row
+  constexpr int TILE_B = TR * EP * 2;
   constexpr int PIECES = TILE_B / 1024, PPW = PIECES / RG_WAVES;
-  constexpr int FM = ring_fm(CPR);
+  constexpr int FM = (CPR >= 16 ? 16 : CPR) - 1;
   constexpr int RB = TR / 16;
   static_assert(PIECES % RG_WAVES == 0, "tile must split into whole 1-KiB pieces per wave");
-  __shared__ __attribute__((aligned(16))) char smem[ring_smem<EP, I8>()];
+  __shared__ __attribute__((aligned(16))) char smem[ring_smem<EP>()];
   char* ring = smem;
   uint64_t* pool_key = (uint64_t*)(smem + RG_SLOTS * TILE_B);
   uint32_t* pool_meta = (uint32_t*)(pool_key + RG_POOL);
@@ -385,20 +310,21 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   const int slab = lb / n_qt, qt = lb % n_qt;
   const int qbase = qt * QPB + w * QPW;
 
-  u32x4 qf[QB][KS];
-  S th[QB];
-  float tqv[QB];
+  bf16x8 qf[QB][KS];
+  float th[QB];
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
     const int qi = qbase + 16 * b + col;
     const bool v = qi < nq;
-    load_query_frags<EP, KS, I8>(q, ldq, v ? qi : 0, g, qf[b]);
-    if constexpr (I8) {
-      tqv[b] = v ? tq[qi] : 0.0f;
-      th[b] = v ? i8_threshold(theta[qi], tqv[b]) : 2147483647;
-    } else {
-      tqv[b] = 0.0f;
-      th[b] = v ? theta[qi] : __builtin_huge_valf();
+    th[b] = v ? theta[qi] : __builtin_huge_valf();
+    const float* qp = q + (int64_t)(v ? qi : 0) * ldq + 8 * g;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const f32x4 v0 = *(const f32x4*)(qp + 32 * s);
+      const f32x4 v1 = *(const f32x4*)(qp + 32 * s + 4);
+      u32x4 u = {pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]), pack_bf16x2(v1[0], v1[1]),
+                 pack_bf16x2(v1[2], v1[3])};
+      qf[b][s] = __builtin_bit_cast(bf16x8, u);
     }
   }
   for (int i = tid; i < QPB; i += 64 * RG_WAVES) qcnt[i] = 0;
@@ -411,7 +337,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   // lane i writes 16-B chunk P = 64p + i = (row r, position pos); its source is chunk
   // pos ^ (r & FM) of that row, so row r's logical chunk c lives at position c ^ (r & FM).
   // Per lane the (row, column byte) of each piece is loop-invariant.
-  const int64_t row_bytes = stride * ld * ES;
+  const int64_t row_bytes = stride * ld * 2;
   // source = wave-uniform tile base (SGPRs) + the lane's 32-bit offset within the tile
   uint32_t voff[PPW];
 #pragma unroll
@@ -475,17 +401,14 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
 
   // Fast reject of a finished tile (lane: RB*4 scores per query block): per-block maxima.
   // NaN scores (the t = 0 placeholder, NaN rows) never pass a >= test.
-  auto tile_max = [&](const A4 (&sc)[RB][QB], S (&mx)[QB]) __attribute__((always_inline)) {
+  auto tile_max = [&](const f32x4 (&sc)[RB][QB], float (&mx)[QB]) __attribute__((always_inline)) {
 #pragma unroll
     for (int b = 0; b < QB; ++b) {
-      S m = sc[0][b][0];
+      float m = sc[0][b][0];
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          if constexpr (I8) m = max(m, sc[rb][b][jj]);
-          else m = fmaxf(m, sc[rb][b][jj]);
-        }
+        for (int jj = 0; jj < 4; ++jj) m = fmaxf(m, sc[rb][b][jj]);
       mx[b] = m;
     }
   };
@@ -493,8 +416,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   // One v_cmp + scalar branch per candidate slot; lanes of a non-empty slot write at
   // wn + (passing lanes below).  An entry past the wave's pool marks its query overflowed
   // (-> exact fallback).  Rows past the slab end (its last tile only) are masked to -inf first.
-  constexpr S S_NONE = I8 ? (S)(-2147483647 - 1) : (S)-__builtin_huge_valf();
-  auto append = [&](A4 (&sc)[RB][QB], const S (&mx)[QB], int t) __attribute__((always_inline)) {
+  auto append = [&](f32x4 (&sc)[RB][QB], const float (&mx)[QB], int t) __attribute__((always_inline)) {
     const int64_t jt = j0 + (int64_t)t * TR;
     if (jt + TR > j1) {
 #pragma unroll
@@ -503,7 +425,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
         for (int jj = 0; jj < 4; ++jj)
           if (jt + 16 * rb + 4 * g + jj >= j1)
 #pragma unroll
-            for (int b = 0; b < QB; ++b) sc[rb][b][jj] = S_NONE;
+            for (int b = 0; b < QB; ++b) sc[rb][b][jj] = -__builtin_huge_valf();
     }
     const uint32_t rlane = (uint32_t)((jt + 4 * g) * stride);
 #pragma unroll
@@ -518,7 +440,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
       for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
-          const S v = sc[rb][b][jj];
+          const float v = sc[rb][b][jj];
           const uint64_t bm = __ballot(v >= th[b]);
           if (bm != 0ull) {
             const uint32_t pos =
@@ -526,7 +448,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
                                                __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
             if (!TT_EXP_NOWRITE && v >= th[b]) {
               if (pos < (uint32_t)RG_WPOOL) {
-                const uint32_t u = __float_as_uint(score_of<I8>(v, tqv[b]));  // not NaN
+                const uint32_t u = __float_as_uint(v + 0.0f);  // not NaN: it passed
                 const uint32_t key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
                 const uint32_t r = rlane + (uint32_t)((16 * rb + jj) * stride);
                 lds_write64(lds_addr(&wkey[pos]), ((uint64_t)key << 32) | (uint64_t)(~r));
@@ -557,19 +479,18 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   // and the slot of tile t-1 is refilled with tile t+PD.  The selection of tile t-1 (per-block
   // max mid-tile, then the candidate scan) runs between tile t's MFMAs.
   // FD + 1 divides KS (the ring index is s % (FD + 1)); 2 steps ahead where registers are tight
-  constexpr int FD = (EP >= 384 && KS % 3 == 0) ? 2 : (KS >= 4 ? 3 : (KS >= 2 ? 1 : 0));
+  constexpr int FD = (EP >= 384 && KS % 3 == 0) ? 2 : (KS >= 4 ? 3 : 1);
   constexpr int S_MID = (KS - FD) / 2;
   static_assert(KS % (FD + 1) == 0 && S_MID < KS - FD, "fragment ring layout");
   for (int t = 0; t < RG_PD && t < n_tiles; ++t) issue(t);
   wait_tiles(n_tiles - 1 < RG_PD - 1 ? n_tiles - 1 : RG_PD - 1);
   lds_barrier();  // tile 0 landed; counters initialised
-  // placeholder "tile -1": never passes (NaN; INT_MIN < every int8 threshold)
-  const S pnone = I8 ? (S)(-2147483647 - 1) : (S)__builtin_nanf("");
-  A4 accp[RB][QB];
+  const float qnan = __builtin_nanf("");
+  f32x4 accp[RB][QB];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-    for (int b = 0; b < QB; ++b) accp[rb][b] = A4{pnone, pnone, pnone, pnone};
+    for (int b = 0; b < QB; ++b) accp[rb][b] = f32x4{qnan, qnan, qnan, qnan};
 
   // Fragment addresses: the tile loop is unrolled by RG_SLOTS so the slot of every tile is a
   // compile-time constant: slots 0-2 address from lrd, slots 3-4 from lrd + 3 TILE_B, and the
@@ -601,12 +522,12 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
       const int t = t0 + U;
       if (t < n_tiles) {
         const bool has_next = t + 1 < n_tiles;
-        A4 acc[RB][QB];
+        f32x4 acc[RB][QB];
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-          for (int b = 0; b < QB; ++b) acc[rb][b] = A4{0, 0, 0, 0};
-        S mx[QB];
+          for (int b = 0; b < QB; ++b) acc[rb][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+        float mx[QB];
         static_for<KS>([&](auto s_) __attribute__((always_inline)) {
           constexpr int s = decltype(s_)::value;
           if constexpr (s + FD < KS) {
@@ -624,10 +545,12 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
 #pragma unroll
           for (int rb = 0; rb < RB; ++rb) reg_tie(fr[s % (FD + 1)][rb]);
 #pragma unroll
-          for (int rb = 0; rb < RB; ++rb)
+          for (int rb = 0; rb < RB; ++rb) {
+            const bf16x8 a = __builtin_bit_cast(bf16x8, fr[s % (FD + 1)][rb]);
 #pragma unroll
             for (int b = 0; b < QB; ++b)
-              acc[rb][b] = mfma_step<I8>(fr[s % (FD + 1)][rb], qf[b][s], acc[rb][b]);
+              acc[rb][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[b][s], acc[rb][b], 0, 0, 0);
+          }
           if constexpr (s == 0) tile_max(accp, mx);  // VALU between this tile's MFMAs
           if constexpr (s == S_MID) {
             if (has_next) {
@@ -643,7 +566,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
             if (TT_EXP_NOSEL) {
 #pragma unroll
               for (int b = 0; b < QB; ++b)
-                if (mx[b] >= th[b]) asm volatile("" ::: "memory");  // (mx: S)
+                if (mx[b] >= th[b]) asm volatile("" ::: "memory");
             }
           }
         });
@@ -656,7 +579,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
     });
   }
   if (n_tiles > 0 && !TT_EXP_NOSEL) {
-    S mx[QB];
+    float mx[QB];
     tile_max(accp, mx);
     append(accp, mx, n_tiles - 1);
   }
@@ -1092,74 +1015,6 @@ __global__ __launch_bounds__(256) void k_query_eps(const float* __restrict__ q, 
   }
 }
 
-// int8 filter, per query (one wave): q' = c o q (c = the catalog's per-dim scales), t = max|q'|/127,
-// m = rne(q'/t) -> the int8 query image; eps2 = 2 eps_q with (n = int8 row, X, R, N catalog
-// bounds, x = c o n + e exactly, |e| <= R, |n| <= N):
-//   x.q - a = e.q + n.(p - t m) + (t n.m - a),   p = c o q (real), a = fl(float(n.m) t)
-//   eps_q = R|q| + N(|q' - t m| + 2^-24 1.01 |q'|) + 2^-24 N t|m| + E 2^-24 X |q|   (x 1.001)
-// where the last term bounds the canonical f32 score's own rounding (as in k_query_eps).
-template <int EP>
-__global__ __launch_bounds__(256) void k_query_prep_i8(const float* __restrict__ q, int nq,
-                                                       int64_t ldq,
-                                                       const float* __restrict__ colscale,
-                                                       float X, float R, float N,
-                                                       int8_t* __restrict__ q8,
-                                                       float* __restrict__ tq,
-                                                       float* __restrict__ eps2) {
-  constexpr int PER = EP / 64;
-  const int qi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (qi >= nq) return;
-  const float* qr = q + (int64_t)qi * ldq;
-  float qp[PER];
-  float sq = 0.0f, amax = 0.0f;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int i = lane + 64 * j;
-    const float v = qr[i];
-    qp[j] = colscale[i] * v;
-    sq = fmaf(v, v, sq);
-    amax = fmaxf(amax, fabsf(qp[j]));
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    sq += __shfl_xor(sq, o, 64);
-    amax = fmaxf(amax, __shfl_xor(amax, o, 64));
-  }
-  const bool bad = !(sq == sq) || !(sq < __builtin_huge_valf());
-  const float t = bad ? __builtin_nanf("") : amax * (1.0f / 127.0f);
-  float sp = 0.0f, sr = 0.0f;
-  int sm = 0;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    int m = 0;
-    if (t > 0.0f) {
-      const float r = rintf(qp[j] / t);
-      m = (int)fminf(127.0f, fmaxf(-127.0f, r));
-    }
-    q8[(int64_t)qi * EP + lane + 64 * j] = (int8_t)m;
-    const float e = fmaf(-t, (float)m, qp[j]);  // one rounding of q' - t m
-    sp = fmaf(qp[j], qp[j], sp);
-    sr = t > 0.0f ? fmaf(e, e, sr) : sr + qp[j] * qp[j];
-    sm += m * m;
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    sp += __shfl_xor(sp, o, 64);
-    sr += __shfl_xor(sr, o, 64);
-    sm += __shfl_xor(sm, o, 64);
-  }
-  if (lane == 0) {
-    const float grow = 1.0f + (float)(EP + 2) * 1.1920929e-07f, up = 1.0f + 2.4e-7f;
-    const float nq_ = sqrtf(sq * grow) * up, np = sqrtf(sp * grow) * up, nr = sqrtf(sr * grow) * up;
-    const float nm = sqrtf((float)sm) * up;  // sm exact (< 2^24)
-    const float g = (float)EP * 5.9604645e-08f * 1.01f;
-    const float u24 = 5.9604645e-08f;
-    const float tt = t > 0.0f ? t : 0.0f;
-    const float e = R * nq_ + N * (nr + u24 * 1.01f * np) + u24 * N * tt * nm * up + g * X * nq_;
-    const float r = 2.0f * e * 1.001f;
-    tq[qi] = t;
-    eps2[qi] = (r == r && !bad) ? r : __builtin_huge_valf();
-  }
-}
-
 __global__ void k_sub_arr(float* x, const float* y, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] = x[i] - y[i];
@@ -1268,8 +1123,6 @@ struct FilterWs {
   int* flags;  // flags[nq], qsel[nq], qsel_n[1] are contiguous (one memset)
   int* qsel;
   int* qsel_n;
-  int8_t* q8;  // int8 filter: query image [nq, ep] and scales [nq]
-  float* tq;
   void* scan_ws;
   int64_t scan_ws_bytes;
   int64_t total;
@@ -1299,8 +1152,6 @@ static FilterWs carve(void* base, const FilterPlan& p, int64_t n, int d, int nq,
   w.flags = fl;
   w.qsel = fl + nq;
   w.qsel_n = fl + 2 * nq;
-  w.q8 = (int8_t*)take((int64_t)nq * tt_padded_dim(d));
-  w.tq = (float*)take((int64_t)nq * 4);
   int64_t sb = 0;
   tt_scan_workspace_bytes(n, d, nq, k, &sb);
   w.scan_ws_bytes = sb;
@@ -1309,31 +1160,21 @@ static FilterWs carve(void* base, const FilterPlan& p, int64_t n, int d, int nq,
   return w;
 }
 
-// The catalog image a filter level streams: bf16 (uint16 elements) or int8 (bytes); ld in
-// elements of the image.
-struct Img {
-  const void* x;
-  int64_t ld;
-  bool i8;
-};
-
-template <int EP, bool I8>
-static void launch_level(const Level& L, const Img& im, int64_t n, const float* q, int nq,
-                         int64_t ldq, const FilterWs& w, hipStream_t st) {
+template <int EP>
+static void launch_level(const Level& L, const uint16_t* xb, int64_t n, int64_t ld,
+                         const float* q, int nq, int64_t ldq, const FilterWs& w,
+                         hipStream_t st) {
   const int nblk = L.n_qt * L.n_slabs;
-  // int8: the query image prepared by filter_init (ld = ep bytes) and its scales
-  const void* qp = I8 ? (const void*)w.q8 : (const void*)q;
-  const int64_t lq = I8 ? EP : ldq;
   if (L.dense) {
     constexpr int QB = EP <= 384 ? 2 : 1;
-    hipLaunchKernelGGL((k_filter_dense<EP, QB, I8>), dim3(nblk), dim3(64 * FL_WAVES), 0, st, im.x,
-                       n, im.ld, qp, nq, lq, w.tq, w.theta, L.stride, L.n_sample, L.rows_per_slab,
+    hipLaunchKernelGGL((k_filter_dense<EP, QB>), dim3(nblk), dim3(64 * FL_WAVES), 0, st, xb, n,
+                       ld, q, nq, ldq, w.theta, L.stride, L.n_sample, L.rows_per_slab,
                        L.n_slabs, L.n_qt, w.lists, w.counts);
   } else {
-    auto kern = L.stride == 1 ? k_filter_ring<EP, true, I8> : k_filter_ring<EP, false, I8>;
-    hipLaunchKernelGGL(kern, dim3(nblk), dim3(64 * RG_WAVES), 0, st, im.x, im.ld, qp, nq, lq,
-                       w.tq, w.theta, L.stride, L.n_sample, L.rows_per_slab, L.n_slabs, L.n_qt,
-                       w.lists, w.counts);
+    auto kern = L.stride == 1 ? k_filter_ring<EP, true> : k_filter_ring<EP, false>;
+    hipLaunchKernelGGL(kern, dim3(nblk), dim3(64 * RG_WAVES), 0, st, xb, ld, q, nq, ldq, w.theta,
+                       L.stride, L.n_sample, L.rows_per_slab, L.n_slabs, L.n_qt, w.lists,
+                       w.counts);
   }
 }
 
@@ -1373,7 +1214,7 @@ extern "C" int tt_filter_fallback_offset(int64_t n, int32_t d, int32_t nq, int32
 
 namespace {
 // Shared prologue of the single-shard call and the sharded stages: validation, plan, carve.
-int filter_setup(const float* db, const void* db_bf16, int64_t n, int32_t d, int64_t ld_db,
+int filter_setup(const float* db, const uint16_t* db_bf16, int64_t n, int32_t d, int64_t ld_db,
                  const float* q, int32_t nq, int64_t ld_q, int32_t k, void* workspace,
                  int64_t workspace_bytes, int* ep_out, FilterPlan* p, FilterWs* w) {
   TT_REQUIRE(n >= 1 && n <= 0x7fffffffLL, "need 1 <= n < 2^31");
@@ -1394,12 +1235,10 @@ int filter_setup(const float* db, const void* db_bf16, int64_t n, int32_t d, int
   return TT_OK;
 }
 
-// colscale != nullptr: the int8 filter (query image, scales and its eps from n_norm_max)
 int filter_init(const FilterWs& w, const float* q, int nq, int64_t ld_q, int ep, float x_norm_max,
-                float x_resid_max, hipStream_t st, const float* colscale = nullptr,
-                float n_norm_max = 0.0f) {
-  TT_REQUIRE(x_norm_max >= 0.0f && x_resid_max >= 0.0f && n_norm_max >= 0.0f,
-             "catalog bounds must be >= 0 (tt_bf16_image_bounds / tt_quantize_i8_rows)");
+                float x_resid_max, hipStream_t st) {
+  TT_REQUIRE(x_norm_max >= 0.0f && x_resid_max >= 0.0f,
+             "x_norm_max / x_resid_max must be >= 0 (tt_bf16_image_bounds)");
   if (hipMemsetAsync(w.flags, 0, ((size_t)2 * nq + 1) * 4, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "hipMemsetAsync(flags)");
   const unsigned fill_grid = (unsigned)((nq + 255) / 256);
@@ -1408,18 +1247,6 @@ int filter_init(const FilterWs& w, const float* q, int nq, int64_t ld_q, int ep,
   hipLaunchKernelGGL(k_fill_f32, dim3(fill_grid), dim3(256), 0, st, w.aref, nq,
                      -__builtin_huge_valf());
   const unsigned eps_grid = (unsigned)((nq + 3) / 4);
-  if (colscale) {
-    switch (ep) {
-#define TT_QP(E)                                                                              \
-  case E:                                                                                     \
-    hipLaunchKernelGGL(k_query_prep_i8<E>, dim3(eps_grid), dim3(256), 0, st, q, nq, ld_q,     \
-                       colscale, x_norm_max, x_resid_max, n_norm_max, w.q8, w.tq, w.eps2);    \
-    break;
-      TT_QP(64) TT_QP(128) TT_QP(256) TT_QP(384) TT_QP(512) TT_QP(768)
-#undef TT_QP
-    }
-    return check_launch("filter_init(int8)");
-  }
   switch (ep) {
 #define TT_QE(E)                                                                              \
   case E:                                                                                     \
@@ -1433,33 +1260,22 @@ int filter_init(const FilterWs& w, const float* q, int nq, int64_t ld_q, int ep,
 }
 
 // level li (+ its selection in `mode`); events around the full-catalog level
-int filter_level(const FilterPlan& p, const FilterWs& w, int li, int mode, const Img& im,
-                 int64_t n, const float* q, int nq, int64_t ld_q, int k, int ep,
+int filter_level(const FilterPlan& p, const FilterWs& w, int li, int mode, const uint16_t* db16,
+                 int64_t n, int64_t ld_db, const float* q, int nq, int64_t ld_q, int k, int ep,
                  hipStream_t st, void* ev_start, void* ev_stop, const float* stats = nullptr,
                  int* pcount = nullptr, float* smax_out = nullptr) {
   const Level& L = p.lv[li];
   const bool last = li == p.n_levels - 1;
   if (last && ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "hipEventRecord(start)");
-  if (im.i8) {
-    switch (ep) {
-      case 128: launch_level<128, true>(L, im, n, q, nq, ld_q, w, st); break;
-      case 256: launch_level<256, true>(L, im, n, q, nq, ld_q, w, st); break;
-      case 384: launch_level<384, true>(L, im, n, q, nq, ld_q, w, st); break;
-      case 512: launch_level<512, true>(L, im, n, q, nq, ld_q, w, st); break;
-      case 768: launch_level<768, true>(L, im, n, q, nq, ld_q, w, st); break;
-      default: return fail(TT_ERR_UNSUPPORTED, "int8 filter: padded dim must be >= 128");
-    }
-  } else {
-    switch (ep) {
-      case 64: launch_level<64, false>(L, im, n, q, nq, ld_q, w, st); break;
-      case 128: launch_level<128, false>(L, im, n, q, nq, ld_q, w, st); break;
-      case 256: launch_level<256, false>(L, im, n, q, nq, ld_q, w, st); break;
-      case 384: launch_level<384, false>(L, im, n, q, nq, ld_q, w, st); break;
-      case 512: launch_level<512, false>(L, im, n, q, nq, ld_q, w, st); break;
-      case 768: launch_level<768, false>(L, im, n, q, nq, ld_q, w, st); break;
-      default: return fail(TT_ERR_UNSUPPORTED, "bad padded dim");
-    }
+  switch (ep) {
+    case 64: launch_level<64>(L, db16, n, ld_db, q, nq, ld_q, w, st); break;
+    case 128: launch_level<128>(L, db16, n, ld_db, q, nq, ld_q, w, st); break;
+    case 256: launch_level<256>(L, db16, n, ld_db, q, nq, ld_q, w, st); break;
+    case 384: launch_level<384>(L, db16, n, ld_db, q, nq, ld_q, w, st); break;
+    case 512: launch_level<512>(L, db16, n, ld_db, q, nq, ld_q, w, st); break;
+    case 768: launch_level<768>(L, db16, n, ld_db, q, nq, ld_q, w, st); break;
+    default: return fail(TT_ERR_UNSUPPORTED, "bad padded dim");
   }
   int rc = check_launch("k_filter");
   if (rc) return rc;
@@ -1522,39 +1338,8 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
   for (int li = 0; li < p.n_levels; ++li) {
     const bool last = li == p.n_levels - 1;
     if (last && li > 0 && (rc = full_threshold(w, nq, st))) return rc;
-    if ((rc = filter_level(p, w, li, last ? 1 : 0, Img{db_bf16, ld_db, false}, n, q, nq, ld_q, k,
-                           ep, st, ev_start, ev_stop)))
-      return rc;
-  }
-  return filter_finish(w, db, n, d, ld_db, row_base, q, nq, ld_q, k, ep, out_score, out_idx, st);
-}
-
-extern "C" int tt_scan_topk_i8f32(const float* db, const int8_t* db_i8, int64_t n, int32_t d,
-                                  int64_t ld_db, int64_t ld_i8, int64_t row_base, const float* q,
-                                  int32_t nq, int64_t ld_q, int32_t k, const float* colscale,
-                                  float x_norm_max, float x_resid_max, float n_norm_max,
-                                  float* out_score, int64_t* out_idx, void* workspace,
-                                  int64_t workspace_bytes, void* stream, void* ev_start,
-                                  void* ev_stop) {
-  TT_REQUIRE(nq >= 0, "nq < 0");
-  if (nq == 0) return TT_OK;
-  TT_REQUIRE(colscale != nullptr && db_i8 != nullptr, "null pointer");
-  TT_REQUIRE(ld_i8 >= tt_padded_dim(d) && ld_i8 % 16 == 0, "ld_i8 must be >= tt_padded_dim(d), % 16");
-  int ep;
-  FilterPlan p;
-  FilterWs w;
-  int rc = filter_setup(db, db_i8, n, d, ld_db, q, nq, ld_q, k, workspace, workspace_bytes, &ep,
-                        &p, &w);
-  if (rc) return rc;
-  if (ep < 128) return fail(TT_ERR_UNSUPPORTED, "int8 filter: d <= 64 (use the bf16 filter)");
-  hipStream_t st = (hipStream_t)stream;
-  if ((rc = filter_init(w, q, nq, ld_q, ep, x_norm_max, x_resid_max, st, colscale, n_norm_max)))
-    return rc;
-  for (int li = 0; li < p.n_levels; ++li) {
-    const bool last = li == p.n_levels - 1;
-    if (last && li > 0 && (rc = full_threshold(w, nq, st))) return rc;
-    if ((rc = filter_level(p, w, li, last ? 1 : 0, Img{db_i8, ld_i8, true}, n, q, nq, ld_q, k, ep,
-                           st, ev_start, ev_stop)))
+    if ((rc = filter_level(p, w, li, last ? 1 : 0, db_bf16, n, ld_db, q, nq, ld_q, k, ep, st,
+                           ev_start, ev_stop)))
       return rc;
   }
   return filter_finish(w, db, n, d, ld_db, row_base, q, nq, ld_q, k, ep, out_score, out_idx, st);
@@ -1645,8 +1430,8 @@ extern "C" int tt_sharded_filter_begin(const uint16_t* sample_bf16, int64_t n_sa
   if ((rc = filter_init(w, q, nq, ld_q, ep, 0.0f, 0.0f, st))) return rc;
   for (int li = 0; li < p.n_levels; ++li) {
     const bool last = li == p.n_levels - 1;
-    if ((rc = filter_level(p, w, li, 0, Img{sample_bf16, ld, false}, n_sample, q, nq, ld_q, k, ep,
-                           st, nullptr, nullptr, nullptr, nullptr, last ? w.cut : nullptr)))
+    if ((rc = filter_level(p, w, li, 0, sample_bf16, n_sample, ld, q, nq, ld_q, k, ep, st, nullptr,
+                           nullptr, nullptr, nullptr, last ? w.cut : nullptr)))
       return rc;
   }
   hipLaunchKernelGGL(k_pack_stats, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, w.theta,
@@ -1674,8 +1459,8 @@ extern "C" int tt_sharded_filter_full(const uint16_t* db_bf16, int64_t n, int32_
   hipLaunchKernelGGL(k_stats_theta, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, stats,
                      w.eps2, nq, w.aref, w.theta);
   if ((rc = check_launch("k_stats_theta"))) return rc;
-  return filter_level(p, w, 0, 2, Img{db_bf16, ld_db, false}, n, q, nq, ld_q, k, ep, st, ev_start,
-                      ev_stop, stats, probe_counts, nullptr);
+  return filter_level(p, w, 0, 2, db_bf16, n, ld_db, q, nq, ld_q, k, ep, st, ev_start, ev_stop,
+                      stats, probe_counts, nullptr);
 }
 
 extern "C" int tt_sharded_filter_finish(const float* db, const uint16_t* db_bf16, int64_t n,

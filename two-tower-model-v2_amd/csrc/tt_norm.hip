@@ -132,109 +132,3 @@ extern "C" int tt_bf16_image_bounds(const float* x, const uint16_t* x_bf16, int6
                      d, ld, out2);
   return check_launch("tt_bf16_image_bounds");
 }
-
-// --------------------------------------------------------------------------- int8 image
-// Catalog image of the int8 filter (tt_scan_topk_i8f32): x ~ c o n with per-dimension scales
-// c (so that outlier dimensions do not widen every row's step) and n = rne(x / c) in
-// [-127, 127].  The bound inputs are MEASURED on the image actually written, so any c is
-// sound; c_i = max_r |x_ri| / 127 makes the residual smallest.
-namespace tt {
-// out[i] = max(out[i], max_r |x_ri|), i < d; NaN elements are skipped (fmaxf)
-__global__ __launch_bounds__(256) void k_absmax_cols(const float* __restrict__ x, int64_t n,
-                                                     int d, int64_t ld, int64_t rows_per_block,
-                                                     float* out) {
-  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
-  const int64_t r1 = r0 + rows_per_block < n ? r0 + rows_per_block : n;
-  for (int i = threadIdx.x; i < d; i += blockDim.x) {
-    float m = 0.0f;
-    for (int64_t r = r0; r < r1; ++r) m = fmaxf(m, fabsf(x[r * ld + i]));
-    atomicMax((unsigned int*)&out[i], __float_as_uint(m));  // non-negative: bit order = order
-  }
-}
-
-// One wave per row: n = rne(x / c) (0 where c == 0 or x is NaN), padding columns [d, ep) = 0;
-// max-combines out3 = {X >= max ||x||, R >= max ||x - c o n||, N >= max ||n||} over non-NaN rows.
-__global__ __launch_bounds__(256) void k_quantize_i8(const float* __restrict__ x, int64_t n, int d,
-                                                     int ep, int64_t ld,
-                                                     const float* __restrict__ colscale,
-                                                     int8_t* __restrict__ out, int64_t ld_out,
-                                                     float* out3) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  float mx = 0.0f, mr = 0.0f;
-  int mn = 0;
-  for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < n; row += (int64_t)gridDim.x * 4) {
-    const float* xr = x + row * ld;
-    int8_t* orow = out + row * ld_out;
-    float sx = 0.0f, sr = 0.0f;
-    int sn = 0;
-    for (int i0 = 4 * lane; i0 < ep; i0 += 256) {  // 4 columns per lane: one 32-bit store
-      uint32_t packed = 0;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = i0 + u;
-        int m = 0;
-        if (i < d) {
-          const float v = xr[i], c = colscale[i];
-          if (c > 0.0f && v == v) {
-            const float r = rintf(v / c);
-            m = (int)fminf(127.0f, fmaxf(-127.0f, r));
-          }
-          const float e = fmaf(-c, (float)m, v);  // one rounding of x - c n
-          sx = fmaf(v, v, sx);
-          sr = fmaf(e, e, sr);
-          sn += m * m;
-        }
-        packed |= (uint32_t)(uint8_t)(int8_t)m << (8 * u);
-      }
-      *(uint32_t*)(orow + i0) = packed;
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      sx += __shfl_xor(sx, o, 64);
-      sr += __shfl_xor(sr, o, 64);
-      sn += __shfl_xor(sn, o, 64);
-    }
-    if (sx == sx && sr == sr) {
-      mx = fmaxf(mx, sx);
-      mr = fmaxf(mr, sr);
-      mn = max(mn, sn);
-    }
-  }
-  if (lane == 0) {
-    const float grow = 1.0f + (float)(d + 3) * 1.1920929e-07f, up = 1.0f + 2.4e-7f;
-    atomicMax((unsigned int*)&out3[0], __float_as_uint(sqrtf(mx * grow) * up));
-    atomicMax((unsigned int*)&out3[1], __float_as_uint(sqrtf(mr * grow) * up));
-    atomicMax((unsigned int*)&out3[2], __float_as_uint(sqrtf((float)mn) * up));  // mn < 2^24
-  }
-}
-}  // namespace tt
-
-extern "C" int tt_absmax_cols_f32(const float* x, int64_t n, int32_t d, int64_t ld, float* out,
-                                  void* stream) {
-  using namespace tt;
-  TT_REQUIRE(n >= 0 && d >= 1 && ld >= d, "need n >= 0, 1 <= d <= ld");
-  TT_REQUIRE(out != nullptr, "out == NULL");
-  if (n == 0) return TT_OK;
-  TT_REQUIRE(x != nullptr, "x == NULL");
-  const int64_t rpb = n < 2048 ? 8 : (n + 2047) / 2048;  // <= 2048 blocks
-  const unsigned grid = (unsigned)((n + rpb - 1) / rpb);
-  hipLaunchKernelGGL(k_absmax_cols, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, n, d, ld,
-                     rpb, out);
-  return check_launch("tt_absmax_cols_f32");
-}
-
-extern "C" int tt_quantize_i8_rows(const float* x, int64_t n, int32_t d, int64_t ld,
-                                   const float* colscale, int8_t* out, int64_t ld_out, float* out3,
-                                   void* stream) {
-  using namespace tt;
-  const int ep = tt_padded_dim(d);
-  TT_REQUIRE(ep > 0, "d > 768");
-  TT_REQUIRE(n >= 0 && ld >= d && ld_out >= ep && ld_out % 4 == 0, "bad sizes / ld_out % 4");
-  TT_REQUIRE(colscale != nullptr && out3 != nullptr, "null pointer");
-  if (n == 0) return TT_OK;
-  TT_REQUIRE(x != nullptr && out != nullptr && ((uintptr_t)out % 4) == 0, "x/out NULL or unaligned");
-  const int64_t blocks64 = (n + 3) / 4;
-  const unsigned grid = (unsigned)(blocks64 < 4096 ? blocks64 : 4096);
-  hipLaunchKernelGGL(k_quantize_i8, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, n, d, ep, ld,
-                     colscale, out, ld_out, out3);
-  return check_launch("tt_quantize_i8_rows");
-}

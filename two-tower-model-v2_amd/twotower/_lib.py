@@ -71,11 +71,6 @@ SIGNATURES = {
     "tt_scan_topk_bf16f32": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _i64, _vp, _i32, _i64,
                                             _i32, ctypes.c_float, ctypes.c_float, _vp, _vp, _vp,
                                             _i64, _vp, _vp, _vp]),
-    "tt_absmax_cols_f32": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _vp]),
-    "tt_quantize_i8_rows": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _vp, _i64, _vp, _vp]),
-    "tt_scan_topk_i8f32": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _i64, _i64, _vp, _i32, _i64,
-                                          _i32, _vp, ctypes.c_float, ctypes.c_float,
-                                          ctypes.c_float, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
     "tt_sharded_workspace_bytes": (ctypes.c_int, [_i64, _i32, _i32, _i32, ctypes.POINTER(_i64)]),
     "tt_sharded_fallback_offset": (ctypes.c_int, [_i64, _i32, _i32, _i32, ctypes.POINTER(_i64)]),
     "tt_sharded_filter_begin": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _i64, _i32, _vp,

@@ -146,61 +146,6 @@ def scan_topk_bf16(db: torch.Tensor, db16: torch.Tensor, n: int, d: int, q: torc
     return out
 
 
-class I8Image:
-    """int8 filter image of a catalog (tt_quantize_i8_rows): rows [n, ep] int8, per-dim
-    scales colscale [ep] f32, measured bounds (X, R, N)."""
-
-    def __init__(self, rows: torch.Tensor, colscale: torch.Tensor, bounds3):
-        self.rows, self.colscale, self.bounds = rows, colscale, tuple(float(v) for v in bounds3)
-
-
-def i8_image(x: torch.Tensor, d: int, colscale: torch.Tensor = None) -> I8Image:
-    """Quantise normalised catalog rows x [n, >= d] f32 (device).  colscale defaults to
-    max_r |x_ri| / 127 per dimension (0 for unused / padding dimensions)."""
-    _check_2d(x, "x")
-    n, ep = x.shape[0], _lib.padded_dim(d)
-    L, st = lib(), stream_ptr()
-    if colscale is None:
-        amax = torch.zeros(ep, dtype=_f32, device=x.device)
-        check(L.tt_absmax_cols_f32(_ptr(x), n, d, x.stride(0), _ptr(amax), st),
-              "tt_absmax_cols_f32")
-        colscale = amax / 127.0
-    rows = torch.empty((n, ep), dtype=torch.int8, device=x.device)
-    b3 = torch.zeros(3, dtype=_f32, device=x.device)
-    check(L.tt_quantize_i8_rows(_ptr(x), n, d, x.stride(0), _ptr(colscale), _ptr(rows),
-                                rows.stride(0), _ptr(b3), st), "tt_quantize_i8_rows")
-    return I8Image(rows, colscale, b3.tolist())
-
-
-def scan_topk_i8(db: torch.Tensor, img: I8Image, n: int, d: int, q: torch.Tensor, k: int,
-                 row_base: int = 0, workspace: torch.Tensor = None, out=None,
-                 events=(None, None)):
-    """Exact top-k (bit-identical to scan_topk) via the int8 filter + f32 re-rank (k <= 128,
-    tt_padded_dim(d) >= 128)."""
-    _check_2d(db, "db")
-    _check_2d(q, "q")
-    nq = q.shape[0]
-    if not (1 <= k <= min(n, FILTER_KMAX)) or n > db.shape[0] or n > img.rows.shape[0]:
-        raise ValueError(f"scan_topk_i8: need 1 <= k ({k}) <= min(n, 128)")
-    if out is None:
-        out = (torch.empty((nq, k), dtype=_f32, device=q.device),
-               torch.empty((nq, k), dtype=torch.int64, device=q.device))
-    if nq == 0:
-        return out
-    need = filter_workspace_bytes(n, d, nq, k)
-    if workspace is None or workspace.numel() < need:
-        workspace = torch.empty(need, dtype=torch.uint8, device=q.device)
-    e0, e1 = events
-    X, R, N = img.bounds
-    check(lib().tt_scan_topk_i8f32(
-        _ptr(db), _ptr(img.rows), n, d, db.stride(0), img.rows.stride(0), row_base, _ptr(q), nq,
-        q.stride(0), k, _ptr(img.colscale), ctypes.c_float(X), ctypes.c_float(R),
-        ctypes.c_float(N), out[0].data_ptr(), out[1].data_ptr(), _ptr(workspace),
-        workspace.numel(), stream_ptr(), e0.cuda_event if e0 is not None else None,
-        e1.cuda_event if e1 is not None else None), "tt_scan_topk_i8f32")
-    return out
-
-
 def sharded_sample(x16: torch.Tensor, n: int) -> torch.Tensor:
     """Rows 0, 16, 32, ... of a bf16 catalog image (the replicated sample of the sharded search)."""
     return x16[:n:_lib.TT_SHARD_SAMPLE_STRIDE].contiguous()
