@@ -126,3 +126,14 @@ def test_infonce_oracle_vs_reference_fixture(golden, case):
     else:
         gn = [t.grad.norm().item() for t in (b, p, n)]
         np.testing.assert_allclose(gn, g[case + "__gnorm"], rtol=1e-5)
+
+
+def test_encoder_cfg_from_checkpoint_weights():
+    """EmbeddingEncoder infers the BertModel shape from the checkpoint's text-encoder weights
+    (sentence-transformers keys, reference item_tower.py:29 model; 32-wide heads)."""
+    from twotower.encoder import encoder_cfg_from_state_dict
+    from twotower.item_tower import random_bert_state_dict
+
+    cfg = dict(vocab=777, hidden=384, layers=3, heads=12, intermediate=1536, max_positions=512,
+               type_vocab=2, ln_eps=1e-12)
+    assert encoder_cfg_from_state_dict(random_bert_state_dict(cfg, 0)) == cfg
