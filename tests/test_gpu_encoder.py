@@ -64,6 +64,29 @@ def test_gemm_bf16_vs_torch(M, N, K):
     torch.testing.assert_close(C.double(), ref, rtol=1e-4, atol=1e-4)  # exact products, f32 sums
 
 
+@pytest.mark.parametrize("M,N,K,act,res", [(60001, 1152, 384, 0, False),
+                                           (70003, 384, 1536, 0, True),
+                                           (65536, 1000, 384, 1, False),
+                                           (66000, 1536, 384, 2, True),
+                                           (70000, 1152, 64, 0, False),
+                                           (40000, 2048, 128, 1, True)])
+def test_gemm_bf16_large_m_ring_kernel(M, N, K, act, res):
+    """M large enough for the 256x128 ring kernel (k_gemm_big): same results as the
+    128x128 kernel's contract -- exact bf16 products, f32 sums, fused epilogue, ragged N/M."""
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    A = torch.randn((M, K), generator=g, device="cuda")
+    W = torch.randn((N, K), generator=g, device="cuda") / K ** 0.5
+    b = torch.randn(N, generator=g, device="cuda")
+    R = torch.randn((M, N), generator=g, device="cuda") if res else None
+    C, C16 = _gemm(A, W, b, R, act, "bf16", want16=True)
+    ref = A.to(torch.bfloat16).double() @ W.to(torch.bfloat16).double().T + b.double()
+    ref = {0: ref, 1: F.gelu(ref), 2: torch.relu(ref)}[act]
+    if res:
+        ref = ref + R.double()
+    torch.testing.assert_close(C.double(), ref, rtol=1e-4, atol=2e-4)
+    assert torch.equal(C16, C.to(torch.bfloat16))
+
+
 @pytest.mark.parametrize("M,N,K", [(8, 8, 384), (513, 517, 768), (3, 100, 64)])
 def test_gemm_ragged_n(M, N, K):
     g = torch.Generator(device="cuda").manual_seed(N)

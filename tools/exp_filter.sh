@@ -4,11 +4,12 @@ set -e
 cd "$(dirname "$0")/../two-tower-model-v2_amd/csrc"
 mkdir -p ../lib/variants ../build/variants
 VARIANTS=${VARIANTS:-"base: nodma:-DTT_EXP_NODMA=1 nosel:-DTT_EXP_NOSEL=1 nobar:-DTT_EXP_NOBAR=1 nowrite:-DTT_EXP_NOWRITE=1 maxonly:-DTT_EXP_MAXONLY=1"}
+FILE=${FILE:-tt_filter}  # the source the variants differ in (tt_filter or tt_encoder)
 rm -f ../lib/variants/lib_*.so
 for v in $VARIANTS; do
   name=${v%%:*}; defs=${v#*:}; defs=${defs//,/ }
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $defs -x hip -c tt_filter.hip -o ../build/variants/tt_filter_$name.o
-  others=$(ls ../build/*.o | grep -v tt_filter)
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $others ../build/variants/tt_filter_$name.o -o ../lib/variants/lib_$name.so
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $defs -x hip -c $FILE.hip -o ../build/variants/${FILE}_$name.o
+  others=$(ls ../build/*.o | grep -v $FILE)
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $others ../build/variants/${FILE}_$name.o -o ../lib/variants/lib_$name.so
 done
 ls -la ../lib/variants

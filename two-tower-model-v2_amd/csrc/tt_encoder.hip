@@ -62,10 +62,104 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
 }
 
+// The bf16 path's GELU: erf by Abramowitz-Stegun 7.1.26 (|error| <= 1.5e-7 absolute, far
+// below the bf16 rounding of the outputs it feeds): ~12 VALU ops instead of erff's ~35, which
+// made the FFN1 GEMM's epilogue VALU-bound.  The f32 (parity) path keeps erff.
+__device__ __forceinline__ float gelu_fast(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = 1.0f - p * t * __expf(-z * z);  // erf(|x| / sqrt 2)
+  return 0.5f * x * (1.0f + (x < 0.0f ? -e : e));
+}
+
+typedef __bf16 bf16x2e __attribute__((ext_vector_type(2)));
+typedef float f32x2e __attribute__((ext_vector_type(2)));
+// two floats -> packed bf16 (round to nearest even) in one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t pack_bf16_hw(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2e{a, b}, bf16x2e));
+}
+
 // XCD-aware tile order: consecutive logical tiles (same A rows, all N tiles) on one XCD.
 __device__ __forceinline__ int enc_xcd_remap(int bid, int nblk) {
   const int q = nblk / 8, r = nblk % 8, x = bid % 8, local = bid / 8;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + local;
+}
+
+// Epilogue of one wave's 64x64 accumulator tile, stored straight from registers.  The MFMAs
+// compute the TRANSPOSED block D = W . A^T, so lane (g = l >> 4, rl = l & 15) of block (i, j)
+// holds C[m = mw0 + 16 i + rl][n = nw0 + 16 j + 4 g + v], v = 0..3: four consecutive columns of
+// one row -> one 16-B (f32) / 8-B (bf16) store, bias and residual read as 16-B vectors; the
+// 4 j-blocks of a row fill its 128-B (bf16) / 256-B (f32) span back to back.
+// C or C16 may be NULL (write only the copy the consumer needs).
+template <bool FAST>
+__device__ __forceinline__ void gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, int nw0,
+                                                   int lane, int M, int N,
+                                                   const float* __restrict__ bias,
+                                                   const float* __restrict__ res, int64_t ldr,
+                                                   float* __restrict__ C, int64_t ldc,
+                                                   uint16_t* __restrict__ C16, int64_t ldc16,
+                                                   int act) {
+  const int g = lane >> 4, rl = lane & 15;
+  const bool vec = (N % 4) == 0 && (ldc % 4) == 0 && (!res || (ldr % 4) == 0) &&
+                   (!C16 || (ldc16 % 4) == 0) && ((uintptr_t)bias % 16) == 0 &&
+                   ((uintptr_t)res % 16) == 0 && ((uintptr_t)C % 16) == 0 &&
+                   ((uintptr_t)C16 % 8) == 0 && mw0 + 64 <= M && nw0 + 64 <= N;
+  if (vec) {
+    // full tile: every bias / residual load is issued before the first use, so their
+    // latencies overlap (a load-use chain per 16x16 block serialises ~16 L2 round trips)
+    f32x4 bv[4], rv[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      bv[j] = bias ? *(const f32x4*)(bias + nw0 + 16 * j + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
+    if (res) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          rv[i][j] = *(const f32x4*)(res + (int64_t)(mw0 + 16 * i + rl) * ldr + nw0 + 16 * j + 4 * g);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t m = mw0 + 16 * i + rl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = nw0 + 16 * j + 4 * g;
+        f32x4 y = acc[i][j] + bv[j];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (act == ACT_GELU) y[u] = FAST ? gelu_fast(y[u]) : gelu_erf(y[u]);
+          else if (act == ACT_RELU) y[u] = y[u] > 0.0f ? y[u] : 0.0f;
+        }
+        if (res) y = y + rv[i][j];
+        if (C) *(f32x4*)(C + m * ldc + n) = y;
+        if (C16) *(uint2*)(C16 + m * ldc16 + n) = uint2{pack_bf16_hw(y[0], y[1]),
+                                                        pack_bf16_hw(y[2], y[3])};
+      }
+    }
+    return;
+  }
+  // edge tiles / unaligned operands: element-wise with bounds checks
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = mw0 + 16 * i + rl;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = nw0 + 16 * j + 4 * g;
+      for (int u = 0; u < 4 && n + u < N; ++u) {
+        float y = acc[i][j][u] + (bias ? bias[n + u] : 0.0f);
+        if (act == ACT_GELU) y = FAST ? gelu_fast(y) : gelu_erf(y);
+        else if (act == ACT_RELU) y = y > 0.0f ? y : 0.0f;
+        if (res) y = y + res[(int64_t)m * ldr + n + u];
+        if (C) C[(int64_t)m * ldc + n + u] = y;
+        if (C16) C16[(int64_t)m * ldc16 + n + u] = f32_to_bf16_rne(y);
+      }
+    }
+  }
 }
 
 template <typename T>
@@ -175,10 +269,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_
             const f32x4 a = __builtin_bit_cast(f32x4, av[s][i]), b = __builtin_bit_cast(f32x4, bv[s][j]);
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[u], a[u], acc[i][j], 0, 0, 0);
           } else {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                __builtin_bit_cast(bf16x8e, av[s][i]), __builtin_bit_cast(bf16x8e, bv[s][j]),
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(  // D = W . A^T (see epilogue)
+                __builtin_bit_cast(bf16x8e, bv[s][j]), __builtin_bit_cast(bf16x8e, av[s][i]),
                 acc[i][j], 0, 0, 0);
           }
         }
@@ -186,59 +280,160 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_
     enc_lds_barrier();
   }
 
-  // Epilogue staged through LDS (the stages are free after the last barrier): each wave
-  // parks its raw 64x64 accumulator tile (row stride 68 floats: conflict-free writes), then
-  // reads it back row-contiguous so bias, residual and the stores are coalesced 16-B (f32) /
-  // 8-B (bf16) accesses.  C or C16 may be NULL (write only the copy the consumer needs).
-  float* tile = (float*)(smem + w * (32 * 68 * 4));  // two halves of 32 rows per wave
-  static_assert(4 * 32 * 68 * 4 <= 2 * GM_STAGE_B, "epilogue tile fits the stage buffers");
-  const bool vec = (N % 4) == 0 && (ldc % 4) == 0 && (!res || (ldr % 4) == 0) &&
-                   (!C16 || (ldc16 % 4) == 0) && ((uintptr_t)bias % 16) == 0 &&
-                   ((uintptr_t)res % 16) == 0 && ((uintptr_t)C % 16) == 0 &&
-                   ((uintptr_t)C16 % 8) == 0;
+  gemm_wave_epilogue<sizeof(T) == 2>(acc, m0 + 64 * wm, n0 + 64 * wn, lane, M, N, bias, res, ldr,
+                                     C, ldc, C16, ldc16, act);
+}
+
+// Large-M bf16 GEMM: persistent blocks (one per CU, 8 waves of 64x64 = 256x128 tiles), a
+// 3-slot LDS ring (48 KB stages) fed two stages ahead, ONE barrier per k-stage.  The ring runs
+// ACROSS tiles: the last two k-steps of a tile already load the first two stages of the
+// block's next tile, so the epilogue's stores and the next tile's pipeline fill overlap
+// instead of each launch-sized tile paying its DMA latency and store drain in full (measured:
+// the 128x128 kernel spends ~3/4 of its time outside the MFMA loop at K = 384).
+// DMA layout / swizzle / fragment reads / epilogue as k_gemm.
+constexpr int GB_BM = 256, GB_BN = 128, GB_SLOTS = 3;
+constexpr int GB_A_B = GB_BM * 128, GB_W_B = GB_BN * 128, GB_STAGE_B = GB_A_B + GB_W_B;
+// timing-only experiment switches (results WRONG when set): tools/exp_filter.sh FILE=tt_encoder
+#ifndef TT_GEXP_NOSTORE
+#define TT_GEXP_NOSTORE 0  // skip the epilogue
+#endif
+
+__global__ __launch_bounds__(512, 1) void k_gemm_big(const uint16_t* __restrict__ A, int64_t lda,
+                                                     const uint16_t* __restrict__ W, int64_t ldw,
+                                                     const float* __restrict__ bias,
+                                                     const float* __restrict__ res, int64_t ldr,
+                                                     float* __restrict__ C, int64_t ldc,
+                                                     uint16_t* __restrict__ C16, int64_t ldc16,
+                                                     int M, int N, int K, int act) {
+  constexpr int BK = 64, EPC = 8;
+  __shared__ __attribute__((aligned(16))) char smem[GB_SLOTS * GB_STAGE_B];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int n_tn = (N + GB_BN - 1) / GB_BN;
+  const int ntiles = ((M + GB_BM - 1) / GB_BM) * n_tn;
+  const int nk = K / BK;
+  // tile r of this block: logical tile (XCD-contiguous ranges; gridDim.x % 8 == 0 keeps a
+  // block on one XCD's range)
+  auto tile_of = [&](int r) { return enc_xcd_remap(blockIdx.x + r * gridDim.x, ntiles); };
+  const int n_mine = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+
+  // DMA: A = 32 pieces of 8 rows x 128 B, W = 16 pieces; wave w issues A pieces w + 8j
+  // (j < 4) and W pieces w + 8j (j < 2).  Chunk swizzle as k_gemm.  Offsets of the current
+  // (cur) and next (nxt) tile.
+  struct Offs {
+    int64_t a[4], w[2];
+  };
+  auto offsets = [&](int lt) __attribute__((always_inline)) {
+    Offs o;
+    const int m0 = (lt / n_tn) * GB_BM, n0 = (lt % n_tn) * GB_BN;
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
+    for (int j = 0; j < 4; ++j) {
+      const int row = 8 * (w + 8 * j) + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      int am = m0 + row;
+      am = am < M ? am : M - 1;
+      o.a[j] = (int64_t)am * lda + c * EPC;
+    }
 #pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
+    for (int j = 0; j < 2; ++j) {
+      const int row = 8 * (w + 8 * j) + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      int wr = n0 + row;
+      wr = wr < N ? wr : N - 1;
+      o.w[j] = (int64_t)wr * ldw + c * EPC;
+    }
+    return o;
+  };
+  auto issue = [&](const Offs& o, int kt, int gs) __attribute__((always_inline)) {
+    char* st = smem + (gs % GB_SLOTS) * GB_STAGE_B;
+    const int64_t k0 = (int64_t)kt * BK;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(A + o.a[j] + k0),
+          (__attribute__((address_space(3))) void*)(st + 1024 * (w + 8 * j)), 16, 0, 0);
 #pragma unroll
-        for (int v = 0; v < 4; ++v)
-          tile[(16 * ii + 4 * g + v) * 68 + 16 * j + rl] = acc[2 * half + ii][j][v];
-    wave_sync();
-#pragma unroll 4
-    for (int it = 0; it < 8; ++it) {
-      const int idx = it * 64 + lane, row = idx >> 4, c4 = idx & 15;
-      const int m = m0 + 64 * wm + 32 * half + row, n = n0 + 64 * wn + 4 * c4;
-      if (m >= M || n >= N) continue;
-      const f32x4 a4 = *(const f32x4*)(tile + row * 68 + 4 * c4);
-      if (vec) {
-        f32x4 y = a4;
-        if (bias) y = y + *(const f32x4*)(bias + n);
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(W + o.w[j] + k0),
+          (__attribute__((address_space(3))) void*)(st + GB_A_B + 1024 * (w + 8 * j)), 16, 0, 0);
+  };
+
+  const int g = lane >> 4, rl = lane & 15;
+  int fa[4][2], fb[4][2];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (act == ACT_GELU) y[u] = gelu_erf(y[u]);
-          else if (act == ACT_RELU) y[u] = y[u] > 0.0f ? y[u] : 0.0f;
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ra = 64 * wm + 16 * i + rl, rb = 64 * wn + 16 * i + rl;
+      const int c = 4 * s + g;
+      fa[i][s] = ra * 128 + 16 * (c ^ ((ra >> 1) & 7));
+      fb[i][s] = GB_A_B + rb * 128 + 16 * (c ^ ((rb >> 1) & 7));
+    }
+
+  if (n_mine <= 0) return;
+  // loads run two k-stages ahead in ONE sequence over (tile r, stage k) of this block
+  int r_i = 0, k_i = 0, g_i = 0;  // next stage to issue and its global index
+  Offs o_i = offsets(tile_of(0));
+  auto issue_next = [&]() __attribute__((always_inline)) {
+    if (r_i >= n_mine) return;
+    issue(o_i, k_i, g_i);
+    ++g_i;
+    if (++k_i == nk) {
+      k_i = 0;
+      if (++r_i < n_mine) o_i = offsets(tile_of(r_i));
+    }
+  };
+  issue_next();
+  issue_next();
+  int gs = 0;  // global stage index of (tile r, k-step 0) = r * nk
+  for (int r = 0; r < n_mine; ++r) {
+    const int lt = tile_of(r);
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt) {
+      // loads allowed in flight: the one stage issued after this one, if any.  The first stage
+      // of a tile also follows the previous tile's epilogue stores: drain everything.
+      if ((kt == 0 && r > 0) || g_i <= gs + kt + 1) enc_wait_vm<0>();
+      else enc_wait_vm<6>();
+      enc_lds_barrier();  // stage visible to all; every wave is done with the slot refilled next
+      issue_next();
+      const uint32_t sb = lds_addr(smem) + (uint32_t)(((gs + kt) % GB_SLOTS) * GB_STAGE_B);
+      u32x4 av[2][4], bv[2][4];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          av[s][i] = lds_read128<0>(sb + fa[i][s]);
+          bv[s][i] = lds_read128<0>(sb + fb[i][s]);
         }
-        if (res) y = y + *(const f32x4*)(res + (int64_t)m * ldr + n);
-        if (C) *(f32x4*)(C + (int64_t)m * ldc + n) = y;
-        if (C16) {
-          const uint2 pk = {(uint32_t)f32_to_bf16_rne(y[0]) | ((uint32_t)f32_to_bf16_rne(y[1]) << 16),
-                            (uint32_t)f32_to_bf16_rne(y[2]) | ((uint32_t)f32_to_bf16_rne(y[3]) << 16)};
-          *(uint2*)(C16 + (int64_t)m * ldc16 + n) = pk;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if (s == 0) lds_wait<8>();
+        else lds_wait<0>();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          reg_tie(av[s][i]);
+          reg_tie(bv[s][i]);
         }
-      } else {
-        for (int u = 0; u < 4 && n + u < N; ++u) {
-          float y = a4[u] + (bias ? bias[n + u] : 0.0f);
-          if (act == ACT_GELU) y = gelu_erf(y);
-          else if (act == ACT_RELU) y = y > 0.0f ? y : 0.0f;
-          if (res) y = y + res[(int64_t)m * ldr + n + u];
-          if (C) C[(int64_t)m * ldc + n + u] = y;
-          if (C16) C16[(int64_t)m * ldc16 + n + u] = f32_to_bf16_rne(y);
-        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(  // D = W . A^T
+                __builtin_bit_cast(bf16x8e, bv[s][j]), __builtin_bit_cast(bf16x8e, av[s][i]),
+                acc[i][j], 0, 0, 0);
       }
     }
-    wave_sync();
+    if (!TT_GEXP_NOSTORE)
+      gemm_wave_epilogue<true>(acc, (lt / n_tn) * GB_BM + 64 * wm, (lt % n_tn) * GB_BN + 64 * wn,
+                               lane, M, N, bias, res, ldr, C, ldc, C16, ldc16, act);
+    else if (acc[0][0][0] == 123.456f && acc[3][3][3] == 1.5f) C[0] = acc[1][1][1];
+    gs += nk;
   }
 }
 
@@ -605,6 +800,27 @@ __global__ __launch_bounds__(256) void k_item_concat(const float* __restrict__ p
 using namespace tt;
 
 // ------------------------------------------------------------------------------- C ABI
+namespace {
+int enc_device_cus() {
+  static const int cus = [] {
+    int d = 0, v = 0;
+    if (hipGetDevice(&d) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && v > 0)
+      return v;
+    return 256;
+  }();
+  return cus;
+}
+// TT_GEMM_BIG=0 in the environment keeps every bf16 GEMM on the 128x128 kernel (A/B timing)
+bool gemm_big_disabled() {
+  static const bool off = [] {
+    const char* e = getenv("TT_GEMM_BIG");
+    return e && e[0] == '0';
+  }();
+  return off;
+}
+}  // namespace
+
 extern "C" int tt_gemm_f32(const float* A, int64_t lda, const float* W, int64_t ldw,
                            const float* bias, const float* residual, int64_t ldr, float* C,
                            int64_t ldc, uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N,
@@ -635,6 +851,15 @@ extern "C" int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, i
   TT_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0,
              "A/W must be 16-B aligned with lda, ldw % 8 == 0");
   TT_REQUIRE(act >= 0 && act <= 2, "bad activation");
+  // large M: the persistent 256x128 ring kernel (one block per CU) once there are at least
+  // two tiles per CU
+  const int nbig = ((M + GB_BM - 1) / GB_BM) * ((N + GB_BN - 1) / GB_BN);
+  const int ncu = enc_device_cus();
+  if (nbig >= 2 * ncu && !gemm_big_disabled()) {
+    hipLaunchKernelGGL(k_gemm_big, dim3(ncu), dim3(512), 0, (hipStream_t)stream, A, lda, W, ldw,
+                       bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
+    return check_launch("tt_gemm_bf16(256x128)");
+  }
   const int nblk = ((M + GM_BM - 1) / GM_BM) * ((N + GM_BN - 1) / GM_BN);
   hipLaunchKernelGGL(k_gemm<uint16_t>, dim3(nblk), dim3(256), 0, (hipStream_t)stream, A, lda, W,
                      ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);

@@ -205,7 +205,12 @@ template <> struct RingCfg<256> { static constexpr int TR = 32, QB = 2; };
 #ifndef TT_RING_HALF
 #define TT_RING_HALF 0  // 4-wave blocks, 2 per CU (independent lockstep groups per CU)
 #endif
-template <> struct RingCfg<384> { static constexpr int TR = TT_RING_HALF ? 16 : 32, QB = 2; };
+#ifndef TT_RING_QB4
+#define TT_RING_QB4 0  // 4-wave blocks, 1 per CU, 64 queries per wave (half the LDS reads/flop)
+#endif
+template <> struct RingCfg<384> {
+  static constexpr int TR = TT_RING_HALF ? 16 : 32, QB = TT_RING_QB4 ? 4 : 2;
+};
 template <> struct RingCfg<512> { static constexpr int TR = 16, QB = 1; };
 template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 
@@ -225,8 +230,9 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #ifndef TT_EXP_MAXONLY
 #define TT_EXP_MAXONLY 0  // per-block max + ballot only (no per-slot scan)
 #endif
-constexpr int RG_WAVES = TT_RING_HALF ? 4 : 8, RG_PD = 3, RG_SLOTS = RG_PD + 1;  // 3 in flight
-constexpr int RG_POOL = 512 * RG_WAVES;        // pool entries per block
+constexpr int RG_WAVES = (TT_RING_HALF || TT_RING_QB4) ? 4 : 8, RG_PD = 3,
+              RG_SLOTS = RG_PD + 1;  // 3 in flight
+constexpr int RG_POOL = (TT_RING_QB4 ? 1024 : 512) * RG_WAVES;  // pool entries per block
 constexpr int RG_BLOCKS_PER_CU = TT_RING_HALF ? 2 : 1;
 constexpr int RG_WPOOL = RG_POOL / RG_WAVES;   // ... per wave (wave-private region)
 constexpr int RG_WFLUSH = RG_WPOOL / 2;
@@ -1087,7 +1093,9 @@ static FilterPlan plan_filter(int64_t n, int nq, int k, int ep) {
   p.n_levels = nl;
   p.max_slabs = 1;
   const int dense_qpb = FL_WAVES * 16 * (ep <= 384 ? 2 : 1);
-  int ring_qpb_v = RG_WAVES * 16 * (ep <= 384 ? 2 : 1);
+  const int ring_qpb_v = ep == 64 ? ring_qpb<64>() : ep == 128 ? ring_qpb<128>()
+                        : ep == 256 ? ring_qpb<256>() : ep == 384 ? ring_qpb<384>()
+                        : ep == 512 ? ring_qpb<512>() : ring_qpb<768>();
   for (int i = 0; i < nl; ++i) {
     Level& L = p.lv[i];
     L.stride = strides[nl - 1 - i];
