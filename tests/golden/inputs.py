@@ -157,3 +157,31 @@ def flatip_inputs(spec):
         x = np.concatenate([base, base, base])[: spec["N"]].copy()
     q = rng.standard_normal((spec["Q"], E), dtype=np.float32)
     return x, q
+
+
+# --------------------------------------------------------------- evaluation metrics (f4)
+EVAL_K = [1, 5, 10, 20]
+
+
+def eval_cases(seed: int = 21, n_products: int = 60, n_buyers: int = 40):
+    """Synthetic evaluation set: metadata (some categories / brands missing or empty),
+    per buyer: interactions, relevant set (0..5 items, some outside the catalog) and the
+    retrieved list (20 distinct ids) a stub index returns."""
+    rng = np.random.default_rng(seed)
+    pids = [f"p{i}" for i in range(n_products)]
+    cats = ["rings", "necklaces", "oil", None, ""]
+    brands = ["Acme", "Damas", None, "Lazurde"]
+    meta = {p: {"text": f"item {p}", "category": cats[rng.integers(0, len(cats))],
+                "brand": brands[rng.integers(0, len(brands))]} for p in pids}
+    events = ["view", "add_to_cart", "purchase"]
+    cases = []
+    for b in range(n_buyers):
+        hist = [{"product_id": pids[rng.integers(0, n_products)],
+                 "event_type": events[rng.integers(0, 3)], "timestamp": None}
+                for _ in range(rng.integers(0, 7))]
+        rel = {pids[j] for j in rng.integers(0, n_products, rng.integers(0, 6))}
+        if b % 7 == 3:
+            rel.add("unknown-item")
+        ret = [pids[j] for j in rng.permutation(n_products)[:20]]
+        cases.append((f"u{b}", hist, rel, ret))
+    return pids, meta, cases

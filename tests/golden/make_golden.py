@@ -6,6 +6,7 @@ What is imported from the reference (read-only at /root/reference; never shipped
   src.models.buyer_tower.BuyerTower      (buyer_tower.py:9)   -> buyer_*.npz
   src.training.losses.InfoNCELoss        (losses.py:8)        -> infonce.npz
   src.utils.config.get_event_weight      (config.py:27)       -> event_weights.json
+  src.evaluation.metrics (functions + Evaluator, stub encoder / index) -> metrics.json
   src.models.item_tower.ItemTower        (item_tower.py:10)   -> item_head.npz; the module
       imports sentence_transformers (absent offline), so a test-only stand-in module supplies
       a SentenceTransformer whose encode() returns fixed, seeded 384-d "text embeddings": the
@@ -150,11 +151,86 @@ def flatip_fixtures():
     np.savez_compressed(os.path.join(HERE, "flatip.npz"), **out)
 
 
+def _stub_sentence_transformers():
+    """test-only stand-in module so that reference modules importing it load (see item_head)."""
+    if "sentence_transformers" in sys.modules:
+        return
+
+    class _StubST(torch.nn.Module):
+        def __init__(self, name):
+            super().__init__()
+
+        def get_sentence_embedding_dimension(self):
+            return 384
+
+    mod = types.ModuleType("sentence_transformers")
+    mod.SentenceTransformer = _StubST
+    sys.modules["sentence_transformers"] = mod
+
+
+def metrics_fixtures():
+    """src/evaluation/metrics.py: every metric function on seeded cases, and
+    Evaluator.evaluate_retrieval / evaluate_diversity / evaluate_coverage driven by stub
+    encoder / index objects that return the cases' retrieved lists."""
+    _stub_sentence_transformers()
+    if "faiss" not in sys.modules:  # imported by vector_db.py at module level; never called here
+        sys.modules["faiss"] = types.ModuleType("faiss")
+    from src.evaluation import metrics as M  # reference module
+
+    pids, meta, cases = gi.eval_cases()
+    per_case = []
+    for _, hist, rel, ret in cases:
+        h = [i["product_id"] for i in hist]
+        row = {"mrr": M.compute_mrr(ret, rel)}
+        for k in gi.EVAL_K:
+            row[f"recall@{k}"] = M.compute_recall_at_k(ret, rel, k)
+            row[f"precision@{k}"] = M.compute_precision_at_k(ret, rel, k)
+            row[f"ndcg@{k}"] = M.compute_ndcg_at_k(ret, rel, k)
+            row[f"hit@{k}"] = M.compute_hit_rate_at_k(ret, rel, k)
+            row[f"cat@{k}"] = M.compute_category_overlap(ret[:k], h, meta)
+            row[f"brand@{k}"] = M.compute_brand_overlap(ret[:k], h, meta)
+            row[f"rel@{k}"] = M.compute_relevance_score(ret[:k], h, meta)
+        for attr in ("category", "brand"):
+            row[f"div_{attr}"] = M.compute_diversity(ret, meta, attr)
+        per_case.append(row)
+
+    index_of = {}
+
+    class StubEncoder:  # encode_buyer -> a one-hot of the case index
+        def encode_buyer(self, interactions):
+            return np.array([float(index_of[id(interactions)])], np.float32)
+
+    class StubDB:
+        def retrieve(self, emb, k=10):
+            ret = cases[int(emb[0])][3]
+            return [(p, 1.0 - 0.01 * r) for r, p in enumerate(ret[:k])]
+
+    test_pairs = []
+    for c, (bid, hist, rel, _) in enumerate(cases):
+        index_of[id(hist)] = c
+        test_pairs.append((bid, hist, rel))
+    ev = M.Evaluator(StubEncoder(), StubDB(), config_path=os.path.join(REF, "configs/config.yaml"))
+    ev.set_product_metadata(meta)
+    out = {"per_case": per_case,
+           "retrieval": ev.evaluate_retrieval(test_pairs, gi.EVAL_K, verbose=False),
+           "div_category": ev.evaluate_diversity(test_pairs, 20, "category"),
+           "div_brand": ev.evaluate_diversity(test_pairs, 20, "brand"),
+           "coverage": ev.evaluate_coverage(test_pairs, 20),
+           "coverage@5": M.compute_coverage(set().union(*[set(c[3][:5]) for c in cases]),
+                                            set(pids))}
+    with open(os.path.join(HERE, "metrics.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["metrics"]:
+        metrics_fixtures()
+        sys.exit(0)
     buyer_fixtures()
     infonce_fixtures()
     event_weight_fixtures()
     item_head_fixtures()
     flatip_fixtures()
+    metrics_fixtures()
     for f in sorted(os.listdir(HERE)):
         print(f, os.path.getsize(os.path.join(HERE, f)))

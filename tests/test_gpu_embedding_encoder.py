@@ -178,3 +178,39 @@ def test_save_item_embeddings_layout(tmp_path):
     assert list(np.load(tmp_path / "out" / "product_ids.npy")) == ["a", "b", "c"]
     assert json.load(open(tmp_path / "out" / "product_id_to_index.json")) == \
         {"a": 0, "b": 1, "c": 2}
+
+
+def test_batched_evaluator_equals_reference_per_buyer_loop(tmp_path):
+    """twotower.evaluation.Evaluator (one batched encode + retrieve_batch) == the reference's
+    per-buyer loop (encode_buyer + retrieve, metrics.py:419-429) on the HIP towers + index."""
+    from twotower import evaluation as E
+    from twotower.encoder import EmbeddingEncoder
+    from twotower.vector_db import VectorDatabase
+
+    path, *_ = _checkpoint(tmp_path, "weighted_avg")
+    enc = EmbeddingEncoder(str(path), config_path=None)
+    meta = _metadata()
+    enc.set_product_metadata(meta)
+    pids = list(meta)
+    db = VectorDatabase(384)
+    db.build_index(enc.encode_items(pids), pids)
+    rng = np.random.default_rng(4)
+    ev_types = ["view", "add_to_cart", "purchase"]
+    pairs = []
+    for b in range(12):
+        hist = [{"product_id": f"p{rng.integers(0, 30)}", "event_type": ev_types[rng.integers(0, 3)]}
+                for _ in range(rng.integers(1, 6))]
+        pairs.append((f"u{b}", hist, {f"p{j}" for j in rng.integers(0, 30, 3)}))
+    ev = E.Evaluator(enc, db, config_path=None)
+    ev.set_product_metadata(meta)
+    got = ev.evaluate_retrieval(pairs, [1, 5, 10], verbose=False)
+    # the reference loop, restated
+    ref = {}
+    for _, inter, rel in pairs:
+        ret = [p for p, _ in db.retrieve(enc.encode_buyer(inter), k=10)]
+        for k in [1, 5, 10]:
+            ref.setdefault(f"recall@{k}", []).append(E.compute_recall_at_k(ret, rel, k))
+            ref.setdefault(f"ndcg@{k}", []).append(E.compute_ndcg_at_k(ret, rel, k))
+        ref.setdefault("mrr", []).append(E.compute_mrr(ret, rel))
+    for key, vals in ref.items():
+        assert got[f"{key}_mean"] == float(np.mean(vals)), key
