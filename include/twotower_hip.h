@@ -254,6 +254,15 @@ int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
                  const float* bias, const float* residual, int64_t ldr, float* C, int64_t ldc,
                  uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N, int32_t K, int32_t act,
                  void* stream);
+/* Fused BertSelfOutput / BertOutput (transformers BertModel, the encoder behind
+ * SentenceTransformer.encode, item_tower.py:116-122): x = LayerNorm(A[M,K] . W[H,K]^T + bias + x)
+ * in place over rows of x [M,H] f32, plus the bf16 copy x_bf16.  bf16 A/W, f32 accumulate and
+ * LayerNorm (biased variance, eps).  H == 384 and K % 64 == 0 (TT_ERR_UNSUPPORTED otherwise);
+ * x, bias, gamma, beta 16-B aligned.  Used by tt_bert_encode's bf16 path. */
+int tt_gemm_ln_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
+                    const float* bias, const float* gamma, const float* beta, float eps, float* x,
+                    int64_t ldx, uint16_t* x_bf16, int64_t ldx16, int32_t M, int32_t H, int32_t K,
+                    void* stream);
 /* torch.nn.LayerNorm over rows of width H <= 1024 (BertLayer LayerNorms). */
 int tt_layernorm_f32(const float* x, int64_t ldx, const float* gamma, const float* beta,
                      float eps, float* y, int64_t ldy, uint16_t* y_bf16, int64_t ldy16,

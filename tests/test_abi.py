@@ -31,7 +31,7 @@ def test_header_declares_expected_entry_points():
                  "tt_weighted_avg_l2_f32", "tt_gather_weighted_avg_l2_f32", "tt_attn_agg_l2_f32",
                  "tt_scan_workspace_bytes", "tt_padded_dim", "tt_last_error", "tt_version",
                  "tt_scan_topk_bf16f32", "tt_bf16_image_bounds", "tt_bert_encode", "tt_gemm_f32",
-                 "tt_gemm_bf16", "tt_layernorm_f32", "tt_attention_varlen_f32", "tt_item_concat"):
+                 "tt_gemm_bf16", "tt_gemm_ln_bf16", "tt_layernorm_f32", "tt_attention_varlen_f32", "tt_item_concat"):
         assert name in fns
 
 

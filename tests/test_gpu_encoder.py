@@ -300,3 +300,43 @@ def test_gemm_bf16_only_output_and_misaligned_bias():
                                        0, None, 1152, only16.data_ptr(), 1152, 300, 1152, 384, 1,
                                        _lib.stream_ptr()), "gemm")
     assert torch.equal(only16, C16)
+
+
+@pytest.mark.parametrize("M,K", [(1, 384), (127, 384), (129, 1536), (5000, 384),
+                                 (70003, 1536), (65536, 384)])
+def test_gemm_ln_bf16_vs_torch(M, K):
+    """Fused BertSelfOutput / BertOutput (k_gemm_ln): x = LayerNorm(A W^T + b + x) in place,
+    plus the bf16 copy; vs the f64 composition over the same bf16 operands.  Covers ragged
+    last tiles, fewer tiles than CUs and several tiles per persistent block."""
+    from twotower import _lib
+
+    H = 384
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    A = torch.randn((M, K), generator=g, device="cuda").to(torch.bfloat16)
+    W = (torch.randn((H, K), generator=g, device="cuda") / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(H, generator=g, device="cuda")
+    gm = torch.randn(H, generator=g, device="cuda")
+    bt = torch.randn(H, generator=g, device="cuda")
+    x = torch.randn((M, H), generator=g, device="cuda") * 2 + 0.5
+    x16 = torch.empty((M, H), device="cuda", dtype=torch.bfloat16)
+    y = A.double() @ W.double().T + b.double() + x.double()
+    ref = F.layer_norm(y, (H,), gm.double(), bt.double(), 1e-12)
+    _lib.check(_lib.lib().tt_gemm_ln_bf16(A.data_ptr(), K, W.data_ptr(), K, b.data_ptr(),
+                                          gm.data_ptr(), bt.data_ptr(), 1e-12, x.data_ptr(), H,
+                                          x16.data_ptr(), H, M, H, K, _lib.stream_ptr()), "gemm_ln")
+    torch.cuda.synchronize()
+    torch.testing.assert_close(x.double(), ref, rtol=2e-5, atol=2e-5)
+    assert torch.equal(x16, x.to(torch.bfloat16))
+
+
+def test_gemm_ln_bf16_rejects_unsupported():
+    from twotower import _lib
+
+    L = _lib.lib()
+    z = torch.zeros(8 * 768, device="cuda")
+    assert L.tt_gemm_ln_bf16(z.data_ptr(), 512, z.data_ptr(), 512, z.data_ptr(), z.data_ptr(),
+                             z.data_ptr(), 1e-12, z.data_ptr(), 512, z.data_ptr(), 512, 4, 512, 64,
+                             _lib.stream_ptr()) == _lib.TT_ERR_UNSUPPORTED
+    assert L.tt_gemm_ln_bf16(z.data_ptr(), 384, z.data_ptr(), 384, z.data_ptr(), z.data_ptr(),
+                             z.data_ptr(), 1e-12, z.data_ptr(), 384, z.data_ptr(), 384, 4, 384, 96,
+                             _lib.stream_ptr()) == _lib.TT_ERR_UNSUPPORTED

@@ -62,6 +62,31 @@ def main():
         ms_t = e0.elapsed_time(e1) / a.iters
         out[f"N{N}_K{K}"] = {"us": round(ms * 1e3, 1), "tflops": round(2 * a.M * N * K / ms / 1e9, 1),
                              "torch_tflops": round(2 * a.M * N * K / ms_t / 1e9, 1)}
+    if a.prec == "bf16":  # fused GEMM + LayerNorm (Wo / W2 of a layer), in place
+        for K in (384, 1536):
+            A = torch.randn(a.M, K, device="cuda").to(dt)
+            W = (torch.randn(384, K, device="cuda") / K ** 0.5).to(dt)
+            b, gm, bt = (torch.randn(384, device="cuda") for _ in range(3))
+            X = torch.randn(a.M, 384, device="cuda")
+            X16 = torch.empty(a.M, 384, device="cuda", dtype=dt)
+
+            def run_ln():
+                _lib.check(L.tt_gemm_ln_bf16(A.data_ptr(), K, W.data_ptr(), K, b.data_ptr(),
+                                             gm.data_ptr(), bt.data_ptr(), 1e-12, X.data_ptr(), 384,
+                                             X16.data_ptr(), 384, a.M, 384, K, _lib.stream_ptr()),
+                           "gemm_ln")
+            for _ in range(3):
+                run_ln()
+            e0.record()
+            for _ in range(a.iters):
+                run_ln()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / a.iters
+            byts = a.M * (2 * K + 384 * 10)
+            out[f"LN_N384_K{K}"] = {"us": round(ms * 1e3, 1),
+                                    "tflops": round(2 * a.M * 384 * K / ms / 1e9, 1),
+                                    "hbm_gbps": round(byts / ms / 1e6, 1)}
     print(json.dumps({"prec": a.prec, "M": a.M, **out}))
 
 

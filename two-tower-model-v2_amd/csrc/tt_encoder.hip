@@ -89,20 +89,27 @@ __device__ __forceinline__ int enc_xcd_remap(int bid, int nblk) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + local;
 }
 
+// timing-only experiment switches (results WRONG when set): tools/exp_filter.sh FILE=tt_encoder
+#ifndef TT_GEXP_NOSTORE
+#define TT_GEXP_NOSTORE 0  // 1: skip k_gemm_big's epilogue; 2: compute it, skip its bf16 stores
+#endif
 // Epilogue of one wave's 64x64 accumulator tile, stored straight from registers.  The MFMAs
 // compute the TRANSPOSED block D = W . A^T, so lane (g = l >> 4, rl = l & 15) of block (i, j)
 // holds C[m = mw0 + 16 i + rl][n = nw0 + 16 j + 4 g + v], v = 0..3: four consecutive columns of
 // one row -> one 16-B (f32) / 8-B (bf16) store, bias and residual read as 16-B vectors; the
 // 4 j-blocks of a row fill its 128-B (bf16) / 256-B (f32) span back to back.
-// C or C16 may be NULL (write only the copy the consumer needs).
+// C or C16 may be NULL (write only the copy the consumer needs).  Returns the number of
+// vector-memory stores the lane issued when it is a compile-time count (16 per output copy on
+// the full-tile path, 8 for a bf16-only output), or 0 for the element-wise edge path: a persistent caller waits for
+// vmcnt(that count) before reusing its DMA ring, without draining the stores.
 template <bool FAST>
-__device__ __forceinline__ void gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, int nw0,
+__device__ __forceinline__ int gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, int nw0,
                                                    int lane, int M, int N,
                                                    const float* __restrict__ bias,
                                                    const float* __restrict__ res, int64_t ldr,
                                                    float* __restrict__ C, int64_t ldc,
                                                    uint16_t* __restrict__ C16, int64_t ldc16,
-                                                   int act) {
+                                                   int act, const float* lbias = nullptr) {
   const int g = lane >> 4, rl = lane & 15;
   const bool vec = (N % 4) == 0 && (ldc % 4) == 0 && (!res || (ldr % 4) == 0) &&
                    (!C16 || (ldc16 % 4) == 0) && ((uintptr_t)bias % 16) == 0 &&
@@ -114,13 +121,48 @@ __device__ __forceinline__ void gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, 
     f32x4 bv[4], rv[4][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      bv[j] = bias ? *(const f32x4*)(bias + nw0 + 16 * j + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
+      bv[j] = lbias  ? *(const f32x4*)(lbias + nw0 + 16 * j + 4 * g)  // LDS copy: no vmcnt wait
+              : bias ? *(const f32x4*)(bias + nw0 + 16 * j + 4 * g)
+                     : f32x4{0.f, 0.f, 0.f, 0.f};
     if (res) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           rv[i][j] = *(const f32x4*)(res + (int64_t)(mw0 + 16 * i + rl) * ldr + nw0 + 16 * j + 4 * g);
+    }
+    if (!C && (ldc16 % 8) == 0 && ((uintptr_t)C16 % 16) == 0) {
+      // bf16-only output: v_permlane16_swap pairs blocks j0 = 2 jp and j1 = 2 jp + 1 so that
+      // each lane holds 8 consecutive columns -> one 16-B store (8 per lane instead of 16
+      // 8-B ones; the epilogue was store-issue-bound).  After the swap lane row g holds
+      // columns 32 jp + 16 (g & 1) + 8 (g >> 1) .. + 7.
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t m = mw0 + 16 * i + rl;
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          uint32_t pk[2][2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int j = 2 * jp + h;
+            f32x4 y = acc[i][j] + bv[j];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              if (act == ACT_GELU) y[u] = FAST ? gelu_fast(y[u]) : gelu_erf(y[u]);
+              else if (act == ACT_RELU) y[u] = y[u] > 0.0f ? y[u] : 0.0f;
+            }
+            if (res) y = y + rv[i][j];
+            pk[h][0] = pack_bf16_hw(y[0], y[1]);
+            pk[h][1] = pack_bf16_hw(y[2], y[3]);
+          }
+          const auto s0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+          const int n = nw0 + 32 * jp + 16 * (g & 1) + 8 * (g >> 1);
+          if (TT_GEXP_NOSTORE != 2 || s0[0] == 0x12345678u)
+            *(u32x4*)(C16 + m * ldc16 + n) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+        }
+      }
+      return 8;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -140,7 +182,7 @@ __device__ __forceinline__ void gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, 
                                                         pack_bf16_hw(y[2], y[3])};
       }
     }
-    return;
+    return (C ? 16 : 0) + (C16 ? 16 : 0);
   }
   // edge tiles / unaligned operands: element-wise with bounds checks
 #pragma unroll
@@ -160,6 +202,7 @@ __device__ __forceinline__ void gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, 
       }
     }
   }
+  return 0;
 }
 
 template <typename T>
@@ -291,14 +334,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_
 // instead of each launch-sized tile paying its DMA latency and store drain in full (measured:
 // the 128x128 kernel spends ~3/4 of its time outside the MFMA loop at K = 384).
 // DMA layout / swizzle / fragment reads / epilogue as k_gemm.
-constexpr int GB_BM = 256, GB_BN = 128, GB_SLOTS = 3;
-constexpr int GB_A_B = GB_BM * 128, GB_W_B = GB_BN * 128, GB_STAGE_B = GB_A_B + GB_W_B;
-// timing-only experiment switches (results WRONG when set): tools/exp_filter.sh FILE=tt_encoder
-#ifndef TT_GEXP_NOSTORE
-#define TT_GEXP_NOSTORE 0  // skip the epilogue
-#endif
+constexpr int GB_BN = 128, GB_MAXN = 2048;
 
-__global__ __launch_bounds__(512, 1) void k_gemm_big(const uint16_t* __restrict__ A, int64_t lda,
+template <int GB_BM, int GB_SLOTS>
+__global__ __launch_bounds__(GB_BM * 2, 512 / (GB_BM * 2)) void k_gemm_big(const uint16_t* __restrict__ A, int64_t lda,
                                                      const uint16_t* __restrict__ W, int64_t ldw,
                                                      const float* __restrict__ bias,
                                                      const float* __restrict__ res, int64_t ldr,
@@ -306,8 +345,18 @@ __global__ __launch_bounds__(512, 1) void k_gemm_big(const uint16_t* __restrict_
                                                      uint16_t* __restrict__ C16, int64_t ldc16,
                                                      int M, int N, int K, int act) {
   constexpr int BK = 64, EPC = 8;
+  constexpr int GB_A_B = GB_BM * 128, GB_W_B = GB_BN * 128, GB_STAGE_B = GB_A_B + GB_W_B;
+  constexpr int NW = GB_BM / 32;        // waves: (BM / 64) x 2 of 64 x 64
+  constexpr int WP = 16 / NW;           // W pieces per wave and stage (A: 4)
+  constexpr int OPS = 4 + WP;           // DMA instructions per lane and stage
   __shared__ __attribute__((aligned(16))) char smem[GB_SLOTS * GB_STAGE_B];
+  // the bias in LDS: a global bias load in the epilogue would wait (in-order vmcnt) for the
+  // next tile's DMA stages issued just before it
+  __shared__ __attribute__((aligned(16))) float sbias[GB_MAXN];
   const int tid = threadIdx.x, lane = tid & 63;
+  const bool lds_bias = bias && N <= GB_MAXN && ((uintptr_t)bias % 16) == 0;
+  if (lds_bias)
+    for (int e = tid; e < N; e += GB_BM * 2) sbias[e] = bias[e];  // visible after stage 0's barrier
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 1, wn = w & 1;
   const int n_tn = (N + GB_BN - 1) / GB_BN;
@@ -318,26 +367,26 @@ __global__ __launch_bounds__(512, 1) void k_gemm_big(const uint16_t* __restrict_
   auto tile_of = [&](int r) { return enc_xcd_remap(blockIdx.x + r * gridDim.x, ntiles); };
   const int n_mine = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
 
-  // DMA: A = 32 pieces of 8 rows x 128 B, W = 16 pieces; wave w issues A pieces w + 8j
-  // (j < 4) and W pieces w + 8j (j < 2).  Chunk swizzle as k_gemm.  Offsets of the current
+  // DMA: A = BM / 8 pieces of 8 rows x 128 B, W = 16 pieces; wave w issues A pieces w + NW j
+  // (j < 4) and W pieces w + NW j (j < WP).  Chunk swizzle as k_gemm.  Offsets of the current
   // (cur) and next (nxt) tile.
   struct Offs {
-    int64_t a[4], w[2];
+    int64_t a[4], w[WP];
   };
   auto offsets = [&](int lt) __attribute__((always_inline)) {
     Offs o;
     const int m0 = (lt / n_tn) * GB_BM, n0 = (lt % n_tn) * GB_BN;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int row = 8 * (w + 8 * j) + (lane >> 3);
+      const int row = 8 * (w + NW * j) + (lane >> 3);
       const int c = (lane & 7) ^ ((row >> 1) & 7);
       int am = m0 + row;
       am = am < M ? am : M - 1;
       o.a[j] = (int64_t)am * lda + c * EPC;
     }
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int row = 8 * (w + 8 * j) + (lane >> 3);
+    for (int j = 0; j < WP; ++j) {
+      const int row = 8 * (w + NW * j) + (lane >> 3);
       const int c = (lane & 7) ^ ((row >> 1) & 7);
       int wr = n0 + row;
       wr = wr < N ? wr : N - 1;
@@ -352,12 +401,12 @@ __global__ __launch_bounds__(512, 1) void k_gemm_big(const uint16_t* __restrict_
     for (int j = 0; j < 4; ++j)
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(A + o.a[j] + k0),
-          (__attribute__((address_space(3))) void*)(st + 1024 * (w + 8 * j)), 16, 0, 0);
+          (__attribute__((address_space(3))) void*)(st + 1024 * (w + NW * j)), 16, 0, 0);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < WP; ++j)
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(W + o.w[j] + k0),
-          (__attribute__((address_space(3))) void*)(st + GB_A_B + 1024 * (w + 8 * j)), 16, 0, 0);
+          (__attribute__((address_space(3))) void*)(st + GB_A_B + 1024 * (w + NW * j)), 16, 0, 0);
   };
 
   const int g = lane >> 4, rl = lane & 15;
@@ -385,9 +434,10 @@ __global__ __launch_bounds__(512, 1) void k_gemm_big(const uint16_t* __restrict_
       if (++r_i < n_mine) o_i = offsets(tile_of(r_i));
     }
   };
-  issue_next();
-  issue_next();
+#pragma unroll
+  for (int p = 0; p < GB_SLOTS - 1; ++p) issue_next();
   int gs = 0;  // global stage index of (tile r, k-step 0) = r * nk
+  int nst = 0;  // stores issued by the previous tile's epilogue (0: unknown -> drain)
   for (int r = 0; r < n_mine; ++r) {
     const int lt = tile_of(r);
     f32x4 acc[4][4];
@@ -398,8 +448,19 @@ __global__ __launch_bounds__(512, 1) void k_gemm_big(const uint16_t* __restrict_
     for (int kt = 0; kt < nk; ++kt) {
       // loads allowed in flight: the one stage issued after this one, if any.  The first stage
       // of a tile also follows the previous tile's epilogue stores: drain everything.
-      if ((kt == 0 && r > 0) || g_i <= gs + kt + 1) enc_wait_vm<0>();
-      else enc_wait_vm<6>();
+      // younger than this stage's loads: the later stages already issued and, at a tile's
+      // first stage, the previous epilogue's stores (16 or 32 per lane, never waited for here;
+      // an edge tile's element-wise epilogue: drain)
+      if (kt == 0 && r > 0) {
+        if (nst == 32) enc_wait_vm<32>();
+        else if (nst == 16) enc_wait_vm<16>();
+        else if (nst == 8) enc_wait_vm<8>();
+        else enc_wait_vm<0>();
+      } else if (g_i <= gs + kt + GB_SLOTS - 2) {
+        enc_wait_vm<0>();
+      } else {
+        enc_wait_vm<OPS * (GB_SLOTS - 2)>();
+      }
       enc_lds_barrier();  // stage visible to all; every wave is done with the slot refilled next
       issue_next();
       const uint32_t sb = lds_addr(smem) + (uint32_t)(((gs + kt) % GB_SLOTS) * GB_STAGE_B);
@@ -429,11 +490,290 @@ __global__ __launch_bounds__(512, 1) void k_gemm_big(const uint16_t* __restrict_
                 acc[i][j], 0, 0, 0);
       }
     }
-    if (!TT_GEXP_NOSTORE)
-      gemm_wave_epilogue<true>(acc, (lt / n_tn) * GB_BM + 64 * wm, (lt % n_tn) * GB_BN + 64 * wn,
-                               lane, M, N, bias, res, ldr, C, ldc, C16, ldc16, act);
+    if (TT_GEXP_NOSTORE != 1)
+      nst = gemm_wave_epilogue<true>(acc, (lt / n_tn) * GB_BM + 64 * wm, (lt % n_tn) * GB_BN + 64 * wn,
+                               lane, M, N, bias, res, ldr, C, ldc, C16, ldc16, act,
+                               lds_bias ? sbias : nullptr);
     else if (acc[0][0][0] == 123.456f && acc[3][3][3] == 1.5f) C[0] = acc[1][1][1];
     gs += nk;
+  }
+}
+
+// Fused GEMM + LayerNorm for the two H-wide GEMMs of a BERT layer (bf16 path):
+//   BertSelfOutput / BertOutput: x = LayerNorm(A . W^T + bias + x)      (A = ctx, K = H; or
+//   A = GELU(ffn), K = I).  One block owns whole 384-wide rows, so the LayerNorm statistics
+// are reduced in LDS inside the epilogue and the pre-LayerNorm sum never reaches HBM: per
+// token row this writes x (f32, the residual stream) and its bf16 copy once, instead of a GEMM
+// writing y and a LayerNorm pass re-reading it (≈3.8 KB/row and one launch saved per call).
+// Persistent blocks (one per CU, 8 waves as 2 (M) x 4 (N), wave tile 64 x 96 = 4 x 6 MFMA
+// blocks), 128 x 384 tiles, k-stages of 64: the A tile (128 rows x 128 B, from HBM) streams
+// through a 3-slot LDS ring issued two stages ahead, W (384 rows x 128 B, L2-resident) through
+// a 2-slot ring one stage ahead; both run across tiles, so the next tile's first stages are in
+// flight during the epilogue.
+// The MFMA computes D = W . A^T as k_gemm_big (lane (g, rl) of block (i, j) holds row
+// 16 i + rl, columns 16 j + 4 g .. + 3).  In place: x is read (residual) before it is
+// overwritten, by the block that owns the rows.
+constexpr int GL_BM = 128, GL_H = 384, GL_NJ = 6, GL_ASLOTS = 3, GL_WSLOTS = 2;
+constexpr int GL_A_B = GL_BM * 128, GL_W_B = GL_H * 128;
+constexpr int GL_WBASE = GL_ASLOTS * GL_A_B, GL_LDS_B = GL_WBASE + GL_WSLOTS * GL_W_B;
+constexpr int GL_STORES = 4 * GL_NJ * 2;  // vector-memory stores per lane in a full tile
+
+__global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__ A, int64_t lda,
+                                                    const uint16_t* __restrict__ W, int64_t ldw,
+                                                    const float* __restrict__ bias,
+                                                    const float* __restrict__ gamma,
+                                                    const float* __restrict__ beta, float eps,
+                                                    float* __restrict__ X, int64_t ldx,
+                                                    uint16_t* __restrict__ X16, int64_t ldx16,
+                                                    int M, int K) {
+  constexpr int BK = 64, EPC = 8;
+  __shared__ __attribute__((aligned(16))) char smem[GL_LDS_B];
+  __shared__ float red[2][4][GL_BM];  // [mean | var pass][wave column wn][tile row]
+  __shared__ __attribute__((aligned(16))) float prm[3][GL_H];  // bias, gamma, beta
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int e = tid; e < GL_H; e += 512) {
+    prm[0][e] = bias[e];
+    prm[1][e] = gamma[e];
+    prm[2][e] = beta[e];
+  }  // visible after the first stage's barrier
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  const int ntiles = (M + GL_BM - 1) / GL_BM;
+  const int nk = K / BK;
+  auto tile_of = [&](int r) { return enc_xcd_remap(blockIdx.x + r * gridDim.x, ntiles); };
+  const int n_mine = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  if (n_mine <= 0) return;
+
+  // DMA: A = 16 pieces of 8 rows x 128 B, W = 48 pieces; wave w issues A pieces w + 8j (j < 2)
+  // and W pieces w + 8j (j < 6); chunk swizzle as k_gemm.
+  // W piece w + 8j = rows 64 j + 8 w + (lane >> 3): a per-lane 32-bit offset (the swizzle
+  // (row >> 1) & 7 does not depend on j) plus the uniform base W + 64 j ldw
+  const int w_row0 = 8 * w + (lane >> 3);
+  const int w_lane = w_row0 * (int)ldw + ((lane & 7) ^ ((w_row0 >> 1) & 7)) * EPC;
+  auto a_offsets = [&](int lt, int64_t (&ao)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = 8 * (w + 8 * j) + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      int am = lt * GL_BM + row;
+      am = am < M ? am : M - 1;
+      ao[j] = (int64_t)am * lda + c * EPC;
+    }
+  };
+  auto issue_a = [&](const int64_t (&ao)[2], int kt, int t) __attribute__((always_inline)) {
+    char* st = smem + (t % GL_ASLOTS) * GL_A_B;
+    const int64_t k0 = (int64_t)kt * BK;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(A + ao[j] + k0),
+          (__attribute__((address_space(3))) void*)(st + 1024 * (w + 8 * j)), 16, 0, 0);
+  };
+  auto issue_w = [&](int kt, int t) __attribute__((always_inline)) {
+    char* st = smem + GL_WBASE + (t % GL_WSLOTS) * GL_W_B;
+    const int64_t k0 = (int64_t)kt * BK;
+#pragma unroll
+    for (int j = 0; j < GL_NJ; ++j)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(W + (k0 + (int64_t)(64 * j) * ldw) + w_lane),
+          (__attribute__((address_space(3))) void*)(st + 1024 * (w + 8 * j)), 16, 0, 0);
+  };
+
+  // fragment rows 64 wm + 16 i + rl (A) / 96 wn + 16 j + rl (W): the swizzle (row >> 1) & 7
+  // = (rl >> 1) & 7 is the same for every i, j, so block i / j is an immediate offset
+  const int g = lane >> 4, rl = lane & 15;
+  uint32_t fa[2], fb[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int c = (4 * s + g) ^ ((rl >> 1) & 7);
+    fa[s] = (64 * wm + rl) * 128 + 16 * c;
+    fb[s] = (96 * wn + rl) * 128 + 16 * c;
+  }
+
+  // the block's stages t = r * nk + kt in one sequence: A(t) issued at stage t - 2, W(t) at
+  // stage t - 1, in the order W(t + 1), A(t + 2), so waiting for W(t) leaves exactly A(t + 1)'s
+  // two pieces younger
+  const int nstages = n_mine * nk;
+  int ra_i = 0, ka_i = 0, ta_i = 0;  // next A stage to issue
+  int64_t ao_i[2];
+  a_offsets(tile_of(0), ao_i);
+  auto issue_next_a = [&]() __attribute__((always_inline)) {
+    if (ta_i >= nstages) return;
+    issue_a(ao_i, ka_i, ta_i);
+    ++ta_i;
+    if (++ka_i == nk) {
+      ka_i = 0;
+      if (++ra_i < n_mine) a_offsets(tile_of(ra_i), ao_i);
+    }
+  };
+  issue_next_a();
+  issue_w(0, 0);
+  issue_next_a();
+  int gs = 0;
+  bool prev_full = true;
+  const float inv_h = 1.0f / (float)GL_H;
+  for (int r = 0; r < n_mine; ++r) {
+    const int m0 = tile_of(r) * GL_BM;
+    f32x4 acc[4][GL_NJ];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < GL_NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt) {
+      // younger than this stage's W pieces: A(t + 1) (2 per lane, if issued) and, at a tile's
+      // first stage, the previous epilogue's residual loads and GL_STORES stores (a ragged
+      // tile: drain all)
+      const int t = gs + kt;
+      if (kt == 0 && r > 0) {
+        if (prev_full) enc_wait_vm<GL_STORES>();
+        else enc_wait_vm<0>();
+      } else if (ta_i > t + 1) {
+        enc_wait_vm<2>();
+      } else {
+        enc_wait_vm<0>();
+      }
+      enc_lds_barrier();  // stage t visible to all; slots of stage t - 1 are free again
+      if (t + 1 < nstages) issue_w(kt + 1 < nk ? kt + 1 : 0, t + 1);
+      issue_next_a();
+      const uint32_t sa = lds_addr(smem) + (uint32_t)((t % GL_ASLOTS) * GL_A_B);
+      const uint32_t sw = lds_addr(smem) + (uint32_t)(GL_WBASE + (t % GL_WSLOTS) * GL_W_B);
+      // fragment reads of both k-halves issued up front (20, the LDS counter holds 15: the
+      // last five of s = 1 go out once s = 0 has landed), s = 1 lands under s = 0's MFMAs
+      u32x4 av[2][4], bv[2][GL_NJ];
+      const uint32_t pa0 = sa + fa[0], pb0 = sw + fb[0], pa1 = sa + fa[1], pb1 = sw + fb[1];
+      av[0][0] = lds_read128<0>(pa0);
+      av[0][1] = lds_read128<2048>(pa0);
+      av[0][2] = lds_read128<4096>(pa0);
+      av[0][3] = lds_read128<6144>(pa0);
+      bv[0][0] = lds_read128<0>(pb0);
+      bv[0][1] = lds_read128<2048>(pb0);
+      bv[0][2] = lds_read128<4096>(pb0);
+      bv[0][3] = lds_read128<6144>(pb0);
+      bv[0][4] = lds_read128<8192>(pb0);
+      bv[0][5] = lds_read128<10240>(pb0);
+      av[1][0] = lds_read128<0>(pa1);
+      av[1][1] = lds_read128<2048>(pa1);
+      av[1][2] = lds_read128<4096>(pa1);
+      av[1][3] = lds_read128<6144>(pa1);
+      bv[1][0] = lds_read128<0>(pb1);
+      lds_wait<5>();
+      bv[1][1] = lds_read128<2048>(pb1);
+      bv[1][2] = lds_read128<4096>(pb1);
+      bv[1][3] = lds_read128<6144>(pb1);
+      bv[1][4] = lds_read128<8192>(pb1);
+      bv[1][5] = lds_read128<10240>(pb1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if (s == 1) lds_wait<0>();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) reg_tie(av[s][i]);
+#pragma unroll
+        for (int j = 0; j < GL_NJ; ++j) reg_tie(bv[s][j]);
+#pragma unroll
+        for (int j = 0; j < GL_NJ; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8e, bv[s][j]), __builtin_bit_cast(bf16x8e, av[s][i]),
+                acc[i][j], 0, 0, 0);
+      }
+    }
+    gs += nk;
+
+    // ---- epilogue: y = acc + bias + x ; x = LayerNorm(y) (biased variance, two passes).
+    // Residual rows are loaded one 16-row block ahead (6 x 16 B per lane in flight while the
+    // previous block is summed); bias / gamma / beta come from LDS.
+    const bool full = m0 + GL_BM <= M;
+    const int nw0 = 96 * wn + 4 * g;
+    const float* xr0 = X + (int64_t)(m0 + 64 * wm + rl) * ldx + nw0;
+    auto xrow = [&](int i) __attribute__((always_inline)) {
+      const int m = m0 + 64 * wm + 16 * i + rl;
+      return X + (int64_t)(m < M ? m : M - 1) * ldx + nw0;  // rows past M: clamped reads
+    };
+    float mean[4], rstd[4];
+    {
+      f32x4 rv[2][GL_NJ];
+      const float* p0 = full ? xr0 : xrow(0);
+#pragma unroll
+      for (int j = 0; j < GL_NJ; ++j) rv[0][j] = *(const f32x4*)(p0 + 16 * j);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i + 1 < 4) {
+          const float* p1 = full ? xr0 + (int64_t)(16 * (i + 1)) * ldx : xrow(i + 1);
+#pragma unroll
+          for (int j = 0; j < GL_NJ; ++j) rv[(i + 1) & 1][j] = *(const f32x4*)(p1 + 16 * j);
+        }
+        float s = 0.0f;
+#pragma unroll
+        for (int j = 0; j < GL_NJ; ++j) {
+          acc[i][j] += rv[i & 1][j] + *(const f32x4*)(&prm[0][nw0 + 16 * j]);
+          s += (acc[i][j][0] + acc[i][j][1]) + (acc[i][j][2] + acc[i][j][3]);
+        }
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        if (g == 0) red[0][wn][64 * wm + 16 * i + rl] = s;
+      }
+    }
+    enc_lds_barrier();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 64 * wm + 16 * i + rl;
+      mean[i] = ((red[0][0][row] + red[0][1][row]) + (red[0][2][row] + red[0][3][row])) * inv_h;
+      float q = 0.0f;
+#pragma unroll
+      for (int j = 0; j < GL_NJ; ++j)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float d = acc[i][j][u] - mean[i];
+          q = fmaf(d, d, q);
+        }
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (g == 0) red[1][wn][row] = q;
+    }
+    enc_lds_barrier();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 64 * wm + 16 * i + rl;
+      const float q = (red[1][0][row] + red[1][1][row]) + (red[1][2][row] + red[1][3][row]);
+      rstd[i] = 1.0f / sqrtf(q * inv_h + eps);
+    }
+#pragma unroll
+    for (int j = 0; j < GL_NJ; ++j) {
+      const int n = nw0 + 16 * j;
+      const f32x4 gm = *(const f32x4*)(&prm[1][n]), bt = *(const f32x4*)(&prm[2][n]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[i][j][u] = (acc[i][j][u] - mean[i]) * rstd[i] * gm[u] + bt[u];
+    }
+    if (full) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t m = m0 + 64 * wm + 16 * i + rl;
+#pragma unroll
+        for (int j = 0; j < GL_NJ; ++j) {
+          const int n = nw0 + 16 * j;
+          *(f32x4*)(X + m * ldx + n) = acc[i][j];
+          *(uint2*)(X16 + m * ldx16 + n) = uint2{pack_bf16_hw(acc[i][j][0], acc[i][j][1]),
+                                                  pack_bf16_hw(acc[i][j][2], acc[i][j][3])};
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t m = m0 + 64 * wm + 16 * i + rl;
+        if (m >= M) continue;
+#pragma unroll
+        for (int j = 0; j < GL_NJ; ++j) {
+          const int n = nw0 + 16 * j;
+          *(f32x4*)(X + m * ldx + n) = acc[i][j];
+          *(uint2*)(X16 + m * ldx16 + n) = uint2{pack_bf16_hw(acc[i][j][0], acc[i][j][1]),
+                                                  pack_bf16_hw(acc[i][j][2], acc[i][j][3])};
+        }
+      }
+    }
+    prev_full = full;
   }
 }
 
@@ -812,12 +1152,20 @@ int enc_device_cus() {
   return cus;
 }
 // TT_GEMM_BIG=0 in the environment keeps every bf16 GEMM on the 128x128 kernel (A/B timing)
-bool gemm_big_disabled() {
+bool gemm_ln_disabled() {  // TT_GEMM_LN=0: unfused GEMM + LayerNorm (A/B timing)
   static const bool off = [] {
-    const char* e = getenv("TT_GEMM_BIG");
+    const char* e = getenv("TT_GEMM_LN");
     return e && e[0] == '0';
   }();
   return off;
+}
+int gemm_big_variant() {  // TT_GEMM_BIG: 0 = 128x128 tiles only, 1 = 256x128 ring (default),
+                          // 2 = 128x128 ring, two blocks per CU
+  static const int v = [] {
+    const char* e = getenv("TT_GEMM_BIG");
+    return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 1;
+  }();
+  return v;
 }
 }  // namespace
 
@@ -853,17 +1201,46 @@ extern "C" int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, i
   TT_REQUIRE(act >= 0 && act <= 2, "bad activation");
   // large M: the persistent 256x128 ring kernel (one block per CU) once there are at least
   // two tiles per CU
-  const int nbig = ((M + GB_BM - 1) / GB_BM) * ((N + GB_BN - 1) / GB_BN);
+  const int nbig = ((M + 255) / 256) * ((N + GB_BN - 1) / GB_BN);
   const int ncu = enc_device_cus();
-  if (nbig >= 2 * ncu && !gemm_big_disabled()) {
-    hipLaunchKernelGGL(k_gemm_big, dim3(ncu), dim3(512), 0, (hipStream_t)stream, A, lda, W, ldw,
-                       bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
+  const int variant = gemm_big_variant();
+  if (nbig >= 2 * ncu && variant == 2) {  // 128x128 tiles, two persistent blocks per CU
+    hipLaunchKernelGGL((k_gemm_big<128, 2>), dim3(2 * ncu), dim3(256), 0, (hipStream_t)stream, A,
+                       lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
+    return check_launch("tt_gemm_bf16(2x128x128)");
+  }
+  if (nbig >= 2 * ncu && variant == 1) {
+    hipLaunchKernelGGL((k_gemm_big<256, 3>), dim3(ncu), dim3(512), 0, (hipStream_t)stream, A, lda,
+                       W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
     return check_launch("tt_gemm_bf16(256x128)");
   }
   const int nblk = ((M + GM_BM - 1) / GM_BM) * ((N + GM_BN - 1) / GM_BN);
   hipLaunchKernelGGL(k_gemm<uint16_t>, dim3(nblk), dim3(256), 0, (hipStream_t)stream, A, lda, W,
                      ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
   return check_launch("tt_gemm_bf16");
+}
+
+extern "C" int tt_gemm_ln_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
+                               const float* bias, const float* gamma, const float* beta,
+                               float eps, float* x, int64_t ldx, uint16_t* x_bf16, int64_t ldx16,
+                               int32_t M, int32_t H, int32_t K, void* stream) {
+  TT_REQUIRE(M >= 0 && K >= 0, "negative size");
+  if (M == 0) return TT_OK;
+  if (H != GL_H) return fail(TT_ERR_UNSUPPORTED, "tt_gemm_ln_bf16: H must be 384");
+  if (K % 64 != 0 || K == 0) return fail(TT_ERR_UNSUPPORTED, "tt_gemm_ln_bf16: need K % 64 == 0");
+  TT_REQUIRE(A && W && bias && gamma && beta && x && x_bf16, "null pointer");
+  TT_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0,
+             "A/W must be 16-B aligned with lda, ldw % 8 == 0");
+  TT_REQUIRE(ldx % 4 == 0 && ldx16 % 4 == 0 && ((uintptr_t)x % 16) == 0 &&
+                 ((uintptr_t)x_bf16 % 8) == 0 && ((uintptr_t)bias % 16) == 0 &&
+                 ((uintptr_t)gamma % 16) == 0 && ((uintptr_t)beta % 16) == 0,
+             "x / bias / gamma / beta must be 16-B aligned (x_bf16 8-B), ldx, ldx16 % 4 == 0");
+  const int ntiles = (M + GL_BM - 1) / GL_BM;
+  const int ncu = enc_device_cus();
+  const int grid = ntiles < ncu ? ntiles : ncu;
+  hipLaunchKernelGGL(k_gemm_ln, dim3(grid), dim3(512), 0, (hipStream_t)stream, A, lda, W, ldw,
+                     bias, gamma, beta, eps, x, ldx, x_bf16, ldx16, M, K);
+  return check_launch("tt_gemm_ln_bf16");
 }
 
 extern "C" int tt_layernorm_f32(const float* x, int64_t ldx, const float* gamma,
@@ -1019,6 +1396,8 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
   TT_REQUIRE(H > 0 && H <= 1024 && I > 0 && NL >= 0 && m->heads > 0, "bad model dims");
   TT_REQUIRE(max_len <= m->max_positions, "max_len > max_position_embeddings");
   const bool bf = prec == TT_PREC_BF16;
+  // bf16 path at H = 384 with row tiles filling the chip: GEMM + LayerNorm fused (k_gemm_ln)
+  const bool fuse_ln = bf && H == GL_H && I % 64 == 0 && !gemm_ln_disabled();
   EncWs w = enc_carve((char*)workspace, T, H, I, bf);
   if (!workspace || workspace_bytes < (int64_t)w.total)
     return fail(TT_ERR_WORKSPACE, "tt_bert_encode: workspace too small");
@@ -1053,28 +1432,40 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
                                    H, nullptr, stream);
     if (rc) return rc;
     // y = ctx Wo^T + bo + x ; x = LN(y)
-    rc = bf ? tt_gemm_bf16(w.ctx16, H, L.wo_bf16, H, L.bo, w.x, H, w.y, H, nullptr, 0, (int)T, H, H,
-                           ACT_NONE, stream)
-            : tt_gemm_f32(w.ctx, H, L.wo, H, L.bo, w.x, H, w.y, H, nullptr, 0, (int)T, H, H,
-                          ACT_NONE, stream);
-    if (rc) return rc;
-    rc = tt_layernorm_f32(w.y, H, L.ln1_g, L.ln1_b, m->ln_eps, w.x, H, bf ? w.x16 : nullptr, H, T,
-                          H, stream);
-    if (rc) return rc;
+    if (fuse_ln) {
+      rc = tt_gemm_ln_bf16(w.ctx16, H, L.wo_bf16, H, L.bo, L.ln1_g, L.ln1_b, m->ln_eps, w.x, H,
+                           w.x16, H, (int)T, H, H, stream);
+      if (rc) return rc;
+    } else {
+      rc = bf ? tt_gemm_bf16(w.ctx16, H, L.wo_bf16, H, L.bo, w.x, H, w.y, H, nullptr, 0, (int)T, H,
+                             H, ACT_NONE, stream)
+              : tt_gemm_f32(w.ctx, H, L.wo, H, L.bo, w.x, H, w.y, H, nullptr, 0, (int)T, H, H,
+                            ACT_NONE, stream);
+      if (rc) return rc;
+      rc = tt_layernorm_f32(w.y, H, L.ln1_g, L.ln1_b, m->ln_eps, w.x, H, bf ? w.x16 : nullptr, H,
+                            T, H, stream);
+      if (rc) return rc;
+    }
     // ff = GELU(x W1^T + b1) ; y = ff W2^T + b2 + x ; x = LN(y)
     rc = bf ? tt_gemm_bf16(w.x16, H, L.w1_bf16, H, L.b1, nullptr, 0, nullptr, I, w.ff16, I, (int)T,
                            I, H, ACT_GELU, stream)
             : tt_gemm_f32(w.x, H, L.w1, H, L.b1, nullptr, 0, w.ff, I, nullptr, 0, (int)T, I, H,
                           ACT_GELU, stream);
     if (rc) return rc;
-    rc = bf ? tt_gemm_bf16(w.ff16, I, L.w2_bf16, I, L.b2, w.x, H, w.y, H, nullptr, 0, (int)T, H, I,
-                           ACT_NONE, stream)
-            : tt_gemm_f32(w.ff, I, L.w2, I, L.b2, w.x, H, w.y, H, nullptr, 0, (int)T, H, I, ACT_NONE,
-                          stream);
-    if (rc) return rc;
-    rc = tt_layernorm_f32(w.y, H, L.ln2_g, L.ln2_b, m->ln_eps, w.x, H, bf ? w.x16 : nullptr, H, T,
-                          H, stream);
-    if (rc) return rc;
+    if (fuse_ln) {
+      rc = tt_gemm_ln_bf16(w.ff16, I, L.w2_bf16, I, L.b2, L.ln2_g, L.ln2_b, m->ln_eps, w.x, H,
+                           w.x16, H, (int)T, H, I, stream);
+      if (rc) return rc;
+    } else {
+      rc = bf ? tt_gemm_bf16(w.ff16, I, L.w2_bf16, I, L.b2, w.x, H, w.y, H, nullptr, 0, (int)T, H,
+                             I, ACT_NONE, stream)
+              : tt_gemm_f32(w.ff, I, L.w2, I, L.b2, w.x, H, w.y, H, nullptr, 0, (int)T, H, I,
+                            ACT_NONE, stream);
+      if (rc) return rc;
+      rc = tt_layernorm_f32(w.y, H, L.ln2_g, L.ln2_b, m->ln_eps, w.x, H, bf ? w.x16 : nullptr, H,
+                            T, H, stream);
+      if (rc) return rc;
+    }
   }
   hipLaunchKernelGGL(k_mean_pool, dim3((unsigned)n_seq), dim3(256), 0, st, w.x, (int64_t)H,
                      cu_seqlens, H, out_pooled, ld_out);

@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("TWOTOWER_HIP_LIB") or os.path.join(_PKG_ROOT, "lib", 
 CSRC = os.path.join(_PKG_ROOT, "csrc")
 
 TT_OK = 0
+TT_ERR_INVALID, TT_ERR_LAUNCH, TT_ERR_UNSUPPORTED, TT_ERR_WORKSPACE = -1, -2, -3, -4
 TT_SHARD_PROBES = 16  # include/twotower_hip.h
 TT_SHARD_SAMPLE_STRIDE = 16
 TT_NORM_ADD_EPS = 0
@@ -94,6 +95,8 @@ SIGNATURES = {
                                    _i32, _i32, _i32, _i32, _vp]),
     "tt_gemm_bf16": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64,
                                     _i32, _i32, _i32, _i32, _vp]),
+    "tt_gemm_ln_bf16": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, ctypes.c_float, _vp,
+                                        _i64, _vp, _i64, _i32, _i32, _i32, _vp]),
     "tt_layernorm_f32": (ctypes.c_int, [_vp, _i64, _vp, _vp, ctypes.c_float, _vp, _i64, _vp, _i64,
                                         _i64, _i32, _vp]),
     "tt_attention_varlen": (ctypes.c_int, [_vp, _i64, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _i64,
