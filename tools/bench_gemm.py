@@ -20,13 +20,20 @@ def main():
     ap.add_argument("--prec", default="bf16")
     ap.add_argument("--M", type=int, default=18340)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", default=None, help="N,K,act,res of one shape (e.g. 1152,384,0,0)")
+    ap.add_argument("--no-torch", action="store_true")
+    ap.add_argument("--no-ln", action="store_true")
     a = ap.parse_args()
     L = _lib.lib()
     dt = torch.bfloat16 if a.prec == "bf16" else torch.float32
     fn = L.tt_gemm_bf16 if a.prec == "bf16" else L.tt_gemm_f32
     out = {}
-    for (N, K, act, res) in [(1152, 384, 0, False), (384, 384, 0, True), (1536, 384, 1, False),
-                             (384, 1536, 0, True)]:
+    shapes = [(1152, 384, 0, False), (384, 384, 0, True), (1536, 384, 1, False),
+              (384, 1536, 0, True)]
+    if a.only:
+        n_, k_, act_, res_ = (int(v) for v in a.only.split(","))
+        shapes = [(n_, k_, act_, bool(res_))]
+    for (N, K, act, res) in shapes:
         A = torch.randn(a.M, K, device="cuda").to(dt)
         W = torch.randn(N, K, device="cuda").to(dt)
         b = torch.randn(N, device="cuda")
@@ -52,6 +59,10 @@ def main():
         ms = e0.elapsed_time(e1) / a.iters
         # library reference point (hipBLASLt through torch): same shape, bf16/f32 in and out
         bb = b.to(dt)
+        if a.no_torch:
+            out[f"N{N}_K{K}"] = {"us": round(ms * 1e3, 1),
+                                 "tflops": round(2 * a.M * N * K / ms / 1e9, 1)}
+            continue
         for _ in range(3):
             torch.nn.functional.linear(A, W, bb)
         e0.record()
@@ -62,7 +73,7 @@ def main():
         ms_t = e0.elapsed_time(e1) / a.iters
         out[f"N{N}_K{K}"] = {"us": round(ms * 1e3, 1), "tflops": round(2 * a.M * N * K / ms / 1e9, 1),
                              "torch_tflops": round(2 * a.M * N * K / ms_t / 1e9, 1)}
-    if a.prec == "bf16":  # fused GEMM + LayerNorm (Wo / W2 of a layer), in place
+    if a.prec == "bf16" and not a.no_ln:  # fused GEMM + LayerNorm (Wo / W2 of a layer), in place
         for K in (384, 1536):
             A = torch.randn(a.M, K, device="cuda").to(dt)
             W = (torch.randn(384, K, device="cuda") / K ** 0.5).to(dt)

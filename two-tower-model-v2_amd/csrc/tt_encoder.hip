@@ -102,7 +102,10 @@ __device__ __forceinline__ int enc_xcd_remap(int bid, int nblk) {
 // vector-memory stores the lane issued when it is a compile-time count (16 per output copy on
 // the full-tile path, 8 for a bf16-only output), or 0 for the element-wise edge path: a persistent caller waits for
 // vmcnt(that count) before reusing its DMA ring, without draining the stores.
-template <bool FAST>
+// ACTC >= 0: the activation as a compile-time constant (no per-element branch); BFO: the
+// caller guarantees the bf16-only output form (C == NULL, res == NULL, C16 16-B aligned,
+// ldc16 % 8 == 0) -- the persistent kernel's specialisations.
+template <bool FAST, int ACTC = -1, bool BFO = false>
 __device__ __forceinline__ int gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, int nw0,
                                                    int lane, int M, int N,
                                                    const float* __restrict__ bias,
@@ -111,6 +114,11 @@ __device__ __forceinline__ int gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, i
                                                    uint16_t* __restrict__ C16, int64_t ldc16,
                                                    int act, const float* lbias = nullptr) {
   const int g = lane >> 4, rl = lane & 15;
+  if constexpr (ACTC >= 0) act = ACTC;
+  if constexpr (BFO) {
+    C = nullptr;
+    res = nullptr;
+  }
   const bool vec = (N % 4) == 0 && (ldc % 4) == 0 && (!res || (ldr % 4) == 0) &&
                    (!C16 || (ldc16 % 4) == 0) && ((uintptr_t)bias % 16) == 0 &&
                    ((uintptr_t)res % 16) == 0 && ((uintptr_t)C % 16) == 0 &&
@@ -131,7 +139,7 @@ __device__ __forceinline__ int gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, i
         for (int j = 0; j < 4; ++j)
           rv[i][j] = *(const f32x4*)(res + (int64_t)(mw0 + 16 * i + rl) * ldr + nw0 + 16 * j + 4 * g);
     }
-    if (!C && (ldc16 % 8) == 0 && ((uintptr_t)C16 % 16) == 0) {
+    if (BFO || (!C && (ldc16 % 8) == 0 && ((uintptr_t)C16 % 16) == 0)) {
       // bf16-only output: v_permlane16_swap pairs blocks j0 = 2 jp and j1 = 2 jp + 1 so that
       // each lane holds 8 consecutive columns -> one 16-B store (8 per lane instead of 16
       // 8-B ones; the epilogue was store-issue-bound).  After the swap lane row g holds
@@ -336,7 +344,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_
 // DMA layout / swizzle / fragment reads / epilogue as k_gemm.
 constexpr int GB_BN = 128, GB_MAXN = 2048;
 
-template <int GB_BM, int GB_SLOTS>
+template <int GB_BM, int GB_SLOTS, int ACT, bool BFO>
 __global__ __launch_bounds__(GB_BM * 2, 512 / (GB_BM * 2)) void k_gemm_big(const uint16_t* __restrict__ A, int64_t lda,
                                                      const uint16_t* __restrict__ W, int64_t ldw,
                                                      const float* __restrict__ bias,
@@ -491,7 +499,7 @@ __global__ __launch_bounds__(GB_BM * 2, 512 / (GB_BM * 2)) void k_gemm_big(const
       }
     }
     if (TT_GEXP_NOSTORE != 1)
-      nst = gemm_wave_epilogue<true>(acc, (lt / n_tn) * GB_BM + 64 * wm, (lt % n_tn) * GB_BN + 64 * wn,
+      nst = gemm_wave_epilogue<true, ACT, BFO>(acc, (lt / n_tn) * GB_BM + 64 * wm, (lt % n_tn) * GB_BN + 64 * wn,
                                lane, M, N, bias, res, ldr, C, ldc, C16, ldc16, act,
                                lds_bias ? sbias : nullptr);
     else if (acc[0][0][0] == 123.456f && acc[3][3][3] == 1.5f) C[0] = acc[1][1][1];
@@ -960,6 +968,23 @@ __global__ __launch_bounds__(256) void k_attn32_mfma(const TI* __restrict__ qkv,
   const int vst = ((Lk + 127) & ~127) + (BF ? 8 : 4);
   char* Ks = sm;
   char* Vt = sm + (size_t)Lk * KROW;
+  if constexpr (sizeof(TI) == 2) {
+    // bf16 input: 16-B chunks (8 dims) of each K / V row -- one global load each (the head's
+    // 64-B slice of a token row is 4 chunks); K rows copied whole, V transposed into V^T
+    for (int e = tid; e < Lk * 4; e += 256) {
+      const int j = e >> 2, c8 = 8 * (e & 3);
+      u32x4 kq = {0u, 0u, 0u, 0u}, vq = {0u, 0u, 0u, 0u};
+      if (j < L) {
+        const TI* row = qkv + (int64_t)(t0 + j) * ldq + h * DH + c8;
+        kq = *(const u32x4*)(row + H);
+        vq = *(const u32x4*)(row + 2 * H);
+      }
+      *(u32x4*)(Ks + j * KROW + c8 * 2) = kq;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        *(uint16_t*)(Vt + ((size_t)(c8 + i) * vst + j) * 2) = (uint16_t)(vq[i >> 1] >> (16 * (i & 1)));
+    }
+  } else
   for (int e = tid; e < Lk * DH; e += 256) {
     const int j = e / DH, c = e % DH;
     float kv = 0.0f, vv = 0.0f;
@@ -1084,10 +1109,10 @@ __global__ __launch_bounds__(256) void k_attn32_mfma(const TI* __restrict__ qkv,
       for (int db = 0; db < 2; ++db) {
         const f32x4 o = acc[db] * inv;
         if (out) *(f32x4*)(out + (int64_t)(t0 + q0 + ql) * ldo + h * DH + 16 * db + 4 * g) = o;
-        if (out16) {
+        if (out16) {  // 4 consecutive dims: one 8-B store
           uint16_t* o16 = out16 + (int64_t)(t0 + q0 + ql) * ldo + h * DH + 16 * db + 4 * g;
-#pragma unroll
-          for (int v = 0; v < 4; ++v) o16[v] = f32_to_bf16_rne(o[v]);
+          *(uint2*)o16 = uint2{(uint32_t)f32_to_bf16_rne(o[0]) | ((uint32_t)f32_to_bf16_rne(o[1]) << 16),
+                               (uint32_t)f32_to_bf16_rne(o[2]) | ((uint32_t)f32_to_bf16_rne(o[3]) << 16)};
         }
       }
     }
@@ -1204,15 +1229,22 @@ extern "C" int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, i
   const int nbig = ((M + 255) / 256) * ((N + GB_BN - 1) / GB_BN);
   const int ncu = enc_device_cus();
   const int variant = gemm_big_variant();
-  if (nbig >= 2 * ncu && variant == 2) {  // 128x128 tiles, two persistent blocks per CU
-    hipLaunchKernelGGL((k_gemm_big<128, 2>), dim3(2 * ncu), dim3(256), 0, (hipStream_t)stream, A,
-                       lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
-    return check_launch("tt_gemm_bf16(2x128x128)");
-  }
-  if (nbig >= 2 * ncu && variant == 1) {
-    hipLaunchKernelGGL((k_gemm_big<256, 3>), dim3(ncu), dim3(512), 0, (hipStream_t)stream, A, lda,
-                       W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
-    return check_launch("tt_gemm_bf16(256x128)");
+  if (nbig >= 2 * ncu && variant >= 1) {
+    // specialisations: activation constant; bf16-only output (QKV, FFN1) without C / residual
+    const bool bfo = !C && !residual && C_bf16 && ldc16 % 8 == 0 && ((uintptr_t)C_bf16 % 16) == 0;
+    auto launch = [&](auto kern, int blocks, int threads) {
+      hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, A, lda, W, ldw,
+                         bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
+      return check_launch("tt_gemm_bf16(persistent)");
+    };
+    if (variant == 2) {  // 128x128 tiles, two persistent blocks per CU
+      if (bfo && act == ACT_NONE) return launch(k_gemm_big<128, 2, ACT_NONE, true>, 2 * ncu, 256);
+      if (bfo && act == ACT_GELU) return launch(k_gemm_big<128, 2, ACT_GELU, true>, 2 * ncu, 256);
+      return launch(k_gemm_big<128, 2, -1, false>, 2 * ncu, 256);
+    }
+    if (bfo && act == ACT_NONE) return launch(k_gemm_big<256, 3, ACT_NONE, true>, ncu, 512);
+    if (bfo && act == ACT_GELU) return launch(k_gemm_big<256, 3, ACT_GELU, true>, ncu, 512);
+    return launch(k_gemm_big<256, 3, -1, false>, ncu, 512);
   }
   const int nblk = ((M + GM_BM - 1) / GM_BM) * ((N + GM_BN - 1) / GM_BN);
   hipLaunchKernelGGL(k_gemm<uint16_t>, dim3(nblk), dim3(256), 0, (hipStream_t)stream, A, lda, W,
@@ -1294,8 +1326,9 @@ extern "C" int tt_attention_varlen_bf16(const uint16_t* qkv, int64_t ld_qkv,
   if (n_seq == 0) return TT_OK;
   TT_REQUIRE(max_len >= 1 && max_len <= 512, "max_len must be in [1, 512]");
   TT_REQUIRE(qkv && cu_seqlens && (out || out_bf16), "null pointer");
-  TT_REQUIRE(ld_qkv % 8 == 0 && ld_out % 4 == 0 && H % 8 == 0 && ((uintptr_t)qkv % 16) == 0,
-             "qkv must be 16-B aligned rows");
+  TT_REQUIRE(ld_qkv % 8 == 0 && ld_out % 4 == 0 && H % 8 == 0 && ((uintptr_t)qkv % 16) == 0 &&
+                 ((uintptr_t)out % 16) == 0 && ((uintptr_t)out_bf16 % 8) == 0,
+             "qkv must be 16-B aligned rows (out 16-B, out_bf16 8-B aligned)");
   if (H / heads != 32)
     return fail(TT_ERR_UNSUPPORTED, "tt_attention_varlen_bf16: head dim must be 32");
   const size_t smem = attn32_smem(max_len, true);
