@@ -69,7 +69,9 @@ def test_gemm_bf16_vs_torch(M, N, K):
                                            (65536, 1000, 384, 1, False),
                                            (66000, 1536, 384, 2, True),
                                            (70000, 1152, 64, 0, False),
-                                           (40000, 2048, 128, 1, True)])
+                                           (40000, 2048, 128, 1, True),
+                                           (50001, 1536, 384, 1, False),
+                                           (33333, 1100, 192, 0, False)])
 def test_gemm_bf16_large_m_ring_kernel(M, N, K, act, res):
     """M large enough for the 256x128 ring kernel (k_gemm_big): same results as the
     128x128 kernel's contract -- exact bf16 products, f32 sums, fused epilogue, ragged N/M."""

@@ -507,6 +507,167 @@ __global__ __launch_bounds__(GB_BM * 2, 512 / (GB_BM * 2)) void k_gemm_big(const
   }
 }
 
+// Wide-tile variant of k_gemm_big: 256 x 256 tiles (8 waves as 4 (M) x 2 (N) of 64 x 128),
+// 2-slot ring of 64-KB stages one stage ahead.  Per stage a CU moves 64 KB HBM/L2 -> LDS for
+// 8.4 MFLOP (131 flop/B, vs 87 for 256 x 128), which is what bounds the persistent 256 x 128
+// kernel at K = 384 (the MFMA pipes sat idle ~70 % waiting for its 48-KB stages).  Wave
+// epilogue = two gemm_wave_epilogue calls (64-column halves).
+template <int ACT, bool BFO>
+__global__ __launch_bounds__(512, 1) void k_gemm_wide(const uint16_t* __restrict__ A, int64_t lda,
+                                                      const uint16_t* __restrict__ W, int64_t ldw,
+                                                      const float* __restrict__ bias,
+                                                      const float* __restrict__ res, int64_t ldr,
+                                                      float* __restrict__ C, int64_t ldc,
+                                                      uint16_t* __restrict__ C16, int64_t ldc16,
+                                                      int M, int N, int K, int act) {
+  constexpr int BM = 256, BN = 256, BK = 64, EPC = 8, SLOTS = 2;
+  constexpr int A_B = BM * 128, STAGE_B = A_B + BN * 128;
+  __shared__ __attribute__((aligned(16))) char smem[SLOTS * STAGE_B];
+  __shared__ __attribute__((aligned(16))) float sbias[GB_MAXN];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const bool lds_bias = bias && N <= GB_MAXN && ((uintptr_t)bias % 16) == 0;
+  if (lds_bias)
+    for (int e = tid; e < N; e += 512) sbias[e] = bias[e];  // visible after stage 0's barrier
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int n_tn = (N + BN - 1) / BN;
+  const int ntiles = ((M + BM - 1) / BM) * n_tn;
+  const int nk = K / BK;
+  auto tile_of = [&](int r) { return enc_xcd_remap(blockIdx.x + r * gridDim.x, ntiles); };
+  const int n_mine = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+
+  // DMA: A and W = 32 pieces each of 8 rows x 128 B; wave w issues pieces w + 8 j (j < 4) of
+  // both.  Row 8 (w + 8 j) + (lane >> 3): the swizzle (row >> 1) & 7 does not depend on j.
+  const int drow = 8 * w + (lane >> 3);
+  const int dchunk = ((lane & 7) ^ ((drow >> 1) & 7)) * EPC;
+  struct Offs {
+    int64_t a[4], w[4];
+  };
+  auto offsets = [&](int lt) __attribute__((always_inline)) {
+    Offs o;
+    const int m0 = (lt / n_tn) * BM, n0 = (lt % n_tn) * BN;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int am = m0 + drow + 64 * j;
+      am = am < M ? am : M - 1;
+      o.a[j] = (int64_t)am * lda + dchunk;
+      int wr = n0 + drow + 64 * j;
+      wr = wr < N ? wr : N - 1;  // rows past N: clamped loads, no stores
+      o.w[j] = (int64_t)wr * ldw + dchunk;
+    }
+    return o;
+  };
+  auto issue = [&](const Offs& o, int kt, int gs) __attribute__((always_inline)) {
+    char* st = smem + (gs & 1) * STAGE_B;
+    const int64_t k0 = (int64_t)kt * BK;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(A + o.a[j] + k0),
+          (__attribute__((address_space(3))) void*)(st + 1024 * (w + 8 * j)), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(W + o.w[j] + k0),
+          (__attribute__((address_space(3))) void*)(st + A_B + 1024 * (w + 8 * j)), 16, 0, 0);
+  };
+
+  // fragment rows 64 wm + 16 i + rl (A) / 128 wn + 16 j + rl (W): swizzle (rl >> 1) & 7 for
+  // every i, j -> blocks are ds_read immediates (2048 B apart)
+  const int g = lane >> 4, rl = lane & 15;
+  uint32_t fa[2], fb[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int c = (4 * s + g) ^ ((rl >> 1) & 7);
+    fa[s] = (64 * wm + rl) * 128 + 16 * c;
+    fb[s] = A_B + (128 * wn + rl) * 128 + 16 * c;
+  }
+
+  if (n_mine <= 0) return;
+  int r_i = 0, k_i = 0, g_i = 0;
+  Offs o_i = offsets(tile_of(0));
+  auto issue_next = [&]() __attribute__((always_inline)) {
+    if (r_i >= n_mine) return;
+    issue(o_i, k_i, g_i);
+    ++g_i;
+    if (++k_i == nk) {
+      k_i = 0;
+      if (++r_i < n_mine) o_i = offsets(tile_of(r_i));
+    }
+  };
+  issue_next();
+  int gs = 0, nst = 0;
+  for (int r = 0; r < n_mine; ++r) {
+    const int lt = tile_of(r);
+    f32x4 acc[2][4][4];  // [column half][i][j]
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt) {
+      // younger than this stage's loads: at a tile's first stage, the previous epilogue's
+      // stores (nst per lane; an edge tile's element-wise epilogue: drain)
+      if (kt == 0 && r > 0 && nst == 16) enc_wait_vm<16>();
+      else if (kt == 0 && r > 0 && nst == 32) enc_wait_vm<32>();
+      else enc_wait_vm<0>();
+      enc_lds_barrier();  // stage visible to all; the other slot is free again
+      issue_next();
+      const uint32_t sb = lds_addr(smem) + (uint32_t)(((gs + kt) & 1) * STAGE_B);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const uint32_t pa = sb + fa[s], pb = sb + fb[s];
+        u32x4 av[4], bv[8];
+        av[0] = lds_read128<0>(pa);
+        av[1] = lds_read128<2048>(pa);
+        av[2] = lds_read128<4096>(pa);
+        av[3] = lds_read128<6144>(pa);
+        bv[0] = lds_read128<0>(pb);
+        bv[1] = lds_read128<2048>(pb);
+        bv[2] = lds_read128<4096>(pb);
+        bv[3] = lds_read128<6144>(pb);
+        bv[4] = lds_read128<8192>(pb);
+        bv[5] = lds_read128<10240>(pb);
+        bv[6] = lds_read128<12288>(pb);
+        bv[7] = lds_read128<14336>(pb);
+        lds_wait<4>();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) reg_tie(av[i]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) reg_tie(bv[j]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8e, bv[j]), __builtin_bit_cast(bf16x8e, av[i]),
+                acc[0][i][j], 0, 0, 0);
+        lds_wait<0>();
+#pragma unroll
+        for (int j = 4; j < 8; ++j) reg_tie(bv[j]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8e, bv[4 + j]), __builtin_bit_cast(bf16x8e, av[i]),
+                acc[1][i][j], 0, 0, 0);
+      }
+    }
+    const int m0 = (lt / n_tn) * BM + 64 * wm, n0 = (lt % n_tn) * BN + 128 * wn;
+    nst = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = gemm_wave_epilogue<true, ACT, BFO>(acc[h], m0, n0 + 64 * h, lane, M, N, bias,
+                                                       res, ldr, C, ldc, C16, ldc16, act,
+                                                       lds_bias ? sbias : nullptr);
+      nst = (h == 0 || (c > 0 && nst > 0)) ? nst + c : 0;
+    }
+    gs += nk;
+  }
+}
+
 // Fused GEMM + LayerNorm for the two H-wide GEMMs of a BERT layer (bf16 path):
 //   BertSelfOutput / BertOutput: x = LayerNorm(A . W^T + bias + x)      (A = ctx, K = H; or
 //   A = GELU(ffn), K = I).  One block owns whole 384-wide rows, so the LayerNorm statistics
@@ -1184,11 +1345,18 @@ bool gemm_ln_disabled() {  // TT_GEMM_LN=0: unfused GEMM + LayerNorm (A/B timing
   }();
   return off;
 }
+bool gemm_wide_disabled() {  // TT_GEMM_WIDE=0: keep 256x128 tiles for the wide GEMMs too
+  static const bool off = [] {
+    const char* e = getenv("TT_GEMM_WIDE");
+    return e && e[0] == '0';
+  }();
+  return off;
+}
 int gemm_big_variant() {  // TT_GEMM_BIG: 0 = 128x128 tiles only, 1 = 256x128 ring (default),
-                          // 2 = 128x128 ring, two blocks per CU
+                          // 2 = 128x128 ring, two blocks per CU, 3 = 256x256 ring
   static const int v = [] {
     const char* e = getenv("TT_GEMM_BIG");
-    return e && e[0] >= '0' && e[0] <= '2' ? e[0] - '0' : 1;
+    return e && e[0] >= '0' && e[0] <= '3' ? e[0] - '0' : 1;
   }();
   return v;
 }
@@ -1237,6 +1405,13 @@ extern "C" int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, i
                          bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
       return check_launch("tt_gemm_bf16(persistent)");
     };
+    // default: 256x256 tiles for the wide bf16-only GEMMs (QKV N = 1152, FFN1 N = 1536:
+    // 534 / 747 us vs 586 / 824 us with 256x128 at 370k tokens), 256x128 otherwise
+    if (variant == 3 || (variant == 1 && bfo && N >= 1024 && !gemm_wide_disabled())) {  // 256x256
+      if (bfo && act == ACT_NONE) return launch(k_gemm_wide<ACT_NONE, true>, ncu, 512);
+      if (bfo && act == ACT_GELU) return launch(k_gemm_wide<ACT_GELU, true>, ncu, 512);
+      return launch(k_gemm_wide<-1, false>, ncu, 512);
+    }
     if (variant == 2) {  // 128x128 tiles, two persistent blocks per CU
       if (bfo && act == ACT_NONE) return launch(k_gemm_big<128, 2, ACT_NONE, true>, 2 * ncu, 256);
       if (bfo && act == ACT_GELU) return launch(k_gemm_big<128, 2, ACT_GELU, true>, 2 * ncu, 256);
