@@ -896,6 +896,155 @@ __global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict_
   }
 }
 
+// Register-resident variant of k_select_wave, used when n_slabs <= 64 (every level the
+// plans here produce): lane s holds slab s's count, and item e of the query's candidate
+// sequence (slabs in order) lives in lane e % 64, register e / 64.  Its slab is found by
+// walking the wave-uniform slab offsets that overlap the item's 64-wide range, so every list
+// load of the query is issued before the first use -- one memory latency per query instead
+// of one per 4 entries of its longest slab -- and no LDS buffer caps the occupancy.  Same
+// outputs as k_select_wave.
+__global__ __launch_bounds__(256) void k_select_reg(const uint64_t* __restrict__ lists,
+                                                    const int* __restrict__ counts, int n_slabs,
+                                                    int k, int J, const float* __restrict__ eps2,
+                                                    int mode, float* __restrict__ theta_out,
+                                                    float* __restrict__ aref,
+                                                    uint64_t* __restrict__ band,
+                                                    int* __restrict__ band_n,
+                                                    int* __restrict__ flags, int* qsel,
+                                                    int* qsel_n, int nq,
+                                                    const float* __restrict__ stats,
+                                                    int* __restrict__ pcount,
+                                                    float* __restrict__ smax_out) {
+  const int lane = threadIdx.x & 63;
+  const int qid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (qid >= nq) return;  // the whole wave (no block-level barriers below)
+  if (flags[qid]) {
+    if (lane == 0 && mode == 0) theta_out[qid] = __builtin_huge_valf();
+    return;
+  }
+  const int* qc = counts + (int64_t)qid * n_slabs;
+  const uint64_t* ql = lists + (int64_t)qid * n_slabs * FL_CAP;
+  const int c = lane < n_slabs ? qc[lane] : 0;
+  int incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    incl += lane >= o ? y : 0;
+  }
+  const int total = __shfl(incl, 63, 64);
+  if (__ballot(c > FL_CAP) != 0ull || total > SW_CAP) {
+    if (lane == 0) {
+      flag_query(qid, flags, qsel, qsel_n);
+      if (mode == 0) theta_out[qid] = __builtin_huge_valf();
+    }
+    return;
+  }
+  const int excl = incl - c;
+  constexpr int PER = SW_CAP / 64;
+  const int ni = (total + 63) / 64;
+  uint32_t hv[PER], lo[PER];
+  // item e = lane + 64 i lives in the last slab with excl <= e: binary search over the
+  // lanes' excl values (non-decreasing; an empty slab shares its successor's excl)
+  // lanes past n_slabs hold excl = INT_MAX: never <= a valid item
+  const int exs = lane < n_slabs ? excl : 0x7fffffff;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    hv[i] = 0u;  // 0 = below every key
+    lo[i] = 0u;
+  }
+  for (int i0 = 0; i0 < ni; i0 += 4) {
+    uint32_t off[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = lane + 64 * (i0 + u);
+      int sl = 0;
+#pragma unroll
+      for (int b = 5; b >= 0; --b) {
+        const int cand = sl + (1 << b);
+        if (__shfl(exs, cand & 63, 64) <= e) sl = cand;
+      }
+      // every lane takes part in the bpermute (an inactive source lane returns garbage)
+      const int base = __shfl(exs, sl, 64);
+      off[u] = e < total ? (uint32_t)(sl * FL_CAP + (e - base)) : 0xffffffffu;
+    }
+    uint64_t key[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) key[u] = off[u] != 0xffffffffu ? ql[off[u]] : 0ull;
+#pragma unroll
+    for (int i = 0; i < PER; i += 4) {
+      if (i == i0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          hv[i + u] = (uint32_t)(key[u] >> 32);
+          lo[i + u] = (uint32_t)key[u];
+        }
+      }
+    }
+  }
+  const int R = mode == 0 ? J : k;
+  if (total < R) {  // fewer than R candidates: a_J = -inf (sample) / cannot certify (full)
+    if (lane == 0) {
+      if (mode == 0) {
+        theta_out[qid] = -__builtin_huge_valf();
+        aref[qid] = -__builtin_huge_valf();
+        if (smax_out) smax_out[qid] = -__builtin_huge_valf();
+      } else {
+        flag_query(qid, flags, qsel, qsel_n);
+      }
+    }
+    return;
+  }
+  uint32_t T = 0;
+  for (int bit = 31; bit >= 0; --bit) {
+    const uint32_t cand = T | (1u << bit);
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      if (i < ni) cnt += hv[i] >= cand ? 1 : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if (cnt >= R) T = cand;
+  }
+  const float A = key_float(T);
+  if (mode == 0) {
+    if (smax_out) {  // sharded: the sample's best a (upper end of the probe range)
+      uint32_t m = 0;
+#pragma unroll
+      for (int i = 0; i < PER; ++i)
+        if (i < ni) m = max(m, hv[i]);
+      for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+      if (lane == 0) smax_out[qid] = key_float(m);
+    }
+    if (lane == 0) {
+      theta_out[qid] = A;
+      aref[qid] = A;
+    }
+    return;
+  }
+  if (!(A >= aref[qid])) {  // the optimistic threshold did not hold
+    if (lane == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
+  const float thr = A - eps2[qid];
+  int nb = 0;
+  uint64_t* qb = band + (int64_t)qid * BAND_CAP;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    if (i < ni) {
+      const bool in = lane + 64 * i < total && key_float(hv[i]) >= thr;
+      const uint64_t bm = __ballot(in);
+      const int pos = nb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+      if (in && pos < BAND_CAP) qb[pos] = ((uint64_t)hv[i] << 32) | lo[i];
+      nb += __popcll(bm);
+    }
+  }
+  if (lane == 0) {
+    if (nb > BAND_CAP) flag_query(qid, flags, qsel, qsel_n);
+    else band_n[qid] = nb;
+  }
+}
+
 // sharded finish: pcount[q][i] = #rows over ALL shards with a >= t_i (all-reduced SUM).
 // pcount[q][0] < k: the sample threshold did not certify -> exact fallback on every shard
 // (identical decision on all ranks).  Else A_k >= t* = the highest probe with >= k rows, so
@@ -1042,6 +1191,13 @@ struct FilterPlan {
 // <= SEL_CAP/2 rows and is scored densely (every row a candidate); the others stream through
 // the ring kernel.  J = rows of a sample level's top list that feed the next threshold: the
 // full catalog has ~16*J rows above a_J(stride-16 sample), comfortably >= k.
+static bool select_reg_disabled() {  // TT_SELECT_REG=0: LDS-staged k_select_wave (A/B)
+  static const bool off = [] {
+    const char* e = getenv("TT_SELECT_REG");
+    return e && e[0] == '0';
+  }();
+  return off;
+}
 static int device_cus() {
   static const int cus = [] {
     int d = 0, v = 0;
@@ -1289,10 +1445,11 @@ int filter_level(const FilterPlan& p, const FilterWs& w, int li, int mode, const
   if (rc) return rc;
   if (last && ev_stop && hipEventRecord((hipEvent_t)ev_stop, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "hipEventRecord(stop)");
-  hipLaunchKernelGGL(k_select_wave, dim3((nq + 3) / 4), dim3(256), 0, st, w.lists, w.counts,
+  auto sel = L.n_slabs <= 64 && mode != 2 && !select_reg_disabled() ? k_select_reg : k_select_wave;
+  hipLaunchKernelGGL(sel, dim3((nq + 3) / 4), dim3(256), 0, st, w.lists, w.counts,
                      L.n_slabs, k, p.J, w.eps2, mode, w.theta, w.aref, w.band, w.band_n, w.flags,
                      w.qsel, w.qsel_n, nq, stats, pcount, smax_out);
-  return check_launch("k_select_wave");
+  return check_launch("k_select");
 }
 
 // the full level's threshold: aref = theta (a_J of the last sample, global max when sharded),
