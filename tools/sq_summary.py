@@ -9,7 +9,7 @@ import os
 import sys
 
 
-def main(d="gpurun_out", kern="k_filter_ring<384, true>"):
+def main(d="gpurun_out", kern="k_filter_ring<384, 1>"):
     res = collections.defaultdict(dict)
     for f in sorted(glob.glob(os.path.join(d, "sq_lib_*_*/run_counter_collection.csv"))):
         var = os.path.basename(os.path.dirname(f))[len("sq_lib_"):].rsplit("_", 1)[0]

@@ -16,7 +16,7 @@ import sys
 
 
 def short_name(k):
-    """'void tt::k_filter_ring<384, true>(unsigned short const*, ...)' -> 'k_filter_ring<384, true>'"""
+    """'void tt::k_filter_ring<384, 1>(unsigned short const*, ...)' -> 'k_filter_ring<384, 1>'"""
     k = re.sub(r"^void\s+", "", k)
     k = k.split("(")[0]
     return k.replace("tt::", "")

@@ -287,9 +287,12 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// FULL: the full-catalog (last) level -- a separate instantiation of the same code so that
-// profiles attribute the dominant launch on its own (bench.py's roofline kernel).
-template <int EP, bool FULL>
+// LVL: 0 = a sample level, 1 = the full-catalog (last) level of a large query batch
+// (> RG_SMALL_NQ queries), 2 = the full level of a small batch -- separate instantiations of
+// the same code so that profiles attribute the dominant launch (bench.py's roofline kernel,
+// 10k queries) on its own, apart from e.g. Mode A's 256-query searches.
+constexpr int RG_SMALL_NQ = 2048;
+template <int EP, int LVL>
 __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring(
     const uint16_t* __restrict__ xb, int64_t ld, const float* __restrict__ q, int nq,
     int64_t ldq, const float* __restrict__ theta, int64_t stride, int64_t n_sample,
@@ -1335,7 +1338,9 @@ static void launch_level(const Level& L, const uint16_t* xb, int64_t n, int64_t 
                        ld, q, nq, ldq, w.theta, L.stride, L.n_sample, L.rows_per_slab,
                        L.n_slabs, L.n_qt, w.lists, w.counts);
   } else {
-    auto kern = L.stride == 1 ? k_filter_ring<EP, true> : k_filter_ring<EP, false>;
+    auto kern = L.stride != 1     ? k_filter_ring<EP, 0>
+                : nq > RG_SMALL_NQ ? k_filter_ring<EP, 1>
+                                   : k_filter_ring<EP, 2>;
     hipLaunchKernelGGL(kern, dim3(nblk), dim3(64 * RG_WAVES), 0, st, xb, ld, q, nq, ldq, w.theta,
                        L.stride, L.n_sample, L.rows_per_slab, L.n_slabs, L.n_qt, w.lists,
                        w.counts);
