@@ -66,21 +66,26 @@ __global__ __launch_bounds__(256) void k_transpose(const float* __restrict__ x, 
 }
 
 // out[c] (+)= sum_r x[r][c]: block per 64 columns, 4 row-strided waves
+// Column sums (bias gradients, 1^T . dY): grid = (column blocks of 64, row chunks of
+// CS_ROWS); a block reduces its chunk in LDS and adds the partial to out[c] with one float
+// atomic per column (out pre-zeroed by the host unless accumulating).  A grid over columns
+// only had 2-12 blocks for the head / attention shapes and walked 51k rows serially (1-5 ms);
+// the atomics make the summation order run-dependent (ulp-level, within the tests' rtol).
+constexpr int CS_ROWS = 256;
 __global__ __launch_bounds__(256) void k_col_sum(const float* __restrict__ x, int64_t ldx,
-                                                 int64_t rows, int cols, float* __restrict__ out,
-                                                 int accumulate) {
+                                                 int64_t rows, int cols, float* __restrict__ out) {
   __shared__ float part[4][64];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int c = blockIdx.x * 64 + lane;
+  const int64_t r0 = (int64_t)blockIdx.y * CS_ROWS;
+  const int64_t r1 = r0 + CS_ROWS < rows ? r0 + CS_ROWS : rows;
   float s = 0.0f;
   if (c < cols)
-    for (int64_t r = w; r < rows; r += 4) s += x[r * ldx + c];
+    for (int64_t r = r0 + w; r < r1; r += 4) s += x[r * ldx + c];
   part[w][lane] = s;
   __syncthreads();
-  if (w == 0 && c < cols) {
-    const float v = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
-    out[c] = accumulate ? out[c] + v : v;
-  }
+  if (w == 0 && c < cols)
+    atomicAdd(out + c, (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]));
 }
 
 __global__ void k_relu_bwd(float* __restrict__ dh, const float* __restrict__ h, int64_t n) {
@@ -185,24 +190,26 @@ __global__ __launch_bounds__(256) void k_weighted_col_sum(const float* __restric
                                                           const float* __restrict__ da,
                                                           int64_t rows, float* __restrict__ dW2,
                                                           float* __restrict__ db2) {
+  // dW2[j] = sum_r da[r] H[r][j], db2 = sum_r da[r]; grid (column blocks, row chunks) with
+  // float atomics, as k_col_sum (outputs pre-zeroed by the host)
   __shared__ float part[4][64];
+  __shared__ float pb[4];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int j = blockIdx.x * 64 + lane;
+  const int64_t r0 = (int64_t)blockIdx.y * CS_ROWS;
+  const int64_t r1 = r0 + CS_ROWS < rows ? r0 + CS_ROWS : rows;
   float s = 0.0f, sb = 0.0f;
-  for (int64_t r = w; r < rows; r += 4) {
+  for (int64_t r = r0 + w; r < r1; r += 4) {
     const float d = da[r];
     if (j < Hd) s = fmaf(d, H[r * Hd + j], s);
     sb += d;
   }
   part[w][lane] = s;
+  if (lane == 0) pb[w] = sb;
   __syncthreads();
-  if (w == 0 && j < Hd) dW2[j] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
-  __syncthreads();
-  if (blockIdx.x == 0) {
-    part[w][lane] = sb;
-    __syncthreads();
-    if (threadIdx.x == 0) *db2 = (part[0][0] + part[1][0]) + (part[2][0] + part[3][0]);
-  }
+  if (w == 0 && j < Hd)
+    atomicAdd(dW2 + j, (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]));
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(db2, (pb[0] + pb[1]) + (pb[2] + pb[3]));
 }
 
 __global__ void k_embedding_bwd(const float* __restrict__ g, int64_t ldg,
@@ -267,8 +274,13 @@ extern "C" int tt_col_sum_f32(const float* x, int64_t ldx, int64_t rows, int32_t
   TT_REQUIRE(rows >= 0 && cols >= 0, "bad sizes");
   if (cols == 0) return TT_OK;
   TT_REQUIRE(x && out, "null pointer");
-  hipLaunchKernelGGL(k_col_sum, dim3((unsigned)((cols + 63) / 64)), dim3(256), 0,
-                     (hipStream_t)stream, x, ldx, rows, cols, out, accumulate);
+  if (!accumulate && hipMemsetAsync(out, 0, (size_t)cols * 4, (hipStream_t)stream) != hipSuccess)
+    return fail(TT_ERR_LAUNCH, "tt_col_sum_f32: hipMemsetAsync");
+  if (rows == 0) return TT_OK;
+  const int64_t chunks = (rows + CS_ROWS - 1) / CS_ROWS;
+  TT_REQUIRE(chunks <= 65535, "rows > 65535 * 256");
+  hipLaunchKernelGGL(k_col_sum, dim3((unsigned)((cols + 63) / 64), (unsigned)chunks), dim3(256), 0,
+                     (hipStream_t)stream, x, ldx, rows, cols, out);
   return check_launch("tt_col_sum_f32");
 }
 
@@ -308,8 +320,13 @@ extern "C" int tt_attn_pool_bwd_f32(const float* dz, int64_t lddz, const float* 
                      onorm, alpha, w, x, S, E, W2, Hd, da_ws, dH);
   int rc = check_launch("k_attn_pool_bwd");
   if (rc) return rc;
-  hipLaunchKernelGGL(k_weighted_col_sum, dim3((unsigned)((Hd + 63) / 64)), dim3(256), 0, st, H,
-                     Hd, da_ws, B * S, dW2, db2);
+  if (hipMemsetAsync(dW2, 0, (size_t)Hd * 4, st) != hipSuccess ||
+      hipMemsetAsync(db2, 0, 4, st) != hipSuccess)
+    return fail(TT_ERR_LAUNCH, "tt_attn_pool_bwd_f32: hipMemsetAsync");
+  const int64_t chunks = (B * S + CS_ROWS - 1) / CS_ROWS;
+  TT_REQUIRE(chunks <= 65535, "B * S > 65535 * 256");
+  hipLaunchKernelGGL(k_weighted_col_sum, dim3((unsigned)((Hd + 63) / 64), (unsigned)chunks),
+                     dim3(256), 0, st, H, Hd, da_ws, B * S, dW2, db2);
   return check_launch("k_weighted_col_sum");
 }
 
