@@ -159,3 +159,44 @@ def test_exchange_gathers_aux_rows_with_queries(tmp_path):
     for r in range(world):
         ok, tot = np.load(tmp_path / f"aux{r}.npy")
         assert ok == 1 and tot == sum(range(1, world + 1))
+
+
+def _grad_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from twotower.train import allreduce_mean
+
+        g = torch.Generator().manual_seed(rank)
+        grads = {"proj0.w": torch.randn(256, 512, generator=g), "att2.b": torch.randn(1, generator=g),
+                 "brand": torch.randn(51, 64, generator=g)}
+        allreduce_mean(grads)
+        q.put((rank, {k: v.clone() for k, v in grads.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_train_gradient_allreduce_mean(world):
+    """configs[4] data-parallel step: every rank ends with the mean of all ranks' gradients
+    (one flat-bucket all-reduce, same key order on every rank)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grad_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = {}
+    for r in range(world):
+        g = torch.Generator().manual_seed(r)
+        for k, v in {"proj0.w": torch.randn(256, 512, generator=g),
+                     "att2.b": torch.randn(1, generator=g),
+                     "brand": torch.randn(51, 64, generator=g)}.items():
+            exp[k] = exp.get(k, 0) + v / world
+    for r in range(world):
+        for k in exp:
+            torch.testing.assert_close(res[r][k], exp[k], rtol=1e-6, atol=1e-6)

@@ -233,8 +233,35 @@ class TwoTowerTrainStep:
                                     self.v[k].data_ptr(), p.numel(), self.lr, b1, b2, self.eps,
                                     self.t, stream_ptr()), "adam")
 
-    def step(self, *args, **kw) -> torch.Tensor:
+    def step(self, *args, group=None, **kw) -> torch.Tensor:
+        """One optimiser step.  With an initialised process group (one process per GPU, the
+        configs[4] 8-GPU layout) every rank runs its own batch and the gradients are averaged
+        over ranks before Adam (data parallel, like DistributedDataParallel around the
+        reference's model)."""
         loss, g = self.forward_backward(*args, **kw)
+        allreduce_mean(g, group)
         self.adam(g)
         self.last_loss = loss
         return loss
+
+
+def allreduce_mean(grads: Dict[str, torch.Tensor], group=None) -> None:
+    """Average gradient tensors over the ranks of ``group`` in place with ONE all-reduce of a
+    flat bucket (the parameters of the trainable towers are ~0.5 M floats: one RCCL call over
+    xGMI instead of one per tensor).  No-op without an initialised multi-rank group."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    world = dist.get_world_size(group)
+    if world == 1:
+        return
+    keys = sorted(grads)  # same order on every rank
+    flat = torch.cat([grads[k].reshape(-1) for k in keys])
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    flat.mul_(1.0 / world)
+    off = 0
+    for k in keys:
+        n = grads[k].numel()
+        grads[k].copy_(flat[off:off + n].view_as(grads[k]))
+        off += n
