@@ -125,7 +125,7 @@ def test_layernorm_vs_torch():
 
 
 @pytest.mark.parametrize("lens", [[1], [7, 64, 128], [3, 200, 1, 512, 33], [31, 32, 33, 17]])
-@pytest.mark.parametrize("kind", ["scalar", "mfma_f32", "mfma_bf16"])
+@pytest.mark.parametrize("kind", ["scalar", "mfma_f32", "mfma_bf16", "bf16_in_out"])
 def test_attention_varlen_vs_torch(lens, kind):
     from twotower import _lib
 
@@ -139,19 +139,28 @@ def test_attention_varlen_vs_torch(lens, kind):
     if kind == "scalar":
         rc = L.tt_attention_varlen_f32(qkv.data_ptr(), 3 * H, cu.data_ptr(), len(lens), max(lens),
                                        H, nh, out.data_ptr(), H, out16.data_ptr(), _lib.stream_ptr())
+    elif kind == "bf16_in_out":  # bf16 qkv -> bf16 context: the fast kernel (k_attn32_bf16)
+        qkv = qkv.to(torch.bfloat16).float()  # the reference sees the rounded input
+        rc = L.tt_attention_varlen_bf16(qkv.to(torch.bfloat16).data_ptr(), 3 * H, cu.data_ptr(),
+                                        len(lens), max(lens), H, nh, None, H, out16.data_ptr(),
+                                        _lib.stream_ptr())
     else:
         rc = L.tt_attention_varlen(qkv.data_ptr(), 3 * H, cu.data_ptr(), len(lens), max(lens), H, nh,
                                    _lib.TT_PREC_BF16 if kind == "mfma_bf16" else _lib.TT_PREC_F32,
                                    out.data_ptr(), H, out16.data_ptr(), _lib.stream_ptr())
     _lib.check(rc, "attn")
-    assert torch.equal(out16, out.to(torch.bfloat16))
+    if kind == "bf16_in_out":
+        torch.cuda.synchronize()
+        out = out16.float()
+    else:
+        assert torch.equal(out16, out.to(torch.bfloat16))
     ref = torch.empty_like(out)
     c = cu.tolist()
     for i in range(len(lens)):
         a, b = c[i], c[i + 1]
         q, k, v = (qkv[a:b, j * H:(j + 1) * H].view(b - a, nh, 32).transpose(0, 1) for j in range(3))
         ref[a:b] = (torch.softmax(q @ k.transpose(1, 2) / 32 ** 0.5, -1) @ v).transpose(0, 1).reshape(b - a, H)
-    tol = 2e-2 if kind == "mfma_bf16" else 1e-5  # bf16 operands: 8-bit mantissa
+    tol = 1e-5 if kind in ("scalar", "mfma_f32") else 2e-2  # bf16 operands: 8-bit mantissa
     torch.testing.assert_close(out, ref, rtol=tol, atol=tol)
 
 
@@ -269,8 +278,11 @@ def test_item_tower_end_to_end_vs_oracle():
 
 
 def test_attention_bf16_input_matches_f32_input():
-    """tt_attention_varlen_bf16 (bf16 qkv) == tt_attention_varlen(prec bf16) on the rounded
-    input: the latter rounds q/k/v to bf16 itself, so the results are bit-identical."""
+    """tt_attention_varlen_bf16 (bf16 qkv, bf16 context: the fast kernel k_attn32_bf16) vs
+    tt_attention_varlen(prec bf16) on the rounded input (it rounds q/k/v to bf16 itself): the
+    same MFMA products; softmax exponentials by exp2 of log2-scaled scores instead of expf,
+    so the bf16 outputs agree to the last bf16 place or so (the probabilities feeding PV are
+    rounded to bf16 in both)."""
     from twotower import _lib
 
     lens = [5, 77, 128, 1]
@@ -285,7 +297,8 @@ def test_attention_bf16_input_matches_f32_input():
                                      _lib.TT_PREC_BF16, a.data_ptr(), H, None, _lib.stream_ptr()), "a")
     _lib.check(L.tt_attention_varlen_bf16(q16.data_ptr(), 3 * H, cu.data_ptr(), 4, 128, H, nh,
                                           None, H, b16.data_ptr(), _lib.stream_ptr()), "b")
-    assert torch.equal(b16, a.to(torch.bfloat16))
+    torch.testing.assert_close(b16.float(), a, rtol=2 ** -7, atol=2e-3)
+    assert (b16.float() - a).abs().mean().item() < 2e-3
 
 
 def test_gemm_bf16_only_output_and_misaligned_bias():

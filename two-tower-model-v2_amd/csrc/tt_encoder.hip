@@ -1280,6 +1280,118 @@ __global__ __launch_bounds__(256) void k_attn32_mfma(const TI* __restrict__ qkv,
   }
 }
 
+// bf16 fast path of k_attn32_mfma (bf16 qkv in, bf16 context out; the f32 instantiations
+// above stay the parity path).  Same MFMA dataflow; the VALU per MFMA (83 in the shared
+// kernel: PMC) is cut by: scores pre-scaled by scale*log2(e) and exponentiated with v_exp_f32
+// (exp2), bf16 packing by v_cvt_pk_bf16_f32, key masking only in a sequence's last 32-key
+// chunk, and V^T staged two keys per lane as packed dwords (8 ds_write_b32 per 2 rows instead
+// of 16 ds_write_b16, no two lanes writing halves of one dword).
+__global__ __launch_bounds__(256) void k_attn32_bf16(const uint16_t* __restrict__ qkv,
+                                                     int64_t ldq, const int32_t* __restrict__ cu,
+                                                     int H, int heads, float scale,
+                                                     uint16_t* __restrict__ out16, int64_t ldo) {
+  constexpr int DH = 32, KROW = DH * 2 + 16;
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, ql = lane & 15;
+  const int sq = blockIdx.x / heads, h = blockIdx.x % heads;
+  const int t0 = cu[sq], L = cu[sq + 1] - t0;
+  const int Lk = (L + 31) & ~31;
+  const int vst = ((Lk + 127) & ~127) + 8;  // V^T row stride (bf16 elements)
+  char* Ks = sm;
+  char* Vt = sm + (size_t)Lk * KROW;
+  // K rows: 16-B chunks copied whole; V^T: lane pair of keys (2p, 2p+1) x 8 dims -> 8 dwords
+  for (int e = tid; e < (Lk / 2) * 4; e += 256) {
+    const int p = e >> 2, c8 = 8 * (e & 3), j = 2 * p;
+    u32x4 k0 = {0u, 0u, 0u, 0u}, k1 = k0, v0 = k0, v1 = k0;
+    const uint16_t* row = qkv + (int64_t)(t0 + j) * ldq + h * DH + c8;
+    if (j < L) {
+      k0 = *(const u32x4*)(row + H);
+      v0 = *(const u32x4*)(row + 2 * H);
+    }
+    if (j + 1 < L) {
+      k1 = *(const u32x4*)(row + ldq + H);
+      v1 = *(const u32x4*)(row + ldq + 2 * H);
+    }
+    *(u32x4*)(Ks + j * KROW + c8 * 2) = k0;
+    *(u32x4*)(Ks + (j + 1) * KROW + c8 * 2) = k1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t a = (v0[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+      const uint32_t b = (v1[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+      *(uint32_t*)(Vt + ((size_t)(c8 + i) * vst + j) * 2) = a | (b << 16);
+    }
+  }
+  __syncthreads();
+  const float sl2 = scale * 1.4426950408889634f;  // scores in log2 units
+  for (int q0 = 16 * w; q0 < L; q0 += 64) {
+    const int qr = q0 + ql < L ? q0 + ql : L - 1;
+    const bf16x8e qf = __builtin_bit_cast(
+        bf16x8e, *(const u32x4*)(qkv + (int64_t)(t0 + qr) * ldq + h * DH + 8 * g));
+    float m = -__builtin_huge_valf(), lsum = 0.0f;
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    for (int kc = 0; kc < Lk; kc += 32) {
+      f32x4 sc[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const u32x4 kf = *(const u32x4*)(Ks + (kc + 16 * b + ql) * KROW + 16 * g);
+        sc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8e, kf), qf,
+                                                        f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0) * sl2;
+      }
+      // sc[b][v] = score(key kc + 16b + 4g + v, query q0 + ql); mask past L (last chunk only)
+      if (kc + 32 > L) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            if (kc + 16 * b + 4 * g + v >= L) sc[b][v] = -__builtin_huge_valf();
+      }
+      float cm = fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
+                       fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
+      cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+      const float mn = fmaxf(m, cm);
+      const float corr = __builtin_amdgcn_exp2f(m - mn);
+      m = mn;
+      float ps = 0.0f;
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          sc[b][v] = __builtin_amdgcn_exp2f(sc[b][v] - mn);
+          ps += sc[b][v];
+        }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      lsum = lsum * corr + ps;
+      acc[0] = acc[0] * corr;
+      acc[1] = acc[1] * corr;
+      // P^T slots: j < 4 <-> key kc + 4g + j, j >= 4 <-> kc + 16 + 4g + (j - 4)
+      const u32x4 pu = {pack_bf16_hw(sc[0][0], sc[0][1]), pack_bf16_hw(sc[0][2], sc[0][3]),
+                        pack_bf16_hw(sc[1][0], sc[1][1]), pack_bf16_hw(sc[1][2], sc[1][3])};
+      const bf16x8e pf = __builtin_bit_cast(bf16x8e, pu);
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const char* vr = Vt + ((size_t)(16 * db + ql) * vst + kc + 4 * g) * 2;
+        const uint64_t lo = *(const uint64_t*)vr, hi = *(const uint64_t*)(vr + 32);
+        const u32x4 vu = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+        acc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8e, vu), pf,
+                                                          acc[db], 0, 0, 0);
+      }
+    }
+    // acc[db][v] = O^T[dim 16 db + 4 g + v][query q0 + ql]
+    if (q0 + ql < L) {
+      const float inv = 1.0f / lsum;
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const f32x4 o = acc[db] * inv;
+        *(uint2*)(out16 + (int64_t)(t0 + q0 + ql) * ldo + h * DH + 16 * db + 4 * g) =
+            uint2{pack_bf16_hw(o[0], o[1]), pack_bf16_hw(o[2], o[3])};
+      }
+    }
+  }
+}
+
 size_t attn32_smem(int max_len, bool bf) {
   const int Lk = (max_len + 31) & ~31;
   const int vst = ((Lk + 127) & ~127) + (bf ? 8 : 4);
@@ -1341,6 +1453,13 @@ int enc_device_cus() {
 bool gemm_ln_disabled() {  // TT_GEMM_LN=0: unfused GEMM + LayerNorm (A/B timing)
   static const bool off = [] {
     const char* e = getenv("TT_GEMM_LN");
+    return e && e[0] == '0';
+  }();
+  return off;
+}
+bool attn_fast_disabled() {  // TT_ATTN_FAST=0: the shared k_attn32_mfma for bf16 too (A/B)
+  static const bool off = [] {
+    const char* e = getenv("TT_ATTN_FAST");
     return e && e[0] == '0';
   }();
   return off;
@@ -1507,6 +1626,16 @@ extern "C" int tt_attention_varlen_bf16(const uint16_t* qkv, int64_t ld_qkv,
   if (H / heads != 32)
     return fail(TT_ERR_UNSUPPORTED, "tt_attention_varlen_bf16: head dim must be 32");
   const size_t smem = attn32_smem(max_len, true);
+  if (!out && out_bf16 && !attn_fast_disabled()) {  // bf16-only output: the fast kernel
+    const void* fb = (const void*)k_attn32_bf16;
+    if (smem > 64 * 1024 &&
+        hipFuncSetAttribute(fb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess)
+      return fail(TT_ERR_LAUNCH, "hipFuncSetAttribute(max dynamic LDS)");
+    hipLaunchKernelGGL(k_attn32_bf16, dim3((unsigned)(n_seq * heads)), dim3(256), smem,
+                       (hipStream_t)stream, qkv, ld_qkv, cu_seqlens, H, heads,
+                       1.0f / sqrtf(32.0f), out_bf16, ld_out);
+    return check_launch("tt_attention_varlen_bf16");
+  }
   const void* fn = (const void*)k_attn32_mfma<true, uint16_t>;
   if (smem > 64 * 1024 &&
       hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess)
