@@ -685,7 +685,17 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wide(const uint16_t* __restrict
 constexpr int GL_BM = 128, GL_H = 384, GL_NJ = 6, GL_ASLOTS = 3, GL_WSLOTS = 2;
 constexpr int GL_A_B = GL_BM * 128, GL_W_B = GL_H * 128;
 constexpr int GL_WBASE = GL_ASLOTS * GL_A_B, GL_LDS_B = GL_WBASE + GL_WSLOTS * GL_W_B;
-constexpr int GL_STORES = 4 * GL_NJ * 2;  // vector-memory stores per lane in a full tile
+constexpr int GL_STORES = 4 * GL_NJ * 2;
+// timing-only experiment switches (results WRONG when set), tools/exp_filter.sh FILE=tt_encoder
+// + tools/exp_gemm.sh.  Measured at M = 370761 (K = 384 / 1536): base 471 / 752 us, no W
+// stream after the prologue 439 / 669, no epilogue 111 / 504 -> the LayerNorm epilogue (its
+// residual reads and x / x16 writes, 1.42 GB at K = 384) is what the fused kernel waits on.
+#ifndef TT_GLEXP_NOW
+#define TT_GLEXP_NOW 0  // W streamed for the first stages only
+#endif
+#ifndef TT_GLEXP_NOEPI
+#define TT_GLEXP_NOEPI 0  // no residual loads / LayerNorm / stores
+#endif  // vector-memory stores per lane in a full tile
 
 __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__ A, int64_t lda,
                                                     const uint16_t* __restrict__ W, int64_t ldw,
@@ -802,7 +812,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
         enc_wait_vm<0>();
       }
       enc_lds_barrier();  // stage t visible to all; slots of stage t - 1 are free again
-      if (t + 1 < nstages) issue_w(kt + 1 < nk ? kt + 1 : 0, t + 1);
+      if (t + 1 < nstages && (!TT_GLEXP_NOW || t + 1 < GL_WSLOTS))
+        issue_w(kt + 1 < nk ? kt + 1 : 0, t + 1);
       issue_next_a();
       const uint32_t sa = lds_addr(smem) + (uint32_t)((t % GL_ASLOTS) * GL_A_B);
       const uint32_t sw = lds_addr(smem) + (uint32_t)(GL_WBASE + (t % GL_WSLOTS) * GL_W_B);
@@ -849,6 +860,16 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
     }
     gs += nk;
 
+    if (TT_GLEXP_NOEPI) {  // keep every accumulator live (no dead-code MFMAs), store nothing
+      float t = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < GL_NJ; ++j) t += (acc[i][j][0] + acc[i][j][1]) + (acc[i][j][2] + acc[i][j][3]);
+      if (t == 1.2345f) X[0] = t;
+      prev_full = false;
+      continue;
+    }
     // ---- epilogue: y = acc + bias + x ; x = LayerNorm(y) (biased variance, two passes).
     // Residual rows are loaded one 16-row block ahead (6 x 16 B per lane in flight while the
     // previous block is summed); bias / gamma / beta come from LDS.
