@@ -357,15 +357,18 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   }
   const int64_t tile_bytes = row_bytes * TR;
   const char* slab_base = (const char*)xb + j0 * row_bytes;
-  auto issue = [&](int t) __attribute__((always_inline)) {
+  // clamp: only the last tile of a ragged slab reads past j1 -- a separate instantiation
+  // behind a scalar branch, so the common path is a uniform base + per-lane 32-bit offset
+  // (the compiler had if-converted both paths into ~48 VALU selects per tile)
+  auto issue_t = [&](int t, auto clamp_) __attribute__((always_inline)) {
+    constexpr bool clamp = decltype(clamp_)::value;
     char* slot = ring + (t % RG_SLOTS) * TILE_B;
     const int64_t jt = j0 + (int64_t)t * TR;
-    const bool clamp = jt + TR > j1;  // wave-uniform: only the slab's last tile
     const char* tb = slab_base + (int64_t)t * tile_bytes;
 #pragma unroll
     for (int pp = 0; pp < PPW; ++pp) {
       const char* src;
-      if (!clamp) {
+      if constexpr (!clamp) {
         src = tb + voff[pp];
       } else {  // recompute the lane's (row, column) of piece pp: rare path, no live registers
         const int P = (w + RG_WAVES * pp) * 64 + lane;
@@ -379,6 +382,10 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
                                            slot + (w + RG_WAVES * pp) * 1024),
                                        16, 0, 0);
     }
+  };
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    if (j0 + (int64_t)(t + 1) * TR > j1) issue_t(t, std::true_type{});
+    else issue_t(t, std::false_type{});
   };
   // Candidate pool: each wave owns RG_WPOOL entries and the counters of its own queries, so
   // appends need no atomics and no cross-wave synchronisation; the pool position `wn` is a
