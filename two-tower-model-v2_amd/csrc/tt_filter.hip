@@ -1221,12 +1221,16 @@ static int device_cus() {
 
 // Slab count of a ring level: the kernel runs one 512-thread block per CU (148 KB LDS), so
 // the n_qt * slabs blocks execute in ceil(blocks / CUs) equal rounds.  Minimise
-// rounds * (rows per slab + per-slab overhead ~ 3 tiles), slabs <= 64 (list memory and
-// k_select work grow with the slab count), slabs >= 1 tile-row chunk of 256 rows.
+// rounds * (rows per slab + per-slab overhead ~ 3 tiles), slabs >= 1 tile-row chunk of 256
+// rows, slabs <= 64 (list memory and k_select work grow with the slab count) -- except for
+// small query batches (n_qt * 64 < 4 CUs' worth of blocks, e.g. the one-buyer /retrieve
+// call): there up to 4 blocks per CU, so the catalog pass uses the whole chip instead of 64
+// CUs (the selection then takes the multi-pass k_select_wave).
 static int64_t ring_slabs(int n_qt, int64_t n_sample) {
   const int ncu = device_cus() * RG_BLOCKS_PER_CU;  // concurrent blocks
   int64_t sl_max = n_sample / 256;
-  if (sl_max > 64) sl_max = 64;
+  const int64_t cap = (int64_t)n_qt * 64 >= 4 * ncu ? 64 : (4 * ncu + n_qt - 1) / n_qt;
+  if (sl_max > cap) sl_max = cap;
   if (sl_max < 1) sl_max = 1;
   int64_t best = 1;
   double best_cost = 1e300;
