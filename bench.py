@@ -339,6 +339,37 @@ def main():
                                           row_base=lo)
         return kernels.scan_topk(shard, hi - lo, E, qall, K, row_base=lo)
 
+    if world == 1 and a.method == "bf16":
+        # the reference's /retrieve pattern: ONE buyer per search (server.py:241-244).  At
+        # nq = 1 the full-catalog level is HBM-bound (bf16 image read once): its achieved
+        # bandwidth against the 8 TB/s peak is the scan's HBM roofline.
+        q1 = q[:1].clone()
+        ws1 = torch.empty(kernels.filter_workspace_bytes(hi - lo, E, 1, K), dtype=torch.uint8,
+                          device=dev)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        for e in ev:
+            e.record(stream)
+        for _ in range(3):
+            kernels.scan_topk_bf16(shard, shard16, hi - lo, E, q1, K, bounds, workspace=ws1)
+        n1, tot, lvl = 20, 0.0, 0.0
+        for _ in range(n1):
+            ev[2].record(stream)
+            kernels.scan_topk_bf16(shard, shard16, hi - lo, E, q1, K, bounds, workspace=ws1,
+                                   events=(ev[0], ev[1]))
+            ev[3].record(stream)
+            torch.cuda.synchronize()
+            tot += ev[2].elapsed_time(ev[3])
+            lvl += ev[0].elapsed_time(ev[1])
+        lvl_ms = lvl / n1
+        result["single_buyer_search"] = {
+            "nq": 1, "ms_per_search": tot / n1, "full_level_ms": lvl_ms,
+            "full_level_bytes": 2.0 * (hi - lo) * ep,
+            "achieved_hbm_gbps": 2.0 * (hi - lo) * ep / (lvl_ms * 1e-3) / 1e9,
+            "hbm_peak_gbps": HBM_PEAK_GBPS,
+            "frac": 2.0 * (hi - lo) * ep / (lvl_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+            "kernel": f"k_filter_ring<{ep}, 2>"}
+        del ws1
+
     cpu_a = None
     if a.mode_a_buyers > 0:
         result["mode_a"], cpu_a = mode_a(a, dev, world, rank, lambda qall: local_search_k(qall),

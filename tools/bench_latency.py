@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--catalog", type=int, default=1_000_000)
     ap.add_argument("--dim", type=int, default=384)
     ap.add_argument("--k", type=int, default=100)
+    ap.add_argument("--nq", default="1,8,32,128,1024")
+    ap.add_argument("--methods", default="f32,bf16")
     a = ap.parse_args()
     N, E, K = a.catalog, a.dim, a.k
     ep = _lib.padded_dim(E)
@@ -30,12 +32,12 @@ def main():
     kernels.l2norm_rows(db, E, 0, out=db, out_bf16=db16)
     bounds = kernels.bf16_image_bounds(db, db16, E).tolist()
     res = {}
-    for nq in (1, 8, 32, 128, 1024):
+    for nq in (int(v) for v in a.nq.split(",")):
         q = torch.zeros((nq, ep), device="cuda")
         q[:, :E] = torch.randn((nq, E), generator=g, device="cuda")
         kernels.l2norm_rows(q, E, 0, out=q)
         row = {}
-        for method in ("f32", "bf16"):
+        for method in a.methods.split(","):
             if method == "bf16":
                 ws = torch.empty(kernels.filter_workspace_bytes(N, E, nq, K), dtype=torch.uint8,
                                  device="cuda")
