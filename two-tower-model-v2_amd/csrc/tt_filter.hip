@@ -227,6 +227,9 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #ifndef TT_EXP_NOWRITE
 #define TT_EXP_NOWRITE 0  // selection control flow without the LDS pool writes
 #endif
+#ifndef TT_EXP_PRIO
+#define TT_EXP_PRIO 0  // s_setprio 1 for waves 4-7 (static priority for the younger half)
+#endif
 #ifndef TT_EXP_MAXONLY
 #define TT_EXP_MAXONLY 0  // per-block max + ballot only (no per-slot scan)
 #endif
@@ -314,6 +317,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (TT_EXP_PRIO && w >= RG_WAVES / 2) __builtin_amdgcn_s_setprio(1);  // younger half (guide)
   const int col = lane & 15, g = lane >> 4;
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
   const int slab = lb / n_qt, qt = lb % n_qt;
