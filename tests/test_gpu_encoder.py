@@ -355,3 +355,27 @@ def test_gemm_ln_bf16_rejects_unsupported():
     assert L.tt_gemm_ln_bf16(z.data_ptr(), 384, z.data_ptr(), 384, z.data_ptr(), z.data_ptr(),
                              z.data_ptr(), 1e-12, z.data_ptr(), 384, z.data_ptr(), 384, 4, 384, 96,
                              _lib.stream_ptr()) == _lib.TT_ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("prec", ["f32", "bf16"])
+def test_encode_batch_device_chunking_changes_nothing(prec):
+    """ItemTower.encode_batch runs chunks of device_batch texts (>= batch_size): every output
+    row depends on its own text only, so any chunking gives bit-identical rows."""
+    from twotower.item_tower import ItemTower, random_bert_state_dict
+
+    cfg = dict(vocab=500, hidden=384, layers=2, heads=12, intermediate=1536, max_positions=512,
+               type_vocab=2, ln_eps=1e-12)
+    it = ItemTower(use_categorical_features=True, encoder_state_dict=random_bert_state_dict(cfg, 3),
+                   encoder_cfg=cfg, prec=prec)
+    it.initialize_categorical_embeddings([f"b{i}" for i in range(9)], [f"c{i}" for i in range(5)])
+    it.cuda()
+    rng = np.random.default_rng(5)
+    texts = [" ".join(f"w{int(x)}" for x in rng.integers(0, 300, rng.integers(1, 60)))
+             for _ in range(301)]
+    brands = [f"b{int(x)}" for x in rng.integers(0, 12, 301)]
+    cats = [f"c{int(x)}" for x in rng.integers(0, 7, 301)]
+    it.device_batch = 4096
+    a = it.encode_batch(texts, brands, cats, batch_size=64)
+    it.device_batch = 1
+    b = it.encode_batch(texts, brands, cats, batch_size=37)
+    assert a.shape == (301, 384) and np.array_equal(a, b)

@@ -363,13 +363,22 @@ class ItemTower(nn.Module):
         return self.head(text_emb, ids[0], ids[1], use_cat=True)
 
     # reference :213-243
+    # texts per device call in encode_batch: every output row depends only on its own text
+    # (packed varlen encoder, row-wise GEMMs / LayerNorm / pooling), so chunking changes no
+    # result -- only how full the GPU is (64 texts ~ 4.6k tokens leave most CUs idle; 4096
+    # texts run the encoder's persistent GEMMs at full occupancy).
+    device_batch = 4096
+
     def encode_batch(self, texts: List[str], brands: Optional[List[str]] = None,
                      categories: Optional[List[str]] = None, batch_size: int = 32) -> np.ndarray:
+        """item_tower.py:213-243.  ``batch_size`` is honoured as the minimum chunk; chunks of
+        ``device_batch`` texts (same results) keep the MI355X busy."""
         self.eval()
+        step = max(int(batch_size), int(self.device_batch))
         outs = []
         with torch.no_grad():
-            for i in range(0, len(texts), batch_size):
-                outs.append(self.forward(texts[i:i + batch_size],
-                                         brands[i:i + batch_size] if brands else None,
-                                         categories[i:i + batch_size] if categories else None))
+            for i in range(0, len(texts), step):
+                outs.append(self.forward(texts[i:i + step],
+                                         brands[i:i + step] if brands else None,
+                                         categories[i:i + step] if categories else None))
         return torch.cat(outs).cpu().numpy()
