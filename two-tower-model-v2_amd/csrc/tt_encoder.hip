@@ -1035,15 +1035,12 @@ __global__ __launch_bounds__(256) void k_embed_ln(const int32_t* __restrict__ id
                                                   const float* __restrict__ beta, float eps,
                                                   float* __restrict__ y, uint16_t* __restrict__ y16,
                                                   int H) {
+  // block per sequence, wave per token (the position is t - cu[seq]; a per-token binary
+  // search over cu was 13 dependent loads per token at 5k sequences)
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < T; t += (int64_t)gridDim.x * 4) {
-    int lo = 0, hi = n_seq;  // sequence: cu[lo] <= t < cu[lo+1]
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (cu[mid] <= t) lo = mid;
-      else hi = mid;
-    }
-    const int p = (int)(t - cu[lo]);
+  const int64_t t0 = cu[blockIdx.x], t1 = cu[blockIdx.x + 1];
+  for (int64_t t = t0 + w; t < t1; t += 4) {
+    const int p = (int)(t - t0);
     int id = ids[t];
     id = (id >= 0 && id < vocab) ? id : 0;
     const float* wr = word + (int64_t)id * H;
@@ -1444,7 +1441,8 @@ __global__ __launch_bounds__(256) void k_mean_pool(const float* __restrict__ x, 
   const float cnt = fmaxf((float)(t1 - t0), 1e-9f);
   for (int e = threadIdx.x; e < H; e += blockDim.x) {
     float s = 0.0f;
-    for (int t = t0; t < t1; ++t) s += x[(int64_t)t * ldx + e];
+#pragma unroll 8
+    for (int t = t0; t < t1; ++t) s += x[(int64_t)t * ldx + e];  // sequential sum, loads ahead
     out[(int64_t)sq * ldo + e] = s / cnt;
   }
 }
@@ -1777,8 +1775,7 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
     return fail(TT_ERR_WORKSPACE, "tt_bert_encode: workspace too small");
   hipStream_t st = (hipStream_t)stream;
   {
-    const int64_t b = (T + 3) / 4;
-    hipLaunchKernelGGL(k_embed_ln, dim3((unsigned)(b < 16384 ? b : 16384)), dim3(256), 0, st, ids,
+    hipLaunchKernelGGL(k_embed_ln, dim3((unsigned)n_seq), dim3(256), 0, st, ids,
                        cu_seqlens, n_seq, T, m->word_emb, m->vocab, m->pos_emb, m->type_emb,
                        m->emb_ln_g, m->emb_ln_b, m->ln_eps, w.x, bf ? w.x16 : nullptr, H);
     int rc = check_launch("k_embed_ln");
