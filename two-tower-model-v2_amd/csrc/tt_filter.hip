@@ -932,6 +932,7 @@ __global__ __launch_bounds__(256) void k_select_reg(const uint64_t* __restrict__
   const int lane = threadIdx.x & 63;
   const int qid = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (qid >= nq) return;  // the whole wave (no block-level barriers below)
+  if (mode == 2 && lane < SH_P) pcount[(int64_t)qid * SH_P + lane] = 0;  // overflow: count 0
   if (flags[qid]) {
     if (lane == 0 && mode == 0) theta_out[qid] = __builtin_huge_valf();
     return;
@@ -994,6 +995,39 @@ __global__ __launch_bounds__(256) void k_select_reg(const uint64_t* __restrict__
         }
       }
     }
+  }
+  if (mode == 2) {
+    // sharded full level: every candidate (a >= theta_g - eps2) is band; the shard's count of
+    // candidates a >= t_i at the SH_P probes (all-reduced SUM by the caller).  The probe loop
+    // stays rolled (unrolling it over the PER registers spilled).
+    const float th = stats[2 * qid], sm = stats[2 * qid + 1];
+#pragma unroll 1
+    for (int t = 0; t < SH_P; ++t) {
+      const float pt = probe_t(th, sm, t);
+      int c = 0;
+#pragma unroll
+      for (int i = 0; i < PER; ++i)
+        if (i < ni) c += __popcll(__ballot(lane + 64 * i < total && key_float(hv[i]) >= pt));
+      if (lane == 0) pcount[(int64_t)qid * SH_P + t] = c;
+    }
+    int nb = 0;
+    uint64_t* qb = band + (int64_t)qid * BAND_CAP;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      if (i < ni) {
+        const bool in = lane + 64 * i < total;
+        const uint64_t bm = __ballot(in);
+        const int pos = nb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+        if (in && pos < BAND_CAP) qb[pos] = ((uint64_t)hv[i] << 32) | lo[i];
+        nb += __popcll(bm);
+      }
+    }
+    if (lane == 0) {
+      if (nb > BAND_CAP) flag_query(qid, flags, qsel, qsel_n);  // this shard: exact fallback
+      else band_n[qid] = nb;
+    }
+    return;
   }
   const int R = mode == 0 ? J : k;
   if (total < R) {  // fewer than R candidates: a_J = -inf (sample) / cannot certify (full)
@@ -1465,7 +1499,7 @@ int filter_level(const FilterPlan& p, const FilterWs& w, int li, int mode, const
   if (rc) return rc;
   if (last && ev_stop && hipEventRecord((hipEvent_t)ev_stop, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "hipEventRecord(stop)");
-  auto sel = L.n_slabs <= 64 && mode != 2 && !select_reg_disabled() ? k_select_reg : k_select_wave;
+  auto sel = L.n_slabs <= 64 && !select_reg_disabled() ? k_select_reg : k_select_wave;
   hipLaunchKernelGGL(sel, dim3((nq + 3) / 4), dim3(256), 0, st, w.lists, w.counts,
                      L.n_slabs, k, p.J, w.eps2, mode, w.theta, w.aref, w.band, w.band_n, w.flags,
                      w.qsel, w.qsel_n, nq, stats, pcount, smax_out);
