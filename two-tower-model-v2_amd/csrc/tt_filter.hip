@@ -227,6 +227,9 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #ifndef TT_EXP_NOWRITE
 #define TT_EXP_NOWRITE 0  // selection control flow without the LDS pool writes
 #endif
+#ifndef TT_EXP_SAMPLE_ROWS
+#define TT_EXP_SAMPLE_ROWS 0  // sample levels append every passing row (not tile maxima)
+#endif
 #ifndef TT_EXP_PRIO
 #define TT_EXP_PRIO 0  // s_setprio 1 for waves 4-7 (static priority for the younger half)
 #endif
@@ -482,6 +485,40 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
         }
     }
   };
+  // Sample levels (LVL 0) only need the J-th best score of the sample, and the J-th largest
+  // of the per-tile maxima is a lower bound of it (the top-J tile maxima are J distinct rows),
+  // i.e. a sound threshold for the next level that is equal to a_J unless two of the top J
+  // rows share a 32-row tile.  So a sample level appends ONE key per (query, tile): its max
+  // (row id unused by the mode-0 selection) -- two cross-lane max steps and one ballot per
+  // query block instead of 8 ballot rounds; at the stride-16 level ~95% of (tile, block)
+  // pairs held a candidate.
+  auto append_tmax = [&](const float (&mx)[QB], int t) __attribute__((always_inline)) {
+    const uint32_t r = (uint32_t)((j0 + (int64_t)t * TR) * stride);
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      float m = mx[b];  // rows past the slab end are clamped copies of a real row: no mask
+      m = fmaxf(m, __shfl_xor(m, 16, 64));
+      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      const bool in = g == 0 && m >= th[b];
+      const uint64_t bm = __ballot(in);
+      if (bm == 0ull) continue;
+      const uint32_t pos =
+          wn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+      if (in) {
+        const uint32_t ql = (uint32_t)(w * QPW + 16 * b + col);
+        if (pos < (uint32_t)RG_WPOOL) {
+          const uint32_t u = __float_as_uint(m + 0.0f);
+          const uint32_t key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+          lds_write64(lds_addr(&wkey[pos]), ((uint64_t)key << 32) | (uint64_t)(~r));
+          lds_write32(lds_addr(&wmeta[pos]), ql);
+        } else {
+          lds_or(lds_addr(&qcnt[ql]), RG_OVF);
+        }
+      }
+      wn += (uint32_t)__popcll(bm);
+    }
+  };
   // wait until only `younger` tiles issued after the awaited one are still in flight
   auto wait_tiles = [&](int younger) __attribute__((always_inline)) {
     if (TT_EXP_NODMA) return;
@@ -582,7 +619,10 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
             if (!TT_EXP_NODMA && t + RG_PD < n_tiles) issue(t + RG_PD);
           }
           if constexpr (s == (KS > 1 ? 1 : 0)) {  // early: tile t-1's scores die before the peak
-            if (!TT_EXP_NOSEL) append(accp, mx, t - 1);
+            if (!TT_EXP_NOSEL) {
+              if constexpr (LVL == 0 && !TT_EXP_SAMPLE_ROWS) append_tmax(mx, t - 1);
+              else append(accp, mx, t - 1);
+            }
             if (TT_EXP_NOSEL) {
 #pragma unroll
               for (int b = 0; b < QB; ++b)
@@ -601,7 +641,8 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   if (n_tiles > 0 && !TT_EXP_NOSEL) {
     float mx[QB];
     tile_max(accp, mx);
-    append(accp, mx, n_tiles - 1);
+    if constexpr (LVL == 0 && !TT_EXP_SAMPLE_ROWS) append_tmax(mx, n_tiles - 1);
+    else append(accp, mx, n_tiles - 1);
   }
   wait_vm<0>();
   flush();
