@@ -1287,6 +1287,18 @@ static bool select_reg_disabled() {  // TT_SELECT_REG=0: LDS-staged k_select_wav
   }();
   return off;
 }
+static bool tmax_first_disabled() {  // TT_FILTER_TMAX_FIRST=0: full sample ladder (A/B)
+  static const bool off = [] {
+    const char* e = getenv("TT_FILTER_TMAX_FIRST");
+    return e && e[0] == '0';
+  }();
+  return off;
+}
+constexpr int64_t SW_CAP_TILES = SW_CAP - 64;  // first-level tiles per query, with margin
+static int64_t ring_tr(int ep) {                 // rows per k_filter_ring tile
+  return ep == 64 ? RingCfg<64>::TR : ep == 128 ? RingCfg<128>::TR : ep == 256 ? RingCfg<256>::TR
+         : ep == 384 ? RingCfg<384>::TR : ep == 512 ? RingCfg<512>::TR : RingCfg<768>::TR;
+}
 static int device_cus() {
   static const int cus = [] {
     int d = 0, v = 0;
@@ -1305,15 +1317,16 @@ static int device_cus() {
 // small query batches (n_qt * 64 < 4 CUs' worth of blocks, e.g. the one-buyer /retrieve
 // call): there up to 4 blocks per CU, so the catalog pass uses the whole chip instead of 64
 // CUs (the selection then takes the multi-pass k_select_wave).
-static int64_t ring_slabs(int n_qt, int64_t n_sample) {
+static int64_t ring_slabs(int n_qt, int64_t n_sample, int64_t sl_min = 1) {
   const int ncu = device_cus() * RG_BLOCKS_PER_CU;  // concurrent blocks
   int64_t sl_max = n_sample / 256;
   const int64_t cap = (int64_t)n_qt * 64 >= 4 * ncu ? 64 : (4 * ncu + n_qt - 1) / n_qt;
   if (sl_max > cap) sl_max = cap;
+  if (sl_max < sl_min) sl_max = sl_min;
   if (sl_max < 1) sl_max = 1;
-  int64_t best = 1;
+  int64_t best = sl_min < 1 ? 1 : sl_min;
   double best_cost = 1e300;
-  for (int64_t sl = 1; sl <= sl_max; ++sl) {
+  for (int64_t sl = best; sl <= sl_max; ++sl) {
     const int64_t rounds = ((int64_t)n_qt * sl + ncu - 1) / ncu;
     const int64_t rows = ((n_sample + sl - 1) / sl + 63) / 64 * 64;
     const double cost = (double)rounds * (double)(rows + 96);
@@ -1339,6 +1352,19 @@ static FilterPlan plan_filter(int64_t n, int nq, int k, int ep) {
     s *= 16;
   }
   strides[nl++] = s;
+  // Tile-max shortcut: a sample level appends one key per (query, 32-row tile), so a sample
+  // whose tiles fit one query's selection buffer can be the FIRST level, at theta = -inf
+  // (every tile max a candidate) -- the coarser levels and their selections (4 launches,
+  // ~0.1 ms at 1M rows) are dropped.  Take the finest such sample; never the last level
+  // (that one appends rows, not tile maxima).  TT_FILTER_TMAX_FIRST=0 restores the ladder.
+  int first = -1;
+  const int64_t TMAX_TR = ring_tr(ep);
+  if (!tmax_first_disabled())
+    for (int i = 1; i < nl && first < 0; ++i) {
+      const int64_t ns = (n + strides[i] - 1) / strides[i];
+      if (ns > SEL_CAP / 2 && (ns + TMAX_TR - 1) / TMAX_TR <= SW_CAP_TILES) first = i;
+    }
+  if (first > 0) nl = first + 1;
   p.n_levels = nl;
   p.max_slabs = 1;
   const int dense_qpb = FL_WAVES * 16 * (ep <= 384 ? 2 : 1);
@@ -1349,12 +1375,15 @@ static FilterPlan plan_filter(int64_t n, int nq, int k, int ep) {
     Level& L = p.lv[i];
     L.stride = strides[nl - 1 - i];
     L.n_sample = (n + L.stride - 1) / L.stride;
-    L.dense = i == 0;
+    L.dense = i == 0 && first < 0;
     const int qpb = L.dense ? dense_qpb : ring_qpb_v;
     L.n_qt = (nq + qpb - 1) / qpb;
     int64_t sl;
     if (L.dense) {
       sl = (L.n_sample + FL_CAP / 2 - 1) / (FL_CAP / 2);  // every row is a candidate
+    } else if (i == 0) {
+      // theta = -inf: every tile of a slab lands in its (query, slab) list of FL_CAP
+      sl = ring_slabs(L.n_qt, L.n_sample, (L.n_sample + FL_CAP * TMAX_TR - 1) / (FL_CAP * TMAX_TR));
     } else {
       sl = ring_slabs(L.n_qt, L.n_sample);
     }
