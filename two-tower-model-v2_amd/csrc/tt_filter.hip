@@ -221,6 +221,9 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #ifndef TT_EXP_NOSEL
 #define TT_EXP_NOSEL 0  // skip candidate selection
 #endif
+#ifndef TT_EXP_NOIDLE
+#define TT_EXP_NOIDLE 0  // small batches: padding-only waves run the MFMA stream too (A/B)
+#endif
 #ifndef TT_EXP_NOBAR
 #define TT_EXP_NOBAR 0  // skip the per-step barrier
 #endif
@@ -542,6 +545,18 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   for (int t = 0; t < RG_PD && t < n_tiles; ++t) issue(t);
   wait_tiles(n_tiles - 1 < RG_PD - 1 ? n_tiles - 1 : RG_PD - 1);
   lds_barrier();  // tile 0 landed; counters initialised
+  // Small batches (LVL 2, e.g. one buyer): a wave without a single real query only moves its
+  // share of the ring DMA, in lockstep with the block's one barrier per tile -- its MFMAs on
+  // padding queries had made the one-buyer full level issue-bound (8 waves x 48 MFMAs / tile).
+  if (LVL == 2 && qbase >= nq && !TT_EXP_NOIDLE) {
+    for (int t = 0; t < n_tiles; ++t) {
+      if (t + 1 < n_tiles) wait_tiles(n_tiles - 2 - t < RG_PD - 2 ? n_tiles - 2 - t : RG_PD - 2);
+      asm volatile("s_barrier" ::: "memory");
+      if (t + RG_PD < n_tiles) issue(t + RG_PD);
+    }
+    wait_vm<0>();
+    return;
+  }
   const float qnan = __builtin_nanf("");
   f32x4 accp[RB][QB];
 #pragma unroll
