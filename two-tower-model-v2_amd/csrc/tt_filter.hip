@@ -548,7 +548,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   // Small batches (LVL 2, e.g. one buyer): a wave without a single real query only moves its
   // share of the ring DMA, in lockstep with the block's one barrier per tile -- its MFMAs on
   // padding queries had made the one-buyer full level issue-bound (8 waves x 48 MFMAs / tile).
-  if (LVL == 2 && qbase >= nq && !TT_EXP_NOIDLE) {
+  if (LVL != 1 && qbase >= nq && !TT_EXP_NOIDLE) {
     for (int t = 0; t < n_tiles; ++t) {
       if (t + 1 < n_tiles) wait_tiles(n_tiles - 2 - t < RG_PD - 2 ? n_tiles - 2 - t : RG_PD - 2);
       asm volatile("s_barrier" ::: "memory");
