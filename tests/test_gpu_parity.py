@@ -88,7 +88,10 @@ def test_scan_bit_exact_vs_oracle(K, oracle_mod, n, d, nq, k):
 
 BF16_CASES = [c for c in SCAN_CASES if c[3] <= 128] + [
     (2049, 384, 5, 128),     # two filter levels, k at the filter's maximum
-    (300000, 384, 40, 100),  # four filter levels
+    (300000, 384, 40, 100),  # tile-max first level at stride 16; 1024 full-level slabs
+    (1000000, 384, 1, 100),  # one buyer at the bench catalog size (grouped k_select_reg)
+    (150000, 384, 3, 10),    # 585 slabs: ragged groups of 10 per lane
+    (70000, 128, 2, 50),     # E = 128, 273 slabs
     (60000, 768, 33, 100),   # E = 768 (one query block per wave)
     (20000, 384, 300, 100),  # several query tiles
     (40000, 512, 9, 64),

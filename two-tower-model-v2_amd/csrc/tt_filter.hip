@@ -221,6 +221,12 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #ifndef TT_EXP_NOSEL
 #define TT_EXP_NOSEL 0  // skip candidate selection
 #endif
+#ifndef TT_EXP_SEL_TIMING
+#define TT_EXP_SEL_TIMING 0  // printf per-phase wall-clock ticks (100 MHz) of k_select_reg
+#endif
+#ifndef TT_EXP_SEL_STOP
+#define TT_EXP_SEL_STOP 0  // timing only: k_select_reg stops after the gather (1) / search (2)
+#endif
 #ifndef TT_EXP_NOIDLE
 #define TT_EXP_NOIDLE 0  // small batches: padding-only waves run the MFMA stream too (A/B)
 #endif
@@ -907,7 +913,7 @@ __global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict_
     return;
   }
   constexpr int PER = SW_CAP / 64;
-  const int ni = (total + 63) / 64;
+  const int ni = __builtin_amdgcn_readfirstlane((total + 63) / 64);
   uint32_t hv[PER];
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
@@ -917,12 +923,12 @@ __global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict_
   uint32_t T = 0;
   for (int bit = 31; bit >= 0; --bit) {
     const uint32_t cand = T | (1u << bit);
+    // wave count by ballot + scalar popcount (a 6-step shuffle reduction per bit was a
+    // ~100-cycle dependent LDS chain: 32 of them dominated a lone query's selection)
     int cnt = 0;
 #pragma unroll
     for (int i = 0; i < PER; ++i)
-      if (i < ni) cnt += hv[i] >= cand ? 1 : 0;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+      if (i < ni) cnt += __popcll(__ballot(hv[i] >= cand));
     if (cnt >= R) T = cand;
   }
   const float A = key_float(T);
@@ -966,13 +972,13 @@ __global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict_
   }
 }
 
-// Register-resident variant of k_select_wave, used when n_slabs <= 64 (every level the
-// plans here produce): lane s holds slab s's count, and item e of the query's candidate
-// sequence (slabs in order) lives in lane e % 64, register e / 64.  Its slab is found by
-// walking the wave-uniform slab offsets that overlap the item's 64-wide range, so every list
-// load of the query is issued before the first use -- one memory latency per query instead
-// of one per 4 entries of its longest slab -- and no LDS buffer caps the occupancy.  Same
-// outputs as k_select_wave.
+// Register-resident variant of k_select_wave (n_slabs <= 64; GROUPED: <= 1024, the
+// small-batch levels' up-to-4-blocks-per-CU slabs, lane s owning slabs [sG, sG + G) with
+// G = ceil(n_slabs / 64)).  Item e of the query's candidate sequence lives in lane e % 64,
+// register e / 64; every list load of the query is issued before the first use, and the
+// selection runs on registers.  Same outputs as k_select_wave.
+constexpr int SR_GMAX = 16;
+template <bool GROUPED>
 __global__ __launch_bounds__(256) void k_select_reg(const uint64_t* __restrict__ lists,
                                                     const int* __restrict__ counts, int n_slabs,
                                                     int k, int J, const float* __restrict__ eps2,
@@ -988,69 +994,113 @@ __global__ __launch_bounds__(256) void k_select_reg(const uint64_t* __restrict__
   const int lane = threadIdx.x & 63;
   const int qid = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (qid >= nq) return;  // the whole wave (no block-level barriers below)
+#if TT_EXP_SEL_TIMING
+  uint64_t tstamp[8];
+  int ntst = 0;
+  tstamp[ntst++] = wall_clock64();
+#endif
   if (mode == 2 && lane < SH_P) pcount[(int64_t)qid * SH_P + lane] = 0;  // overflow: count 0
   if (flags[qid]) {
     if (lane == 0 && mode == 0) theta_out[qid] = __builtin_huge_valf();
     return;
   }
+
+#if TT_EXP_SEL_TIMING
+  tstamp[ntst++] = wall_clock64();
+#endif
   const int* qc = counts + (int64_t)qid * n_slabs;
   const uint64_t* ql = lists + (int64_t)qid * n_slabs * FL_CAP;
-  const int c = lane < n_slabs ? qc[lane] : 0;
+  constexpr int GM = GROUPED ? SR_GMAX : 1;
+  const int G = GROUPED ? (n_slabs + 63) / 64 : 1;  // slabs per lane
+  const int wv = threadIdx.x >> 6;
+  __shared__ uint16_t tbl_s[4][SW_CAP];     // item -> slab
+  __shared__ int soff_s[4][64 * GM];        // slab -> first item
+  int cj[GM];
+  int c = 0;
+  bool over = false;
+#pragma unroll
+  for (int j = 0; j < GM; ++j) {
+    const int sj = lane * G + j;
+    cj[j] = j < G && sj < n_slabs ? qc[sj] : 0;
+    c += cj[j];
+    over |= cj[j] > FL_CAP;
+  }
   int incl = c;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const int y = __shfl_up(incl, o, 64);
     incl += lane >= o ? y : 0;
   }
-  const int total = __shfl(incl, 63, 64);
-  if (__ballot(c > FL_CAP) != 0ull || total > SW_CAP) {
+  // wave-uniform in SGPRs: loop guards on ni become scalar branches (as a VGPR value the
+  // compiler had turned them into exec-masked regions with a VGPR counter)
+  const int total = __builtin_amdgcn_readfirstlane(__shfl(incl, 63, 64));
+  if (__ballot(over) != 0ull || total > SW_CAP) {
     if (lane == 0) {
       flag_query(qid, flags, qsel, qsel_n);
       if (mode == 0) theta_out[qid] = __builtin_huge_valf();
     }
     return;
   }
-  const int excl = incl - c;
   constexpr int PER = SW_CAP / 64;
-  const int ni = (total + 63) / 64;
+  const int ni = __builtin_amdgcn_readfirstlane((total + 63) / 64);
+
+#if TT_EXP_SEL_TIMING
+  tstamp[ntst++] = wall_clock64();
+#endif
   uint32_t hv[PER], lo[PER];
-  // item e = lane + 64 i lives in the last slab with excl <= e: binary search over the
-  // lanes' excl values (non-decreasing; an empty slab shares its successor's excl)
-  // lanes past n_slabs hold excl = INT_MAX: never <= a valid item
-  const int exs = lane < n_slabs ? excl : 0x7fffffff;
+  // item e of the query's candidate sequence (slabs in order) lives in lane e % 64, register
+  // e / 64.  Each lane writes the slab id of its slabs' items into a wave-private LDS table
+  // (plus each slab's first item); an item then needs two independent-per-item LDS reads to
+  // address its list entry, so all of the query's list loads are in flight at once.  (A
+  // per-item binary search over the lanes' offsets -- 6 dependent bpermutes -- made a lone
+  // query's selection latency-bound: ~30-40 us.)
+  {
+    int o = incl - c;
+#pragma unroll
+    for (int j = 0; j < GM; ++j) {
+      const int sj = lane * G + j;
+      if (j < G && sj < n_slabs) {
+        soff_s[wv][sj] = o;
+        for (int t = 0; t < cj[j]; ++t) tbl_s[wv][o + t] = (uint16_t)sj;
+        o += cj[j];
+      }
+    }
+  }
+  wave_sync();
+
+#if TT_EXP_SEL_TIMING
+  tstamp[ntst++] = wall_clock64();
+#endif
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     hv[i] = 0u;  // 0 = below every key
     lo[i] = 0u;
+    if (i < ni) {
+      const int e = lane + 64 * i;
+      if (e < total) {
+        const int sl = tbl_s[wv][e];
+        const uint64_t key = ql[(int64_t)sl * FL_CAP + (e - soff_s[wv][sl])];
+        hv[i] = (uint32_t)(key >> 32);
+        lo[i] = (uint32_t)key;
+      }
+    }
   }
-  for (int i0 = 0; i0 < ni; i0 += 4) {
-    uint32_t off[4];
+
+#if TT_EXP_SEL_TIMING
+  tstamp[ntst++] = wall_clock64();
+#endif
+#if TT_EXP_SEL_TIMING
+  { uint32_t m = 0;
+    for (int i = 0; i < PER; ++i) m ^= hv[i];
+    if (m == 0x1234567u) theta_out[qid] = 1.f; }
+  tstamp[ntst++] = wall_clock64();
+#endif
+  if (TT_EXP_SEL_STOP == 1) {  // timing only: stop after the gather
+    uint32_t m = 0;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = lane + 64 * (i0 + u);
-      int sl = 0;
-#pragma unroll
-      for (int b = 5; b >= 0; --b) {
-        const int cand = sl + (1 << b);
-        if (__shfl(exs, cand & 63, 64) <= e) sl = cand;
-      }
-      // every lane takes part in the bpermute (an inactive source lane returns garbage)
-      const int base = __shfl(exs, sl, 64);
-      off[u] = e < total ? (uint32_t)(sl * FL_CAP + (e - base)) : 0xffffffffu;
-    }
-    uint64_t key[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) key[u] = off[u] != 0xffffffffu ? ql[off[u]] : 0ull;
-#pragma unroll
-    for (int i = 0; i < PER; i += 4) {
-      if (i == i0) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          hv[i + u] = (uint32_t)(key[u] >> 32);
-          lo[i + u] = (uint32_t)key[u];
-        }
-      }
-    }
+    for (int i = 0; i < PER; ++i) m ^= hv[i] ^ lo[i];
+    if (m == 0x12345u) theta_out[qid] = 0.f;
+    return;
   }
   if (mode == 2) {
     // sharded full level: every candidate (a >= theta_g - eps2) is band; the shard's count of
@@ -1101,15 +1151,25 @@ __global__ __launch_bounds__(256) void k_select_reg(const uint64_t* __restrict__
   uint32_t T = 0;
   for (int bit = 31; bit >= 0; --bit) {
     const uint32_t cand = T | (1u << bit);
+    // wave count by ballot + scalar popcount (a 6-step shuffle reduction per bit was a
+    // ~100-cycle dependent LDS chain: 32 of them dominated a lone query's selection)
     int cnt = 0;
 #pragma unroll
-    for (int i = 0; i < PER; ++i)
-      if (i < ni) cnt += hv[i] >= cand ? 1 : 0;
+    for (int i0 = 0; i0 < PER; i0 += 4)  // one branch per 4 registers (unused ones hold 0)
+      if (i0 < ni)
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+        for (int u = 0; u < 4; ++u) cnt += __popcll(__ballot(hv[i0 + u] >= cand));
     if (cnt >= R) T = cand;
   }
+  if (TT_EXP_SEL_STOP == 2) {  // timing only: stop after the bitwise search
+    if (lane == 0 && T == 0x12345u) theta_out[qid] = 0.f;
+    return;
+  }
   const float A = key_float(T);
+
+#if TT_EXP_SEL_TIMING
+  tstamp[ntst++] = wall_clock64();
+#endif
   if (mode == 0) {
     if (smax_out) {  // sharded: the sample's best a (upper end of the probe range)
       uint32_t m = 0;
@@ -1143,6 +1203,14 @@ __global__ __launch_bounds__(256) void k_select_reg(const uint64_t* __restrict__
       nb += __popcll(bm);
     }
   }
+#if TT_EXP_SEL_TIMING
+  tstamp[ntst++] = wall_clock64();
+  if (lane == 0 && qid == 0 && n_slabs > 64)
+    printf("SELT mode=%d n_slabs=%d total=%d: %d %d %d %d %d %d %d\n", mode, n_slabs, total,
+           (int)(tstamp[1] - tstamp[0]), (int)(tstamp[2] - tstamp[1]), (int)(tstamp[3] - tstamp[2]),
+           (int)(tstamp[4] - tstamp[3]), (int)(tstamp[5] - tstamp[4]), (int)(tstamp[6] - tstamp[5]),
+           ntst > 7 ? (int)(tstamp[7] - tstamp[6]) : -1);
+#endif
   if (lane == 0) {
     if (nb > BAND_CAP) flag_query(qid, flags, qsel, qsel_n);
     else band_n[qid] = nb;
@@ -1584,7 +1652,10 @@ int filter_level(const FilterPlan& p, const FilterWs& w, int li, int mode, const
   if (rc) return rc;
   if (last && ev_stop && hipEventRecord((hipEvent_t)ev_stop, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "hipEventRecord(stop)");
-  auto sel = L.n_slabs <= 64 && !select_reg_disabled() ? k_select_reg : k_select_wave;
+  auto sel = select_reg_disabled()  ? k_select_wave
+             : L.n_slabs <= 64      ? k_select_reg<false>
+             : L.n_slabs <= 64 * SR_GMAX ? k_select_reg<true>
+                                    : k_select_wave;
   hipLaunchKernelGGL(sel, dim3((nq + 3) / 4), dim3(256), 0, st, w.lists, w.counts,
                      L.n_slabs, k, p.J, w.eps2, mode, w.theta, w.aref, w.band, w.band_n, w.flags,
                      w.qsel, w.qsel_n, nq, stats, pcount, smax_out);
