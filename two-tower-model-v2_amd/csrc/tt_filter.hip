@@ -814,7 +814,8 @@ __global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict_
                                                      int* qsel_n, int nq,
                                                      const float* __restrict__ stats,
                                                      int* __restrict__ pcount,
-                                                     float* __restrict__ smax_out) {
+                                                     float* __restrict__ smax_out,
+                                                     int fin) {
   __shared__ uint64_t buf[4][SW_CAP];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int qid = blockIdx.x * 4 + w;
@@ -941,8 +942,8 @@ __global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict_
       for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
       if (lane == 0) smax_out[qid] = key_float(m);
     }
-    if (lane == 0) {
-      theta_out[qid] = A;
+    if (lane == 0) {  // fin: the next level is the full one -> its threshold A - 2 eps
+      theta_out[qid] = fin ? A - eps2[qid] : A;
       aref[qid] = A;
     }
     return;
@@ -990,7 +991,8 @@ __global__ __launch_bounds__(256) void k_select_reg(const uint64_t* __restrict__
                                                     int* qsel_n, int nq,
                                                     const float* __restrict__ stats,
                                                     int* __restrict__ pcount,
-                                                    float* __restrict__ smax_out) {
+                                                    float* __restrict__ smax_out,
+                                                    int fin) {
   const int lane = threadIdx.x & 63;
   const int qid = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (qid >= nq) return;  // the whole wave (no block-level barriers below)
@@ -1179,8 +1181,8 @@ __global__ __launch_bounds__(256) void k_select_reg(const uint64_t* __restrict__
       for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
       if (lane == 0) smax_out[qid] = key_float(m);
     }
-    if (lane == 0) {
-      theta_out[qid] = A;
+    if (lane == 0) {  // fin: the next level is the full one -> its threshold A - 2 eps
+      theta_out[qid] = fin ? A - eps2[qid] : A;
       aref[qid] = A;
     }
     return;
@@ -1316,9 +1318,19 @@ __global__ void k_fill_f32(float* x, int n, float v) {
 template <int EP>
 __global__ __launch_bounds__(256) void k_query_eps(const float* __restrict__ q, int nq,
                                                    int64_t ldq, float X, float R,
-                                                   float* __restrict__ eps2) {
+                                                   float* __restrict__ eps2,
+                                                   float* __restrict__ theta,
+                                                   float* __restrict__ aref,
+                                                   int* __restrict__ flags,
+                                                   int* __restrict__ qsel_n) {
   const int qi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (qi >= nq) return;
+  if (lane == 0) {  // filter state of query qi
+    theta[qi] = -__builtin_huge_valf();
+    aref[qi] = -__builtin_huge_valf();
+    flags[qi] = 0;
+    if (qi == 0) *qsel_n = 0;
+  }
   const float* qr = q + (int64_t)qi * ldq;
   float sq = 0.0f, st = 0.0f, sr = 0.0f;
   for (int i = lane; i < EP; i += 64) {
@@ -1610,19 +1622,13 @@ int filter_init(const FilterWs& w, const float* q, int nq, int64_t ld_q, int ep,
                 float x_resid_max, hipStream_t st) {
   TT_REQUIRE(x_norm_max >= 0.0f && x_resid_max >= 0.0f,
              "x_norm_max / x_resid_max must be >= 0 (tt_bf16_image_bounds)");
-  if (hipMemsetAsync(w.flags, 0, ((size_t)2 * nq + 1) * 4, st) != hipSuccess)
-    return fail(TT_ERR_LAUNCH, "hipMemsetAsync(flags)");
-  const unsigned fill_grid = (unsigned)((nq + 255) / 256);
-  hipLaunchKernelGGL(k_fill_f32, dim3(fill_grid), dim3(256), 0, st, w.theta, nq,
-                     -__builtin_huge_valf());
-  hipLaunchKernelGGL(k_fill_f32, dim3(fill_grid), dim3(256), 0, st, w.aref, nq,
-                     -__builtin_huge_valf());
+  // one launch: k_query_eps also resets flags / theta / aref / qsel_n (was a memset + 2 fills)
   const unsigned eps_grid = (unsigned)((nq + 3) / 4);
   switch (ep) {
 #define TT_QE(E)                                                                              \
   case E:                                                                                     \
     hipLaunchKernelGGL(k_query_eps<E>, dim3(eps_grid), dim3(256), 0, st, q, nq, ld_q,         \
-                       x_norm_max, x_resid_max, w.eps2);                                      \
+                       x_norm_max, x_resid_max, w.eps2, w.theta, w.aref, w.flags, w.qsel_n); \
     break;
     TT_QE(64) TT_QE(128) TT_QE(256) TT_QE(384) TT_QE(512) TT_QE(768)
 #undef TT_QE
@@ -1634,7 +1640,7 @@ int filter_init(const FilterWs& w, const float* q, int nq, int64_t ld_q, int ep,
 int filter_level(const FilterPlan& p, const FilterWs& w, int li, int mode, const uint16_t* db16,
                  int64_t n, int64_t ld_db, const float* q, int nq, int64_t ld_q, int k, int ep,
                  hipStream_t st, void* ev_start, void* ev_stop, const float* stats = nullptr,
-                 int* pcount = nullptr, float* smax_out = nullptr) {
+                 int* pcount = nullptr, float* smax_out = nullptr, int fin = 0) {
   const Level& L = p.lv[li];
   const bool last = li == p.n_levels - 1;
   if (last && ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
@@ -1658,7 +1664,7 @@ int filter_level(const FilterPlan& p, const FilterWs& w, int li, int mode, const
                                     : k_select_wave;
   hipLaunchKernelGGL(sel, dim3((nq + 3) / 4), dim3(256), 0, st, w.lists, w.counts,
                      L.n_slabs, k, p.J, w.eps2, mode, w.theta, w.aref, w.band, w.band_n, w.flags,
-                     w.qsel, w.qsel_n, nq, stats, pcount, smax_out);
+                     w.qsel, w.qsel_n, nq, stats, pcount, smax_out, fin);
   return check_launch("k_select");
 }
 
@@ -1712,9 +1718,11 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
   if ((rc = filter_init(w, q, nq, ld_q, ep, x_norm_max, x_resid_max, st))) return rc;
   for (int li = 0; li < p.n_levels; ++li) {
     const bool last = li == p.n_levels - 1;
-    if (last && li > 0 && (rc = full_threshold(w, nq, st))) return rc;
+    // the last sample level's selection writes the full level's threshold a_J - 2 eps itself
+    // (was a copy + k_sub_arr launch: full_threshold, kept for the sharded protocol)
+    const int fin = li == p.n_levels - 2;
     if ((rc = filter_level(p, w, li, last ? 1 : 0, db_bf16, n, ld_db, q, nq, ld_q, k, ep, st,
-                           ev_start, ev_stop)))
+                           ev_start, ev_stop, nullptr, nullptr, nullptr, fin)))
       return rc;
   }
   return filter_finish(w, db, n, d, ld_db, row_base, q, nq, ld_q, k, ep, out_score, out_idx, st);
