@@ -171,7 +171,9 @@ def _grad_worker(rank, world, port, q):
         grads = {"proj0.w": torch.randn(256, 512, generator=g), "att2.b": torch.randn(1, generator=g),
                  "brand": torch.randn(51, 64, generator=g)}
         allreduce_mean(grads)
-        q.put((rank, {k: v.clone() for k, v in grads.items()}))
+        # numpy by value: a torch tensor crosses the queue as a shared-memory handle that dies
+        # with this process if it exits before the parent has received it
+        q.put((rank, {k: v.numpy().copy() for k, v in grads.items()}))
     finally:
         dist.destroy_process_group()
 
@@ -199,4 +201,4 @@ def test_train_gradient_allreduce_mean(world):
             exp[k] = exp.get(k, 0) + v / world
     for r in range(world):
         for k in exp:
-            torch.testing.assert_close(res[r][k], exp[k], rtol=1e-6, atol=1e-6)
+            torch.testing.assert_close(torch.from_numpy(res[r][k]), exp[k], rtol=1e-6, atol=1e-6)
