@@ -706,6 +706,9 @@ constexpr int GL_STORES = 4 * GL_NJ * 2;
 // + tools/exp_gemm.sh.  Measured at M = 370761 (K = 384 / 1536): base 471 / 752 us, no W
 // stream after the prologue 439 / 669, no epilogue 111 / 504 -> the LayerNorm epilogue (its
 // residual reads and x / x16 writes, 1.42 GB at K = 384) is what the fused kernel waits on.
+#ifndef TT_GL_NT
+#define TT_GL_NT 0  // A (read once: a block owns whole rows) non-temporal: A/B no change
+#endif
 #ifndef TT_GLEXP_NOW
 #define TT_GLEXP_NOW 0  // W streamed for the first stages only
 #endif
@@ -762,7 +765,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
     for (int j = 0; j < 2; ++j)
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(A + ao[j] + k0),
-          (__attribute__((address_space(3))) void*)(st + 1024 * (w + 8 * j)), 16, 0, 0);
+          (__attribute__((address_space(3))) void*)(st + 1024 * (w + 8 * j)), 16, 0,
+          TT_GL_NT ? 2 : 0);
   };
   auto issue_w = [&](int kt, int t) __attribute__((always_inline)) {
     char* st = smem + GL_WBASE + (t % GL_WSLOTS) * GL_W_B;

@@ -242,6 +242,16 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #ifndef TT_EXP_PRIO
 #define TT_EXP_PRIO 0  // s_setprio 1 for waves 4-7 (static priority for the younger half)
 #endif
+#ifndef TT_RING_NT
+// Non-temporal (aux = 2) ring DMA.  1 (default): the small-batch full level (LVL 2: one query
+// tile, so every catalog byte is read exactly once) -- one-buyer full level 0.139 -> 0.124 ms
+// (5.6 -> 6.2 TB/s), batched level unchanged; 3 = every level: the batched full level, whose
+// 40 query tiles re-read the catalog from L2/MALL, 6.85 -> 7.29 ms (A/B, same box).
+#define TT_RING_NT 1
+#endif
+#ifndef TT_RR_NT
+#define TT_RR_NT 0  // k_rerank: band rows loaded non-temporal (A/B: re-rank 0.65 -> 1.75 ms)
+#endif
 #ifndef TT_EXP_MAXONLY
 #define TT_EXP_MAXONLY 0  // per-block max + ballot only (no per-slot scan)
 #endif
@@ -396,7 +406,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(
                                            slot + (w + RG_WAVES * pp) * 1024),
-                                       16, 0, 0);
+                                       16, 0, ((TT_RING_NT >= 1 && LVL == 2) || TT_RING_NT >= 3) ? 2 : 0);
     }
   };
   auto issue = [&](int t) __attribute__((always_inline)) {
@@ -1277,7 +1287,14 @@ __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, in
     float acc = 0.0f;
 #pragma unroll 4
     for (int t = 0; t < EP / 16; ++t) {
+#if TT_RR_NT
+      const f32x4 x0 = __builtin_nontemporal_load(xr + 4 * t + 0),
+                  x1 = __builtin_nontemporal_load(xr + 4 * t + 1),
+                  x2 = __builtin_nontemporal_load(xr + 4 * t + 2),
+                  x3 = __builtin_nontemporal_load(xr + 4 * t + 3);
+#else
       const f32x4 x0 = xr[4 * t + 0], x1 = xr[4 * t + 1], x2 = xr[4 * t + 2], x3 = xr[4 * t + 3];
+#endif
       const float* qt = qs + 16 * t;
       // canonical order: for i: for g: d = 16t + 4g + i
 #pragma unroll
