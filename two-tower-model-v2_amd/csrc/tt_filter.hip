@@ -249,6 +249,15 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 // 40 query tiles re-read the catalog from L2/MALL, 6.85 -> 7.29 ms (A/B, same box).
 #define TT_RING_NT 1
 #endif
+#ifndef TT_RR_STAGED
+// k_rerank: 1 (default) = wave-cooperative 256-B row pieces through an LDS stage, 0 = each
+// thread loads its own row (64 rows per wave-instruction): re-rank ~0.65 -> ~0.45 ms per 10k
+// queries at 1M x 384 (search minus full level 1.34 -> 1.13-1.15 ms, A/B on two boxes)
+#define TT_RR_STAGED 1
+#endif
+#ifndef TT_RR_PF
+#define TT_RR_PF 1  // k_rerank staged: chunks loaded ahead (2: 128 more VGPRs, +0.28 ms)
+#endif
 #ifndef TT_RR_NT
 #define TT_RR_NT 0  // k_rerank: band rows loaded non-temporal (A/B: re-rank 0.65 -> 1.75 ms)
 #endif
@@ -1281,6 +1290,83 @@ __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, in
     qband = buf;
   }
   __syncthreads();
+#if TT_RR_STAGED
+  // Each wave takes 64 band rows at a time and fetches them 64 dimensions (256 B per row) per
+  // chunk: 16 lanes per row, 4 rows per wave-instruction, 16 instructions in flight (the next
+  // chunk is loaded while this one is summed).  The chunk goes through a wave-private LDS
+  // stage (16-B pieces XOR-swizzled by row: conflict-free writes and reads), and lane j then
+  // runs row j's canonical FMA chain over those 64 dimensions -- the same order as below.
+  // (Thread-per-row loads put 64 rows into every wave-instruction.)
+  {
+    __shared__ __attribute__((aligned(16))) char stage[4][64 * 256];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    char* st = stage[w];
+    const int sub = lane >> 4, piece = lane & 15;
+    for (int e0 = 64 * w; e0 < nb; e0 += 256) {
+      const int ej = e0 + lane;
+      const uint32_t rj = key_row(qband[ej < nb ? ej : e0]);
+      const float* rp[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t r = (uint32_t)__shfl((int)rj, 4 * i + sub, 64);
+        rp[i] = db + (int64_t)r * ld + 4 * piece;
+      }
+      constexpr int NC = EP / 64, PF = TT_RR_PF;  // chunks; chunks loaded ahead
+      float acc = 0.0f;
+      // stage chunk c from v, refill v with chunk c + PF, run the chain over chunk c
+      auto chunk = [&](int c, f32x4 (&v)[16]) __attribute__((always_inline)) {
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = 4 * i + sub;
+          *(f32x4*)(st + row * 256 + 16 * (piece ^ (row & 15))) = v[i];
+        }
+        asm volatile("" ::: "memory");
+        if (c + PF < NC) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) v[i] = *(const f32x4*)(rp[i] + 64 * (c + PF));
+        }
+        const char* my = st + lane * 256;
+        const int sw = lane & 15;
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+          const f32x4 x0 = *(const f32x4*)(my + 16 * ((4 * tt + 0) ^ sw));
+          const f32x4 x1 = *(const f32x4*)(my + 16 * ((4 * tt + 1) ^ sw));
+          const f32x4 x2 = *(const f32x4*)(my + 16 * ((4 * tt + 2) ^ sw));
+          const f32x4 x3 = *(const f32x4*)(my + 16 * ((4 * tt + 3) ^ sw));
+          const float* qt = qs + 64 * c + 16 * tt;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            acc = fmaf(x0[i], qt[0 + i], acc);
+            acc = fmaf(x1[i], qt[4 + i], acc);
+            acc = fmaf(x2[i], qt[8 + i], acc);
+            acc = fmaf(x3[i], qt[12 + i], acc);
+          }
+        }
+      };
+      f32x4 v0[16], v1[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v0[i] = *(const f32x4*)rp[i];
+      if (PF == 2 && NC > 1) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v1[i] = *(const f32x4*)(rp[i] + 64);
+      }
+      if constexpr (PF == 1) {
+#pragma unroll 1
+        for (int c = 0; c < NC; ++c) chunk(c, v0);
+      } else {
+#pragma unroll 1
+        for (int c = 0; c < NC; c += 2) {
+          chunk(c, v0);
+          if (c + 1 < NC) chunk(c + 1, v1);
+        }
+      }
+      asm volatile("" ::: "memory");
+      if (ej < nb) buf[ej] = acc != acc ? 0ull : make_key(acc, rj);
+    }
+  }
+  __syncthreads();
+#else
   for (int e = threadIdx.x; e < nb; e += blockDim.x) {
     const uint32_t r = key_row(qband[e]);
     const f32x4* xr = (const f32x4*)(db + (int64_t)r * ld);
@@ -1307,6 +1393,7 @@ __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, in
     }
     buf[e] = acc != acc ? 0ull : make_key(acc, r);
   }
+#endif
   const int np = pow2_at_least(nb);
   for (int i = nb + threadIdx.x; i < np; i += blockDim.x) buf[i] = 0ull;
   block_sort_desc(buf, np);
