@@ -249,6 +249,15 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 // 40 query tiles re-read the catalog from L2/MALL, 6.85 -> 7.29 ms (A/B, same box).
 #define TT_RING_NT 1
 #endif
+// Candidate scan of the previous tile split into per-query-block pieces spread between the
+// MFMAs (1, default) instead of one burst at step 1 (0): batched full level 6.81 -> 6.65 ms
+// (A/B x2, same box); per-(query block, row block) pieces (2): 6.75 ms.
+#ifndef TT_SPLIT_APPEND
+#define TT_SPLIT_APPEND 1
+#endif
+#ifndef TT_SPLIT_STEP
+#define TT_SPLIT_STEP 0  // k-steps between pieces (0: KS / pieces)
+#endif
 #ifndef TT_RR_STAGED
 // k_rerank: 1 (default) = wave-cooperative 256-B row pieces through an LDS stage, 0 = each
 // thread loads its own row (64 rows per wave-instruction): re-rank ~0.65 -> ~0.45 ms per 10k
@@ -467,9 +476,10 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   // One v_cmp + scalar branch per candidate slot; lanes of a non-empty slot write at
   // wn + (passing lanes below).  An entry past the wave's pool marks its query overflowed
   // (-> exact fallback).  Rows past the slab end (its last tile only) are masked to -inf first.
-  auto append = [&](f32x4 (&sc)[RB][QB], const float (&mx)[QB], int t) __attribute__((always_inline)) {
+  auto append = [&](f32x4 (&sc)[RB][QB], const float (&mx)[QB], int t, int b_lo,
+                    int b_hi, int rb_lo, int rb_hi) __attribute__((always_inline)) {
     const int64_t jt = j0 + (int64_t)t * TR;
-    if (jt + TR > j1) {
+    if (b_lo == 0 && rb_lo == 0 && jt + TR > j1) {
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
@@ -481,6 +491,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
     const uint32_t rlane = (uint32_t)((jt + 4 * g) * stride);
 #pragma unroll
     for (int b = 0; b < QB; ++b) {
+      if (b < b_lo || b >= b_hi) continue;
       if (__ballot(mx[b] >= th[b]) == 0ull) continue;
       if (TT_EXP_MAXONLY) {
         asm volatile("" ::: "memory");
@@ -491,6 +502,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
       for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
+          if (rb < rb_lo || rb >= rb_hi) continue;
           const float v = sc[rb][b][jj];
           const uint64_t bm = __ballot(v >= th[b]);
           if (bm != 0ull) {
@@ -566,6 +578,8 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   // FD + 1 divides KS (the ring index is s % (FD + 1)); 2 steps ahead where registers are tight
   constexpr int FD = (EP >= 384 && KS % 3 == 0) ? 2 : (KS >= 4 ? 3 : 1);
   constexpr int S_MID = (KS - FD) / 2;
+  constexpr int SPLIT_SP1 = TT_SPLIT_STEP > 0 ? TT_SPLIT_STEP : KS / QB;         // see below
+  constexpr int SPLIT_SP2 = TT_SPLIT_STEP > 0 ? TT_SPLIT_STEP : KS / (QB * RB);
   static_assert(KS % (FD + 1) == 0 && S_MID < KS - FD, "fragment ring layout");
   for (int t = 0; t < RG_PD && t < n_tiles; ++t) issue(t);
   wait_tiles(n_tiles - 1 < RG_PD - 1 ? n_tiles - 1 : RG_PD - 1);
@@ -658,10 +672,32 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
             if (!TT_EXP_NOBAR) asm volatile("s_barrier" ::: "memory");
             if (!TT_EXP_NODMA && t + RG_PD < n_tiles) issue(t + RG_PD);
           }
+          // TT_SPLIT_APPEND: query block b's candidate scan at step 1 + b * KS / QB (spread
+          // between the MFMAs) instead of all blocks at step 1
+          // Candidate scan of tile t-1 in pieces spread between tile t's MFMAs: piece P at step
+          // 1 + P * SP (TT_SPLIT_APPEND 1: one query block per piece; 2: one (query block, row
+          // block) per piece); piece 0 runs at step 1 below.
+          constexpr int NP = TT_SPLIT_APPEND == 2 ? QB * RB : QB;  // pieces per tile
+          constexpr int SP = TT_SPLIT_STEP > 0 ? TT_SPLIT_STEP : (NP > 0 ? KS / NP : 1);
+          if constexpr (TT_SPLIT_APPEND && LVL != 0 && NP > 1 && 1 + (NP - 1) * SP < KS &&
+                        s > 1 && (s - 1) % SP == 0 && (s - 1) / SP < NP) {
+            constexpr int P = (s - 1) / SP;
+            if (!TT_EXP_NOSEL) {
+              if constexpr (TT_SPLIT_APPEND == 2)
+                append(accp, mx, t - 1, P / RB, P / RB + 1, P % RB, P % RB + 1);
+              else
+                append(accp, mx, t - 1, P, P + 1, 0, RB);
+            }
+          }
           if constexpr (s == (KS > 1 ? 1 : 0)) {  // early: tile t-1's scores die before the peak
             if (!TT_EXP_NOSEL) {
               if constexpr (LVL == 0 && !TT_EXP_SAMPLE_ROWS) append_tmax(mx, t - 1);
-              else append(accp, mx, t - 1);
+              else if constexpr (TT_SPLIT_APPEND == 2 && QB * RB > 1 &&
+                                 1 + (QB * RB - 1) * SPLIT_SP2 < KS)
+                append(accp, mx, t - 1, 0, 1, 0, 1);
+              else if constexpr (TT_SPLIT_APPEND == 1 && QB > 1 && 1 + (QB - 1) * SPLIT_SP1 < KS)
+                append(accp, mx, t - 1, 0, 1, 0, RB);
+              else append(accp, mx, t - 1, 0, QB, 0, RB);
             }
             if (TT_EXP_NOSEL) {
 #pragma unroll
@@ -682,7 +718,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
     float mx[QB];
     tile_max(accp, mx);
     if constexpr (LVL == 0 && !TT_EXP_SAMPLE_ROWS) append_tmax(mx, n_tiles - 1);
-    else append(accp, mx, n_tiles - 1);
+    else append(accp, mx, n_tiles - 1, 0, QB, 0, RB);
   }
   wait_vm<0>();
   flush();
