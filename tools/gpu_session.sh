@@ -22,7 +22,7 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     bench_f32) run bench_f32 600 python bench.py --method f32 --no-cpu-baseline ${BENCH_ARGS:-} ;;
-    prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 3 --warmup 1 ${BENCH_ARGS:-} ;;
+    prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps ${PROF_STEPS:-3} --warmup ${PROF_WARMUP:-1} ${BENCH_ARGS:-} ;;
     pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 2 --warmup 1 ${BENCH_ARGS:-}
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 2 --warmup 1 ${BENCH_ARGS:-} ;;
     sq)    run pmc_sq1 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA --kernel-trace -d gpurun_out/pmc_sq1 -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 1 --warmup 1 ${BENCH_ARGS:-}
