@@ -255,6 +255,9 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #ifndef TT_SPLIT_APPEND
 #define TT_SPLIT_APPEND 1
 #endif
+#ifndef TT_SPLIT_TMAX
+#define TT_SPLIT_TMAX 0  // sample levels: tile-max appends split the same way (A/B: +15 us)
+#endif
 #ifndef TT_SPLIT_STEP
 #define TT_SPLIT_STEP 0  // k-steps between pieces (0: KS / pieces)
 #endif
@@ -532,10 +535,11 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   // (row id unused by the mode-0 selection) -- two cross-lane max steps and one ballot per
   // query block instead of 8 ballot rounds; at the stride-16 level ~95% of (tile, block)
   // pairs held a candidate.
-  auto append_tmax = [&](const float (&mx)[QB], int t) __attribute__((always_inline)) {
+  auto append_tmax = [&](const float (&mx)[QB], int t, int b_lo, int b_hi) __attribute__((always_inline)) {
     const uint32_t r = (uint32_t)((j0 + (int64_t)t * TR) * stride);
 #pragma unroll
     for (int b = 0; b < QB; ++b) {
+      if (b < b_lo || b >= b_hi) continue;
       float m = mx[b];  // rows past the slab end are clamped copies of a real row: no mask
       m = fmaxf(m, __shfl_xor(m, 16, 64));
       m = fmaxf(m, __shfl_xor(m, 32, 64));
@@ -679,11 +683,13 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
           // block) per piece); piece 0 runs at step 1 below.
           constexpr int NP = TT_SPLIT_APPEND == 2 ? QB * RB : QB;  // pieces per tile
           constexpr int SP = TT_SPLIT_STEP > 0 ? TT_SPLIT_STEP : (NP > 0 ? KS / NP : 1);
-          if constexpr (TT_SPLIT_APPEND && LVL != 0 && NP > 1 && 1 + (NP - 1) * SP < KS &&
+          if constexpr (TT_SPLIT_APPEND && NP > 1 && 1 + (NP - 1) * SP < KS &&
                         s > 1 && (s - 1) % SP == 0 && (s - 1) / SP < NP) {
             constexpr int P = (s - 1) / SP;
             if (!TT_EXP_NOSEL) {
-              if constexpr (TT_SPLIT_APPEND == 2)
+              if constexpr (LVL == 0 && !TT_EXP_SAMPLE_ROWS) {
+                if constexpr (TT_SPLIT_TMAX && TT_SPLIT_APPEND == 1) append_tmax(mx, t - 1, P, P + 1);
+              } else if constexpr (TT_SPLIT_APPEND == 2)
                 append(accp, mx, t - 1, P / RB, P / RB + 1, P % RB, P % RB + 1);
               else
                 append(accp, mx, t - 1, P, P + 1, 0, RB);
@@ -691,7 +697,10 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
           }
           if constexpr (s == (KS > 1 ? 1 : 0)) {  // early: tile t-1's scores die before the peak
             if (!TT_EXP_NOSEL) {
-              if constexpr (LVL == 0 && !TT_EXP_SAMPLE_ROWS) append_tmax(mx, t - 1);
+              if constexpr (LVL == 0 && !TT_EXP_SAMPLE_ROWS)
+                append_tmax(mx, t - 1, 0,
+                            (TT_SPLIT_TMAX && TT_SPLIT_APPEND == 1 && QB > 1 &&
+                             1 + (QB - 1) * SPLIT_SP1 < KS) ? 1 : QB);
               else if constexpr (TT_SPLIT_APPEND == 2 && QB * RB > 1 &&
                                  1 + (QB * RB - 1) * SPLIT_SP2 < KS)
                 append(accp, mx, t - 1, 0, 1, 0, 1);
@@ -717,7 +726,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   if (n_tiles > 0 && !TT_EXP_NOSEL) {
     float mx[QB];
     tile_max(accp, mx);
-    if constexpr (LVL == 0 && !TT_EXP_SAMPLE_ROWS) append_tmax(mx, n_tiles - 1);
+    if constexpr (LVL == 0 && !TT_EXP_SAMPLE_ROWS) append_tmax(mx, n_tiles - 1, 0, QB);
     else append(accp, mx, n_tiles - 1, 0, QB, 0, RB);
   }
   wait_vm<0>();
