@@ -258,6 +258,9 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #ifndef TT_SPLIT_TMAX
 #define TT_SPLIT_TMAX 0  // sample levels: tile-max appends split the same way (A/B: +15 us)
 #endif
+#ifndef TT_SPLIT_START
+#define TT_SPLIT_START 2  // k-step of the first piece (2 vs 1: 6.64 vs 6.72 ms, A/B x2)
+#endif
 #ifndef TT_SPLIT_STEP
 #define TT_SPLIT_STEP 0  // k-steps between pieces (0: KS / pieces)
 #endif
@@ -584,6 +587,9 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   constexpr int S_MID = (KS - FD) / 2;
   constexpr int SPLIT_SP1 = TT_SPLIT_STEP > 0 ? TT_SPLIT_STEP : KS / QB;         // see below
   constexpr int SPLIT_SP2 = TT_SPLIT_STEP > 0 ? TT_SPLIT_STEP : KS / (QB * RB);
+  // TT_SPLIT_START > 1: the per-query-block pieces start at that step instead of step 1
+  constexpr bool SPLIT_MOVED = TT_SPLIT_START > 1 && TT_SPLIT_APPEND == 1 && LVL != 0 &&
+                               QB > 1 && TT_SPLIT_START + (QB - 1) * SPLIT_SP1 < KS;
   static_assert(KS % (FD + 1) == 0 && S_MID < KS - FD, "fragment ring layout");
   for (int t = 0; t < RG_PD && t < n_tiles; ++t) issue(t);
   wait_tiles(n_tiles - 1 < RG_PD - 1 ? n_tiles - 1 : RG_PD - 1);
@@ -683,7 +689,12 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
           // block) per piece); piece 0 runs at step 1 below.
           constexpr int NP = TT_SPLIT_APPEND == 2 ? QB * RB : QB;  // pieces per tile
           constexpr int SP = TT_SPLIT_STEP > 0 ? TT_SPLIT_STEP : (NP > 0 ? KS / NP : 1);
-          if constexpr (TT_SPLIT_APPEND && NP > 1 && 1 + (NP - 1) * SP < KS &&
+          if constexpr (SPLIT_MOVED && s >= TT_SPLIT_START && (s - TT_SPLIT_START) % SPLIT_SP1 == 0 &&
+                        (s - TT_SPLIT_START) / SPLIT_SP1 < QB) {
+            constexpr int P = (s - TT_SPLIT_START) / SPLIT_SP1;
+            if (!TT_EXP_NOSEL) append(accp, mx, t - 1, P, P + 1, 0, RB);
+          }
+          if constexpr (!SPLIT_MOVED && TT_SPLIT_APPEND && NP > 1 && 1 + (NP - 1) * SP < KS &&
                         s > 1 && (s - 1) % SP == 0 && (s - 1) / SP < NP) {
             constexpr int P = (s - 1) / SP;
             if (!TT_EXP_NOSEL) {
@@ -701,7 +712,8 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
                 append_tmax(mx, t - 1, 0,
                             (TT_SPLIT_TMAX && TT_SPLIT_APPEND == 1 && QB > 1 &&
                              1 + (QB - 1) * SPLIT_SP1 < KS) ? 1 : QB);
-              else if constexpr (TT_SPLIT_APPEND == 2 && QB * RB > 1 &&
+              else if constexpr (SPLIT_MOVED) {
+              } else if constexpr (TT_SPLIT_APPEND == 2 && QB * RB > 1 &&
                                  1 + (QB * RB - 1) * SPLIT_SP2 < KS)
                 append(accp, mx, t - 1, 0, 1, 0, 1);
               else if constexpr (TT_SPLIT_APPEND == 1 && QB > 1 && 1 + (QB - 1) * SPLIT_SP1 < KS)
