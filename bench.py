@@ -148,6 +148,28 @@ def mode_a(a, dev, world, rank, search_local, k, E):
     return res, cpu_inputs
 
 
+def self_check(a, out, q, table, shard, dev, world, nsub=64):
+    """The timed path checks its own results: nsub of this rank's buyers (spread over all
+    query tiles) re-searched by the exact f32 MFMA scan (tt_scan_topk_f32, bit-exact vs the C
+    oracle in tests/) over the WHOLE catalog; ids and scores must match bit for bit."""
+    N, E, K, B = a.catalog, a.dim, a.k, q.shape[0]
+    sub = torch.linspace(0, B - 1, min(nsub, B), device=dev).round().long().unique()
+    if world == 1:
+        full = shard
+    else:  # the whole catalog, normalised exactly like the shards were
+        full = torch.empty_like(table)
+        kernels.l2norm_rows(table, E, _lib.TT_NORM_ADD_EPS, out=full)
+    fs, fi = kernels.scan_topk(full, N, E, q[sub].contiguous(), K)
+    bad = ((out[1][sub] != fi) | (out[0][sub] != fs)).any(dim=1).sum().to(torch.int64)
+    n = torch.tensor([sub.numel()], device=dev, dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(bad)
+        dist.all_reduce(n)
+        del full
+    return {"queries": int(n.item()), "mismatched_queries": int(bad.item()),
+            "vs": "tt_scan_topk_f32 over the whole catalog (exact f32, bit-exact ids+scores)"}
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", 0))
@@ -273,6 +295,7 @@ def main():
         dt, scan_ms, search_ms = t.tolist()
     fallback = (kernels.filter_fallback_count(ws, hi - lo, E, nq, K, sharded=staged)
                 if a.method == "bf16" else 0)
+    check = self_check(a, out, q, table, shard, dev, world)
     ms_per_step = dt / a.steps * 1e3
     value = world * B / (dt / a.steps)
 
@@ -305,6 +328,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
+        "self_check": check,
         "dtype": "bf16 filter + f32 exact scores" if a.method == "bf16" else "f32",
         "data": "synthetic (random-normal item embeddings, uniform 20-event histories, event mix 0.75/0.17/0.08)",
         "config": {

@@ -82,15 +82,33 @@ def dot(x: np.ndarray, q: np.ndarray) -> float:
     return float(lib().tto_dot(_fp(x), _fp(q), x.shape[0]))
 
 
-def scan_topk(db: np.ndarray, q: np.ndarray, k: int, row_base: int = 0):
-    """Canonical-f32 exact top-k; bit-exact reference for tt_scan_topk_f32."""
+def scan_topk(db: np.ndarray, q: np.ndarray, k: int, row_base: int = 0, threads: int = 0):
+    """Canonical-f32 exact top-k; bit-exact reference for tt_scan_topk_f32.
+
+    threads > 1 splits the queries over a thread pool (ctypes drops the GIL; queries are
+    independent, so the result does not depend on the split).  0 = min(16, cpu count)."""
     db, q = _c32(db), _c32(q)
     n, d = db.shape
     nq = q.shape[0]
     s = np.empty((nq, k), np.float32)
     i = np.empty((nq, k), np.int64)
-    lib().tto_scan_topk(_fp(db), n, d, d, row_base, _fp(q), nq, d, k, _fp(s),
-                        i.ctypes.data_as(_i64p))
+    L = lib()
+
+    def run(a, b):
+        if b > a:
+            L.tto_scan_topk(_fp(db), n, d, d, row_base, _fp(q[a:b]), b - a, d, k, _fp(s[a:b]),
+                            i[a:b].ctypes.data_as(_i64p))
+
+    t = threads or min(16, os.cpu_count() or 1)
+    if t <= 1 or nq * n < (1 << 22):
+        run(0, nq)
+        return s, i
+    from concurrent.futures import ThreadPoolExecutor
+
+    t = min(t, nq)
+    cuts = [nq * j // t for j in range(t + 1)]
+    with ThreadPoolExecutor(t) as ex:
+        list(ex.map(lambda j: run(cuts[j], cuts[j + 1]), range(t)))
     return s, i
 
 

@@ -113,20 +113,84 @@ static int cmp_pair(const void* pa, const void* pb) {
   return 0;
 }
 
+/* tto_dot for ROWS consecutive rows at once: the same per-row fmaf chain (order unchanged),
+ * ROWS independent chains interleaved so the fma latency is hidden.  Columns >= d read as 0
+ * (the padded tail block takes the branchy path). */
+#define ROWS 8
+static void dot_rows(const float* db, int64_t ld_db, int nr, const float* q, int32_t d,
+                     float* out) {
+  float acc[ROWS] = {0};
+  const int32_t full = d / 16, dp = (d + 15) / 16 * 16;
+  for (int32_t t = 0; t < full; t++)
+    for (int i = 0; i < 4; i++)
+      for (int g = 0; g < 4; g++) {
+        const int32_t e = 16 * t + 4 * g + i;
+        const float qv = q[e];
+        if (nr == ROWS)
+          for (int r = 0; r < ROWS; r++) acc[r] = fmaf(db[r * ld_db + e], qv, acc[r]);
+        else
+          for (int r = 0; r < nr; r++) acc[r] = fmaf(db[r * ld_db + e], qv, acc[r]);
+      }
+  for (int32_t t = full; t < dp / 16; t++)
+    for (int i = 0; i < 4; i++)
+      for (int g = 0; g < 4; g++) {
+        const int32_t e = 16 * t + 4 * g + i;
+        const float qv = e < d ? q[e] : 0.0f;
+        for (int r = 0; r < nr; r++) acc[r] = fmaf(e < d ? db[r * ld_db + e] : 0.0f, qv, acc[r]);
+      }
+  for (int r = 0; r < nr; r++) out[r] = acc[r];
+}
+
+/* bounded heap of the k best pairs; heap[0] = the worst kept (better() is a strict total
+ * order over distinct rows, so the kept set is exactly the sorted prefix of all pairs) */
+static void heap_sift(tto_pair* h, int32_t m, int32_t j) {
+  for (;;) {
+    int32_t c = 2 * j + 1, w = j;
+    if (c < m && better(&h[w], &h[c])) w = c;
+    if (c + 1 < m && better(&h[w], &h[c + 1])) w = c + 1;
+    if (w == j) return;
+    tto_pair t = h[j];
+    h[j] = h[w];
+    h[w] = t;
+    j = w;
+  }
+}
+static void heap_push(tto_pair* h, int32_t* m, int32_t k, tto_pair p) {
+  if (*m < k) {
+    int32_t j = (*m)++;
+    h[j] = p;
+    while (j > 0) { /* sift up: parent must be worse than (better than) child */
+      int32_t par = (j - 1) / 2;
+      if (!better(&h[par], &h[j])) break;
+      tto_pair t = h[par];
+      h[par] = h[j];
+      h[j] = t;
+      j = par;
+    }
+  } else if (better(&p, &h[0])) {
+    h[0] = p;
+    heap_sift(h, *m, 0);
+  }
+}
+
 /* Exact top-k (faiss IndexFlatIP.search semantics, vector_db.py:159-160): scores by
  * tto_dot, sorted descending, ties -> lower row; NaN never returned; tail (-inf, -1). */
 void tto_scan_topk(const float* db, int64_t n, int32_t d, int64_t ld_db, int64_t row_base,
                    const float* q, int32_t nq, int64_t ld_q, int32_t k, float* out_s,
                    int64_t* out_i) {
-  tto_pair* buf = (tto_pair*)malloc(sizeof(tto_pair) * (size_t)(n > 0 ? n : 1));
+  tto_pair* buf = (tto_pair*)malloc(sizeof(tto_pair) * (size_t)(k > 0 ? k : 1));
+  float sc[ROWS];
   for (int32_t qi = 0; qi < nq; qi++) {
-    int64_t m = 0;
-    for (int64_t r = 0; r < n; r++) {
-      float s = tto_dot(db + r * ld_db, q + qi * ld_q, d);
-      if (s != s) continue;
-      buf[m].s = s + 0.0f;
-      buf[m].i = row_base + r;
-      m++;
+    int32_t m = 0;
+    for (int64_t r0 = 0; r0 < n; r0 += ROWS) {
+      const int nr = n - r0 < ROWS ? (int)(n - r0) : ROWS;
+      dot_rows(db + r0 * ld_db, ld_db, nr, q + qi * ld_q, d, sc);
+      for (int r = 0; r < nr; r++) {
+        const float s = sc[r];
+        if (s != s) continue;
+        tto_pair p = {s + 0.0f, row_base + r0 + r};
+        heap_push(buf, &m, k, p);
+      }
     }
     qsort(buf, (size_t)m, sizeof(tto_pair), cmp_pair);
     for (int32_t j = 0; j < k; j++) {

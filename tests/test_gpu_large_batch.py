@@ -1,0 +1,154 @@
+"""Parity of the large-batch bf16 filter path: more than RG_SMALL_NQ = 2048 queries per launch,
+so the full-catalog level is the k_filter_ring<EP, 1> instantiation (tt_filter.hip:1717) that
+bench.py's headline number runs -- the retrieve_batch pattern of configs[2]
+(reference src/inference/vector_db.py:171-209, 10k buyers per batch).
+
+Bar: bit-exact ids and scores.  Oracles: the C restatement (oracle.scan_topk, canonical f32,
+threaded over queries) for every query where that finishes in seconds, and the exact f32
+MFMA scan (tt_scan_topk_f32, itself bit-exact vs the C oracle in test_gpu_parity.py) for
+every query of the full-size case, plus a C-oracle subset there."""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_parity import _sharded_search_emulated, bounds, dev_rows
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def K():
+    from twotower import kernels
+
+    return kernels
+
+
+def _bf16_search(K, xd, n, d, qd, k):
+    x16 = xd.to(torch.bfloat16)
+    ws = torch.empty(K.filter_workspace_bytes(n, d, qd.shape[0], k), dtype=torch.uint8,
+                     device="cuda")
+    s, i = K.scan_topk_bf16(xd, x16, n, d, qd, k, bounds(K, xd, x16, d), workspace=ws)
+    torch.cuda.synchronize()
+    return s, i, K.filter_fallback_count(ws, n, d, qd.shape[0], k)
+
+
+def _iid(oracle_mod, rng, n, nq, d=384):
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
+    q = oracle_mod.l2norm_rows(rng.standard_normal((nq, d)).astype(np.float32), 0)
+    return x, q
+
+
+def test_large_batch_threshold_is_crossed():
+    """The cases below only test the LVL-1 kernel if they exceed its batch threshold."""
+    import re
+    import os
+
+    src = open(os.path.join(os.path.dirname(__file__), "..", "two-tower-model-v2_amd", "csrc",
+                            "tt_filter.hip")).read()
+    assert int(re.search(r"constexpr int RG_SMALL_NQ = (\d+);", src).group(1)) == 2048
+
+
+@pytest.mark.parametrize("nq", [2049, 4096])
+def test_large_batch_iid_bit_exact_vs_oracle(K, oracle_mod, nq):
+    """n = 100k, k = 100: every query bit-exact vs the C oracle (2049 = one query past the
+    threshold, a 1-query ragged last tile; 4096 = 16 full 256-query tiles)."""
+    rng = np.random.default_rng(nq)
+    n, d, k = 100_000, 384, 100
+    x, q = _iid(oracle_mod, rng, n, nq)
+    s, i, fb = _bf16_search(K, dev_rows(x), n, d, dev_rows(q), k)
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    assert np.array_equal(i.cpu().numpy(), ri)
+    assert np.array_equal(s.cpu().numpy(), rs)
+    assert fb == 0  # iid data: the optimistic thresholds hold
+
+
+def test_large_batch_clustered_bit_exact(K, oracle_mod):
+    """Near-duplicate clusters (tiny score gaps, band overflow -> exact fallback for some
+    queries) and queries that sit on a cluster centre, nq = 4096 (ragged n)."""
+    rng = np.random.default_rng(101)
+    n, d, nq, k = 100_003, 384, 4096, 100
+    c = rng.standard_normal((200, d)).astype(np.float32)
+    x = c[rng.integers(0, 200, n)] + 2e-3 * rng.standard_normal((n, d)).astype(np.float32)
+    x = oracle_mod.l2norm_rows(x, 0)
+    q = rng.standard_normal((nq, d)).astype(np.float32)
+    q[::3] = c[rng.integers(0, 200, len(q[::3]))]
+    q = oracle_mod.l2norm_rows(q, 0)
+    s, i, fb = _bf16_search(K, dev_rows(x), n, d, dev_rows(q), k)
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    assert np.array_equal(i.cpu().numpy(), ri)
+    assert np.array_equal(s.cpu().numpy(), rs)
+
+
+def test_large_batch_duplicates_and_special_queries(K, oracle_mod):
+    """Exact duplicate rows (ties on both scores -> lower row first), zero queries (all scores
+    0: rows 0..k-1), a NaN catalog row, nq = 4096."""
+    rng = np.random.default_rng(102)
+    n, d, nq, k = 60_000, 384, 4096, 128
+    base = oracle_mod.l2norm_rows(rng.standard_normal((n // 4, d)).astype(np.float32), 0)
+    x = np.concatenate([base] * 4)
+    x[777] = np.nan
+    q = oracle_mod.l2norm_rows(rng.standard_normal((nq, d)).astype(np.float32), 0)
+    q[::5] = base[rng.integers(0, n // 4, len(q[::5]))]
+    q[17] = 0.0
+    q[4095] = 0.0
+    s, i, fb = _bf16_search(K, dev_rows(x), n, d, dev_rows(q), k)
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    gi = i.cpu().numpy()
+    assert np.array_equal(gi, ri)
+    assert np.array_equal(s.cpu().numpy(), rs)
+    assert np.array_equal(gi[17], np.arange(k)) and not np.isin(777, gi).any()
+
+
+@pytest.mark.parametrize("d,k", [(128, 50), (768, 100)])
+def test_large_batch_other_dims(K, oracle_mod, d, k):
+    """Other padded widths of the same instantiation family (E = 128 32-row tiles, E = 768
+    16-row tiles / one query block per wave)."""
+    rng = np.random.default_rng(d + 7)
+    n, nq = 50_000, 2500
+    x, q = _iid(oracle_mod, rng, n, nq, d)
+    s, i, _ = _bf16_search(K, dev_rows(x), n, d, dev_rows(q), k)
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    assert np.array_equal(i.cpu().numpy(), ri)
+    assert np.array_equal(s.cpu().numpy(), rs)
+
+
+@pytest.mark.slow
+def test_configs2_full_size_bit_exact(K, oracle_mod):
+    """configs[2] exactly as bench.py runs it: 1M x 384 catalog, 10k queries, k = 100.
+    Every query bit-exact vs the exact f32 MFMA scan; 64 queries (spread over all 40 query
+    tiles, incl. the 16-query last tile) bit-exact vs the C oracle; no fallbacks."""
+    n, d, nq, k = 1_000_000, 384, 10_000, 100
+    g = torch.Generator(device="cuda").manual_seed(2)
+    x = torch.randn((n, d), generator=g, device="cuda")
+    K.l2norm_rows(x, d, 0, out=x)
+    q = torch.randn((nq, d), generator=g, device="cuda")
+    K.l2norm_rows(q, d, 0, out=q)
+    s, i, fb = _bf16_search(K, x, n, d, q, k)
+    fs, fi = K.scan_topk(x, n, d, q, k)
+    assert fb == 0
+    assert torch.equal(i, fi), int((i != fi).any(dim=1).sum())
+    assert torch.equal(s, fs)
+    sub = np.unique(np.concatenate([np.linspace(0, nq - 1, 60).astype(int),
+                                    [255, 256, 9983, 9999]]))
+    rs, ri = oracle_mod.scan_topk(x.cpu().numpy(), q[sub].cpu().numpy(), k)
+    assert np.array_equal(i[sub].cpu().numpy(), ri)
+    assert np.array_equal(s[sub].cpu().numpy(), rs)
+
+
+@pytest.mark.slow
+def test_sharded_protocol_large_batch_w8(K, oracle_mod):
+    """The W = 8 staged sharded filter with W.B = 4096 queries per rank launch (> 2048: the
+    per-shard full level is the large-batch instantiation), 1M rows: merged results bit-exact
+    vs the single-catalog f32 scan (all queries) and the C oracle (a subset)."""
+    rng = np.random.default_rng(8)
+    n, nq, k, W = 1_000_000, 4096, 100, 8
+    x, q = _iid(oracle_mod, rng, n, nq)
+    x[n // 2: n // 2 + 50] = x[:50]  # duplicates across shards
+    ms, mi, fb = _sharded_search_emulated(K, x, q, W, k)
+    fs, fi = K.scan_topk(dev_rows(x), n, 384, dev_rows(q), k)
+    assert np.array_equal(mi, fi.cpu().numpy())
+    assert np.array_equal(ms, fs.cpu().numpy())
+    assert max(fb) <= nq // 100, fb
+    sub = np.arange(0, nq, 97)
+    rs, ri = oracle_mod.scan_topk(x, q[sub], k)
+    assert np.array_equal(mi[sub], ri) and np.array_equal(ms[sub], rs)

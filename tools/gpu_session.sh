@@ -18,7 +18,7 @@ run() {  # name timeout cmd...
 }
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider ${PYTEST_ARGS:-} ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     bench_f32) run bench_f32 600 python bench.py --method f32 --no-cpu-baseline ${BENCH_ARGS:-} ;;
