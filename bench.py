@@ -54,12 +54,16 @@ def parse():
                    help="bf16: bf16 MFMA filter + exact f32 re-rank; f32: exact f32 MFMA scan "
                         "(identical results)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-single", type=int, default=128)
-    p.add_argument("--cpu-batch", type=int, default=2048)
+    p.add_argument("--cpu-single", type=int, default=32, help="per repetition (median of 5)")
+    p.add_argument("--cpu-batch", type=int, default=512, help="per repetition (median of 5)")
     p.add_argument("--mode-a-buyers", type=int, default=256,
                    help="Mode A sample per rank (history texts re-encoded); 0 disables")
     p.add_argument("--mode-a-prec", choices=["bf16", "f32"], default="bf16")
     p.add_argument("--mode-a-steps", type=int, default=3)
+    p.add_argument("--no-extra", action="store_true",
+                   help="skip the configs[1] leg, the batch sweep and the f32 Mode A leg")
+    p.add_argument("--configs1-texts", type=int, default=100_000)
+    p.add_argument("--sweep", default="1,8,16,32,256")
     return p.parse_args()
 
 
@@ -79,6 +83,168 @@ def synth_text_ids(rng, n, vocab, lo=16, hi=128):
         L = int(rng.integers(lo, hi + 1))
         out.append([0] + (3 + (rng.zipf(1.1, size=L - 2) % 30000) % (vocab - 3)).tolist() + [2])
     return out
+
+
+def synth_text_ids_fast(rng, n, vocab, lo=16, hi=128):
+    """synth_text_ids in one vectorised draw (same distribution; for the 100k-text leg)."""
+    lens = rng.integers(lo, hi + 1, n)
+    body = 3 + (rng.zipf(1.1, size=int((lens - 2).sum())) % 30000) % (vocab - 3)
+    cu = np.concatenate([[0], np.cumsum(lens - 2)])
+    return [[0] + body[cu[i]:cu[i + 1]].tolist() + [2] for i in range(n)]
+
+
+def encoder_flops(lens, E_out=384):
+    """SURVEY.md 8(d) per text: L (42.47e6 + 18432 L) (12-layer MiniLM encoder, L tokens)
+    + 0.46e6 (projection head)."""
+    L = np.asarray(lens, np.float64)
+    return float((L * (42.47e6 + 18432.0 * L)).sum() + 0.46e6 * len(L))
+
+
+def configs1(a, dev, rank):
+    """BASELINE.json configs[1]: 100k products x 384-d, item-tower encode at batch 256 +
+    brute-force top-100 (scripts/generate_embeddings.py:52 -> ItemTower.encode_batch,
+    item_tower.py:213-243; then VectorDatabase.retrieve_batch, vector_db.py:171-209).
+    One step = one batch of 256 product texts: MiniLM-L12 encode (HIP, packed varlen) +
+    projection head + F.normalize -> q/(||q||+1e-8) -> exact top-100 of the 256 new item
+    embeddings over the 100k x 384 catalog.  bf16 encoder over all 100k texts (the whole
+    generate_embeddings pass); the f32 (parity) encoder on a 16-batch sample."""
+    from twotower.item_tower import MINILM_L12, BertEncoder, ItemTower, pack_sequences, \
+        random_bert_state_dict
+
+    cfg, E, K, BS = MINILM_L12, 384, 100, 256
+    n_txt = a.configs1_texts
+    rng = np.random.default_rng(200 + rank)
+    seqs = synth_text_ids_fast(rng, n_txt, cfg["vocab"])
+    bid = rng.integers(0, 51, n_txt).tolist()
+    cid = rng.integers(0, 21, n_txt).tolist()
+
+    class _Dim:
+        def get_sentence_embedding_dimension(self):
+            return cfg["hidden"]
+
+    torch.manual_seed(0)
+    it = ItemTower(text_encoder=_Dim())
+    it.initialize_categorical_embeddings([f"brand{i}" for i in range(50)],
+                                         [f"cat{i}" for i in range(20)])
+    it.to(dev).eval()
+    sd = random_bert_state_dict(cfg, 0)
+    ep = _lib.padded_dim(E)
+    g = torch.Generator(device=dev).manual_seed(2)
+    cat = torch.zeros((100_000, ep), device=dev)
+    cat[:, :E] = torch.randn((100_000, E), generator=g, device=dev)
+    cat16 = torch.empty_like(cat, dtype=torch.bfloat16)
+    kernels.l2norm_rows(cat, E, _lib.TT_NORM_ADD_EPS, out=cat, out_bf16=cat16)
+    bnd = kernels.bf16_image_bounds(cat, cat16, E).tolist()
+    ws = torch.empty(kernels.filter_workspace_bytes(100_000, E, BS, K), dtype=torch.uint8,
+                     device=dev)
+    qn = torch.zeros((BS, ep), device=dev)
+    batches = [pack_sequences(seqs[i:i + BS], dev) for i in range(0, n_txt, BS)]
+    out = {"workload": "configs[1]: 100k products x 384-d, batch 256 item-tower encode "
+                       "(MiniLM-L12 arch, seeded random weights, synthetic Zipf token ids, "
+                       "L ~ U[16,128]) + exact top-100 over a 100k x 384 catalog",
+           "texts": n_txt, "batch": BS}
+    res = {}
+    for prec, nb in (("bf16", len(batches)), ("f32", min(16, len(batches)))):
+        enc = BertEncoder(sd, cfg, device=dev, prec=prec)
+        pooled = torch.empty((BS, cfg["hidden"]), device=dev)
+        e_enc = [torch.cuda.Event(enable_timing=True) for _ in range(2 * nb)]
+        e_srch = [torch.cuda.Event(enable_timing=True) for _ in range(nb)]
+
+        def step(j, timed):
+            ids, cu, mx = batches[j]
+            nt = cu.numel() - 1
+            if timed:
+                e_enc[2 * j].record()
+            enc.encode_packed(ids, cu, mx, out=pooled[:nt])
+            y = it.head(pooled[:nt], bid[j * BS:j * BS + nt], cid[j * BS:j * BS + nt],
+                        use_cat=True)
+            if timed:
+                e_enc[2 * j + 1].record()
+            kernels.l2norm_rows(y, E, _lib.TT_NORM_ADD_EPS, out=qn[:nt])
+            r = kernels.scan_topk_bf16(cat, cat16, 100_000, E, qn[:nt], K, bnd, workspace=ws)
+            if timed:
+                e_srch[j].record()
+            return y, r
+
+        step(0, False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for j in range(nb):
+            step(j, True)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        enc_ms = sum(e_enc[2 * j].elapsed_time(e_enc[2 * j + 1]) for j in range(nb))
+        srch_ms = sum(e_enc[2 * j + 1].elapsed_time(e_srch[j]) for j in range(nb))
+        lens = [len(x) for x in seqs[:nb * BS]]
+        fl = encoder_flops(lens)
+        peak = BF16_MFMA_PEAK_TFLOPS if prec == "bf16" else F32_MFMA_PEAK_TFLOPS
+        res[prec] = {"texts_timed": min(n_txt, nb * BS), "texts_per_s": min(n_txt, nb * BS) / dt,
+                     "ms_per_batch": dt / nb * 1e3, "encode_ms_per_batch": enc_ms / nb,
+                     "search_ms_per_batch": srch_ms / nb,
+                     "encode_tflops": fl / (enc_ms * 1e-3) / 1e12,
+                     "encode_mfma_frac": fl / (enc_ms * 1e-3) / 1e12 / peak,
+                     "mfma_peak_tflops": peak,
+                     "tokens_timed": int(sum(lens))}
+        if prec == "bf16":
+            y16 = step(0, False)[0].clone()
+        else:
+            y32 = step(0, False)[0]
+        del enc
+        torch.cuda.empty_cache()
+    # bf16 encoder vs the f32 (parity) encoder on the L2-normalised item embeddings
+    # (item_tower.py:209): worst cosine distance over the first batch
+    cos = (y16 * y32).sum(dim=1)
+    res["bf16_vs_f32_item_cosine"] = {"min_cos": float(cos.min()),
+                                      "max_1_minus_cos": float((1 - cos).max()),
+                                      "max_abs_diff": float((y16 - y32).abs().max())}
+    out.update(res)
+    out["value"] = res["bf16"]["texts_per_s"]
+    out["unit"] = "texts/s (encode + top-100 per batch of 256)"
+    return out
+
+
+def batch_sweep(a, shard, shard16, n, E, K, bounds, dev):
+    """SURVEY.md 8(d) query-batch sweep over the 1M x 384 catalog (vector_db.py:160,197):
+    end-to-end search time per call (every launch of tt_scan_topk_bf16f32, queries resident),
+    fraction of the HBM peak for the algorithmic bytes 4NE + 4BE + 12Bk (the f32 catalog read
+    once) and for the bytes the bf16 filter's full level actually streams (2NE)."""
+    ep = _lib.padded_dim(E)
+    g = torch.Generator(device=dev).manual_seed(9)
+    res = {}
+    stream = torch.cuda.current_stream()
+    for B in (int(v) for v in a.sweep.split(",") if v):
+        q = torch.zeros((B, ep), device=dev)
+        q[:, :E] = torch.randn((B, E), generator=g, device=dev)
+        kernels.l2norm_rows(q, E, _lib.TT_NORM_ADD_EPS, out=q)
+        ws = torch.empty(kernels.filter_workspace_bytes(n, E, B, K), dtype=torch.uint8,
+                         device=dev)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        for e in ev:
+            e.record(stream)
+        for _ in range(3):
+            kernels.scan_topk_bf16(shard, shard16, n, E, q, K, bounds, workspace=ws)
+        tot, lvl = [], []
+        for _ in range(21):
+            torch.cuda.synchronize()
+            ev[2].record(stream)
+            kernels.scan_topk_bf16(shard, shard16, n, E, q, K, bounds, workspace=ws,
+                                   events=(ev[0], ev[1]))
+            ev[3].record(stream)
+            torch.cuda.synchronize()
+            tot.append(ev[2].elapsed_time(ev[3]))
+            lvl.append(ev[0].elapsed_time(ev[1]))
+        t, l_ = float(np.median(tot)), float(np.median(lvl))
+        alg = 4.0 * n * E + 4.0 * B * E + 12.0 * B * K
+        res[str(B)] = {"ms_per_search": t, "queries_per_s": B / (t * 1e-3),
+                       "full_level_ms": l_,
+                       "alg_bytes": alg, "alg_hbm_gbps": alg / (t * 1e-3) / 1e9,
+                       "alg_frac": alg / (t * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                       "bf16_pass_gbps_end_to_end": 2.0 * n * ep / (t * 1e-3) / 1e9,
+                       "bf16_pass_frac_end_to_end": 2.0 * n * ep / (t * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                       "full_level_frac": 2.0 * n * ep / (l_ * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+        del ws
+    return {"catalog": f"{n} x {E}", "k": K, "timing": "median of 21 synchronised calls",
+            "by_batch": res}
 
 
 def mode_a(a, dev, world, rank, search_local, k, E):
@@ -142,9 +308,9 @@ def mode_a(a, dev, world, rank, search_local, k, E):
            "model": "MiniLM-L12 architecture (12L/384h/12 heads/FFN 1536, vocab 250037), "
                     "seeded random weights; synthetic token ids, L ~ U[16,128]"}
     cpu_inputs = (sd, cfg, {k2: v.detach().cpu() for k2, v in it.state_dict().items()},
-                  [seqs[b * S:(b + 1) * S] for b in range(4)],
-                  [bid[b * S:(b + 1) * S] for b in range(4)],
-                  [cid[b * S:(b + 1) * S] for b in range(4)], w[:4].cpu().numpy())
+                  [seqs[b * S:(b + 1) * S] for b in range(8)],
+                  [bid[b * S:(b + 1) * S] for b in range(8)],
+                  [cid[b * S:(b + 1) * S] for b in range(8)], w[:8].cpu().numpy())
     return res, cpu_inputs
 
 
@@ -398,6 +564,14 @@ def main():
     if a.mode_a_buyers > 0:
         result["mode_a"], cpu_a = mode_a(a, dev, world, rank, lambda qall: local_search_k(qall),
                                          K, E)
+    if world == 1 and not a.no_extra:
+        result["batch_sweep"] = batch_sweep(a, shard, shard16, hi - lo, E, K, bounds, dev)
+        if a.mode_a_buyers > 0 and a.mode_a_prec == "bf16":
+            a32 = argparse.Namespace(**vars(a))
+            a32.mode_a_prec, a32.mode_a_steps = "f32", 1
+            m32, _ = mode_a(a32, dev, world, rank, lambda qall: local_search_k(qall), K, E)
+            result["mode_a_f32"] = m32
+        result["configs1"] = configs1(a, dev, rank)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         sys.path.insert(0, ROOT)
         from oracle import cpu_baseline
@@ -415,7 +589,7 @@ def main():
         if cpu_a is not None:
             sd_, cfg_, head_, seqs_, bid_, cid_, w_ = cpu_a
             result["mode_a"]["cpu_baseline"] = cpu_baseline.run_mode_a(
-                sd_, cfg_, head_, seqs_, bid_, cid_, w_, cat_np, K, n_buyers=3)
+                sd_, cfg_, head_, seqs_, bid_, cid_, w_, cat_np, K, n_buyers=8)
             result["mode_a"]["gpu_over_cpu_single"] = (
                 result["mode_a"]["value"] / result["mode_a"]["cpu_baseline"]["value"])
     if rank == 0:

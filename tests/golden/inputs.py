@@ -185,3 +185,80 @@ def eval_cases(seed: int = 21, n_products: int = 60, n_buyers: int = 40):
         ret = [pids[j] for j in rng.permutation(n_products)[:20]]
         cases.append((f"u{b}", hist, rel, ret))
     return pids, meta, cases
+
+
+# ------------------------------------------------ VectorDatabase / server fixtures (a10-a12, f1, f2)
+# Generated by tests/golden/make_retrieval_golden.py through the reference's own VectorDatabase
+# and FastAPI /retrieve handler.
+VDB_CASES = dict(
+    {name: dict(spec) for name, spec in FLATIP_CASES.items()},
+    short_ids=dict(N=50, Q=6, k=45, seed=61, n_ids=40),       # idx < len(product_ids) filter
+    f64_input=dict(N=300, Q=6, k=20, seed=62, dtype="f64"),   # normalised in f64, then cast
+    unicode_ids=dict(N=30, Q=4, k=10, seed=63, unicode=True),
+    scaled_zero_row=dict(N=500, Q=6, k=50, seed=64, scale=1e3, zero_row=7),
+    server=dict(N=200, Q=1, k=10, seed=65, prefix="SKU-"),
+)
+
+
+def vdb_inputs(spec):
+    """(embeddings, queries, product_ids) of one VectorDatabase case."""
+    x, q = flatip_inputs(spec)
+    if "scale" in spec:
+        x = x * np.float32(spec["scale"])
+    if "zero_row" in spec:
+        x[spec["zero_row"]] = 0.0
+    if spec.get("dtype") == "f64":
+        rng = np.random.default_rng(spec["seed"] + 1000)
+        x = x.astype(np.float64) + rng.standard_normal(x.shape) * 1e-9
+        q = q.astype(np.float64)
+    n_ids = spec.get("n_ids", x.shape[0])
+    if spec.get("unicode"):
+        ids = [f"منتج-{j}" for j in range(n_ids)]
+    else:
+        ids = [f"{spec.get('prefix', 'p')}{j}" for j in range(n_ids)]
+    return x, q, ids
+
+
+def stub_buyer_embedding(interactions, E):
+    """Deterministic stand-in for EmbeddingEncoder.encode_buyer in the /retrieve fixtures:
+    a seeded vector keyed by the interaction list."""
+    import zlib
+
+    key = "|".join(f"{i['product_id']}:{i['event_type']}" for i in interactions)
+    rng = np.random.default_rng(zlib.crc32(key.encode("utf-8")))
+    return rng.standard_normal(E).astype(np.float32)
+
+
+def server_products():
+    """products_df columns (reference schema): duplicates (first row wins), NaN / None
+    cells, Arabic text; SKU-3, SKU-11 and SKU-150..199 are absent (-> 'N/A' records)."""
+    rng = np.random.default_rng(66)
+    ids = [f"SKU-{j}" for j in range(150) if j not in (3, 11)] + ["SKU-5", "SKU-8"]
+    brands = ["Damas", "Lazurde", None, float("nan"), "Acme"]
+    cats = ["خواتم", "rings", float("nan"), None, "oil"]
+    return {
+        "product_id": ids,
+        "title": [f"خاتم ذهب {j}" if j % 3 else (float("nan") if j % 2 else f"title {j}")
+                  for j in range(len(ids))],
+        "description": [f"desc {j}" if j % 5 else "" for j in range(len(ids))],
+        "brand": [brands[int(rng.integers(0, len(brands)))] for _ in ids],
+        "category": [cats[int(rng.integers(0, len(cats)))] for _ in ids],
+    }
+
+
+def server_photos():
+    return {f"SKU-{j}": f"https://img.example/{j}.jpg" for j in range(0, 200, 4)}
+
+
+def server_requests():
+    rng = np.random.default_rng(67)
+    events = ["view", "add_to_cart", "purchase", "AddToCart", "buy", "wishlist"]
+    reqs = []
+    for b, k in enumerate([10, 1, 5, 50, 200, 250, 1000]):
+        n = int(rng.integers(1, 8))
+        inter = [{"product_id": f"SKU-{int(rng.integers(0, 200))}",
+                  "event_type": events[int(rng.integers(0, len(events)))],
+                  "timestamp": None if b % 2 else f"2024-01-0{1 + j}T10:00:00"}
+                 for j in range(n)]
+        reqs.append({"buyer_id": f"buyer-{b}", "recent_interactions": inter, "k": k})
+    return reqs

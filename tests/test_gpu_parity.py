@@ -242,7 +242,7 @@ def test_scan_row_base_and_merge_equal_single_shard(K, oracle_mod):
 
 
 @pytest.mark.parametrize("case", list(gi.FLATIP_CASES))
-def test_vector_db_matches_reference_fixture(golden, oracle_mod, case):
+def test_vector_db_matches_f64_flatip_restatement(golden, oracle_mod, case):
     """Full reference API path: build_index -> retrieve_batch / retrieve vs the f64
     restatement of faiss IndexFlatIP over the reference's numpy-normalised catalog."""
     from twotower import VectorDatabase

@@ -71,3 +71,23 @@ def test_retrieve_products_flow():
                              [{"product_id": "a", "event_type": "view"}], k=2)
     assert body["buyer_id"] == "u1" and [p["product_id"] for p in body["products"]] == ["b", "a"]
     assert body["products"][1]["title"] == "خاتم ذهب"
+
+
+def test_catalog_matches_reference_server_fixture(golden):
+    """Responses of the reference FastAPI /retrieve handler itself (server.py:212-286, run
+    through fastapi.testclient by tests/golden/make_retrieval_golden.py): assembling the
+    reference's own retrieved (id, score) lists gives the same records, field for field."""
+    import json
+
+    import inputs as gi
+    from twotower.serving import ProductCatalog
+
+    cases = json.load(open(os.path.join(ROOT, "tests", "golden", "server.json"),
+                           encoding="utf-8"))
+    cat = ProductCatalog(pd.DataFrame(gi.server_products()), gi.server_photos())
+    assert len(cases) == len(gi.server_requests())
+    for c in cases:
+        assert c["status"] == 200
+        ref = c["response"]["products"]
+        got = cat.assemble([(p["product_id"], p["score"]) for p in ref])
+        assert got == ref
