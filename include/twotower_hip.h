@@ -325,6 +325,10 @@ int tt_col_sum_f32(const float* x, int64_t ldx, int64_t rows, int32_t cols, floa
                    int32_t accumulate, void* stream);
 /* dh[i] = 0 where h[i] <= 0 (ReLU backward, in place). */
 int tt_relu_backward_f32(float* dh, const float* h, int64_t n, void* stream);
+/* nn.Dropout(p) of the item projection (item_tower.py:61; active in train mode,
+ * trainer.py:167) with a caller-drawn keep mask: x[i] = keep[i] ? x[i]*scale : 0 in place,
+ * scale = 1/(1-p).  Applied to the incoming gradient it is the backward. */
+int tt_dropout_apply_f32(float* x, const uint8_t* keep, float scale, int64_t n, void* stream);
 /* BuyerTower.attention_aggregation after H = relu(x W1^T + b1) (buyer_tower.py:85-99):
  * a = H.W2 + b2, c = a*w, alpha = softmax_S(c), o = sum alpha x, z = F.normalize(o).
  * H [B*S, Hd], x [B, S, E], w [B, S]; saves alpha [B, S], onorm [B]. S <= 128, E <= 1024. */

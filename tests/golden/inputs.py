@@ -262,3 +262,32 @@ def server_requests():
                  for j in range(n)]
         reqs.append({"buyer_id": f"buyer-{b}", "recent_interactions": inter, "k": k})
     return reqs
+
+
+# ------------------------------------------------ Trainer._encode_buyer_sequences_batched (f3)
+def trainer_texts():
+    return [f"نص المنتج {j}" for j in range(40)] + ["positive fallback A", "positive fallback B"]
+
+
+def trainer_batch():
+    """(product_metadata, buyer_sequences, positive_texts) in the collate_fn format: tuples of
+    (pid, weight) / (pid, weight, timestamp), malformed entries, unknown ids, an empty and an
+    all-unknown history (-> positive-text fallback), a 130-item history (-> last 100)."""
+    rng = np.random.default_rng(71)
+    texts = trainer_texts()
+    meta = {f"p{j}": {"text": texts[j], "brand": None, "category": None} for j in range(40)}
+    seqs = []
+    for b in range(5):
+        seq = []
+        for _ in range(int(rng.integers(1, 25))):
+            pid = f"p{int(rng.integers(0, 45))}"  # p40..p44: not in the metadata
+            w = float(rng.choice([1.0, 5.0, 10.0]))
+            seq.append((pid, w, "2024-01-01") if rng.random() < 0.5 else (pid, w))
+        if b == 2:
+            seq.append(("p1",))  # malformed: skipped
+        seqs.append(seq)
+    seqs.append([])                                     # empty -> fallback
+    seqs.append([("p41", 5.0), ("p44", 1.0)])           # all unknown -> fallback
+    seqs.append([(f"p{j % 40}", float(1 + j % 3)) for j in range(130)])  # truncation
+    pos = [texts[j] for j in range(5)] + [texts[40], texts[41], texts[7]]
+    return meta, seqs, pos

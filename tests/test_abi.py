@@ -83,3 +83,14 @@ def test_product_path_has_no_cpu_fallback():
     bt = BuyerTower(384, "weighted_avg")
     with pytest.raises(HipUnavailable):
         bt(torch.ones(1, 3, 384), torch.ones(1, 3))
+
+
+def test_shipped_library_reads_no_ab_switches():
+    """The A/B kernel switches are read from the environment only in timing builds
+    (-DTT_TIMING_BUILD): the shipped library always runs the path the GPU suite tests."""
+    from twotower import _lib
+
+    raw = open(_lib.LIB_PATH, "rb").read()
+    for name in (b"TT_GEMM_LN", b"TT_ATTN_FAST", b"TT_GEMM_WIDE", b"TT_GEMM_BIG",
+                 b"TT_SELECT_REG", b"TT_FILTER_TMAX_FIRST"):
+        assert name not in raw, name

@@ -214,3 +214,25 @@ def test_batched_evaluator_equals_reference_per_buyer_loop(tmp_path):
         ref.setdefault("mrr", []).append(E.compute_mrr(ret, rel))
     for key, vals in ref.items():
         assert got[f"{key}_mean"] == float(np.mean(vals)), key
+
+
+@pytest.mark.parametrize("aggregation", ["weighted_avg", "attention"])
+def test_mode_b_unknown_ids_match_encode_buyer(tmp_path, aggregation):
+    """History ids missing from the resident table (and from the metadata) are encoded as
+    encode_buyer encodes them (metadata {} -> text ' ', encoder.py:280-292): Mode B equals
+    the per-buyer reference path instead of raising KeyError."""
+    from twotower.encoder import EmbeddingEncoder
+
+    path, *_ = _checkpoint(tmp_path, aggregation)
+    enc = EmbeddingEncoder(str(path), config_path=None)
+    meta = _metadata()
+    enc.set_product_metadata(meta)
+    pids = list(meta)[:20]  # p20..p29 known to the metadata but not in the table
+    enc.set_item_embeddings(pids, enc.encode_items(pids))
+    hists = [[{"product_id": "p3", "event_type": "view"},
+              {"product_id": "p25", "event_type": "purchase"},
+              {"product_id": "not-a-product", "event_type": "add_to_cart"}],
+             [{"product_id": "p1", "event_type": "view"}],
+             [{"product_id": "ghost", "event_type": "view"}]]
+    single = np.stack([enc.encode_buyer(h) for h in hists])
+    np.testing.assert_allclose(enc.encode_buyers(hists, mode="B"), single, rtol=0, atol=1e-6)

@@ -229,6 +229,7 @@ def test_item_head_vs_reference_fixture(golden, use_cat):
         for k, v in gi.item_head_weights(use_cat).items():
             dict(it.named_parameters())[k].copy_(torch.from_numpy(v))
     texts, brands, cats = gi.item_batch()
+    it.eval()  # as the fixture was made (the projection's Dropout is active in train mode)
     y = it(texts, brands if use_cat else None, cats if use_cat else None)
     assert y.is_cuda
     tag = "cat" if use_cat else "nocat"
@@ -262,6 +263,7 @@ def test_item_tower_end_to_end_vs_oracle():
     it = ItemTower(use_categorical_features=True, encoder_state_dict=sd, encoder_cfg=cfg,
                    prec="f32")
     it.initialize_categorical_embeddings(gi.BRANDS, gi.CATEGORIES)
+    it.eval()
     texts = ["خاتم ذهب عيار 21", "", "necklace gold 18k Damas", "   ", "زيت محرك 5W-30"]
     brands = ["Damas", None, "Acme", "Unknown", "Lazurde"]
     cats = ["rings", "necklaces", None, "bracelets", "engine-oil"]

@@ -152,3 +152,45 @@ def test_sharded_protocol_large_batch_w8(K, oracle_mod):
     sub = np.arange(0, nq, 97)
     rs, ri = oracle_mod.scan_topk(x, q[sub], k)
     assert np.array_equal(mi[sub], ri) and np.array_equal(ms[sub], rs)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("nq", [1, 4096])
+def test_10m_rows_single_gpu_bit_exact(K, oracle_mod, nq):
+    """configs[3]'s whole 10M x 384 catalog resident on ONE MI355X (15.4 GB f32 + 7.7 GB bf16
+    image): the bf16 filter path bit-exact vs the f32 scan for every query, and vs the C
+    oracle for a 16-query subset."""
+    n, d, k = 10_000_000, 384, 100
+    g = torch.Generator(device="cuda").manual_seed(10)
+    x = torch.randn((n, d), generator=g, device="cuda")
+    K.l2norm_rows(x, d, 0, out=x)
+    q = torch.randn((nq, d), generator=g, device="cuda")
+    K.l2norm_rows(q, d, 0, out=q)
+    s, i, fb = _bf16_search(K, x, n, d, q, k)
+    fs, fi = K.scan_topk(x, n, d, q, k)
+    assert fb == 0
+    assert torch.equal(i, fi) and torch.equal(s, fs)
+    sub = np.unique(np.linspace(0, nq - 1, 16).astype(int))
+    rs, ri = oracle_mod.scan_topk(x.cpu().numpy(), q[sub].cpu().numpy(), k)
+    assert np.array_equal(i[sub].cpu().numpy(), ri)
+    assert np.array_equal(s[sub].cpu().numpy(), rs)
+
+
+@pytest.mark.slow
+def test_sharded_protocol_10m_w8(K, oracle_mod):
+    """configs[3] layout emulated on one GPU: 10M rows in 8 row shards (1.25M each), the
+    staged protocol for W.B = 2048 queries, merged == the single-catalog f32 scan."""
+    n, nq, k, W = 10_000_000, 2048, 100, 8
+    g = torch.Generator(device="cuda").manual_seed(11)
+    xd = torch.randn((n, 384), generator=g, device="cuda")
+    K.l2norm_rows(xd, 384, 0, out=xd)
+    qd = torch.randn((nq, 384), generator=g, device="cuda")
+    K.l2norm_rows(qd, 384, 0, out=qd)
+    x, q = xd.cpu().numpy(), qd.cpu().numpy()
+    fs, fi = K.scan_topk(xd, n, 384, qd, k)
+    del xd
+    torch.cuda.empty_cache()
+    ms, mi, fb = _sharded_search_emulated(K, x, q, W, k)
+    assert np.array_equal(mi, fi.cpu().numpy())
+    assert np.array_equal(ms, fs.cpu().numpy())
+    assert max(fb) <= nq // 100, fb

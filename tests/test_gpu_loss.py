@@ -84,7 +84,7 @@ def test_two_tower_forward_simplified_and_loss():
     it = ItemTower(text_encoder=Stub())
     it.initialize_categorical_embeddings(gi.BRANDS, gi.CATEGORIES)
     bt = BuyerTower(384, "attention")
-    m = TwoTowerModel(it, bt)
+    m = TwoTowerModel(it, bt).eval()
     B, N, S = 3, 4, 5
     rng = np.random.default_rng(4)
     items = torch.from_numpy(rng.standard_normal((B, S, 384)).astype(np.float32))

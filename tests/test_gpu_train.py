@@ -32,21 +32,27 @@ def _setup(E=384, use_cat=True, seed=0):
     return it, bt
 
 
-def _reference_step(it, bt, items, w, pos, neg, pb, pc, nb, nc, tau, lr):
+def _reference_step(it, bt, items, w, pos, neg, pb, pc, nb, nc, tau, lr, keep=None):
+    """keep (None: eval mode, dropout off): the [B + B*N, hidden] keep mask of the
+    projection's nn.Dropout(0.1) in train mode, rows = positives then negatives."""
     from oracle import losses_ref
 
     it, bt = copy.deepcopy(it).cpu(), copy.deepcopy(bt).cpu()
     B, N = neg.shape[:2]
 
-    def head(text, bid, cid):
+    def head(text, bid, cid, kp):
         x = text
         if it.use_categorical_features:
             x = torch.cat([text, it.brand_embedding(bid.long()), it.category_embedding(cid.long())], 1)
-        return F.normalize(it.projection(x), p=2, dim=1)
+        if kp is None:
+            return F.normalize(it.projection(x), p=2, dim=1)
+        h = torch.relu(it.projection[0](x)) * kp.float() / (1.0 - it.projection[2].p)
+        return F.normalize(it.projection[3](h), p=2, dim=1)
 
-    it.eval()  # dropout off (the HIP step has no dropout either)
-    p = head(pos, pb, pc)
-    n = head(neg.reshape(B * N, -1), nb.reshape(-1), nc.reshape(-1)).view(B, N, -1)
+    it.eval()
+    p = head(pos, pb, pc, keep[:B] if keep is not None else None)
+    n = head(neg.reshape(B * N, -1), nb.reshape(-1), nc.reshape(-1),
+             keep[B:] if keep is not None else None).view(B, N, -1)
     a = bt.attention(items).squeeze(-1) * w
     zb = F.normalize((torch.softmax(a, 1).unsqueeze(-1) * items).sum(1), p=2, dim=1)
     loss = losses_ref.infonce(zb, p, n, tau)
@@ -90,6 +96,7 @@ def test_train_step_matches_torch_autograd_and_adam(E, use_cat):
     nc = torch.from_numpy(rng.integers(0, 5, (B, N)).astype(np.int32))
     ref_loss, ref_g, ref_after = _reference_step(it, bt, items, w, pos, neg, pb, pc, nb, nc, tau, lr)
 
+    it.eval()  # dropout off here; train mode: test_train_step_dropout_fixed_mask
     step = TwoTowerTrainStep(it, bt, temperature=tau, lr=lr, prec="f32")
     cu = lambda t: t.cuda()  # noqa: E731
     loss, g = step.forward_backward(cu(items), cu(w), cu(pos), cu(neg), cu(pb), cu(pc), cu(nb),
@@ -118,6 +125,91 @@ def test_train_step_matches_torch_autograd_and_adam(E, use_cat):
     for k, ref in ref_after.items():
         diff = (names[k].detach().cpu() - ref).abs()
         assert (diff > 1e-6).float().mean().item() < 1e-3, k
+
+
+def test_train_step_dropout_fixed_mask():
+    """Train mode (the reference Trainer calls model.train(), trainer.py:167): the
+    projection's nn.Dropout(0.1) (item_tower.py:61) is applied with the step's keep mask and
+    scaled 1/(1-p), in the forward and the backward -- checked with a fixed mask against
+    torch autograd applying the same mask."""
+    from twotower.train import TwoTowerTrainStep
+
+    B, N, S, E, tau, lr = 8, 4, 5, 384, 0.07, 1e-3
+    it, bt = _setup(E, True, seed=4)
+    it.train()
+    rng = np.random.default_rng(44)
+    items = torch.from_numpy(rng.standard_normal((B, S, E)).astype(np.float32))
+    w = torch.from_numpy(rng.integers(1, 11, (B, S)).astype(np.float32))
+    pos = torch.from_numpy(rng.standard_normal((B, 384)).astype(np.float32) * 0.3)
+    neg = torch.from_numpy(rng.standard_normal((B, N, 384)).astype(np.float32) * 0.3)
+    z = lambda *sh: torch.zeros(sh, dtype=torch.int32)  # noqa: E731
+    keep = torch.from_numpy((rng.random((B + B * N, 256)) >= 0.1).astype(np.uint8))
+    ref_loss, ref_g, _ = _reference_step(it, bt, items, w, pos, neg, z(B), z(B), z(B, N),
+                                         z(B, N), tau, lr, keep=keep)
+    step = TwoTowerTrainStep(it, bt, temperature=tau, lr=lr, prec="f32")
+    seen = []
+
+    def fixed(shape, p, dev):
+        assert tuple(shape) == tuple(keep.shape) and p == 0.1
+        seen.append(1)
+        return keep.to(dev)
+
+    step.keep_fn = fixed
+    cu = lambda t: t.cuda()  # noqa: E731
+    loss, g = step.forward_backward(cu(items), cu(w), cu(pos), cu(neg), cu(z(B)), cu(z(B)),
+                                    cu(z(B, N)), cu(z(B, N)))
+    assert seen == [1]
+    assert abs(loss.item() - ref_loss) < 1e-5 * max(1, abs(ref_loss))
+    for k, v in ref_g.items():
+        got = g[k].detach().cpu().reshape(v.shape)
+        scale = v.abs().max().item() + 1e-12
+        assert (got - v).abs().max().item() <= 1e-4 * scale + 1e-6, k
+    # eval mode: no mask is drawn
+    it.eval()
+    step.forward_backward(cu(items), cu(w), cu(pos), cu(neg))
+    assert seen == [1]
+
+
+def test_item_head_autograd_dropout_train_mode():
+    """ItemTower.head under autograd in train mode: the HIP ItemHeadFn with the keep mask the
+    module drew == torch applying that mask; eval mode is deterministic (no dropout)."""
+    import twotower.train as T
+
+    it, _ = _setup(384, True, seed=6)
+    it.cuda().train()
+    rng = np.random.default_rng(7)
+    text = torch.from_numpy(rng.standard_normal((10, 384)).astype(np.float32)).cuda()
+    text.requires_grad_(True)
+    masks = []
+    orig = T.dropout_keep
+
+    def rec(shape, p, dev):
+        m = orig(shape, p, dev)
+        masks.append(m)
+        return m
+
+    T.dropout_keep = rec
+    try:
+        y = it.head(text, [1] * 10, [2] * 10, use_cat=True)
+    finally:
+        T.dropout_keep = orig
+    assert len(masks) == 1 and masks[0].shape == (10, 256)
+    y.square().sum().backward()
+    ref_it = copy.deepcopy(it).cpu()
+    tx = text.detach().cpu().requires_grad_(True)
+    x = torch.cat([tx, ref_it.brand_embedding(torch.ones(10, dtype=torch.long)),
+                   ref_it.category_embedding(torch.full((10,), 2, dtype=torch.long))], 1)
+    h = torch.relu(ref_it.projection[0](x)) * masks[0].cpu().float() / 0.9
+    ry = F.normalize(ref_it.projection[3](h), p=2, dim=1)
+    ry.square().sum().backward()
+    torch.testing.assert_close(y.detach().cpu(), ry.detach(), rtol=0, atol=2e-6)
+    torch.testing.assert_close(text.grad.cpu(), tx.grad, rtol=0, atol=1e-5)
+    g0, r0 = it.projection[0].weight.grad.cpu(), ref_it.projection[0].weight.grad
+    assert (g0 - r0).abs().max().item() <= 1e-4 * r0.abs().max().item() + 1e-6
+    it.eval()
+    with torch.no_grad():
+        a, b = it.head(text, [1] * 10, [2] * 10, use_cat=True), it.head(text, [1] * 10, [2] * 10, use_cat=True)
+    assert torch.equal(a, b)
 
 
 def test_train_step_bf16_loss_decreases():

@@ -8,7 +8,7 @@ rm -f ../lib/variants/lib_*.so
 for v in $VARIANTS; do
   name=${v%%:*}; defs=${v#*:}; defs=${defs//,/ }
   for f in tt_filter tt_encoder; do
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $defs -x hip -c $f.hip -o ../build/variants/${f}_$name.o 2>/dev/null &
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -DTT_TIMING_BUILD $defs -x hip -c $f.hip -o ../build/variants/${f}_$name.o 2>/dev/null &
   done
   wait
   others=$(ls ../build/*.o | grep -v "tt_filter\|tt_encoder")

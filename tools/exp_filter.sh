@@ -8,7 +8,7 @@ FILE=${FILE:-tt_filter}  # the source the variants differ in (tt_filter or tt_en
 rm -f ../lib/variants/lib_*.so
 for v in $VARIANTS; do
   name=${v%%:*}; defs=${v#*:}; defs=${defs//,/ }
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $defs -x hip -c $FILE.hip -o ../build/variants/${FILE}_$name.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -DTT_TIMING_BUILD $defs -x hip -c $FILE.hip -o ../build/variants/${FILE}_$name.o
   others=$(ls ../build/*.o | grep -v $FILE)
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $others ../build/variants/${FILE}_$name.o -o ../lib/variants/lib_$name.so
 done

@@ -13,6 +13,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string>
 
 #include "../../include/twotower_hip.h"
@@ -28,6 +29,26 @@ int check_launch(const char* what);
   do {                                                                            \
     if (!(cond)) return ::tt::fail(TT_ERR_INVALID, std::string(__func__) + ": " + (msg)); \
   } while (0)
+
+// ----------------------------------------------------------------------------- A/B switches
+// Alternate kernel paths kept for A/B timing are chosen from the environment ONLY in a
+// timing build (-DTT_TIMING_BUILD, tools/exp_*.sh).  The shipped library ignores the
+// environment and always runs the default path -- the one the GPU tests cover.
+#ifdef TT_TIMING_BUILD
+inline int env_switch(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e && e[0] >= '0' && e[0] <= '9' ? e[0] - '0' : dflt;
+}
+#else
+inline int env_switch(const char*, int dflt) { return dflt; }
+#endif
+// A compile-time experiment macro that changes results (or the tested schedule) may only be
+// set in a timing build: `#error` otherwise (see the users of TT_CHECK_EXP).
+#ifdef TT_TIMING_BUILD
+#define TT_CHECK_EXP(cond, what)
+#else
+#define TT_CHECK_EXP(cond, what) static_assert(!(cond), what " is a timing-only switch: build with -DTT_TIMING_BUILD")
+#endif
 
 // ----------------------------------------------------------------------------- device utils
 typedef float f32x4 __attribute__((ext_vector_type(4)));

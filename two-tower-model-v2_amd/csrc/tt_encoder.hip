@@ -715,6 +715,8 @@ constexpr int GL_STORES = 4 * GL_NJ * 2;
 #ifndef TT_GLEXP_NOEPI
 #define TT_GLEXP_NOEPI 0  // no residual loads / LayerNorm / stores
 #endif  // vector-memory stores per lane in a full tile
+TT_CHECK_EXP(TT_GEXP_NOSTORE || TT_GWEXP_NOEPI || TT_GLEXP_NOW || TT_GLEXP_NOEPI || TT_GL_NT,
+             "TT_G*EXP_* / TT_GL_NT (results wrong or untested)");
 
 __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__ A, int64_t lda,
                                                     const uint16_t* __restrict__ W, int64_t ldw,
@@ -1489,32 +1491,23 @@ int enc_device_cus() {
   return cus;
 }
 // TT_GEMM_BIG=0 in the environment keeps every bf16 GEMM on the 128x128 kernel (A/B timing)
-bool gemm_ln_disabled() {  // TT_GEMM_LN=0: unfused GEMM + LayerNorm (A/B timing)
-  static const bool off = [] {
-    const char* e = getenv("TT_GEMM_LN");
-    return e && e[0] == '0';
-  }();
+bool gemm_ln_disabled() {  // TT_GEMM_LN=0: unfused GEMM + LayerNorm (timing builds only)
+  static const bool off = env_switch("TT_GEMM_LN", 1) == 0;
   return off;
 }
-bool attn_fast_disabled() {  // TT_ATTN_FAST=0: the shared k_attn32_mfma for bf16 too (A/B)
-  static const bool off = [] {
-    const char* e = getenv("TT_ATTN_FAST");
-    return e && e[0] == '0';
-  }();
+bool attn_fast_disabled() {  // TT_ATTN_FAST=0: the shared k_attn32_mfma for bf16 too
+  static const bool off = env_switch("TT_ATTN_FAST", 1) == 0;
   return off;
 }
 bool gemm_wide_disabled() {  // TT_GEMM_WIDE=0: keep 256x128 tiles for the wide GEMMs too
-  static const bool off = [] {
-    const char* e = getenv("TT_GEMM_WIDE");
-    return e && e[0] == '0';
-  }();
+  static const bool off = env_switch("TT_GEMM_WIDE", 1) == 0;
   return off;
 }
 int gemm_big_variant() {  // TT_GEMM_BIG: 0 = 128x128 tiles only, 1 = 256x128 ring (default),
                           // 2 = 128x128 ring, two blocks per CU, 3 = 256x256 ring
   static const int v = [] {
-    const char* e = getenv("TT_GEMM_BIG");
-    return e && e[0] >= '0' && e[0] <= '3' ? e[0] - '0' : 1;
+    const int e = env_switch("TT_GEMM_BIG", 1);
+    return e >= 0 && e <= 3 ? e : 1;
   }();
   return v;
 }

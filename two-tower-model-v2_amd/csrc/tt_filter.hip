@@ -279,6 +279,12 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #ifndef TT_EXP_MAXONLY
 #define TT_EXP_MAXONLY 0  // per-block max + ballot only (no per-slot scan)
 #endif
+TT_CHECK_EXP(TT_EXP_NODMA || TT_EXP_NOSEL || TT_EXP_NOWRITE || TT_EXP_NOBAR || TT_EXP_MAXONLY ||
+                 TT_EXP_SEL_STOP || TT_EXP_SEL_TIMING, "TT_EXP_* (results wrong / printf)");
+TT_CHECK_EXP(TT_RING_HALF || TT_RING_QB4 || TT_EXP_NOIDLE || TT_EXP_SAMPLE_ROWS || TT_EXP_PRIO ||
+                 TT_RING_NT != 1 || TT_SPLIT_APPEND != 1 || TT_SPLIT_TMAX || TT_SPLIT_START != 2 ||
+                 TT_SPLIT_STEP || TT_RR_STAGED != 1 || TT_RR_PF != 1 || TT_RR_NT,
+             "a non-default ring/re-rank schedule (untested by the GPU suite)");
 constexpr int RG_WAVES = (TT_RING_HALF || TT_RING_QB4) ? 4 : 8, RG_PD = 3,
               RG_SLOTS = RG_PD + 1;  // 3 in flight
 constexpr int RG_POOL = (TT_RING_QB4 ? 1024 : 512) * RG_WAVES;  // pool entries per block
@@ -1536,18 +1542,12 @@ struct FilterPlan {
 // <= SEL_CAP/2 rows and is scored densely (every row a candidate); the others stream through
 // the ring kernel.  J = rows of a sample level's top list that feed the next threshold: the
 // full catalog has ~16*J rows above a_J(stride-16 sample), comfortably >= k.
-static bool select_reg_disabled() {  // TT_SELECT_REG=0: LDS-staged k_select_wave (A/B)
-  static const bool off = [] {
-    const char* e = getenv("TT_SELECT_REG");
-    return e && e[0] == '0';
-  }();
+static bool select_reg_disabled() {  // TT_SELECT_REG=0: LDS-staged k_select_wave (timing builds)
+  static const bool off = env_switch("TT_SELECT_REG", 1) == 0;
   return off;
 }
-static bool tmax_first_disabled() {  // TT_FILTER_TMAX_FIRST=0: full sample ladder (A/B)
-  static const bool off = [] {
-    const char* e = getenv("TT_FILTER_TMAX_FIRST");
-    return e && e[0] == '0';
-  }();
+static bool tmax_first_disabled() {  // TT_FILTER_TMAX_FIRST=0: full sample ladder (timing builds)
+  static const bool off = env_switch("TT_FILTER_TMAX_FIRST", 1) == 0;
   return off;
 }
 constexpr int64_t SW_CAP_TILES = SW_CAP - 64;  // first-level tiles per query, with margin

@@ -94,6 +94,16 @@ __global__ void k_relu_bwd(float* __restrict__ dh, const float* __restrict__ h, 
     if (!(h[i] > 0.0f)) dh[i] = 0.0f;
 }
 
+// nn.Dropout(p) with a given keep mask (item_tower.py:61, active under model.train(),
+// trainer.py:167): x[i] = keep[i] ? x[i] * scale : 0, scale = 1 / (1 - p).  The same call on
+// the incoming gradient is the backward.
+__global__ void k_dropout(float* __restrict__ x, const uint8_t* __restrict__ keep, float scale,
+                          int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    x[i] = keep[i] ? x[i] * scale : 0.0f;
+}
+
 // Attention pooling, one block per buyer (S <= 128, hidden Hd <= 256, E <= 1024):
 //   a_s = H_s . W2 + b2 ; c_s = a_s * w_s ; alpha = softmax(c) ; o = sum_s alpha_s x_s ;
 //   z = o / max(||o||, 1e-12).  Saves alpha [B, S] and ||o|| [B] for the backward.
@@ -290,6 +300,16 @@ extern "C" int tt_relu_backward_f32(float* dh, const float* h, int64_t n, void* 
   TT_REQUIRE(dh && h, "null pointer");
   hipLaunchKernelGGL(k_relu_bwd, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, dh, h, n);
   return check_launch("tt_relu_backward_f32");
+}
+
+extern "C" int tt_dropout_apply_f32(float* x, const uint8_t* keep, float scale, int64_t n,
+                                    void* stream) {
+  TT_REQUIRE(n >= 0, "n < 0");
+  if (n == 0) return TT_OK;
+  TT_REQUIRE(x && keep, "null pointer");
+  hipLaunchKernelGGL(k_dropout, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, keep,
+                     scale, n);
+  return check_launch("tt_dropout_apply_f32");
 }
 
 extern "C" int tt_attn_pool_fwd_f32(const float* H, int32_t Hd, const float* W2, float b2,

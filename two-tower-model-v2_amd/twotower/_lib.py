@@ -114,6 +114,7 @@ SIGNATURES = {
     "tt_transpose_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i32, _vp]),
     "tt_col_sum_f32": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _i32, _vp]),
     "tt_relu_backward_f32": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
+    "tt_dropout_apply_f32": (ctypes.c_int, [_vp, _vp, ctypes.c_float, _i64, _vp]),
     "tt_attn_pool_fwd_f32": (ctypes.c_int, [_vp, _i32, _vp, ctypes.c_float, _vp, _vp, _i64, _i32,
                                             _i32, _vp, _vp, _vp, _i64, _vp]),
     "tt_attn_pool_bwd_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _i32,

@@ -15,7 +15,7 @@ import torch
 
 from . import _lib, kernels
 from ._lib import check, lib, stream_ptr
-from .train import GemmOps, _p
+from .train import GemmOps, _p, apply_dropout
 
 
 class AttnAggFn(torch.autograd.Function):
@@ -65,7 +65,7 @@ class AttnAggFn(torch.autograd.Function):
 
 class ItemHeadFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, text, bids, cids, brand_tab, cat_tab, W0, b0, W3, b3):
+    def forward(ctx, text, bids, cids, brand_tab, cat_tab, W0, b0, W3, b3, keep=None, pdrop=0.0):
         dev = text.device
         ops = GemmOps("f32", dev)
         R, Ht = text.shape
@@ -84,10 +84,13 @@ class ItemHeadFn(torch.autograd.Function):
             raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({R}x{width} and "
                                f"{W0.shape[1]}x{W0.shape[0]})")
         h = ops.gemm(x, W0.contiguous(), b0.contiguous(), _lib.TT_ACT_RELU)
+        if keep is not None:  # nn.Dropout (item_tower.py:61) in train mode
+            apply_dropout(h, keep, pdrop)
         y = ops.gemm(h, W3.contiguous(), b3.contiguous())
         E = y.shape[1]
         z = kernels.l2norm_rows(y, E, _lib.TT_NORM_MAX_EPS, out=torch.empty_like(y))
-        ctx.save_for_backward(x, h, y, z, W0, W3, bids, cids)
+        ctx.save_for_backward(x, h, y, z, W0, W3, bids, cids, keep)
+        ctx.pdrop = pdrop
         ctx.dims = (Ht, C, brand_tab is not None,
                     tuple(brand_tab.shape) if brand_tab is not None else None,
                     tuple(cat_tab.shape) if cat_tab is not None else None)
@@ -95,7 +98,7 @@ class ItemHeadFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dz):
-        x, h, y, z, W0, W3, bids, cids = ctx.saved_tensors
+        x, h, y, z, W0, W3, bids, cids, keep = ctx.saved_tensors
         Ht, C, use_cat, bshape, cshape = ctx.dims
         ops = GemmOps("f32", x.device)
         R, E = y.shape
@@ -105,6 +108,8 @@ class ItemHeadFn(torch.autograd.Function):
                                            R, E, dy.data_ptr(), E, stream_ptr()), "norm_bwd")
         db3, dW3 = ops.colsum(dy), ops.dW(dy, h)
         dh = ops.gemm(dy, ops.T(W3.contiguous(), ops.kpad(E)))
+        if keep is not None:  # dropout backward (h is post-dropout: dropped entries are 0)
+            apply_dropout(dh, keep, ctx.pdrop)
         check(lib().tt_relu_backward_f32(dh.data_ptr(), h.data_ptr(), dh.numel(), stream_ptr()),
               "relu_bwd")
         db0, dW0 = ops.colsum(dh), ops.dW(dh, x)
@@ -126,4 +131,4 @@ class ItemHeadFn(torch.autograd.Function):
                         dbt = gt
                     else:
                         dct = gt
-        return dtext, None, None, dbt, dct, dW0, db0, dW3, db3
+        return dtext, None, None, dbt, dct, dW0, db0, dW3, db3, None, None

@@ -152,8 +152,9 @@ class EmbeddingEncoder:
 
     def _item_inputs(self, product_ids: Sequence[str]):
         texts, brands, categories = [], [], []
+        meta = self.product_metadata or {}
         for pid in product_ids:
-            m = self.product_metadata.get(pid, {})
+            m = meta.get(pid, {})
             texts.append(m.get("text", ""))
             brands.append(m.get("brand"))
             categories.append(m.get("category"))
@@ -220,8 +221,12 @@ class EmbeddingEncoder:
         for b, (_, wt) in enumerate(hist):
             w[b, : len(wt)] = torch.tensor(wt, dtype=torch.float32)
         w = w.to(self.device)
+        unknown = []
+        if mode == "B":  # ids outside the resident table: encoded like the reference does
+            unknown = sorted({x for p, _ in hist for x in p if x not in self._table_rows})
         with torch.no_grad():
-            if mode == "B" and self.model.buyer_tower.aggregation_method == "weighted_avg":
+            if (mode == "B" and not unknown
+                    and self.model.buyer_tower.aggregation_method == "weighted_avg"):
                 rows = torch.zeros((B, max(S, 1)), dtype=torch.int64)
                 for b, (p, _) in enumerate(hist):
                     rows[b, : len(p)] = torch.tensor([self._table_rows[x] for x in p],
@@ -233,9 +238,7 @@ class EmbeddingEncoder:
                 flat = [x for p, _ in hist for x in p]
                 if flat:
                     if mode == "B":
-                        idx = torch.tensor([self._table_rows[x] for x in flat],
-                                           device=self.device)
-                        enc = self._table[idx, :E]
+                        enc = self._mode_b_rows(flat, unknown, E)
                     else:
                         enc = self.model.item_tower(*self._item_inputs(flat))
                     o = 0
@@ -244,6 +247,22 @@ class EmbeddingEncoder:
                         o += len(p)
                 out = self.model.buyer_tower(items, w)
         return out.cpu().numpy() if as_numpy else out
+
+    def _mode_b_rows(self, flat, unknown, E):
+        """History rows for Mode B: table rows for resident ids; an id missing from the table
+        gets what encode_buyer would compute for it (its metadata, {} if unknown: text ' ',
+        no brand / category, encoder.py:280-292), so Mode B never fails where Mode A works."""
+        rows = [self._table_rows.get(x, -1) for x in flat]
+        enc = torch.empty((len(flat), E), dtype=torch.float32, device=self.device)
+        have = [i for i, r in enumerate(rows) if r >= 0]
+        if have:
+            enc[have] = self._table[torch.tensor([rows[i] for i in have], device=self.device), :E]
+        if unknown:
+            extra = self.model.item_tower(*self._item_inputs(unknown))
+            pos = {x: j for j, x in enumerate(unknown)}
+            miss = [i for i, r in enumerate(rows) if r < 0]
+            enc[miss] = extra[torch.tensor([pos[flat[i]] for i in miss], device=self.device)]
+        return enc
 
     # reference :307-335
     def save_item_embeddings(self, product_ids: List[str], embeddings: np.ndarray,

@@ -307,16 +307,20 @@ class ItemTower(nn.Module):
         C = self.categorical_embedding_dim if use_cat else 0
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
             from .autograd_ops import ItemHeadFn  # training: HIP forward + backward
+            from .train import dropout_keep
 
             l0, l3 = self.projection[0], self.projection[3]
             ids = lambda v: (torch.tensor(v, dtype=torch.int32, device=dev)  # noqa: E731
                              if v is not None else None)
             bt = self.brand_embedding.weight.to(dev) if use_cat else None
             ct = self.category_embedding.weight.to(dev) if use_cat else None
+            pdrop = self.projection[2].p if self.training else 0.0
+            keep = dropout_keep((text_emb.shape[0], l0.weight.shape[0]), pdrop, dev) \
+                if pdrop > 0 else None
             return ItemHeadFn.apply(text_emb, ids(brand_ids) if use_cat else None,
                                     ids(cat_ids) if use_cat else None, bt, ct,
                                     l0.weight.to(dev), l0.bias.to(dev), l3.weight.to(dev),
-                                    l3.bias.to(dev))
+                                    l3.bias.to(dev), keep, pdrop)
         width = Ht + 2 * C
         l0, l3 = self.projection[0], self.projection[3]
         x = torch.empty((B, width), dtype=torch.float32, device=dev)
@@ -347,6 +351,11 @@ class ItemTower(nn.Module):
         check(lib().tt_gemm_f32(x.data_ptr(), x.stride(0), w0.data_ptr(), w0.stride(0),
                                 b0.data_ptr(), None, 0, h.data_ptr(), h.stride(0), None, 0, B, hdim,
                                 width, _lib.TT_ACT_RELU, stream_ptr()), "projection.0")
+        if self.training and self.projection[2].p > 0:  # nn.Dropout (:61) in train mode
+            from .train import apply_dropout, dropout_keep
+
+            p = self.projection[2].p
+            apply_dropout(h, dropout_keep(h.shape, p, dev), p)
         y = torch.empty((B, E), dtype=torch.float32, device=dev)
         check(lib().tt_gemm_f32(h.data_ptr(), h.stride(0), w3.data_ptr(), w3.stride(0),
                                 b3.data_ptr(), None, 0, y.data_ptr(), y.stride(0), None, 0, B, E,

@@ -27,6 +27,20 @@ def _p(t):
     return t.data_ptr() if t is not None else None
 
 
+def dropout_keep(shape, p: float, device) -> torch.Tensor:
+    """Keep mask of nn.Dropout(p) (uint8, 1 = keep), drawn from torch's device RNG."""
+    return (torch.rand(shape, device=device) >= p).to(torch.uint8)
+
+
+def apply_dropout(x: torch.Tensor, keep: torch.Tensor, p: float) -> torch.Tensor:
+    """In place x = x * keep / (1 - p) (tt_dropout_apply_f32); also the backward on a grad."""
+    if keep.shape != x.shape or keep.dtype != torch.uint8 or not x.is_contiguous():
+        raise ValueError("dropout: keep must be a uint8 mask of x's shape, x contiguous")
+    check(lib().tt_dropout_apply_f32(x.data_ptr(), keep.contiguous().data_ptr(),
+                                     1.0 / (1.0 - p), x.numel(), stream_ptr()), "dropout")
+    return x
+
+
 class GemmOps:
     """GEMM-shaped pieces of the backward passes on the HIP kernels (f32 or bf16 MFMA)."""
 
@@ -88,8 +102,9 @@ class TwoTowerTrainStep:
 
     def __init__(self, item_tower, buyer_tower, temperature: float = 0.07, lr: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, prec: str = "f32"):
-        if buyer_tower.aggregation_method != "attention":
-            raise ValueError("the configs[4] step trains the attention aggregation")
+        if buyer_tower.aggregation_method not in ("attention", "weighted_avg"):
+            raise ValueError(f"Unknown aggregation method: {buyer_tower.aggregation_method}")
+        self.attention = buyer_tower.aggregation_method == "attention"
         if prec not in ("f32", "bf16"):
             raise ValueError("prec must be 'f32' or 'bf16'")
         self.it, self.bt = item_tower, buyer_tower
@@ -103,13 +118,17 @@ class TwoTowerTrainStep:
         self.v = {k: torch.zeros_like(v) for k, v in self.params.items()}
         self.t = 0
         self.last_loss = None
+        # nn.Dropout(0.1) of the projection (item_tower.py:61): active when the item tower is
+        # in train mode, as under the reference Trainer (model.train(), trainer.py:167)
+        self.keep_fn = dropout_keep
 
     def _params(self) -> Dict[str, torch.Tensor]:
         it, bt = self.it, self.bt
         p = {"proj0.w": it.projection[0].weight, "proj0.b": it.projection[0].bias,
-             "proj3.w": it.projection[3].weight, "proj3.b": it.projection[3].bias,
-             "att0.w": bt.attention[0].weight, "att0.b": bt.attention[0].bias,
-             "att2.w": bt.attention[2].weight, "att2.b": bt.attention[2].bias}
+             "proj3.w": it.projection[3].weight, "proj3.b": it.projection[3].bias}
+        if self.attention:  # weighted_avg has no parameters (buyer_tower.py:43-68)
+            p.update({"att0.w": bt.attention[0].weight, "att0.b": bt.attention[0].bias,
+                      "att2.w": bt.attention[2].weight, "att2.b": bt.attention[2].bias})
         if it.use_categorical_features and it.brand_embedding is not None:
             p["brand"] = it.brand_embedding.weight
             p["cat"] = it.category_embedding.weight
@@ -164,23 +183,29 @@ class TwoTowerTrainStep:
                                        x.data_ptr(), width, None, stream_ptr()), "concat")
         else:
             x.copy_(text)
-        # item head forward
+        # item head forward (Linear -> ReLU -> Dropout -> Linear)
         h = self._gemm(x, P["proj0.w"], P["proj0.b"], _lib.TT_ACT_RELU)
+        pdrop = self.it.projection[2].p if self.it.training else 0.0
+        keep = self.keep_fn(h.shape, pdrop, self.dev) if pdrop > 0 else None
+        if keep is not None:
+            apply_dropout(h, keep, pdrop)
         y = self._gemm(h, P["proj3.w"], P["proj3.b"])
         z = kernels.l2norm_rows(y, E, _lib.TT_NORM_MAX_EPS, out=torch.empty_like(y))
-        # buyer attention forward
-        X = buyer_items.reshape(B * S, E).contiguous()
-        Hb = self._gemm(X, P["att0.w"], P["att0.b"], _lib.TT_ACT_RELU)
-        Hd = Hb.shape[1]
         w = weights.contiguous().to(torch.float32)
-        alpha = torch.empty((B, S), dtype=torch.float32, device=self.dev)
-        onorm = torch.empty(B, dtype=torch.float32, device=self.dev)
-        zb = torch.empty((B, E), dtype=torch.float32, device=self.dev)
-        b2 = float(P["att2.b"].item())
-        check(lib().tt_attn_pool_fwd_f32(Hb.data_ptr(), Hd, P["att2.w"].data_ptr(), b2,
-                                         w.data_ptr(), X.data_ptr(), B, S, E, alpha.data_ptr(),
-                                         onorm.data_ptr(), zb.data_ptr(), E, stream_ptr()),
-              "attn_pool_fwd")
+        if not self.attention:  # weighted average + F.normalize: no trainable parameters
+            zb = kernels.weighted_avg_l2(buyer_items, w)
+        else:  # buyer attention forward
+            X = buyer_items.reshape(B * S, E).contiguous()
+            Hb = self._gemm(X, P["att0.w"], P["att0.b"], _lib.TT_ACT_RELU)
+            Hd = Hb.shape[1]
+            alpha = torch.empty((B, S), dtype=torch.float32, device=self.dev)
+            onorm = torch.empty(B, dtype=torch.float32, device=self.dev)
+            zb = torch.empty((B, E), dtype=torch.float32, device=self.dev)
+            b2 = float(P["att2.b"].item())
+            check(lib().tt_attn_pool_fwd_f32(Hb.data_ptr(), Hd, P["att2.w"].data_ptr(), b2,
+                                             w.data_ptr(), X.data_ptr(), B, S, E,
+                                             alpha.data_ptr(), onorm.data_ptr(), zb.data_ptr(),
+                                             E, stream_ptr()), "attn_pool_fwd")
         # InfoNCE forward + backward
         loss, (gb, gp, gn) = infonce(zb, z[:B], z[B:].view(B, N, E), self.tau, self.prec)
         g = {}
@@ -192,6 +217,8 @@ class TwoTowerTrainStep:
         g["proj3.b"] = self._colsum(dy)
         g["proj3.w"] = self._dW(dy, h)
         dh = self._gemm(dy, self._T(P["proj3.w"], self._kpad(E)))       # dy W3
+        if keep is not None:  # dropout backward; h is post-dropout (dropped entries 0)
+            apply_dropout(dh, keep, pdrop)
         check(lib().tt_relu_backward_f32(dh.data_ptr(), h.data_ptr(), dh.numel(), stream_ptr()),
               "relu_bwd")
         g["proj0.b"] = self._colsum(dh)
@@ -206,6 +233,8 @@ class TwoTowerTrainStep:
                                                           idsv.data_ptr(), R, C, gt.data_ptr(),
                                                           stream_ptr()), "emb_bwd")
                 g[key] = gt
+        if not self.attention:
+            return loss, g
         # buyer attention backward
         dW2 = torch.empty(Hd, dtype=torch.float32, device=self.dev)
         db2 = torch.empty(1, dtype=torch.float32, device=self.dev)
