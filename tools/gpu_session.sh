@@ -18,7 +18,11 @@ run() {  # name timeout cmd...
 }
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ;;
+    tests) if [ -n "${PYTEST_K:-}" ]; then
+             run pytest_gpu 900 python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "$PYTEST_K"
+           else
+             run pytest_gpu 900 python -u -m pytest ${PYTEST_FILES:-tests} -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}
+           fi ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     bench_f32) run bench_f32 600 python bench.py --method f32 --no-cpu-baseline ${BENCH_ARGS:-} ;;

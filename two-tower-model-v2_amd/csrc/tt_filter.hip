@@ -1301,6 +1301,292 @@ __global__ __launch_bounds__(256) void k_select_reg(const uint64_t* __restrict__
   }
 }
 
+// --------------------------------------------------------------------------- small batches
+// Small query batches (nq <= SM_NQ: the one-buyer /retrieve call, Mode A's 256-buyer
+// searches): one 1024-thread block per query instead of one wave.  A lone query's
+// k_select_reg (one wave walking up to 2048 keys and 32 dependent ballot steps) and
+// k_rerank (6 dependent 256-B chunk rounds per 64 band rows) were latency-bound: 16-25 us
+// each.  Here the whole block gathers the candidate keys into LDS, a 4-pass 8-bit radix
+// select finds the R-th largest score, and (last level) the band's exact scores come from
+// the f32 MFMA in one round: a wave scores 16 band rows with v_mfma_f32_16x16x4_f32, lane
+// group g holding dims 16t+4g..+3 -- the canonical fma order (t, i, g), bit-identical to
+// the f32 scan and k_rerank -- all of its 16-B row loads in flight at once.
+#ifndef TT_EXP_SMALL_TIMING
+#define TT_EXP_SMALL_TIMING 0  // timing builds: printf phase ticks of k_final_small (query 0)
+#endif
+TT_CHECK_EXP(TT_EXP_SMALL_TIMING, "TT_EXP_SMALL_TIMING (printf)");
+#if TT_EXP_SMALL_TIMING
+#define SM_TICK(i) if (threadIdx.x == 0) tk[i] = wall_clock64();
+#else
+#define SM_TICK(i)
+#endif
+constexpr int SM_THREADS = 1024, SM_WAVES = SM_THREADS / 64;
+constexpr int SM_NQ = 256;
+constexpr int SM_PER = SW_CAP / SM_THREADS;  // keys per thread in the radix select
+
+struct SmallLds {
+  uint64_t key[SW_CAP];   // the query's candidate keys (orderable score << 32 | ~row)
+  int wred[SM_WAVES];
+  int hist[256];
+  int pick[2];
+  int nb;
+};
+
+// Gather the query's per-slab candidate lists into s.key (n_slabs <= SM_THREADS).  Returns
+// the candidate count, or -1 when a list overflowed / the total exceeds SW_CAP.
+__device__ int small_collect(const uint64_t* __restrict__ lists, const int* __restrict__ counts,
+                             int n_slabs, int qid, SmallLds& s) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c = tid < n_slabs ? counts[(int64_t)qid * n_slabs + tid] : 0;
+  int incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    incl += lane >= o ? y : 0;
+  }
+  if (lane == 63) s.wred[w] = incl;
+  const int over = __syncthreads_or(c > FL_CAP);
+  int base = 0, total = 0;
+#pragma unroll
+  for (int i = 0; i < SM_WAVES; ++i) {
+    const int v = s.wred[i];
+    base += i < w ? v : 0;
+    total += v;
+  }
+  if (over || total > SW_CAP) return -1;
+  const uint64_t* l = lists + ((int64_t)qid * n_slabs + tid) * FL_CAP;
+  const int e0 = base + incl - c;
+#pragma unroll 4
+  for (int i = 0; i < c; ++i) s.key[e0 + i] = l[i];
+  __syncthreads();
+  return total;
+}
+
+// R-th largest high word (orderable score) of the keys h (0 = no key), block-wide radix
+// select, 4 passes of 8 bits.  Caller guarantees at least R nonzero keys.
+__device__ uint32_t small_radix_select(const uint32_t (&h)[SM_PER], int R, SmallLds& s) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t prefix = 0, pmask = 0;
+  int r = R;
+#pragma unroll 1
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    if (tid < 256) s.hist[tid] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SM_PER; ++j)
+      if (h[j] != 0u && (h[j] & pmask) == prefix) atomicAdd(&s.hist[(h[j] >> shift) & 255u], 1);
+    __syncthreads();
+    if (w == 0) {
+      const int b0 = s.hist[4 * lane], b1 = s.hist[4 * lane + 1], b2 = s.hist[4 * lane + 2],
+                b3 = s.hist[4 * lane + 3];
+      const int mine = b0 + b1 + b2 + b3;
+      int suf = mine;  // keys in bins >= 4 lane
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_down(suf, o, 64);
+        suf += lane + o < 64 ? y : 0;
+      }
+      const uint64_t m = __ballot(suf >= r);
+      const int L = 63 - __builtin_clzll(m);
+      if (lane == L) {
+        int above = suf - mine, b = 0;
+        const int bins[4] = {b0, b1, b2, b3};
+#pragma unroll
+        for (int bb = 3; bb >= 0; --bb) {
+          if (above + bins[bb] >= r) {
+            b = bb;
+            break;
+          }
+          above += bins[bb];
+        }
+        s.pick[0] = 4 * L + b;
+        s.pick[1] = r - above;
+      }
+    }
+    __syncthreads();
+    prefix |= (uint32_t)s.pick[0] << shift;
+    pmask |= 0xffu << shift;
+    r = s.pick[1];
+    __syncthreads();
+  }
+  return prefix;
+}
+
+// Sample level of a small batch (mode 0 of k_select_reg): theta_out = a_J (fin: a_J - eps2).
+__global__ __launch_bounds__(SM_THREADS) void k_select_small(
+    const uint64_t* __restrict__ lists, const int* __restrict__ counts, int n_slabs, int J,
+    const float* __restrict__ eps2, float* __restrict__ theta_out, float* __restrict__ aref,
+    int* __restrict__ flags, int* qsel, int* qsel_n, int fin) {
+  __shared__ SmallLds s;
+  const int qid = blockIdx.x, tid = threadIdx.x;
+  if (flags[qid]) {
+    if (tid == 0) theta_out[qid] = __builtin_huge_valf();
+    return;
+  }
+  const int total = small_collect(lists, counts, n_slabs, qid, s);
+  if (total < 0) {
+    if (tid == 0) {
+      flag_query(qid, flags, qsel, qsel_n);
+      theta_out[qid] = __builtin_huge_valf();
+    }
+    return;
+  }
+  if (total < J) {  // fewer than J candidates: a_J = -inf
+    if (tid == 0) theta_out[qid] = aref[qid] = -__builtin_huge_valf();
+    return;
+  }
+  uint32_t h[SM_PER];
+#pragma unroll
+  for (int j = 0; j < SM_PER; ++j) {
+    const int e = tid + j * SM_THREADS;
+    h[j] = e < total ? (uint32_t)(s.key[e] >> 32) : 0u;
+  }
+  const float A = key_float(small_radix_select(h, J, s));
+  if (tid == 0) {
+    theta_out[qid] = fin ? A - eps2[qid] : A;
+    aref[qid] = A;
+  }
+}
+
+// Full level of a small batch: selection (mode 1 of k_select_reg) + exact re-rank (k_rerank)
+// in one launch.  A_k = k-th best a; A_k < aref -> the optimistic threshold failed (flag);
+// band = candidates with a >= A_k - eps2 (<= BAND_CAP, else flag); exact canonical f32
+// scores of the band rows by f32 MFMA; sort (score desc, row asc); top-k out.
+template <int EP>
+__global__ __launch_bounds__(SM_THREADS) void k_final_small(
+    const uint64_t* __restrict__ lists, const int* __restrict__ counts, int n_slabs, int k,
+    const float* __restrict__ eps2, const float* __restrict__ aref, int* __restrict__ flags,
+    int* qsel, int* qsel_n, const float* __restrict__ db, int64_t ld,
+    const float* __restrict__ q, int64_t ldq, int64_t row_base, float* __restrict__ out_s,
+    int64_t* __restrict__ out_i) {
+  __shared__ SmallLds s;
+  __shared__ uint32_t brow[BAND_CAP];
+  __shared__ uint64_t sbuf[BAND_CAP];
+  __shared__ __attribute__((aligned(16))) float qs[EP];
+  const int qid = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+#if TT_EXP_SMALL_TIMING
+  uint64_t tk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  SM_TICK(0)
+  if (flags[qid]) return;  // served by the exact fallback
+  const int total = small_collect(lists, counts, n_slabs, qid, s);
+  SM_TICK(1)
+  if (total < k) {  // overflow (-1) or too few candidates to certify: exact fallback
+    if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
+  uint32_t h[SM_PER];
+#pragma unroll
+  for (int j = 0; j < SM_PER; ++j) {
+    const int e = tid + j * SM_THREADS;
+    h[j] = e < total ? (uint32_t)(s.key[e] >> 32) : 0u;
+  }
+  const float A = key_float(small_radix_select(h, k, s));
+  SM_TICK(2)
+  if (!(A >= aref[qid])) {
+    if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
+  const float thr = A - eps2[qid];
+  if (tid == 0) s.nb = 0;
+  for (int i = tid; i < EP; i += SM_THREADS) qs[i] = q[(int64_t)qid * ldq + i];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < SM_PER; ++j) {
+    const int e = tid + j * SM_THREADS;
+    if (h[j] != 0u && key_float(h[j]) >= thr) {
+      const int pos = atomicAdd(&s.nb, 1);
+      if (pos < BAND_CAP) brow[pos] = key_row(s.key[e]);
+    }
+  }
+  __syncthreads();
+  const int nb = s.nb;
+  SM_TICK(3)
+  if (nb > BAND_CAP) {
+    if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
+  // exact scores: wave w takes band rows [16 gi, 16 gi + 16), gi = w, w + SM_WAVES, ...  Lane
+  // (r, g) loads row r's dims 16t + 4g .. +3 for every t (all loads in flight) and the chain
+  // runs on v_mfma_f32_16x16x4_f32 with the query in every column: the canonical order
+  // (t, i, g), bit-identical to the f32 scan.  (Per-row VALU fma chains after an LDS
+  // transpose: 0.182 vs 0.177 ms per one-buyer search, 0.292 vs 0.276 ms at 256 queries.)
+  {
+    const int r16 = lane & 15, g = lane >> 4;
+    constexpr int NT = EP / 16, TCH = NT <= 24 ? NT : 16;  // t-steps per load batch
+    static_assert(NT % TCH == 0, "load batches must tile the row");
+    for (int gi = w; 16 * gi < nb; gi += SM_WAVES) {
+      const int e = 16 * gi + r16;
+      const uint32_t row = brow[e < nb ? e : nb - 1];
+      const float* xr = db + (int64_t)row * ld + 4 * g;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+      for (int t0 = 0; t0 < NT; t0 += TCH) {
+        f32x4 a[TCH];
+#pragma unroll
+        for (int t = 0; t < TCH; ++t) a[t] = *(const f32x4*)(xr + 16 * (t0 + t));
+#pragma unroll
+        for (int t = 0; t < TCH; ++t) {
+          const f32x4 b = *(const f32x4*)(qs + 16 * (t0 + t) + 4 * g);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][0], b[0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][1], b[1], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][2], b[2], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][3], b[3], acc, 0, 0, 0);
+        }
+      }
+      if (r16 == 0) {  // D[row 4g + j][col 0] sits in lane 16 g
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int ej = 16 * gi + 4 * g + j;
+          if (ej < nb) sbuf[ej] = acc[j] != acc[j] ? 0ull : make_key(acc[j], brow[ej]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  SM_TICK(4)
+  // (score desc, row asc) order by rank: rank(e) = #keys ahead of key e (keys of distinct
+  // rows are distinct; equal keys -- only NaN scores, key 0 -- are ordered by position), so
+  // every band entry knows its output slot without a sort: ~nb compares per entry, over 4
+  // threads per entry when nb <= 256 (the bitonic sorts this replaces spent 36 dependent
+  // stages: 4.6 us in one wave, 7.5 us block-wide).
+  {
+    const int per = nb <= 256 ? 4 : 1;
+    const int e = tid / per, part = tid % per;
+    int rank = 0;
+    uint64_t me = 0ull;
+    if (e < nb) {
+      me = sbuf[e];
+      for (int j = part; j < nb; j += per) {
+        const uint64_t o = sbuf[j];
+        rank += (o > me || (o == me && j < e)) ? 1 : 0;
+      }
+    }
+    if (per == 4) {  // the 4 partial counts sit in adjacent lanes of one wave
+      rank += __shfl_xor(rank, 1, 64);
+      rank += __shfl_xor(rank, 2, 64);
+    }
+    if (e < nb && part == 0 && rank < k) {
+      float sc = -__builtin_huge_valf();
+      int64_t ix = -1;
+      if (me != 0ull) {  // NaN score: key 0 ranks last, reported as (-inf, -1)
+        sc = key_score(me);
+        ix = row_base + (int64_t)key_row(me);
+      }
+      out_s[(int64_t)qid * k + rank] = sc;
+      out_i[(int64_t)qid * k + rank] = ix;
+    }
+    // every slot < k is written: nb >= k (the band holds the k candidates >= A_k)
+  }
+  SM_TICK(5)
+#if TT_EXP_SMALL_TIMING
+  if (tid == 0 && qid == 0)
+    printf("SMALLT nb=%d total=%d collect %d radix %d band %d score %d rank %d (x10ns)\n",
+           nb, total, (int)(tk[1] - tk[0]), (int)(tk[2] - tk[1]), (int)(tk[3] - tk[2]),
+           (int)(tk[4] - tk[3]), (int)(tk[5] - tk[4]));
+#endif
+}
+
 // sharded finish: pcount[q][i] = #rows over ALL shards with a >= t_i (all-reduced SUM).
 // pcount[q][0] < k: the sample threshold did not certify -> exact fallback on every shard
 // (identical decision on all ranks).  Else A_k >= t* = the highest probe with >= k rows, so
@@ -1801,7 +2087,8 @@ int filter_init(const FilterWs& w, const float* q, int nq, int64_t ld_q, int ep,
 int filter_level(const FilterPlan& p, const FilterWs& w, int li, int mode, const uint16_t* db16,
                  int64_t n, int64_t ld_db, const float* q, int nq, int64_t ld_q, int k, int ep,
                  hipStream_t st, void* ev_start, void* ev_stop, const float* stats = nullptr,
-                 int* pcount = nullptr, float* smax_out = nullptr, int fin = 0) {
+                 int* pcount = nullptr, float* smax_out = nullptr, int fin = 0,
+                 bool no_select = false) {
   const Level& L = p.lv[li];
   const bool last = li == p.n_levels - 1;
   if (last && ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
@@ -1819,6 +2106,7 @@ int filter_level(const FilterPlan& p, const FilterWs& w, int li, int mode, const
   if (rc) return rc;
   if (last && ev_stop && hipEventRecord((hipEvent_t)ev_stop, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "hipEventRecord(stop)");
+  if (no_select) return TT_OK;
   auto sel = select_reg_disabled()  ? k_select_wave
              : L.n_slabs <= 64      ? k_select_reg<false>
              : L.n_slabs <= 64 * SR_GMAX ? k_select_reg<true>
@@ -1877,14 +2165,41 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
   if ((rc = filter_init(w, q, nq, ld_q, ep, x_norm_max, x_resid_max, st))) return rc;
+  // small batches: block-per-query selection (k_select_small) and a fused selection +
+  // f32-MFMA re-rank of the full level (k_final_small)
+  bool small = nq <= SM_NQ && !select_reg_disabled();
+  for (int li = 0; li < p.n_levels; ++li) small = small && p.lv[li].n_slabs <= SM_THREADS;
   for (int li = 0; li < p.n_levels; ++li) {
     const bool last = li == p.n_levels - 1;
     // the last sample level's selection writes the full level's threshold a_J - 2 eps itself
     // (was a copy + k_sub_arr launch: full_threshold, kept for the sharded protocol)
     const int fin = li == p.n_levels - 2;
     if ((rc = filter_level(p, w, li, last ? 1 : 0, db_bf16, n, ld_db, q, nq, ld_q, k, ep, st,
-                           ev_start, ev_stop, nullptr, nullptr, nullptr, fin)))
+                           ev_start, ev_stop, nullptr, nullptr, nullptr, fin, small)))
       return rc;
+    if (small && !last) {
+      hipLaunchKernelGGL(k_select_small, dim3(nq), dim3(SM_THREADS), 0, st, w.lists, w.counts,
+                         p.lv[li].n_slabs, p.J, w.eps2, w.theta, w.aref, w.flags, w.qsel,
+                         w.qsel_n, fin);
+      if ((rc = check_launch("k_select_small"))) return rc;
+    }
+  }
+  if (small) {
+    TT_REQUIRE(db != nullptr && out_score && out_idx, "null pointer");
+    const int ns = p.lv[p.n_levels - 1].n_slabs;
+    switch (ep) {
+#define TT_FS(E)                                                                              \
+  case E:                                                                                     \
+    hipLaunchKernelGGL(k_final_small<E>, dim3(nq), dim3(SM_THREADS), 0, st, w.lists,          \
+                       w.counts, ns, k, w.eps2, w.aref, w.flags, w.qsel, w.qsel_n, db, ld_db, \
+                       q, ld_q, row_base, out_score, out_idx);                                \
+    break;
+      TT_FS(64) TT_FS(128) TT_FS(256) TT_FS(384) TT_FS(512) TT_FS(768)
+#undef TT_FS
+    }
+    if ((rc = check_launch("k_final_small"))) return rc;
+    return tt_scan_topk_f32_select(db, n, d, ld_db, row_base, q, nq, ld_q, k, w.qsel, w.qsel_n,
+                                   out_score, out_idx, w.scan_ws, w.scan_ws_bytes, st);
   }
   return filter_finish(w, db, n, d, ld_db, row_base, q, nq, ld_q, k, ep, out_score, out_idx, st);
 }

@@ -44,45 +44,6 @@ struct ScanCfg {
 using CfgNarrow = ScanCfg<4, 192, 256>;
 using CfgWide = ScanCfg<1, 1280, 2048>;
 
-// Bitonic sort, descending, of 64*PER keys held PER per lane (element e = lane*PER + r).
-template <int PER>
-__device__ __forceinline__ void bitonic_desc(uint64_t (&key)[PER], int lane) {
-  constexpr int N = 64 * PER;
-#pragma unroll
-  for (int size = 2; size <= N; size <<= 1) {
-#pragma unroll
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      if (stride >= PER) {
-        const int lm = stride / PER;
-#pragma unroll
-        for (int r = 0; r < PER; ++r) {
-          const int e = lane * PER + r;
-          const uint64_t o = shfl_xor_u64(key[r], lm);
-          const bool up = (e & size) == 0;
-          const bool lower = (e & stride) == 0;
-          const bool keep_max = (lower == up);
-          const uint64_t mx = key[r] > o ? key[r] : o;
-          const uint64_t mn = key[r] > o ? o : key[r];
-          key[r] = keep_max ? mx : mn;
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < PER; ++r) {
-          if ((r & stride) == 0) {
-            const int r2 = r | stride;
-            const int e = lane * PER + r;
-            const bool up = (e & size) == 0;
-            const uint64_t a = key[r], b = key[r2];
-            const uint64_t mx = a > b ? a : b, mn = a > b ? b : a;
-            key[r] = up ? mx : mn;
-            key[r2] = up ? mn : mx;
-          }
-        }
-      }
-    }
-  }
-}
-
 template <int PER>
 __device__ __forceinline__ uint64_t pick(const uint64_t (&key)[PER], int r) {
   uint64_t v = key[0];
