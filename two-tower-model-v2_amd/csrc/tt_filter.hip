@@ -236,9 +236,6 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #ifndef TT_EXP_NOWRITE
 #define TT_EXP_NOWRITE 0  // selection control flow without the LDS pool writes
 #endif
-#ifndef TT_EXP_SAMPLE_ROWS
-#define TT_EXP_SAMPLE_ROWS 0  // sample levels append every passing row (not tile maxima)
-#endif
 #ifndef TT_EXP_PRIO
 #define TT_EXP_PRIO 0  // s_setprio 1 for waves 4-7 (static priority for the younger half)
 #endif
@@ -248,21 +245,6 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 // (5.6 -> 6.2 TB/s), batched level unchanged; 3 = every level: the batched full level, whose
 // 40 query tiles re-read the catalog from L2/MALL, 6.85 -> 7.29 ms (A/B, same box).
 #define TT_RING_NT 1
-#endif
-// Candidate scan of the previous tile split into per-query-block pieces spread between the
-// MFMAs (1, default) instead of one burst at step 1 (0): batched full level 6.81 -> 6.65 ms
-// (A/B x2, same box); per-(query block, row block) pieces (2): 6.75 ms.
-#ifndef TT_SPLIT_APPEND
-#define TT_SPLIT_APPEND 1
-#endif
-#ifndef TT_SPLIT_TMAX
-#define TT_SPLIT_TMAX 0  // sample levels: tile-max appends split the same way (A/B: +15 us)
-#endif
-#ifndef TT_SPLIT_START
-#define TT_SPLIT_START 2  // k-step of the first piece (2 vs 1: 6.64 vs 6.72 ms, A/B x2)
-#endif
-#ifndef TT_SPLIT_STEP
-#define TT_SPLIT_STEP 0  // k-steps between pieces (0: KS / pieces)
 #endif
 #ifndef TT_RR_STAGED
 // k_rerank: 1 (default) = wave-cooperative 256-B row pieces through an LDS stage, 0 = each
@@ -281,23 +263,23 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #endif
 TT_CHECK_EXP(TT_EXP_NODMA || TT_EXP_NOSEL || TT_EXP_NOWRITE || TT_EXP_NOBAR || TT_EXP_MAXONLY ||
                  TT_EXP_SEL_STOP || TT_EXP_SEL_TIMING, "TT_EXP_* (results wrong / printf)");
-TT_CHECK_EXP(TT_RING_HALF || TT_RING_QB4 || TT_EXP_NOIDLE || TT_EXP_SAMPLE_ROWS || TT_EXP_PRIO ||
-                 TT_RING_NT != 1 || TT_SPLIT_APPEND != 1 || TT_SPLIT_TMAX || TT_SPLIT_START != 2 ||
-                 TT_SPLIT_STEP || TT_RR_STAGED != 1 || TT_RR_PF != 1 || TT_RR_NT,
+TT_CHECK_EXP(TT_RING_HALF || TT_RING_QB4 || TT_EXP_NOIDLE || TT_EXP_PRIO ||
+                 TT_RING_NT != 1 || TT_RR_STAGED != 1 || TT_RR_PF != 1 || TT_RR_NT,
              "a non-default ring/re-rank schedule (untested by the GPU suite)");
 constexpr int RG_WAVES = (TT_RING_HALF || TT_RING_QB4) ? 4 : 8, RG_PD = 3,
               RG_SLOTS = RG_PD + 1;  // 3 in flight
-constexpr int RG_POOL = (TT_RING_QB4 ? 1024 : 512) * RG_WAVES;  // pool entries per block
+// Pool entries per wave: a query block's scan appends at most 16 x TR <= 512 (16 x 32 rows, all
+// passing); it starts with wn <= RG_WFLUSH, so its writes need no bounds check.
+constexpr int RG_WFLUSH = 256;
+constexpr int RG_WPOOL = RG_WFLUSH + (TT_RING_QB4 ? 1024 : 512);
+constexpr int RG_POOL = RG_WPOOL * RG_WAVES;  // pool entries per block
 constexpr int RG_BLOCKS_PER_CU = TT_RING_HALF ? 2 : 1;
-constexpr int RG_WPOOL = RG_POOL / RG_WAVES;   // ... per wave (wave-private region)
-constexpr int RG_WFLUSH = RG_WPOOL / 2;
-constexpr uint32_t RG_OVF = 1u << 30;  // marks a (query, slab) list whose entries were dropped
 
 template <int EP>
 constexpr int ring_qpb() { return RG_WAVES * 16 * RingCfg<EP>::QB; }
 template <int EP>
 constexpr int ring_smem() {
-  return RG_SLOTS * RingCfg<EP>::TR * EP * 2 + RG_POOL * 12 + ring_qpb<EP>() * 4 + 16;
+  return RG_SLOTS * RingCfg<EP>::TR * EP * 2 + RG_POOL * 8 + ring_qpb<EP>() * 4 + 16;
 }
 
 // LDS ops of the ring kernel's append path, in inline asm: the compiler cannot prove they do
@@ -308,9 +290,6 @@ __device__ __forceinline__ uint32_t lds_add_rtn(uint32_t addr, uint32_t v) {
   asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
                : "=&v"(r) : "v"(addr), "v"(v) : "memory");
   return r;
-}
-__device__ __forceinline__ void lds_or(uint32_t addr, uint32_t v) {
-  asm volatile("ds_or_b32 %0, %1" ::"v"(addr), "v"(v) : "memory");
 }
 __device__ __forceinline__ void lds_write64(uint32_t addr, uint64_t v) {
   asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(v) : "memory");
@@ -360,12 +339,13 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   constexpr int PIECES = TILE_B / 1024, PPW = PIECES / RG_WAVES;
   constexpr int FM = (CPR >= 16 ? 16 : CPR) - 1;
   constexpr int RB = TR / 16;
+  constexpr int QSH = QPW == 16 ? 4 : QPW == 32 ? 5 : 6;  // pool entry: query bits
+  static_assert((1 << QSH) == QPW, "queries per wave: a power of two");
   static_assert(PIECES % RG_WAVES == 0, "tile must split into whole 1-KiB pieces per wave");
   __shared__ __attribute__((aligned(16))) char smem[ring_smem<EP>()];
   char* ring = smem;
   uint64_t* pool_key = (uint64_t*)(smem + RG_SLOTS * TILE_B);
-  uint32_t* pool_meta = (uint32_t*)(pool_key + RG_POOL);
-  int* qcnt = (int*)(pool_meta + RG_POOL);
+  int* qcnt = (int*)(pool_key + RG_POOL);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -402,7 +382,9 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   // lane i writes 16-B chunk P = 64p + i = (row r, position pos); its source is chunk
   // pos ^ (r & FM) of that row, so row r's logical chunk c lives at position c ^ (r & FM).
   // Per lane the (row, column byte) of each piece is loop-invariant.
-  const int64_t row_bytes = stride * ld * 2;
+  // sample levels read every stride-th row; the full level (LVL 1, 2) is the catalog itself
+  const int64_t strd = LVL == 0 ? stride : 1;
+  const int64_t row_bytes = strd * ld * 2;
   // source = wave-uniform tile base (SGPRs) + the lane's 32-bit offset within the tile
   uint32_t voff[PPW];
 #pragma unroll
@@ -443,20 +425,26 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
     if (j0 + (int64_t)(t + 1) * TR > j1) issue_t(t, std::true_type{});
     else issue_t(t, std::false_type{});
   };
-  // Candidate pool: each wave owns RG_WPOOL entries and the counters of its own queries, so
-  // appends need no atomics and no cross-wave synchronisation; the pool position `wn` is a
-  // wave-uniform (scalar) count.  Flush (rare): per-(query, slab) list slots are assigned by
-  // LDS atomics on the wave's own counters.  In-order LDS within a wave orders everything.
+  // Candidate pool: each wave owns RG_WPOOL 8-byte entries and the counters of its own queries,
+  // so appends need no atomics and no cross-wave synchronisation; the pool position `wn` is a
+  // wave-uniform (scalar) count.  Entry = (orderable score << 32) | (row offset in the slab's
+  // sample << QSH) | (query within the wave): one ds_write_b64 per candidate (the separate
+  // query word of the first version cost a second write and its address).  Flush (rare):
+  // per-(query, slab) list slots are assigned by LDS atomics on the wave's own counters, the
+  // global key (score, ~row) rebuilt.  In-order LDS within a wave orders everything.
   uint64_t* wkey = pool_key + w * RG_WPOOL;
-  uint32_t* wmeta = pool_meta + w * RG_WPOOL;
   uint32_t wn = 0;
   auto flush = [&]() __attribute__((always_inline)) {
     const int n = wn < (uint32_t)RG_WPOOL ? (int)wn : RG_WPOOL;
     for (int i = lane; i < n; i += 64) {
-      const uint32_t ql = wmeta[i];
-      const uint32_t slot_i = lds_add_rtn(lds_addr(&qcnt[ql]), 1u) & ~RG_OVF;
+      const uint64_t e = wkey[i];
+      const uint32_t lo = (uint32_t)e;
+      const uint32_t ql = (uint32_t)(w * QPW) + (lo & (QPW - 1));
+      const uint32_t slot_i = lds_add_rtn(lds_addr(&qcnt[ql]), 1u);
+      const uint32_t row = (uint32_t)((j0 + (int64_t)(lo >> QSH)) * strd);
       if (slot_i < (uint32_t)FL_CAP)
-        lists[((int64_t)(qt * QPB + (int)ql) * n_slabs + slab) * FL_CAP + slot_i] = wkey[i];
+        lists[((int64_t)(qt * QPB + (int)ql) * n_slabs + slab) * FL_CAP + slot_i] =
+            (e & 0xffffffff00000000ull) | (uint64_t)(~row);
     }
     wn = 0;
   };
@@ -484,23 +472,21 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
       mx[b] = m;
     }
   };
+  // orderable 32-bit image of a passing (so not NaN) score; -0 -> +0
+  auto okey = [](float v) __attribute__((always_inline)) {
+    const uint32_t u = __float_as_uint(v + 0.0f);
+    return u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u);
+  };
+  // the lane's part of a pool entry's low word: row 4g (+16 rb + jj) of the tile, query col
+  const uint32_t lo_lane = ((uint32_t)(4 * g) << QSH) | (uint32_t)col;
   // Append the passing scores of tile t (lane: rows jt + 16rb + 4g + jj, query 16b + col).
-  // One v_cmp + scalar branch per candidate slot; lanes of a non-empty slot write at
-  // wn + (passing lanes below).  An entry past the wave's pool marks its query overflowed
-  // (-> exact fallback).  Rows past the slab end (its last tile only) are masked to -inf first.
-  auto append = [&](f32x4 (&sc)[RB][QB], const float (&mx)[QB], int t, int b_lo,
-                    int b_hi, int rb_lo, int rb_hi) __attribute__((always_inline)) {
-    const int64_t jt = j0 + (int64_t)t * TR;
-    if (b_lo == 0 && rb_lo == 0 && jt + TR > j1) {
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj)
-          if (jt + 16 * rb + 4 * g + jj >= j1)
-#pragma unroll
-            for (int b = 0; b < QB; ++b) sc[rb][b][jj] = -__builtin_huge_valf();
-    }
-    const uint32_t rlane = (uint32_t)((jt + 4 * g) * stride);
+  // One v_cmp + scalar branch per candidate slot; the lanes of a non-empty slot write at
+  // wn + (passing lanes below).  The pool is flushed first if this block's scan could overrun
+  // it (rare), so the writes carry no bounds check.  Rows past the slab end were set to -inf
+  // when the tile finished.
+  auto append = [&](const f32x4 (&sc)[RB][QB], const float (&mx)[QB], int t, int b_lo,
+                    int b_hi) __attribute__((always_inline)) {
+    const uint32_t lo_tile = lo_lane + ((uint32_t)(t * TR) << QSH);
 #pragma unroll
     for (int b = 0; b < QB; ++b) {
       if (b < b_lo || b >= b_hi) continue;
@@ -509,28 +495,19 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
         asm volatile("" ::: "memory");
         continue;
       }
-      const uint32_t ql = (uint32_t)(w * QPW + 16 * b + col);
+      if (wn > (uint32_t)RG_WFLUSH) flush();
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
-          if (rb < rb_lo || rb >= rb_hi) continue;
           const float v = sc[rb][b][jj];
           const uint64_t bm = __ballot(v >= th[b]);
           if (bm != 0ull) {
-            const uint32_t pos =
-                wn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
-                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
             if (!TT_EXP_NOWRITE && v >= th[b]) {
-              if (pos < (uint32_t)RG_WPOOL) {
-                const uint32_t u = __float_as_uint(v + 0.0f);  // not NaN: it passed
-                const uint32_t key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-                const uint32_t r = rlane + (uint32_t)((16 * rb + jj) * stride);
-                lds_write64(lds_addr(&wkey[pos]), ((uint64_t)key << 32) | (uint64_t)(~r));
-                lds_write32(lds_addr(&wmeta[pos]), ql);
-              } else {
-                lds_or(lds_addr(&qcnt[ql]), RG_OVF);
-              }
+              const uint32_t pos = __builtin_amdgcn_mbcnt_hi(
+                  (uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, wn));
+              const uint32_t lo = lo_tile + ((uint32_t)(16 * rb + jj) << QSH) + 16u * b;
+              lds_write64(lds_addr(&wkey[pos]), ((uint64_t)okey(v) << 32) | lo);
             }
             wn += (uint32_t)__popcll(bm);
           }
@@ -545,7 +522,8 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   // query block instead of 8 ballot rounds; at the stride-16 level ~95% of (tile, block)
   // pairs held a candidate.
   auto append_tmax = [&](const float (&mx)[QB], int t, int b_lo, int b_hi) __attribute__((always_inline)) {
-    const uint32_t r = (uint32_t)((j0 + (int64_t)t * TR) * stride);
+    const uint32_t lo_t = ((uint32_t)(t * TR) << QSH) | (uint32_t)col;
+    if (wn > (uint32_t)RG_WFLUSH) flush();  // <= 16 entries per block follow
 #pragma unroll
     for (int b = 0; b < QB; ++b) {
       if (b < b_lo || b >= b_hi) continue;
@@ -555,20 +533,9 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
       const bool in = g == 0 && m >= th[b];
       const uint64_t bm = __ballot(in);
       if (bm == 0ull) continue;
-      const uint32_t pos =
-          wn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
-                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
-      if (in) {
-        const uint32_t ql = (uint32_t)(w * QPW + 16 * b + col);
-        if (pos < (uint32_t)RG_WPOOL) {
-          const uint32_t u = __float_as_uint(m + 0.0f);
-          const uint32_t key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-          lds_write64(lds_addr(&wkey[pos]), ((uint64_t)key << 32) | (uint64_t)(~r));
-          lds_write32(lds_addr(&wmeta[pos]), ql);
-        } else {
-          lds_or(lds_addr(&qcnt[ql]), RG_OVF);
-        }
-      }
+      const uint32_t pos = __builtin_amdgcn_mbcnt_hi(
+          (uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, wn));
+      if (in) lds_write64(lds_addr(&wkey[pos]), ((uint64_t)okey(m) << 32) | (lo_t + 16u * b));
       wn += (uint32_t)__popcll(bm);
     }
   };
@@ -591,11 +558,14 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   // FD + 1 divides KS (the ring index is s % (FD + 1)); 2 steps ahead where registers are tight
   constexpr int FD = (EP >= 384 && KS % 3 == 0) ? 2 : (KS >= 4 ? 3 : 1);
   constexpr int S_MID = (KS - FD) / 2;
-  constexpr int SPLIT_SP1 = TT_SPLIT_STEP > 0 ? TT_SPLIT_STEP : KS / QB;         // see below
-  constexpr int SPLIT_SP2 = TT_SPLIT_STEP > 0 ? TT_SPLIT_STEP : KS / (QB * RB);
-  // TT_SPLIT_START > 1: the per-query-block pieces start at that step instead of step 1
-  constexpr bool SPLIT_MOVED = TT_SPLIT_START > 1 && TT_SPLIT_APPEND == 1 && LVL != 0 &&
-                               QB > 1 && TT_SPLIT_START + (QB - 1) * SPLIT_SP1 < KS;
+  // Candidate scan of tile t-1 in one piece per query block, spread between tile t's MFMAs:
+  // block P at step S0 + P * KS / QB (batched full level 6.81 -> 6.65 ms against all blocks at
+  // step 1; S0 = 2 vs 1: 6.72 -> 6.64 ms; finer pieces and other spacings measured slower).
+  // Sample levels append their tile maxima at step 1.
+  constexpr int SP = KS / QB;
+  constexpr int S0 = LVL == 0 ? 1
+                     : (QB > 1 && 2 + (QB - 1) * SP < KS) ? 2
+                     : (QB > 1 && 1 + (QB - 1) * SP < KS) ? 1 : -1;  // -1: every block at step 1
   static_assert(KS % (FD + 1) == 0 && S_MID < KS - FD, "fragment ring layout");
   for (int t = 0; t < RG_PD && t < n_tiles; ++t) issue(t);
   wait_tiles(n_tiles - 1 < RG_PD - 1 ? n_tiles - 1 : RG_PD - 1);
@@ -688,64 +658,47 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
             if (!TT_EXP_NOBAR) asm volatile("s_barrier" ::: "memory");
             if (!TT_EXP_NODMA && t + RG_PD < n_tiles) issue(t + RG_PD);
           }
-          // TT_SPLIT_APPEND: query block b's candidate scan at step 1 + b * KS / QB (spread
-          // between the MFMAs) instead of all blocks at step 1
-          // Candidate scan of tile t-1 in pieces spread between tile t's MFMAs: piece P at step
-          // 1 + P * SP (TT_SPLIT_APPEND 1: one query block per piece; 2: one (query block, row
-          // block) per piece); piece 0 runs at step 1 below.
-          constexpr int NP = TT_SPLIT_APPEND == 2 ? QB * RB : QB;  // pieces per tile
-          constexpr int SP = TT_SPLIT_STEP > 0 ? TT_SPLIT_STEP : (NP > 0 ? KS / NP : 1);
-          if constexpr (SPLIT_MOVED && s >= TT_SPLIT_START && (s - TT_SPLIT_START) % SPLIT_SP1 == 0 &&
-                        (s - TT_SPLIT_START) / SPLIT_SP1 < QB) {
-            constexpr int P = (s - TT_SPLIT_START) / SPLIT_SP1;
-            if (!TT_EXP_NOSEL) append(accp, mx, t - 1, P, P + 1, 0, RB);
-          }
-          if constexpr (!SPLIT_MOVED && TT_SPLIT_APPEND && NP > 1 && 1 + (NP - 1) * SP < KS &&
-                        s > 1 && (s - 1) % SP == 0 && (s - 1) / SP < NP) {
-            constexpr int P = (s - 1) / SP;
-            if (!TT_EXP_NOSEL) {
-              if constexpr (LVL == 0 && !TT_EXP_SAMPLE_ROWS) {
-                if constexpr (TT_SPLIT_TMAX && TT_SPLIT_APPEND == 1) append_tmax(mx, t - 1, P, P + 1);
-              } else if constexpr (TT_SPLIT_APPEND == 2)
-                append(accp, mx, t - 1, P / RB, P / RB + 1, P % RB, P % RB + 1);
-              else
-                append(accp, mx, t - 1, P, P + 1, 0, RB);
+          if constexpr (LVL == 0 || S0 < 0) {
+            if constexpr (s == 1) {  // early: tile t-1's scores die before the peak
+              if constexpr (LVL == 0) {
+                if (!TT_EXP_NOSEL) append_tmax(mx, t - 1, 0, QB);
+              } else {
+                if (!TT_EXP_NOSEL) append(accp, mx, t - 1, 0, QB);
+              }
             }
+          } else if constexpr (s >= S0 && (s - S0) % SP == 0 && (s - S0) / SP < QB) {
+            constexpr int P = (s - S0) / SP;
+            if (!TT_EXP_NOSEL) append(accp, mx, t - 1, P, P + 1);
           }
-          if constexpr (s == (KS > 1 ? 1 : 0)) {  // early: tile t-1's scores die before the peak
-            if (!TT_EXP_NOSEL) {
-              if constexpr (LVL == 0 && !TT_EXP_SAMPLE_ROWS)
-                append_tmax(mx, t - 1, 0,
-                            (TT_SPLIT_TMAX && TT_SPLIT_APPEND == 1 && QB > 1 &&
-                             1 + (QB - 1) * SPLIT_SP1 < KS) ? 1 : QB);
-              else if constexpr (SPLIT_MOVED) {
-              } else if constexpr (TT_SPLIT_APPEND == 2 && QB * RB > 1 &&
-                                 1 + (QB * RB - 1) * SPLIT_SP2 < KS)
-                append(accp, mx, t - 1, 0, 1, 0, 1);
-              else if constexpr (TT_SPLIT_APPEND == 1 && QB > 1 && 1 + (QB - 1) * SPLIT_SP1 < KS)
-                append(accp, mx, t - 1, 0, 1, 0, RB);
-              else append(accp, mx, t - 1, 0, QB, 0, RB);
-            }
-            if (TT_EXP_NOSEL) {
+          if (TT_EXP_NOSEL && s == 1) {
 #pragma unroll
-              for (int b = 0; b < QB; ++b)
-                if (mx[b] >= th[b]) asm volatile("" ::: "memory");
-            }
+            for (int b = 0; b < QB; ++b)
+              if (mx[b] >= th[b]) asm volatile("" ::: "memory");
           }
         });
-        if (wn >= (uint32_t)RG_WFLUSH) flush();
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
           for (int b = 0; b < QB; ++b) accp[rb][b] = acc[rb][b];
+        // the slab's last tile (full level): rows past j1 are clamped DMA copies of row j1 - 1
+        if (LVL != 0 && j0 + (int64_t)(t + 1) * TR > j1) {
+          const int lim = (int)(j1 - (j0 + (int64_t)t * TR));
+#pragma unroll
+          for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
+              if (16 * rb + 4 * g + jj >= lim)
+#pragma unroll
+                for (int b = 0; b < QB; ++b) accp[rb][b][jj] = -__builtin_huge_valf();
+        }
       }
     });
   }
   if (n_tiles > 0 && !TT_EXP_NOSEL) {
     float mx[QB];
     tile_max(accp, mx);
-    if constexpr (LVL == 0 && !TT_EXP_SAMPLE_ROWS) append_tmax(mx, n_tiles - 1, 0, QB);
-    else append(accp, mx, n_tiles - 1, 0, QB, 0, RB);
+    if constexpr (LVL == 0) append_tmax(mx, n_tiles - 1, 0, QB);
+    else append(accp, mx, n_tiles - 1, 0, QB);
   }
   wait_vm<0>();
   flush();
@@ -755,7 +708,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
     if (qi < nq) {
       const uint32_t c = (uint32_t)qcnt[w * QPW + i];
       counts[(int64_t)qi * n_slabs + slab] =
-          (c & RG_OVF) || c > (uint32_t)FL_CAP ? FL_CAP + 1 : (int)c;
+          c > (uint32_t)FL_CAP ? FL_CAP + 1 : (int)c;
     }
   }
 }
@@ -1930,6 +1883,8 @@ static FilterPlan plan_filter(int64_t n, int nq, int k, int ep) {
       sl = ring_slabs(L.n_qt, L.n_sample);
     }
     if (sl < 1) sl = 1;
+    // k_filter_ring's pool entries hold a row offset within the slab in 32 - 5 bits
+    if (!L.dense && sl < ((L.n_sample + (1 << 26) - 1) >> 26)) sl = (L.n_sample + (1 << 26) - 1) >> 26;
     int64_t r = (L.n_sample + sl - 1) / sl;
     r = (r + 63) / 64 * 64;
     L.rows_per_slab = (int)r;
