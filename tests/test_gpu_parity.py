@@ -95,6 +95,11 @@ BF16_CASES = [c for c in SCAN_CASES if c[3] <= 128] + [
     (60000, 768, 33, 100),   # E = 768 (one query block per wave)
     (20000, 384, 300, 100),  # several query tiles
     (40000, 512, 9, 64),
+    # small batches (block-per-query selection): ragged sizes, every E
+    (65600, 384, 1, 100),
+    (250001, 768, 7, 128),   # E = 768, k at the maximum
+    (130000, 64, 256, 100),  # the largest coarse batch
+    (99999, 512, 2, 1),
 ]
 
 
@@ -154,12 +159,13 @@ def test_bf16_filter_exact_under_biased_rounding(K, oracle_mod):
     assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
 
 
-def test_bf16_filter_no_fallback_on_iid_data(K):
+@pytest.mark.parametrize("nq", [1, 16, 256, 300])
+def test_bf16_filter_no_fallback_on_iid_data(K, nq):
     """The optimistic threshold must hold on iid data: no query may need the exact fallback
-    (a performance property: fallbacks are correct but slow)."""
+    (a performance property: fallbacks are correct but slow).  nq <= 256: the small path."""
     from twotower import _lib
 
-    n, d, nq, k = 400000, 384, 300, 100
+    n, d, k = 1000000, 384, 100
     g = torch.Generator(device="cuda").manual_seed(5)
     db = torch.randn((n, d), generator=g, device="cuda")
     K.l2norm_rows(db, d, 0, out=db)
@@ -187,6 +193,22 @@ def test_bf16_filter_fallback_is_exact(K, oracle_mod, resid):
     rs, ri = oracle_mod.scan_topk(x, q, k)
     assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
     assert K.filter_fallback_count(ws, n, d, nq, k) == nq  # every query took the fallback
+
+
+@pytest.mark.parametrize("nq", [1, 5, 64])
+def test_bf16_filter_small_batch_clustered(K, oracle_mod, nq):
+    """Small batches on clustered data: tight clusters can push a query's full level past the
+    small path's candidate cap -> exact fallback; the results stay bit-exact either way."""
+    rng = np.random.default_rng(90 + nq)
+    base = oracle_mod.l2norm_rows(rng.standard_normal((300, 384)).astype(np.float32), 0)
+    x = np.repeat(base, 400, axis=0) + rng.standard_normal((120000, 384)).astype(np.float32) * 0.05
+    x = oracle_mod.l2norm_rows(x, 0)
+    q = oracle_mod.l2norm_rows(base[:nq] + rng.standard_normal((nq, 384)).astype(np.float32) * 0.02, 0)
+    db = dev_rows(x)
+    db16 = db.to(torch.bfloat16)
+    s, i = K.scan_topk_bf16(db, db16, x.shape[0], 384, dev_rows(q), 100, bounds(K, db, db16, 384))
+    rs, ri = oracle_mod.scan_topk(x, q, 100)
+    assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
 
 
 def test_bf16_filter_clusters_and_ties(K, oracle_mod):

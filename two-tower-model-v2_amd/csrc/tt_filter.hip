@@ -9,9 +9,10 @@
 //   |a(r) - s(r)| <= eps_q, computed per query by k_query_eps from the catalog bounds
 //   X >= max||x_r||, R >= max||x_r - bf16(x_r)|| (tt_bf16_image_bounds):
 //     x.q - x~.q~ = (x - x~).q + x~.(q - q~)          (Cauchy-Schwarz on both terms)
-//     eps_q = R|q| + (X+R)|q - q~| + 2E 2^-24 (X+R)|q~| + E 2^-24 X|q|      (x 1.001)
-//   The last two terms bound the f32 accumulation of a (any order, 2 roundings per add
-//   allowed) and of the canonical fma chain s over E = padded-dim terms.  Using the measured
+//     eps_q = R|q| + (X+R)|q - q~| + 2E 2^-23 (X+R)|q~| + E 2^-24 X|q|      (x 1.001)
+//   The last two terms bound the f32 accumulation of a (any order, 2 roundings per add, each
+//   faithful -- the MFMA's internal rounding mode is not specified, so 2^-23 not 2^-24) and of
+//   the canonical fma chain s (round to nearest) over E = padded-dim terms.  Using the measured
 //   rounding residuals instead of the worst case u = 2^-8 per operand keeps eps ~2x tighter
 //   for real data while staying a bound.
 //
@@ -321,6 +322,33 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// 2 eps_q from the query's squared norms |q|^2, |q~|^2, |q - q~|^2 (any summation order: the
+// growth factor covers it).  The last two terms bound the f32 accumulations: E 2^-24 X|q| the
+// canonical fma chain of s (v_fma_f32 / fmaf, round to nearest), 2E 2^-23 (X+R)|q~| the
+// MFMA's accumulation of a, whose internal rounding is not specified: any faithful rounding
+// (error < 1 ulp = 2^-23 relative, round-toward-zero included), two roundings per addition.
+template <int EP>
+__device__ __forceinline__ float query_eps2(float sq, float st, float sr, float X, float R) {
+  const float grow = 1.0f + (float)(EP + 2) * 1.1920929e-07f, up = 1.0f + 2.4e-7f;
+  const float nq_ = sqrtf(sq * grow) * up, nt = sqrtf(st * grow) * up, nr = sqrtf(sr * grow) * up;
+  const float g24 = (float)EP * 5.9604645e-08f * 1.01f;  // E 2^-24 (first order + slack)
+  const float g23 = 2.0f * g24;                           // E 2^-23
+  const float e = R * nq_ + (X + R) * nr + 2.0f * g23 * (X + R) * nt + g24 * X * nq_;
+  const float r = 2.0f * e * 1.001f;
+  return r == r ? r : __builtin_huge_valf();  // a NaN query: widest band (never returned)
+}
+
+// Per-query filter state, initialised by the first level of a search (k_query_eps's work,
+// folded into that launch): eps2 from the catalog bounds X, R; aref = -inf; flags = 0;
+// *qsel_n = 0.  eps2 == nullptr: a later level (theta read from the previous selection).
+struct QueryInit {
+  float X, R;
+  float* eps2;
+  float* aref;
+  int* flags;
+  int* qsel_n;
+};
+
 // LVL: 0 = a sample level, 1 = the full-catalog (last) level of a large query batch
 // (> RG_SMALL_NQ queries), 2 = the full level of a small batch -- separate instantiations of
 // the same code so that profiles attribute the dominant launch (bench.py's roofline kernel,
@@ -331,7 +359,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
     const uint16_t* __restrict__ xb, int64_t ld, const float* __restrict__ q, int nq,
     int64_t ldq, const float* __restrict__ theta, int64_t stride, int64_t n_sample,
     int rows_per_slab, int n_slabs, int n_qt, uint64_t* __restrict__ lists,
-    int* __restrict__ counts) {
+    int* __restrict__ counts, QueryInit qinit) {
   constexpr int TR = RingCfg<EP>::TR, QB = RingCfg<EP>::QB;
   constexpr int KS = EP / 32, QPW = 16 * QB, QPB = RG_WAVES * QPW;
   constexpr int CPR = EP / 8;  // 16-B chunks per row
@@ -357,12 +385,14 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
 
   bf16x8 qf[QB][KS];
   float th[QB];
+  const bool init = qinit.eps2 != nullptr;  // first level: theta = -inf, query state set here
 #pragma unroll
   for (int b = 0; b < QB; ++b) {
     const int qi = qbase + 16 * b + col;
     const bool v = qi < nq;
-    th[b] = v ? theta[qi] : __builtin_huge_valf();
+    th[b] = !v ? __builtin_huge_valf() : init ? -__builtin_huge_valf() : theta[qi];
     const float* qp = q + (int64_t)(v ? qi : 0) * ldq + 8 * g;
+    float sq = 0.0f, st = 0.0f, sr = 0.0f;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const f32x4 v0 = *(const f32x4*)(qp + 32 * s);
@@ -370,6 +400,31 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
       u32x4 u = {pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]), pack_bf16x2(v1[0], v1[1]),
                  pack_bf16x2(v1[2], v1[3])};
       qf[b][s] = __builtin_bit_cast(bf16x8, u);
+      if (init && slab == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float x = i < 4 ? v0[i] : v1[i - 4];
+          const uint32_t h = (u[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+          const float xt = __uint_as_float(h << 16);
+          sq = fmaf(x, x, sq);
+          st = fmaf(xt, xt, st);
+          sr = fmaf(x - xt, x - xt, sr);
+        }
+      }
+    }
+    if (init && slab == 0) {  // lanes col, col+16, col+32, col+48 hold the query's 4 parts
+      sq += __shfl_xor(sq, 16, 64);
+      st += __shfl_xor(st, 16, 64);
+      sr += __shfl_xor(sr, 16, 64);
+      sq += __shfl_xor(sq, 32, 64);
+      st += __shfl_xor(st, 32, 64);
+      sr += __shfl_xor(sr, 32, 64);
+      if (v && g == 0) {
+        qinit.eps2[qi] = query_eps2<EP>(sq, st, sr, qinit.X, qinit.R);
+        qinit.aref[qi] = -__builtin_huge_valf();
+        qinit.flags[qi] = 0;
+        if (qi == 0) *qinit.qsel_n = 0;
+      }
     }
   }
   for (int i = tid; i < QPB; i += 64 * RG_WAVES) qcnt[i] = 0;
@@ -1275,10 +1330,11 @@ TT_CHECK_EXP(TT_EXP_SMALL_TIMING, "TT_EXP_SMALL_TIMING (printf)");
 #endif
 constexpr int SM_THREADS = 1024, SM_WAVES = SM_THREADS / 64;
 constexpr int SM_NQ = 256;
-constexpr int SM_PER = SW_CAP / SM_THREADS;  // keys per thread in the radix select
+constexpr int SM_CAP = SW_CAP;  // candidates per query the small path selects from
+constexpr int SM_PER = SM_CAP / SM_THREADS;  // keys per thread in the radix select
 
 struct SmallLds {
-  uint64_t key[SW_CAP];   // the query's candidate keys (orderable score << 32 | ~row)
+  uint64_t key[SM_CAP];   // the query's candidate keys (orderable score << 32 | ~row)
   int wred[SM_WAVES];
   int hist[256];
   int pick[2];
@@ -1286,7 +1342,7 @@ struct SmallLds {
 };
 
 // Gather the query's per-slab candidate lists into s.key (n_slabs <= SM_THREADS).  Returns
-// the candidate count, or -1 when a list overflowed / the total exceeds SW_CAP.
+// the candidate count, or -1 when a list overflowed / the total exceeds SM_CAP.
 __device__ int small_collect(const uint64_t* __restrict__ lists, const int* __restrict__ counts,
                              int n_slabs, int qid, SmallLds& s) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1306,7 +1362,7 @@ __device__ int small_collect(const uint64_t* __restrict__ lists, const int* __re
     base += i < w ? v : 0;
     total += v;
   }
-  if (over || total > SW_CAP) return -1;
+  if (over || total > SM_CAP) return -1;
   const uint64_t* l = lists + ((int64_t)qid * n_slabs + tid) * FL_CAP;
   const int e0 = base + incl - c;
 #pragma unroll 4
@@ -1750,14 +1806,7 @@ __global__ __launch_bounds__(256) void k_query_eps(const float* __restrict__ q, 
     st += __shfl_xor(st, o, 64);
     sr += __shfl_xor(sr, o, 64);
   }
-  if (lane == 0) {
-    const float grow = 1.0f + (float)(EP + 2) * 1.1920929e-07f, up = 1.0f + 2.4e-7f;
-    const float nq_ = sqrtf(sq * grow) * up, nt = sqrtf(st * grow) * up, nr = sqrtf(sr * grow) * up;
-    const float g = (float)EP * 5.9604645e-08f * 1.01f;  // E 2^-24 (first order + slack)
-    const float e = R * nq_ + (X + R) * nr + 2.0f * g * (X + R) * nt + g * X * nq_;
-    const float r = 2.0f * e * 1.001f;
-    eps2[qi] = r == r ? r : __builtin_huge_valf();  // a NaN query: widest band (never returned)
-  }
+  if (lane == 0) eps2[qi] = query_eps2<EP>(sq, st, sr, X, R);
 }
 
 __global__ void k_sub_arr(float* x, const float* y, int n) {
@@ -1774,6 +1823,7 @@ struct Level {
 
 struct FilterPlan {
   int n_levels, max_slabs, J;
+  bool small;  // block-per-query selection path (k_select_small / k_final_small)
   Level lv[8];
 };
 
@@ -1891,6 +1941,8 @@ static FilterPlan plan_filter(int64_t n, int nq, int k, int ep) {
     L.n_slabs = (int)((L.n_sample + r - 1) / r);
     if (L.n_slabs > p.max_slabs) p.max_slabs = L.n_slabs;
   }
+  p.small = nq <= SM_NQ && !select_reg_disabled();
+  for (int i = 0; i < nl; ++i) p.small = p.small && p.lv[i].n_slabs <= SM_THREADS;
   return p;
 }
 
@@ -1946,7 +1998,7 @@ static FilterWs carve(void* base, const FilterPlan& p, int64_t n, int d, int nq,
 template <int EP>
 static void launch_level(const Level& L, const uint16_t* xb, int64_t n, int64_t ld,
                          const float* q, int nq, int64_t ldq, const FilterWs& w,
-                         hipStream_t st) {
+                         hipStream_t st, const QueryInit& qi) {
   const int nblk = L.n_qt * L.n_slabs;
   if (L.dense) {
     constexpr int QB = EP <= 384 ? 2 : 1;
@@ -1959,7 +2011,7 @@ static void launch_level(const Level& L, const uint16_t* xb, int64_t n, int64_t 
                                    : k_filter_ring<EP, 2>;
     hipLaunchKernelGGL(kern, dim3(nblk), dim3(64 * RG_WAVES), 0, st, xb, ld, q, nq, ldq, w.theta,
                        L.stride, L.n_sample, L.rows_per_slab, L.n_slabs, L.n_qt, w.lists,
-                       w.counts);
+                       w.counts, qi);
   }
 }
 
@@ -2020,10 +2072,18 @@ int filter_setup(const float* db, const uint16_t* db_bf16, int64_t n, int32_t d,
   return TT_OK;
 }
 
+// Per-query state (eps2, theta, aref, flags, qsel_n).  fold != nullptr and a ring first level
+// (the tmax-first plan): that launch initialises it (*fold filled in, no launch here).
 int filter_init(const FilterWs& w, const float* q, int nq, int64_t ld_q, int ep, float x_norm_max,
-                float x_resid_max, hipStream_t st) {
+                float x_resid_max, hipStream_t st, const FilterPlan* p = nullptr,
+                QueryInit* fold = nullptr) {
   TT_REQUIRE(x_norm_max >= 0.0f && x_resid_max >= 0.0f,
              "x_norm_max / x_resid_max must be >= 0 (tt_bf16_image_bounds)");
+  if (fold) *fold = QueryInit{0.0f, 0.0f, nullptr, nullptr, nullptr, nullptr};
+  if (fold && p && !p->lv[0].dense && p->n_levels > 1) {
+    *fold = QueryInit{x_norm_max, x_resid_max, w.eps2, w.aref, w.flags, w.qsel_n};
+    return TT_OK;
+  }
   // one launch: k_query_eps also resets flags / theta / aref / qsel_n (was a memset + 2 fills)
   const unsigned eps_grid = (unsigned)((nq + 3) / 4);
   switch (ep) {
@@ -2043,18 +2103,19 @@ int filter_level(const FilterPlan& p, const FilterWs& w, int li, int mode, const
                  int64_t n, int64_t ld_db, const float* q, int nq, int64_t ld_q, int k, int ep,
                  hipStream_t st, void* ev_start, void* ev_stop, const float* stats = nullptr,
                  int* pcount = nullptr, float* smax_out = nullptr, int fin = 0,
-                 bool no_select = false) {
+                 bool no_select = false,
+                 const QueryInit& qi = QueryInit{0.0f, 0.0f, nullptr, nullptr, nullptr, nullptr}) {
   const Level& L = p.lv[li];
   const bool last = li == p.n_levels - 1;
   if (last && ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "hipEventRecord(start)");
   switch (ep) {
-    case 64: launch_level<64>(L, db16, n, ld_db, q, nq, ld_q, w, st); break;
-    case 128: launch_level<128>(L, db16, n, ld_db, q, nq, ld_q, w, st); break;
-    case 256: launch_level<256>(L, db16, n, ld_db, q, nq, ld_q, w, st); break;
-    case 384: launch_level<384>(L, db16, n, ld_db, q, nq, ld_q, w, st); break;
-    case 512: launch_level<512>(L, db16, n, ld_db, q, nq, ld_q, w, st); break;
-    case 768: launch_level<768>(L, db16, n, ld_db, q, nq, ld_q, w, st); break;
+    case 64: launch_level<64>(L, db16, n, ld_db, q, nq, ld_q, w, st, qi); break;
+    case 128: launch_level<128>(L, db16, n, ld_db, q, nq, ld_q, w, st, qi); break;
+    case 256: launch_level<256>(L, db16, n, ld_db, q, nq, ld_q, w, st, qi); break;
+    case 384: launch_level<384>(L, db16, n, ld_db, q, nq, ld_q, w, st, qi); break;
+    case 512: launch_level<512>(L, db16, n, ld_db, q, nq, ld_q, w, st, qi); break;
+    case 768: launch_level<768>(L, db16, n, ld_db, q, nq, ld_q, w, st, qi); break;
     default: return fail(TT_ERR_UNSUPPORTED, "bad padded dim");
   }
   int rc = check_launch("k_filter");
@@ -2119,18 +2180,19 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
                         &p, &w);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
-  if ((rc = filter_init(w, q, nq, ld_q, ep, x_norm_max, x_resid_max, st))) return rc;
+  QueryInit qinit;
+  if ((rc = filter_init(w, q, nq, ld_q, ep, x_norm_max, x_resid_max, st, &p, &qinit))) return rc;
   // small batches: block-per-query selection (k_select_small) and a fused selection +
   // f32-MFMA re-rank of the full level (k_final_small)
-  bool small = nq <= SM_NQ && !select_reg_disabled();
-  for (int li = 0; li < p.n_levels; ++li) small = small && p.lv[li].n_slabs <= SM_THREADS;
+  const bool small = p.small;
   for (int li = 0; li < p.n_levels; ++li) {
     const bool last = li == p.n_levels - 1;
     // the last sample level's selection writes the full level's threshold a_J - 2 eps itself
     // (was a copy + k_sub_arr launch: full_threshold, kept for the sharded protocol)
     const int fin = li == p.n_levels - 2;
     if ((rc = filter_level(p, w, li, last ? 1 : 0, db_bf16, n, ld_db, q, nq, ld_q, k, ep, st,
-                           ev_start, ev_stop, nullptr, nullptr, nullptr, fin, small)))
+                           ev_start, ev_stop, nullptr, nullptr, nullptr, fin, small,
+                           li == 0 ? qinit : QueryInit{0.0f, 0.0f, nullptr, nullptr, nullptr, nullptr})))
       return rc;
     if (small && !last) {
       hipLaunchKernelGGL(k_select_small, dim3(nq), dim3(SM_THREADS), 0, st, w.lists, w.counts,

@@ -146,6 +146,45 @@ def scan_topk_bf16(db: torch.Tensor, db16: torch.Tensor, n: int, d: int, q: torc
     return out
 
 
+class PreparedSearch:
+    """scan_topk_bf16 for a fixed (catalog, nq, k): validation, workspace, output buffers and
+    the C arguments are set up once, so a call is one ctypes call (the serving pattern: the
+    /retrieve path searches one buyer at a time, server.py:241-244 -> vector_db.py:160).
+
+    Returns the same (scores, ids) tensors on every call (overwritten in place)."""
+
+    def __init__(self, db: torch.Tensor, db16: torch.Tensor, n: int, d: int, nq: int, k: int,
+                 bounds, row_base: int = 0):
+        _check_2d(db, "db")
+        _check_2d(db16, "db16", torch.bfloat16)
+        if db16.shape[0] < n or db16.stride(0) != db.stride(0):
+            raise ValueError("db16 must be the bf16 image of db (same rows and leading dim)")
+        if not (1 <= k <= min(n, FILTER_KMAX)) or n > db.shape[0] or nq < 1:
+            raise ValueError(f"PreparedSearch: need nq >= 1, 1 <= k ({k}) <= min(n, 128)")
+        self.db, self.db16, self.nq, self.d = db, db16, nq, d
+        dev = db.device
+        self.out = (torch.empty((nq, k), dtype=_f32, device=dev),
+                    torch.empty((nq, k), dtype=torch.int64, device=dev))
+        self.ws = torch.empty(filter_workspace_bytes(n, d, nq, k), dtype=torch.uint8, device=dev)
+        self.ld_q = _lib.padded_dim(d)
+        self._fn = lib().tt_scan_topk_bf16f32
+        x_norm_max, x_resid_max = (float(v) for v in bounds)
+        self._head = (_ptr(db), _ptr(db16), n, d, db.stride(0), row_base)
+        self._tail = (k, ctypes.c_float(x_norm_max), ctypes.c_float(x_resid_max),
+                      _ptr(self.out[0]), _ptr(self.out[1]), _ptr(self.ws), self.ws.numel())
+
+    def __call__(self, q: torch.Tensor):
+        if (q.shape != (self.nq, self.ld_q) or q.dtype != _f32 or q.device != self.db.device
+                or not q.is_contiguous()):
+            raise ValueError(f"PreparedSearch: q must be a contiguous f32 [{self.nq}, "
+                             f"{self.ld_q}] tensor on {self.db.device}")
+        rc = self._fn(*self._head, q.data_ptr(), self.nq, self.ld_q, *self._tail,
+                      torch.cuda.current_stream().cuda_stream, None, None)
+        if rc:
+            check(rc, "tt_scan_topk_bf16f32")
+        return self.out
+
+
 def sharded_sample(x16: torch.Tensor, n: int) -> torch.Tensor:
     """Rows 0, 16, 32, ... of a bf16 catalog image (the replicated sample of the sharded search)."""
     return x16[:n:_lib.TT_SHARD_SAMPLE_STRIDE].contiguous()
