@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import statistics
 import os
 import sys
 import time
@@ -193,6 +194,7 @@ def configs1(a, dev, rank):
         torch.cuda.empty_cache()
     # bf16 encoder vs the f32 (parity) encoder on the L2-normalised item embeddings
     # (item_tower.py:209): worst cosine distance over the first batch
+    y16, y32 = y16.detach(), y32.detach()
     cos = (y16 * y32).sum(dim=1)
     res["bf16_vs_f32_item_cosine"] = {"min_cos": float(cos.min()),
                                       "max_1_minus_cos": float((1 - cos).max()),
@@ -585,18 +587,33 @@ def main():
             e.record(stream)
         for _ in range(3):
             kernels.scan_topk_bf16(shard, shard16, hi - lo, E, q1, K, bounds, workspace=ws1)
-        n1, tot, lvl = 20, 0.0, 0.0
-        for _ in range(n1):
+        n1, tot, lvl = 21, [], []
+        for _ in range(n1):  # per-call wrapper (validation, output allocation every call)
             ev[2].record(stream)
             kernels.scan_topk_bf16(shard, shard16, hi - lo, E, q1, K, bounds, workspace=ws1,
                                    events=(ev[0], ev[1]))
             ev[3].record(stream)
             torch.cuda.synchronize()
-            tot += ev[2].elapsed_time(ev[3])
-            lvl += ev[0].elapsed_time(ev[1])
-        lvl_ms = lvl / n1
+            tot.append(ev[2].elapsed_time(ev[3]))
+            lvl.append(ev[0].elapsed_time(ev[1]))
+        lvl_ms = statistics.median(lvl)
+        # the serving path (VectorDatabase.retrieve -> FlatIPIndex.search): a PreparedSearch
+        # bound once, one C call per buyer; median of 21 synchronised calls
+        ps = kernels.PreparedSearch(shard, shard16, hi - lo, E, 1, K, bounds, row_base=lo)
+        for _ in range(3):
+            ps(q1)
+        prep = []
+        for _ in range(n1):
+            ev[2].record(stream)
+            ps(q1)
+            ev[3].record(stream)
+            torch.cuda.synchronize()
+            prep.append(ev[2].elapsed_time(ev[3]))
+        del ps
         result["single_buyer_search"] = {
-            "nq": 1, "ms_per_search": tot / n1, "full_level_ms": lvl_ms,
+            "nq": 1, "ms_per_search": statistics.median(prep),
+            "timing": "median of 21 synchronised calls, HIP events on the launch stream",
+            "wrapper_ms_per_search": statistics.median(tot), "full_level_ms": lvl_ms,
             "full_level_bytes": 2.0 * (hi - lo) * ep,
             "achieved_hbm_gbps": 2.0 * (hi - lo) * ep / (lvl_ms * 1e-3) / 1e9,
             "hbm_peak_gbps": HBM_PEAK_GBPS,

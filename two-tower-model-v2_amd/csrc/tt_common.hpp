@@ -53,6 +53,14 @@ inline int env_switch(const char*, int dflt) { return dflt; }
 // ----------------------------------------------------------------------------- device utils
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// XCD-aware block id: blocks b and b+8 run on the same XCD (observed placement, speed only).
+// Give every XCD a contiguous range of logical ids so that blocks sharing data (the slabs of
+// a filter level, the heads of one sequence in attention) share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+  const int q = nblk / 8, r = nblk % 8, x = bid % 8, local = bid / 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + local;
+}
+
 // Orders LDS traffic between lanes of ONE wave (no workgroup barrier: waves of a block
 // run independent control flow in the scan kernel).
 __device__ __forceinline__ void wave_sync() {

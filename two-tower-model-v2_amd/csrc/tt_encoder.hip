@@ -1163,7 +1163,8 @@ __global__ __launch_bounds__(256) void k_attn32_mfma(const TI* __restrict__ qkv,
   extern __shared__ __attribute__((aligned(16))) char sm[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, ql = lane & 15;
-  const int sq = blockIdx.x / heads, h = blockIdx.x % heads;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);  // a sequence's heads on one XCD (see below)
+  const int sq = lb / heads, h = lb % heads;
   const int t0 = cu[sq], L = cu[sq + 1] - t0;
   const int Lk = (L + 31) & ~31;
   const int vst = ((Lk + 127) & ~127) + (BF ? 8 : 4);
@@ -1334,12 +1335,22 @@ __global__ __launch_bounds__(256) void k_attn32_bf16(const uint16_t* __restrict_
   extern __shared__ __attribute__((aligned(16))) char sm[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, ql = lane & 15;
-  const int sq = blockIdx.x / heads, h = blockIdx.x % heads;
+  // the heads of one sequence read 64-B halves of the same 128-B lines of qkv: keep them on
+  // one XCD (one L2) -- with the hardware's round-robin placement each XCD fetched every line
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int sq = lb / heads, h = lb % heads;
   const int t0 = cu[sq], L = cu[sq + 1] - t0;
   const int Lk = (L + 31) & ~31;
   const int vst = ((Lk + 127) & ~127) + 8;  // V^T row stride (bf16 elements)
   char* Ks = sm;
   char* Vt = sm + (size_t)Lk * KROW;
+  // this wave's first query fragment is loaded before the K/V staging, so its latency overlaps
+  // the staging loads instead of following the barrier (then one group ahead in the loop)
+  auto load_q = [&](int q0_) {
+    const int qr = q0_ + ql < L ? q0_ + ql : L - 1;
+    return *(const u32x4*)(qkv + (int64_t)(t0 + qr) * ldq + h * DH + 8 * g);
+  };
+  u32x4 qnext = load_q(16 * w < L ? 16 * w : 0);
   // K rows: 16-B chunks copied whole; V^T: lane pair of keys (2p, 2p+1) x 8 dims -> 8 dwords
   for (int e = tid; e < (Lk / 2) * 4; e += 256) {
     const int p = e >> 2, c8 = 8 * (e & 3), j = 2 * p;
@@ -1365,9 +1376,8 @@ __global__ __launch_bounds__(256) void k_attn32_bf16(const uint16_t* __restrict_
   __syncthreads();
   const float sl2 = scale * 1.4426950408889634f;  // scores in log2 units
   for (int q0 = 16 * w; q0 < L; q0 += 64) {
-    const int qr = q0 + ql < L ? q0 + ql : L - 1;
-    const bf16x8e qf = __builtin_bit_cast(
-        bf16x8e, *(const u32x4*)(qkv + (int64_t)(t0 + qr) * ldq + h * DH + 8 * g));
+    const bf16x8e qf = __builtin_bit_cast(bf16x8e, qnext);
+    if (q0 + 64 < L) qnext = load_q(q0 + 64);
     float m = -__builtin_huge_valf(), lsum = 0.0f;
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     for (int kc = 0; kc < Lk; kc += 32) {

@@ -58,12 +58,6 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return (uint32_t)f32_to_bf16_rne(lo) | ((uint32_t)f32_to_bf16_rne(hi) << 16);
 }
 
-// XCD-aware block id: blocks b and b+8 run on the same XCD (observed placement, speed only).
-// Give every XCD a contiguous range of logical ids so that its co-resident blocks share slabs.
-__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
-  const int q = nblk / 8, r = nblk % 8, x = bid % 8, local = bid / 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + local;
-}
 
 // --------------------------------------------------------------------------- filter
 // Block: FL_WAVES waves over the same slab rows; wave w owns QB*16 queries (B fragments of
@@ -1461,6 +1455,11 @@ __global__ __launch_bounds__(SM_THREADS) void k_select_small(
 // in one launch.  A_k = k-th best a; A_k < aref -> the optimistic threshold failed (flag);
 // band = candidates with a >= A_k - eps2 (<= BAND_CAP, else flag); exact canonical f32
 // scores of the band rows by f32 MFMA; sort (score desc, row asc); top-k out.
+// The band's row gathers (~180 random 1.5 KB rows per query) are memory-latency bound on one
+// CU: 9-14 us of the one-buyer search.  Measured and not adopted: splitting a query over 8
+// blocks that meet through a global counter (25-30 us: the agent-scope release/acquire that
+// makes one block's scores visible to another XCD writes back / invalidates L2), and the full
+// level touching its candidates' f32 rows as it flushes them (no change).
 template <int EP>
 __global__ __launch_bounds__(SM_THREADS) void k_final_small(
     const uint64_t* __restrict__ lists, const int* __restrict__ counts, int n_slabs, int k,
@@ -1472,7 +1471,9 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_small(
   __shared__ uint32_t brow[BAND_CAP];
   __shared__ uint64_t sbuf[BAND_CAP];
   __shared__ __attribute__((aligned(16))) float qs[EP];
-  const int qid = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  __shared__ int wcnt[SM_WAVES];
+  const int qid = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
 #if TT_EXP_SMALL_TIMING
   uint64_t tk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -1497,35 +1498,50 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_small(
     return;
   }
   const float thr = A - eps2[qid];
-  if (tid == 0) s.nb = 0;
   for (int i = tid; i < EP; i += SM_THREADS) qs[i] = q[(int64_t)qid * ldq + i];
-  __syncthreads();
+  // band positions by a block-wide prefix count (deterministic order)
+  int mine = 0;
 #pragma unroll
-  for (int j = 0; j < SM_PER; ++j) {
-    const int e = tid + j * SM_THREADS;
-    if (h[j] != 0u && key_float(h[j]) >= thr) {
-      const int pos = atomicAdd(&s.nb, 1);
-      if (pos < BAND_CAP) brow[pos] = key_row(s.key[e]);
-    }
+  for (int j = 0; j < SM_PER; ++j) mine += (h[j] != 0u && key_float(h[j]) >= thr) ? 1 : 0;
+  int incl = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    incl += lane >= o ? y : 0;
   }
+  if (lane == 63) wcnt[w] = incl;
   __syncthreads();
-  const int nb = s.nb;
+  int base = 0, nb = 0;
+#pragma unroll
+  for (int i = 0; i < SM_WAVES; ++i) {
+    base += i < w ? wcnt[i] : 0;
+    nb += wcnt[i];
+  }
   SM_TICK(3)
   if (nb > BAND_CAP) {
     if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
     return;
   }
-  // exact scores: wave w takes band rows [16 gi, 16 gi + 16), gi = w, w + SM_WAVES, ...  Lane
-  // (r, g) loads row r's dims 16t + 4g .. +3 for every t (all loads in flight) and the chain
-  // runs on v_mfma_f32_16x16x4_f32 with the query in every column: the canonical order
-  // (t, i, g), bit-identical to the f32 scan.  (Per-row VALU fma chains after an LDS
+  {
+    int pos = base + incl - mine;
+#pragma unroll
+    for (int j = 0; j < SM_PER; ++j) {
+      const int e = tid + j * SM_THREADS;
+      if (h[j] != 0u && key_float(h[j]) >= thr) brow[pos++] = key_row(s.key[e]);
+    }
+  }
+  __syncthreads();
+  // exact scores: wave w takes band rows [16 gr, 16 gr + 16), gr = w, w + SM_WAVES, ...  Lane
+  // (r, g) loads row r's dims 16t + 4g .. +3 for every t (all loads in flight) and
+  // the chain runs on v_mfma_f32_16x16x4_f32 with the query in every column: the canonical
+  // order (t, i, g), bit-identical to the f32 scan.  (Per-row VALU fma chains after an LDS
   // transpose: 0.182 vs 0.177 ms per one-buyer search, 0.292 vs 0.276 ms at 256 queries.)
   {
     const int r16 = lane & 15, g = lane >> 4;
     constexpr int NT = EP / 16, TCH = NT <= 24 ? NT : 16;  // t-steps per load batch
     static_assert(NT % TCH == 0, "load batches must tile the row");
-    for (int gi = w; 16 * gi < nb; gi += SM_WAVES) {
-      const int e = 16 * gi + r16;
+    for (int gr = w; 16 * gr < nb; gr += SM_WAVES) {
+      const int e = 16 * gr + r16;
       const uint32_t row = brow[e < nb ? e : nb - 1];
       const float* xr = db + (int64_t)row * ld + 4 * g;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -1546,7 +1562,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_small(
       if (r16 == 0) {  // D[row 4g + j][col 0] sits in lane 16 g
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int ej = 16 * gi + 4 * g + j;
+          const int ej = 16 * gr + 4 * g + j;
           if (ej < nb) sbuf[ej] = acc[j] != acc[j] ? 0ull : make_key(acc[j], brow[ej]);
         }
       }
