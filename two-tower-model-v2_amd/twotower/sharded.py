@@ -35,6 +35,12 @@ def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
     return rank * n // world, (rank + 1) * n // world
 
 
+def _dist_on() -> bool:
+    """Collectives run whenever a process group exists -- at world size 1 too (trivially),
+    so a one-GPU run exercises the RCCL calls of the W-GPU path."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def _world(group) -> Tuple[int, int]:
     if not dist.is_available() or not dist.is_initialized():
         return 0, 1
@@ -50,6 +56,7 @@ class TopkExchange:
                  aux_width: int = 0):
         self.group = group
         self.rank, self.world = _world(group)
+        self.active = _dist_on()
         self.b, self.k = int(b_local), int(k)
         dev = device if device is not None else "cpu"
         self.qall = torch.empty((self.world * self.b, width), dtype=torch.float32, device=dev)
@@ -61,7 +68,7 @@ class TopkExchange:
     def gather_queries(self, q: Tensor) -> Tensor:
         if q.shape[0] != self.b:
             raise ValueError(f"expected {self.b} local queries, got {q.shape[0]}")
-        if self.world == 1:
+        if not self.active:
             return q
         dist.all_gather_into_tensor(self.qall, q.contiguous(), group=self.group)
         return self.qall
@@ -76,7 +83,7 @@ class TopkExchange:
 
     def gather_aux(self, aux: Tensor) -> Tensor:
         """Per-query side data [B, aux_width] f32 (the sharded filter's stats), same order."""
-        if self.world == 1:
+        if not self.active:
             return aux
         dist.all_gather_into_tensor(self.aux_all, aux.contiguous(), group=self.group)
         return self.aux_all
@@ -91,7 +98,7 @@ class TopkExchange:
             s, i = local_search(qall, self.gather_aux(aux))
         else:
             s, i = local_search(qall)
-        if self.world == 1:
+        if not self.active:
             return s, i
         s_recv, i_recv = self.return_results(s, i)
         return merge(s_recv, i_recv, self.k)
@@ -100,8 +107,7 @@ class TopkExchange:
 def sharded_search(q: Tensor, k: int, local_search, merge, group=None):
     """Ragged variant: ranks may hold different numbers of queries.  Batches are padded to
     the group's maximum (one extra all-reduce) and the padding rows are dropped."""
-    rank, world = _world(group)
-    if world == 1:
+    if not _dist_on():
         return local_search(q)
     b = torch.tensor([q.shape[0]], dtype=torch.int64, device=q.device)
     dist.all_reduce(b, op=dist.ReduceOp.MAX, group=group)
@@ -140,7 +146,7 @@ class ShardedFlatIP:
         if x.shape[0] != self.hi - self.lo:
             raise ValueError(f"rank {self.rank} owns {self.hi - self.lo} rows, got {x.shape[0]}")
         self.index.add(x)
-        if self.world > 1:
+        if _dist_on():
             self._build_sample()
 
     def _build_sample(self) -> None:
@@ -169,7 +175,7 @@ class ShardedFlatIP:
     def _staged(self, k: int, method: str) -> bool:
         """Every rank takes the same branch: decided from (n_global, world, k, method) only."""
         smallest = self.n_global // self.world
-        return (self.world > 1 and method in ("auto", "bf16") and 1 <= k <= 128
+        return (_dist_on() and method in ("auto", "bf16") and 1 <= k <= 128
                 and smallest >= k)
 
     def search(self, q: Tensor, k: int, method: str = "auto"):
