@@ -3,7 +3,9 @@
 set -e
 cd "$(dirname "$0")/../two-tower-model-v2_amd/csrc"
 mkdir -p ../lib/variants ../build/variants
-VARIANTS=${VARIANTS:-"base: nodma:-DTT_EXP_NODMA=1 nosel:-DTT_EXP_NOSEL=1 nobar:-DTT_EXP_NOBAR=1 nowrite:-DTT_EXP_NOWRITE=1 maxonly:-DTT_EXP_MAXONLY=1"}
+VARIANTS=${VARIANTS:-"base: nosel:-DTT_EXP_NOSEL=1 nowrite:-DTT_EXP_NOWRITE=1 maxonly:-DTT_EXP_MAXONLY=1"}
+# (skipping the DMA or the per-tile barrier left garbage candidate rows: memory faults in the
+# re-rank, so those switches were removed)
 FILE=${FILE:-tt_filter}  # the source the variants differ in (tt_filter or tt_encoder)
 rm -f ../lib/variants/lib_*.so
 for v in $VARIANTS; do

@@ -210,9 +210,6 @@ template <> struct RingCfg<512> { static constexpr int TR = 16, QB = 1; };
 template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 
 // Experiment switches (timing-only builds, results WRONG when set): tools/exp_filter.sh
-#ifndef TT_EXP_NODMA
-#define TT_EXP_NODMA 0  // skip the DMA issue/wait: MFMA + selection on stale LDS
-#endif
 #ifndef TT_EXP_NOSEL
 #define TT_EXP_NOSEL 0  // skip candidate selection
 #endif
@@ -224,9 +221,6 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #endif
 #ifndef TT_EXP_NOIDLE
 #define TT_EXP_NOIDLE 0  // small batches: padding-only waves run the MFMA stream too (A/B)
-#endif
-#ifndef TT_EXP_NOBAR
-#define TT_EXP_NOBAR 0  // skip the per-step barrier
 #endif
 #ifndef TT_EXP_NOWRITE
 #define TT_EXP_NOWRITE 0  // selection control flow without the LDS pool writes
@@ -256,16 +250,21 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #ifndef TT_EXP_MAXONLY
 #define TT_EXP_MAXONLY 0  // per-block max + ballot only (no per-slot scan)
 #endif
-TT_CHECK_EXP(TT_EXP_NODMA || TT_EXP_NOSEL || TT_EXP_NOWRITE || TT_EXP_NOBAR || TT_EXP_MAXONLY ||
+TT_CHECK_EXP(TT_EXP_NOSEL || TT_EXP_NOWRITE || TT_EXP_MAXONLY ||
                  TT_EXP_SEL_STOP || TT_EXP_SEL_TIMING, "TT_EXP_* (results wrong / printf)");
 TT_CHECK_EXP(TT_RING_HALF || TT_RING_QB4 || TT_EXP_NOIDLE || TT_EXP_PRIO ||
                  TT_RING_NT != 1 || TT_RR_STAGED != 1 || TT_RR_PF != 1 || TT_RR_NT,
              "a non-default ring/re-rank schedule (untested by the GPU suite)");
-constexpr int RG_WAVES = (TT_RING_HALF || TT_RING_QB4) ? 4 : 8, RG_PD = 3,
+#ifndef TT_RING_PD
+// ring tiles in flight; 4 (5 slots, the pool's flush mark lowered to fit LDS): 6.33 -> 6.49 ms
+#define TT_RING_PD 3
+#endif
+TT_CHECK_EXP(TT_RING_PD != 3, "TT_RING_PD");
+constexpr int RG_WAVES = (TT_RING_HALF || TT_RING_QB4) ? 4 : 8, RG_PD = TT_RING_PD,
               RG_SLOTS = RG_PD + 1;  // 3 in flight
 // Pool entries per wave: a query block's scan appends at most 16 x TR <= 512 (16 x 32 rows, all
 // passing); it starts with wn <= RG_WFLUSH, so its writes need no bounds check.
-constexpr int RG_WFLUSH = 256;
+constexpr int RG_WFLUSH = TT_RING_PD > 3 ? 64 : 256;
 constexpr int RG_WPOOL = RG_WFLUSH + (TT_RING_QB4 ? 1024 : 512);
 constexpr int RG_POOL = RG_WPOOL * RG_WAVES;  // pool entries per block
 constexpr int RG_BLOCKS_PER_CU = TT_RING_HALF ? 2 : 1;
@@ -447,27 +446,30 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   // clamp: only the last tile of a ragged slab reads past j1 -- a separate instantiation
   // behind a scalar branch, so the common path is a uniform base + per-lane 32-bit offset
   // (the compiler had if-converted both paths into ~48 VALU selects per tile)
+  // Each tile is read through a buffer resource based at the tile (scalar registers, TR rows
+  // of range): the per-lane offset is the 32-bit voffset, so a piece costs no 64-bit VALU
+  // address add (buffer_load_dwordx4 ... offen lds).
   auto issue_t = [&](int t, auto clamp_) __attribute__((always_inline)) {
     constexpr bool clamp = decltype(clamp_)::value;
     char* slot = ring + (t % RG_SLOTS) * TILE_B;
     const int64_t jt = j0 + (int64_t)t * TR;
-    const char* tb = slab_base + (int64_t)t * tile_bytes;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(slab_base + (int64_t)t * tile_bytes), 0, (int)tile_bytes, 0x00020000);
 #pragma unroll
     for (int pp = 0; pp < PPW; ++pp) {
-      const char* src;
+      uint32_t off;
       if constexpr (!clamp) {
-        src = tb + voff[pp];
+        off = voff[pp];
       } else {  // recompute the lane's (row, column) of piece pp: rare path, no live registers
         const int P = (w + RG_WAVES * pp) * 64 + lane;
         const int r = P / CPR;
         int64_t j = jt + r;
         j = j < j1 ? j : j1 - 1;
-        src = (const char*)xb + j * row_bytes + 16 * ((P % CPR) ^ (r & FM));
+        off = (uint32_t)((j - jt) * row_bytes) + 16u * (uint32_t)((P % CPR) ^ (r & FM));
       }
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(
-                                           slot + (w + RG_WAVES * pp) * 1024),
-                                       16, 0, ((TT_RING_NT >= 1 && LVL == 2) || TT_RING_NT >= 3) ? 2 : 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(slot + (w + RG_WAVES * pp) * 1024), 16,
+          off, 0, 0, ((TT_RING_NT >= 1 && LVL == 2) || TT_RING_NT >= 3) ? 2 : 0);
     }
   };
   auto issue = [&](int t) __attribute__((always_inline)) {
@@ -590,7 +592,6 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   };
   // wait until only `younger` tiles issued after the awaited one are still in flight
   auto wait_tiles = [&](int younger) __attribute__((always_inline)) {
-    if (TT_EXP_NODMA) return;
     if (younger >= 3) wait_vm<3 * PPW>();
     else if (younger == 2) wait_vm<2 * PPW>();
     else if (younger == 1) wait_vm<PPW>();
@@ -704,8 +705,8 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
               const int younger = n_tiles - 2 - t < RG_PD - 2 ? n_tiles - 2 - t : RG_PD - 2;
               wait_tiles(younger);
             }
-            if (!TT_EXP_NOBAR) asm volatile("s_barrier" ::: "memory");
-            if (!TT_EXP_NODMA && t + RG_PD < n_tiles) issue(t + RG_PD);
+            asm volatile("s_barrier" ::: "memory");
+            if (t + RG_PD < n_tiles) issue(t + RG_PD);
           }
           if constexpr (LVL == 0 || S0 < 0) {
             if constexpr (s == 1) {  // early: tile t-1's scores die before the peak
@@ -2123,6 +2124,9 @@ int filter_level(const FilterPlan& p, const FilterWs& w, int li, int mode, const
                  const QueryInit& qi = QueryInit{0.0f, 0.0f, nullptr, nullptr, nullptr, nullptr}) {
   const Level& L = p.lv[li];
   const bool last = li == p.n_levels - 1;
+  // k_filter_ring addresses a tile (TR sample rows) through one buffer resource: < 2 GiB
+  if (!L.dense && L.stride * ld_db * 2 * ring_tr(ep) > 0x7fffffffLL)
+    return fail(TT_ERR_UNSUPPORTED, "bf16 filter: catalog sample stride too large");
   if (last && ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "hipEventRecord(start)");
   switch (ep) {
