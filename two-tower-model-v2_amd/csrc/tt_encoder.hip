@@ -1323,10 +1323,10 @@ __global__ __launch_bounds__(256) void k_attn32_mfma(const TI* __restrict__ qkv,
 
 // bf16 fast path of k_attn32_mfma (bf16 qkv in, bf16 context out; the f32 instantiations
 // above stay the parity path).  Same MFMA dataflow; the VALU per MFMA (83 in the shared
-// kernel: PMC) is cut by: scores pre-scaled by scale*log2(e) and exponentiated with v_exp_f32
-// (exp2), bf16 packing by v_cvt_pk_bf16_f32, key masking only in a sequence's last 32-key
-// chunk, and V^T staged two keys per lane as packed dwords (8 ds_write_b32 per 2 rows instead
-// of 16 ds_write_b16, no two lanes writing halves of one dword).
+// kernel: PMC) is cut by: scores scaled by scale*log2(e) inside the exponent (v_exp_f32 =
+// exp2), a two-pass softmax (below), bf16 packing by v_cvt_pk_bf16_f32, key masking only in a
+// sequence's last 32-key chunk, and V^T staged two keys per lane as packed dwords (8
+// ds_write_b32 per 2 rows instead of 16 ds_write_b16, no two lanes writing halves of a dword).
 __global__ __launch_bounds__(256) void k_attn32_bf16(const uint16_t* __restrict__ qkv,
                                                      int64_t ldq, const int32_t* __restrict__ cu,
                                                      int H, int heads, float scale,
@@ -1375,18 +1375,22 @@ __global__ __launch_bounds__(256) void k_attn32_bf16(const uint16_t* __restrict_
   }
   __syncthreads();
   const float sl2 = scale * 1.4426950408889634f;  // scores in log2 units
+  // Two passes over the keys per 16-query group (the kernel is VALU-bound, the MFMAs cheap):
+  // pass 1 finds each query's maximum raw score (lane-partial maxima, one cross-lane reduce),
+  // pass 2 recomputes S and accumulates exp2(s * sl2 - m * sl2) and P.V with that fixed
+  // offset -- no per-chunk cross-lane max, rescale of the accumulators or correction exp of
+  // the online form (59 -> ~32 VALU per 32-key chunk), and the row sums stay lane-partial
+  // until the end.  Measured: the same 284 us per layer at 365k tokens as the online form
+  // (the VALU was not the limiter); kept for its exact row maximum.
   for (int q0 = 16 * w; q0 < L; q0 += 64) {
     const bf16x8e qf = __builtin_bit_cast(bf16x8e, qnext);
     if (q0 + 64 < L) qnext = load_q(q0 + 64);
-    float m = -__builtin_huge_valf(), lsum = 0.0f;
-    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-    for (int kc = 0; kc < Lk; kc += 32) {
-      f32x4 sc[2];
+    auto scores = [&](int kc, f32x4 (&sc)[2]) __attribute__((always_inline)) {
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const u32x4 kf = *(const u32x4*)(Ks + (kc + 16 * b + ql) * KROW + 16 * g);
         sc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8e, kf), qf,
-                                                        f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0) * sl2;
+                                                        f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
       }
       // sc[b][v] = score(key kc + 16b + 4g + v, query q0 + ql); mask past L (last chunk only)
       if (kc + 32 > L) {
@@ -1396,26 +1400,29 @@ __global__ __launch_bounds__(256) void k_attn32_bf16(const uint16_t* __restrict_
           for (int v = 0; v < 4; ++v)
             if (kc + 16 * b + 4 * g + v >= L) sc[b][v] = -__builtin_huge_valf();
       }
-      float cm = fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
-                       fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3])));
-      cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
-      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
-      const float mn = fmaxf(m, cm);
-      const float corr = __builtin_amdgcn_exp2f(m - mn);
-      m = mn;
-      float ps = 0.0f;
+    };
+    float m = -__builtin_huge_valf();
+    for (int kc = 0; kc < Lk; kc += 32) {
+      f32x4 sc[2];
+      scores(kc, sc);
+      m = fmaxf(m, fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
+                         fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3]))));
+    }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    const float m2 = m * sl2;
+    float lpart = 0.0f;
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    for (int kc = 0; kc < Lk; kc += 32) {
+      f32x4 sc[2];
+      scores(kc, sc);
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          sc[b][v] = __builtin_amdgcn_exp2f(sc[b][v] - mn);
-          ps += sc[b][v];
+          sc[b][v] = __builtin_amdgcn_exp2f(fmaf(sc[b][v], sl2, -m2));
+          lpart += sc[b][v];
         }
-      ps += __shfl_xor(ps, 16, 64);
-      ps += __shfl_xor(ps, 32, 64);
-      lsum = lsum * corr + ps;
-      acc[0] = acc[0] * corr;
-      acc[1] = acc[1] * corr;
       // P^T slots: j < 4 <-> key kc + 4g + j, j >= 4 <-> kc + 16 + 4g + (j - 4)
       const u32x4 pu = {pack_bf16_hw(sc[0][0], sc[0][1]), pack_bf16_hw(sc[0][2], sc[0][3]),
                         pack_bf16_hw(sc[1][0], sc[1][1]), pack_bf16_hw(sc[1][2], sc[1][3])};
@@ -1429,6 +1436,8 @@ __global__ __launch_bounds__(256) void k_attn32_bf16(const uint16_t* __restrict_
                                                           acc[db], 0, 0, 0);
       }
     }
+    float lsum = lpart + __shfl_xor(lpart, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
     // acc[db][v] = O^T[dim 16 db + 4 g + v][query q0 + ql]
     if (q0 + ql < L) {
       const float inv = 1.0f / lsum;
