@@ -66,18 +66,46 @@ __device__ __forceinline__ float gelu_erf(float x) {
 // below the bf16 rounding of the outputs it feeds): ~12 VALU ops instead of erff's ~35, which
 // made the FFN1 GEMM's epilogue VALU-bound.  The f32 (parity) path keeps erff.
 __device__ __forceinline__ float gelu_fast(float x) {
+  // the exact operation sequence of gelu2_fast's lanes (below), so that the element-wise edge
+  // path and the packed full-tile path give identical bits (chunking never changes a row)
   const float z = fabsf(x) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
-  float p = fmaf(1.061405429f, t, -1.453152027f);
+  const float t = __builtin_amdgcn_rcpf(fmaf(z, 0.3275911f, 1.0f));
+  float p = fmaf(t, 1.061405429f, -1.453152027f);
   p = fmaf(p, t, 1.421413741f);
   p = fmaf(p, t, -0.284496736f);
   p = fmaf(p, t, 0.254829592f);
-  const float e = 1.0f - p * t * __expf(-z * z);  // erf(|x| / sqrt 2)
-  return 0.5f * x * (1.0f + (x < 0.0f ? -e : e));
+  const float ex = __builtin_amdgcn_exp2f((z * -1.4426950408889634f) * z);
+  const float e = copysignf(fmaf(-(p * t), ex, 1.0f), x);  // erf(x / sqrt 2)
+  const float hx = x * 0.5f;
+  return fmaf(hx, e, hx);
 }
 
 typedef __bf16 bf16x2e __attribute__((ext_vector_type(2)));
 typedef float f32x2e __attribute__((ext_vector_type(2)));
+// gelu_fast on two values with packed math (v_pk_fma_f32 / v_pk_mul_f32 take both lanes of a
+// pair per instruction): 20 instructions per pair instead of ~30 -- the FFN1 epilogue's GELU
+// was all of its non-MFMA VALU (PMC: 5.4 VALU per MFMA, i.e. VALU-issue-bound).  The same
+// A-S 7.1.26 formula; only the operation grouping differs from gelu_fast.
+__device__ __forceinline__ f32x2e gelu2_fast(f32x2e x) {
+  const f32x2e one = {1.0f, 1.0f};
+  const f32x2e z = __builtin_elementwise_abs(x) * 0.70710678118654752f;
+  const f32x2e d = __builtin_elementwise_fma(z, f32x2e{0.3275911f, 0.3275911f}, one);
+  const f32x2e t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2e p = __builtin_elementwise_fma(t, f32x2e{1.061405429f, 1.061405429f},
+                                       f32x2e{-1.453152027f, -1.453152027f});
+  p = __builtin_elementwise_fma(p, t, f32x2e{1.421413741f, 1.421413741f});
+  p = __builtin_elementwise_fma(p, t, f32x2e{-0.284496736f, -0.284496736f});
+  p = __builtin_elementwise_fma(p, t, f32x2e{0.254829592f, 0.254829592f});
+  const f32x2e zz = (z * -1.4426950408889634f) * z;  // -z^2 log2(e)
+  const f32x2e ex = {__builtin_amdgcn_exp2f(zz.x), __builtin_amdgcn_exp2f(zz.y)};
+  const f32x2e e = __builtin_elementwise_copysign(__builtin_elementwise_fma(-(p * t), ex, one), x);
+  const f32x2e hx = x * 0.5f;
+  return __builtin_elementwise_fma(hx, e, hx);  // 0.5 x (1 + erf(x / sqrt 2))
+}
+__device__ __forceinline__ void gelu4_fast(f32x4& y) {
+  const f32x2e lo = gelu2_fast(f32x2e{y[0], y[1]}), hi = gelu2_fast(f32x2e{y[2], y[3]});
+  y = f32x4{lo.x, lo.y, hi.x, hi.y};
+}
 // two floats -> packed bf16 (round to nearest even) in one v_cvt_pk_bf16_f32
 __device__ __forceinline__ uint32_t pack_bf16_hw(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2e{a, b}, bf16x2e));
@@ -154,10 +182,14 @@ __device__ __forceinline__ int gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, i
           for (int h = 0; h < 2; ++h) {
             const int j = 2 * jp + h;
             f32x4 y = acc[i][j] + bv[j];
+            if (FAST && act == ACT_GELU) {
+              gelu4_fast(y);
+            } else {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              if (act == ACT_GELU) y[u] = FAST ? gelu_fast(y[u]) : gelu_erf(y[u]);
-              else if (act == ACT_RELU) y[u] = y[u] > 0.0f ? y[u] : 0.0f;
+              for (int u = 0; u < 4; ++u) {
+                if (act == ACT_GELU) y[u] = gelu_erf(y[u]);
+                else if (act == ACT_RELU) y[u] = y[u] > 0.0f ? y[u] : 0.0f;
+              }
             }
             if (res) y = y + rv[i][j];
             pk[h][0] = pack_bf16_hw(y[0], y[1]);
@@ -179,10 +211,14 @@ __device__ __forceinline__ int gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, i
       for (int j = 0; j < 4; ++j) {
         const int n = nw0 + 16 * j + 4 * g;
         f32x4 y = acc[i][j] + bv[j];
+        if (FAST && act == ACT_GELU) {
+          gelu4_fast(y);
+        } else {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (act == ACT_GELU) y[u] = FAST ? gelu_fast(y[u]) : gelu_erf(y[u]);
-          else if (act == ACT_RELU) y[u] = y[u] > 0.0f ? y[u] : 0.0f;
+          for (int u = 0; u < 4; ++u) {
+            if (act == ACT_GELU) y[u] = gelu_erf(y[u]);
+            else if (act == ACT_RELU) y[u] = y[u] > 0.0f ? y[u] : 0.0f;
+          }
         }
         if (res) y = y + rv[i][j];
         if (C) *(f32x4*)(C + m * ldc + n) = y;
