@@ -1784,6 +1784,123 @@ __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, in
   }
 }
 
+// Sharded finish: a shard's part of a query's band is small (~1/W of it: ~25 rows at W = 8),
+// and the block-per-query k_rerank (74 KB LDS: 2 blocks, i.e. 2 queries, per CU; a block-wide
+// bitonic sort) spent 1.7 ms on 80k such queries.  Here one WAVE owns a query: the cut filter
+// compacts the kept band rows by ballot into a wave-private list (<= RW_CAP; more -> the
+// query takes this shard's exact fallback, which keeps the protocol sound), the rows are
+// scored by the staged 64-row gather of k_rerank (same canonical FMA order, bit-identical),
+// and each kept row's output slot is its rank (#keys ahead) -- no sort, no block barrier.
+constexpr int RW_CAP = 256;
+template <int EP>
+__global__ __launch_bounds__(256) void k_rerank_wave(
+    const float* __restrict__ db, int64_t ld, const float* __restrict__ q, int64_t ldq,
+    const uint64_t* __restrict__ band, const int* __restrict__ band_n, int* flags, int* qsel,
+    int* qsel_n, int nq, int k, int64_t row_base, const float* __restrict__ cut,
+    float* __restrict__ out_s, int64_t* __restrict__ out_i) {
+  __shared__ __attribute__((aligned(16))) char stage[4][64 * 256];
+  __shared__ uint64_t kept[4][RW_CAP];
+  __shared__ __attribute__((aligned(16))) float qsh[4][EP];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int qid = blockIdx.x * 4 + w;
+  if (qid >= nq || flags[qid]) return;  // (flagged: served by the exact fallback)
+  float* qs = qsh[w];
+  uint64_t* buf = kept[w];
+  char* st = stage[w];
+  for (int i = lane; i < EP; i += 64) qs[i] = q[(int64_t)qid * ldq + i];
+  const int nb_all = band_n[qid];
+  const uint64_t* qband = band + (int64_t)qid * BAND_CAP;
+  const float c = cut[qid];
+  int nb = 0;
+  for (int e0 = 0; e0 < nb_all; e0 += 64) {
+    const int e = e0 + lane;
+    const uint64_t key = e < nb_all ? qband[e] : 0ull;
+    const bool keep = e < nb_all && key_float((uint32_t)(key >> 32)) >= c;
+    const uint64_t bm = __ballot(keep);
+    const int pos = nb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+    if (keep && pos < RW_CAP) buf[pos] = key;
+    nb += (int)__popcll(bm);
+  }
+  if (nb > RW_CAP) {  // this shard's part of the band is too large for the wave list
+    if (lane == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
+  wave_sync();
+  const int sub = lane >> 4, piece = lane & 15;
+  for (int e0 = 0; e0 < nb; e0 += 64) {
+    const int ej = e0 + lane;
+    const uint32_t rj = key_row(buf[ej < nb ? ej : e0]);
+    const float* rp[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t r = (uint32_t)__shfl((int)rj, 4 * i + sub, 64);
+      rp[i] = db + (int64_t)r * ld + 4 * piece;
+    }
+    constexpr int NC = EP / 64;
+    float acc = 0.0f;
+    f32x4 v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = *(const f32x4*)rp[i];
+#pragma unroll 1
+    for (int cc = 0; cc < NC; ++cc) {
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = 4 * i + sub;
+        *(f32x4*)(st + row * 256 + 16 * (piece ^ (row & 15))) = v[i];
+      }
+      asm volatile("" ::: "memory");
+      if (cc + 1 < NC) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = *(const f32x4*)(rp[i] + 64 * (cc + 1));
+      }
+      const char* my = st + lane * 256;
+      const int sw = lane & 15;
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const f32x4 x0 = *(const f32x4*)(my + 16 * ((4 * tt + 0) ^ sw));
+        const f32x4 x1 = *(const f32x4*)(my + 16 * ((4 * tt + 1) ^ sw));
+        const f32x4 x2 = *(const f32x4*)(my + 16 * ((4 * tt + 2) ^ sw));
+        const f32x4 x3 = *(const f32x4*)(my + 16 * ((4 * tt + 3) ^ sw));
+        const float* qt = qs + 64 * cc + 16 * tt;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc = fmaf(x0[i], qt[0 + i], acc);
+          acc = fmaf(x1[i], qt[4 + i], acc);
+          acc = fmaf(x2[i], qt[8 + i], acc);
+          acc = fmaf(x3[i], qt[12 + i], acc);
+        }
+      }
+      wave_sync();  // every lane's chain read this chunk before the next one is staged
+    }
+    // the key can replace the band key in place: lane ej owns slot ej (read above)
+    if (ej < nb) buf[ej] = acc != acc ? 0ull : make_key(acc, rj);
+  }
+  wave_sync();
+  // output slot = rank (keys of distinct rows are distinct; equal keys -- NaN scores, key 0 --
+  // are ordered by position); slots nb .. k-1 stay (-inf, -1)
+  for (int e0 = 0; e0 < nb; e0 += 64) {
+    const int e = e0 + lane;
+    if (e < nb) {
+      const uint64_t me = buf[e];
+      int rank = 0;
+      for (int j = 0; j < nb; ++j) {
+        const uint64_t o = buf[j];
+        rank += (o > me || (o == me && j < e)) ? 1 : 0;
+      }
+      if (rank < k) {
+        out_s[(int64_t)qid * k + rank] = me ? key_score(me) : -__builtin_huge_valf();
+        out_i[(int64_t)qid * k + rank] = me ? row_base + (int64_t)key_row(me) : -1;
+      }
+    }
+  }
+  for (int i = nb + lane; i < k; i += 64) {
+    out_s[(int64_t)qid * k + i] = -__builtin_huge_valf();
+    out_i[(int64_t)qid * k + i] = -1;
+  }
+}
+
 __global__ void k_fill_i32(int* x, int n, int v) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] = v;
@@ -1836,6 +1953,7 @@ struct Level {
   int64_t stride, n_sample;
   int rows_per_slab, n_slabs, n_qt;
   bool dense;
+  bool tmax;  // appends tile maxima (k_filter_ring<EP, 0>): every level sampled at stride > 1
 };
 
 struct FilterPlan {
@@ -1938,6 +2056,7 @@ static FilterPlan plan_filter(int64_t n, int nq, int k, int ep) {
     L.stride = strides[nl - 1 - i];
     L.n_sample = (n + L.stride - 1) / L.stride;
     L.dense = i == 0 && first < 0;
+    L.tmax = L.stride != 1;
     const int qpb = L.dense ? dense_qpb : ring_qpb_v;
     L.n_qt = (nq + qpb - 1) / qpb;
     int64_t sl;
@@ -2023,7 +2142,7 @@ static void launch_level(const Level& L, const uint16_t* xb, int64_t n, int64_t 
                        ld, q, nq, ldq, w.theta, L.stride, L.n_sample, L.rows_per_slab,
                        L.n_slabs, L.n_qt, w.lists, w.counts);
   } else {
-    auto kern = L.stride != 1     ? k_filter_ring<EP, 0>
+    auto kern = L.tmax            ? k_filter_ring<EP, 0>
                 : nq > RG_SMALL_NQ ? k_filter_ring<EP, 1>
                                    : k_filter_ring<EP, 2>;
     hipLaunchKernelGGL(kern, dim3(nblk), dim3(64 * RG_WAVES), 0, st, xb, ld, q, nq, ldq, w.theta,
@@ -2171,8 +2290,13 @@ int filter_finish(const FilterWs& w, const float* db, int64_t n, int32_t d, int6
   switch (ep) {
 #define TT_RR(E)                                                                              \
   case E:                                                                                     \
-    hipLaunchKernelGGL(k_rerank<E>, dim3(nq), dim3(256), 0, st, db, ld_db, q, ld_q, w.band,   \
-                       w.band_n, w.flags, k, row_base, cut, out_score, out_idx);              \
+    if (cut)                                                                                  \
+      hipLaunchKernelGGL(k_rerank_wave<E>, dim3((nq + 3) / 4), dim3(256), 0, st, db, ld_db, q, \
+                         ld_q, w.band, w.band_n, w.flags, w.qsel, w.qsel_n, nq, k, row_base,  \
+                         cut, out_score, out_idx);                                            \
+    else                                                                                      \
+      hipLaunchKernelGGL(k_rerank<E>, dim3(nq), dim3(256), 0, st, db, ld_db, q, ld_q, w.band, \
+                         w.band_n, w.flags, k, row_base, cut, out_score, out_idx);            \
     break;
     TT_RR(64) TT_RR(128) TT_RR(256) TT_RR(384) TT_RR(512) TT_RR(768)
 #undef TT_RR
@@ -2322,6 +2446,34 @@ extern "C" int tt_sharded_filter_begin(const uint16_t* sample_bf16, int64_t n_sa
                         workspace_bytes, &ep, &p, &w);
   if (rc) return rc;
   p = plan_filter(n_sample, nq, k, ep);  // same J as the single-catalog call for this k
+  {
+    // The replicated sample IS the single-catalog call's first (tile-max) level when its
+    // tiles fit one selection: one level at theta = -inf whose J-th largest tile maximum (a
+    // lower bound of a_J, exactly the single-GPU threshold) replaces the sample's own two-level
+    // ladder and its exact a_J -- one filter launch and one selection fewer per step.  Only
+    // when the level's slabs fit the workspace carved for the generic plan.
+    const int64_t TR = ring_tr(ep);
+    const int qpb = ep == 64 ? ring_qpb<64>() : ep == 128 ? ring_qpb<128>()
+                    : ep == 256 ? ring_qpb<256>() : ep == 384 ? ring_qpb<384>()
+                    : ep == 512 ? ring_qpb<512>() : ring_qpb<768>();
+    if (n_sample > SEL_CAP / 2 && (n_sample + TR - 1) / TR <= SW_CAP_TILES && p.n_levels > 1) {
+      Level L;
+      L.stride = 1;
+      L.n_sample = n_sample;
+      L.dense = false;
+      L.tmax = true;
+      L.n_qt = (nq + qpb - 1) / qpb;
+      int64_t sl = ring_slabs(L.n_qt, n_sample, (n_sample + FL_CAP * TR - 1) / (FL_CAP * TR));
+      int64_t r = (n_sample + sl - 1) / sl;
+      r = (r + 63) / 64 * 64;
+      L.rows_per_slab = (int)r;
+      L.n_slabs = (int)((n_sample + r - 1) / r);
+      if (L.n_slabs <= p.max_slabs) {
+        p.n_levels = 1;
+        p.lv[0] = L;
+      }
+    }
+  }
   hipStream_t st = (hipStream_t)stream;
   if ((rc = filter_init(w, q, nq, ld_q, ep, 0.0f, 0.0f, st))) return rc;
   for (int li = 0; li < p.n_levels; ++li) {
