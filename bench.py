@@ -488,10 +488,12 @@ def main():
     def step(ev=None):
         kernels.gather_weighted_avg_l2(table, E, hist, w, out=q)  # Mode B buyer encode
         kernels.l2norm_rows(q, E, _lib.TT_NORM_ADD_EPS, out=q)    # retrieve_batch :189-190
-        if staged:  # this rank's thresholds from the replicated sample, gathered with q
-            kernels.sharded_begin(sample16, E, q, K, stats=stats, workspace=ws_begin)
+        if staged:  # this rank's thresholds from the replicated sample, gathered with q;
+            # the query all-gather runs (async, RCCL stream) under the begin stage's kernels
             return ex.search(q, lambda qall, sall: local_search(qall, ev, sall),
-                             kernels.merge_topk, aux=stats)
+                             kernels.merge_topk,
+                             aux=lambda: kernels.sharded_begin(sample16, E, q, K, stats=stats,
+                                                               workspace=ws_begin))
         return ex.search(q, lambda qall: local_search(qall, ev), kernels.merge_topk)
 
     for _ in range(a.warmup):

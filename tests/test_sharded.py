@@ -144,8 +144,11 @@ def _aux_worker(rank, world, port, out_dir):
 
         ex = TopkExchange(B, 4, k, aux_width=2)
         ex.search(q, local, lambda s, i, kk: (s[rank], i[rank]), aux=aux)
+        ok0 = seen.pop("ok")
+        # aux as a callable (the bench's overlapped form: async query gather under it)
+        ex.search(q, local, lambda s, i, kk: (s[rank], i[rank]), aux=lambda: aux.clone())
         np.save(os.path.join(out_dir, f"aux{rank}.npy"),
-                np.array([seen["ok"], seen["sum"]], dtype=np.int64))
+                np.array([ok0 and seen["ok"], seen["sum"]], dtype=np.int64))
     finally:
         dist.destroy_process_group()
 

@@ -65,13 +65,16 @@ class TopkExchange:
         self.s_recv = torch.empty((self.world, self.b, self.k), dtype=torch.float32, device=dev)
         self.i_recv = torch.empty((self.world, self.b, self.k), dtype=torch.int64, device=dev)
 
-    def gather_queries(self, q: Tensor) -> Tensor:
+    def gather_queries(self, q: Tensor, async_op: bool = False):
+        """[B, w] my queries -> [W*B, w] every rank's (rank-major).  async_op: returns
+        (qall, work); qall is valid on the current stream after work.wait()."""
         if q.shape[0] != self.b:
             raise ValueError(f"expected {self.b} local queries, got {q.shape[0]}")
         if not self.active:
-            return q
-        dist.all_gather_into_tensor(self.qall, q.contiguous(), group=self.group)
-        return self.qall
+            return (q, None) if async_op else q
+        work = dist.all_gather_into_tensor(self.qall, q.contiguous(), group=self.group,
+                                           async_op=async_op)
+        return (self.qall, work) if async_op else self.qall
 
     def return_results(self, s_shard: Tensor, i_shard: Tensor) -> Tuple[Tensor, Tensor]:
         """[W*B, k] per-shard results for every rank's queries -> [W, B, k] for my queries."""
@@ -92,12 +95,19 @@ class TopkExchange:
                merge: Callable[[Tensor, Tensor, int], Tuple[Tensor, Tensor]],
                aux: Optional[Tensor] = None):
         """q: my B queries -> (scores [B, k], global ids [B, k]) over the whole catalog.
-        With aux [B, a]: local_search(qall, aux_all) gets every rank's aux rows too."""
-        qall = self.gather_queries(q)
-        if aux is not None:
-            s, i = local_search(qall, self.gather_aux(aux))
+        With aux [B, a]: local_search(qall, aux_all) gets every rank's aux rows too.  aux may
+        be a callable producing them (the sharded filter's begin stage): the query all-gather
+        is then launched first, asynchronously, and overlaps that computation."""
+        if callable(aux):
+            qall, work = self.gather_queries(q, async_op=True)
+            aux_all = self.gather_aux(aux())
+            if work is not None:
+                work.wait()
+            s, i = local_search(qall, aux_all)
+        elif aux is not None:
+            s, i = local_search(self.gather_queries(q), self.gather_aux(aux))
         else:
-            s, i = local_search(qall)
+            s, i = local_search(self.gather_queries(q))
         if not self.active:
             return s, i
         s_recv, i_recv = self.return_results(s, i)
@@ -192,9 +202,10 @@ class ShardedFlatIP:
                                                   min(k, self.sample16.shape[0]))
             if self._ws_begin is None or self._ws_begin.numel() < need:
                 self._ws_begin = torch.empty(need, dtype=torch.uint8, device=ix.device)
-            stats = kernels.sharded_begin(self.sample16, ix.d, q, k, workspace=self._ws_begin)
-            return self._ex.search(q, lambda qa, sa: self._local_staged(qa, sa, k),
-                                   kernels.merge_topk, aux=stats)
+            return self._ex.search(
+                q, lambda qa, sa: self._local_staged(qa, sa, k), kernels.merge_topk,
+                aux=lambda: kernels.sharded_begin(self.sample16, ix.d, q, k,
+                                                  workspace=self._ws_begin))
         return self._ex.search(q, lambda qa: self._local(qa, k, method), kernels.merge_topk)
 
     def _local_staged(self, qa: Tensor, stats: Tensor, k: int):
