@@ -1999,7 +1999,9 @@ static int device_cus() {
 // CUs (the selection then takes the multi-pass k_select_wave).
 static int64_t ring_slabs(int n_qt, int64_t n_sample, int64_t sl_min = 1) {
   const int ncu = device_cus() * RG_BLOCKS_PER_CU;  // concurrent blocks
-  int64_t sl_max = n_sample / 256;
+  // slabs of >= 128 rows (4 tiles); was 256, which capped the one-buyer stride-16 level
+  // (62.5k rows) at 244 slabs, whose 64-row rounding then left 196 blocks on 256 CUs
+  int64_t sl_max = n_sample / 128;
   const int64_t cap = (int64_t)n_qt * 64 >= 4 * ncu ? 64 : (4 * ncu + n_qt - 1) / n_qt;
   if (sl_max > cap) sl_max = cap;
   if (sl_max < sl_min) sl_max = sl_min;
