@@ -1363,35 +1363,46 @@ __global__ __launch_bounds__(256) void k_attn32_mfma(const TI* __restrict__ qkv,
 // exp2), a two-pass softmax (below), bf16 packing by v_cvt_pk_bf16_f32, key masking only in a
 // sequence's last 32-key chunk, and V^T staged two keys per lane as packed dwords (8
 // ds_write_b32 per 2 rows instead of 16 ds_write_b16, no two lanes writing halves of a dword).
-__global__ __launch_bounds__(256) void k_attn32_bf16(const uint16_t* __restrict__ qkv,
-                                                     int64_t ldq, const int32_t* __restrict__ cu,
-                                                     int H, int heads, float scale,
-                                                     uint16_t* __restrict__ out16, int64_t ldo) {
+// HG heads of one sequence per block, 4 waves per head: HG = 2 stages 2 consecutive heads
+// (their Q/K/V slices are a full 128-B line of a qkv row instead of half of one) and amortises
+// the block's fixed latency (cu loads, staging, barrier) over 2 heads.
+template <int HG>
+__global__ __launch_bounds__(256 * HG) void k_attn32_bf16(
+    const uint16_t* __restrict__ qkv, int64_t ldq, const int32_t* __restrict__ cu, int H,
+    int heads, float scale, uint16_t* __restrict__ out16, int64_t ldo) {
   constexpr int DH = 32, KROW = DH * 2 + 16;
+  constexpr int WPH = 4, NT = 64 * HG * WPH;
   extern __shared__ __attribute__((aligned(16))) char sm[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int hh = w / WPH, wsub = w % WPH;
   const int g = lane >> 4, ql = lane & 15;
-  // the heads of one sequence read 64-B halves of the same 128-B lines of qkv: keep them on
-  // one XCD (one L2) -- with the hardware's round-robin placement each XCD fetched every line
+  // the heads of one sequence read parts of the same 128-B lines of qkv: keep them on one XCD
+  // (one L2) -- with the hardware's round-robin placement each XCD fetched every line
+  const int groups = heads / HG;
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
-  const int sq = lb / heads, h = lb % heads;
+  const int sq = lb / groups, h0 = (lb % groups) * HG, h = h0 + hh;
   const int t0 = cu[sq], L = cu[sq + 1] - t0;
   const int Lk = (L + 31) & ~31;
   const int vst = ((Lk + 127) & ~127) + 8;  // V^T row stride (bf16 elements)
-  char* Ks = sm;
-  char* Vt = sm + (size_t)Lk * KROW;
+  const size_t per_head = (size_t)Lk * KROW + (size_t)32 * vst * 2;
+  char* Ks = sm + hh * per_head;
+  char* Vt = Ks + (size_t)Lk * KROW;
   // this wave's first query fragment is loaded before the K/V staging, so its latency overlaps
   // the staging loads instead of following the barrier (then one group ahead in the loop)
   auto load_q = [&](int q0_) {
     const int qr = q0_ + ql < L ? q0_ + ql : L - 1;
     return *(const u32x4*)(qkv + (int64_t)(t0 + qr) * ldq + h * DH + 8 * g);
   };
-  u32x4 qnext = load_q(16 * w < L ? 16 * w : 0);
-  // K rows: 16-B chunks copied whole; V^T: lane pair of keys (2p, 2p+1) x 8 dims -> 8 dwords
-  for (int e = tid; e < (Lk / 2) * 4; e += 256) {
-    const int p = e >> 2, c8 = 8 * (e & 3), j = 2 * p;
+  u32x4 qnext = load_q(16 * wsub < L ? 16 * wsub : 0);
+  // K rows: 16-B chunks copied whole; V^T: lane pair of keys (2p, 2p+1) x 8 dims -> 8 dwords;
+  // item e = (key pair p, head hs of the group, 8-dim chunk c8), chunk fastest
+  for (int e = tid; e < (Lk / 2) * 4 * HG; e += NT) {
+    const int cc = e % (4 * HG), hs = cc >> 2;
+    const int p = e / (4 * HG), c8 = 8 * (cc & 3), j = 2 * p;
+    char* Ks = sm + hs * per_head;
+    char* Vt = Ks + (size_t)Lk * KROW;
     u32x4 k0 = {0u, 0u, 0u, 0u}, k1 = k0, v0 = k0, v1 = k0;
-    const uint16_t* row = qkv + (int64_t)(t0 + j) * ldq + h * DH + c8;
+    const uint16_t* row = qkv + (int64_t)(t0 + j) * ldq + (h0 + hs) * DH + c8;
     if (j < L) {
       k0 = *(const u32x4*)(row + H);
       v0 = *(const u32x4*)(row + 2 * H);
@@ -1418,9 +1429,9 @@ __global__ __launch_bounds__(256) void k_attn32_bf16(const uint16_t* __restrict_
   // the online form (59 -> ~32 VALU per 32-key chunk), and the row sums stay lane-partial
   // until the end.  Measured: the same 284 us per layer at 365k tokens as the online form
   // (the VALU was not the limiter); kept for its exact row maximum.
-  for (int q0 = 16 * w; q0 < L; q0 += 64) {
+  for (int q0 = 16 * wsub; q0 < L; q0 += 16 * WPH) {
     const bf16x8e qf = __builtin_bit_cast(bf16x8e, qnext);
-    if (q0 + 64 < L) qnext = load_q(q0 + 64);
+    if (q0 + 16 * WPH < L) qnext = load_q(q0 + 16 * WPH);
     auto scores = [&](int kc, f32x4 (&sc)[2]) __attribute__((always_inline)) {
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
@@ -1714,13 +1725,22 @@ extern "C" int tt_attention_varlen_bf16(const uint16_t* qkv, int64_t ld_qkv,
     return fail(TT_ERR_UNSUPPORTED, "tt_attention_varlen_bf16: head dim must be 32");
   const size_t smem = attn32_smem(max_len, true);
   if (!out && out_bf16 && !attn_fast_disabled()) {  // bf16-only output: the fast kernel
-    const void* fb = (const void*)k_attn32_bf16;
-    if (smem > 64 * 1024 &&
-        hipFuncSetAttribute(fb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess)
+    // two heads per block (a full 128-B line per row part; 1 / 3 / 4 heads: 285 / 329 / 332 us
+    // per layer at 365k tokens vs 274 us)
+    const bool h2 = heads % 2 == 0 && 2 * smem <= 160 * 1024;
+    const void* fb = h2 ? (const void*)k_attn32_bf16<2> : (const void*)k_attn32_bf16<1>;
+    const size_t sm = h2 ? 2 * smem : smem;
+    if (sm > 64 * 1024 &&
+        hipFuncSetAttribute(fb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm) != hipSuccess)
       return fail(TT_ERR_LAUNCH, "hipFuncSetAttribute(max dynamic LDS)");
-    hipLaunchKernelGGL(k_attn32_bf16, dim3((unsigned)(n_seq * heads)), dim3(256), smem,
-                       (hipStream_t)stream, qkv, ld_qkv, cu_seqlens, H, heads,
-                       1.0f / sqrtf(32.0f), out_bf16, ld_out);
+    if (h2)
+      hipLaunchKernelGGL(k_attn32_bf16<2>, dim3((unsigned)(n_seq * heads / 2)), dim3(512), sm,
+                         (hipStream_t)stream, qkv, ld_qkv, cu_seqlens, H, heads,
+                         1.0f / sqrtf(32.0f), out_bf16, ld_out);
+    else
+      hipLaunchKernelGGL(k_attn32_bf16<1>, dim3((unsigned)(n_seq * heads)), dim3(256), sm,
+                         (hipStream_t)stream, qkv, ld_qkv, cu_seqlens, H, heads,
+                         1.0f / sqrtf(32.0f), out_bf16, ld_out);
     return check_launch("tt_attention_varlen_bf16");
   }
   const void* fn = (const void*)k_attn32_mfma<true, uint16_t>;
