@@ -269,11 +269,27 @@ constexpr int RG_WPOOL = RG_WFLUSH + (TT_RING_QB4 ? 1024 : 512);
 constexpr int RG_POOL = RG_WPOOL * RG_WAVES;  // pool entries per block
 constexpr int RG_BLOCKS_PER_CU = TT_RING_HALF ? 2 : 1;
 
-template <int EP>
-constexpr int ring_qpb() { return RG_WAVES * 16 * RingCfg<EP>::QB; }
-template <int EP>
+// Per-instantiation shape (LVL: see k_filter_ring).  The batched full level at E = 384
+// (bench.py's roofline kernel) keeps THREE 16-query blocks per wave (384 queries per block):
+// each 24 KB catalog tile feeds 1.5x the MFMAs, so the per-tile DMA pieces, barrier and waits
+// weigh 1/3 less and the A-fragment reads per MFMA drop from 1/2 to 1/3.  The query fragments
+// (144 VGPRs) leave room for one k-step of fragment read-ahead and a 3-slot ring (2 tiles in
+// flight: 1.5x the compute per tile covers the same lead time): 6.26-6.33 -> 5.99-6.02 ms
+// (A/B x2, one box).  Small batches (LVL 2: one-buyer searches are HBM-bound and want 3 tiles
+// in flight) and sample levels keep two blocks per wave.
+template <int EP, int LVL>
+struct RingK {
+  static constexpr int QB = (EP == 384 && LVL == 1 && !TT_RING_HALF && !TT_RING_QB4)
+                                ? 3 : RingCfg<EP>::QB;
+  static constexpr int PD = QB == 3 ? 2 : RG_PD;
+  static constexpr int SLOTS = PD + 1;
+};
+template <int EP, int LVL = 0>
+constexpr int ring_qpb() { return RG_WAVES * 16 * RingK<EP, LVL>::QB; }
+template <int EP, int LVL>
 constexpr int ring_smem() {
-  return RG_SLOTS * RingCfg<EP>::TR * EP * 2 + RG_POOL * 8 + ring_qpb<EP>() * 4 + 16;
+  return RingK<EP, LVL>::SLOTS * RingCfg<EP>::TR * EP * 2 + RG_POOL * 8 +
+         ring_qpb<EP, LVL>() * 4 + 16;
 }
 
 // LDS ops of the ring kernel's append path, in inline asm: the compiler cannot prove they do
@@ -353,17 +369,18 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
     int64_t ldq, const float* __restrict__ theta, int64_t stride, int64_t n_sample,
     int rows_per_slab, int n_slabs, int n_qt, uint64_t* __restrict__ lists,
     int* __restrict__ counts, QueryInit qinit) {
-  constexpr int TR = RingCfg<EP>::TR, QB = RingCfg<EP>::QB;
+  constexpr int TR = RingCfg<EP>::TR, QB = RingK<EP, LVL>::QB;
+  constexpr int RG_PD = RingK<EP, LVL>::PD, RG_SLOTS = RingK<EP, LVL>::SLOTS;
   constexpr int KS = EP / 32, QPW = 16 * QB, QPB = RG_WAVES * QPW;
   constexpr int CPR = EP / 8;  // 16-B chunks per row
   constexpr int TILE_B = TR * EP * 2;
   constexpr int PIECES = TILE_B / 1024, PPW = PIECES / RG_WAVES;
   constexpr int FM = (CPR >= 16 ? 16 : CPR) - 1;
   constexpr int RB = TR / 16;
-  constexpr int QSH = QPW == 16 ? 4 : QPW == 32 ? 5 : 6;  // pool entry: query bits
-  static_assert((1 << QSH) == QPW, "queries per wave: a power of two");
+  constexpr int QSH = QPW <= 16 ? 4 : QPW <= 32 ? 5 : 6;  // pool entry: query bits
+  static_assert((1 << QSH) >= QPW, "queries per wave fit the pool entry's query bits");
   static_assert(PIECES % RG_WAVES == 0, "tile must split into whole 1-KiB pieces per wave");
-  __shared__ __attribute__((aligned(16))) char smem[ring_smem<EP>()];
+  __shared__ __attribute__((aligned(16))) char smem[ring_smem<EP, LVL>()];
   char* ring = smem;
   uint64_t* pool_key = (uint64_t*)(smem + RG_SLOTS * TILE_B);
   int* qcnt = (int*)(pool_key + RG_POOL);
@@ -490,7 +507,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
     for (int i = lane; i < n; i += 64) {
       const uint64_t e = wkey[i];
       const uint32_t lo = (uint32_t)e;
-      const uint32_t ql = (uint32_t)(w * QPW) + (lo & (QPW - 1));
+      const uint32_t ql = (uint32_t)(w * QPW) + (lo & ((1u << QSH) - 1));
       const uint32_t slot_i = lds_add_rtn(lds_addr(&qcnt[ql]), 1u);
       const uint32_t row = (uint32_t)((j0 + (int64_t)(lo >> QSH)) * strd);
       if (slot_i < (uint32_t)FL_CAP)
@@ -606,7 +623,10 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   // and the slot of tile t-1 is refilled with tile t+PD.  The selection of tile t-1 (per-block
   // max mid-tile, then the candidate scan) runs between tile t's MFMAs.
   // FD + 1 divides KS (the ring index is s % (FD + 1)); 2 steps ahead where registers are tight
-  constexpr int FD = (EP >= 384 && KS % 3 == 0) ? 2 : (KS >= 4 ? 3 : 1);
+  // (three query blocks per wave: 6 MFMAs per k-step already cover one step of read-ahead,
+  // and the fragment registers of a second step would spill)
+  constexpr int FD = QB >= 3 ? 1 : (EP >= 384 && KS % 3 == 0) ? 2 : (KS >= 4 ? 3 : 1);
+  static_assert(RG_SLOTS >= 3, "ring depth");
   constexpr int S_MID = (KS - FD) / 2;
   // Candidate scan of tile t-1 in one piece per query block, spread between tile t's MFMAs:
   // block P at step S0 + P * KS / QB (batched full level 6.81 -> 6.65 ms against all blocks at
@@ -2050,16 +2070,23 @@ static FilterPlan plan_filter(int64_t n, int nq, int k, int ep) {
   p.n_levels = nl;
   p.max_slabs = 1;
   const int dense_qpb = FL_WAVES * 16 * (ep <= 384 ? 2 : 1);
-  const int ring_qpb_v = ep == 64 ? ring_qpb<64>() : ep == 128 ? ring_qpb<128>()
-                        : ep == 256 ? ring_qpb<256>() : ep == 384 ? ring_qpb<384>()
-                        : ep == 512 ? ring_qpb<512>() : ring_qpb<768>();
+  // queries per block of the ring instantiation a level will run (launch_level's rule)
+  auto ring_qpb_v = [&](bool tmax) {
+    if (!tmax && nq > RG_SMALL_NQ)
+      return ep == 64 ? ring_qpb<64, 1>() : ep == 128 ? ring_qpb<128, 1>()
+             : ep == 256 ? ring_qpb<256, 1>() : ep == 384 ? ring_qpb<384, 1>()
+             : ep == 512 ? ring_qpb<512, 1>() : ring_qpb<768, 1>();
+    return ep == 64 ? ring_qpb<64>() : ep == 128 ? ring_qpb<128>()
+           : ep == 256 ? ring_qpb<256>() : ep == 384 ? ring_qpb<384>()
+           : ep == 512 ? ring_qpb<512>() : ring_qpb<768>();
+  };
   for (int i = 0; i < nl; ++i) {
     Level& L = p.lv[i];
     L.stride = strides[nl - 1 - i];
     L.n_sample = (n + L.stride - 1) / L.stride;
     L.dense = i == 0 && first < 0;
     L.tmax = L.stride != 1;
-    const int qpb = L.dense ? dense_qpb : ring_qpb_v;
+    const int qpb = L.dense ? dense_qpb : ring_qpb_v(L.stride != 1);
     L.n_qt = (nq + qpb - 1) / qpb;
     int64_t sl;
     if (L.dense) {
