@@ -38,8 +38,9 @@ def _encode(table: torch.Tensor, hist: np.ndarray, w: np.ndarray) -> np.ndarray:
 
 def _gemv(cat: torch.Tensor, q: np.ndarray) -> torch.Tensor:
     """catalog [n, d] . q [d] on the CPU through MKL's threaded sgemm path.  torch.mv on this
-    shape takes a slow path (1M x 384: 205 ms vs 29 ms for cat @ q[:, None] on 8 threads here)
-    -- the round-1 baseline used it and understated the CPU by ~3-7x."""
+    shape takes a slow path in the build container (1M x 384: 205 ms vs 29 ms for
+    cat @ q[:, None] on 8 threads); on the GPU box's host both run ~100-140 ms on 16 threads
+    (host-limited there), so the reported baseline barely moved."""
     return (cat @ torch.from_numpy(q)[:, None])[:, 0]
 
 
