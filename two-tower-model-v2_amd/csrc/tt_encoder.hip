@@ -734,10 +734,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wide(const uint16_t* __restrict
 // The MFMA computes D = W . A^T as k_gemm_big (lane (g, rl) of block (i, j) holds row
 // 16 i + rl, columns 16 j + 4 g .. + 3).  In place: x is read (residual) before it is
 // overwritten, by the block that owns the rows.
-constexpr int GL_BM = 128, GL_H = 384, GL_NJ = 6, GL_ASLOTS = 3, GL_WSLOTS = 2;
-constexpr int GL_A_B = GL_BM * 128, GL_W_B = GL_H * 128;
-constexpr int GL_WBASE = GL_ASLOTS * GL_A_B, GL_LDS_B = GL_WBASE + GL_WSLOTS * GL_W_B;
-constexpr int GL_STORES = 4 * GL_NJ * 2;
+constexpr int GL_H = 384, GL_NJ = 6, GL_ASLOTS = 3, GL_WSLOTS = 2;
+constexpr int GL_W_B = GL_H * 128;
 // timing-only experiment switches (results WRONG when set), tools/exp_filter.sh FILE=tt_encoder
 // + tools/exp_gemm.sh.  Measured at M = 370761 (K = 384 / 1536): base 471 / 752 us, no W
 // stream after the prologue 439 / 669, no epilogue 111 / 504 -> the LayerNorm epilogue (its
@@ -754,6 +752,9 @@ constexpr int GL_STORES = 4 * GL_NJ * 2;
 TT_CHECK_EXP(TT_GEXP_NOSTORE || TT_GWEXP_NOEPI || TT_GLEXP_NOW || TT_GLEXP_NOEPI || TT_GL_NT,
              "TT_G*EXP_* / TT_GL_NT (results wrong or untested)");
 
+// BM = 128 (8 waves of 64 x 96) or 96 (8 waves of 48 x 96: a batch of ~18k token rows is
+// 144 tiles of 128 on 256 CUs, 192 of 96 -- tt_gemm_ln_bf16 picks by rounds x tile cost).
+template <int BM>
 __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__ A, int64_t lda,
                                                     const uint16_t* __restrict__ W, int64_t ldw,
                                                     const float* __restrict__ bias,
@@ -762,9 +763,11 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
                                                     float* __restrict__ X, int64_t ldx,
                                                     uint16_t* __restrict__ X16, int64_t ldx16,
                                                     int M, int K) {
-  constexpr int BK = 64, EPC = 8;
-  __shared__ __attribute__((aligned(16))) char smem[GL_LDS_B];
-  __shared__ float red[2][4][GL_BM];  // [mean | var pass][wave column wn][tile row]
+  constexpr int BK = 64, EPC = 8, MI = BM / 32, WR = BM / 2;  // 16-row blocks / rows per wave
+  constexpr int A_B = BM * 128, WBASE = GL_ASLOTS * A_B, STORES = MI * GL_NJ * 2;
+  static_assert(BM == 128 || BM == 96, "k_gemm_ln: BM");
+  __shared__ __attribute__((aligned(16))) char smem[WBASE + GL_WSLOTS * GL_W_B];
+  __shared__ float red[2][4][BM];  // [mean | var pass][wave column wn][tile row]
   __shared__ __attribute__((aligned(16))) float prm[3][GL_H];  // bias, gamma, beta
   const int tid = threadIdx.x, lane = tid & 63;
   for (int e = tid; e < GL_H; e += 512) {
@@ -774,40 +777,46 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
   }  // visible after the first stage's barrier
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 2, wn = w & 3;
-  const int ntiles = (M + GL_BM - 1) / GL_BM;
+  const int ntiles = (M + BM - 1) / BM;
   const int nk = K / BK;
   auto tile_of = [&](int r) { return enc_xcd_remap(blockIdx.x + r * gridDim.x, ntiles); };
   const int n_mine = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
   if (n_mine <= 0) return;
 
-  // DMA: A = 16 pieces of 8 rows x 128 B, W = 48 pieces; wave w issues A pieces w + 8j (j < 2)
-  // and W pieces w + 8j (j < 6); chunk swizzle as k_gemm.
+  // DMA: A = BM / 8 pieces of 8 rows x 128 B, W = 48 pieces; wave w issues A pieces w + 8j
+  // (j < 2; at BM = 96 pieces 12..15 fold onto 8..11, written twice with the same bytes, so
+  // every wave issues 2 and the vmcnt accounting is uniform) and W pieces w + 8j (j < 6);
+  // chunk swizzle as k_gemm.
   // W piece w + 8j = rows 64 j + 8 w + (lane >> 3): a per-lane 32-bit offset (the swizzle
   // (row >> 1) & 7 does not depend on j) plus the uniform base W + 64 j ldw
   const int w_row0 = 8 * w + (lane >> 3);
   const int w_lane = w_row0 * (int)ldw + ((lane & 7) ^ ((w_row0 >> 1) & 7)) * EPC;
+  auto apiece = [&](int j) {
+    const int pc = w + 8 * j;
+    return pc < BM / 8 ? pc : pc - 4;
+  };
   auto a_offsets = [&](int lt, int64_t (&ao)[2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int row = 8 * (w + 8 * j) + (lane >> 3);
+      const int row = 8 * apiece(j) + (lane >> 3);
       const int c = (lane & 7) ^ ((row >> 1) & 7);
-      int am = lt * GL_BM + row;
+      int am = lt * BM + row;
       am = am < M ? am : M - 1;
       ao[j] = (int64_t)am * lda + c * EPC;
     }
   };
   auto issue_a = [&](const int64_t (&ao)[2], int kt, int t) __attribute__((always_inline)) {
-    char* st = smem + (t % GL_ASLOTS) * GL_A_B;
+    char* st = smem + (t % GL_ASLOTS) * A_B;
     const int64_t k0 = (int64_t)kt * BK;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(A + ao[j] + k0),
-          (__attribute__((address_space(3))) void*)(st + 1024 * (w + 8 * j)), 16, 0,
+          (__attribute__((address_space(3))) void*)(st + 1024 * apiece(j)), 16, 0,
           TT_GL_NT ? 2 : 0);
   };
   auto issue_w = [&](int kt, int t) __attribute__((always_inline)) {
-    char* st = smem + GL_WBASE + (t % GL_WSLOTS) * GL_W_B;
+    char* st = smem + WBASE + (t % GL_WSLOTS) * GL_W_B;
     const int64_t k0 = (int64_t)kt * BK;
 #pragma unroll
     for (int j = 0; j < GL_NJ; ++j)
@@ -816,14 +825,14 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
           (__attribute__((address_space(3))) void*)(st + 1024 * (w + 8 * j)), 16, 0, 0);
   };
 
-  // fragment rows 64 wm + 16 i + rl (A) / 96 wn + 16 j + rl (W): the swizzle (row >> 1) & 7
+  // fragment rows WR wm + 16 i + rl (A) / 96 wn + 16 j + rl (W): the swizzle (row >> 1) & 7
   // = (rl >> 1) & 7 is the same for every i, j, so block i / j is an immediate offset
   const int g = lane >> 4, rl = lane & 15;
   uint32_t fa[2], fb[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const int c = (4 * s + g) ^ ((rl >> 1) & 7);
-    fa[s] = (64 * wm + rl) * 128 + 16 * c;
+    fa[s] = (WR * wm + rl) * 128 + 16 * c;
     fb[s] = (96 * wn + rl) * 128 + 16 * c;
   }
 
@@ -850,19 +859,19 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
   bool prev_full = true;
   const float inv_h = 1.0f / (float)GL_H;
   for (int r = 0; r < n_mine; ++r) {
-    const int m0 = tile_of(r) * GL_BM;
-    f32x4 acc[4][GL_NJ];
+    const int m0 = tile_of(r) * BM;
+    f32x4 acc[MI][GL_NJ];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < GL_NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int kt = 0; kt < nk; ++kt) {
       // younger than this stage's W pieces: A(t + 1) (2 per lane, if issued) and, at a tile's
-      // first stage, the previous epilogue's residual loads and GL_STORES stores (a ragged
+      // first stage, the previous epilogue's residual loads and STORES stores (a ragged
       // tile: drain all)
       const int t = gs + kt;
       if (kt == 0 && r > 0) {
-        if (prev_full) enc_wait_vm<GL_STORES>();
+        if (prev_full) enc_wait_vm<STORES>();
         else enc_wait_vm<0>();
       } else if (ta_i > t + 1) {
         enc_wait_vm<2>();
@@ -873,16 +882,16 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
       if (t + 1 < nstages && (!TT_GLEXP_NOW || t + 1 < GL_WSLOTS))
         issue_w(kt + 1 < nk ? kt + 1 : 0, t + 1);
       issue_next_a();
-      const uint32_t sa = lds_addr(smem) + (uint32_t)((t % GL_ASLOTS) * GL_A_B);
-      const uint32_t sw = lds_addr(smem) + (uint32_t)(GL_WBASE + (t % GL_WSLOTS) * GL_W_B);
-      // fragment reads of both k-halves issued up front (20, the LDS counter holds 15: the
-      // last five of s = 1 go out once s = 0 has landed), s = 1 lands under s = 0's MFMAs
-      u32x4 av[2][4], bv[2][GL_NJ];
+      const uint32_t sa = lds_addr(smem) + (uint32_t)((t % GL_ASLOTS) * A_B);
+      const uint32_t sw = lds_addr(smem) + (uint32_t)(WBASE + (t % GL_WSLOTS) * GL_W_B);
+      // fragment reads of both k-halves issued up front (2 (MI + 6); the LDS counter holds 15:
+      // the last five of s = 1 go out once s = 0 has landed), s = 1 lands under s = 0's MFMAs
+      u32x4 av[2][MI], bv[2][GL_NJ];
       const uint32_t pa0 = sa + fa[0], pb0 = sw + fb[0], pa1 = sa + fa[1], pb1 = sw + fb[1];
       av[0][0] = lds_read128<0>(pa0);
       av[0][1] = lds_read128<2048>(pa0);
       av[0][2] = lds_read128<4096>(pa0);
-      av[0][3] = lds_read128<6144>(pa0);
+      if constexpr (MI > 3) av[0][3] = lds_read128<6144>(pa0);
       bv[0][0] = lds_read128<0>(pb0);
       bv[0][1] = lds_read128<2048>(pb0);
       bv[0][2] = lds_read128<4096>(pb0);
@@ -892,9 +901,9 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
       av[1][0] = lds_read128<0>(pa1);
       av[1][1] = lds_read128<2048>(pa1);
       av[1][2] = lds_read128<4096>(pa1);
-      av[1][3] = lds_read128<6144>(pa1);
+      if constexpr (MI > 3) av[1][3] = lds_read128<6144>(pa1);
       bv[1][0] = lds_read128<0>(pb1);
-      lds_wait<5>();
+      lds_wait<MI + 1>();  // s = 0's MI + 6 reads have landed
       bv[1][1] = lds_read128<2048>(pb1);
       bv[1][2] = lds_read128<4096>(pb1);
       bv[1][3] = lds_read128<6144>(pb1);
@@ -904,13 +913,13 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
       for (int s = 0; s < 2; ++s) {
         if (s == 1) lds_wait<0>();
 #pragma unroll
-        for (int i = 0; i < 4; ++i) reg_tie(av[s][i]);
+        for (int i = 0; i < MI; ++i) reg_tie(av[s][i]);
 #pragma unroll
         for (int j = 0; j < GL_NJ; ++j) reg_tie(bv[s][j]);
 #pragma unroll
         for (int j = 0; j < GL_NJ; ++j)
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < MI; ++i)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                 __builtin_bit_cast(bf16x8e, bv[s][j]), __builtin_bit_cast(bf16x8e, av[s][i]),
                 acc[i][j], 0, 0, 0);
@@ -921,7 +930,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
     if (TT_GLEXP_NOEPI) {  // keep every accumulator live (no dead-code MFMAs), store nothing
       float t = 0.0f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < GL_NJ; ++j) t += (acc[i][j][0] + acc[i][j][1]) + (acc[i][j][2] + acc[i][j][3]);
       if (t == 1.2345f) X[0] = t;
@@ -931,22 +940,22 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
     // ---- epilogue: y = acc + bias + x ; x = LayerNorm(y) (biased variance, two passes).
     // Residual rows are loaded one 16-row block ahead (6 x 16 B per lane in flight while the
     // previous block is summed); bias / gamma / beta come from LDS.
-    const bool full = m0 + GL_BM <= M;
+    const bool full = m0 + BM <= M;
     const int nw0 = 96 * wn + 4 * g;
-    const float* xr0 = X + (int64_t)(m0 + 64 * wm + rl) * ldx + nw0;
+    const float* xr0 = X + (int64_t)(m0 + WR * wm + rl) * ldx + nw0;
     auto xrow = [&](int i) __attribute__((always_inline)) {
-      const int m = m0 + 64 * wm + 16 * i + rl;
+      const int m = m0 + WR * wm + 16 * i + rl;
       return X + (int64_t)(m < M ? m : M - 1) * ldx + nw0;  // rows past M: clamped reads
     };
-    float mean[4], rstd[4];
+    float mean[MI], rstd[MI];
     {
       f32x4 rv[2][GL_NJ];
       const float* p0 = full ? xr0 : xrow(0);
 #pragma unroll
       for (int j = 0; j < GL_NJ; ++j) rv[0][j] = *(const f32x4*)(p0 + 16 * j);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (i + 1 < 4) {
+      for (int i = 0; i < MI; ++i) {
+        if (i + 1 < MI) {
           const float* p1 = full ? xr0 + (int64_t)(16 * (i + 1)) * ldx : xrow(i + 1);
 #pragma unroll
           for (int j = 0; j < GL_NJ; ++j) rv[(i + 1) & 1][j] = *(const f32x4*)(p1 + 16 * j);
@@ -959,13 +968,13 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
         }
         s += __shfl_xor(s, 16, 64);
         s += __shfl_xor(s, 32, 64);
-        if (g == 0) red[0][wn][64 * wm + 16 * i + rl] = s;
+        if (g == 0) red[0][wn][WR * wm + 16 * i + rl] = s;
       }
     }
     enc_lds_barrier();
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = 64 * wm + 16 * i + rl;
+    for (int i = 0; i < MI; ++i) {
+      const int row = WR * wm + 16 * i + rl;
       mean[i] = ((red[0][0][row] + red[0][1][row]) + (red[0][2][row] + red[0][3][row])) * inv_h;
       float q = 0.0f;
 #pragma unroll
@@ -981,8 +990,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
     }
     enc_lds_barrier();
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = 64 * wm + 16 * i + rl;
+    for (int i = 0; i < MI; ++i) {
+      const int row = WR * wm + 16 * i + rl;
       const float q = (red[1][0][row] + red[1][1][row]) + (red[1][2][row] + red[1][3][row]);
       rstd[i] = 1.0f / sqrtf(q * inv_h + eps);
     }
@@ -991,14 +1000,14 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
       const int n = nw0 + 16 * j;
       const f32x4 gm = *(const f32x4*)(&prm[1][n]), bt = *(const f32x4*)(&prm[2][n]);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int u = 0; u < 4; ++u) acc[i][j][u] = (acc[i][j][u] - mean[i]) * rstd[i] * gm[u] + bt[u];
     }
     if (full) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t m = m0 + 64 * wm + 16 * i + rl;
+      for (int i = 0; i < MI; ++i) {
+        const int64_t m = m0 + WR * wm + 16 * i + rl;
 #pragma unroll
         for (int j = 0; j < GL_NJ; ++j) {
           const int n = nw0 + 16 * j;
@@ -1009,8 +1018,8 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t m = m0 + 64 * wm + 16 * i + rl;
+      for (int i = 0; i < MI; ++i) {
+        const int64_t m = m0 + WR * wm + 16 * i + rl;
         if (m >= M) continue;
 #pragma unroll
         for (int j = 0; j < GL_NJ; ++j) {
@@ -1077,11 +1086,14 @@ __global__ __launch_bounds__(256) void k_embed_ln(const int32_t* __restrict__ id
                                                   const float* __restrict__ beta, float eps,
                                                   float* __restrict__ y, uint16_t* __restrict__ y16,
                                                   int H) {
-  // block per sequence, wave per token (the position is t - cu[seq]; a per-token binary
-  // search over cu was 13 dependent loads per token at 5k sequences)
+  // blocks (sequence, chunk of 4 tokens), wave per token (the position is t - cu[seq]; a
+  // per-token binary search over cu was 13 dependent loads per token at 5k sequences).  Was a
+  // block per sequence whose waves walked its tokens: at configs[1]'s 256 sequences that is
+  // ~18 dependent gather round trips per wave (129 us per batch); the loop below still covers
+  // every token when gridDim.y * 4 < a sequence's length.
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t t0 = cu[blockIdx.x], t1 = cu[blockIdx.x + 1];
-  for (int64_t t = t0 + w; t < t1; t += 4) {
+  for (int64_t t = t0 + 4 * (int64_t)blockIdx.y + w; t < t1; t += 4 * (int64_t)gridDim.y) {
     const int p = (int)(t - t0);
     int id = ids[t];
     id = (id >= 0 && id < vocab) ? id : 0;
@@ -1561,6 +1573,10 @@ bool gemm_ln_disabled() {  // TT_GEMM_LN=0: unfused GEMM + LayerNorm (timing bui
   static const bool off = env_switch("TT_GEMM_LN", 1) == 0;
   return off;
 }
+bool gemm_ln96_enabled() {  // TT_GEMM_LN96=0: 128-row k_gemm_ln tiles only (A/B timing)
+  static const bool on = env_switch("TT_GEMM_LN96", 1) != 0;
+  return on;
+}
 bool attn_fast_disabled() {  // TT_ATTN_FAST=0: the shared k_attn32_mfma for bf16 too
   static const bool off = env_switch("TT_ATTN_FAST", 1) == 0;
   return off;
@@ -1624,7 +1640,16 @@ extern "C" int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, i
     };
     // default: 256x256 tiles for the wide bf16-only GEMMs (QKV N = 1152, FFN1 N = 1536:
     // 534 / 747 us vs 586 / 824 us with 256x128 at 370k tokens), 256x128 otherwise
-    if (variant == 3 || (variant == 1 && bfo && N >= 1024 && !gemm_wide_disabled())) {  // 256x256
+    // ... unless M is small enough that 256x256 tiles quantise badly onto the CUs (at most
+    // two rounds): rounds x tile cost with a 256x128 tile at 0.54 of a 256x256 one.
+    // configs[1]'s QKV (~18k rows, N = 1152): 360 wide tiles = 2 rounds vs 648 narrow = 3 x
+    // 0.54 (41.7 -> ~33 us); FFN1 (N = 1536) and the Mode A shapes (28+ rounds, where the
+    // wide tile measured faster: 546 vs 586 us QKV) stay wide.
+    const int64_t mt = (M + 255) / 256, ntw = mt * ((N + 255) / 256), ntn = mt * ((N + 127) / 128);
+    const bool narrow_pays =
+        ntw <= 2 * ncu && ((ntn + ncu - 1) / ncu) * 54 < ((ntw + ncu - 1) / ncu) * 100;
+    if (variant == 3 ||
+        (variant == 1 && bfo && N >= 1024 && !gemm_wide_disabled() && !narrow_pays)) {  // 256x256
       if (bfo && act == ACT_NONE) return launch(k_gemm_wide<ACT_NONE, true>, ncu, 512);
       if (bfo && act == ACT_GELU) return launch(k_gemm_wide<ACT_GELU, true>, ncu, 512);
       return launch(k_gemm_wide<-1, false>, ncu, 512);
@@ -1659,11 +1684,18 @@ extern "C" int tt_gemm_ln_bf16(const uint16_t* A, int64_t lda, const uint16_t* W
                  ((uintptr_t)x_bf16 % 8) == 0 && ((uintptr_t)bias % 16) == 0 &&
                  ((uintptr_t)gamma % 16) == 0 && ((uintptr_t)beta % 16) == 0,
              "x / bias / gamma / beta must be 16-B aligned (x_bf16 8-B), ldx, ldx16 % 4 == 0");
-  const int ntiles = (M + GL_BM - 1) / GL_BM;
+  // row-tile height: rounds (ceil(tiles / CUs)) x (BM + ~32 rows of fixed cost per tile); 96
+  // only when strictly cheaper -- a configs[1] batch (~18k rows: 144 tiles of 128 = one
+  // 56%-full round, 192 of 96); at Mode A's 365k rows 128 and 96 tie and 128 stays
   const int ncu = enc_device_cus();
+  const int64_t t128 = (M + 127) / 128, t96 = (M + 95) / 96;
+  const bool b96 = gemm_ln96_enabled() &&
+                   ((t96 + ncu - 1) / ncu) * (96 + 32) < ((t128 + ncu - 1) / ncu) * (128 + 32);
+  const int ntiles = (int)(b96 ? t96 : t128);
   const int grid = ntiles < ncu ? ntiles : ncu;
-  hipLaunchKernelGGL(k_gemm_ln, dim3(grid), dim3(512), 0, (hipStream_t)stream, A, lda, W, ldw,
-                     bias, gamma, beta, eps, x, ldx, x_bf16, ldx16, M, K);
+  hipLaunchKernelGGL(b96 ? k_gemm_ln<96> : k_gemm_ln<128>, dim3(grid), dim3(512), 0,
+                     (hipStream_t)stream, A, lda, W, ldw, bias, gamma, beta, eps, x, ldx, x_bf16,
+                     ldx16, M, K);
   return check_launch("tt_gemm_ln_bf16");
 }
 
@@ -1847,7 +1879,8 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
     return fail(TT_ERR_WORKSPACE, "tt_bert_encode: workspace too small");
   hipStream_t st = (hipStream_t)stream;
   {
-    hipLaunchKernelGGL(k_embed_ln, dim3((unsigned)n_seq), dim3(256), 0, st, ids,
+    const unsigned chunks = (unsigned)(max_len > 4 ? (max_len + 3) / 4 : 1);
+    hipLaunchKernelGGL(k_embed_ln, dim3((unsigned)n_seq, chunks), dim3(256), 0, st, ids,
                        cu_seqlens, n_seq, T, m->word_emb, m->vocab, m->pos_emb, m->type_emb,
                        m->emb_ln_g, m->emb_ln_b, m->ln_eps, w.x, bf ? w.x16 : nullptr, H);
     int rc = check_launch("k_embed_ln");

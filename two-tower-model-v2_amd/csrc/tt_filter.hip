@@ -2040,7 +2040,7 @@ static int64_t ring_slabs(int n_qt, int64_t n_sample, int64_t sl_min = 1) {
   return best;
 }
 
-static FilterPlan plan_filter(int64_t n, int nq, int k, int ep) {
+static FilterPlan plan_filter_uncached(int64_t n, int nq, int k, int ep) {
   FilterPlan p;
   // ~16*J full-catalog rows lie above a_J(stride-16 sample); J = k/8 + 12 keeps that count
   // >= k with ~3.5 sigma margin on iid scores (fewer only under heavy clustering -> fallback)
@@ -2109,6 +2109,30 @@ static FilterPlan plan_filter(int64_t n, int nq, int k, int ep) {
   p.small = nq <= SM_NQ && !select_reg_disabled();
   for (int i = 0; i < nl; ++i) p.small = p.small && p.lv[i].n_slabs <= SM_THREADS;
   return p;
+}
+
+// plan_filter_uncached's slab searches cost ~9 us of host time per one-buyer call (two
+// ring_slabs scans of up to 1024 candidates) -- ahead of the first launch, so on the
+// synchronised /retrieve path they are latency.  Plans depend only on (n, nq, k, ep) and
+// process-constant switches, so the last few are kept per thread.
+static FilterPlan plan_filter(int64_t n, int nq, int k, int ep) {
+  struct Entry {
+    int64_t n;
+    int nq, k, ep;
+    FilterPlan p;
+  };
+  constexpr int NC = 8;
+  thread_local Entry cache[NC];
+  thread_local int used = 0, next = 0;
+  for (int i = 0; i < used; ++i)
+    if (cache[i].n == n && cache[i].nq == nq && cache[i].k == k && cache[i].ep == ep)
+      return cache[i].p;
+  Entry& e = cache[next];
+  e.n = n, e.nq = nq, e.k = k, e.ep = ep;
+  e.p = plan_filter_uncached(n, nq, k, ep);
+  next = (next + 1) % NC;
+  if (used < NC) ++used;
+  return e.p;
 }
 
 struct FilterWs {
