@@ -91,6 +91,6 @@ def test_shipped_library_reads_no_ab_switches():
     from twotower import _lib
 
     raw = open(_lib.LIB_PATH, "rb").read()
-    for name in (b"TT_GEMM_LN", b"TT_ATTN_FAST", b"TT_GEMM_WIDE", b"TT_GEMM_BIG",
+    for name in (b"TT_GEMM_LN", b"TT_GEMM_LN96", b"TT_ATTN_FAST", b"TT_GEMM_WIDE", b"TT_GEMM_BIG",
                  b"TT_SELECT_REG", b"TT_FILTER_TMAX_FIRST"):
         assert name not in raw, name
