@@ -433,6 +433,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
         qinit.eps2[qi] = query_eps2<EP>(sq, st, sr, qinit.X, qinit.R);
         qinit.aref[qi] = -__builtin_huge_valf();
         qinit.flags[qi] = 0;
+        qinit.qsel_n[1 + qi] = 0;  // done[qi] (FilterWs layout)
         if (qi == 0) *qinit.qsel_n = 0;
       }
     }
@@ -1945,6 +1946,7 @@ __global__ __launch_bounds__(256) void k_query_eps(const float* __restrict__ q, 
     theta[qi] = -__builtin_huge_valf();
     aref[qi] = -__builtin_huge_valf();
     flags[qi] = 0;
+    qsel_n[1 + qi] = 0;  // done[qi] (FilterWs layout)
     if (qi == 0) *qsel_n = 0;
   }
   const float* qr = q + (int64_t)qi * ldq;
@@ -2144,9 +2146,10 @@ struct FilterWs {
   float* cut;
   uint64_t* band;
   int* band_n;
-  int* flags;  // flags[nq], qsel[nq], qsel_n[1] are contiguous (one memset)
-  int* qsel;
-  int* qsel_n;
+  int* flags;  // flags[nq], qsel[nq], qsel_n[1], done[nq] are contiguous: the per-query
+  int* qsel;   // init zeroes flags[qi] and qsel_n[1 + qi] (= done[qi], the fused fallback
+  int* qsel_n; // merge's per-tile arrival counter)
+  int* done;
   void* scan_ws;
   int64_t scan_ws_bytes;
   int64_t total;
@@ -2172,10 +2175,11 @@ static FilterWs carve(void* base, const FilterPlan& p, int64_t n, int d, int nq,
   w.cut = (float*)take((int64_t)nq * 4);
   w.band = (uint64_t*)take((int64_t)nq * BAND_CAP * 8);
   w.band_n = (int*)take((int64_t)nq * 4);
-  int* fl = (int*)take(((int64_t)2 * nq + 1) * 4);
+  int* fl = (int*)take(((int64_t)3 * nq + 1) * 4);
   w.flags = fl;
   w.qsel = fl + nq;
   w.qsel_n = fl + 2 * nq;
+  w.done = w.qsel_n + 1;
   int64_t sb = 0;
   tt_scan_workspace_bytes(n, d, nq, k, &sb);
   w.scan_ws_bytes = sb;
@@ -2208,13 +2212,15 @@ static void launch_level(const Level& L, const uint16_t* xb, int64_t n, int64_t 
 
 using namespace tt;
 
-// implemented in tt_scan.hip: exact f32 scan restricted to a device-side query list
-extern "C" int tt_scan_topk_f32_select(const float* db, int64_t n, int32_t d, int64_t ld_db,
-                                       int64_t row_base, const float* q, int32_t nq,
-                                       int64_t ld_q, int32_t k, const int32_t* qsel,
-                                       const int32_t* qsel_n, float* out_score,
-                                       int64_t* out_idx, void* workspace,
-                                       int64_t workspace_bytes, void* stream);
+// implemented in tt_scan.hip: exact f32 scan restricted to a device-side query list, the slab
+// merge fused into the same launch
+namespace tt {
+int scan_f32_select_fused(const float* db, int64_t n, int32_t d, int64_t ld_db, int64_t row_base,
+                          const float* q, int32_t nq, int64_t ld_q, int32_t k,
+                          const int32_t* qsel, const int32_t* qsel_n, int* done,
+                          float* out_score, int64_t* out_idx, void* workspace,
+                          int64_t workspace_bytes, void* stream);
+}
 
 extern "C" int tt_filter_workspace_bytes(int64_t n, int32_t d, int32_t nq, int32_t k,
                                          int64_t* bytes) {
@@ -2357,8 +2363,8 @@ int filter_finish(const FilterWs& w, const float* db, int64_t n, int32_t d, int6
   int rc = check_launch("k_rerank");
   if (rc) return rc;
   // exact fallback for flagged queries (blocks exit at once when none is flagged)
-  return tt_scan_topk_f32_select(db, n, d, ld_db, row_base, q, nq, ld_q, k, w.qsel, w.qsel_n,
-                                 out_score, out_idx, w.scan_ws, w.scan_ws_bytes, st);
+  return scan_f32_select_fused(db, n, d, ld_db, row_base, q, nq, ld_q, k, w.qsel, w.qsel_n,
+                               w.done, out_score, out_idx, w.scan_ws, w.scan_ws_bytes, st);
 }
 }  // namespace
 
@@ -2412,8 +2418,8 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
 #undef TT_FS
     }
     if ((rc = check_launch("k_final_small"))) return rc;
-    return tt_scan_topk_f32_select(db, n, d, ld_db, row_base, q, nq, ld_q, k, w.qsel, w.qsel_n,
-                                   out_score, out_idx, w.scan_ws, w.scan_ws_bytes, st);
+    return scan_f32_select_fused(db, n, d, ld_db, row_base, q, nq, ld_q, k, w.qsel, w.qsel_n,
+                                 w.done, out_score, out_idx, w.scan_ws, w.scan_ws_bytes, st);
   }
   return filter_finish(w, db, n, d, ld_db, row_base, q, nq, ld_q, k, ep, out_score, out_idx, st);
 }

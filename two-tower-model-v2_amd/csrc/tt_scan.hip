@@ -99,14 +99,25 @@ __device__ __noinline__ void compact_query(float* sc, uint16_t* ro, int* cntp, f
   wave_sync();
 }
 
+template <typename IdxT>
+__device__ void merge_lists_block(uint64_t* buf, int& bcnt, uint32_t& th_key, int qid,
+                                  const float* __restrict__ in_s, const IdxT* __restrict__ in_i,
+                                  const int* __restrict__ in_c, int n_lists,
+                                  int64_t list_stride_q, int64_t list_stride_l, int k_in, int k,
+                                  int64_t row_base, float* out_s, int64_t* out_i,
+                                  const int* qsel);
+constexpr int MG_CAP = 8192;
+
 template <int EP, class Cfg>
 __global__ __launch_bounds__(64 * Cfg::kWaves, ((EP <= 384 && Cfg::kWaves > 1) ? 2 : 1)) void k_scan_topk_f32(
     const float* __restrict__ db, int64_t n, int64_t ld_db, const float* __restrict__ q,
     int nq, int64_t ld_q, int k, int rows_per_slab, int n_slabs,
     float* __restrict__ ws_score, int* __restrict__ ws_row, int* __restrict__ ws_cnt,
-    const int* __restrict__ qsel, const int* __restrict__ qsel_n) {
+    const int* __restrict__ qsel, const int* __restrict__ qsel_n, int* __restrict__ done,
+    int64_t row_base, float* __restrict__ out_s, int64_t* __restrict__ out_i) {
   constexpr int SC_QPB = Cfg::kQPB, SC_CAND = Cfg::kCand;
-  __shared__ typename Cfg::Smem sm;
+  static_assert(sizeof(typename Cfg::Smem) >= MG_CAP * 8, "merge buffer aliases the scan state");
+  __shared__ __attribute__((aligned(16))) typename Cfg::Smem sm;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ql = lane & 15, g = lane >> 4;
   const int qt = blockIdx.x, slab = blockIdx.y;
@@ -201,6 +212,28 @@ __global__ __launch_bounds__(64 * Cfg::kWaves, ((EP <= 384 && Cfg::kWaves > 1) ?
                                &sm.theta[w][qq], k, lane, ws_score + base * k,
                                ws_row + base * k, ws_cnt + base, (int)s0);
   }
+  if (!done) return;
+  // Fused merge (the filter's exact fallback): the last slab block of query tile qt to finish
+  // merges the tile's queries -- one launch instead of scan + k_merge_lists, and with no
+  // query flagged (the common case) every block has already returned above.  done[qt] is
+  // zeroed by the search's per-query init; agent-scope fences publish the slab lists across
+  // XCDs (their L2s are not coherent with each other).
+  __shared__ int last, bcnt;
+  __shared__ uint32_t th_key;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(&done[qt], 1) == n_slabs - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  uint64_t* buf = reinterpret_cast<uint64_t*>(&sm);  // the scan state is dead
+  for (int qq = 0; qq < SC_QPB; ++qq) {
+    const int qg = qt * SC_QPB + qq;
+    if (qg >= nq) break;
+    merge_lists_block<int>(buf, bcnt, th_key, qg, ws_score, ws_row, ws_cnt, n_slabs,
+                           (int64_t)n_slabs * k, (int64_t)k, k, k, row_base, out_s, out_i, qsel);
+  }
+  if (threadIdx.x == 0) done[qt] = 0;
 }
 
 // ----------------------------------------------------------------------------- merge
@@ -209,7 +242,6 @@ __global__ __launch_bounds__(64 * Cfg::kWaves, ((EP <= 384 && Cfg::kWaves > 1) ?
 // ignored).  theta = max over FULL lists (cnt == k_in >= k) of the k-th entry is a
 // lower bound of the global k-th best; entries below it are skipped.  Survivors are
 // collected in LDS in rounds (sort + truncate when the buffer would overflow).
-constexpr int MG_CAP = 8192;
 constexpr int MG_CHUNK = 4096;
 
 __device__ void block_bitonic_desc(uint64_t* buf, int n_pow2) {
@@ -237,20 +269,14 @@ __device__ __forceinline__ int next_pow2(int v) {
   return p;
 }
 
+// One query's merge by the whole block (any block size); buf = MG_CAP keys of LDS.
 template <typename IdxT>
-__global__ __launch_bounds__(256) void k_merge_lists(const float* __restrict__ in_s,
-                                                     const IdxT* __restrict__ in_i,
-                                                     const int* __restrict__ in_c,
-                                                     int n_lists, int64_t list_stride_q,
-                                                     int64_t list_stride_l, int k_in, int k,
-                                                     int64_t row_base, float* out_s,
-                                                     int64_t* out_i, const int* qsel,
-                                                     const int* qsel_n) {
-  __shared__ uint64_t buf[MG_CAP];
-  __shared__ int bcnt;
-  __shared__ uint32_t th_key;
-  const int qid = blockIdx.x;
-  if (qsel && qid >= *qsel_n) return;
+__device__ void merge_lists_block(uint64_t* buf, int& bcnt, uint32_t& th_key, int qid,
+                                  const float* __restrict__ in_s, const IdxT* __restrict__ in_i,
+                                  const int* __restrict__ in_c, int n_lists,
+                                  int64_t list_stride_q, int64_t list_stride_l, int k_in, int k,
+                                  int64_t row_base, float* out_s, int64_t* out_i,
+                                  const int* qsel) {
   const int64_t orow = qsel ? qsel[qid] : qid;
   const float* qs = in_s + (int64_t)qid * list_stride_q;
   const IdxT* qix = in_i + (int64_t)qid * list_stride_q;
@@ -317,6 +343,25 @@ __global__ __launch_bounds__(256) void k_merge_lists(const float* __restrict__ i
     out_s[orow * k + i] = s;
     out_i[orow * k + i] = ix;
   }
+  __syncthreads();  // buf / bcnt / th_key free for the block's next query
+}
+
+template <typename IdxT>
+__global__ __launch_bounds__(256) void k_merge_lists(const float* __restrict__ in_s,
+                                                     const IdxT* __restrict__ in_i,
+                                                     const int* __restrict__ in_c,
+                                                     int n_lists, int64_t list_stride_q,
+                                                     int64_t list_stride_l, int k_in, int k,
+                                                     int64_t row_base, float* out_s,
+                                                     int64_t* out_i, const int* qsel,
+                                                     const int* qsel_n) {
+  __shared__ uint64_t buf[MG_CAP];
+  __shared__ int bcnt;
+  __shared__ uint32_t th_key;
+  const int qid = blockIdx.x;
+  if (qsel && qid >= *qsel_n) return;
+  merge_lists_block<IdxT>(buf, bcnt, th_key, qid, in_s, in_i, in_c, n_lists, list_stride_q,
+                          list_stride_l, k_in, k, row_base, out_s, out_i, qsel);
 }
 
 // ----------------------------------------------------------------------------- host
@@ -374,7 +419,7 @@ static int scan_f32_impl(const float* db, int64_t n, int32_t d, int64_t ld_db,
                          int64_t row_base, const float* q, int32_t nq, int64_t ld_q, int32_t k,
                          const int32_t* qsel, const int32_t* qsel_n, float* out_score,
                          int64_t* out_idx, void* workspace, int64_t workspace_bytes,
-                         void* stream, void* ev_start, void* ev_stop) {
+                         void* stream, void* ev_start, void* ev_stop, int* done = nullptr) {
   TT_REQUIRE(n >= 1, "empty catalog");
   TT_REQUIRE(n <= 0x7fffffffLL, "shard rows must fit int32");
   TT_REQUIRE(nq >= 0, "nq < 0");
@@ -403,11 +448,11 @@ static int scan_f32_impl(const float* db, int64_t n, int32_t d, int64_t ld_db,
     if (wide)                                                                                \
       hipLaunchKernelGGL((k_scan_topk_f32<E, CfgWide>), grid, block, 0, st, db, n, ld_db, q, \
                          nq, ld_q, k, p.rows_per_slab, p.n_slabs, ws_s, ws_r, ws_c, qsel,    \
-                         qsel_n);                                                            \
+                         qsel_n, done, row_base, out_score, out_idx);                        \
     else                                                                                     \
       hipLaunchKernelGGL((k_scan_topk_f32<E, CfgNarrow>), grid, block, 0, st, db, n, ld_db,  \
                          q, nq, ld_q, k, p.rows_per_slab, p.n_slabs, ws_s, ws_r, ws_c, qsel, \
-                         qsel_n);                                                            \
+                         qsel_n, done, row_base, out_score, out_idx);                        \
     break;
   if (ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "tt_scan_topk_f32_timed: hipEventRecord(start) failed");
@@ -426,6 +471,7 @@ static int scan_f32_impl(const float* db, int64_t n, int32_t d, int64_t ld_db,
   if (rc) return rc;
   if (ev_stop && hipEventRecord((hipEvent_t)ev_stop, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "tt_scan_topk_f32_timed: hipEventRecord(stop) failed");
+  if (done) return TT_OK;  // merged inside the scan launch
   hipLaunchKernelGGL(k_merge_lists<int>, dim3(nq), dim3(256), 0, st, ws_s, ws_r, ws_c,
                      p.n_slabs, (int64_t)p.n_slabs * k, (int64_t)k, k, k, row_base, out_score,
                      out_idx, qsel, qsel_n);
@@ -462,6 +508,20 @@ extern "C" int tt_scan_topk_f32_select(const float* db, int64_t n, int32_t d, in
   return scan_f32_impl(db, n, d, ld_db, row_base, q, nq, ld_q, k, qsel, qsel_n, out_score,
                        out_idx, workspace, workspace_bytes, stream, nullptr, nullptr);
 }
+
+namespace tt {
+// The bf16 filter's exact fallback (tt_filter.hip): the select-mode scan with the slab merge
+// fused into the scan launch (done: >= one zeroed counter per flagged-query tile).
+int scan_f32_select_fused(const float* db, int64_t n, int32_t d, int64_t ld_db, int64_t row_base,
+                          const float* q, int32_t nq, int64_t ld_q, int32_t k,
+                          const int32_t* qsel, const int32_t* qsel_n, int* done,
+                          float* out_score, int64_t* out_idx, void* workspace,
+                          int64_t workspace_bytes, void* stream) {
+  TT_REQUIRE(qsel && qsel_n && done, "qsel / qsel_n / done must be device pointers");
+  return scan_f32_impl(db, n, d, ld_db, row_base, q, nq, ld_q, k, qsel, qsel_n, out_score,
+                       out_idx, workspace, workspace_bytes, stream, nullptr, nullptr, done);
+}
+}  // namespace tt
 
 extern "C" int tt_topk_merge_f32(const float* in_score, const int64_t* in_idx, int32_t n_lists,
                                  int32_t nq, int32_t k_in, int32_t k, float* out_score,
