@@ -1808,11 +1808,15 @@ __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, in
 // Sharded finish: a shard's part of a query's band is small (~1/W of it: ~25 rows at W = 8),
 // and the block-per-query k_rerank (74 KB LDS: 2 blocks, i.e. 2 queries, per CU; a block-wide
 // bitonic sort) spent 1.7 ms on 80k such queries.  Here one WAVE owns a query: the cut filter
-// compacts the kept band rows by ballot into a wave-private list (<= RW_CAP; more -> the
-// query takes this shard's exact fallback, which keeps the protocol sound), the rows are
+// compacts the kept band rows by ballot into a wave-private list of RW_CAP keys, the rows are
 // scored by the staged 64-row gather of k_rerank (same canonical FMA order, bit-identical),
-// and each kept row's output slot is its rank (#keys ahead) -- no sort, no block barrier.
+// and each kept row's output slot is its rank (#keys ahead) -- no sort, no block barrier.  A
+// shard whose part of the band outgrows the list (W = 2: ~8% of iid queries kept > 256 rows
+// and used to take the shard's exact f32 fallback, 1642 of 20k queries per step) scores what
+// it holds and keeps only its top k (rank < k: a row of the query's top k has fewer than k
+// keys ahead of it in any subset), then goes on appending.
 constexpr int RW_CAP = 256;
+static_assert(RW_CAP - 64 >= FL_KMAX, "a reduced list leaves room for a 64-key chunk");
 template <int EP>
 __global__ __launch_bounds__(256) void k_rerank_wave(
     const float* __restrict__ db, int64_t ld, const float* __restrict__ q, int64_t ldq,
@@ -1832,84 +1836,107 @@ __global__ __launch_bounds__(256) void k_rerank_wave(
   const int nb_all = band_n[qid];
   const uint64_t* qband = band + (int64_t)qid * BAND_CAP;
   const float c = cut[qid];
-  int nb = 0;
+  const int sub = lane >> 4, piece = lane & 15;
+  int nb = 0, ns = 0;  // kept keys buf[0, nb); buf[0, ns) already hold exact-score keys
+  // exact keys for buf[from, nb) (band keys -> (canonical f32 score, row) keys, in place)
+  auto score_from = [&](int from) __attribute__((always_inline)) {
+    wave_sync();
+    for (int e0 = from; e0 < nb; e0 += 64) {
+      const int ej = e0 + lane;
+      const uint32_t rj = key_row(buf[ej < nb ? ej : e0]);
+      const float* rp[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t r = (uint32_t)__shfl((int)rj, 4 * i + sub, 64);
+        rp[i] = db + (int64_t)r * ld + 4 * piece;
+      }
+      constexpr int NC = EP / 64;
+      float acc = 0.0f;
+      f32x4 v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = *(const f32x4*)rp[i];
+#pragma unroll 1
+      for (int cc = 0; cc < NC; ++cc) {
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = 4 * i + sub;
+          *(f32x4*)(st + row * 256 + 16 * (piece ^ (row & 15))) = v[i];
+        }
+        asm volatile("" ::: "memory");
+        if (cc + 1 < NC) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) v[i] = *(const f32x4*)(rp[i] + 64 * (cc + 1));
+        }
+        const char* my = st + lane * 256;
+        const int sw = lane & 15;
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+          const f32x4 x0 = *(const f32x4*)(my + 16 * ((4 * tt + 0) ^ sw));
+          const f32x4 x1 = *(const f32x4*)(my + 16 * ((4 * tt + 1) ^ sw));
+          const f32x4 x2 = *(const f32x4*)(my + 16 * ((4 * tt + 2) ^ sw));
+          const f32x4 x3 = *(const f32x4*)(my + 16 * ((4 * tt + 3) ^ sw));
+          const float* qt = qs + 64 * cc + 16 * tt;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            acc = fmaf(x0[i], qt[0 + i], acc);
+            acc = fmaf(x1[i], qt[4 + i], acc);
+            acc = fmaf(x2[i], qt[8 + i], acc);
+            acc = fmaf(x3[i], qt[12 + i], acc);
+          }
+        }
+        wave_sync();  // every lane's chain read this chunk before the next one is staged
+      }
+      // the key can replace the band key in place: lane ej owns slot ej (read above)
+      if (ej < nb) buf[ej] = acc != acc ? 0ull : make_key(acc, rj);
+    }
+    ns = nb;
+    wave_sync();
+  };
+  // rank of key me at position e among buf[0, nb) (keys of distinct rows are distinct; equal
+  // keys -- NaN scores, key 0 -- are ordered by position)
+  auto rank_of = [&](uint64_t me, int e) __attribute__((always_inline)) {
+    int rank = 0;
+    for (int j = 0; j < nb; ++j) {
+      const uint64_t o = buf[j];
+      rank += (o > me || (o == me && j < e)) ? 1 : 0;
+    }
+    return rank;
+  };
   for (int e0 = 0; e0 < nb_all; e0 += 64) {
+    if (nb > RW_CAP - 64) {  // rare: keep the top k of the list (all scored) and go on
+      score_from(ns);
+      uint64_t mine[RW_CAP / 64];
+      int rk[RW_CAP / 64];
+#pragma unroll
+      for (int cc = 0; cc < RW_CAP / 64; ++cc) {
+        const int e = 64 * cc + lane;
+        mine[cc] = e < nb ? buf[e] : 0ull;
+        rk[cc] = e < nb ? rank_of(mine[cc], e) : RW_CAP;
+      }
+      wave_sync();
+#pragma unroll
+      for (int cc = 0; cc < RW_CAP / 64; ++cc)
+        if (rk[cc] < k) buf[rk[cc]] = mine[cc];
+      nb = ns = nb < k ? nb : k;
+      wave_sync();
+    }
     const int e = e0 + lane;
     const uint64_t key = e < nb_all ? qband[e] : 0ull;
     const bool keep = e < nb_all && key_float((uint32_t)(key >> 32)) >= c;
     const uint64_t bm = __ballot(keep);
     const int pos = nb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
-    if (keep && pos < RW_CAP) buf[pos] = key;
+    if (keep) buf[pos] = key;
     nb += (int)__popcll(bm);
   }
-  if (nb > RW_CAP) {  // this shard's part of the band is too large for the wave list
-    if (lane == 0) flag_query(qid, flags, qsel, qsel_n);
-    return;
-  }
-  wave_sync();
-  const int sub = lane >> 4, piece = lane & 15;
-  for (int e0 = 0; e0 < nb; e0 += 64) {
-    const int ej = e0 + lane;
-    const uint32_t rj = key_row(buf[ej < nb ? ej : e0]);
-    const float* rp[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const uint32_t r = (uint32_t)__shfl((int)rj, 4 * i + sub, 64);
-      rp[i] = db + (int64_t)r * ld + 4 * piece;
-    }
-    constexpr int NC = EP / 64;
-    float acc = 0.0f;
-    f32x4 v[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = *(const f32x4*)rp[i];
-#pragma unroll 1
-    for (int cc = 0; cc < NC; ++cc) {
-      asm volatile("" ::: "memory");
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int row = 4 * i + sub;
-        *(f32x4*)(st + row * 256 + 16 * (piece ^ (row & 15))) = v[i];
-      }
-      asm volatile("" ::: "memory");
-      if (cc + 1 < NC) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = *(const f32x4*)(rp[i] + 64 * (cc + 1));
-      }
-      const char* my = st + lane * 256;
-      const int sw = lane & 15;
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt) {
-        const f32x4 x0 = *(const f32x4*)(my + 16 * ((4 * tt + 0) ^ sw));
-        const f32x4 x1 = *(const f32x4*)(my + 16 * ((4 * tt + 1) ^ sw));
-        const f32x4 x2 = *(const f32x4*)(my + 16 * ((4 * tt + 2) ^ sw));
-        const f32x4 x3 = *(const f32x4*)(my + 16 * ((4 * tt + 3) ^ sw));
-        const float* qt = qs + 64 * cc + 16 * tt;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          acc = fmaf(x0[i], qt[0 + i], acc);
-          acc = fmaf(x1[i], qt[4 + i], acc);
-          acc = fmaf(x2[i], qt[8 + i], acc);
-          acc = fmaf(x3[i], qt[12 + i], acc);
-        }
-      }
-      wave_sync();  // every lane's chain read this chunk before the next one is staged
-    }
-    // the key can replace the band key in place: lane ej owns slot ej (read above)
-    if (ej < nb) buf[ej] = acc != acc ? 0ull : make_key(acc, rj);
-  }
-  wave_sync();
-  // output slot = rank (keys of distinct rows are distinct; equal keys -- NaN scores, key 0 --
-  // are ordered by position); slots nb .. k-1 stay (-inf, -1)
+  score_from(ns);
+  // output slot = rank; slots nb .. k-1 stay (-inf, -1)
   for (int e0 = 0; e0 < nb; e0 += 64) {
     const int e = e0 + lane;
     if (e < nb) {
       const uint64_t me = buf[e];
-      int rank = 0;
-      for (int j = 0; j < nb; ++j) {
-        const uint64_t o = buf[j];
-        rank += (o > me || (o == me && j < e)) ? 1 : 0;
-      }
+      const int rank = rank_of(me, e);
       if (rank < k) {
         out_s[(int64_t)qid * k + rank] = me ? key_score(me) : -__builtin_huge_valf();
         out_i[(int64_t)qid * k + rank] = me ? row_base + (int64_t)key_row(me) : -1;
