@@ -178,21 +178,26 @@ def test_bf16_filter_no_fallback_on_iid_data(K, nq):
     assert K.filter_fallback_count(ws, n, d, nq, k) == 0
 
 
+@pytest.mark.parametrize("nq", [20, 150, 2100])
 @pytest.mark.parametrize("resid", [0.5, 4.0])
-def test_bf16_filter_fallback_is_exact(K, oracle_mod, resid):
+def test_bf16_filter_fallback_is_exact(K, oracle_mod, resid, nq):
     """A loose bound overflows the candidate lists: every query then takes the exact
-    fallback launch, and the results must not change."""
+    fallback launch, and the results must not change.  The fallback merges its slab lists
+    inside the scan launch (the last slab block of each 64-query tile): nq = 150 is three
+    tiles, the last ragged; 2100 is 33 tiles behind the batched (> 2048) filter path.  Run
+    twice on one workspace (the per-tile arrival counters are re-zeroed by each search)."""
     rng = np.random.default_rng(77)
-    n, d, nq, k = 30000, 384, 20, 100
+    n, d, k = 30000, 384, 100
     x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
     q = oracle_mod.l2norm_rows(rng.standard_normal((nq, d)).astype(np.float32), 0)
     db = dev_rows(x)
     ws = torch.empty(K.filter_workspace_bytes(n, d, nq, k), dtype=torch.uint8, device="cuda")
-    s, i = K.scan_topk_bf16(db, db.to(torch.bfloat16), n, d, dev_rows(q), k, (1.0, resid),
-                            workspace=ws)
     rs, ri = oracle_mod.scan_topk(x, q, k)
-    assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
-    assert K.filter_fallback_count(ws, n, d, nq, k) == nq  # every query took the fallback
+    for _ in range(2):
+        s, i = K.scan_topk_bf16(db, db.to(torch.bfloat16), n, d, dev_rows(q), k, (1.0, resid),
+                                workspace=ws)
+        assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
+        assert K.filter_fallback_count(ws, n, d, nq, k) == nq  # every query fell back
 
 
 @pytest.mark.parametrize("nq", [1, 5, 64])
