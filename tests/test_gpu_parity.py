@@ -347,6 +347,25 @@ def test_gather_weighted_avg_bit_exact(K, oracle_mod):
     assert np.array_equal(out[:, :384], oracle_mod.gather_weighted_avg_l2(table, hist, w))
 
 
+@pytest.mark.parametrize("d,s", [(64, 3), (128, 70), (640, 5), (1000, 9), (1024, 66)])
+def test_weighted_avg_register_shapes_bit_exact(K, oracle_mod, d, s):
+    """Every per-lane register shape of k_weighted_avg_l2 (PER 2/6/12/16 elements, 4/2/1 rows
+    read ahead), history lengths that are not a multiple of the read-ahead and span two
+    64-row chunks, invalid history ids; dense and gathered forms bit-exact vs the oracle."""
+    rng = np.random.default_rng(d + s)
+    b = 37
+    items = rng.standard_normal((b, s, d)).astype(np.float32)
+    w = gi.event_weights(rng, (b, s))
+    got = K.weighted_avg_l2(torch.from_numpy(items).cuda(), torch.from_numpy(w).cuda()).cpu().numpy()
+    assert np.array_equal(got, oracle_mod.weighted_avg_l2(items, w))
+    table = rng.standard_normal((500, d)).astype(np.float32)
+    hist = rng.integers(-1, 500, (b, s))
+    out = K.gather_weighted_avg_l2(torch.from_numpy(table).cuda(), d,  # ld = d (up to 1024)
+                                   torch.from_numpy(hist).cuda(),
+                                   torch.from_numpy(w).cuda()).cpu().numpy()
+    assert np.array_equal(out[:, :d], oracle_mod.gather_weighted_avg_l2(table, hist, w))
+
+
 @pytest.mark.parametrize("case", [c for c, s in gi.BUYER_CASES.items()
                                   if s["method"] == "attention"])
 def test_attention_vs_oracle_and_reference(K, oracle_mod, golden, case):

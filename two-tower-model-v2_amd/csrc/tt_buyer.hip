@@ -35,18 +35,21 @@ __device__ __forceinline__ void normalize_store(float* row_s, int d, int depth, 
 }
 
 // items: dense [b][s][d] (gather == false) or table rows selected by hist (gather == true).
-// One wave per buyer; lane owns elements e = lane + 64 i.  The s history rows are walked in
-// order (canonical accumulation order), 64 at a time: lane j of a chunk computes that row's
-// normalised weight and id once, and __shfl broadcasts them, so the loop body is only the
-// row loads (all i of a row issued together, coalesced 256-B wave loads) and the FMAs.
-template <bool GATHER>
+// One wave per buyer; lane owns elements e = lane + 64 i, i < PER (PER = ceil(d / 64), a
+// template so d = 384 holds 6 accumulators, not 16).  The s history rows are walked in order
+// (canonical accumulation order), 64 at a time: lane j of a chunk computes that row's
+// normalised weight and id once, and __shfl broadcasts them.  The loads of RU consecutive
+// rows are issued before their FMAs (RU x PER coalesced 256-B wave loads in flight): one HBM
+// round trip per RU rows instead of per row -- the gather was latency-bound (one row per
+// round trip: 79 us for 10k buyers x 20 rows x 1.5 KB).  Arithmetic order is unchanged.
+template <bool GATHER, int PER>
 __global__ __launch_bounds__(256) void k_weighted_avg_l2(const float* __restrict__ src,
                                                          int64_t ld_src, int64_t n_table,
                                                          const int64_t* __restrict__ hist,
                                                          const float* __restrict__ w, int64_t b,
                                                          int s, int d, float* __restrict__ out,
                                                          int64_t ld_out, int depth) {
-  constexpr int PER = BY_MAXD / 64;
+  constexpr int RU = PER <= 6 ? 4 : PER <= 12 ? 2 : 1;
   __shared__ float buf[4][BY_MAXD];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float* row_s = buf[wv];
@@ -71,19 +74,26 @@ __global__ __launch_bounds__(256) void k_weighted_avg_l2(const float* __restrict
           my_r = bi * s + j0 + lane;
         }
       }
-      for (int jj = 0; jj < jn; ++jj) {
-        const float nw = __shfl(my_nw, jj, 64);
-        const int64_t r = (int64_t)(((uint64_t)(uint32_t)__shfl((int)(my_r >> 32), jj, 64) << 32) |
-                                    (uint32_t)__shfl((int)my_r, jj, 64));
-        const float* xr = GATHER ? src + r * ld_src : src + r * (int64_t)d;
-        float x[PER];
+      for (int jj0 = 0; jj0 < jn; jj0 += RU) {
+        float x[RU][PER], nw[RU];
 #pragma unroll
-        for (int i = 0; i < PER; ++i) {
-          const int e = lane + 64 * i;
-          x[i] = (r >= 0 && e < d) ? xr[e] : 0.0f;
+        for (int u = 0; u < RU; ++u) {
+          const int jj = jj0 + u < jn ? jj0 + u : jn - 1;  // past jn: a repeat, never added
+          nw[u] = __shfl(my_nw, jj, 64);
+          const int64_t r = (int64_t)(((uint64_t)(uint32_t)__shfl((int)(my_r >> 32), jj, 64) << 32) |
+                                      (uint32_t)__shfl((int)my_r, jj, 64));
+          const float* xr = GATHER ? src + r * ld_src : src + r * (int64_t)d;
+#pragma unroll
+          for (int i = 0; i < PER; ++i) {
+            const int e = lane + 64 * i;
+            x[u][i] = (r >= 0 && e < d) ? xr[e] : 0.0f;
+          }
         }
 #pragma unroll
-        for (int i = 0; i < PER; ++i) acc[i] = acc[i] + __fmul_rn(x[i], nw);
+        for (int u = 0; u < RU; ++u)
+          if (jj0 + u < jn)
+#pragma unroll
+            for (int i = 0; i < PER; ++i) acc[i] = acc[i] + __fmul_rn(x[u][i], nw[u]);
       }
     }
 #pragma unroll
@@ -96,6 +106,22 @@ __global__ __launch_bounds__(256) void k_weighted_avg_l2(const float* __restrict
     for (int e = d + lane; e < ld_out; e += 64) out[bi * ld_out + e] = 0.0f;
     wave_sync();
   }
+}
+
+// launch k_weighted_avg_l2 with the smallest PER that covers d (d <= BY_MAXD)
+template <bool GATHER>
+static void launch_weighted_avg(hipStream_t st, const float* src, int64_t ld_src, int64_t n_table,
+                                const int64_t* hist, const float* w, int64_t b, int s, int d,
+                                float* out, int64_t ld_out, int depth, unsigned grid) {
+  const int per = (d + 63) / 64;
+#define TT_WAVG(P)                                                                       \
+  hipLaunchKernelGGL((k_weighted_avg_l2<GATHER, P>), dim3(grid), dim3(256), 0, st, src, \
+                     ld_src, n_table, hist, w, b, s, d, out, ld_out, depth)
+  if (per <= 2) TT_WAVG(2);
+  else if (per <= 6) TT_WAVG(6);
+  else if (per <= 12) TT_WAVG(12);
+  else TT_WAVG(16);
+#undef TT_WAVG
 }
 
 // attention aggregation: one block (256 threads) per buyer; h <= 256, d <= BY_MAXD.
@@ -172,9 +198,8 @@ extern "C" int tt_weighted_avg_l2_f32(const float* items, int64_t b, int32_t s, 
   TT_REQUIRE(b >= 0 && s >= 1 && d >= 1 && ld_out >= d, "bad sizes");
   TT_REQUIRE(d <= BY_MAXD, "d > 1024");
   if (b == 0) return TT_OK;
-  hipLaunchKernelGGL(k_weighted_avg_l2<false>, dim3(grid_for(b, 4, 16384)), dim3(256), 0,
-                     (hipStream_t)stream, items, (int64_t)d, (int64_t)0, (const int64_t*)nullptr,
-                     w, b, s, d, out, ld_out, pw_perfect_depth(d));
+  launch_weighted_avg<false>((hipStream_t)stream, items, (int64_t)d, (int64_t)0, nullptr, w, b,
+                             s, d, out, ld_out, pw_perfect_depth(d), grid_for(b, 4, 16384));
   return check_launch("tt_weighted_avg_l2_f32");
 }
 
@@ -185,9 +210,8 @@ extern "C" int tt_gather_weighted_avg_l2_f32(const float* table, int64_t n_table
   TT_REQUIRE(b >= 0 && s >= 1 && d >= 1 && ld_out >= d && ld_table >= d, "bad sizes");
   TT_REQUIRE(d <= BY_MAXD, "d > 1024");
   if (b == 0) return TT_OK;
-  hipLaunchKernelGGL(k_weighted_avg_l2<true>, dim3(grid_for(b, 4, 16384)), dim3(256), 0,
-                     (hipStream_t)stream, table, ld_table, n_table, hist, w, b, s, d, out,
-                     ld_out, pw_perfect_depth(d));
+  launch_weighted_avg<true>((hipStream_t)stream, table, ld_table, n_table, hist, w, b, s, d,
+                            out, ld_out, pw_perfect_depth(d), grid_for(b, 4, 16384));
   return check_launch("tt_gather_weighted_avg_l2_f32");
 }
 

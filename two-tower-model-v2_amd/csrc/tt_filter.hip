@@ -2024,6 +2024,10 @@ static bool tmax_first_disabled() {  // TT_FILTER_TMAX_FIRST=0: full sample ladd
   return off;
 }
 constexpr int64_t SW_CAP_TILES = SW_CAP - 64;  // first-level tiles per query, with margin
+#ifndef TT_SAMPLE_J_ADD
+#define TT_SAMPLE_J_ADD 12  // J = ceil(k / 8) + TT_SAMPLE_J_ADD (plan_filter)
+#endif
+TT_CHECK_EXP(TT_SAMPLE_J_ADD != 12, "TT_SAMPLE_J_ADD");
 static int64_t ring_tr(int ep) {                 // rows per k_filter_ring tile
   return ep == 64 ? RingCfg<64>::TR : ep == 128 ? RingCfg<128>::TR : ep == 256 ? RingCfg<256>::TR
          : ep == 384 ? RingCfg<384>::TR : ep == 512 ? RingCfg<512>::TR : RingCfg<768>::TR;
@@ -2073,7 +2077,7 @@ static FilterPlan plan_filter_uncached(int64_t n, int nq, int k, int ep) {
   FilterPlan p;
   // ~16*J full-catalog rows lie above a_J(stride-16 sample); J = k/8 + 12 keeps that count
   // >= k with ~3.5 sigma margin on iid scores (fewer only under heavy clustering -> fallback)
-  p.J = (k + 7) / 8 + 12;
+  p.J = (k + 7) / 8 + TT_SAMPLE_J_ADD;
   if (p.J > k) p.J = k;
   int64_t strides[8];
   int nl = 0;
