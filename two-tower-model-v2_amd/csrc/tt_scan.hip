@@ -114,13 +114,14 @@ __global__ __launch_bounds__(64 * Cfg::kWaves, ((EP <= 384 && Cfg::kWaves > 1) ?
     int nq, int64_t ld_q, int k, int rows_per_slab, int n_slabs,
     float* __restrict__ ws_score, int* __restrict__ ws_row, int* __restrict__ ws_cnt,
     const int* __restrict__ qsel, const int* __restrict__ qsel_n, int* __restrict__ done,
-    int64_t row_base, float* __restrict__ out_s, int64_t* __restrict__ out_i) {
+    int64_t row_base, float* __restrict__ out_s, int64_t* __restrict__ out_i, int qt_off,
+    int done_off) {
   constexpr int SC_QPB = Cfg::kQPB, SC_CAND = Cfg::kCand;
   static_assert(sizeof(typename Cfg::Smem) >= MG_CAP * 8, "merge buffer aliases the scan state");
   __shared__ __attribute__((aligned(16))) typename Cfg::Smem sm;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ql = lane & 15, g = lane >> 4;
-  const int qt = blockIdx.x, slab = blockIdx.y;
+  const int qt = blockIdx.x + qt_off, slab = blockIdx.y;
   if (qsel) nq = *qsel_n;  // fallback mode: slots 0..nq-1 map to queries qsel[slot]
   if (qt * SC_QPB >= nq) return;
   const int qi = qt * SC_QPB + w * SC_QPW + ql;
@@ -222,7 +223,7 @@ __global__ __launch_bounds__(64 * Cfg::kWaves, ((EP <= 384 && Cfg::kWaves > 1) ?
   __shared__ uint32_t th_key;
   __threadfence();
   __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(&done[qt], 1) == n_slabs - 1;
+  if (threadIdx.x == 0) last = atomicAdd(&done[qt + done_off], 1) == n_slabs - 1;
   __syncthreads();
   if (!last) return;
   __threadfence();
@@ -233,7 +234,7 @@ __global__ __launch_bounds__(64 * Cfg::kWaves, ((EP <= 384 && Cfg::kWaves > 1) ?
     merge_lists_block<int>(buf, bcnt, th_key, qg, ws_score, ws_row, ws_cnt, n_slabs,
                            (int64_t)n_slabs * k, (int64_t)k, k, k, row_base, out_s, out_i, qsel);
   }
-  if (threadIdx.x == 0) done[qt] = 0;
+  if (threadIdx.x == 0) done[qt + done_off] = 0;
 }
 
 // ----------------------------------------------------------------------------- merge
@@ -371,9 +372,11 @@ struct ScanPlan {
 
 static bool wide_k(int k) { return k > CfgNarrow::kKMax; }
 
+static int qpb_of(int k) { return wide_k(k) ? CfgWide::kQPB : CfgNarrow::kQPB; }
+
 static ScanPlan plan_scan(int64_t n, int nq, int k) {
   ScanPlan p;
-  const int qpb = wide_k(k) ? CfgWide::kQPB : CfgNarrow::kQPB;
+  const int qpb = qpb_of(k);
   p.qt = (nq + qpb - 1) / qpb;
   // enough blocks to fill 256 CUs x 2, slabs no longer than SC_MAX_SLAB_ROWS
   int64_t s_min = (n + SC_MAX_SLAB_ROWS - 1) / SC_MAX_SLAB_ROWS;
@@ -411,6 +414,10 @@ extern "C" int tt_scan_workspace_bytes(int64_t n, int32_t d, int32_t nq, int32_t
   const ScanPlan p = plan_scan(n, nq, k);
   const int64_t entries = (int64_t)nq * p.n_slabs * k;
   int64_t b = entries * 8 + (int64_t)nq * p.n_slabs * 4;
+  if (p.qt > 1) {  // the fused fallback's first query tile, on its own wide slab plan
+    const ScanPlan pa = plan_scan(n, qpb_of(k), k);
+    b += (int64_t)qpb_of(k) * pa.n_slabs * (8 * (int64_t)k + 4);
+  }
   *bytes = (b + 255) / 256 * 256;
   return TT_OK;
 }
@@ -442,33 +449,54 @@ static int scan_f32_impl(const float* db, int64_t n, int32_t d, int64_t ld_db,
   int* ws_c = ws_r + entries;
   hipStream_t st = (hipStream_t)stream;
   const bool wide = wide_k(k);
-  dim3 grid(p.qt, p.n_slabs), block(wide ? 64 * CfgWide::kWaves : 64 * CfgNarrow::kWaves);
-#define TT_SCAN_CASE(E)                                                                      \
-  case E:                                                                                    \
-    if (wide)                                                                                \
-      hipLaunchKernelGGL((k_scan_topk_f32<E, CfgWide>), grid, block, 0, st, db, n, ld_db, q, \
-                         nq, ld_q, k, p.rows_per_slab, p.n_slabs, ws_s, ws_r, ws_c, qsel,    \
-                         qsel_n, done, row_base, out_score, out_idx);                        \
-    else                                                                                     \
-      hipLaunchKernelGGL((k_scan_topk_f32<E, CfgNarrow>), grid, block, 0, st, db, n, ld_db,  \
-                         q, nq, ld_q, k, p.rows_per_slab, p.n_slabs, ws_s, ws_r, ws_c, qsel, \
-                         qsel_n, done, row_base, out_score, out_idx);                        \
+  const dim3 block(wide ? 64 * CfgWide::kWaves : 64 * CfgNarrow::kWaves);
+  // launch (tiles [qt0, qt1) of the plan ps, lists at (s_, r_, c_), done counters + doff)
+  auto launch = [&](const ScanPlan& ps, int qt0, int qt1, float* s_, int* r_, int* c_,
+                    int doff) -> int {
+    const dim3 grid(qt1 - qt0, ps.n_slabs);
+#define TT_SCAN_CASE(E)                                                                       \
+  case E:                                                                                     \
+    if (wide)                                                                                 \
+      hipLaunchKernelGGL((k_scan_topk_f32<E, CfgWide>), grid, block, 0, st, db, n, ld_db, q,  \
+                         nq, ld_q, k, ps.rows_per_slab, ps.n_slabs, s_, r_, c_, qsel, qsel_n, \
+                         done, row_base, out_score, out_idx, qt0, doff);                      \
+    else                                                                                      \
+      hipLaunchKernelGGL((k_scan_topk_f32<E, CfgNarrow>), grid, block, 0, st, db, n, ld_db,   \
+                         q, nq, ld_q, k, ps.rows_per_slab, ps.n_slabs, s_, r_, c_, qsel,      \
+                         qsel_n, done, row_base, out_score, out_idx, qt0, doff);              \
     break;
+    switch (ep) {
+      TT_SCAN_CASE(64)
+      TT_SCAN_CASE(128)
+      TT_SCAN_CASE(256)
+      TT_SCAN_CASE(384)
+      TT_SCAN_CASE(512)
+      TT_SCAN_CASE(768)
+      default:
+        return fail(TT_ERR_UNSUPPORTED, "tt_scan_topk_f32: bad padded dim");
+    }
+#undef TT_SCAN_CASE
+    return check_launch("k_scan_topk_f32");
+  };
   if (ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "tt_scan_topk_f32_timed: hipEventRecord(start) failed");
-  switch (ep) {
-    TT_SCAN_CASE(64)
-    TT_SCAN_CASE(128)
-    TT_SCAN_CASE(256)
-    TT_SCAN_CASE(384)
-    TT_SCAN_CASE(512)
-    TT_SCAN_CASE(768)
-    default:
-      return fail(TT_ERR_UNSUPPORTED, "tt_scan_topk_f32: bad padded dim");
+  int rc;
+  if (done && p.qt > 1) {
+    // Fused fallback of a large batch: the flagged queries are compacted into slots
+    // 0 .. *qsel_n, so a handful of them all sit in query tile 0.  On the batch's plan that
+    // tile would get p.n_slabs blocks (16 at 1M rows: 2 flagged queries of a 10k batch cost
+    // 16 ms); tile 0 runs on its own one-tile plan instead (up to 512 slabs, lists after the
+    // batch plan's, done counter p.qt), the other tiles on the batch plan.  Both launches
+    // exit at once when nothing (or nothing past tile 0) is flagged.
+    const ScanPlan pa = plan_scan(n, qpb_of(k), k);
+    float* sa = (float*)(ws_c + (int64_t)nq * p.n_slabs);
+    int* ra = (int*)(sa + (int64_t)qpb_of(k) * pa.n_slabs * k);
+    int* ca = ra + (int64_t)qpb_of(k) * pa.n_slabs * k;
+    if ((rc = launch(pa, 0, 1, sa, ra, ca, p.qt))) return rc;
+    if ((rc = launch(p, 1, p.qt, ws_s, ws_r, ws_c, 0))) return rc;
+  } else if ((rc = launch(p, 0, p.qt, ws_s, ws_r, ws_c, 0))) {
+    return rc;
   }
-#undef TT_SCAN_CASE
-  int rc = check_launch("k_scan_topk_f32");
-  if (rc) return rc;
   if (ev_stop && hipEventRecord((hipEvent_t)ev_stop, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "tt_scan_topk_f32_timed: hipEventRecord(stop) failed");
   if (done) return TT_OK;  // merged inside the scan launch
