@@ -308,6 +308,9 @@ def catalog_10m(a, dev, nq=10_000, n=10_000_000):
             "hbm_resident_gb": (x.numel() * 4 + x16.numel() * 2) / 1e9}
 
 
+CPU_MODE_A_BUYERS = 32
+
+
 def mode_a(a, dev, world, rank, search_local, k, E):
     """Mode A: EmbeddingEncoder.encode_buyer as written (src/inference/encoder.py:286-303):
     each buyer's S history texts are re-encoded by the item tower (MiniLM encoder on HIP,
@@ -368,10 +371,11 @@ def mode_a(a, dev, world, rank, search_local, k, E):
            "texts_per_s": world * B * S / dt,
            "model": "MiniLM-L12 architecture (12L/384h/12 heads/FFN 1536, vocab 250037), "
                     "seeded random weights; synthetic token ids, L ~ U[16,128]"}
+    nc = min(CPU_MODE_A_BUYERS, B)  # the CPU baseline's sample (>= 32 buyers)
     cpu_inputs = (sd, cfg, {k2: v.detach().cpu() for k2, v in it.state_dict().items()},
-                  [seqs[b * S:(b + 1) * S] for b in range(8)],
-                  [bid[b * S:(b + 1) * S] for b in range(8)],
-                  [cid[b * S:(b + 1) * S] for b in range(8)], w[:8].cpu().numpy())
+                  [seqs[b * S:(b + 1) * S] for b in range(nc)],
+                  [bid[b * S:(b + 1) * S] for b in range(nc)],
+                  [cid[b * S:(b + 1) * S] for b in range(nc)], w[:nc].cpu().numpy())
     return res, cpu_inputs
 
 
@@ -670,7 +674,7 @@ def main():
         if cpu_a is not None:
             sd_, cfg_, head_, seqs_, bid_, cid_, w_ = cpu_a
             result["mode_a"]["cpu_baseline"] = cpu_baseline.run_mode_a(
-                sd_, cfg_, head_, seqs_, bid_, cid_, w_, cat_np, K, n_buyers=8)
+                sd_, cfg_, head_, seqs_, bid_, cid_, w_, cat_np, K, n_buyers=CPU_MODE_A_BUYERS)
             result["mode_a"]["gpu_over_cpu_single"] = (
                 result["mode_a"]["value"] / result["mode_a"]["cpu_baseline"]["value"])
     if rank == 0:

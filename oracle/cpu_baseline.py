@@ -143,7 +143,7 @@ def run(table_np: np.ndarray, catalog_np: np.ndarray, hist: np.ndarray, w: np.nd
 
 
 def run_mode_a(sd, cfg, head_sd, seqs_per_buyer, brand_ids, cat_ids, w, catalog_np, k,
-               n_buyers: int = 8, threads: int | None = None, reps: int = 5) -> dict:
+               n_buyers: int = 32, threads: int | None = None, reps: int = 5) -> dict:
     """Mode A per buyer: encode S history texts (bert_ref, torch CPU f32) -> head ->
     weighted average -> F.normalize -> q/(||q||+1e-8) -> exact top-k (nq = 1)."""
     from . import bert_ref
