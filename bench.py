@@ -208,9 +208,9 @@ def configs1(a, dev, rank):
 def batch_sweep(a, shard, shard16, n, E, K, bounds, dev):
     """SURVEY.md 8(d) query-batch sweep over the 1M x 384 catalog (vector_db.py:160,197):
     end-to-end search time per call (every launch of tt_scan_topk_bf16f32, queries resident;
-    kernels.PreparedSearch as the serving path calls it, the per-call wrapper beside it),
-    fraction of the HBM peak for the algorithmic bytes 4NE + 4BE + 12Bk (the f32 catalog read
-    once) and for the bytes the bf16 filter's full level actually streams (2NE)."""
+    kernels.PreparedSearch as the serving path calls it, the per-call wrapper beside it) and
+    the fraction of the HBM peak for the bytes the search streams: the bf16 image once (2NE),
+    end to end and for the full-catalog level alone."""
     ep = _lib.padded_dim(E)
     g = torch.Generator(device=dev).manual_seed(9)
     res = {}
@@ -251,11 +251,11 @@ def batch_sweep(a, shard, shard16, n, E, K, bounds, dev):
             prep.append(ev[2].elapsed_time(ev[3]))
         del ps
         t = float(np.median(prep))
-        alg = 4.0 * n * E + 4.0 * B * E + 12.0 * B * K
+        # bytes the search actually streams: the bf16 image once (the full level; the sample
+        # level, selection and re-rank add ~5% and are not counted), so frac <= 1
         res[str(B)] = {"ms_per_search": t, "queries_per_s": B / (t * 1e-3),
                        "wrapper_ms_per_search": tw, "full_level_ms": l_,
-                       "alg_bytes": alg, "alg_hbm_gbps": alg / (t * 1e-3) / 1e9,
-                       "alg_frac": alg / (t * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                       "bf16_pass_bytes": 2.0 * n * ep,
                        "bf16_pass_gbps_end_to_end": 2.0 * n * ep / (t * 1e-3) / 1e9,
                        "bf16_pass_frac_end_to_end": 2.0 * n * ep / (t * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                        "full_level_frac": 2.0 * n * ep / (l_ * 1e-3) / 1e9 / HBM_PEAK_GBPS}
@@ -302,6 +302,77 @@ def catalog_10m(a, dev, nq=10_000, n=10_000_000):
                         "k=100", "ms_per_search": t, "queries_per_s": nq / (t * 1e-3),
             "full_level_ms": float(np.median(lvl)),
             "full_level_tflops": fl / (float(np.median(lvl)) * 1e-3) / 1e12,
+            "fallback_queries": fb,
+            "self_check": {"queries": 64, "mismatched_queries": bad,
+                           "vs": "tt_scan_topk_f32 (exact f32)"},
+            "hbm_resident_gb": (x.numel() * 4 + x16.numel() * 2) / 1e9}
+
+
+def catalog_10m_768(a, dev, nq=10_000, n=10_000_000):
+    """configs[4]'s search workload on ONE MI355X: the whole 10M x 768 catalog resident (30.7 GB
+    f32 + 15.4 GB bf16 image), 10k buyers x 20 history rows gathered from it (Mode B), encoded
+    by BuyerTower.attention_aggregation (buyer_tower.py:70-101; tt_attn_agg_l2_f32, seeded MLP
+    128 hidden), re-normalised (vector_db.py:189-190) and searched top-100 (bf16 filter + exact
+    f32 re-rank).  The full level (k_filter_ring<768, 1>) is reported against the bf16 peak;
+    64 queries are re-checked against the exact f32 scan."""
+    E, K, S, Hd = 768, 100, 20, 128
+    g = torch.Generator(device=dev).manual_seed(13)
+    x = torch.randn((n, E), generator=g, device=dev)
+    x16 = torch.empty((n, E), device=dev, dtype=torch.bfloat16)
+    kernels.l2norm_rows(x, E, _lib.TT_NORM_ADD_EPS, out=x, out_bf16=x16)
+    bnd = kernels.bf16_image_bounds(x, x16, E).tolist()
+    hist = torch.randint(0, n, (nq, S), generator=g, device=dev)
+    w = event_mix(g, (nq, S), dev)
+    W1 = torch.randn((Hd, E), generator=g, device=dev) / E ** 0.5
+    b1 = 0.1 * torch.randn(Hd, generator=g, device=dev)
+    W2 = torch.randn((1, Hd), generator=g, device=dev) / Hd ** 0.5
+    b2 = 0.1 * torch.randn(1, generator=g, device=dev)
+    items = torch.empty((nq, S, E), device=dev)
+    b = torch.empty((nq, E), device=dev)
+    q = torch.empty((nq, E), device=dev)
+    ws = torch.empty(kernels.filter_workspace_bytes(n, E, nq, K), dtype=torch.uint8, device=dev)
+    out = (torch.empty((nq, K), device=dev), torch.empty((nq, K), device=dev, dtype=torch.int64))
+    stream = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    for e in ev:
+        e.record(stream)
+
+    def step(timed):
+        if timed:
+            ev[4].record(stream)
+        torch.index_select(x, 0, hist.view(-1), out=items.view(-1, E))   # Mode B gather
+        kernels.attn_agg_l2(items, w, W1, b1, W2, b2, out=b)                # BuyerTower
+        kernels.l2norm_rows(b, E, _lib.TT_NORM_ADD_EPS, out=q)               # retrieve_batch
+        if timed:
+            ev[5].record(stream)
+        kernels.scan_topk_bf16(x, x16, n, E, q, K, bnd, workspace=ws, out=out,
+                               events=(ev[0], ev[1]) if timed else (None, None))
+
+    step(False)
+    tot, lvl, enc = [], [], []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        ev[2].record(stream)
+        step(True)
+        ev[3].record(stream)
+        torch.cuda.synchronize()
+        tot.append(ev[2].elapsed_time(ev[3]))
+        lvl.append(ev[0].elapsed_time(ev[1]))
+        enc.append(ev[4].elapsed_time(ev[5]))
+    fb = kernels.filter_fallback_count(ws, n, E, nq, K)
+    del ws
+    sub = torch.linspace(0, nq - 1, 64, device=dev).round().long()
+    fs, fi = kernels.scan_topk(x, n, E, q[sub].contiguous(), K)
+    bad = int(((out[1][sub] != fi) | (out[0][sub] != fs)).any(dim=1).sum())
+    t, tl = float(np.median(tot)), float(np.median(lvl))
+    fl = 2.0 * nq * n * E
+    return {"workload": "configs[4] search: 10M x 768 catalog on one GPU, 10k buyers x 20 "
+                        "history rows, attention aggregation (MLP 768-128-1), k=100",
+            "ms_per_step": t, "buyers_per_s": nq / (t * 1e-3),
+            "encode_ms": float(np.median(enc)), "full_level_ms": tl,
+            "full_level_kernel": "k_filter_ring<768, 1>",
+            "full_level_tflops": fl / (tl * 1e-3) / 1e12,
+            "full_level_frac_bf16_peak": fl / (tl * 1e-3) / 1e12 / BF16_MFMA_PEAK_TFLOPS,
             "fallback_queries": fb,
             "self_check": {"queries": 64, "mismatched_queries": bad,
                            "vs": "tt_scan_topk_f32 (exact f32)"},
@@ -656,6 +727,8 @@ def main():
         result["configs1"] = configs1(a, dev, rank)
         torch.cuda.empty_cache()
         result["catalog_10m"] = catalog_10m(a, dev)
+        torch.cuda.empty_cache()
+        result["catalog_10m_768"] = catalog_10m_768(a, dev)
         torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         sys.path.insert(0, ROOT)

@@ -148,6 +148,12 @@ int tt_sharded_workspace_bytes(int64_t n, int32_t d, int32_t nq, int32_t k, int6
 /* byte offset in the full/finish workspace of the int32 count of queries that took the
  * exact fallback on this shard (diagnostic) */
 int tt_sharded_fallback_offset(int64_t n, int32_t d, int32_t nq, int32_t k, int64_t* offset);
+/* Diagnostic (tests): byte offsets in a filter workspace of the band keys ([nq][offsets[4]]
+ * uint64 (orderable score << 32 | ~row)), the band counts [nq] int32, the per-query fallback
+ * flags [nq] int32 and the fallback count int32 (offsets[0..3]); offsets[4] = the band capacity
+ * per query.  sharded = 0: tt_scan_topk_bf16f32's workspace; 1: the full/finish workspace. */
+int tt_filter_workspace_layout(int64_t n, int32_t d, int32_t nq, int32_t k, int32_t sharded,
+                               int64_t* offsets);
 int tt_sharded_filter_begin(const uint16_t* sample_bf16, int64_t n_sample, int32_t d, int64_t ld,
                             const float* q, int32_t nq, int64_t ld_q, int32_t k, float* stats,
                             void* workspace, int64_t workspace_bytes, void* stream);

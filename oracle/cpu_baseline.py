@@ -36,12 +36,72 @@ def _encode(table: torch.Tensor, hist: np.ndarray, w: np.ndarray) -> np.ndarray:
     return F.normalize((x * nw).sum(dim=1), p=2, dim=1).numpy()
 
 
-def _gemv(cat: torch.Tensor, q: np.ndarray) -> torch.Tensor:
-    """catalog [n, d] . q [d] on the CPU through MKL's threaded sgemm path.  torch.mv on this
-    shape takes a slow path in the build container (1M x 384: 205 ms vs 29 ms for
-    cat @ q[:, None] on 8 threads); on the GPU box's host both run ~100-140 ms on 16 threads
-    (host-limited there), so the reported baseline barely moved."""
+def _gemv_torch_mm(cat: torch.Tensor, q: np.ndarray) -> torch.Tensor:
+    """catalog [n, d] . q [d] through torch's matmul (MKL sgemm with one column)."""
     return (cat @ torch.from_numpy(q)[:, None])[:, 0]
+
+
+def _gemv_torch_mv(cat: torch.Tensor, q: np.ndarray) -> torch.Tensor:
+    return torch.mv(cat, torch.from_numpy(q))
+
+
+def _gemv_numpy(cat: torch.Tensor, q: np.ndarray) -> torch.Tensor:
+    """numpy's BLAS sgemv (OpenBLAS in numpy's wheel)."""
+    return torch.from_numpy(cat.numpy() @ q)
+
+
+GEMVS = {"torch_matmul": _gemv_torch_mm, "torch_mv": _gemv_torch_mv, "numpy_sgemv": _gemv_numpy}
+_gemv = _gemv_torch_mm  # replaced by the fastest (implementation, threads) pick in run()
+
+
+def _thread_counts() -> list:
+    """Host threads to try: the whole affinity mask and the box's CPU share (OMP_NUM_THREADS;
+    on the GPU box the mask shows every CPU of the machine, the share is 16)."""
+    try:
+        allc = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        allc = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", allc))
+    return sorted({allc, share})
+
+
+def _set_threads(t: int):
+    torch.set_num_threads(t)
+    try:
+        from threadpoolctl import threadpool_limits
+
+        threadpool_limits(t)  # numpy's BLAS pool
+    except Exception:  # pragma: no cover
+        pass
+
+
+def pick_gemv(cat: torch.Tensor, one_buyer, reps: int = 3) -> dict:
+    """Time one reference-faithful buyer (encode + nq=1 GEMV + top-k: one_buyer()) with every
+    GEMV implementation at every thread count (median of reps) and install the fastest as
+    _gemv (timing the whole buyer, not the GEMV alone: numpy's BLAS pool and torch's OpenMP
+    pool spin against each other).  Round 2 used torch matmul at OMP_NUM_THREADS only: 137 ms
+    for the 1M x 384 GEMV (11 GB/s) on the GPU box's EPYC 9575F."""
+    global _gemv
+    table = {}
+    best = None
+    for t in _thread_counts():
+        _set_threads(t)
+        for name, fn in GEMVS.items():
+            _gemv = fn
+            one_buyer()
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                one_buyer()
+                ts.append(time.perf_counter() - t0)
+            ms = float(np.median(ts)) * 1e3
+            table[f"{name}@{t}"] = ms
+            if best is None or ms < best[0]:
+                best = (ms, name, t)
+    ms, name, t = best
+    _gemv = GEMVS[name]
+    _set_threads(t)
+    return {"ms_per_buyer_by_impl_threads": table, "picked": f"{name}@{t}", "threads": t}
 
 
 def _norm(q: np.ndarray) -> np.ndarray:
@@ -79,8 +139,6 @@ def _median_rate(fn, units: int, reps: int):
 def run(table_np: np.ndarray, catalog_np: np.ndarray, hist: np.ndarray, w: np.ndarray, k: int,
         single_buyers: int = 16, batch_buyers: int = 256, threads: int | None = None,
         reps: int = 5) -> dict:
-    threads = threads or int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    torch.set_num_threads(threads)
     table = torch.from_numpy(table_np)
     cat = torch.from_numpy(catalog_np)
     try:
@@ -99,6 +157,10 @@ def run(table_np: np.ndarray, catalog_np: np.ndarray, hist: np.ndarray, w: np.nd
             return v.numpy(), i.numpy()
         kind = "port"
 
+    gemv = pick_gemv(cat, lambda: search(_norm(_encode(table, hist[:1], w[:1])), k))
+    if threads:
+        _set_threads(threads)
+    threads = threads or gemv["threads"]
     # warm-up (one buyer each way)
     search(_norm(_encode(table, hist[:1], w[:1])), k)
     search(_norm(_encode(table, hist[:64], w[:64])), k)
@@ -119,6 +181,14 @@ def run(table_np: np.ndarray, catalog_np: np.ndarray, hist: np.ndarray, w: np.nd
 
     v_single, r_single = _median_rate(single, single_buyers, reps)
     v_batch, r_batch = _median_rate(batched, nb, reps)
+    # the other thread count(s), one repetition each, reported beside the value
+    others = {}
+    for t in _thread_counts():
+        if t != threads:
+            _set_threads(t)
+            others[str(t)] = {"single_value": _median_rate(single, single_buyers, 1)[0],
+                              "batched_value": _median_rate(batched, nb, 1)[0]}
+    _set_threads(threads)
     # where the nq = 1 time goes: the catalog GEMV alone
     q1 = _norm(_encode(table, hist[:1], w[:1]))
     t0 = time.perf_counter()
@@ -133,10 +203,13 @@ def run(table_np: np.ndarray, catalog_np: np.ndarray, hist: np.ndarray, w: np.nd
         "sample": (f"(i) {single_buyers} buyers one at a time (nq=1) and (ii) {nb} buyers "
                    f"batched 64/query-block, Mode B weighted-avg encode, exact top-{k} over "
                    f"{catalog_np.shape[0]}x{catalog_np.shape[1]} f32, torch-CPU GEMV/sgemm + "
-                   f"topk; median of {reps} repetitions of each"),
+                   f"topk; median of {reps} repetitions of each; GEMV implementation and "
+                   f"thread count = the fastest of a probe over both"),
         "batched_value": v_batch,
         "single_rates": r_single, "batched_rates": r_batch,
         "nq1_gemv_ms": gemv_ms,
+        "gemv_probe": gemv,
+        "other_thread_counts": others,
         "host": host_info(threads),
         "seconds": time.perf_counter() - t_all,
     }
@@ -148,8 +221,8 @@ def run_mode_a(sd, cfg, head_sd, seqs_per_buyer, brand_ids, cat_ids, w, catalog_
     weighted average -> F.normalize -> q/(||q||+1e-8) -> exact top-k (nq = 1)."""
     from . import bert_ref
 
-    threads = threads or int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    torch.set_num_threads(threads)
+    threads = threads or torch.get_num_threads()  # run() left the fastest GEMV setting
+    _set_threads(threads)
     cat = torch.from_numpy(catalog_np)
 
     def one(b):

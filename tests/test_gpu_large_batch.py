@@ -135,52 +135,73 @@ def test_configs2_full_size_bit_exact(K, oracle_mod):
     assert np.array_equal(s[sub].cpu().numpy(), rs)
 
 
-@pytest.mark.slow
-def test_configs2_few_flagged_queries_fallback(K, oracle_mod):
-    """1M x 384, 10k queries, k = 100 with 3 queries (in different query tiles) that each sit
-    on a cluster of 1500 near-copies: their band overflows BAND_CAP, so exactly those take the
-    exact f32 fallback.  The flagged queries are compacted into the fallback's query tile 0,
-    which runs on its own one-tile slab plan (tt_scan.hip scan_f32_impl): bit-exact, and the
-    search costs well under 2x the unflagged one (on the batch's 16-slab plan the 3 queries
-    were 1.5 GB f32 scans by 16 CUs: ~16 ms on top of a ~7 ms search)."""
-    n, d, nq, k = 1_000_000, 384, 10_000, 100
+def _flagged_scenario(K, n_picked):
+    """1M x 384, 10k queries, k = 100; n_picked queries (spread over the batch) each sit on a
+    cluster of 1500 near-copies, so their band overflows BAND_CAP and exactly those take the
+    exact f32 fallback.  Every other query is orthogonal to the picked ones (a cluster of 1500
+    equal scores inside a query's top-k band overflows it too; iid queries reach it at ~1e-3
+    per query), and the picked queries are orthonormal."""
+    n, d, nq = 1_000_000, 384, 10_000
     g = torch.Generator(device="cuda").manual_seed(5)
     x = torch.randn((n, d), generator=g, device="cuda")
     q = torch.randn((nq, d), generator=g, device="cuda")
     K.l2norm_rows(q, d, 0, out=q)
-    picked = [17, 4242, 9998]
-    # every other query orthogonal to the picked ones: a cluster of 1500 equal scores inside a
-    # query's top-k band overflows it too (iid queries reach it at ~1e-3 per query)
+    picked = np.unique(np.linspace(17, nq - 2, n_picked).astype(int)).tolist()
     basis = torch.linalg.qr(q[picked].T.cpu())[0].cuda()
+    q[picked] = basis.T.contiguous()  # picked queries orthonormal: no cross-cluster bands
     rest = torch.ones(nq, dtype=torch.bool, device="cuda")
     rest[picked] = False
     q[rest] -= (q[rest] @ basis) @ basis.T
     K.l2norm_rows(q, d, 0, out=q)
+    step = (n - 100_000) // len(picked)
     for j, qi in enumerate(picked):
-        rows = torch.arange(100_000 + 300_000 * j, 100_000 + 300_000 * j + 1500, device="cuda")
+        rows = torch.arange(100_000 + step * j, 100_000 + step * j + 1500, device="cuda")
         x[rows] = q[qi] + 1e-3 * torch.randn((1500, d), generator=g, device="cuda")
     K.l2norm_rows(x, d, 0, out=x)
     x16 = x.to(torch.bfloat16)
-    ws = torch.empty(K.filter_workspace_bytes(n, d, nq, k), dtype=torch.uint8, device="cuda")
+    # the same batch with the clustered queries replaced by iid ones (orthogonal already)
+    q2 = q.clone()
+    q2[picked] = q[[1, 2, 3] * (len(picked) // 3) + [1, 2, 3][:len(picked) % 3]]
+    return x, x16, q, q2, picked
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("n_picked", [3, 40])
+def test_configs2_flagged_queries_fallback_bit_exact(K, oracle_mod, n_picked):
+    """A few (3: one 16-query tile of the adaptive fallback) or more (40: three tiles) flagged
+    queries of a 10k batch (tt_scan.hip k_scan_fallback / k_merge_fallback: the flagged slots
+    are spread over the whole chip on the device): exactly those fall back, bit-exact."""
+    n, d, k = 1_000_000, 384, 100
+    x, x16, q, q2, picked = _flagged_scenario(K, n_picked)
+    ws = torch.empty(K.filter_workspace_bytes(n, d, q.shape[0], k), dtype=torch.uint8,
+                     device="cuda")
     bnd = bounds(K, x, x16, d)
-
-    def search(qq):
-        s, i = K.scan_topk_bf16(x, x16, n, d, qq, k, bnd, workspace=ws)
-        torch.cuda.synchronize()
-        return s, i, K.filter_fallback_count(ws, n, d, qq.shape[0], k)
-
-    s, i, fb = search(q)
-    assert fb == len(picked)
-    sub = picked + [0, 5000, 9999]
+    s, i = K.scan_topk_bf16(x, x16, n, d, q, k, bnd, workspace=ws)
+    torch.cuda.synchronize()
+    assert K.filter_fallback_count(ws, n, d, q.shape[0], k) == len(picked)
+    fs, fi = K.scan_topk(x, n, d, q, k)
+    assert torch.equal(i, fi) and torch.equal(s, fs)
+    sub = picked[:8] + [0, 5000, 9999]
     rs, ri = oracle_mod.scan_topk(x.cpu().numpy(), q[sub].cpu().numpy(), k)
     assert np.array_equal(i[sub].cpu().numpy(), ri)
     assert np.array_equal(s[sub].cpu().numpy(), rs)
-    # the same batch with the clustered queries replaced by iid ones: no fallback
-    q2 = q.clone()
-    q2[picked] = q[[1, 2, 3]]  # already orthogonal to the clusters
-    assert search(q2)[2] == 0
+    K.scan_topk_bf16(x, x16, n, d, q2, k, bnd, workspace=ws)
+    torch.cuda.synchronize()
+    assert K.filter_fallback_count(ws, n, d, q.shape[0], k) == 0
 
-    def timed(qq, reps=5):
+
+@pytest.mark.slow
+def test_configs2_few_flagged_queries_fallback_cost(K):
+    """Cost guard (a performance property, kept apart from the parity tests above): 3 flagged
+    queries of a 10k batch add < 20% to the search (median of 7 each way).  Round 2's fallback
+    ran them as one 64-query f32 tile over the catalog: 1.43-1.48 ms on a ~6.9 ms search."""
+    n, d, k = 1_000_000, 384, 100
+    x, x16, q, q2, picked = _flagged_scenario(K, 3)
+    ws = torch.empty(K.filter_workspace_bytes(n, d, q.shape[0], k), dtype=torch.uint8,
+                     device="cuda")
+    bnd = bounds(K, x, x16, d)
+
+    def timed(qq, reps=7):
         t = []
         for _ in range(reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -191,9 +212,10 @@ def test_configs2_few_flagged_queries_fallback(K, oracle_mod):
             t.append(e0.elapsed_time(e1))
         return sorted(t)[reps // 2]
 
+    timed(q, 2)
     t_fb, t_none = timed(q), timed(q2)
     print(f"search with 3 flagged queries {t_fb:.3f} ms, none flagged {t_none:.3f} ms")
-    assert t_fb < 2.0 * t_none
+    assert t_fb < 1.2 * t_none
 
 
 @pytest.mark.slow

@@ -182,10 +182,11 @@ def test_bf16_filter_no_fallback_on_iid_data(K, nq):
 @pytest.mark.parametrize("resid", [0.5, 4.0])
 def test_bf16_filter_fallback_is_exact(K, oracle_mod, resid, nq):
     """A loose bound overflows the candidate lists: every query then takes the exact
-    fallback launch, and the results must not change.  The fallback merges its slab lists
-    inside the scan launch (the last slab block of each 64-query tile): nq = 150 is three
-    tiles, the last ragged; 2100 is 33 tiles behind the batched (> 2048) filter path.  Run
-    twice on one workspace (the per-tile arrival counters are re-zeroed by each search)."""
+    fallback launch, and the results must not change.  nq = 20: one 64-query tile, its slab
+    lists merged inside the scan launch by the last slab block (run twice on one workspace:
+    the arrival counter is re-zeroed by each search); nq = 150 (the small path) and 2100 (the
+    batched > 2048 path): the adaptive fallback (k_scan_fallback: 16-query tiles spread over
+    the chip on the device, then k_merge_fallback), ragged last tiles."""
     rng = np.random.default_rng(77)
     n, d, k = 30000, 384, 100
     x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
@@ -423,24 +424,28 @@ def test_scan_full_size_properties(K, oracle_mod):
     assert not missing.any()
 
 
-def _sharded_search_emulated(K, x, q, W, k, owners=None):
+def _sharded_search_emulated(K, x, q, W, k, owners=None, between=None):
     """The row-sharded protocol with W shards on one GPU: per-owner begin on the global
-    sample, stats 'all-gathered' by concatenation, probe counts 'all-reduced' by summing."""
+    sample, stats 'all-gathered' by concatenation, probe counts 'all-reduced' by summing.
+    x, q: host arrays or device row tensors [rows, ep]; between(r, workspace) runs after
+    the full stages, before shard r's finish (fault injection)."""
     from twotower.sharded import shard_range
 
-    n = x.shape[0]
-    nq = q.shape[0]
-    qd = dev_rows(q)
-    xd = dev_rows(x)
+    if isinstance(x, torch.Tensor):
+        xd, qd, d = x, q, x.shape[1]
+    else:
+        xd, qd, d = dev_rows(x), dev_rows(q), x.shape[1]
+    n = xd.shape[0]
+    nq = qd.shape[0]
     x16 = xd.to(torch.bfloat16)
     sample = K.sharded_sample(x16, n)
     groups = owners or [(r * nq // W, (r + 1) * nq // W) for r in range(W)]
-    stats = torch.cat([K.sharded_begin(sample, 384, qd[a:b], k) for a, b in groups])
+    stats = torch.cat([K.sharded_begin(sample, d, qd[a:b], k) for a, b in groups])
     shards = []
     bmax = torch.zeros(2)
     for r in range(W):
         lo, hi = shard_range(n, r, W)
-        bd = torch.tensor(bounds(K, xd[lo:hi], x16[lo:hi], 384))
+        bd = torch.tensor(bounds(K, xd[lo:hi], x16[lo:hi], d))
         bmax = torch.maximum(bmax, bd)
         shards.append((lo, hi))
     pcs = [torch.empty((nq, 16), dtype=torch.int32, device="cuda") for _ in range(W)]
@@ -452,22 +457,24 @@ def _sharded_search_emulated(K, x, q, W, k, owners=None):
 
     L, st = _lib.lib(), _lib.stream_ptr()
     for r, (lo, hi) in enumerate(shards):
-        wss[r] = torch.empty(K.sharded_workspace_bytes(hi - lo, 384, nq, k), dtype=torch.uint8,
+        wss[r] = torch.empty(K.sharded_workspace_bytes(hi - lo, d, nq, k), dtype=torch.uint8,
                              device="cuda")
         _lib.check(L.tt_sharded_filter_full(
-            x16[lo:].data_ptr(), hi - lo, 384, x16.stride(0), qd.data_ptr(), nq, qd.stride(0), k,
+            x16[lo:].data_ptr(), hi - lo, d, x16.stride(0), qd.data_ptr(), nq, qd.stride(0), k,
             ctypes.c_float(bmax[0]), ctypes.c_float(bmax[1]), stats.data_ptr(), pcs[r].data_ptr(),
             wss[r].data_ptr(), wss[r].numel(), st, None, None), "full")
     total = torch.stack(pcs).sum(0, dtype=torch.int32)
     for r, (lo, hi) in enumerate(shards):
+        if between is not None:
+            between(r, wss[r])
         s_ = torch.empty((nq, k), device="cuda")
         i_ = torch.empty((nq, k), device="cuda", dtype=torch.int64)
         _lib.check(L.tt_sharded_filter_finish(
-            xd[lo:].data_ptr(), x16[lo:].data_ptr(), hi - lo, 384, xd.stride(0), lo, qd.data_ptr(),
+            xd[lo:].data_ptr(), x16[lo:].data_ptr(), hi - lo, d, xd.stride(0), lo, qd.data_ptr(),
             nq, qd.stride(0), k, stats.data_ptr(), total.data_ptr(), s_.data_ptr(), i_.data_ptr(),
             wss[r].data_ptr(), wss[r].numel(), st), "finish")
         outs[r] = (s_, i_)
-    fb = [K.filter_fallback_count(wss[r], hi - lo, 384, nq, k, sharded=True)
+    fb = [K.filter_fallback_count(wss[r], hi - lo, d, nq, k, sharded=True)
           for r, (lo, hi) in enumerate(shards)]
     ms, mi = K.merge_topk(torch.stack([o[0] for o in outs]), torch.stack([o[1] for o in outs]), k)
     return ms.cpu().numpy(), mi.cpu().numpy(), fb
@@ -523,3 +530,35 @@ def test_sharded_finish_wave_list_overflow_is_reduced(K, oracle_mod):
     rs, ri = oracle_mod.scan_topk(x, q, k)
     assert np.array_equal(mi, ri) and np.array_equal(ms, rs)
     assert sum(fb) == 0, fb
+
+
+def test_sharded_finish_corrupt_band_row_falls_back(K, oracle_mod):
+    """Bounds check of decoded candidate rows (k_rerank_wave): a band key whose row decodes
+    past the shard (here row 0xffffffff, planted in the workspace between the full and finish
+    stages) is never read -- the query takes that shard's exact f32 fallback instead, and the
+    merged result stays bit-exact with no fault."""
+    rng = np.random.default_rng(41)
+    n, W, k, nq = 50000, 2, 100, 8
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, 384)).astype(np.float32), 0)
+    q = oracle_mod.l2norm_rows(rng.standard_normal((nq, 384)).astype(np.float32), 0)
+    from twotower.sharded import shard_range
+
+    planted = {}
+
+    def corrupt(r, ws):
+        if r != 0:
+            return
+        lo, hi = shard_range(n, 0, W)
+        lay = K.filter_workspace_layout(hi - lo, 384, nq, k, sharded=True)
+        band_n = ws[lay["band_n"]:lay["band_n"] + 4 * nq].view(torch.int32)
+        qi = int(torch.argmax(band_n).item())
+        assert int(band_n[qi]) > 0
+        keys = ws[lay["band"]:lay["band"] + 8 * nq * lay["band_cap"]].view(torch.int64)
+        e = qi * lay["band_cap"]
+        keys[e] = keys[e] & ~0xFFFFFFFF  # low word 0 -> row ~0 = 0xffffffff
+        planted["q"] = qi
+
+    ms, mi, fb = _sharded_search_emulated(K, x, q, W, k, between=corrupt)
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    assert np.array_equal(mi, ri) and np.array_equal(ms, rs)
+    assert fb[0] >= 1 and "q" in planted

@@ -1486,7 +1486,7 @@ template <int EP>
 __global__ __launch_bounds__(SM_THREADS) void k_final_small(
     const uint64_t* __restrict__ lists, const int* __restrict__ counts, int n_slabs, int k,
     const float* __restrict__ eps2, const float* __restrict__ aref, int* __restrict__ flags,
-    int* qsel, int* qsel_n, const float* __restrict__ db, int64_t ld,
+    int* qsel, int* qsel_n, const float* __restrict__ db, int64_t ld, int64_t n_rows,
     const float* __restrict__ q, int64_t ldq, int64_t row_base, float* __restrict__ out_s,
     int64_t* __restrict__ out_i) {
   __shared__ SmallLds s;
@@ -1544,15 +1544,23 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_small(
     if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
     return;
   }
+  bool bad_row = false;  // a decoded row >= n_rows is never read: exact fallback instead
   {
     int pos = base + incl - mine;
 #pragma unroll
     for (int j = 0; j < SM_PER; ++j) {
       const int e = tid + j * SM_THREADS;
-      if (h[j] != 0u && key_float(h[j]) >= thr) brow[pos++] = key_row(s.key[e]);
+      if (h[j] != 0u && key_float(h[j]) >= thr) {
+        const uint32_t r = key_row(s.key[e]);
+        bad_row |= (int64_t)r >= n_rows;
+        brow[pos++] = (int64_t)r < n_rows ? r : 0u;
+      }
     }
   }
-  __syncthreads();
+  if (__syncthreads_or(bad_row)) {
+    if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
   // exact scores: wave w takes band rows [16 gr, 16 gr + 16), gr = w, w + SM_WAVES, ...  Lane
   // (r, g) loads row r's dims 16t + 4g .. +3 for every t (all loads in flight) and
   // the chain runs on v_mfma_f32_16x16x4_f32 with the query in every column: the canonical
@@ -1659,13 +1667,16 @@ template <int EP>
 __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, int64_t ld,
                                                 const float* __restrict__ q, int64_t ldq,
                                                 const uint64_t* __restrict__ band,
-                                                const int* __restrict__ band_n,
-                                                const int* __restrict__ flags, int k,
+                                                const int* __restrict__ band_n, int* flags,
+                                                int* qsel, int* qsel_n, int64_t n_rows, int k,
                                                 int64_t row_base,
                                                 const float* __restrict__ cut,
                                                 float* __restrict__ out_s,
                                                 int64_t* __restrict__ out_i) {
   __shared__ uint64_t buf[BAND_CAP];
+  // A decoded candidate row >= n_rows (a corrupted list or band entry) is never read: the row
+  // is clamped for the loads and the query goes to the exact fallback instead (bad_row).
+  bool bad_row = false;
   __shared__ __attribute__((aligned(16))) float qs[EP];
   __shared__ int nkeep;
   const int qid = blockIdx.x;
@@ -1700,7 +1711,11 @@ __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, in
     const int sub = lane >> 4, piece = lane & 15;
     for (int e0 = 64 * w; e0 < nb; e0 += 256) {
       const int ej = e0 + lane;
-      const uint32_t rj = key_row(qband[ej < nb ? ej : e0]);
+      uint32_t rj = key_row(qband[ej < nb ? ej : e0]);
+      if ((int64_t)rj >= n_rows) {
+        bad_row = true;
+        rj = 0;
+      }
       const float* rp[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -1761,10 +1776,13 @@ __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, in
       if (ej < nb) buf[ej] = acc != acc ? 0ull : make_key(acc, rj);
     }
   }
-  __syncthreads();
 #else
   for (int e = threadIdx.x; e < nb; e += blockDim.x) {
-    const uint32_t r = key_row(qband[e]);
+    uint32_t r = key_row(qband[e]);
+    if ((int64_t)r >= n_rows) {
+      bad_row = true;
+      r = 0;
+    }
     const f32x4* xr = (const f32x4*)(db + (int64_t)r * ld);
     float acc = 0.0f;
 #pragma unroll 4
@@ -1790,6 +1808,10 @@ __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, in
     buf[e] = acc != acc ? 0ull : make_key(acc, r);
   }
 #endif
+  if (__syncthreads_or(bad_row)) {
+    if (threadIdx.x == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
   const int np = pow2_at_least(nb);
   for (int i = nb + threadIdx.x; i < np; i += blockDim.x) buf[i] = 0ull;
   block_sort_desc(buf, np);
@@ -1821,7 +1843,7 @@ template <int EP>
 __global__ __launch_bounds__(256) void k_rerank_wave(
     const float* __restrict__ db, int64_t ld, const float* __restrict__ q, int64_t ldq,
     const uint64_t* __restrict__ band, const int* __restrict__ band_n, int* flags, int* qsel,
-    int* qsel_n, int nq, int k, int64_t row_base, const float* __restrict__ cut,
+    int* qsel_n, int nq, int64_t n_rows, int k, int64_t row_base, const float* __restrict__ cut,
     float* __restrict__ out_s, int64_t* __restrict__ out_i) {
   __shared__ __attribute__((aligned(16))) char stage[4][64 * 256];
   __shared__ uint64_t kept[4][RW_CAP];
@@ -1838,12 +1860,17 @@ __global__ __launch_bounds__(256) void k_rerank_wave(
   const float c = cut[qid];
   const int sub = lane >> 4, piece = lane & 15;
   int nb = 0, ns = 0;  // kept keys buf[0, nb); buf[0, ns) already hold exact-score keys
+  bool bad_row = false;  // a decoded row >= n_rows is never read: exact fallback instead
   // exact keys for buf[from, nb) (band keys -> (canonical f32 score, row) keys, in place)
   auto score_from = [&](int from) __attribute__((always_inline)) {
     wave_sync();
     for (int e0 = from; e0 < nb; e0 += 64) {
       const int ej = e0 + lane;
-      const uint32_t rj = key_row(buf[ej < nb ? ej : e0]);
+      uint32_t rj = key_row(buf[ej < nb ? ej : e0]);
+      if ((int64_t)rj >= n_rows) {
+        bad_row = true;
+        rj = 0;
+      }
       const float* rp[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -1931,6 +1958,10 @@ __global__ __launch_bounds__(256) void k_rerank_wave(
     nb += (int)__popcll(bm);
   }
   score_from(ns);
+  if (__ballot(bad_row) != 0ull) {
+    if (lane == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
   // output slot = rank; slots nb .. k-1 stay (-inf, -1)
   for (int e0 = 0; e0 < nb; e0 += 64) {
     const int e = e0 + lane;
@@ -2275,6 +2306,31 @@ extern "C" int tt_filter_fallback_offset(int64_t n, int32_t d, int32_t nq, int32
   return TT_OK;
 }
 
+// Diagnostic layout of a filter workspace (tests): byte offsets of the band keys
+// [nq][BAND_CAP] u64, band counts [nq] i32, flags [nq] i32, the fallback count i32, and
+// offsets[4] = BAND_CAP.  sharded != 0: the tt_sharded_filter_full/_finish workspace.
+extern "C" int tt_filter_workspace_layout(int64_t n, int32_t d, int32_t nq, int32_t k,
+                                          int32_t sharded, int64_t* offsets) {
+  TT_REQUIRE(offsets != nullptr && n >= 1 && nq >= 1 && k >= 1, "bad arguments");
+  const int ep = tt_padded_dim(d);
+  TT_REQUIRE(ep > 0, "d > 768");
+  FilterPlan p = plan_filter(n, nq, k, ep);
+  if (sharded) {
+    const Level last = p.lv[p.n_levels - 1];
+    p.n_levels = 1;
+    p.lv[0] = last;
+    p.max_slabs = last.n_slabs;
+  }
+  const FilterWs w = carve(nullptr, p, n, d, nq, k);
+  char* b = (char*)4096;
+  offsets[0] = (int64_t)((char*)w.band - b);
+  offsets[1] = (int64_t)((char*)w.band_n - b);
+  offsets[2] = (int64_t)((char*)w.flags - b);
+  offsets[3] = (int64_t)((char*)w.qsel_n - b);
+  offsets[4] = BAND_CAP;
+  return TT_OK;
+}
+
 namespace {
 // Shared prologue of the single-shard call and the sharded stages: validation, plan, carve.
 int filter_setup(const float* db, const uint16_t* db_bf16, int64_t n, int32_t d, int64_t ld_db,
@@ -2382,11 +2438,12 @@ int filter_finish(const FilterWs& w, const float* db, int64_t n, int32_t d, int6
   case E:                                                                                     \
     if (cut)                                                                                  \
       hipLaunchKernelGGL(k_rerank_wave<E>, dim3((nq + 3) / 4), dim3(256), 0, st, db, ld_db, q, \
-                         ld_q, w.band, w.band_n, w.flags, w.qsel, w.qsel_n, nq, k, row_base,  \
-                         cut, out_score, out_idx);                                            \
+                         ld_q, w.band, w.band_n, w.flags, w.qsel, w.qsel_n, nq, n, k,         \
+                         row_base, cut, out_score, out_idx);                                  \
     else                                                                                      \
       hipLaunchKernelGGL(k_rerank<E>, dim3(nq), dim3(256), 0, st, db, ld_db, q, ld_q, w.band, \
-                         w.band_n, w.flags, k, row_base, cut, out_score, out_idx);            \
+                         w.band_n, w.flags, w.qsel, w.qsel_n, n, k, row_base, cut, out_score, \
+                         out_idx);                                                            \
     break;
     TT_RR(64) TT_RR(128) TT_RR(256) TT_RR(384) TT_RR(512) TT_RR(768)
 #undef TT_RR
@@ -2443,7 +2500,7 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
   case E:                                                                                     \
     hipLaunchKernelGGL(k_final_small<E>, dim3(nq), dim3(SM_THREADS), 0, st, w.lists,          \
                        w.counts, ns, k, w.eps2, w.aref, w.flags, w.qsel, w.qsel_n, db, ld_db, \
-                       q, ld_q, row_base, out_score, out_idx);                                \
+                       n, q, ld_q, row_base, out_score, out_idx);                             \
     break;
       TT_FS(64) TT_FS(128) TT_FS(256) TT_FS(384) TT_FS(512) TT_FS(768)
 #undef TT_FS

@@ -108,23 +108,22 @@ __device__ void merge_lists_block(uint64_t* buf, int& bcnt, uint32_t& th_key, in
                                   const int* qsel);
 constexpr int MG_CAP = 8192;
 
+// Scan one (query tile, row slab) work item: query slots [qbase, qbase + kQPB) of [0, nq)
+// (qsel: slot -> query row), catalog rows [s0, s1).  Each query's sorted slab top-k goes to
+// the lists at index (slot * n_slabs + slab).  A wave whose 16 slots are all past nq skips the
+// scan (a handful of flagged fallback queries then costs one wave's MFMAs, not the tile's).
 template <int EP, class Cfg>
-__global__ __launch_bounds__(64 * Cfg::kWaves, ((EP <= 384 && Cfg::kWaves > 1) ? 2 : 1)) void k_scan_topk_f32(
-    const float* __restrict__ db, int64_t n, int64_t ld_db, const float* __restrict__ q,
-    int nq, int64_t ld_q, int k, int rows_per_slab, int n_slabs,
-    float* __restrict__ ws_score, int* __restrict__ ws_row, int* __restrict__ ws_cnt,
-    const int* __restrict__ qsel, const int* __restrict__ qsel_n, int* __restrict__ done,
-    int64_t row_base, float* __restrict__ out_s, int64_t* __restrict__ out_i, int qt_off,
-    int done_off) {
-  constexpr int SC_QPB = Cfg::kQPB, SC_CAND = Cfg::kCand;
-  static_assert(sizeof(typename Cfg::Smem) >= MG_CAP * 8, "merge buffer aliases the scan state");
-  __shared__ __attribute__((aligned(16))) typename Cfg::Smem sm;
+__device__ __forceinline__ void scan_tile(const float* __restrict__ db, int64_t n, int64_t ld_db,
+                                          const float* __restrict__ q, int nq, int64_t ld_q,
+                                          int k, int64_t s0, int64_t s1, int n_slabs, int slab,
+                                          int qbase, float* __restrict__ ws_score,
+                                          int* __restrict__ ws_row, int* __restrict__ ws_cnt,
+                                          const int* __restrict__ qsel, typename Cfg::Smem& sm) {
+  constexpr int SC_CAND = Cfg::kCand;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ql = lane & 15, g = lane >> 4;
-  const int qt = blockIdx.x + qt_off, slab = blockIdx.y;
-  if (qsel) nq = *qsel_n;  // fallback mode: slots 0..nq-1 map to queries qsel[slot]
-  if (qt * SC_QPB >= nq) return;
-  const int qi = qt * SC_QPB + w * SC_QPW + ql;
+  const int wbase = qbase + w * SC_QPW;
+  const int qi = wbase + ql;
   const bool qvalid = qi < nq;
 
   // query fragment: dims 16t + 4g .. +3 of query qi
@@ -145,13 +144,12 @@ __global__ __launch_bounds__(64 * Cfg::kWaves, ((EP <= 384 && Cfg::kWaves > 1) ?
   wave_sync();
   float theta = -__builtin_huge_valf();
 
-  const int64_t s0 = (int64_t)slab * rows_per_slab;
-  const int64_t s1 = (s0 + rows_per_slab < n) ? s0 + rows_per_slab : n;
   float* my_sc = sm.score[w][ql];
   uint16_t* my_ro = sm.roff[w][ql];
   int* my_cnt = &sm.cnt[w][ql];
 
-  for (int64_t rb = s0; rb < s1; rb += SC_ROWS) {
+  const int64_t s_end = wbase < nq ? s1 : s0;  // idle wave: no rows
+  for (int64_t rb = s0; rb < s_end; rb += SC_ROWS) {
     const int64_t ra = (rb + ql < n) ? rb + ql : n - 1;
     const int64_t rc = (rb + 16 + ql < n) ? rb + 16 + ql : n - 1;
     const float* pa = db + ra * ld_db + 4 * g;
@@ -204,26 +202,45 @@ __global__ __launch_bounds__(64 * Cfg::kWaves, ((EP <= 384 && Cfg::kWaves > 1) ?
     }
   }
 
-  // flush: sorted top-k of every valid query of this wave -> workspace [nq][n_slabs][k]
+  // flush: sorted top-k of every valid query of this wave -> lists [slot][n_slabs][k]
   for (int qq = 0; qq < SC_QPW; ++qq) {
-    const int qg = qt * SC_QPB + w * SC_QPW + qq;
+    const int qg = wbase + qq;
     if (qg >= nq) break;
     const int64_t base = ((int64_t)qg * n_slabs + slab);
     compact_query<Cfg::kSortN>(sm.score[w][qq], sm.roff[w][qq], &sm.cnt[w][qq],
                                &sm.theta[w][qq], k, lane, ws_score + base * k,
                                ws_row + base * k, ws_cnt + base, (int)s0);
   }
+}
+
+template <int EP, class Cfg>
+__global__ __launch_bounds__(64 * Cfg::kWaves, ((EP <= 384 && Cfg::kWaves > 1) ? 2 : 1)) void k_scan_topk_f32(
+    const float* __restrict__ db, int64_t n, int64_t ld_db, const float* __restrict__ q,
+    int nq, int64_t ld_q, int k, int rows_per_slab, int n_slabs,
+    float* __restrict__ ws_score, int* __restrict__ ws_row, int* __restrict__ ws_cnt,
+    const int* __restrict__ qsel, const int* __restrict__ qsel_n, int* __restrict__ done,
+    int64_t row_base, float* __restrict__ out_s, int64_t* __restrict__ out_i) {
+  constexpr int SC_QPB = Cfg::kQPB;
+  static_assert(sizeof(typename Cfg::Smem) >= MG_CAP * 8, "merge buffer aliases the scan state");
+  __shared__ __attribute__((aligned(16))) typename Cfg::Smem sm;
+  const int qt = blockIdx.x, slab = blockIdx.y;
+  if (qsel) nq = *qsel_n;  // fallback mode: slots 0..nq-1 map to queries qsel[slot]
+  if (qt * SC_QPB >= nq) return;
+  const int64_t s0 = (int64_t)slab * rows_per_slab;
+  const int64_t s1 = (s0 + rows_per_slab < n) ? s0 + rows_per_slab : n;
+  scan_tile<EP, Cfg>(db, n, ld_db, q, nq, ld_q, k, s0, s1, n_slabs, slab, qt * SC_QPB, ws_score,
+                     ws_row, ws_cnt, qsel, sm);
   if (!done) return;
-  // Fused merge (the filter's exact fallback): the last slab block of query tile qt to finish
-  // merges the tile's queries -- one launch instead of scan + k_merge_lists, and with no
-  // query flagged (the common case) every block has already returned above.  done[qt] is
-  // zeroed by the search's per-query init; agent-scope fences publish the slab lists across
-  // XCDs (their L2s are not coherent with each other).
+  // Fused merge (the filter's exact fallback of a one-tile batch, nq <= 64): the last slab
+  // block to finish merges the tile's queries -- one launch instead of scan + k_merge_lists,
+  // and with no query flagged (the common case) every block has already returned above.
+  // done[0] is zeroed by the search's per-query init; agent-scope fences publish the slab
+  // lists across XCDs (their L2s are not coherent with each other).
   __shared__ int last, bcnt;
   __shared__ uint32_t th_key;
   __threadfence();
   __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(&done[qt + done_off], 1) == n_slabs - 1;
+  if (threadIdx.x == 0) last = atomicAdd(&done[qt], 1) == n_slabs - 1;
   __syncthreads();
   if (!last) return;
   __threadfence();
@@ -234,7 +251,62 @@ __global__ __launch_bounds__(64 * Cfg::kWaves, ((EP <= 384 && Cfg::kWaves > 1) ?
     merge_lists_block<int>(buf, bcnt, th_key, qg, ws_score, ws_row, ws_cnt, n_slabs,
                            (int64_t)n_slabs * k, (int64_t)k, k, k, row_base, out_s, out_i, qsel);
   }
-  if (threadIdx.x == 0) done[qt + done_off] = 0;
+  if (threadIdx.x == 0) done[qt] = 0;
+}
+
+// ---------------------------------------------------------------------- adaptive fallback
+// The bf16 filter's exact fallback for batches of more than one 64-query tile.  How many
+// queries were flagged is known only on the device (*qsel_n), so the decomposition is chosen
+// there: the flagged slots form tiles of 16 (one wave each, ScanCfg<1, ...>), and the fixed
+// grid of FB_GRID one-wave blocks is spread over (tile, slab) items -- a few flagged queries
+// get the whole chip (~FB_GRID slabs of >= 512 rows) instead of one 64-query tile's slabs on
+// the batch plan (1.43-1.48 ms for 3 flagged queries of a 10k batch at 1M rows, round 2).
+// Blocks walk the items grid-stride; k_merge_fallback merges each slot's slab lists.
+constexpr int FB_GRID = 2048;  // one-wave blocks: 8 per CU (18.5 KB LDS each)
+using CfgFb = ScanCfg<1, 192, 256>;
+struct FbPlan {
+  int tiles, spt, rows;
+};
+__host__ __device__ inline FbPlan fb_plan(int64_t n, int nflag) {
+  FbPlan p;
+  p.tiles = (nflag + SC_QPW - 1) / SC_QPW;
+  const int64_t smin = (n + SC_MAX_SLAB_ROWS - 1) / SC_MAX_SLAB_ROWS;  // uint16 row offsets
+  const int64_t smax = (n + 511) / 512;                                  // >= 512 rows per slab
+  int64_t s = p.tiles > 0 ? FB_GRID / p.tiles : 1;
+  if (s > smax) s = smax;
+  if (s < smin) s = smin;
+  if (s < 1) s = 1;
+  int64_t r = (n + s - 1) / s;
+  r = (r + SC_ROWS - 1) / SC_ROWS * SC_ROWS;
+  p.rows = (int)r;
+  p.spt = (int)((n + r - 1) / r);
+  return p;
+}
+// list entries (of k) the fallback of up to nq flagged queries may write
+static int64_t fb_items_max(int64_t n, int nq) {
+  const int64_t tmax = (nq + SC_QPW - 1) / SC_QPW;
+  const int64_t smin = (n + SC_MAX_SLAB_ROWS - 1) / SC_MAX_SLAB_ROWS;
+  const int64_t a = FB_GRID, b = tmax * (smin > 1 ? smin : 1);
+  return (a > b ? a : b) + 1;
+}
+
+template <int EP>
+__global__ __launch_bounds__(64, 2) void k_scan_fallback(
+    const float* __restrict__ db, int64_t n, int64_t ld_db, const float* __restrict__ q,
+    int64_t ld_q, int k, const int* __restrict__ qsel, const int* __restrict__ qsel_n,
+    float* __restrict__ ws_score, int* __restrict__ ws_row, int* __restrict__ ws_cnt) {
+  __shared__ __attribute__((aligned(16))) typename CfgFb::Smem sm;
+  const int nq = *qsel_n;
+  if (nq == 0) return;
+  const FbPlan p = fb_plan(n, nq);
+  const int items = p.tiles * p.spt;
+  for (int it = blockIdx.x; it < items; it += gridDim.x) {
+    const int tile = it / p.spt, slab = it % p.spt;
+    const int64_t s0 = (int64_t)slab * p.rows;
+    const int64_t s1 = (s0 + p.rows < n) ? s0 + p.rows : n;
+    scan_tile<EP, CfgFb>(db, n, ld_db, q, nq, ld_q, k, s0, s1, p.spt, slab, tile * SC_QPW,
+                         ws_score, ws_row, ws_cnt, qsel, sm);
+  }
 }
 
 // ----------------------------------------------------------------------------- merge
@@ -365,6 +437,24 @@ __global__ __launch_bounds__(256) void k_merge_lists(const float* __restrict__ i
                           list_stride_l, k_in, k, row_base, out_s, out_i, qsel);
 }
 
+// Merge of the adaptive fallback's slab lists: block-strided over the flagged slots.
+__global__ __launch_bounds__(256) void k_merge_fallback(const float* __restrict__ ws_score,
+                                                        const int* __restrict__ ws_row,
+                                                        const int* __restrict__ ws_cnt, int64_t n,
+                                                        int k, int64_t row_base, float* out_s,
+                                                        int64_t* out_i, const int* qsel,
+                                                        const int* qsel_n) {
+  __shared__ uint64_t buf[MG_CAP];
+  __shared__ int bcnt;
+  __shared__ uint32_t th_key;
+  const int nq = *qsel_n;
+  if (nq == 0) return;
+  const int spt = fb_plan(n, nq).spt;
+  for (int slot = blockIdx.x; slot < nq; slot += gridDim.x)
+    merge_lists_block<int>(buf, bcnt, th_key, slot, ws_score, ws_row, ws_cnt, spt,
+                           (int64_t)spt * k, (int64_t)k, k, k, row_base, out_s, out_i, qsel);
+}
+
 // ----------------------------------------------------------------------------- host
 struct ScanPlan {
   int qt, n_slabs, rows_per_slab;
@@ -414,9 +504,9 @@ extern "C" int tt_scan_workspace_bytes(int64_t n, int32_t d, int32_t nq, int32_t
   const ScanPlan p = plan_scan(n, nq, k);
   const int64_t entries = (int64_t)nq * p.n_slabs * k;
   int64_t b = entries * 8 + (int64_t)nq * p.n_slabs * 4;
-  if (p.qt > 1) {  // the fused fallback's first query tile, on its own wide slab plan
-    const ScanPlan pa = plan_scan(n, qpb_of(k), k);
-    b += (int64_t)qpb_of(k) * pa.n_slabs * (8 * (int64_t)k + 4);
+  if (p.qt > 1 && k <= CfgFb::kKMax) {  // the adaptive fallback's lists (the same memory)
+    const int64_t fb = fb_items_max(n, nq) * SC_QPW * (8 * (int64_t)k + 4);
+    b = b > fb ? b : fb;
   }
   *bytes = (b + 255) / 256 * 256;
   return TT_OK;
@@ -450,53 +540,64 @@ static int scan_f32_impl(const float* db, int64_t n, int32_t d, int64_t ld_db,
   hipStream_t st = (hipStream_t)stream;
   const bool wide = wide_k(k);
   const dim3 block(wide ? 64 * CfgWide::kWaves : 64 * CfgNarrow::kWaves);
-  // launch (tiles [qt0, qt1) of the plan ps, lists at (s_, r_, c_), done counters + doff)
-  auto launch = [&](const ScanPlan& ps, int qt0, int qt1, float* s_, int* r_, int* c_,
-                    int doff) -> int {
-    const dim3 grid(qt1 - qt0, ps.n_slabs);
+  if (done && p.qt > 1) {
+    // The filter's exact fallback for a batch of more than one 64-query tile: the flagged
+    // queries are compacted into slots 0 .. *qsel_n, and the adaptive kernel decides on the
+    // device how to spread them over the chip; its merge follows.  Both launches exit at once
+    // when nothing is flagged.
+    TT_REQUIRE(k <= CfgFb::kKMax, "fallback: k > 128");
+    float* fs = (float*)workspace;
+    int* fr = (int*)(fs + fb_items_max(n, nq) * SC_QPW * k);
+    int* fc = fr + fb_items_max(n, nq) * SC_QPW * k;
+#define TT_FB_CASE(E)                                                                         \
+  case E:                                                                                     \
+    hipLaunchKernelGGL(k_scan_fallback<E>, dim3(FB_GRID), dim3(64), 0, st, db, n, ld_db, q,   \
+                       ld_q, k, qsel, qsel_n, fs, fr, fc);                                    \
+    break;
+    switch (ep) {
+      TT_FB_CASE(64)
+      TT_FB_CASE(128)
+      TT_FB_CASE(256)
+      TT_FB_CASE(384)
+      TT_FB_CASE(512)
+      TT_FB_CASE(768)
+      default:
+        return fail(TT_ERR_UNSUPPORTED, "fallback: bad padded dim");
+    }
+#undef TT_FB_CASE
+    int rc = check_launch("k_scan_fallback");
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_merge_fallback, dim3(256), dim3(256), 0, st, fs, fr, fc, n, k, row_base,
+                       out_score, out_idx, qsel, qsel_n);
+    return check_launch("k_merge_fallback");
+  }
+  const dim3 grid(p.qt, p.n_slabs);
 #define TT_SCAN_CASE(E)                                                                       \
   case E:                                                                                     \
     if (wide)                                                                                 \
       hipLaunchKernelGGL((k_scan_topk_f32<E, CfgWide>), grid, block, 0, st, db, n, ld_db, q,  \
-                         nq, ld_q, k, ps.rows_per_slab, ps.n_slabs, s_, r_, c_, qsel, qsel_n, \
-                         done, row_base, out_score, out_idx, qt0, doff);                      \
+                         nq, ld_q, k, p.rows_per_slab, p.n_slabs, ws_s, ws_r, ws_c, qsel,     \
+                         qsel_n, done, row_base, out_score, out_idx);                         \
     else                                                                                      \
       hipLaunchKernelGGL((k_scan_topk_f32<E, CfgNarrow>), grid, block, 0, st, db, n, ld_db,   \
-                         q, nq, ld_q, k, ps.rows_per_slab, ps.n_slabs, s_, r_, c_, qsel,      \
-                         qsel_n, done, row_base, out_score, out_idx, qt0, doff);              \
+                         q, nq, ld_q, k, p.rows_per_slab, p.n_slabs, ws_s, ws_r, ws_c, qsel,  \
+                         qsel_n, done, row_base, out_score, out_idx);                         \
     break;
-    switch (ep) {
-      TT_SCAN_CASE(64)
-      TT_SCAN_CASE(128)
-      TT_SCAN_CASE(256)
-      TT_SCAN_CASE(384)
-      TT_SCAN_CASE(512)
-      TT_SCAN_CASE(768)
-      default:
-        return fail(TT_ERR_UNSUPPORTED, "tt_scan_topk_f32: bad padded dim");
-    }
-#undef TT_SCAN_CASE
-    return check_launch("k_scan_topk_f32");
-  };
   if (ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "tt_scan_topk_f32_timed: hipEventRecord(start) failed");
-  int rc;
-  if (done && p.qt > 1) {
-    // Fused fallback of a large batch: the flagged queries are compacted into slots
-    // 0 .. *qsel_n, so a handful of them all sit in query tile 0.  On the batch's plan that
-    // tile would get p.n_slabs blocks (16 at 1M rows: 2 flagged queries of a 10k batch cost
-    // 16 ms); tile 0 runs on its own one-tile plan instead (up to 512 slabs, lists after the
-    // batch plan's, done counter p.qt), the other tiles on the batch plan.  Both launches
-    // exit at once when nothing (or nothing past tile 0) is flagged.
-    const ScanPlan pa = plan_scan(n, qpb_of(k), k);
-    float* sa = (float*)(ws_c + (int64_t)nq * p.n_slabs);
-    int* ra = (int*)(sa + (int64_t)qpb_of(k) * pa.n_slabs * k);
-    int* ca = ra + (int64_t)qpb_of(k) * pa.n_slabs * k;
-    if ((rc = launch(pa, 0, 1, sa, ra, ca, p.qt))) return rc;
-    if ((rc = launch(p, 1, p.qt, ws_s, ws_r, ws_c, 0))) return rc;
-  } else if ((rc = launch(p, 0, p.qt, ws_s, ws_r, ws_c, 0))) {
-    return rc;
+  switch (ep) {
+    TT_SCAN_CASE(64)
+    TT_SCAN_CASE(128)
+    TT_SCAN_CASE(256)
+    TT_SCAN_CASE(384)
+    TT_SCAN_CASE(512)
+    TT_SCAN_CASE(768)
+    default:
+      return fail(TT_ERR_UNSUPPORTED, "tt_scan_topk_f32: bad padded dim");
   }
+#undef TT_SCAN_CASE
+  int rc = check_launch("k_scan_topk_f32");
+  if (rc) return rc;
   if (ev_stop && hipEventRecord((hipEvent_t)ev_stop, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "tt_scan_topk_f32_timed: hipEventRecord(stop) failed");
   if (done) return TT_OK;  // merged inside the scan launch
@@ -538,8 +639,9 @@ extern "C" int tt_scan_topk_f32_select(const float* db, int64_t n, int32_t d, in
 }
 
 namespace tt {
-// The bf16 filter's exact fallback (tt_filter.hip): the select-mode scan with the slab merge
-// fused into the scan launch (done: >= one zeroed counter per flagged-query tile).
+// The bf16 filter's exact fallback (tt_filter.hip): nq <= 64 -> the select-mode scan with the
+// slab merge fused into the scan launch (done: ONE zeroed counter, done[0], reset by the last
+// block); nq > 64 -> the adaptive fallback (k_scan_fallback + k_merge_fallback; done unused).
 int scan_f32_select_fused(const float* db, int64_t n, int32_t d, int64_t ld_db, int64_t row_base,
                           const float* q, int32_t nq, int64_t ld_q, int32_t k,
                           const int32_t* qsel, const int32_t* qsel_n, int* done,

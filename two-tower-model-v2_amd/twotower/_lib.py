@@ -74,6 +74,8 @@ SIGNATURES = {
                                             _i64, _vp, _vp, _vp]),
     "tt_sharded_workspace_bytes": (ctypes.c_int, [_i64, _i32, _i32, _i32, ctypes.POINTER(_i64)]),
     "tt_sharded_fallback_offset": (ctypes.c_int, [_i64, _i32, _i32, _i32, ctypes.POINTER(_i64)]),
+    "tt_filter_workspace_layout": (ctypes.c_int, [_i64, _i32, _i32, _i32, _i32,
+                                                  ctypes.POINTER(_i64)]),
     "tt_sharded_filter_begin": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _i64, _i32, _vp,
                                                _vp, _i64, _vp]),
     "tt_sharded_filter_full": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _i32, _i64, _i32,

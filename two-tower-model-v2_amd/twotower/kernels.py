@@ -114,6 +114,16 @@ def filter_fallback_count(workspace: torch.Tensor, n: int, d: int, nq: int, k: i
     return int(workspace[off.value:off.value + 4].view(torch.int32).item())
 
 
+def filter_workspace_layout(n: int, d: int, nq: int, k: int, sharded: bool = False) -> dict:
+    """Byte offsets of the band keys / counts, fallback flags and fallback count inside a
+    filter workspace (tt_filter_workspace_layout; diagnostic, for tests)."""
+    off = (ctypes.c_int64 * 5)()
+    check(lib().tt_filter_workspace_layout(n, d, nq, k, int(sharded), off),
+          "tt_filter_workspace_layout")
+    return {"band": off[0], "band_n": off[1], "flags": off[2], "fallback_count": off[3],
+            "band_cap": off[4]}
+
+
 def scan_topk_bf16(db: torch.Tensor, db16: torch.Tensor, n: int, d: int, q: torch.Tensor,
                    k: int, bounds, row_base: int = 0, workspace: torch.Tensor = None,
                    out=None, events=(None, None)):
