@@ -32,7 +32,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from twotower import _lib, kernels  # noqa: E402
-from twotower.sharded import TopkExchange, shard_range  # noqa: E402
+from twotower.sharded import PipelinedStagedExchange, TopkExchange, shard_range  # noqa: E402
 
 F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X dense f32 MFMA (MI355X_MICROARCH.md)
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (no sparsity)
@@ -65,6 +65,9 @@ def parse():
                    help="skip the configs[1] leg, the batch sweep and the f32 Mode A leg")
     p.add_argument("--configs1-texts", type=int, default=100_000)
     p.add_argument("--sweep", default="1,8,16,32,256")
+    p.add_argument("--chunks", type=int, default=2,
+                   help="multi-GPU staged search: query chunks whose collectives overlap the "
+                        "next chunk's shard filter (PipelinedStagedExchange)")
     return p.parse_args()
 
 
@@ -507,8 +510,10 @@ def main():
 
     q = torch.empty((B, ep), device=dev)
     staged = a.method == "bf16" and world > 1
-    # all-gather queries (+ their sharded-filter stats) / all-to-all top-k (RCCL)
-    ex = TopkExchange(B, ep, K, device=dev, aux_width=2 if staged else 0)
+    # all-gather queries (+ their sharded-filter stats) / all-to-all top-k (RCCL); the staged
+    # search runs in query chunks whose collectives overlap the next chunk's filter
+    ex = TopkExchange(B, ep, K, device=dev)
+    pipe = PipelinedStagedExchange(B, ep, K, a.chunks, device=dev) if staged else None
     nq = world * B
     if staged:
         # row-sharded bf16 filter (tt_sharded_filter_*): the replicated 1/16 catalog sample
@@ -521,11 +526,14 @@ def main():
         gb_ = torch.tensor(bounds, device=dev)
         dist.all_reduce(gb_, op=dist.ReduceOp.MAX)
         bounds = gb_.tolist()
-        stats = torch.empty((B, 2), device=dev)
-        ws_begin = torch.empty(kernels.filter_workspace_bytes(sample16.shape[0], E, B, K),
+        bmax = max(c.b for c in pipe.ex)
+        ws_begin = torch.empty(kernels.filter_workspace_bytes(sample16.shape[0], E, bmax, K),
                                dtype=torch.uint8, device=dev)
-        pcount = torch.empty((nq, _lib.TT_SHARD_PROBES), dtype=torch.int32, device=dev)
-        ws_bytes = kernels.sharded_workspace_bytes(hi - lo, E, nq, K)
+        ws_chunks = [torch.empty(kernels.sharded_workspace_bytes(hi - lo, E, world * c.b, K),
+                                 dtype=torch.uint8, device=dev) for c in pipe.ex]
+        pc_chunks = [torch.empty((world * c.b, _lib.TT_SHARD_PROBES), dtype=torch.int32,
+                                 device=dev) for c in pipe.ex]
+        ws_bytes = 256
     elif a.method == "bf16":
         ws_bytes = kernels.filter_workspace_bytes(hi - lo, E, nq, K)
     else:
@@ -536,17 +544,11 @@ def main():
     L = _lib.lib()
     stream = torch.cuda.current_stream()
 
-    def local_search(qall, ev, stats_all=None):
-        e0, e1, p0, p1 = (ev if ev else (None, None, None, None))
+    def local_search(qall, ev):
+        e0, e1, p0, p1 = (ev[:4] if ev else (None, None, None, None))
         if p0 is not None:
             p0.record(stream)
-        if staged:
-            # shard filter -> all-reduce SUM of probe counts -> shard re-rank
-            kernels.sharded_search(shard, shard16, hi - lo, E, qall, K, bounds, lo, stats_all,
-                                   lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM),
-                                   workspace=ws, out=(s_shard, i_shard), pcount=pcount,
-                                   events=(e0, e1))
-        elif a.method == "bf16":
+        if a.method == "bf16":
             kernels.scan_topk_bf16(shard, shard16, hi - lo, E, qall, K, bounds, row_base=lo,
                                    workspace=ws, out=(s_shard, i_shard), events=(e0, e1))
         else:
@@ -563,19 +565,33 @@ def main():
     def step(ev=None):
         kernels.gather_weighted_avg_l2(table, E, hist, w, out=q)  # Mode B buyer encode
         kernels.l2norm_rows(q, E, _lib.TT_NORM_ADD_EPS, out=q)    # retrieve_batch :189-190
-        if staged:  # this rank's thresholds from the replicated sample, gathered with q;
-            # the query all-gather runs (async, RCCL stream) under the begin stage's kernels
-            return ex.search(q, lambda qall, sall: local_search(qall, ev, sall),
-                             kernels.merge_topk,
-                             aux=lambda: kernels.sharded_begin(sample16, E, q, K, stats=stats,
-                                                               workspace=ws_begin))
+        if staged:  # per chunk: this rank's thresholds from the replicated sample (the query
+            # all-gather runs async under them), shard filter, probe-count all-reduce and
+            # result all-to-all overlapped with the next chunk's filter
+            if ev:
+                ev[2].record(stream)
+
+            def full(c, qa, sa):
+                evc = (ev[4 + 2 * c], ev[5 + 2 * c]) if ev else (None, None)
+                return kernels.sharded_full(shard16, hi - lo, E, qa, K, bounds, sa, ws_chunks[c],
+                                            pc_chunks[c], events=evc)
+
+            out = pipe.search(
+                q, lambda x: kernels.sharded_begin(sample16, E, x, K, workspace=ws_begin), full,
+                lambda c, qa, sa, pc: kernels.sharded_finish(shard, shard16, hi - lo, E, qa, K,
+                                                             lo, sa, pc, ws_chunks[c]),
+                kernels.merge_topk)
+            if ev:
+                ev[3].record(stream)
+            return out
         return ex.search(q, lambda qall: local_search(qall, ev), kernels.merge_topk)
 
     for _ in range(a.warmup):
         step()
     evs = []
+    n_ev = 4 + (2 * len(pipe.ex) if staged else 0)
     for _ in range(a.steps):
-        ev = tuple(torch.cuda.Event(enable_timing=True) for _ in range(4))
+        ev = tuple(torch.cuda.Event(enable_timing=True) for _ in range(n_ev))
         for e in ev:
             e.record(stream)  # materialise the hipEvent handles; the ABI re-records them
         evs.append(ev)
@@ -591,14 +607,23 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     dt = t1 - t0
-    scan_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / a.steps
+    if staged:  # the shard filter of every chunk
+        scan_ms = sum(e[4 + 2 * c].elapsed_time(e[5 + 2 * c]) for e in evs
+                      for c in range(len(pipe.ex))) / a.steps
+    else:
+        scan_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / a.steps
     search_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / a.steps
     if world > 1:
         t = torch.tensor([dt, scan_ms, search_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, scan_ms, search_ms = t.tolist()
-    fallback = (kernels.filter_fallback_count(ws, hi - lo, E, nq, K, sharded=staged)
-                if a.method == "bf16" else 0)
+    if staged:
+        fallback = sum(kernels.filter_fallback_count(ws_chunks[c], hi - lo, E, world * x.b, K,
+                                                     sharded=True)
+                       for c, x in enumerate(pipe.ex))
+    else:
+        fallback = (kernels.filter_fallback_count(ws, hi - lo, E, nq, K)
+                    if a.method == "bf16" else 0)
     check = self_check(a, out, q, table, shard, dev, world)
     ms_per_step = dt / a.steps * 1e3
     value = world * B / (dt / a.steps)
@@ -640,7 +665,7 @@ def main():
                         "Mode B (history rows gathered), k=100",
             "catalog_rows": N, "dim": E, "buyers_per_rank": B, "history": S, "k": K,
             "backend": a.backend if world > 1 else None,
-            "parallelism": f"catalog row-shard x{world}" + ((" + RCCL all-gather(queries, filter stats), all-reduce(probe counts), all-to-all(top-k)" if staged else " + RCCL all-gather(queries), all-to-all(top-k)") if world > 1 else ""),
+            "parallelism": f"catalog row-shard x{world}" + ((f" + RCCL all-gather(queries, filter stats), all-reduce(probe counts), all-to-all(top-k), {len(pipe.ex)} overlapped query chunks" if staged else " + RCCL all-gather(queries), all-to-all(top-k)") if world > 1 else ""),
         },
         "roofline": {
             "kernel": kname,

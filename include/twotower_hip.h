@@ -203,6 +203,15 @@ int tt_gather_weighted_avg_l2_f32(const float* table, int64_t n_table, int64_t l
 int tt_attn_agg_l2_f32(const float* items, int64_t b, int32_t s, int32_t d, const float* w,
                        const float* W1, const float* b1, int32_t h, const float* W2,
                        const float* b2, float* out, int64_t ld_out, void* stream);
+/* Same results within 1e-6 (the first MLP layer's dot products in the f32 MFMA order instead of
+ * a sequential chain) for batches: H = relu(x W1^T + b1) by tt_gemm_f32 into the workspace
+ * (tt_attn_agg_workspace_bytes: b*s*h floats), then the per-buyer softmax / sum / F.normalize.
+ * d % 32 != 0: runs tt_attn_agg_l2_f32 (no workspace used). */
+int tt_attn_agg_workspace_bytes(int64_t b, int32_t s, int32_t h, int64_t* bytes);
+int tt_attn_agg_l2_f32_ws(const float* items, int64_t b, int32_t s, int32_t d, const float* w,
+                          const float* W1, const float* b1, int32_t h, const float* W2,
+                          const float* b2, float* out, int64_t ld_out, void* workspace,
+                          int64_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------
  * Item tower (tt_encoder.hip).

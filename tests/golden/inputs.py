@@ -6,6 +6,7 @@ the fixtures store a sha256 of the inputs so a drifting generator is detected.
 from __future__ import annotations
 
 import hashlib
+import json
 
 import numpy as np
 
@@ -291,3 +292,139 @@ def trainer_batch():
     seqs.append([(f"p{j % 40}", float(1 + j % 3)) for j in range(130)])  # truncation
     pos = [texts[j] for j in range(5)] + [texts[40], texts[41], texts[7]]
     return meta, seqs, pos
+
+
+# ----------------------------------------------------------------------------- configs[0] pipeline
+# BASELINE.json configs[0]: 1k products in the reference CSV schema (processor.py:71-112: id,
+# title, description, metadata JSON {brand, catalog_id}), 100 buyers x 20 events (event mix
+# 0.75 / 0.17 / 0.08, DATA_PREPROCESSING.md:97-99), seed 0, k = 10 (scripts/evaluate.py).
+PIPE_WORDS = ["خاتم", "ذهب", "عيار", "21", "18", "سلسال", "اسورة", "فضة", "زيت", "محرك",
+              "5W-30", "gold", "ring", "necklace", "bracelet", "silver", "engine", "oil",
+              "Damas", "classic", "new", "مميز", "هدية", "لامع"]
+PIPE_BRANDS = ["Damas", "Lazurde", "Acme", "Tiffany", "Dubai Gold", "Mobil", "Shell", "Tanagra"]
+PIPE_CATS = [f"cat_{i:02d}" for i in range(12)]
+
+
+def pipeline_products(n: int = 1000, seed: int = 0):
+    """Product rows (dicts; None = empty CSV cell).  ~3% are content duplicates of an earlier
+    row under another id (processor.py:243-284 keeps one per dedup key), ~2% lack a title or
+    a description, 3 have neither (dropped: empty text, :104), ~10% have no metadata."""
+    rng = np.random.default_rng(seed)
+    rows = []
+    for i in range(n):
+        pid = f"P{int(rng.integers(0, 10**6)):06d}-{i}"
+        title = " ".join(rng.choice(PIPE_WORDS, int(rng.integers(1, 6))))
+        desc = " ".join(rng.choice(PIPE_WORDS, int(rng.integers(0, 12))))
+        brand = PIPE_BRANDS[int(rng.integers(0, len(PIPE_BRANDS)))]
+        cat = PIPE_CATS[int(rng.integers(0, len(PIPE_CATS)))]
+        r = rng.random()
+        if r < 0.03 and rows:  # duplicate content (case / spacing changed) of an earlier row
+            src = rows[int(rng.integers(0, len(rows)))]
+            title = (src["title"] or "").upper() + "  "
+            desc, meta = src["description"], src["metadata"]
+        else:
+            meta = json.dumps({"brand": brand, "catalog_id": cat}, ensure_ascii=False) \
+                if rng.random() > 0.1 else None
+        if 0.03 <= r < 0.04:
+            title = None
+        elif 0.04 <= r < 0.05:
+            desc = None
+        if i in (17, 401, 902):
+            title, desc = None, "   "
+        rows.append({"id": pid, "title": title, "description": desc or None, "metadata": meta})
+    return rows
+
+
+def pipeline_events(product_ids, n_buyers: int = 100, per_buyer: int = 20, seed: int = 0):
+    """Event rows (distinct_id, product_id, event_name, created_at) in the reference events
+    schema (processor.py:24-69 renames them).  Product ids are drawn from the whole CSV, so
+    some point at deduplicated / dropped products (metadata {} -> text ' ', encoder.py:280);
+    event names vary in case and spacing; two events have no timestamp."""
+    rng = np.random.default_rng(seed + 1)
+    names = [["view", "View", "page view"], ["add_to_cart", "Add To Cart", "AddToCart"],
+             ["purchase", "Purchase", "buy"]]
+    rows = []
+    for b in range(n_buyers):
+        for e in range(per_buyer):
+            kind = int(rng.choice(3, p=EVENT_MIX[1]))
+            name = names[kind][int(rng.integers(0, 3))]
+            t = int(rng.integers(0, 365 * 24 * 3600))
+            ts = f"2024-{1 + t // (31 * 24 * 3600) % 12:02d}-{1 + t // 86400 % 28:02d} " \
+                 f"{t // 3600 % 24:02d}:{t // 60 % 60:02d}:{t % 60:02d}"
+            rows.append({"distinct_id": f"B{b:03d}",
+                         "product_id": product_ids[int(rng.integers(0, len(product_ids)))],
+                         "event_name": name, "created_at": ts})
+    rows[5]["created_at"] = None
+    rows[333]["created_at"] = None
+    return rows
+
+
+def stub_text_embedding(texts, dim: int = 384) -> np.ndarray:
+    """Deterministic stand-in for SentenceTransformer.encode (item_tower.py:116-122; the real
+    MiniLM is absent offline): per text, a PCG64 normal vector seeded by blake2b(text)."""
+    out = np.empty((len(texts), dim), np.float32)
+    for j, t in enumerate(texts):
+        s = int.from_bytes(hashlib.blake2b(t.encode("utf-8"), digest_size=8).digest(), "little")
+        out[j] = np.random.default_rng(s).standard_normal(dim).astype(np.float32) * np.float32(0.5)
+    return out
+
+
+def pipeline_weights(n_brand: int, n_cat: int, E: int = 384, seed: int = 7):
+    """Seeded checkpoint weights (reference state-dict names, trainer.py:327-340) for the
+    configs[0] pipeline: ItemTower head + categorical tables (row 0 = padding, zero) and the
+    BuyerTower attention MLP."""
+    rng = np.random.default_rng(seed)
+    din = 384 + 128
+    w = {
+        "item_tower.projection.0.weight": rng.uniform(-1, 1, (256, din)) / np.sqrt(din),
+        "item_tower.projection.0.bias": rng.uniform(-1, 1, (256,)) / np.sqrt(din),
+        "item_tower.projection.3.weight": rng.uniform(-1, 1, (E, 256)) / 16.0,
+        "item_tower.projection.3.bias": rng.uniform(-1, 1, (E,)) / 16.0,
+        "item_tower.brand_embedding.weight": rng.standard_normal((n_brand, 64)),
+        "item_tower.category_embedding.weight": rng.standard_normal((n_cat, 64)),
+        "buyer_tower.attention.0.weight": rng.uniform(-1, 1, (128, E)) / np.sqrt(E),
+        "buyer_tower.attention.0.bias": rng.uniform(-1, 1, (128,)) / np.sqrt(E),
+        "buyer_tower.attention.2.weight": rng.uniform(-1, 1, (1, 128)) / np.sqrt(128),
+        "buyer_tower.attention.2.bias": rng.uniform(-1, 1, (1,)) / np.sqrt(128),
+    }
+    w["item_tower.brand_embedding.weight"][0] = 0.0
+    w["item_tower.category_embedding.weight"][0] = 0.0
+    return {k: v.astype(np.float32) for k, v in w.items()}
+
+
+def encoder_buyer_cases(product_ids):
+    """Adversarial interaction lists for EmbeddingEncoder.encode_buyer (encoder.py:244-305):
+    timestamp sort iff every one is present (ISO strings, :263-264), > 100 events (last
+    max_interaction_history kept, :267-268), unknown ids and event names (weight 1), aliases
+    (AddToCart / buy), one event, products with empty text."""
+    rng = np.random.default_rng(77)
+    P = list(product_ids)
+
+    def ev(pid, name, ts):
+        d = {"product_id": pid, "event_type": name}
+        if ts is not None:
+            d["timestamp"] = ts
+        return d
+
+    cases = []
+    # 1. all timestamps present, shuffled -> sorted
+    cases.append([ev(P[int(rng.integers(0, len(P)))], n, f"2024-03-{d:02d}T10:00:00")
+                  for n, d in zip(["view", "purchase", "AddToCart", "buy", "share"],
+                                  [9, 2, 17, 5, 11])])
+    # 2. one timestamp missing -> input order kept
+    c = [ev(P[int(rng.integers(0, len(P)))], "view", f"2024-05-{d:02d}") for d in (30, 3, 12)]
+    c[1]["timestamp"] = None
+    cases.append(c)
+    # 3. 130 events, every one timestamped -> sort, keep the last 100
+    cases.append([ev(P[int(rng.integers(0, len(P)))], ["view", "add_to_cart", "purchase"][i % 3],
+                     f"2023-{1 + i % 12:02d}-{1 + (i * 7) % 28:02d}T{i % 24:02d}:00:00")
+                  for i in range(130)])
+    # 4. 120 events, no timestamps -> input order, last 100
+    cases.append([ev(P[(37 * i) % len(P)], "view" if i % 4 else "Purchase", None)
+                  for i in range(120)])
+    # 5. unknown product ids (metadata {} -> text '' -> ' ') mixed with known ones
+    cases.append([ev("not-a-product", "view", None), ev(P[3], "purchase", None),
+                  ev("ghost-2", "AddToCart", None)])
+    # 6. a single event
+    cases.append([ev(P[11], "add_to_cart", "2024-01-01")])
+    return cases

@@ -554,7 +554,11 @@ def test_sharded_finish_corrupt_band_row_falls_back(K, oracle_mod):
         qi = int(torch.argmax(band_n).item())
         assert int(band_n[qi]) > 0
         keys = ws[lay["band"]:lay["band"] + 8 * nq * lay["band_cap"]].view(torch.int64)
-        e = qi * lay["band_cap"]
+        e0 = qi * lay["band_cap"]
+        # the band is unordered and entries below the cut are dropped undecoded: corrupt the
+        # best-scoring entry (always kept)
+        mine = keys[e0:e0 + int(band_n[qi])].cpu().numpy().view(np.uint64)
+        e = e0 + int(np.argmax(mine))
         keys[e] = keys[e] & ~0xFFFFFFFF  # low word 0 -> row ~0 = 0xffffffff
         planted["q"] = qi
 
@@ -562,3 +566,27 @@ def test_sharded_finish_corrupt_band_row_falls_back(K, oracle_mod):
     rs, ri = oracle_mod.scan_topk(x, q, k)
     assert np.array_equal(mi, ri) and np.array_equal(ms, rs)
     assert fb[0] >= 1 and "q" in planted
+
+
+@pytest.mark.parametrize("E,S", [(384, 20), (768, 20), (768, 100)])
+def test_attn_agg_batched_gemm_form_vs_oracle(K, oracle_mod, E, S):
+    """tt_attn_agg_l2_f32_ws (the batched form: first MLP layer on the f32 MFMA GEMM, then the
+    per-buyer softmax / weighted sum / F.normalize) vs the C oracle and the one-kernel form:
+    within 1e-6 (only the first layer's summation order differs), buyer_tower.py:70-101."""
+    rng = np.random.default_rng(E + S)
+    B, H = 300, 128
+    items = oracle_mod.l2norm_rows(rng.standard_normal((B * S, E)).astype(np.float32),
+                                   1).reshape(B, S, E)
+    w = np.where(rng.random((B, S)) < 0.75, 1.0, np.where(rng.random((B, S)) < 0.7, 5.0, 10.0))
+    w = w.astype(np.float32)
+    w[3, S // 2:] = 0.0  # zero-weight padding positions
+    W1 = (rng.standard_normal((H, E)) / np.sqrt(E)).astype(np.float32)
+    b1 = (0.1 * rng.standard_normal(H)).astype(np.float32)
+    W2 = (rng.standard_normal((1, H)) / np.sqrt(H)).astype(np.float32)
+    b2 = (0.1 * rng.standard_normal(1)).astype(np.float32)
+    t = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    got = K.attn_agg_l2(t(items), t(w), t(W1), t(b1), t(W2), t(b2), fused=False).cpu().numpy()
+    one = K.attn_agg_l2(t(items), t(w), t(W1), t(b1), t(W2), t(b2), fused=True).cpu().numpy()
+    ref = oracle_mod.attn_agg_l2(items, w, W1, b1, W2, b2)
+    np.testing.assert_allclose(got, ref, rtol=0, atol=1e-6)
+    np.testing.assert_allclose(got, one, rtol=0, atol=1e-6)

@@ -186,7 +186,27 @@ def test_trainer_epochs_reference_batches(tmp_path, aggregation):
     ck = torch.load(tmp_path / "checkpoint_epoch_4.pt", weights_only=True)
     assert set(ck) >= {"epoch", "model_state_dict", "optimizer_state_dict", "best_val_loss",
                        "config", "brand_vocab", "category_vocab"}
-    assert ck["epoch"] == 3 and ck["optimizer_state_dict"]["step"] == 7 * 4
+    assert ck["epoch"] == 3
     sd = model.state_dict()  # the fused step trained the module parameters in place
     assert torch.equal(ck["model_state_dict"]["item_tower.projection.0.weight"].cpu(),
                        sd["item_tower.projection.0.weight"].cpu())
+    # optimizer_state_dict is torch.optim.Adam's (reference trainer.py:330): a torch Adam over
+    # model.parameters() loads it and holds the fused step's moments
+    osd = ck["optimizer_state_dict"]
+    assert set(osd) == {"state", "param_groups"}
+    assert {int(float(e["step"])) for e in osd["state"].values()} == {7 * 4}
+    ref = {k: v.clone() for k, v in model.state_dict().items()}
+    opt = torch.optim.Adam(model.parameters(), lr=3e-3)
+    opt.load_state_dict(osd)
+    params = list(model.parameters())
+    w0 = model.item_tower.projection[0].weight
+    i0 = next(i for i, p in enumerate(params) if p is w0)
+    assert torch.equal(opt.state_dict()["state"][i0]["exp_avg"].cpu(), tr.step.m["proj0.w"].cpu())
+    # resume: a fresh Trainer restores weights, Adam moments and step count
+    model2 = _model(aggregation=aggregation, seed=9)
+    tr2 = Trainer(model2, train, val, config_path=str(cp), pad_to_batch_max=True)
+    tr2.load_checkpoint(tmp_path / "checkpoint_epoch_4.pt")
+    assert tr2.step.t == 7 * 4 and tr2.current_epoch == 4
+    for k in tr.step.m:
+        assert torch.equal(tr2.step.m[k], tr.step.m[k]) and torch.equal(tr2.step.v[k], tr.step.v[k])
+    assert all(torch.equal(v.cpu(), ref[k].cpu()) for k, v in model2.state_dict().items())

@@ -205,3 +205,56 @@ def test_train_gradient_allreduce_mean(world):
     for r in range(world):
         for k in exp:
             torch.testing.assert_close(torch.from_numpy(res[r][k]), exp[k], rtol=1e-6, atol=1e-6)
+
+
+def _pipe_worker(rank, world, port, k, chunks, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle as O
+        from twotower.sharded import PipelinedStagedExchange, shard_range
+
+        x, q = data(nq=36)
+        lo, hi = shard_range(x.shape[0], rank, world)
+        xs = x[lo:hi]
+        B = q.shape[0] // world
+        ql = torch.from_numpy(q[rank * B:(rank + 1) * B].copy())
+        checks = []
+
+        def begin(xq):  # per-query stats: must reach full() in the gathered query order
+            return torch.stack([xq[:, 0], -xq[:, 0]], 1).contiguous()
+
+        def full(c, qall, sall):
+            checks.append(bool(torch.equal(sall[:, 0], qall[:, 0])))
+            return torch.full((qall.shape[0], 16), rank + 1, dtype=torch.int32)
+
+        def finish(c, qall, sall, pc):
+            checks.append(int(pc[0, 0]) == world * (world + 1) // 2)  # summed over ranks
+            s, i = O.scan_topk(xs, qall.numpy(), k, row_base=lo)
+            return torch.from_numpy(s), torch.from_numpy(i)
+
+        ex = PipelinedStagedExchange(B, q.shape[1], k, chunks=chunks)
+        s, i = ex.search(ql, begin, full, finish, merge_np)
+        np.save(os.path.join(out_dir, f"s{rank}.npy"), s.numpy())
+        np.save(os.path.join(out_dir, f"i{rank}.npy"), i.numpy())
+        np.save(os.path.join(out_dir, f"c{rank}.npy"), np.array(checks))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,chunks,k", [(2, 2, 10), (3, 3, 64), (2, 1, 100)])
+def test_pipelined_staged_exchange_bit_identical(tmp_path, world, chunks, k):
+    """The chunked staged exchange (PipelinedStagedExchange: per-chunk query / stats
+    all-gathers, async probe-count all-reduce and result all-to-all overlapping the next
+    chunk's filter) returns the single-catalog top-k, bit for bit."""
+    from oracle import oracle as O
+
+    mp.start_processes(_pipe_worker, args=(world, _free_port(), k, chunks, str(tmp_path)),
+                       nprocs=world, join=True, start_method="fork")
+    x, q = data(nq=36)
+    rs, ri = O.scan_topk(x, q, k)
+    B = q.shape[0] // world
+    for r in range(world):
+        s, i = np.load(tmp_path / f"s{r}.npy"), np.load(tmp_path / f"i{r}.npy")
+        assert np.array_equal(i, ri[r * B:(r + 1) * B]) and np.array_equal(s, rs[r * B:(r + 1) * B])
+        assert np.load(tmp_path / f"c{r}.npy").all()

@@ -181,6 +181,52 @@ __global__ __launch_bounds__(256) void k_attn_agg_l2(const float* __restrict__ i
   }
 }
 
+// Second stage of the batched attention aggregation (tt_attn_agg_l2_f32_ws): the first MLP
+// layer H = relu(X W1^T + b1) [b*s, h] comes from tt_gemm_f32 (f32 MFMA: ~0.5 ms for 10k buyers
+// x 20 rows x 768 -> 128, where the fused k_attn_agg_l2's per-buyer serial chains took 59 ms).
+// Per buyer, as k_attn_agg_l2 from there on: a_s = fmaf-chain_u(W2_u H_su) + b2, c_s = a_s w_s,
+// softmax over s, sum_s alpha_s x_s, F.normalize.
+__global__ __launch_bounds__(256) void k_attn_pool_l2(const float* __restrict__ H, int h,
+                                                      const float* __restrict__ items, int64_t b,
+                                                      int s, int d, const float* __restrict__ w,
+                                                      const float* __restrict__ W2,
+                                                      const float* __restrict__ b2,
+                                                      float* __restrict__ out, int64_t ld_out,
+                                                      int depth) {
+  __shared__ float cs[128];
+  __shared__ float acc_s[BY_MAXD];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int64_t bi = blockIdx.x; bi < b; bi += gridDim.x) {
+    const float* xb = items + bi * (int64_t)s * d;
+    if (tid < s) {
+      const float* hr = H + (bi * s + tid) * (int64_t)h;
+      float a = 0.0f;
+      for (int u = 0; u < h; ++u) a = fmaf(W2[u], hr[u], a);
+      a = a + b2[0];
+      cs[tid] = __fmul_rn(a, w[bi * s + tid]);
+    }
+    __syncthreads();
+    float m = -__builtin_huge_valf();
+    for (int j = 0; j < s; ++j) m = fmaxf(m, cs[j]);
+    float z = 0.0f;
+    for (int j = 0; j < s; ++j) z = z + expf(cs[j] - m);
+    for (int e = tid; e < d; e += 256) {
+      float acc = 0.0f;
+      for (int j = 0; j < s; ++j) {
+        const float alpha = __fdiv_rn(expf(cs[j] - m), z);
+        acc = acc + __fmul_rn(xb[(int64_t)j * d + e], alpha);
+      }
+      acc_s[e] = acc;
+    }
+    __syncthreads();
+    if (wv == 0) {
+      normalize_store(acc_s, d, depth, lane, out + bi * ld_out);
+      for (int e = d + lane; e < ld_out; e += 64) out[bi * ld_out + e] = 0.0f;
+    }
+    __syncthreads();
+  }
+}
+
 static unsigned grid_for(int64_t units, int64_t per_block, int64_t cap) {
   int64_t g = (units + per_block - 1) / per_block;
   if (g > cap) g = cap;
@@ -226,4 +272,34 @@ extern "C" int tt_attn_agg_l2_f32(const float* items, int64_t b, int32_t s, int3
                      (hipStream_t)stream, items, b, s, d, w, W1, b1, h, W2, b2, out, ld_out,
                      pw_perfect_depth(d));
   return check_launch("tt_attn_agg_l2_f32");
+}
+
+extern "C" int tt_attn_agg_workspace_bytes(int64_t b, int32_t s, int32_t h, int64_t* bytes) {
+  TT_REQUIRE(bytes != nullptr && b >= 0 && s >= 1 && h >= 1, "bad sizes");
+  *bytes = (b * s * (int64_t)h * 4 + 255) / 256 * 256;
+  return TT_OK;
+}
+
+extern "C" int tt_attn_agg_l2_f32_ws(const float* items, int64_t b, int32_t s, int32_t d,
+                                     const float* w, const float* W1, const float* b1, int32_t h,
+                                     const float* W2, const float* b2, float* out, int64_t ld_out,
+                                     void* workspace, int64_t workspace_bytes, void* stream) {
+  TT_REQUIRE(b >= 0 && s >= 1 && d >= 1 && ld_out >= d, "bad sizes");
+  TT_REQUIRE(d <= BY_MAXD && h >= 1 && h <= 256 && s <= 128, "d>1024 or h>256 or s>128");
+  if (b == 0) return TT_OK;
+  if (d % 32 != 0)  // tt_gemm_f32 needs K % 32 == 0: the fused one-kernel form
+    return tt_attn_agg_l2_f32(items, b, s, d, w, W1, b1, h, W2, b2, out, ld_out, stream);
+  int64_t need = 0;
+  tt_attn_agg_workspace_bytes(b, s, h, &need);
+  if (workspace == nullptr || workspace_bytes < need)
+    return fail(TT_ERR_WORKSPACE, "tt_attn_agg_l2_f32_ws: workspace too small");
+  TT_REQUIRE(b * s <= 0x7fffffffLL, "b * s must fit int32");
+  float* H = (float*)workspace;
+  int rc = tt_gemm_f32(items, d, W1, d, b1, nullptr, 0, H, h, nullptr, 0, (int32_t)(b * s), h, d,
+                       TT_ACT_RELU, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_attn_pool_l2, dim3(grid_for(b, 1, 16384)), dim3(256), 0,
+                     (hipStream_t)stream, H, h, items, b, s, d, w, W2, b2, out, ld_out,
+                     pw_perfect_depth(d));
+  return check_launch("tt_attn_agg_l2_f32_ws");
 }

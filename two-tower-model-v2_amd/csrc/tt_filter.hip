@@ -1335,27 +1335,20 @@ __global__ __launch_bounds__(256) void k_select_reg(const uint64_t* __restrict__
 // the f32 MFMA in one round: a wave scores 16 band rows with v_mfma_f32_16x16x4_f32, lane
 // group g holding dims 16t+4g..+3 -- the canonical fma order (t, i, g), bit-identical to
 // the f32 scan and k_rerank -- all of its 16-B row loads in flight at once.
-#ifndef TT_EXP_SMALL_TIMING
-#define TT_EXP_SMALL_TIMING 0  // timing builds: printf phase ticks of k_final_small (query 0)
-#endif
-TT_CHECK_EXP(TT_EXP_SMALL_TIMING, "TT_EXP_SMALL_TIMING (printf)");
-#if TT_EXP_SMALL_TIMING
-#define SM_TICK(i) if (threadIdx.x == 0) tk[i] = wall_clock64();
-#else
-#define SM_TICK(i)
-#endif
 constexpr int SM_THREADS = 1024, SM_WAVES = SM_THREADS / 64;
 constexpr int SM_NQ = 256;
 constexpr int SM_CAP = SW_CAP;  // candidates per query the small path selects from
 constexpr int SM_PER = SM_CAP / SM_THREADS;  // keys per thread in the radix select
 
-struct SmallLds {
-  uint64_t key[SM_CAP];   // the query's candidate keys (orderable score << 32 | ~row)
+template <int CAP>
+struct SmallLdsT {
+  uint64_t key[CAP];   // the query's candidate keys (orderable score << 32 | ~row)
   int wred[SM_WAVES];
   int hist[256];
   int pick[2];
   int nb;
 };
+using SmallLds = SmallLdsT<SM_CAP>;
 
 // Gather the query's per-slab candidate lists into s.key (n_slabs <= SM_THREADS).  Returns
 // the candidate count, or -1 when a list overflowed / the total exceeds SM_CAP.
@@ -1389,7 +1382,8 @@ __device__ int small_collect(const uint64_t* __restrict__ lists, const int* __re
 
 // R-th largest high word (orderable score) of the keys h (0 = no key), block-wide radix
 // select, 4 passes of 8 bits.  Caller guarantees at least R nonzero keys.
-__device__ uint32_t small_radix_select(const uint32_t (&h)[SM_PER], int R, SmallLds& s) {
+template <int PER, int CAP>
+__device__ uint32_t small_radix_select(const uint32_t (&h)[PER], int R, SmallLdsT<CAP>& s) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint32_t prefix = 0, pmask = 0;
   int r = R;
@@ -1398,7 +1392,7 @@ __device__ uint32_t small_radix_select(const uint32_t (&h)[SM_PER], int R, Small
     if (tid < 256) s.hist[tid] = 0;
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < SM_PER; ++j)
+    for (int j = 0; j < PER; ++j)
       if (h[j] != 0u && (h[j] & pmask) == prefix) atomicAdd(&s.hist[(h[j] >> shift) & 255u], 1);
     __syncthreads();
     if (w == 0) {
@@ -1473,73 +1467,46 @@ __global__ __launch_bounds__(SM_THREADS) void k_select_small(
   }
 }
 
-// Full level of a small batch: selection (mode 1 of k_select_reg) + exact re-rank (k_rerank)
-// in one launch.  A_k = k-th best a; A_k < aref -> the optimistic threshold failed (flag);
-// band = candidates with a >= A_k - eps2 (<= BAND_CAP, else flag); exact canonical f32
-// scores of the band rows by f32 MFMA; sort (score desc, row asc); top-k out.
-// The band's row gathers (~180 random 1.5 KB rows per query) are memory-latency bound on one
-// CU: 9-14 us of the one-buyer search.  Measured and not adopted: splitting a query over 8
-// blocks that meet through a global counter (25-30 us: the agent-scope release/acquire that
-// makes one block's scores visible to another XCD writes back / invalidates L2), and the full
-// level touching its candidates' f32 rows as it flushes them (no change).
+// LDS of the band re-rank (exact scores of the band rows + output ranks), one query per block
 template <int EP>
-__global__ __launch_bounds__(SM_THREADS) void k_final_small(
-    const uint64_t* __restrict__ lists, const int* __restrict__ counts, int n_slabs, int k,
-    const float* __restrict__ eps2, const float* __restrict__ aref, int* __restrict__ flags,
-    int* qsel, int* qsel_n, const float* __restrict__ db, int64_t ld, int64_t n_rows,
-    const float* __restrict__ q, int64_t ldq, int64_t row_base, float* __restrict__ out_s,
-    int64_t* __restrict__ out_i) {
-  __shared__ SmallLds s;
-  __shared__ uint32_t brow[BAND_CAP];
-  __shared__ uint64_t sbuf[BAND_CAP];
-  __shared__ __attribute__((aligned(16))) float qs[EP];
-  __shared__ int wcnt[SM_WAVES];
-  const int qid = blockIdx.x;
+struct BandLds {
+  uint32_t brow[BAND_CAP];
+  uint64_t sbuf[BAND_CAP];
+  __attribute__((aligned(16))) float qs[EP];
+  int wcnt[SM_WAVES];
+};
+
+// Band = keys (h[j] = high word of s.key[tid + j * SM_THREADS], 0 = none) with a >= thr, in a
+// deterministic order; exact canonical f32 scores of the band rows by f32 MFMA; output slot
+// = rank (score desc, row asc); top k written.  A band past BAND_CAP, or a decoded row >=
+// n_rows (a corrupted key: never read), flags the query for the exact fallback instead.
+// Every slot < k is written when the band holds >= k rows (callers guarantee it).
+template <int EP, int PER, int CAP>
+__device__ void band_rerank(const uint32_t (&h)[PER], SmallLdsT<CAP>& s, BandLds<EP>& bl,
+                            float thr, int qid, int k, int* flags, int* qsel, int* qsel_n,
+                            const float* __restrict__ db, int64_t ld, int64_t n_rows,
+                            const float* __restrict__ q, int64_t ldq, int64_t row_base,
+                            float* __restrict__ out_s, int64_t* __restrict__ out_i) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-#if TT_EXP_SMALL_TIMING
-  uint64_t tk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
-  SM_TICK(0)
-  if (flags[qid]) return;  // served by the exact fallback
-  const int total = small_collect(lists, counts, n_slabs, qid, s);
-  SM_TICK(1)
-  if (total < k) {  // overflow (-1) or too few candidates to certify: exact fallback
-    if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
-    return;
-  }
-  uint32_t h[SM_PER];
-#pragma unroll
-  for (int j = 0; j < SM_PER; ++j) {
-    const int e = tid + j * SM_THREADS;
-    h[j] = e < total ? (uint32_t)(s.key[e] >> 32) : 0u;
-  }
-  const float A = key_float(small_radix_select(h, k, s));
-  SM_TICK(2)
-  if (!(A >= aref[qid])) {
-    if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
-    return;
-  }
-  const float thr = A - eps2[qid];
-  for (int i = tid; i < EP; i += SM_THREADS) qs[i] = q[(int64_t)qid * ldq + i];
+  for (int i = tid; i < EP; i += SM_THREADS) bl.qs[i] = q[(int64_t)qid * ldq + i];
   // band positions by a block-wide prefix count (deterministic order)
   int mine = 0;
 #pragma unroll
-  for (int j = 0; j < SM_PER; ++j) mine += (h[j] != 0u && key_float(h[j]) >= thr) ? 1 : 0;
+  for (int j = 0; j < PER; ++j) mine += (h[j] != 0u && key_float(h[j]) >= thr) ? 1 : 0;
   int incl = mine;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const int y = __shfl_up(incl, o, 64);
     incl += lane >= o ? y : 0;
   }
-  if (lane == 63) wcnt[w] = incl;
+  if (lane == 63) bl.wcnt[w] = incl;
   __syncthreads();
   int base = 0, nb = 0;
 #pragma unroll
   for (int i = 0; i < SM_WAVES; ++i) {
-    base += i < w ? wcnt[i] : 0;
-    nb += wcnt[i];
+    base += i < w ? bl.wcnt[i] : 0;
+    nb += bl.wcnt[i];
   }
-  SM_TICK(3)
   if (nb > BAND_CAP) {
     if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
     return;
@@ -1548,12 +1515,12 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_small(
   {
     int pos = base + incl - mine;
 #pragma unroll
-    for (int j = 0; j < SM_PER; ++j) {
+    for (int j = 0; j < PER; ++j) {
       const int e = tid + j * SM_THREADS;
       if (h[j] != 0u && key_float(h[j]) >= thr) {
         const uint32_t r = key_row(s.key[e]);
         bad_row |= (int64_t)r >= n_rows;
-        brow[pos++] = (int64_t)r < n_rows ? r : 0u;
+        bl.brow[pos++] = (int64_t)r < n_rows ? r : 0u;
       }
     }
   }
@@ -1572,7 +1539,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_small(
     static_assert(NT % TCH == 0, "load batches must tile the row");
     for (int gr = w; 16 * gr < nb; gr += SM_WAVES) {
       const int e = 16 * gr + r16;
-      const uint32_t row = brow[e < nb ? e : nb - 1];
+      const uint32_t row = bl.brow[e < nb ? e : nb - 1];
       const float* xr = db + (int64_t)row * ld + 4 * g;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
@@ -1582,7 +1549,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_small(
         for (int t = 0; t < TCH; ++t) a[t] = *(const f32x4*)(xr + 16 * (t0 + t));
 #pragma unroll
         for (int t = 0; t < TCH; ++t) {
-          const f32x4 b = *(const f32x4*)(qs + 16 * (t0 + t) + 4 * g);
+          const f32x4 b = *(const f32x4*)(bl.qs + 16 * (t0 + t) + 4 * g);
           acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][0], b[0], acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][1], b[1], acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][2], b[2], acc, 0, 0, 0);
@@ -1593,13 +1560,12 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_small(
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int ej = 16 * gr + 4 * g + j;
-          if (ej < nb) sbuf[ej] = acc[j] != acc[j] ? 0ull : make_key(acc[j], brow[ej]);
+          if (ej < nb) bl.sbuf[ej] = acc[j] != acc[j] ? 0ull : make_key(acc[j], bl.brow[ej]);
         }
       }
     }
   }
   __syncthreads();
-  SM_TICK(4)
   // (score desc, row asc) order by rank: rank(e) = #keys ahead of key e (keys of distinct
   // rows are distinct; equal keys -- only NaN scores, key 0 -- are ordered by position), so
   // every band entry knows its output slot without a sort: ~nb compares per entry, over 4
@@ -1611,9 +1577,9 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_small(
     int rank = 0;
     uint64_t me = 0ull;
     if (e < nb) {
-      me = sbuf[e];
+      me = bl.sbuf[e];
       for (int j = part; j < nb; j += per) {
-        const uint64_t o = sbuf[j];
+        const uint64_t o = bl.sbuf[j];
         rank += (o > me || (o == me && j < e)) ? 1 : 0;
       }
     }
@@ -1631,15 +1597,340 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_small(
       out_s[(int64_t)qid * k + rank] = sc;
       out_i[(int64_t)qid * k + rank] = ix;
     }
-    // every slot < k is written: nb >= k (the band holds the k candidates >= A_k)
   }
-  SM_TICK(5)
-#if TT_EXP_SMALL_TIMING
-  if (tid == 0 && qid == 0)
-    printf("SMALLT nb=%d total=%d collect %d radix %d band %d score %d rank %d (x10ns)\n",
-           nb, total, (int)(tk[1] - tk[0]), (int)(tk[2] - tk[1]), (int)(tk[3] - tk[2]),
-           (int)(tk[4] - tk[3]), (int)(tk[5] - tk[4]));
-#endif
+}
+
+// Full level of a small batch: selection (mode 1 of k_select_reg) + exact re-rank (k_rerank)
+// in one launch.  A_k = k-th best a; A_k < aref -> the optimistic threshold failed (flag);
+// band = candidates with a >= A_k - eps2 (<= BAND_CAP, else flag); exact canonical f32
+// scores of the band rows by f32 MFMA; sort (score desc, row asc); top-k out.
+// The band's row gathers (~180 random 1.5 KB rows per query) are memory-latency bound on one
+// CU: 9-14 us of the one-buyer search.  Measured and not adopted: splitting a query over 8
+// blocks that meet through a global counter (25-30 us: the agent-scope release/acquire that
+// makes one block's scores visible to another XCD writes back / invalidates L2), and the full
+// level touching its candidates' f32 rows as it flushes them (no change).
+template <int EP>
+__global__ __launch_bounds__(SM_THREADS) void k_final_small(
+    const uint64_t* __restrict__ lists, const int* __restrict__ counts, int n_slabs, int k,
+    const float* __restrict__ eps2, const float* __restrict__ aref, int* __restrict__ flags,
+    int* qsel, int* qsel_n, const float* __restrict__ db, int64_t ld, int64_t n_rows,
+    const float* __restrict__ q, int64_t ldq, int64_t row_base, float* __restrict__ out_s,
+    int64_t* __restrict__ out_i) {
+  __shared__ SmallLds s;
+  __shared__ BandLds<EP> bl;
+  const int qid = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (flags[qid]) return;  // served by the exact fallback
+  const int total = small_collect(lists, counts, n_slabs, qid, s);
+  if (total < k) {  // overflow (-1) or too few candidates to certify: exact fallback
+    if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
+  uint32_t h[SM_PER];
+#pragma unroll
+  for (int j = 0; j < SM_PER; ++j) {
+    const int e = tid + j * SM_THREADS;
+    h[j] = e < total ? (uint32_t)(s.key[e] >> 32) : 0u;
+  }
+  const float A = key_float(small_radix_select(h, k, s));
+  if (!(A >= aref[qid])) {
+    if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
+  band_rerank<EP>(h, s, bl, A - eps2[qid], qid, k, flags, qsel, qsel_n, db, ld, n_rows, q, ldq,
+                  row_base, out_s, out_i);
+}
+
+// ------------------------------------------------------------ single-pass small batches
+// nq <= TM_NQ (the one-buyer /retrieve call, server.py:241-244 -> vector_db.py:160): ONE
+// streaming pass instead of sample level -> selection -> full level.  One block per CU
+// (G = #CUs, one round, no tail), each owning a contiguous slab; the bf16 image streams
+// HBM -> LDS through the ring of k_filter_ring (buffer_load ... lds, non-temporal, 3 tiles in
+// flight, one s_barrier per tile) and ONE wave scores it on bf16 MFMA (a 16-query block).  The
+// wave keeps, per query, the slab's running top-TM_M of a in an LDS buffer (append a >= tau,
+// the running TM_M-th best; compact by a wave bitonic sort when the buffer nears full: a
+// streaming top-m, ~TM_M ln(rows / TM_M) appends per query and slab) and writes it sorted.
+// k_final_topm then takes, per query, the union U of the G lists: A = k-th best a of U; a slab
+// dropped only rows with a <= tau_b (its TM_M-th best), so if every full list has
+// tau_b < A - 2 eps, U holds every row with a >= A - 2 eps (and A is the catalog's A_k):
+// the band, re-ranked exactly as in k_final_small.  Otherwise the query is flagged for the
+// exact fallback.  Bytes: the bf16 image once; no sample level, no per-level selections.
+constexpr int TM_NQ = 16;     // queries per search on this path (one MFMA query block)
+constexpr int TM_M = 16;      // rows kept per (query, slab)
+constexpr int TM_BUF = 256;   // per-query candidate buffer (wave bitonic sort of 4 keys / lane)
+constexpr int TM_SLOTS = 4, TM_PD = 3;  // ring slots, tiles in flight
+constexpr int TM_WAVES = 8;
+constexpr int TM_CAP = 4096;  // final: keys per query (G x TM_M, G <= 256)
+
+template <int EP>
+constexpr int topm_smem() {
+  return TM_SLOTS * RingCfg<EP>::TR * EP * 2 + TM_NQ * TM_BUF * 8;
+}
+
+template <int EP>
+__global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
+    const uint16_t* __restrict__ xb, int64_t ld, int64_t n, const float* __restrict__ q, int nq,
+    int64_t ldq, int rows_per_blk, uint64_t* __restrict__ lists, int* __restrict__ counts,
+    int* __restrict__ flags, int* __restrict__ qsel_n) {
+  constexpr int TR = RingCfg<EP>::TR, KS = EP / 32, CPR = EP / 8, RB = TR / 16;
+  constexpr int TILE_B = TR * EP * 2, PIECES = TILE_B / 1024, PPW = PIECES / TM_WAVES;
+  constexpr int FM = (CPR >= 16 ? 16 : CPR) - 1;
+  static_assert(PIECES % TM_WAVES == 0, "tile must split into whole 1-KiB pieces per wave");
+  __shared__ __attribute__((aligned(16))) char smem[topm_smem<EP>()];
+  char* ring = smem;
+  uint64_t* tbuf = (uint64_t*)(smem + TM_SLOTS * TILE_B);  // [TM_NQ][TM_BUF]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int G = gridDim.x, blk = blockIdx.x;
+  if (blk == 0 && tid < nq) {  // per-query fallback state (FilterWs: flags, qsel, qsel_n, done)
+    flags[tid] = 0;
+    qsel_n[1 + tid] = 0;
+    if (tid == 0) *qsel_n = 0;
+  }
+  const int64_t j0 = (int64_t)blk * rows_per_blk;
+  const int64_t j1 = (j0 + rows_per_blk < n) ? j0 + rows_per_blk : n;
+  const int n_tiles = j0 < j1 ? (int)((j1 - j0 + TR - 1) / TR) : 0;
+
+  // wave 0: the query fragments (bf16 B operands, 16 queries) and per-query top-m state
+  bf16x8 qf[KS];
+  const bool qv = col < nq;
+  float tau = qv ? -__builtin_huge_valf() : __builtin_huge_valf();
+  int cnt = 0;  // appended keys of query `col` (same in the 4 lanes of a column)
+  if (w == 0) {
+    const float* qp = q + (int64_t)(qv ? col : 0) * ldq + 8 * g;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const f32x4 v0 = *(const f32x4*)(qp + 32 * s);
+      const f32x4 v1 = *(const f32x4*)(qp + 32 * s + 4);
+      u32x4 u = {pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]), pack_bf16x2(v1[0], v1[1]),
+                 pack_bf16x2(v1[2], v1[3])};
+      qf[s] = __builtin_bit_cast(bf16x8, u);
+    }
+  }
+  wait_vm<0>();  // the query loads / init stores retire before the ring's counted waits
+
+  const int64_t tile_bytes = (int64_t)ld * 2 * TR;
+  const char* slab_base = (const char*)xb + j0 * ld * 2;
+  uint32_t voff[PPW];
+#pragma unroll
+  for (int pp = 0; pp < PPW; ++pp) {
+    const int P = (w + TM_WAVES * pp) * 64 + lane;
+    const int r = P / CPR;
+    voff[pp] = (uint32_t)(r * ld * 2) + 16u * (uint32_t)((P % CPR) ^ (r & FM));
+  }
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    char* slot = ring + (t % TM_SLOTS) * TILE_B;
+    const int64_t jt = j0 + (int64_t)t * TR;
+    const bool clamp = jt + TR > j1;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(slab_base + (int64_t)t * tile_bytes), 0, (int)tile_bytes, 0x00020000);
+#pragma unroll
+    for (int pp = 0; pp < PPW; ++pp) {
+      uint32_t off = voff[pp];
+      if (clamp) {  // rows past the slab end read a copy of its last row (masked below)
+        const int P = (w + TM_WAVES * pp) * 64 + lane;
+        const int r = P / CPR;
+        int64_t j = jt + r;
+        j = j < j1 ? j : j1 - 1;
+        off = (uint32_t)((j - jt) * ld * 2) + 16u * (uint32_t)((P % CPR) ^ (r & FM));
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(slot + (w + TM_WAVES * pp) * 1024), 16,
+          off, 0, 0, 2);
+    }
+  };
+  auto wait_tiles = [&](int younger) __attribute__((always_inline)) {
+    if (younger >= 2) wait_vm<2 * PPW>();
+    else if (younger == 1) wait_vm<PPW>();
+    else wait_vm<0>();
+  };
+  uint32_t lrd[RB][4];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb) {
+    const int r = 16 * rb + col, f = r & FM, h = f >> 2;
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+      lrd[rb][v] = lds_addr(ring) + 16 * (r * CPR + (g ^ (f & 3))) + 64 * (v ^ h);
+  }
+  // compaction of query c's buffer: sort (wave bitonic, 4 keys per lane), keep the top TM_M,
+  // tau = the TM_M-th key's score (rare: plain LDS accesses, the ring may drain once)
+  auto compact = [&](int c) __attribute__((always_inline)) {
+    uint64_t* b = tbuf + c * TM_BUF;
+    const int cc = __shfl(cnt, c, 64);
+    uint64_t key[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = lane * 4 + r;
+      key[r] = e < cc ? b[e] : 0ull;
+    }
+    bitonic_desc<4>(key, lane);
+    wave_sync();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = lane * 4 + r;
+      if (e < TM_M) b[e] = key[r];
+    }
+    const uint32_t hk = __shfl((uint32_t)(key[(TM_M - 1) % 4] >> 32), (TM_M - 1) / 4, 64);
+    const int nc = cc < TM_M ? cc : TM_M;
+    if (col == c) {
+      cnt = nc;
+      if (nc == TM_M) tau = key_float(hk);
+    }
+    wave_sync();
+  };
+
+  for (int t = 0; t < TM_PD && t < n_tiles; ++t) issue(t);
+  for (int t = 0; t < n_tiles; ++t) {
+    wait_tiles(n_tiles - 1 - t < TM_PD - 1 ? n_tiles - 1 - t : TM_PD - 1);
+    lds_barrier();  // tile t landed (every wave's pieces); every wave is done with tile t-1
+    if (t + TM_PD < n_tiles) issue(t + TM_PD);  // into the slot of tile t-1
+    if (w == 0) {
+      const uint32_t so = (uint32_t)((t % TM_SLOTS) * TILE_B);
+      f32x4 acc[RB];
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // k-steps in groups of 4 (KS < 4 for E = 64): reads issued together, one counted wait,
+      // the fragments tied through it (reg_tie: no MFMA may be scheduled above the wait)
+      static_for<(KS + 3) / 4>([&](auto u_) __attribute__((always_inline)) {
+        constexpr int U = decltype(u_)::value;
+        constexpr int NV = KS - 4 * U < 4 ? KS - 4 * U : 4;
+        u32x4 fr[RB][4];
+        static_for<NV>([&](auto v_) __attribute__((always_inline)) {
+          constexpr int V = decltype(v_)::value;
+#pragma unroll
+          for (int rb = 0; rb < RB; ++rb) fr[rb][V] = lds_read128<256 * U>(lrd[rb][V] + so);
+        });
+        lds_wait<0>();
+        static_for<NV>([&](auto v_) __attribute__((always_inline)) {
+          constexpr int V = decltype(v_)::value;
+#pragma unroll
+          for (int rb = 0; rb < RB; ++rb) reg_tie(fr[rb][V]);
+#pragma unroll
+          for (int rb = 0; rb < RB; ++rb)
+            acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8, fr[rb][V]), qf[4 * U + V], acc[rb], 0, 0, 0);
+        });
+      });
+      // lane: rows jt + 16 rb + 4 g + jj of query col.  Appends a >= tau (NaN never passes);
+      // positions within a column by ballot (no atomics): the 4 lanes of a column hold cnt.
+      const int64_t jt = j0 + (int64_t)t * TR;
+      const uint64_t colmask = 0x0001000100010001ull << col;
+      const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int64_t row = jt + 16 * rb + 4 * g + jj;
+          const float v = acc[rb][jj];
+          const bool pass = row < j1 && v >= tau;
+          const uint64_t bm = __ballot(pass);
+          if (bm != 0ull) {
+            const uint64_t mc = bm & colmask;
+            if (pass) {
+              const int pos = cnt + __popcll(mc & below);
+              lds_write64(lds_addr(tbuf + col * TM_BUF + pos), make_key(v, (uint32_t)row));
+            }
+            cnt += __popcll(mc);
+          }
+        }
+      const uint64_t need = __ballot(lane < 16 && cnt > TM_BUF - TR);
+      if (need != 0ull) {
+        lds_wait<0>();
+        uint64_t nd = need;
+        while (nd) {
+          const int c = __builtin_ctzll(nd);
+          nd &= nd - 1;
+          compact(c);
+        }
+      }
+    }
+  }
+  wait_vm<0>();
+  if (w == 0) {
+    lds_wait<0>();
+    for (int c = 0; c < nq; ++c) {
+      compact(c);
+      const int nc = __shfl(cnt, c, 64);
+      if (lane < nc) lists[((int64_t)c * G + blk) * TM_M + lane] = tbuf[c * TM_BUF + lane];
+      if (lane == 0) counts[(int64_t)c * G + blk] = nc;
+    }
+  }
+}
+
+// Final of the single-pass path, one block per query: union U of the G slab lists, A = k-th
+// best a of U; every full list's TM_M-th a (tau_b) must be < A - 2 eps (else the query takes
+// the exact fallback: a slab may have dropped a band row); band = U's keys with a >= A - 2 eps,
+// re-ranked exactly (band_rerank).  eps is computed here from the query (k_query_eps).
+template <int EP>
+__global__ __launch_bounds__(SM_THREADS) void k_final_topm(
+    const uint64_t* __restrict__ lists, const int* __restrict__ counts, int G, int k, float X,
+    float R, int* __restrict__ flags, int* qsel, int* qsel_n, const float* __restrict__ db,
+    int64_t ld, int64_t n_rows, const float* __restrict__ q, int64_t ldq, int64_t row_base,
+    float* __restrict__ out_s, int64_t* __restrict__ out_i) {
+  constexpr int PER = TM_CAP / SM_THREADS;
+  __shared__ SmallLdsT<TM_CAP> s;
+  __shared__ BandLds<EP> bl;
+  __shared__ float eps_s;
+  __shared__ uint32_t tau_max;
+  const int qid = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) tau_max = 0u;
+  if (w == 0) {  // 2 eps_q from the query's norms (same expression as k_query_eps)
+    const float* qr = q + (int64_t)qid * ldq;
+    float sq = 0.0f, st = 0.0f, sr = 0.0f;
+    for (int i = lane; i < EP; i += 64) {
+      const float v = qr[i], vt = __uint_as_float((uint32_t)f32_to_bf16_rne(v) << 16);
+      sq = fmaf(v, v, sq);
+      st = fmaf(vt, vt, st);
+      sr = fmaf(v - vt, v - vt, sr);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      sq += __shfl_xor(sq, o, 64);
+      st += __shfl_xor(st, o, 64);
+      sr += __shfl_xor(sr, o, 64);
+    }
+    if (lane == 0) eps_s = query_eps2<EP>(sq, st, sr, X, R);
+  }
+  // collect: slab b's list (G <= SM_THREADS) at a prefix offset; tau_max over full lists
+  const int c = tid < G ? counts[(int64_t)qid * G + tid] : 0;
+  int incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    incl += lane >= o ? y : 0;
+  }
+  if (lane == 63) s.wred[w] = incl;
+  __syncthreads();
+  int base = 0, total = 0;
+#pragma unroll
+  for (int i = 0; i < SM_WAVES; ++i) {
+    const int v = s.wred[i];
+    base += i < w ? v : 0;
+    total += v;
+  }
+  const uint64_t* l = lists + ((int64_t)qid * G + tid) * TM_M;
+  const int e0 = base + incl - c;
+  for (int i = 0; i < c; ++i) s.key[e0 + i] = l[i];
+  if (c == TM_M) atomicMax(&tau_max, (uint32_t)(l[TM_M - 1] >> 32));
+  __syncthreads();
+  if (total < k) {  // (a NaN query: no finite score anywhere) -> exact fallback
+    if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
+  uint32_t h[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int e = tid + j * SM_THREADS;
+    h[j] = e < total ? (uint32_t)(s.key[e] >> 32) : 0u;
+  }
+  const float A = key_float(small_radix_select(h, k, s));
+  const float thr = A - eps_s;
+  if (tau_max != 0u && key_float(tau_max) >= thr) {  // a slab may have dropped a band row
+    if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
+  band_rerank<EP>(h, s, bl, thr, qid, k, flags, qsel, qsel_n, db, ld, n_rows, q, ldq, row_base,
+                  out_s, out_i);
 }
 
 // sharded finish: pcount[q][i] = #rows over ALL shards with a >= t_i (all-reduced SUM).
@@ -2039,6 +2330,7 @@ struct Level {
 struct FilterPlan {
   int n_levels, max_slabs, J;
   bool small;  // block-per-query selection path (k_select_small / k_final_small)
+  bool topm;   // single-pass path (k_filter_topm + k_final_topm), nq <= TM_NQ
   Level lv[8];
 };
 
@@ -2048,6 +2340,10 @@ struct FilterPlan {
 // full catalog has ~16*J rows above a_J(stride-16 sample), comfortably >= k.
 static bool select_reg_disabled() {  // TT_SELECT_REG=0: LDS-staged k_select_wave (timing builds)
   static const bool off = env_switch("TT_SELECT_REG", 1) == 0;
+  return off;
+}
+static bool topm_disabled() {  // TT_FILTER_TOPM=0: the multi-level small path (timing builds)
+  static const bool off = env_switch("TT_FILTER_TOPM", 1) == 0;
   return off;
 }
 static bool tmax_first_disabled() {  // TT_FILTER_TMAX_FIRST=0: full sample ladder (timing builds)
@@ -2172,6 +2468,11 @@ static FilterPlan plan_filter_uncached(int64_t n, int nq, int k, int ep) {
   }
   p.small = nq <= SM_NQ && !select_reg_disabled();
   for (int i = 0; i < nl; ++i) p.small = p.small && p.lv[i].n_slabs <= SM_THREADS;
+  // single pass for the smallest batches: lists [nq][G][TM_M] and counts [nq][G] fit the
+  // level workspace once max_slabs >= G (FL_CAP >= TM_M)
+  p.topm = nq <= TM_NQ && !topm_disabled() && device_cus() * TM_M <= TM_CAP &&
+           device_cus() <= SM_THREADS;
+  if (p.topm && p.max_slabs < device_cus()) p.max_slabs = device_cus();
   return p;
 }
 
@@ -2332,10 +2633,23 @@ extern "C" int tt_filter_workspace_layout(int64_t n, int32_t d, int32_t nq, int3
 }
 
 namespace {
+// the full level of a shard as a one-level plan: stride 1, dense when the shard is small
+FilterPlan plan_full(int64_t n, int nq, int k, int ep) {
+  FilterPlan p = plan_filter(n, nq, k, ep);
+  const Level last = p.lv[p.n_levels - 1];
+  p.n_levels = 1;
+  p.lv[0] = last;
+  p.max_slabs = last.n_slabs;
+  p.topm = false;
+  return p;
+}
+
 // Shared prologue of the single-shard call and the sharded stages: validation, plan, carve.
+// full_only: the sharded full / finish stages' one-level plan (plan_full).
 int filter_setup(const float* db, const uint16_t* db_bf16, int64_t n, int32_t d, int64_t ld_db,
                  const float* q, int32_t nq, int64_t ld_q, int32_t k, void* workspace,
-                 int64_t workspace_bytes, int* ep_out, FilterPlan* p, FilterWs* w) {
+                 int64_t workspace_bytes, int* ep_out, FilterPlan* p, FilterWs* w,
+                 bool full_only = false) {
   TT_REQUIRE(n >= 1 && n <= 0x7fffffffLL, "need 1 <= n < 2^31");
   TT_REQUIRE(nq >= 1, "nq < 1");
   TT_REQUIRE(k >= 1 && k <= n, "need 1 <= k <= n");
@@ -2346,7 +2660,7 @@ int filter_setup(const float* db, const uint16_t* db_bf16, int64_t n, int32_t d,
              "ld must be >= tt_padded_dim(d), ld_db % 8 == 0 (zero padded)");
   TT_REQUIRE((db == nullptr || ((uintptr_t)db % 16) == 0) && ((uintptr_t)db_bf16 % 16) == 0 &&
                  ((uintptr_t)q % 16) == 0, "pointers must be 16-B aligned");
-  *p = plan_filter(n, nq, k, ep);
+  *p = full_only ? plan_full(n, nq, k, ep) : plan_filter(n, nq, k, ep);
   *w = carve(workspace, *p, n, d, nq, k);
   if (workspace == nullptr || workspace_bytes < w->total)
     return fail(TT_ERR_WORKSPACE, "bf16 filter: workspace too small");
@@ -2471,6 +2785,42 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
                         &p, &w);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
+  if (p.topm) {  // single pass: stream + per-slab top-m, final, exact fallback
+    TT_REQUIRE(db != nullptr && out_score && out_idx, "null pointer");
+    TT_REQUIRE(x_norm_max >= 0.0f && x_resid_max >= 0.0f,
+               "x_norm_max / x_resid_max must be >= 0 (tt_bf16_image_bounds)");
+    const int G = device_cus();
+    const int rows_per_blk = (int)((n + G - 1) / G);
+    if (ld_db * 2 * ring_tr(ep) > 0x7fffffffLL)
+      return fail(TT_ERR_UNSUPPORTED, "bf16 filter: row too long");
+    if (ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
+      return fail(TT_ERR_LAUNCH, "hipEventRecord(start)");
+    switch (ep) {
+#define TT_TM(E)                                                                              \
+  case E:                                                                                     \
+    hipLaunchKernelGGL(k_filter_topm<E>, dim3(G), dim3(64 * TM_WAVES), 0, st, db_bf16, ld_db, \
+                       n, q, nq, ld_q, rows_per_blk, w.lists, w.counts, w.flags, w.qsel_n);   \
+    break;
+      TT_TM(64) TT_TM(128) TT_TM(256) TT_TM(384) TT_TM(512) TT_TM(768)
+#undef TT_TM
+    }
+    if ((rc = check_launch("k_filter_topm"))) return rc;
+    if (ev_stop && hipEventRecord((hipEvent_t)ev_stop, st) != hipSuccess)
+      return fail(TT_ERR_LAUNCH, "hipEventRecord(stop)");
+    switch (ep) {
+#define TT_TF(E)                                                                              \
+  case E:                                                                                     \
+    hipLaunchKernelGGL(k_final_topm<E>, dim3(nq), dim3(SM_THREADS), 0, st, w.lists, w.counts, \
+                       G, k, x_norm_max, x_resid_max, w.flags, w.qsel, w.qsel_n, db, ld_db,   \
+                       n, q, ld_q, row_base, out_score, out_idx);                             \
+    break;
+      TT_TF(64) TT_TF(128) TT_TF(256) TT_TF(384) TT_TF(512) TT_TF(768)
+#undef TT_TF
+    }
+    if ((rc = check_launch("k_final_topm"))) return rc;
+    return scan_f32_select_fused(db, n, d, ld_db, row_base, q, nq, ld_q, k, w.qsel, w.qsel_n,
+                                 w.done, out_score, out_idx, w.scan_ws, w.scan_ws_bytes, st);
+  }
   QueryInit qinit;
   if ((rc = filter_init(w, q, nq, ld_q, ep, x_norm_max, x_resid_max, st, &p, &qinit))) return rc;
   // small batches: block-per-query selection (k_select_small) and a fused selection +
@@ -2514,16 +2864,6 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
 
 // ------------------------------------------------------------------ sharded (multi-GPU)
 namespace {
-// the full level of a shard as a one-level plan: stride 1, dense when the shard is small
-FilterPlan plan_full(int64_t n, int nq, int k, int ep) {
-  FilterPlan p = plan_filter(n, nq, k, ep);
-  const Level last = p.lv[p.n_levels - 1];
-  p.n_levels = 1;
-  p.lv[0] = last;
-  p.max_slabs = last.n_slabs;
-  return p;
-}
-
 __global__ void k_pack_stats(const float* __restrict__ theta, const float* __restrict__ smax,
                              int nq, float* __restrict__ stats) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2546,13 +2886,8 @@ __global__ void k_stats_theta(const float* __restrict__ stats, const float* __re
 int sharded_setup(const float* db, const uint16_t* db_bf16, int64_t n, int32_t d, int64_t ld_db,
                   const float* q, int32_t nq, int64_t ld_q, int32_t k, void* workspace,
                   int64_t workspace_bytes, int* ep, FilterPlan* p, FilterWs* w) {
-  int rc = filter_setup(db, db_bf16, n, d, ld_db, q, nq, ld_q, k, workspace, workspace_bytes, ep,
-                        p, w);
-  if (rc) return rc;
-  *p = plan_full(n, nq, k, *ep);
-  *w = carve(workspace, *p, n, d, nq, k);
-  if (workspace_bytes < w->total) return fail(TT_ERR_WORKSPACE, "sharded filter: workspace too small");
-  return TT_OK;
+  return filter_setup(db, db_bf16, n, d, ld_db, q, nq, ld_q, k, workspace, workspace_bytes, ep, p,
+                      w, true);
 }
 }  // namespace
 

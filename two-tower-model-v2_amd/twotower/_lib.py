@@ -90,6 +90,9 @@ SIGNATURES = {
                                                      _i32, _vp, _i64, _vp]),
     "tt_attn_agg_l2_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp,
                                           _vp, _i64, _vp]),
+    "tt_attn_agg_workspace_bytes": (ctypes.c_int, [_i64, _i32, _i32, ctypes.POINTER(_i64)]),
+    "tt_attn_agg_l2_f32_ws": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp,
+                                             _vp, _i64, _vp, _i64, _vp]),
     "tt_bert_workspace_bytes": (ctypes.c_int, [_i64, _i32, _i32, _i32, ctypes.POINTER(_i64)]),
     "tt_bert_encode": (ctypes.c_int, [ctypes.POINTER(BertModel), _vp, _vp, _i32, _i64, _i32, _i32,
                                       _vp, _i64, _vp, _i64, _vp]),

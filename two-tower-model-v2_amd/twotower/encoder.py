@@ -61,16 +61,19 @@ class EmbeddingEncoder:
 
     def __init__(self, model_path: Optional[str], config_path: Optional[str] = "configs/config.yaml",
                  device: Optional[str] = None, model: Optional[TwoTowerModel] = None,
-                 tokenizer=None, prec: str = "f32"):
+                 tokenizer=None, prec: str = "f32", text_encoder=None):
         """reference :18-43.  ``config_path=None`` uses the reference's shipped config;
         ``model`` skips the checkpoint (an already-built TwoTowerModel); ``prec`` is the text
-        encoder's GEMM precision ("f32" = parity mode, "bf16" = throughput mode)."""
+        encoder's GEMM precision ("f32" = parity mode, "bf16" = throughput mode);
+        ``text_encoder`` replaces the HIP MiniLM (any object with the SentenceTransformer
+        surface ItemTower uses: ``encode``, ``get_sentence_embedding_dimension``)."""
         self.config = (load_config(config_path) if config_path is not None
                        else copy.deepcopy(DEFAULT_CONFIG))
         if device is not None and not str(device).startswith("cuda"):
             raise _lib.HipUnavailable(f"device {device!r}: the MI355X path has no CPU compute")
         self.device = _lib.device()
-        self.model = model if model is not None else self._load_model(model_path, tokenizer, prec)
+        self.model = (model if model is not None
+                      else self._load_model(model_path, tokenizer, prec, text_encoder))
         self.model.eval()
         self.model.to(self.device)
         self.product_metadata = None
@@ -78,7 +81,8 @@ class EmbeddingEncoder:
         self._table_rows: Optional[Dict[str, int]] = None
 
     # reference :45-130
-    def _load_model(self, model_path: str, tokenizer=None, prec: str = "f32") -> TwoTowerModel:
+    def _load_model(self, model_path: str, tokenizer=None, prec: str = "f32",
+                    text_encoder=None) -> TwoTowerModel:
         checkpoint = torch.load(model_path, map_location="cpu", weights_only=True)
         model_config = (checkpoint["config"]["model"] if "config" in checkpoint
                         else self.config["model"])
@@ -90,6 +94,8 @@ class EmbeddingEncoder:
         it = model_config["item_tower"]
         if enc_sd:
             enc_cfg = encoder_cfg_from_state_dict(enc_sd)
+        elif text_encoder is not None:
+            enc_cfg = MINILM_L12
         else:
             warnings.warn("checkpoint holds no text-encoder weights: seeded stand-in MiniLM")
             enc_cfg = MINILM_L12
@@ -99,8 +105,8 @@ class EmbeddingEncoder:
             categorical_embedding_dim=it["categorical_embedding_dim"],
             projection_hidden_dim=it["projection_hidden_dim"],
             freeze_text_encoder=self.config["training"]["freeze_text_encoder"],
-            tokenizer=tokenizer, encoder_state_dict=enc_sd or None, encoder_cfg=enc_cfg,
-            prec=prec)
+            text_encoder=text_encoder, tokenizer=tokenizer, encoder_state_dict=enc_sd or None,
+            encoder_cfg=enc_cfg, prec=prec)
         if it["use_categorical_features"]:
             for kind in ("brand", "category"):
                 key = f"item_tower.{kind}_embedding.weight"

@@ -228,23 +228,64 @@ def sharded_workspace_bytes(n: int, d: int, nq: int, k: int) -> int:
     return v.value
 
 
+def sharded_full(db16: torch.Tensor, n: int, d: int, q: torch.Tensor, k: int, bounds,
+                 stats: torch.Tensor, workspace: torch.Tensor, pcount: torch.Tensor = None,
+                 events=(None, None)) -> torch.Tensor:
+    """Stage 2 of the row-sharded search (tt_sharded_filter_full): all ranks' queries q
+    [nq, ep] with their gathered stats [nq, 2] against this rank's shard -> probe counts
+    [nq, TT_SHARD_PROBES] int32, to be all-reduced (SUM) over the ranks before
+    sharded_finish with the SAME workspace.  bounds: the whole catalog's (MAX over shards)."""
+    _check_2d(db16, "db16", torch.bfloat16)
+    _check_2d(q, "q")
+    nq = q.shape[0]
+    if not (1 <= k <= min(n, FILTER_KMAX)) or n > db16.shape[0]:
+        raise ValueError(f"sharded_full: need 1 <= k ({k}) <= min(n, 128)")
+    if tuple(stats.shape) != (nq, 2) or stats.dtype != _f32 or not stats.is_contiguous():
+        raise ValueError("sharded_full: stats must be contiguous float32 [nq, 2]")
+    if workspace is None or workspace.numel() < sharded_workspace_bytes(n, d, nq, k):
+        raise ValueError("sharded_full: workspace smaller than sharded_workspace_bytes")
+    if pcount is None or pcount.numel() < nq * _lib.TT_SHARD_PROBES:
+        pcount = torch.empty((nq, _lib.TT_SHARD_PROBES), dtype=torch.int32, device=q.device)
+    pcount = pcount.view(-1)[: nq * _lib.TT_SHARD_PROBES]
+    x_norm_max, x_resid_max = (float(v) for v in bounds)
+    e0, e1 = events
+    check(lib().tt_sharded_filter_full(_ptr(db16), n, d, db16.stride(0), _ptr(q), nq, q.stride(0),
+                                       k, ctypes.c_float(x_norm_max), ctypes.c_float(x_resid_max),
+                                       _ptr(stats), _ptr(pcount), _ptr(workspace),
+                                       workspace.numel(), stream_ptr(),
+                                       e0.cuda_event if e0 is not None else None,
+                                       e1.cuda_event if e1 is not None else None),
+          "tt_sharded_filter_full")
+    return pcount
+
+
+def sharded_finish(db: torch.Tensor, db16: torch.Tensor, n: int, d: int, q: torch.Tensor, k: int,
+                   row_base: int, stats: torch.Tensor, pcount: torch.Tensor,
+                   workspace: torch.Tensor, out=None):
+    """Stage 3 (tt_sharded_filter_finish) with the all-reduced probe counts: this shard's part
+    of the global top-k [nq, k] (global row ids), merged across ranks with merge_topk."""
+    _check_2d(db, "db")
+    nq = q.shape[0]
+    if out is None:
+        out = (torch.empty((nq, k), dtype=_f32, device=q.device),
+               torch.empty((nq, k), dtype=torch.int64, device=q.device))
+    check(lib().tt_sharded_filter_finish(_ptr(db), _ptr(db16), n, d, db.stride(0), row_base,
+                                         _ptr(q), nq, q.stride(0), k, _ptr(stats), _ptr(pcount),
+                                         out[0].data_ptr(), out[1].data_ptr(), _ptr(workspace),
+                                         workspace.numel(), stream_ptr()),
+          "tt_sharded_filter_finish")
+    return out
+
+
 def sharded_search(db: torch.Tensor, db16: torch.Tensor, n: int, d: int, q: torch.Tensor, k: int,
                    bounds, row_base: int, stats: torch.Tensor, allreduce_sum,
                    workspace: torch.Tensor = None, out=None, pcount: torch.Tensor = None,
                    events=(None, None)):
-    """Stages 2-3 of the row-sharded search (tt_sharded_filter_full / _finish): all ranks'
-    queries q [nq, ep] and their gathered stats [nq, 2] against this rank's shard; between the
-    stages allreduce_sum(t) sums the probe counts [nq, 16] int32 over ranks in place.
-    Returns this shard's part of the global top-k; merge the ranks' parts with merge_topk.
-    bounds must hold for the whole catalog (MAX over the shards)."""
+    """Stages 2-3 of the row-sharded search (sharded_full, allreduce_sum(probe counts) in
+    place, sharded_finish).  Returns this shard's part of the global top-k; merge the ranks'
+    parts with merge_topk.  bounds must hold for the whole catalog (MAX over the shards)."""
     _check_2d(db, "db")
-    _check_2d(db16, "db16", torch.bfloat16)
-    _check_2d(q, "q")
     nq = q.shape[0]
-    if not (1 <= k <= min(n, FILTER_KMAX)) or n > db.shape[0]:
-        raise ValueError(f"sharded_search: need 1 <= k ({k}) <= min(n, 128)")
-    if tuple(stats.shape) != (nq, 2) or stats.dtype != _f32 or not stats.is_contiguous():
-        raise ValueError("sharded_search: stats must be contiguous float32 [nq, 2]")
     if out is None:
         out = (torch.empty((nq, k), dtype=_f32, device=q.device),
                torch.empty((nq, k), dtype=torch.int64, device=q.device))
@@ -253,25 +294,9 @@ def sharded_search(db: torch.Tensor, db16: torch.Tensor, n: int, d: int, q: torc
     need = sharded_workspace_bytes(n, d, nq, k)
     if workspace is None or workspace.numel() < need:
         workspace = torch.empty(need, dtype=torch.uint8, device=q.device)
-    if pcount is None or pcount.numel() < nq * _lib.TT_SHARD_PROBES:
-        pcount = torch.empty((nq, _lib.TT_SHARD_PROBES), dtype=torch.int32, device=q.device)
-    pcount = pcount.view(-1)[: nq * _lib.TT_SHARD_PROBES]
-    x_norm_max, x_resid_max = (float(v) for v in bounds)
-    L, st = lib(), stream_ptr()
-    e0, e1 = events
-    check(L.tt_sharded_filter_full(_ptr(db16), n, d, db16.stride(0), _ptr(q), nq, q.stride(0), k,
-                                   ctypes.c_float(x_norm_max), ctypes.c_float(x_resid_max),
-                                   _ptr(stats), _ptr(pcount), _ptr(workspace), workspace.numel(),
-                                   st, e0.cuda_event if e0 is not None else None,
-                                   e1.cuda_event if e1 is not None else None),
-          "tt_sharded_filter_full")
+    pcount = sharded_full(db16, n, d, q, k, bounds, stats, workspace, pcount, events)
     allreduce_sum(pcount)
-    check(L.tt_sharded_filter_finish(_ptr(db), _ptr(db16), n, d, db.stride(0), row_base, _ptr(q),
-                                     nq, q.stride(0), k, _ptr(stats), _ptr(pcount),
-                                     out[0].data_ptr(), out[1].data_ptr(), _ptr(workspace),
-                                     workspace.numel(), st),
-          "tt_sharded_filter_finish")
-    return out
+    return sharded_finish(db, db16, n, d, q, k, row_base, stats, pcount, workspace, out)
 
 
 def merge_topk(scores: torch.Tensor, idx: torch.Tensor, k: int):
@@ -321,7 +346,14 @@ def gather_weighted_avg_l2(table: torch.Tensor, d: int, hist: torch.Tensor, w: t
     return out
 
 
-def attn_agg_l2(items, w, W1, b1, W2, b2, out=None):
+ATTN_WS_MIN_ROWS = 256  # b*s from which the GEMM-based form (tt_attn_agg_l2_f32_ws) runs
+
+
+def attn_agg_l2(items, w, W1, b1, W2, b2, out=None, fused: bool = None):
+    """BuyerTower.attention_aggregation + F.normalize (buyer_tower.py:70-101).  Batches of
+    >= ATTN_WS_MIN_ROWS history rows take the two-stage form (first MLP layer as an f32 MFMA
+    GEMM, tt_attn_agg_l2_f32_ws); smaller ones (e.g. one /retrieve buyer) the one-kernel form.
+    fused=True/False forces one of them."""
     require_device(items, "item_embeddings")
     if items.dim() != 3 or w.shape != items.shape[:2]:
         raise ValueError("attn_agg_l2: items [B,S,E] and weights [B,S] required")
@@ -332,7 +364,18 @@ def attn_agg_l2(items, w, W1, b1, W2, b2, out=None):
     h = W1.shape[0]
     if out is None:
         out = torch.empty((b, d), dtype=_f32, device=items.device)
-    check(lib().tt_attn_agg_l2_f32(_ptr(items), b, s, d, _ptr(w), _ptr(W1), _ptr(b1), h, _ptr(W2),
-                                   _ptr(b2), _ptr(out), out.stride(0), stream_ptr()),
-          "tt_attn_agg_l2_f32")
+    if fused is None:
+        fused = b * s < ATTN_WS_MIN_ROWS or d % 32 != 0
+    if fused:
+        check(lib().tt_attn_agg_l2_f32(_ptr(items), b, s, d, _ptr(w), _ptr(W1), _ptr(b1), h,
+                                       _ptr(W2), _ptr(b2), _ptr(out), out.stride(0),
+                                       stream_ptr()), "tt_attn_agg_l2_f32")
+        return out
+    need = ctypes.c_int64(0)
+    check(lib().tt_attn_agg_workspace_bytes(b, s, h, ctypes.byref(need)),
+          "tt_attn_agg_workspace_bytes")
+    ws = torch.empty(need.value, dtype=torch.uint8, device=items.device)
+    check(lib().tt_attn_agg_l2_f32_ws(_ptr(items), b, s, d, _ptr(w), _ptr(W1), _ptr(b1), h,
+                                      _ptr(W2), _ptr(b2), _ptr(out), out.stride(0), _ptr(ws),
+                                      ws.numel(), stream_ptr()), "tt_attn_agg_l2_f32_ws")
     return out

@@ -114,6 +114,85 @@ class TopkExchange:
         return merge(s_recv, i_recv, self.k)
 
 
+class PipelinedStagedExchange:
+    """The staged sharded search (tt_sharded_filter_begin / _full / _finish) with the ranks'
+    queries in ``chunks`` chunks whose collectives overlap the next chunk's shard filter.
+
+    Per step (every rank, C chunks of its B queries):
+      1. per chunk: all-gather the queries (async on RCCL's stream), begin() on my chunk while
+         it is in flight, all-gather its stats;
+      2. chunk c: full(c) -> probe counts, all-reduce SUM launched async; chunk c-1's finish()
+         and its result all-to-all (async) are issued after chunk c's filter was enqueued, so
+         the all-reduce and all-to-all of one chunk run under the filter of the next;
+      3. per chunk: wait for its all-to-all, merge the W sorted lists.
+    ``begin(q_c) -> stats [b_c, 2]``; ``full(c, qall_c, sall_c) -> pcount [W*b_c, P] int32``;
+    ``finish(c, qall_c, sall_c, pcount) -> (scores, ids) [W*b_c, k]`` (chunk-private
+    workspaces: chunk c's band lists live until its finish).  Queries are independent, so the
+    result is bit-identical to one unchunked search (and to one GPU searching the catalog)."""
+
+    def __init__(self, b_local: int, width: int, k: int, chunks: int = 2, device=None,
+                 group=None):
+        self.group = group
+        self.rank, self.world = _world(group)
+        self.active = _dist_on()
+        self.b, self.k = int(b_local), int(k)
+        chunks = max(1, min(int(chunks), self.b))
+        cut = [self.b * c // chunks for c in range(chunks + 1)]
+        self.bounds = [(cut[c], cut[c + 1]) for c in range(chunks)]
+        self.ex = [TopkExchange(hi - lo, width, k, device=device, group=group, aux_width=2)
+                   for lo, hi in self.bounds]
+
+    def _a2a(self, ex: TopkExchange, s: Tensor, i: Tensor):
+        if not self.active:
+            return None
+        w1 = dist.all_to_all_single(ex.s_recv.view(self.world * ex.b, self.k), s.contiguous(),
+                                    group=self.group, async_op=True)
+        w2 = dist.all_to_all_single(ex.i_recv.view(self.world * ex.b, self.k), i.contiguous(),
+                                    group=self.group, async_op=True)
+        return (w1, w2)
+
+    def search(self, q: Tensor, begin, full, finish, merge):
+        if q.shape[0] != self.b:
+            raise ValueError(f"expected {self.b} local queries, got {q.shape[0]}")
+        C = len(self.ex)
+        qc = [q[lo:hi] for lo, hi in self.bounds]
+        gathered = [ex.gather_queries(x, async_op=True) for ex, x in zip(self.ex, qc)]
+        sall = [ex.gather_aux(begin(x)) for ex, x in zip(self.ex, qc)]
+        qall = []
+        for qa, work in gathered:
+            if work is not None:
+                work.wait()
+            qall.append(qa)
+        outs = [None] * C
+        pend = None
+        for c in range(C + 1):
+            nxt = None
+            if c < C:
+                pc = full(c, qall[c], sall[c])
+                w = (dist.all_reduce(pc, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                     if self.active else None)
+                nxt = (c, pc, w)
+            if pend is not None:
+                cp, pcp, wp = pend
+                if wp is not None:
+                    wp.wait()
+                s, i = finish(cp, qall[cp], sall[cp], pcp)
+                outs[cp] = (s, i, self._a2a(self.ex[cp], s, i))
+            pend = nxt
+        res_s, res_i = [], []
+        for c, (s, i, works) in enumerate(outs):
+            if works is None:  # no process group: the local result is the global one
+                res_s.append(s)
+                res_i.append(i)
+                continue
+            for wk in works:
+                wk.wait()
+            ms, mi = merge(self.ex[c].s_recv, self.ex[c].i_recv, self.k)
+            res_s.append(ms)
+            res_i.append(mi)
+        return torch.cat(res_s), torch.cat(res_i)
+
+
 def sharded_search(q: Tensor, k: int, local_search, merge, group=None):
     """Ragged variant: ranks may hold different numbers of queries.  Batches are padded to
     the group's maximum (one extra all-reduce) and the padding rows are dropped."""
@@ -148,6 +227,9 @@ class ShardedFlatIP:
         self.lo, self.hi = shard_range(self.n_global, self.rank, self.world)
         self.index = FlatIPIndex(d, device=device, row_base=self.lo)
         self._ex: Optional[TopkExchange] = None
+        self._pipe: Optional[PipelinedStagedExchange] = None
+        self._ws_chunks = []
+        self.chunks = 2  # staged search: query chunks whose collectives overlap the next filter
         self.sample16: Optional[Tensor] = None
         self.bounds = (0.0, 0.0)
         self._ws_begin: Optional[Tensor] = None
@@ -192,33 +274,41 @@ class ShardedFlatIP:
         from . import kernels
 
         staged = self._staged(k, method)
-        if (self._ex is None or self._ex.b != q.shape[0] or self._ex.k != k
-                or (self._ex.aux_all is None) == staged):
-            self._ex = TopkExchange(q.shape[0], q.shape[1], k, device=q.device, group=self.group,
-                                    aux_width=2 if staged else 0)
         if staged:
-            ix = self.index
-            need = kernels.filter_workspace_bytes(self.sample16.shape[0], ix.d, q.shape[0],
-                                                  min(k, self.sample16.shape[0]))
-            if self._ws_begin is None or self._ws_begin.numel() < need:
-                self._ws_begin = torch.empty(need, dtype=torch.uint8, device=ix.device)
-            return self._ex.search(
-                q, lambda qa, sa: self._local_staged(qa, sa, k), kernels.merge_topk,
-                aux=lambda: kernels.sharded_begin(self.sample16, ix.d, q, k,
-                                                  workspace=self._ws_begin))
+            return self._search_staged(q, k)
+        if self._ex is None or self._ex.b != q.shape[0] or self._ex.k != k:
+            self._ex = TopkExchange(q.shape[0], q.shape[1], k, device=q.device, group=self.group)
         return self._ex.search(q, lambda qa: self._local(qa, k, method), kernels.merge_topk)
 
-    def _local_staged(self, qa: Tensor, stats: Tensor, k: int):
+    def _search_staged(self, q: Tensor, k: int):
+        """The staged bf16 protocol through PipelinedStagedExchange (self.chunks chunks)."""
         from . import kernels
 
         ix = self.index
-        need = kernels.sharded_workspace_bytes(ix.ntotal, ix.d, qa.shape[0], k)
-        if ix._ws is None or ix._ws.numel() < need:
-            ix._ws = torch.empty(need, dtype=torch.uint8, device=ix.device)
-        g = self.group
-        return kernels.sharded_search(
-            ix.xb, ix.xb16, ix.ntotal, ix.d, qa, k, self.bounds, ix.row_base, stats,
-            lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=g), workspace=ix._ws)
+        p = self._pipe
+        if p is None or p.b != q.shape[0] or p.k != k or len(p.ex) != min(self.chunks, q.shape[0]):
+            p = self._pipe = PipelinedStagedExchange(q.shape[0], q.shape[1], k, self.chunks,
+                                                     device=q.device, group=self.group)
+        bmax = max(ex.b for ex in p.ex)
+        need = kernels.filter_workspace_bytes(self.sample16.shape[0], ix.d, bmax,
+                                              min(k, self.sample16.shape[0]))
+        if self._ws_begin is None or self._ws_begin.numel() < need:
+            self._ws_begin = torch.empty(need, dtype=torch.uint8, device=ix.device)
+        while len(self._ws_chunks) < len(p.ex):
+            self._ws_chunks.append(None)
+        for c, ex in enumerate(p.ex):  # chunk-private: chunk c's bands live until its finish
+            need = kernels.sharded_workspace_bytes(ix.ntotal, ix.d, p.world * ex.b, k)
+            if self._ws_chunks[c] is None or self._ws_chunks[c].numel() < need:
+                self._ws_chunks[c] = torch.empty(need, dtype=torch.uint8, device=ix.device)
+        ws = self._ws_chunks
+        return p.search(
+            q,
+            lambda x: kernels.sharded_begin(self.sample16, ix.d, x, k, workspace=self._ws_begin),
+            lambda c, qa, sa: kernels.sharded_full(ix.xb16, ix.ntotal, ix.d, qa, k, self.bounds,
+                                                   sa, ws[c]),
+            lambda c, qa, sa, pc: kernels.sharded_finish(ix.xb, ix.xb16, ix.ntotal, ix.d, qa, k,
+                                                         ix.row_base, sa, pc, ws[c]),
+            kernels.merge_topk)
 
     def _local(self, qa: Tensor, k: int, method: str):
         """Local top-k with global ids; a shard smaller than k pads with (-inf, -1)."""

@@ -153,11 +153,16 @@ class TwoTowerTrainStep:
         return self.ops.colsum(x)
 
     # ------------------------------------------------------------------ the step
+    def forward_loss(self, *args, **kw) -> torch.Tensor:
+        """The loss alone (the reference's validate: forward + criterion under no_grad,
+        trainer.py:245-319): no backward GEMMs, no gradients."""
+        return self.forward_backward(*args, grads=False, **kw)[0]
+
     def forward_backward(self, buyer_items, weights, pos_text, neg_text, pos_brand=None,
-                         pos_cat=None, neg_brand=None, neg_cat=None):
+                         pos_cat=None, neg_brand=None, neg_cat=None, grads: bool = True):
         """buyer_items [B,S,E], weights [B,S], pos_text [B,Ht], neg_text [B,N,Ht] (device f32);
         *_brand / *_cat: int32 id tensors (vocab ids, 0 = <UNK>) or None.
-        Returns (loss tensor, grads dict keyed like self.params)."""
+        Returns (loss tensor, grads dict keyed like self.params; {} when grads=False)."""
         P = self.params
         B, S, E = buyer_items.shape
         N = neg_text.shape[1]
@@ -207,6 +212,8 @@ class TwoTowerTrainStep:
                                              alpha.data_ptr(), onorm.data_ptr(), zb.data_ptr(),
                                              E, stream_ptr()), "attn_pool_fwd")
         # InfoNCE forward + backward
+        if not grads:
+            return infonce(zb, z[:B], z[B:].view(B, N, E), self.tau, self.prec, grads=False)[0], {}
         loss, (gb, gp, gn) = infonce(zb, z[:B], z[B:].view(B, N, E), self.tau, self.prec)
         g = {}
         # item head backward
@@ -252,6 +259,45 @@ class TwoTowerTrainStep:
         g["att0.b"] = self._colsum(dHb)
         g["att0.w"] = self._dW(dHb, X)
         return loss, g
+
+    # torch.optim.Adam state dict (the reference saves optimizer.state_dict(), trainer.py:330):
+    # 'state' indexed by the position of the parameter in model.parameters(), 'param_groups'
+    # with Adam's defaults.  Parameters the fused step does not train (the frozen text
+    # encoder) have no state entry, as under torch Adam when they never received a gradient.
+    def optimizer_state_dict(self, model) -> Dict:
+        pos = {p.data_ptr(): i for i, p in enumerate(model.parameters())}
+        state = {}
+        for k, p in self.params.items():
+            if self.t > 0:
+                state[pos[p.data_ptr()]] = {"step": torch.tensor(float(self.t)),
+                                            "exp_avg": self.m[k].detach().cpu().clone(),
+                                            "exp_avg_sq": self.v[k].detach().cpu().clone()}
+        group = {"lr": self.lr, "betas": tuple(self.betas), "eps": self.eps, "weight_decay": 0,
+                 "amsgrad": False, "maximize": False, "foreach": None, "capturable": False,
+                 "differentiable": False, "fused": None, "decoupled_weight_decay": False,
+                 "params": list(range(len(pos)))}
+        return {"state": state, "param_groups": [group]}
+
+    def load_optimizer_state_dict(self, model, sd: Dict) -> None:
+        """Restore Adam's step count and moments from optimizer_state_dict's format (or a
+        torch.optim.Adam state dict over model.parameters())."""
+        pos = {p.data_ptr(): i for i, p in enumerate(model.parameters())}
+        st = sd["state"]
+        steps = set()
+        for k, p in self.params.items():
+            e = st.get(pos[p.data_ptr()])
+            if e is None:
+                continue
+            self.m[k].copy_(torch.as_tensor(e["exp_avg"]).view_as(self.m[k]))
+            self.v[k].copy_(torch.as_tensor(e["exp_avg_sq"]).view_as(self.v[k]))
+            steps.add(int(float(e["step"])))
+        if len(steps) > 1:
+            raise ValueError(f"inconsistent Adam step counts in the state dict: {sorted(steps)}")
+        self.t = steps.pop() if steps else 0
+        g = sd.get("param_groups", [{}])[0]
+        self.lr = g.get("lr", self.lr)
+        self.betas = tuple(g.get("betas", self.betas))
+        self.eps = g.get("eps", self.eps)
 
     def adam(self, grads: Dict[str, torch.Tensor]) -> None:
         self.t += 1

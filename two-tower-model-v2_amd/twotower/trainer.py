@@ -16,8 +16,9 @@ weights) and loop structure:
       criterion -> backward -> optimizer.step (:211-231).  The sentence encoder is frozen
       (freeze_text_encoder, item_tower.py:40-42), so the positive / negative text embeddings
       are inputs of the step, like the history rows.
-  validate (:245-319)  the same forward in eval mode, loss only.
-  save_checkpoint / train (:321-378)  the reference's checkpoint dict and epoch loop.
+  validate (:245-319)  the same forward in eval mode, loss only (no backward work).
+  save_checkpoint / train (:321-378)  the reference's checkpoint dict (optimizer_state_dict
+      in torch.optim.Adam's format) and epoch loop; load_checkpoint resumes from it.
 
 The trainable parameters are those the reference's Adam updates with a frozen text encoder
 (projection, brand / category embeddings, attention MLP); the fused step keeps Adam's moments
@@ -149,7 +150,7 @@ class Trainer:
         with torch.no_grad():
             for batch in self.val_loader:
                 items, w, pos, neg, (pb, pc, nb, nc) = self._batch_inputs(batch)
-                loss, _ = self.step.forward_backward(items, w, pos, neg, pb, pc, nb, nc)
+                loss = self.step.forward_loss(items, w, pos, neg, pb, pc, nb, nc)
                 total += loss.item()
                 n += 1
         return total / n if n > 0 else 0.0
@@ -158,9 +159,7 @@ class Trainer:
     def save_checkpoint(self, is_best: bool = False):
         self.checkpoint_dir.mkdir(parents=True, exist_ok=True)
         checkpoint = {"epoch": self.current_epoch, "model_state_dict": self.model.state_dict(),
-                      "optimizer_state_dict": {"step": self.step.t,
-                                               "exp_avg": dict(self.step.m),
-                                               "exp_avg_sq": dict(self.step.v)},
+                      "optimizer_state_dict": self.step.optimizer_state_dict(self.model),
                       "best_val_loss": self.best_val_loss, "config": self.config}
         it = self.model.item_tower
         if getattr(it, "brand_vocab", None) is not None:
@@ -171,6 +170,19 @@ class Trainer:
         if is_best:
             torch.save(checkpoint, self.checkpoint_dir / "best_model.pt")
             print(f"Saved best model with validation loss: {self.best_val_loss:.4f}")
+
+    def load_checkpoint(self, path) -> Dict:
+        """Resume from a save_checkpoint file (the reference saves but never reloads): model
+        weights, Adam moments / step (torch.optim.Adam's state-dict format), epoch and best
+        validation loss.  Read with weights_only=True."""
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        self.model.load_state_dict(ck["model_state_dict"])
+        self.model.to(self.device)
+        if "optimizer_state_dict" in ck:
+            self.step.load_optimizer_state_dict(self.model, ck["optimizer_state_dict"])
+        self.current_epoch = int(ck.get("epoch", 0)) + 1
+        self.best_val_loss = float(ck.get("best_val_loss", float("inf")))
+        return ck
 
     # reference :354-378
     def train(self):

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import json
 import struct
+import threading
 from pathlib import Path
 from typing import List, Optional, Tuple
 
@@ -44,6 +45,10 @@ class FlatIPIndex:
         self.ntotal = 0
         self._ws = None
         self._prepared = {}  # (nq, k, ntotal, xb ptr) -> kernels.PreparedSearch (host search)
+        # the prepared searches and the workspace are shared state: host searches from
+        # several threads are serialised (faiss' search is re-entrant; the reference's /retrieve
+        # runs on one event-loop thread, server.py:212-244)
+        self._lock = threading.Lock()
 
     def _append(self, rows: torch.Tensor, rows16: torch.Tensor) -> None:
         if rows.shape[0]:  # build-time statistic over the new rows (max-combined)
@@ -104,19 +109,21 @@ class FlatIPIndex:
         q = torch.zeros((x.shape[0], self.ep), dtype=torch.float32, device=self.device)
         q[:, : self.d].copy_(torch.from_numpy(x))
         nq = x.shape[0]
-        if 1 <= nq <= 256 and 1 <= k <= min(self.ntotal, kernels.FILTER_KMAX):
-            # the /retrieve pattern (one buyer per call): arguments, outputs and workspace are
-            # bound once per (nq, k, index state); results are copied out before returning
-            key = (nq, k, self.ntotal, self.xb.data_ptr())
-            ps = self._prepared.get(key)
-            if ps is None:
-                self._prepared.clear()
-                ps = self._prepared[key] = kernels.PreparedSearch(
-                    self.xb, self.xb16, self.ntotal, self.d, nq, k, self.bounds, self.row_base)
-            s, i = ps(q)
-        else:
-            s, i = self.search_device(q, k)
-        return s.cpu().numpy(), i.cpu().numpy()
+        with self._lock:  # outputs / workspace are reused: copied out before the next call
+            if 1 <= nq <= 256 and 1 <= k <= min(self.ntotal, kernels.FILTER_KMAX):
+                # the /retrieve pattern (one buyer per call): arguments, outputs and workspace
+                # are bound once per (nq, k, index state); results copied out before returning
+                key = (nq, k, self.ntotal, self.xb.data_ptr())
+                ps = self._prepared.get(key)
+                if ps is None:
+                    self._prepared.clear()
+                    ps = self._prepared[key] = kernels.PreparedSearch(
+                        self.xb, self.xb16, self.ntotal, self.d, nq, k, self.bounds,
+                        self.row_base)
+                s, i = ps(q)
+            else:
+                s, i = self.search_device(q, k)
+            return s.cpu().numpy(), i.cpu().numpy()
 
     def reconstruct(self, i: int) -> np.ndarray:
         return self.xb[i, : self.d].cpu().numpy()
