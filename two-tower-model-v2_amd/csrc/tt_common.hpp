@@ -69,6 +69,43 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Wave64 scans / reductions on DPP lane moves (VALU, a few cycles per step).  __shfl is a
+// ds_bpermute through the LDS pipe: ~100+ cycles of latency per dependent step, which is what
+// a one-block latency-bound kernel (the small-batch final) spends its time on.
+// Inclusive prefix sum over lanes 0..63: row_shr 1/2/4/8 within rows of 16, then row_bcast 15
+// (row r's total into row r + 1, rows 1 and 3) and row_bcast 31 (rows 0-1's total into rows
+// 2 and 3).  Lanes whose source is outside the row read 0 (old = 0, bound_ctrl off).
+__device__ __forceinline__ int wave_incl_sum(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+  return x;
+}
+__device__ __forceinline__ int wave_sum(int x) {
+  return __builtin_amdgcn_readlane(wave_incl_sum(x), 63);
+}
+// max over the wave of unsigned values (0 = identity), same DPP pattern
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  int x = (int)v;
+  auto mx = [](int a, int b) { return (int)((uint32_t)a > (uint32_t)b ? (uint32_t)a : (uint32_t)b); };
+  x = mx(x, __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false));
+  x = mx(x, __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false));
+  x = mx(x, __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false));
+  x = mx(x, __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false));
+  x = mx(x, __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false));
+  x = mx(x, __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false));
+  return (uint32_t)__builtin_amdgcn_readlane(x, 63);
+}
+// sum over aligned lane quads (lanes 4i .. 4i + 3), result in every lane of the quad
+__device__ __forceinline__ int quad_sum(int x) {
+  x += __builtin_amdgcn_mov_dpp(x, 0xb1, 0xf, 0xf, false);  // quad_perm [1, 0, 3, 2]
+  x += __builtin_amdgcn_mov_dpp(x, 0x4e, 0xf, 0xf, false);  // quad_perm [2, 3, 0, 1]
+  return x;
+}
+
 // Monotone map float -> uint32 (larger float -> larger key).  -0 is folded to +0 so that
 // equal scores compare equal; NaN maps to 0 (below every finite value and -inf).
 __device__ __forceinline__ uint32_t float_key(float f) {

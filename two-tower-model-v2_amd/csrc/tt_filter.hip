@@ -222,6 +222,15 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #ifndef TT_EXP_NOIDLE
 #define TT_EXP_NOIDLE 0  // small batches: padding-only waves run the MFMA stream too (A/B)
 #endif
+#ifndef TT_EXP_FINAL_STOP
+#define TT_EXP_FINAL_STOP 0  // timing only: k_final_topm returns after the collect (1) / select (2)
+#endif
+#ifndef TT_EXP_FINAL_TIMING
+#define TT_EXP_FINAL_TIMING 0  // printf k_final_topm phase wall-clock ticks (100 MHz), block 0
+#endif
+#ifndef TT_EXP_TM_SLOTS
+#define TT_EXP_TM_SLOTS 4  // single-pass small batches: ring slots (A/B)
+#endif
 #ifndef TT_EXP_NOWRITE
 #define TT_EXP_NOWRITE 0  // selection control flow without the LDS pool writes
 #endif
@@ -251,7 +260,9 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #define TT_EXP_MAXONLY 0  // per-block max + ballot only (no per-slot scan)
 #endif
 TT_CHECK_EXP(TT_EXP_NOSEL || TT_EXP_NOWRITE || TT_EXP_MAXONLY ||
-                 TT_EXP_SEL_STOP || TT_EXP_SEL_TIMING, "TT_EXP_* (results wrong / printf)");
+                 TT_EXP_SEL_STOP || TT_EXP_SEL_TIMING || TT_EXP_FINAL_STOP ||
+                 TT_EXP_FINAL_TIMING || TT_EXP_TM_SLOTS != 4,
+             "TT_EXP_* (results wrong / printf / untested schedule)");
 TT_CHECK_EXP(TT_RING_HALF || TT_RING_QB4 || TT_EXP_NOIDLE || TT_EXP_PRIO ||
                  TT_RING_NT != 1 || TT_RR_STAGED != 1 || TT_RR_PF != 1 || TT_RR_NT,
              "a non-default ring/re-rank schedule (untested by the GPU suite)");
@@ -345,6 +356,27 @@ __device__ __forceinline__ float query_eps2(float sq, float st, float sr, float 
   const float e = R * nq_ + (X + R) * nr + 2.0f * g23 * (X + R) * nt + g24 * X * nq_;
   const float r = 2.0f * e * 1.001f;
   return r == r ? r : __builtin_huge_valf();  // a NaN query: widest band (never returned)
+}
+
+// 2 eps_q of one query, computed by one wave (every lane gets the value): the norms of q, of
+// its bf16 image and of the residual (the ONE expression every path uses: k_query_eps, the
+// single-pass small batches)
+template <int EP>
+__device__ __forceinline__ float query_eps2_wave(const float* __restrict__ qr, float X, float R,
+                                                 int lane) {
+  float sq = 0.0f, st = 0.0f, sr = 0.0f;
+  for (int i = lane; i < EP; i += 64) {
+    const float v = qr[i], vt = __uint_as_float((uint32_t)f32_to_bf16_rne(v) << 16);
+    sq = fmaf(v, v, sq);
+    st = fmaf(vt, vt, st);
+    sr = fmaf(v - vt, v - vt, sr);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    sq += __shfl_xor(sq, o, 64);
+    st += __shfl_xor(st, o, 64);
+    sr += __shfl_xor(sr, o, 64);
+  }
+  return query_eps2<EP>(sq, st, sr, X, R);
 }
 
 // Per-query filter state, initialised by the first level of a search (k_query_eps's work,
@@ -641,10 +673,12 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   for (int t = 0; t < RG_PD && t < n_tiles; ++t) issue(t);
   wait_tiles(n_tiles - 1 < RG_PD - 1 ? n_tiles - 1 : RG_PD - 1);
   lds_barrier();  // tile 0 landed; counters initialised
-  // Small batches (LVL 2, e.g. one buyer): a wave without a single real query only moves its
-  // share of the ring DMA, in lockstep with the block's one barrier per tile -- its MFMAs on
-  // padding queries had made the one-buyer full level issue-bound (8 waves x 48 MFMAs / tile).
-  if (LVL != 1 && qbase >= nq && !TT_EXP_NOIDLE) {
+  // A wave without a single real query only moves its share of the ring DMA, in lockstep with
+  // the block's one barrier per tile: small batches (LVL 2, e.g. one buyer: its MFMAs on
+  // padding queries had made the one-buyer full level issue-bound, 8 waves x 48 MFMAs / tile)
+  // and the last, partial query tile of a large batch (LVL 1: 10k queries = 26 tiles of 384 +
+  // 16, so 7 of that tile's 8 waves; its lone computing wave then has its SIMD to itself).
+  if (qbase >= nq && !TT_EXP_NOIDLE) {
     for (int t = 0; t < n_tiles; ++t) {
       if (t + 1 < n_tiles) wait_tiles(n_tiles - 2 - t < RG_PD - 2 ? n_tiles - 2 - t : RG_PD - 2);
       asm volatile("s_barrier" ::: "memory");
@@ -1344,9 +1378,8 @@ template <int CAP>
 struct SmallLdsT {
   uint64_t key[CAP];   // the query's candidate keys (orderable score << 32 | ~row)
   int wred[SM_WAVES];
-  int hist[256];
-  int pick[2];
-  int nb;
+  uint32_t wmax[SM_WAVES];
+  int hist[3][256];    // radix select: pass p counts into hist[p % 3] (one barrier per pass)
 };
 using SmallLds = SmallLdsT<SM_CAP>;
 
@@ -1380,53 +1413,90 @@ __device__ int small_collect(const uint64_t* __restrict__ lists, const int* __re
   return total;
 }
 
+// One radix pass of a block-wide select: key j (act) is counted in bin (0..255, larger bin =
+// larger key); every wave then scans the histogram itself (no pick broadcast): lane l owns
+// bins 255 - 4 l (c0) down to 252 - 4 l (c3), so the inclusive prefix over lanes (DPP) counts
+// the keys in bins >= 252 - 4 l, and F = the first lane reaching r.  Returns the bin holding
+// the r-th largest key; r becomes its rank inside that bin.  `next` (the following pass's
+// histogram) is zeroed before the barrier.  Atomics land at distinct-ish bins (the callers'
+// bin maps spread the keys), so no wave aggregation.
+template <int PER, class BinF>
+__device__ __forceinline__ int radix_pass(int* hist, int* next, BinF binof, int& r) {
+  const int tid = threadIdx.x, lane = tid & 63;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    uint32_t bin;
+    if (binof(j, bin)) atomicAdd(&hist[bin], 1);
+  }
+  if (next && tid < 256) next[tid] = 0;
+  __syncthreads();
+  const int c0 = hist[255 - 4 * lane], c1 = hist[254 - 4 * lane], c2 = hist[253 - 4 * lane],
+            c3 = hist[252 - 4 * lane];
+  const int mine = c0 + c1 + c2 + c3;
+  const int incl = wave_incl_sum(mine);
+  const int F = __builtin_ctzll(__ballot(incl >= r));
+  int above = __builtin_amdgcn_readlane(incl - mine, F);
+  const int f0 = __builtin_amdgcn_readlane(c0, F), f1 = __builtin_amdgcn_readlane(c1, F),
+            f2 = __builtin_amdgcn_readlane(c2, F);
+  int bin = 252 - 4 * F;
+  if (above + f0 >= r) {
+    bin = 255 - 4 * F;
+  } else if (above + f0 + f1 >= r) {
+    bin = 254 - 4 * F;
+    above += f0;
+  } else if (above + f0 + f1 + f2 >= r) {
+    bin = 253 - 4 * F;
+    above += f0 + f1;
+  } else {
+    above += f0 + f1 + f2;
+  }
+  r -= above;
+  return bin;
+}
+
 // R-th largest high word (orderable score) of the keys h (0 = no key), block-wide radix
-// select, 4 passes of 8 bits.  Caller guarantees at least R nonzero keys.
+// select.  Caller guarantees at least R nonzero keys.  ONE barrier per pass; pass p counts
+// into hist[p % 3], zeroed during pass p - 1 (after barrier p - 2, which every reader of that
+// buffer's previous use, pass p - 3, had passed).
+// hmax != 0 (the max nonzero h): a first pass over 16-bit prefixes in a window of 255 below
+// hmax's -- the candidates' scores cluster (a fixed top byte puts nearly every key in one or
+// two bins, and serialised same-address atomics), while 255 prefix steps (2^-7 relative each)
+// spread them -- then the low two bytes: 3 passes.  The r-th key outside the window (bin 0 =
+// "255 or more below") -> the plain 4 passes of 8 bits.  (Four passes with wave-aggregated
+// atomics and four barriers each: 5.4 us of the one-buyer final.)
 template <int PER, int CAP>
-__device__ uint32_t small_radix_select(const uint32_t (&h)[PER], int R, SmallLdsT<CAP>& s) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  uint32_t prefix = 0, pmask = 0;
-  int r = R;
-#pragma unroll 1
-  for (int shift = 24; shift >= 0; shift -= 8) {
-    if (tid < 256) s.hist[tid] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < PER; ++j)
-      if (h[j] != 0u && (h[j] & pmask) == prefix) atomicAdd(&s.hist[(h[j] >> shift) & 255u], 1);
-    __syncthreads();
-    if (w == 0) {
-      const int b0 = s.hist[4 * lane], b1 = s.hist[4 * lane + 1], b2 = s.hist[4 * lane + 2],
-                b3 = s.hist[4 * lane + 3];
-      const int mine = b0 + b1 + b2 + b3;
-      int suf = mine;  // keys in bins >= 4 lane
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_down(suf, o, 64);
-        suf += lane + o < 64 ? y : 0;
-      }
-      const uint64_t m = __ballot(suf >= r);
-      const int L = 63 - __builtin_clzll(m);
-      if (lane == L) {
-        int above = suf - mine, b = 0;
-        const int bins[4] = {b0, b1, b2, b3};
-#pragma unroll
-        for (int bb = 3; bb >= 0; --bb) {
-          if (above + bins[bb] >= r) {
-            b = bb;
-            break;
-          }
-          above += bins[bb];
-        }
-        s.pick[0] = 4 * L + b;
-        s.pick[1] = r - above;
-      }
+__device__ uint32_t small_radix_select(const uint32_t (&h)[PER], int R, SmallLdsT<CAP>& s,
+                                       uint32_t hmax = 0u) {
+  const int tid = threadIdx.x;
+  if (tid < 256) s.hist[0][tid] = 0;
+  __syncthreads();
+  int r = R, pc = 0, shift = 24;
+  uint32_t prefix = 0u, pmask = 0u;
+  if (hmax != 0u) {
+    const uint32_t top = hmax >> 16;
+    const int b = radix_pass<PER>(s.hist[0], s.hist[1], [&](int j, uint32_t& bin) {
+      const uint32_t d = top - (h[j] >> 16);
+      bin = 255u - (d < 255u ? d : 255u);
+      return h[j] != 0u;
+    }, r);
+    pc = 1;
+    if (b > 0) {
+      prefix = (top - (uint32_t)(255 - b)) << 16;
+      pmask = 0xffff0000u;
+      shift = 8;
+    } else {
+      r = R;
     }
-    __syncthreads();
-    prefix |= (uint32_t)s.pick[0] << shift;
+  }
+#pragma unroll 1
+  for (; shift >= 0; shift -= 8, ++pc) {
+    const int b = radix_pass<PER>(s.hist[pc % 3], shift > 0 ? s.hist[(pc + 1) % 3] : nullptr,
+                                  [&](int j, uint32_t& bin) {
+                                    bin = (h[j] >> shift) & 255u;
+                                    return h[j] != 0u && (h[j] & pmask) == prefix;
+                                  }, r);
+    prefix |= (uint32_t)b << shift;
     pmask |= 0xffu << shift;
-    r = s.pick[1];
-    __syncthreads();
   }
   return prefix;
 }
@@ -1476,29 +1546,47 @@ struct BandLds {
   int wcnt[SM_WAVES];
 };
 
-// Band = keys (h[j] = high word of s.key[tid + j * SM_THREADS], 0 = none) with a >= thr, in a
-// deterministic order; exact canonical f32 scores of the band rows by f32 MFMA; output slot
-// = rank (score desc, row asc); top k written.  A band past BAND_CAP, or a decoded row >=
-// n_rows (a corrupted key: never read), flags the query for the exact fallback instead.
-// Every slot < k is written when the band holds >= k rows (callers guarantee it).
-template <int EP, int PER, int CAP>
-__device__ void band_rerank(const uint32_t (&h)[PER], SmallLdsT<CAP>& s, BandLds<EP>& bl,
-                            float thr, int qid, int k, int* flags, int* qsel, int* qsel_n,
-                            const float* __restrict__ db, int64_t ld, int64_t n_rows,
-                            const float* __restrict__ q, int64_t ldq, int64_t row_base,
-                            float* __restrict__ out_s, int64_t* __restrict__ out_i) {
+// Exact canonical f32 scores of 16 rows: lane (r, g) = (lane & 15, lane >> 4) names row `row`
+// (one per r), loads its dims 16t + 4g .. +3 for every t (all loads in flight), and the chain
+// runs on v_mfma_f32_16x16x4_f32 with the query (LDS, f32) in every column: the canonical order
+// (t, i, g), bit-identical to the f32 scan.  D[row 4g + j][col 0] comes back in lane 16 g,
+// element j.  (Per-row VALU fma chains after an LDS transpose: 0.182 vs 0.177 ms per one-buyer
+// search, 0.292 vs 0.276 ms at 256 queries.)
+template <int EP>
+__device__ __forceinline__ f32x4 exact16(const float* __restrict__ db, int64_t ld, uint32_t row,
+                                         const float* qs, int lane) {
+  const int g = lane >> 4;
+  constexpr int NT = EP / 16, TCH = NT <= 24 ? NT : 16;  // t-steps per load batch
+  static_assert(NT % TCH == 0, "load batches must tile the row");
+  const float* xr = db + (int64_t)row * ld + 4 * g;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int t0 = 0; t0 < NT; t0 += TCH) {
+    f32x4 a[TCH];
+#pragma unroll
+    for (int t = 0; t < TCH; ++t) a[t] = *(const f32x4*)(xr + 16 * (t0 + t));
+#pragma unroll
+    for (int t = 0; t < TCH; ++t) {
+      const f32x4 b = *(const f32x4*)(qs + 16 * (t0 + t) + 4 * g);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][0], b[0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][1], b[1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][2], b[2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][3], b[3], acc, 0, 0, 0);
+    }
+  }
+  return acc;
+}
+
+// Band positions: keys (h[j] = high word of key slot tid + j * SM_THREADS, 0 = none) with
+// a >= thr get consecutive positions in a deterministic order (block-wide prefix count).
+// Returns the band size nb; *pos0 = this thread's first position.
+template <int EP, int PER>
+__device__ int band_positions(const uint32_t (&h)[PER], float thr, BandLds<EP>& bl, int* pos0) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int i = tid; i < EP; i += SM_THREADS) bl.qs[i] = q[(int64_t)qid * ldq + i];
-  // band positions by a block-wide prefix count (deterministic order)
   int mine = 0;
 #pragma unroll
   for (int j = 0; j < PER; ++j) mine += (h[j] != 0u && key_float(h[j]) >= thr) ? 1 : 0;
-  int incl = mine;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(incl, o, 64);
-    incl += lane >= o ? y : 0;
-  }
+  const int incl = wave_incl_sum(mine);
   if (lane == 63) bl.wcnt[w] = incl;
   __syncthreads();
   int base = 0, nb = 0;
@@ -1507,56 +1595,84 @@ __device__ void band_rerank(const uint32_t (&h)[PER], SmallLdsT<CAP>& s, BandLds
     base += i < w ? bl.wcnt[i] : 0;
     nb += bl.wcnt[i];
   }
+  *pos0 = base + incl - mine;
+  return nb;
+}
+
+// Output of a band whose exact keys bl.sbuf[0, nb) are known: slot = rank (score desc, row
+// asc): rank(e) = #keys ahead of key e (keys of distinct rows are distinct; equal keys -- only
+// NaN scores, key 0 -- are ordered by position), so every band entry knows its output slot
+// without a sort: ~nb compares per entry, over 4 threads per entry when nb <= 256 (the bitonic
+// sorts this replaces spent 36 dependent stages: 4.6 us in one wave, 7.5 us block-wide).
+template <int EP>
+__device__ void band_rank_out(BandLds<EP>& bl, int nb, int qid, int k, int64_t row_base,
+                              float* __restrict__ out_s, int64_t* __restrict__ out_i) {
+  const int tid = threadIdx.x;
+  const int per = nb <= 256 ? 4 : 1;
+  const int e = tid / per, part = tid % per;
+  int rank = 0;
+  uint64_t me = 0ull;
+  if (e < nb) {
+    me = bl.sbuf[e];
+#pragma unroll 8
+    for (int j = part; j < nb; j += per) {
+      const uint64_t o = bl.sbuf[j];
+      rank += (o > me || (o == me && j < e)) ? 1 : 0;
+    }
+  }
+  if (per == 4) rank = quad_sum(rank);  // the 4 partial counts sit in one lane quad
+  if (e < nb && part == 0 && rank < k) {
+    float sc = -__builtin_huge_valf();
+    int64_t ix = -1;
+    if (me != 0ull) {  // NaN score: key 0 ranks last, reported as (-inf, -1)
+      sc = key_score(me);
+      ix = row_base + (int64_t)key_row(me);
+    }
+    out_s[(int64_t)qid * k + rank] = sc;
+    out_i[(int64_t)qid * k + rank] = ix;
+  }
+}
+
+// Band = keys with a >= thr (band_positions); exact canonical f32 scores of the band rows
+// (exact16, 16 rows per wave pass); output by rank (band_rank_out).  A band past BAND_CAP, or
+// a decoded row >= n_rows (a corrupted key: never read), flags the query for the exact
+// fallback instead.  Every slot < k is written when the band holds >= k rows (callers
+// guarantee it).
+template <int EP, int PER, int CAP>
+__device__ void band_rerank(const uint32_t (&h)[PER], SmallLdsT<CAP>& s, BandLds<EP>& bl,
+                            float thr, int qid, int k, int* flags, int* qsel, int* qsel_n,
+                            const float* __restrict__ db, int64_t ld, int64_t n_rows,
+                            const float* __restrict__ q, int64_t ldq, int64_t row_base,
+                            float* __restrict__ out_s, int64_t* __restrict__ out_i) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = tid; i < EP; i += SM_THREADS) bl.qs[i] = q[(int64_t)qid * ldq + i];
+  int pos;
+  const int nb = band_positions<EP>(h, thr, bl, &pos);
   if (nb > BAND_CAP) {
     if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
     return;
   }
   bool bad_row = false;  // a decoded row >= n_rows is never read: exact fallback instead
-  {
-    int pos = base + incl - mine;
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int e = tid + j * SM_THREADS;
-      if (h[j] != 0u && key_float(h[j]) >= thr) {
-        const uint32_t r = key_row(s.key[e]);
-        bad_row |= (int64_t)r >= n_rows;
-        bl.brow[pos++] = (int64_t)r < n_rows ? r : 0u;
-      }
+  for (int j = 0; j < PER; ++j) {
+    const int e = tid + j * SM_THREADS;
+    if (h[j] != 0u && key_float(h[j]) >= thr) {
+      const uint32_t r = key_row(s.key[e]);
+      bad_row |= (int64_t)r >= n_rows;
+      bl.brow[pos++] = (int64_t)r < n_rows ? r : 0u;
     }
   }
   if (__syncthreads_or(bad_row)) {
     if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
     return;
   }
-  // exact scores: wave w takes band rows [16 gr, 16 gr + 16), gr = w, w + SM_WAVES, ...  Lane
-  // (r, g) loads row r's dims 16t + 4g .. +3 for every t (all loads in flight) and
-  // the chain runs on v_mfma_f32_16x16x4_f32 with the query in every column: the canonical
-  // order (t, i, g), bit-identical to the f32 scan.  (Per-row VALU fma chains after an LDS
-  // transpose: 0.182 vs 0.177 ms per one-buyer search, 0.292 vs 0.276 ms at 256 queries.)
+  // exact scores: wave w takes band rows [16 gr, 16 gr + 16), gr = w, w + SM_WAVES, ...
   {
     const int r16 = lane & 15, g = lane >> 4;
-    constexpr int NT = EP / 16, TCH = NT <= 24 ? NT : 16;  // t-steps per load batch
-    static_assert(NT % TCH == 0, "load batches must tile the row");
     for (int gr = w; 16 * gr < nb; gr += SM_WAVES) {
       const int e = 16 * gr + r16;
-      const uint32_t row = bl.brow[e < nb ? e : nb - 1];
-      const float* xr = db + (int64_t)row * ld + 4 * g;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-      for (int t0 = 0; t0 < NT; t0 += TCH) {
-        f32x4 a[TCH];
-#pragma unroll
-        for (int t = 0; t < TCH; ++t) a[t] = *(const f32x4*)(xr + 16 * (t0 + t));
-#pragma unroll
-        for (int t = 0; t < TCH; ++t) {
-          const f32x4 b = *(const f32x4*)(bl.qs + 16 * (t0 + t) + 4 * g);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][0], b[0], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][1], b[1], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][2], b[2], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t][3], b[3], acc, 0, 0, 0);
-        }
-      }
-      if (r16 == 0) {  // D[row 4g + j][col 0] sits in lane 16 g
+      const f32x4 acc = exact16<EP>(db, ld, bl.brow[e < nb ? e : nb - 1], bl.qs, lane);
+      if (r16 == 0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int ej = 16 * gr + 4 * g + j;
@@ -1566,38 +1682,7 @@ __device__ void band_rerank(const uint32_t (&h)[PER], SmallLdsT<CAP>& s, BandLds
     }
   }
   __syncthreads();
-  // (score desc, row asc) order by rank: rank(e) = #keys ahead of key e (keys of distinct
-  // rows are distinct; equal keys -- only NaN scores, key 0 -- are ordered by position), so
-  // every band entry knows its output slot without a sort: ~nb compares per entry, over 4
-  // threads per entry when nb <= 256 (the bitonic sorts this replaces spent 36 dependent
-  // stages: 4.6 us in one wave, 7.5 us block-wide).
-  {
-    const int per = nb <= 256 ? 4 : 1;
-    const int e = tid / per, part = tid % per;
-    int rank = 0;
-    uint64_t me = 0ull;
-    if (e < nb) {
-      me = bl.sbuf[e];
-      for (int j = part; j < nb; j += per) {
-        const uint64_t o = bl.sbuf[j];
-        rank += (o > me || (o == me && j < e)) ? 1 : 0;
-      }
-    }
-    if (per == 4) {  // the 4 partial counts sit in adjacent lanes of one wave
-      rank += __shfl_xor(rank, 1, 64);
-      rank += __shfl_xor(rank, 2, 64);
-    }
-    if (e < nb && part == 0 && rank < k) {
-      float sc = -__builtin_huge_valf();
-      int64_t ix = -1;
-      if (me != 0ull) {  // NaN score: key 0 ranks last, reported as (-inf, -1)
-        sc = key_score(me);
-        ix = row_base + (int64_t)key_row(me);
-      }
-      out_s[(int64_t)qid * k + rank] = sc;
-      out_i[(int64_t)qid * k + rank] = ix;
-    }
-  }
+  band_rank_out<EP>(bl, nb, qid, k, row_base, out_s, out_i);
 }
 
 // Full level of a small batch: selection (mode 1 of k_select_reg) + exact re-rank (k_rerank)
@@ -1658,7 +1743,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_small(
 constexpr int TM_NQ = 16;     // queries per search on this path (one MFMA query block)
 constexpr int TM_M = 16;      // rows kept per (query, slab)
 constexpr int TM_BUF = 256;   // per-query candidate buffer (wave bitonic sort of 4 keys / lane)
-constexpr int TM_SLOTS = 4, TM_PD = 3;  // ring slots, tiles in flight
+constexpr int TM_SLOTS = TT_EXP_TM_SLOTS, TM_PD = TM_SLOTS - 1;  // ring slots, tiles in flight
 constexpr int TM_WAVES = 8;
 constexpr int TM_CAP = 4096;  // final: keys per query (G x TM_M, G <= 256)
 
@@ -1670,13 +1755,15 @@ constexpr int topm_smem() {
 template <int EP>
 __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
     const uint16_t* __restrict__ xb, int64_t ld, int64_t n, const float* __restrict__ q, int nq,
-    int64_t ldq, int rows_per_blk, uint64_t* __restrict__ lists, int* __restrict__ counts,
-    int* __restrict__ flags, int* __restrict__ qsel_n) {
+    int64_t ldq, int rows_per_blk, const float* __restrict__ db, float X, float R,
+    float* __restrict__ eps2, uint64_t* __restrict__ lists, uint64_t* __restrict__ xkeys,
+    int* __restrict__ counts, int* __restrict__ flags, int* __restrict__ qsel_n) {
   constexpr int TR = RingCfg<EP>::TR, KS = EP / 32, CPR = EP / 8, RB = TR / 16;
   constexpr int TILE_B = TR * EP * 2, PIECES = TILE_B / 1024, PPW = PIECES / TM_WAVES;
   constexpr int FM = (CPR >= 16 ? 16 : CPR) - 1;
   static_assert(PIECES % TM_WAVES == 0, "tile must split into whole 1-KiB pieces per wave");
   __shared__ __attribute__((aligned(16))) char smem[topm_smem<EP>()];
+  __shared__ int ncs[TM_NQ];
   char* ring = smem;
   uint64_t* tbuf = (uint64_t*)(smem + TM_SLOTS * TILE_B);  // [TM_NQ][TM_BUF]
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1741,7 +1828,9 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
     }
   };
   auto wait_tiles = [&](int younger) __attribute__((always_inline)) {
-    if (younger >= 2) wait_vm<2 * PPW>();
+    static_assert(TM_PD <= 4, "wait_tiles covers up to 3 younger tiles");
+    if (younger >= 3) wait_vm<3 * PPW>();
+    else if (younger == 2) wait_vm<2 * PPW>();
     else if (younger == 1) wait_vm<PPW>();
     else wait_vm<0>();
   };
@@ -1780,72 +1869,79 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
     wave_sync();
   };
 
+  // appends of tile t's scores (lane: rows jt + 16 rb + 4 g + jj of query col): a >= tau
+  // (NaN never passes); positions within a column by ballot (no atomics): the 4 lanes of a
+  // column hold cnt.  Then the compactions the buffers need.
+  auto appends = [&](const f32x4 (&acc)[RB], int t) __attribute__((always_inline)) {
+    const int64_t jt = j0 + (int64_t)t * TR;
+    const uint64_t colmask = 0x0001000100010001ull << col;
+    const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int64_t row = jt + 16 * rb + 4 * g + jj;
+        const float v = acc[rb][jj];
+        const bool pass = row < j1 && v >= tau;
+        const uint64_t bm = __ballot(pass);
+        if (bm != 0ull) {
+          const uint64_t mc = bm & colmask;
+          if (pass) {
+            const int pos = cnt + __popcll(mc & below);
+            lds_write64(lds_addr(tbuf + col * TM_BUF + pos), make_key(v, (uint32_t)row));
+          }
+          cnt += __popcll(mc);
+        }
+      }
+    const uint64_t need = __ballot(lane < 16 && cnt > TM_BUF - TR);
+    if (need != 0ull) {
+      lds_wait<0>();
+      uint64_t nd = need;
+      while (nd) {
+        const int c = __builtin_ctzll(nd);
+        nd &= nd - 1;
+        compact(c);
+      }
+    }
+  };
+
+  // wave 0, per tile t: issue ALL of tile t's fragment reads (RB x KS x 16 B per lane), run
+  // tile t-1's appends while they are in flight, one wait, then tile t's MFMA chain (its
+  // scores are appended in the next iteration: the LDS latency hides behind the append VALU)
+  f32x4 acc[RB];
   for (int t = 0; t < TM_PD && t < n_tiles; ++t) issue(t);
+  if (w == 1 && blk < nq) {  // 2 eps of query blk for the final, while the first tiles land
+    const float e = query_eps2_wave<EP>(q + (int64_t)blk * ldq, X, R, lane);
+    if (lane == 0) eps2[blk] = e;
+  }
   for (int t = 0; t < n_tiles; ++t) {
     wait_tiles(n_tiles - 1 - t < TM_PD - 1 ? n_tiles - 1 - t : TM_PD - 1);
     lds_barrier();  // tile t landed (every wave's pieces); every wave is done with tile t-1
     if (t + TM_PD < n_tiles) issue(t + TM_PD);  // into the slot of tile t-1
     if (w == 0) {
       const uint32_t so = (uint32_t)((t % TM_SLOTS) * TILE_B);
-      f32x4 acc[RB];
+      u32x4 fr[RB][KS];
+      static_for<KS>([&](auto s_) __attribute__((always_inline)) {
+        constexpr int S = decltype(s_)::value;
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) fr[rb][S] = lds_read128<256 * (S / 4)>(lrd[rb][S % 4] + so);
+      });
+      if (t > 0) appends(acc, t - 1);
+      lds_wait<0>();
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
-      // k-steps in groups of 4 (KS < 4 for E = 64): reads issued together, one counted wait,
-      // the fragments tied through it (reg_tie: no MFMA may be scheduled above the wait)
-      static_for<(KS + 3) / 4>([&](auto u_) __attribute__((always_inline)) {
-        constexpr int U = decltype(u_)::value;
-        constexpr int NV = KS - 4 * U < 4 ? KS - 4 * U : 4;
-        u32x4 fr[RB][4];
-        static_for<NV>([&](auto v_) __attribute__((always_inline)) {
-          constexpr int V = decltype(v_)::value;
+      static_for<KS>([&](auto s_) __attribute__((always_inline)) {
+        constexpr int S = decltype(s_)::value;
 #pragma unroll
-          for (int rb = 0; rb < RB; ++rb) fr[rb][V] = lds_read128<256 * U>(lrd[rb][V] + so);
-        });
-        lds_wait<0>();
-        static_for<NV>([&](auto v_) __attribute__((always_inline)) {
-          constexpr int V = decltype(v_)::value;
+        for (int rb = 0; rb < RB; ++rb) reg_tie(fr[rb][S]);
 #pragma unroll
-          for (int rb = 0; rb < RB; ++rb) reg_tie(fr[rb][V]);
-#pragma unroll
-          for (int rb = 0; rb < RB; ++rb)
-            acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                __builtin_bit_cast(bf16x8, fr[rb][V]), qf[4 * U + V], acc[rb], 0, 0, 0);
-        });
+        for (int rb = 0; rb < RB; ++rb)
+          acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fr[rb][S]),
+                                                            qf[S], acc[rb], 0, 0, 0);
       });
-      // lane: rows jt + 16 rb + 4 g + jj of query col.  Appends a >= tau (NaN never passes);
-      // positions within a column by ballot (no atomics): the 4 lanes of a column hold cnt.
-      const int64_t jt = j0 + (int64_t)t * TR;
-      const uint64_t colmask = 0x0001000100010001ull << col;
-      const uint64_t below = (1ull << lane) - 1ull;
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int64_t row = jt + 16 * rb + 4 * g + jj;
-          const float v = acc[rb][jj];
-          const bool pass = row < j1 && v >= tau;
-          const uint64_t bm = __ballot(pass);
-          if (bm != 0ull) {
-            const uint64_t mc = bm & colmask;
-            if (pass) {
-              const int pos = cnt + __popcll(mc & below);
-              lds_write64(lds_addr(tbuf + col * TM_BUF + pos), make_key(v, (uint32_t)row));
-            }
-            cnt += __popcll(mc);
-          }
-        }
-      const uint64_t need = __ballot(lane < 16 && cnt > TM_BUF - TR);
-      if (need != 0ull) {
-        lds_wait<0>();
-        uint64_t nd = need;
-        while (nd) {
-          const int c = __builtin_ctzll(nd);
-          nd &= nd - 1;
-          compact(c);
-        }
-      }
     }
   }
+  if (w == 0 && n_tiles > 0) appends(acc, n_tiles - 1);
   wait_vm<0>();
   if (w == 0) {
     lds_wait<0>();
@@ -1853,7 +1949,28 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
       compact(c);
       const int nc = __shfl(cnt, c, 64);
       if (lane < nc) lists[((int64_t)c * G + blk) * TM_M + lane] = tbuf[c * TM_BUF + lane];
-      if (lane == 0) counts[(int64_t)c * G + blk] = nc;
+      if (lane == 0) {
+        counts[(int64_t)c * G + blk] = nc;
+        ncs[c] = nc;
+      }
+    }
+  }
+  // exact keys of the kept rows (every block in parallel, one 16-row exact16 pass per query
+  // over the 8 waves, the f32 query read from L2 alongside the rows): the final then ranks its
+  // band without gathering f32 rows on one CU
+  __syncthreads();  // the sorted lists (tbuf) and ncs visible to every wave
+  for (int c = w; c < nq; c += TM_WAVES) {
+    const int nc = ncs[c], r16 = lane & 15, g4 = 4 * (lane >> 4);
+    if (nc == 0) continue;
+    const uint64_t* tb = tbuf + c * TM_BUF;
+    const f32x4 acc =
+        exact16<EP>(db, ld, key_row(tb[r16 < nc ? r16 : 0]), q + (int64_t)c * ldq, lane);
+    if (r16 == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (g4 + j < nc)
+          xkeys[((int64_t)c * G + blk) * TM_M + g4 + j] =
+              acc[j] != acc[j] ? 0ull : make_key(acc[j], key_row(tb[g4 + j]));
     }
   }
 }
@@ -1861,76 +1978,123 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
 // Final of the single-pass path, one block per query: union U of the G slab lists, A = k-th
 // best a of U; every full list's TM_M-th a (tau_b) must be < A - 2 eps (else the query takes
 // the exact fallback: a slab may have dropped a band row); band = U's keys with a >= A - 2 eps,
-// re-ranked exactly (band_rerank).  eps is computed here from the query (k_query_eps).
+// output in the order of their exact keys, which the streaming blocks computed for every kept
+// row (no f32 row gathers here).  2 eps comes from the streaming kernel (query_eps2_wave).
+// One block, latency-bound: ~15 us with shuffle (ds_bpermute) scans and four barriers per
+// radix pass, DPP scans and one barrier per pass now.
 template <int EP>
 __global__ __launch_bounds__(SM_THREADS) void k_final_topm(
-    const uint64_t* __restrict__ lists, const int* __restrict__ counts, int G, int k, float X,
-    float R, int* __restrict__ flags, int* qsel, int* qsel_n, const float* __restrict__ db,
-    int64_t ld, int64_t n_rows, const float* __restrict__ q, int64_t ldq, int64_t row_base,
+    const uint64_t* __restrict__ lists, const uint64_t* __restrict__ xkeys,
+    const int* __restrict__ counts, int G, int k, const float* __restrict__ eps2,
+    int* __restrict__ flags, int* qsel, int* qsel_n, int64_t n_rows, int64_t row_base,
     float* __restrict__ out_s, int64_t* __restrict__ out_i) {
   constexpr int PER = TM_CAP / SM_THREADS;
-  __shared__ SmallLdsT<TM_CAP> s;
+  __shared__ SmallLdsT<1> s;
   __shared__ BandLds<EP> bl;
   __shared__ float eps_s;
-  __shared__ uint32_t tau_max;
   const int qid = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (tid == 0) tau_max = 0u;
-  if (w == 0) {  // 2 eps_q from the query's norms (same expression as k_query_eps)
-    const float* qr = q + (int64_t)qid * ldq;
-    float sq = 0.0f, st = 0.0f, sr = 0.0f;
-    for (int i = lane; i < EP; i += 64) {
-      const float v = qr[i], vt = __uint_as_float((uint32_t)f32_to_bf16_rne(v) << 16);
-      sq = fmaf(v, v, sq);
-      st = fmaf(vt, vt, st);
-      sr = fmaf(v - vt, v - vt, sr);
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      sq += __shfl_xor(sq, o, 64);
-      st += __shfl_xor(st, o, 64);
-      sr += __shfl_xor(sr, o, 64);
-    }
-    if (lane == 0) eps_s = query_eps2<EP>(sq, st, sr, X, R);
-  }
-  // collect: slab b's list (G <= SM_THREADS) at a prefix offset; tau_max over full lists
-  const int c = tid < G ? counts[(int64_t)qid * G + tid] : 0;
-  int incl = c;
+#if TT_EXP_FINAL_TIMING
+  uint64_t ts[8];
+  int nts = 0;
+#define TT_FTS() (ts[nts++] = wall_clock64())
+#else
+#define TT_FTS() ((void)0)
+#endif
+  TT_FTS();
+  // collect: slot e = slab e / TM_M, entry e % TM_M (0 = no key: the radix select and the band
+  // skip it); the count, approximate key and exact key of every slot loaded together, before
+  // the query's eps loads (one round trip; a per-slab copy loop had serialised ~16 dependent
+  // L2 round trips); slots past a list's count hold stale keys and are masked
+  uint32_t h[PER];
+  uint64_t xk[PER];
+  {
+    int cj[PER];
+    uint64_t kk[PER];
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(incl, o, 64);
-    incl += lane >= o ? y : 0;
+    for (int j = 0; j < PER; ++j) {
+      const int e = tid + j * SM_THREADS, b = e / TM_M;
+      const int64_t o = ((int64_t)qid * G + (b < G ? b : 0)) * TM_M + e % TM_M;
+      cj[j] = b < G ? counts[(int64_t)qid * G + b] : 0;
+      kk[j] = lists[o];
+      xk[j] = xkeys[o];
+    }
+    int mine = 0;
+    uint32_t tmax = 0u;  // max over full lists of their TM_M-th key (tau_b)
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = (tid + j * SM_THREADS) % TM_M;
+      const bool ok = i < cj[j];
+      h[j] = ok ? (uint32_t)(kk[j] >> 32) : 0u;
+      if (!ok) xk[j] = 0ull;
+      if (ok && i == TM_M - 1) tmax = tmax > h[j] ? tmax : h[j];
+      mine += h[j] != 0u;
+    }
+    mine = wave_sum(mine);
+    tmax = wave_max_u32(tmax);
+    uint32_t hm = 0u;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) hm = hm > h[j] ? hm : h[j];
+    hm = wave_max_u32(hm);
+    if (tid == 0) eps_s = eps2[qid];
+    if (lane == 0) {
+      s.wred[w] = mine;
+      s.wmax[w] = hm;
+      bl.wcnt[w] = (int)tmax;  // (orderable keys as int: only compared after the reinterpret)
+    }
   }
-  if (lane == 63) s.wred[w] = incl;
   __syncthreads();
-  int base = 0, total = 0;
+  uint32_t tau_max = 0u, hmax = 0u;
 #pragma unroll
   for (int i = 0; i < SM_WAVES; ++i) {
-    const int v = s.wred[i];
-    base += i < w ? v : 0;
-    total += v;
+    const uint32_t y = (uint32_t)bl.wcnt[i], z = s.wmax[i];
+    tau_max = tau_max > y ? tau_max : y;
+    hmax = hmax > z ? hmax : z;
   }
-  const uint64_t* l = lists + ((int64_t)qid * G + tid) * TM_M;
-  const int e0 = base + incl - c;
-  for (int i = 0; i < c; ++i) s.key[e0 + i] = l[i];
-  if (c == TM_M) atomicMax(&tau_max, (uint32_t)(l[TM_M - 1] >> 32));
-  __syncthreads();
-  if (total < k) {  // (a NaN query: no finite score anywhere) -> exact fallback
+  TT_FTS();
+  int n_keys = 0;
+#pragma unroll
+  for (int i = 0; i < SM_WAVES; ++i) n_keys += s.wred[i];
+  if (n_keys < k) {  // (a NaN query: no finite score anywhere) -> exact fallback
     if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
     return;
   }
-  uint32_t h[PER];
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int e = tid + j * SM_THREADS;
-    h[j] = e < total ? (uint32_t)(s.key[e] >> 32) : 0u;
-  }
-  const float A = key_float(small_radix_select(h, k, s));
+  if (TT_EXP_FINAL_STOP == 1) return;
+  const float A = key_float(small_radix_select(h, k, s, hmax));
+  TT_FTS();
+  if (TT_EXP_FINAL_STOP == 2) return;
   const float thr = A - eps_s;
   if (tau_max != 0u && key_float(tau_max) >= thr) {  // a slab may have dropped a band row
     if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
     return;
   }
-  band_rerank<EP>(h, s, bl, thr, qid, k, flags, qsel, qsel_n, db, ld, n_rows, q, ldq, row_base,
-                  out_s, out_i);
+  // band = keys with a >= A - 2 eps; their exact keys came from the streaming kernel
+  int pos;
+  const int nb = band_positions<EP>(h, thr, bl, &pos);
+  if (nb > BAND_CAP) {
+    if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
+  bool bad_row = false;  // a decoded row >= n_rows (corrupted key): exact fallback instead
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if (h[j] != 0u && key_float(h[j]) >= thr) {
+      bad_row |= xk[j] != 0ull && (int64_t)key_row(xk[j]) >= n_rows;
+      bl.sbuf[pos++] = xk[j];
+    }
+  if (__syncthreads_or(bad_row)) {
+    if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
+  TT_FTS();
+  band_rank_out<EP>(bl, nb, qid, k, row_base, out_s, out_i);
+  TT_FTS();
+#if TT_EXP_FINAL_TIMING
+  if (qid == 0 && tid == 0)
+    printf("final_topm ticks: collect %d select %d band %d rank %d (nb %d)\n",
+           (int)(ts[1] - ts[0]), (int)(ts[2] - ts[1]), (int)(ts[3] - ts[2]), (int)(ts[4] - ts[3]),
+           nb);
+#endif
+#undef TT_FTS
 }
 
 // sharded finish: pcount[q][i] = #rows over ALL shards with a >= t_i (all-reduced SUM).
@@ -2298,20 +2462,8 @@ __global__ __launch_bounds__(256) void k_query_eps(const float* __restrict__ q, 
     qsel_n[1 + qi] = 0;  // done[qi] (FilterWs layout)
     if (qi == 0) *qsel_n = 0;
   }
-  const float* qr = q + (int64_t)qi * ldq;
-  float sq = 0.0f, st = 0.0f, sr = 0.0f;
-  for (int i = lane; i < EP; i += 64) {
-    const float v = qr[i], vt = __uint_as_float((uint32_t)f32_to_bf16_rne(v) << 16);
-    sq = fmaf(v, v, sq);
-    st = fmaf(vt, vt, st);
-    sr = fmaf(v - vt, v - vt, sr);
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    sq += __shfl_xor(sq, o, 64);
-    st += __shfl_xor(st, o, 64);
-    sr += __shfl_xor(sr, o, 64);
-  }
-  if (lane == 0) eps2[qi] = query_eps2<EP>(sq, st, sr, X, R);
+  const float e = query_eps2_wave<EP>(q + (int64_t)qi * ldq, X, R, lane);
+  if (lane == 0) eps2[qi] = e;
 }
 
 __global__ void k_sub_arr(float* x, const float* y, int n) {
@@ -2791,6 +2943,11 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
                "x_norm_max / x_resid_max must be >= 0 (tt_bf16_image_bounds)");
     const int G = device_cus();
     const int rows_per_blk = (int)((n + G - 1) / G);
+    // lists [nq][G][TM_M] approximate keys, then the exact keys, same shape (plan_filter sized
+    // the list region for max_slabs >= G lists of FL_CAP >= 2 TM_M per query)
+    static_assert(2 * TM_M <= FL_CAP, "topm lists + exact keys must fit the list region");
+    TT_REQUIRE(p.max_slabs >= G, "topm plan: list region smaller than one list per CU");
+    uint64_t* xkeys = w.lists + (int64_t)nq * G * TM_M;
     if (ld_db * 2 * ring_tr(ep) > 0x7fffffffLL)
       return fail(TT_ERR_UNSUPPORTED, "bf16 filter: row too long");
     if (ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
@@ -2799,7 +2956,8 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
 #define TT_TM(E)                                                                              \
   case E:                                                                                     \
     hipLaunchKernelGGL(k_filter_topm<E>, dim3(G), dim3(64 * TM_WAVES), 0, st, db_bf16, ld_db, \
-                       n, q, nq, ld_q, rows_per_blk, w.lists, w.counts, w.flags, w.qsel_n);   \
+                       n, q, nq, ld_q, rows_per_blk, db, x_norm_max, x_resid_max, w.eps2,     \
+                       w.lists, xkeys, w.counts, w.flags, w.qsel_n);                          \
     break;
       TT_TM(64) TT_TM(128) TT_TM(256) TT_TM(384) TT_TM(512) TT_TM(768)
 #undef TT_TM
@@ -2810,9 +2968,9 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
     switch (ep) {
 #define TT_TF(E)                                                                              \
   case E:                                                                                     \
-    hipLaunchKernelGGL(k_final_topm<E>, dim3(nq), dim3(SM_THREADS), 0, st, w.lists, w.counts, \
-                       G, k, x_norm_max, x_resid_max, w.flags, w.qsel, w.qsel_n, db, ld_db,   \
-                       n, q, ld_q, row_base, out_score, out_idx);                             \
+    hipLaunchKernelGGL(k_final_topm<E>, dim3(nq), dim3(SM_THREADS), 0, st, w.lists, xkeys,    \
+                       w.counts, G, k, w.eps2, w.flags, w.qsel, w.qsel_n, n, row_base,        \
+                       out_score, out_idx);                                                   \
     break;
       TT_TF(64) TT_TF(128) TT_TF(256) TT_TF(384) TT_TF(512) TT_TF(768)
 #undef TT_TF

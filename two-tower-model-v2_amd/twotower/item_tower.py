@@ -142,7 +142,7 @@ class BertEncoder:
         m.layer = ctypes.cast(layers, ctypes.POINTER(_lib.BertLayer))
         self._layers = layers
         self._model = m
-        self._ws = None
+        self._ws = {}  # per HIP stream: encodes may run concurrently on several streams
 
     @property
     def hidden(self) -> int:
@@ -169,13 +169,15 @@ class BertEncoder:
         if max_len > self.cfg["max_positions"]:
             raise ValueError(f"sequence longer than max_position_embeddings ({max_len})")
         need = self.workspace_bytes(T)
-        if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty(need, dtype=torch.uint8, device=ids.device)
+        st = stream_ptr()
+        ws = self._ws.get(st)
+        if ws is None or ws.numel() < need:
+            ws = self._ws[st] = torch.empty(need, dtype=torch.uint8, device=ids.device)
         check(lib().tt_bert_encode(ctypes.byref(self._model), ids.data_ptr(),
                                    cu_seqlens.data_ptr(), n, T, int(max_len),
                                    _lib.TT_PREC_BF16 if self.prec == "bf16" else _lib.TT_PREC_F32,
-                                   out.data_ptr(), out.stride(0), self._ws.data_ptr(),
-                                   self._ws.numel(), stream_ptr()), "tt_bert_encode")
+                                   out.data_ptr(), out.stride(0), ws.data_ptr(), ws.numel(), st),
+              "tt_bert_encode")
         return out
 
     def encode_ids(self, seqs: Sequence[Sequence[int]]) -> torch.Tensor:
