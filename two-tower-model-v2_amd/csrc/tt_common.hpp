@@ -132,43 +132,74 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-// Bitonic sort, descending, of 64*PER keys held PER per lane (element e = lane*PER + r).
-template <int PER>
-__device__ __forceinline__ void bitonic_desc(uint64_t (&key)[PER], int lane) {
-  constexpr int N = 64 * PER;
+// Value of lane (lane ^ M): DPP for M < 16 (quad_perm, or a row shift left / right picked by
+// the lane's bit M: VALU moves, a few cycles), ds_bpermute (__shfl_xor) for M = 16, 32.  The
+// whole wave must be active (a DPP read of a disabled lane does not return its register).
+template <int M>
+__device__ __forceinline__ uint32_t lane_xor_u32(uint32_t x, int lane) {
+  if constexpr (M == 1) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xb1, 0xf, 0xf, false);  // [1,0,3,2]
+  } else if constexpr (M == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4e, 0xf, 0xf, false);  // [2,3,0,1]
+  } else if constexpr (M == 4 || M == 8) {
+    const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x100 + M, 0xf, 0xf, false);
+    const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x110 + M, 0xf, 0xf, false);
+    return (lane & M) ? dn : up;  // row_shl M: lane i reads i + M; row_shr M: i - M
+  } else {
+    return (uint32_t)__shfl_xor((int)x, M, 64);
+  }
+}
+template <int M>
+__device__ __forceinline__ uint64_t lane_xor_u64(uint64_t v, int lane) {
+  const uint32_t lo = lane_xor_u32<M>((uint32_t)v, lane);
+  const uint32_t hi = lane_xor_u32<M>((uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Bitonic sort, descending, of 64*PER keys held PER per lane (element e = lane*PER + r), the
+// whole wave active.  Stages unrolled at compile time so the lane exchanges (lane ^ stride/PER)
+// are DPP moves except for partner distances 16 and 32 (3 of the 21 cross-lane stages at
+// PER = 4): the ds_bpermute exchange of every stage (~100+ cycles of latency each) made a
+// 256-key sort ~2.5 us.
+template <int PER, int SIZE, int STRIDE>
+__device__ __forceinline__ void bitonic_steps(uint64_t (&key)[PER], int lane) {
+  if constexpr (STRIDE >= PER) {
+    constexpr int LM = STRIDE / PER;
 #pragma unroll
-  for (int size = 2; size <= N; size <<= 1) {
+    for (int r = 0; r < PER; ++r) {
+      const int e = lane * PER + r;
+      const uint64_t o = lane_xor_u64<LM>(key[r], lane);
+      const bool up = (e & SIZE) == 0;
+      const bool lower = (e & STRIDE) == 0;
+      const bool keep_max = (lower == up);
+      const uint64_t mx = key[r] > o ? key[r] : o;
+      const uint64_t mn = key[r] > o ? o : key[r];
+      key[r] = keep_max ? mx : mn;
+    }
+  } else {
 #pragma unroll
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      if (stride >= PER) {
-        const int lm = stride / PER;
-#pragma unroll
-        for (int r = 0; r < PER; ++r) {
-          const int e = lane * PER + r;
-          const uint64_t o = shfl_xor_u64(key[r], lm);
-          const bool up = (e & size) == 0;
-          const bool lower = (e & stride) == 0;
-          const bool keep_max = (lower == up);
-          const uint64_t mx = key[r] > o ? key[r] : o;
-          const uint64_t mn = key[r] > o ? o : key[r];
-          key[r] = keep_max ? mx : mn;
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < PER; ++r) {
-          if ((r & stride) == 0) {
-            const int r2 = r | stride;
-            const int e = lane * PER + r;
-            const bool up = (e & size) == 0;
-            const uint64_t a = key[r], b = key[r2];
-            const uint64_t mx = a > b ? a : b, mn = a > b ? b : a;
-            key[r] = up ? mx : mn;
-            key[r2] = up ? mn : mx;
-          }
-        }
+    for (int r = 0; r < PER; ++r) {
+      if ((r & STRIDE) == 0) {
+        const int r2 = r | STRIDE;
+        const int e = lane * PER + r;
+        const bool up = (e & SIZE) == 0;
+        const uint64_t a = key[r], b = key[r2];
+        const uint64_t mx = a > b ? a : b, mn = a > b ? b : a;
+        key[r] = up ? mx : mn;
+        key[r2] = up ? mn : mx;
       }
     }
   }
+  if constexpr (STRIDE > 1) bitonic_steps<PER, SIZE, STRIDE / 2>(key, lane);
+}
+template <int PER, int SIZE>
+__device__ __forceinline__ void bitonic_sizes(uint64_t (&key)[PER], int lane) {
+  bitonic_steps<PER, SIZE, SIZE / 2>(key, lane);
+  if constexpr (SIZE < 64 * PER) bitonic_sizes<PER, SIZE * 2>(key, lane);
+}
+template <int PER>
+__device__ __forceinline__ void bitonic_desc(uint64_t (&key)[PER], int lane) {
+  bitonic_sizes<PER, 2>(key, lane);
 }
 
 // numpy pairwise float32 sum of v[i]*v[i] (i < n, stride 1), sequential in ONE lane.
