@@ -765,7 +765,7 @@ def main():
             "achieved_hbm_gbps": 2.0 * (hi - lo) * ep / (lvl_ms * 1e-3) / 1e9,
             "hbm_peak_gbps": HBM_PEAK_GBPS,
             "frac": 2.0 * (hi - lo) * ep / (lvl_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
-            "kernel": f"k_filter_ring<{ep}, 2>"}
+            "kernel": f"k_filter_topm<{ep}>"}
         del ws1
 
     cpu_a = None

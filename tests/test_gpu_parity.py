@@ -100,6 +100,13 @@ BF16_CASES = [c for c in SCAN_CASES if c[3] <= 128] + [
     (250001, 768, 7, 128),   # E = 768, k at the maximum
     (130000, 64, 256, 100),  # the largest coarse batch
     (99999, 512, 2, 1),
+    # the single-pass path (nq <= 4): one slab per CU, ragged / tiny slabs, every E shape
+    (1000, 384, 3, 10),      # slabs of 4 rows: first tiles partly out of range
+    (4096, 384, 4, 100),     # 16 rows per slab: the tile-max bound never fills
+    (3000, 100, 2, 50),      # E padded to 128
+    (5000, 768, 4, 100),     # E = 768: one compute wave per tile
+    (40000, 64, 4, 100),     # E = 64: two k-steps per tile
+    (250001, 768, 3, 128),   # k at the maximum, ragged last slab
 ]
 
 
@@ -159,7 +166,30 @@ def test_bf16_filter_exact_under_biased_rounding(K, oracle_mod):
     assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
 
 
-@pytest.mark.parametrize("nq", [1, 16, 256, 300])
+def test_bf16_single_pass_clustered_slab_takes_fallback(K, oracle_mod):
+    """The single-pass small-batch path keeps 16 rows per slab (one slab per CU): a catalog
+    whose best rows crowd into ONE slab (40 near-copies of the query, consecutive) breaks its
+    certification (that slab's 16th kept row is inside the band), so the query must take the
+    exact fallback -- and still come out bit-exact."""
+    rng = np.random.default_rng(83)
+    n, d, k = 200000, 384, 100
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    q = rng.standard_normal((1, d)).astype(np.float32)
+    x[5000:5040] = q + 0.05 * rng.standard_normal((40, d)).astype(np.float32)
+    x = oracle_mod.l2norm_rows(x, 0)
+    q = oracle_mod.l2norm_rows(q, 0)
+    db = dev_rows(x)
+    db16 = db.to(torch.bfloat16)
+    ws = torch.empty(K.filter_workspace_bytes(n, d, 1, k), dtype=torch.uint8, device="cuda")
+    s, i = K.scan_topk_bf16(db, db16, n, d, dev_rows(q), k, bounds(K, db, db16, d),
+                            workspace=ws)
+    torch.cuda.synchronize()
+    assert K.filter_fallback_count(ws, n, d, 1, k) == 1
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
+
+
+@pytest.mark.parametrize("nq", [1, 4, 16, 256, 300])
 def test_bf16_filter_no_fallback_on_iid_data(K, nq):
     """The optimistic threshold must hold on iid data: no query may need the exact fallback
     (a performance property: fallbacks are correct but slow).  nq <= 256: the small path."""

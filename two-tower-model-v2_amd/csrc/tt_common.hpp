@@ -18,6 +18,7 @@
 
 #include "../../include/twotower_hip.h"
 
+#include <type_traits>
 namespace tt {
 
 // ----------------------------------------------------------------------------- errors
@@ -200,6 +201,96 @@ __device__ __forceinline__ void bitonic_sizes(uint64_t (&key)[PER], int lane) {
 template <int PER>
 __device__ __forceinline__ void bitonic_desc(uint64_t (&key)[PER], int lane) {
   bitonic_sizes<PER, 2>(key, lane);
+}
+
+// Sort each row of 16 lanes (one key per lane) descending: the bitonic network of 16 on DPP
+// exchanges only (10 stages).  Row 0 (lanes 0..15) comes out descending; the other rows are
+// sorted too, in either direction (callers use row 0).
+__device__ __forceinline__ void bitonic_desc16_rows(uint64_t& key, int lane) {
+  auto step = [&](auto size_, auto stride_) __attribute__((always_inline)) {
+    constexpr int SIZE = decltype(size_)::value, STRIDE = decltype(stride_)::value;
+    const uint64_t o = lane_xor_u64<STRIDE>(key, lane);
+    const bool keep_max = ((lane & STRIDE) == 0) == ((lane & SIZE) == 0);
+    const uint64_t mx = key > o ? key : o, mn = key > o ? o : key;
+    key = keep_max ? mx : mn;
+  };
+  using std::integral_constant;
+  step(integral_constant<int, 2>{}, integral_constant<int, 1>{});
+  step(integral_constant<int, 4>{}, integral_constant<int, 2>{});
+  step(integral_constant<int, 4>{}, integral_constant<int, 1>{});
+  step(integral_constant<int, 8>{}, integral_constant<int, 4>{});
+  step(integral_constant<int, 8>{}, integral_constant<int, 2>{});
+  step(integral_constant<int, 8>{}, integral_constant<int, 1>{});
+  step(integral_constant<int, 16>{}, integral_constant<int, 8>{});
+  step(integral_constant<int, 16>{}, integral_constant<int, 4>{});
+  step(integral_constant<int, 16>{}, integral_constant<int, 2>{});
+  step(integral_constant<int, 16>{}, integral_constant<int, 1>{});
+}
+
+// Top 16 of the nonzero keys held PER per lane (whole wave active), without sorting them
+// all: the 16th largest high word x is built MSB-first (32 steps; a step counts the keys with
+// hi >= candidate by ballot + scalar popcount), ties at x resolved by the same search on the
+// low word among them; the <= 16 winners are placed by ballot prefix into lanes 0..15 through
+// `scratch` (LDS, 16 entries; the caller orders it against other LDS use) and sorted there
+// (bitonic_desc16_rows).  Returns lane i < n's key (i-th largest), 0 in the other lanes;
+// *n_out = min(16, #nonzero).  (A full bitonic sort of 128-256 64-bit keys per compaction:
+// ~2-3.6 us of one wave; this: a few hundred scalar-heavy instructions.)
+template <int PER>
+__device__ __forceinline__ uint64_t wave_top16(const uint64_t (&key)[PER], int lane,
+                                               uint64_t* scratch, int* n_out) {
+  int total = 0;
+#pragma unroll
+  for (int r = 0; r < PER; ++r) total += __popcll(__ballot(key[r] != 0ull));
+  uint32_t x = 0u, xl = 0u;  // select: hi > x, or hi == x and lo >= xl
+  if (total > 16) {
+#pragma unroll 1
+    for (int bit = 31; bit >= 0; --bit) {
+      const uint32_t cand = x | (1u << bit);
+      int c = 0;
+#pragma unroll
+      for (int r = 0; r < PER; ++r) c += __popcll(__ballot((uint32_t)(key[r] >> 32) >= cand));
+      if (c >= 16) x = cand;
+    }
+    int gt = 0, eq = 0;
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+      const uint32_t h = (uint32_t)(key[r] >> 32);
+      gt += __popcll(__ballot(h > x));
+      eq += __popcll(__ballot(h == x));
+    }
+    const int need = 16 - gt;  // >= 1 ties to take
+    if (eq > need) {
+#pragma unroll 1
+      for (int bit = 31; bit >= 0; --bit) {
+        const uint32_t cand = xl | (1u << bit);
+        int c = 0;
+#pragma unroll
+        for (int r = 0; r < PER; ++r)
+          c += __popcll(__ballot((uint32_t)(key[r] >> 32) == x && (uint32_t)key[r] >= cand));
+        if (c >= need) xl = cand;
+      }
+    }
+  } else {
+    x = 1u;  // every nonzero key (a real key's high word is >= 1)
+  }
+  int base = 0;
+#pragma unroll
+  for (int r = 0; r < PER; ++r) {
+    const uint32_t h = (uint32_t)(key[r] >> 32);
+    const bool sel = key[r] != 0ull && (h > x || (h == x && (uint32_t)key[r] >= xl));
+    const uint64_t bm = __ballot(sel);
+    const int pos = base + (int)__builtin_amdgcn_mbcnt_hi(
+                               (uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+    if (sel) scratch[pos] = key[r];
+    base += __popcll(bm);
+  }
+  wave_sync();
+  const int n = base < 16 ? base : 16;
+  uint64_t k = lane < n ? scratch[lane] : 0ull;
+  wave_sync();
+  bitonic_desc16_rows(k, lane);
+  *n_out = n;
+  return lane < 16 ? k : 0ull;
 }
 
 // numpy pairwise float32 sum of v[i]*v[i] (i < n, stride 1), sequential in ONE lane.

@@ -228,6 +228,9 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #ifndef TT_EXP_FINAL_TIMING
 #define TT_EXP_FINAL_TIMING 0  // printf k_final_topm phase wall-clock ticks (100 MHz), block 0
 #endif
+#ifndef TT_EXP_TM_STATS
+#define TT_EXP_TM_STATS 0  // printf per-block compaction / append counts and phase ticks (block 0, 100)
+#endif
 #ifndef TT_EXP_TM_SLOTS
 #define TT_EXP_TM_SLOTS 4  // single-pass small batches: ring slots (A/B)
 #endif
@@ -261,7 +264,7 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #endif
 TT_CHECK_EXP(TT_EXP_NOSEL || TT_EXP_NOWRITE || TT_EXP_MAXONLY ||
                  TT_EXP_SEL_STOP || TT_EXP_SEL_TIMING || TT_EXP_FINAL_STOP ||
-                 TT_EXP_FINAL_TIMING || TT_EXP_TM_SLOTS != 4,
+                 TT_EXP_FINAL_TIMING || TT_EXP_TM_STATS || TT_EXP_TM_SLOTS != 4,
              "TT_EXP_* (results wrong / printf / untested schedule)");
 TT_CHECK_EXP(TT_RING_HALF || TT_RING_QB4 || TT_EXP_NOIDLE || TT_EXP_PRIO ||
                  TT_RING_NT != 1 || TT_RR_STAGED != 1 || TT_RR_PF != 1 || TT_RR_NT,
@@ -1731,18 +1734,25 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_small(
 // streaming pass instead of sample level -> selection -> full level.  One block per CU
 // (G = #CUs, one round, no tail), each owning a contiguous slab; the bf16 image streams
 // HBM -> LDS through the ring of k_filter_ring (buffer_load ... lds, non-temporal, 3 tiles in
-// flight, one s_barrier per tile) and ONE wave scores it on bf16 MFMA (a 16-query block).  The
-// wave keeps, per query, the slab's running top-TM_M of a in an LDS buffer (append a >= tau,
-// the running TM_M-th best; compact by a wave bitonic sort when the buffer nears full: a
-// streaming top-m, ~TM_M ln(rows / TM_M) appends per query and slab) and writes it sorted.
+// flight, one s_barrier per tile) and one wave per 16-row block of a tile scores it on bf16
+// MFMA (a 16-query block).  Each such wave keeps, per query, the running top-TM_M of its rows'
+// a in an LDS buffer (append a >= tau, its running TM_M-th best; compact by a wave bitonic sort
+// when the buffer nears full: a streaming top-m, ~TM_M ln(rows / TM_M) appends per query); at
+// the end the waves' lists merge into the slab's sorted top-TM_M, and the block computes the
+// exact keys of those rows (exact16).
 // k_final_topm then takes, per query, the union U of the G lists: A = k-th best a of U; a slab
 // dropped only rows with a <= tau_b (its TM_M-th best), so if every full list has
 // tau_b < A - 2 eps, U holds every row with a >= A - 2 eps (and A is the catalog's A_k):
 // the band, re-ranked exactly as in k_final_small.  Otherwise the query is flagged for the
 // exact fallback.  Bytes: the bf16 image once; no sample level, no per-level selections.
-constexpr int TM_NQ = 16;     // queries per search on this path (one MFMA query block)
+constexpr int TM_NQ = 16;     // queries per MFMA query block (the buffers' query capacity)
+// queries per search that take this path: per-tile appends, tile-max bounds and compactions
+// grow with the query count, and from 8 queries on the multi-level path is as fast (one-buyer
+// latency, topm vs multi-level, ms: nq 1 0.139 / 0.181, 2 0.145 / 0.195, 4 0.158 / 0.184,
+// 8 0.188 / 0.186, 16 0.225 / 0.189)
+constexpr int TM_NQ_RUN = 4;
 constexpr int TM_M = 16;      // rows kept per (query, slab)
-constexpr int TM_BUF = 256;   // per-query candidate buffer (wave bitonic sort of 4 keys / lane)
+constexpr int TM_BUF = 256;   // candidate buffer per query, split over the compute waves
 constexpr int TM_SLOTS = TT_EXP_TM_SLOTS, TM_PD = TM_SLOTS - 1;  // ring slots, tiles in flight
 constexpr int TM_WAVES = 8;
 constexpr int TM_CAP = 4096;  // final: keys per query (G x TM_M, G <= 256)
@@ -1779,12 +1789,23 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
   const int64_t j1 = (j0 + rows_per_blk < n) ? j0 + rows_per_blk : n;
   const int n_tiles = j0 < j1 ? (int)((j1 - j0 + TR - 1) / TR) : 0;
 
-  // wave 0: the query fragments (bf16 B operands, 16 queries) and per-query top-m state
+  // compute waves w < CW (one per 16-row block of a tile: the scoring of a tile is split so
+  // that no single wave's per-tile work -- fragment reads, MFMAs, appends -- paces the ring;
+  // one wave scoring the whole tile: 131 vs 122 us for the same stream without that work).
+  // Each holds the query fragments (bf16 B operands, 16 queries) and its own per-query top-m
+  // buffers tbuf[w][c][TMB].
+  constexpr int CW = RB, TMB = TM_BUF / CW, CPER = TMB / 64;
+  static_assert(TMB % 64 == 0 && TMB >= 2 * TM_M && CW <= TM_WAVES, "top-m buffer shape");
+  const bool cw = w < CW;
+  uint64_t* wbuf = tbuf + (cw ? w : 0) * TM_NQ * TMB;
   bf16x8 qf[KS];
   const bool qv = col < nq;
   float tau = qv ? -__builtin_huge_valf() : __builtin_huge_valf();
   int cnt = 0;  // appended keys of query `col` (same in the 4 lanes of a column)
-  if (w == 0) {
+  float tm[16], tmin = -__builtin_huge_valf();  // tile-max bound of tau (appends)
+  int st_compact = 0;
+  uint64_t st_t0 = TT_EXP_TM_STATS ? wall_clock64() : 0, st_t1 = 0, st_t2 = 0;
+  if (cw) {
     const float* qp = q + (int64_t)(qv ? col : 0) * ldq + 8 * g;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
@@ -1834,66 +1855,112 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
     else if (younger == 1) wait_vm<PPW>();
     else wait_vm<0>();
   };
-  uint32_t lrd[RB][4];
-#pragma unroll
-  for (int rb = 0; rb < RB; ++rb) {
-    const int r = 16 * rb + col, f = r & FM, h = f >> 2;
+  // fragment read offsets of the wave's row block (rows 16 w + col of a tile)
+  uint32_t lrd[4];
+  {
+    const int r = 16 * (cw ? w : 0) + col, f = r & FM, h = f >> 2;
 #pragma unroll
     for (int v = 0; v < 4; ++v)
-      lrd[rb][v] = lds_addr(ring) + 16 * (r * CPR + (g ^ (f & 3))) + 64 * (v ^ h);
+      lrd[v] = lds_addr(ring) + 16 * (r * CPR + (g ^ (f & 3))) + 64 * (v ^ h);
   }
-  // compaction of query c's buffer: sort (wave bitonic, 4 keys per lane), keep the top TM_M,
-  // tau = the TM_M-th key's score (rare: plain LDS accesses, the ring may drain once)
+  // compaction of query c's buffer to its sorted top TM_M (wave_top16: a bitwise select, not a
+  // sort of the buffer); tau = the TM_M-th key's score
+  static_assert(TM_M == 16, "wave_top16 keeps 16");
   auto compact = [&](int c) __attribute__((always_inline)) {
-    uint64_t* b = tbuf + c * TM_BUF;
+    uint64_t* b = wbuf + c * TMB;
     const int cc = __shfl(cnt, c, 64);
-    uint64_t key[4];
+    uint64_t key[CPER];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int e = lane * 4 + r;
+    for (int r = 0; r < CPER; ++r) {
+      const int e = lane * CPER + r;
       key[r] = e < cc ? b[e] : 0ull;
     }
-    bitonic_desc<4>(key, lane);
-    wave_sync();
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int e = lane * 4 + r;
-      if (e < TM_M) b[e] = key[r];
-    }
-    const uint32_t hk = __shfl((uint32_t)(key[(TM_M - 1) % 4] >> 32), (TM_M - 1) / 4, 64);
-    const int nc = cc < TM_M ? cc : TM_M;
+    int nc;
+    const uint64_t k = wave_top16<CPER>(key, lane, b, &nc);
+    if (lane < nc) b[lane] = k;
+    const uint32_t hk = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(k >> 32), TM_M - 1);
     if (col == c) {
       cnt = nc;
-      if (nc == TM_M) tau = key_float(hk);
+      if (nc == TM_M) tau = fmaxf(tau, key_float(hk));
     }
     wave_sync();
   };
 
-  // appends of tile t's scores (lane: rows jt + 16 rb + 4 g + jj of query col): a >= tau
+  // appends of tile t's scores (lane: rows jt + 16 w + 4 g + jj of query col): a >= tau
   // (NaN never passes); positions within a column by ballot (no atomics): the 4 lanes of a
   // column hold cnt.  Then the compactions the buffers need.
-  auto appends = [&](const f32x4 (&acc)[RB], int t) __attribute__((always_inline)) {
-    const int64_t jt = j0 + (int64_t)t * TR;
+  auto appends = [&](const f32x4& acc, int t) __attribute__((always_inline)) {
+    const int64_t jt = j0 + (int64_t)t * TR + 16 * w;
     const uint64_t colmask = 0x0001000100010001ull << col;
     const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb)
+    for (int jj = 0; jj < 4; ++jj) {
+      const int64_t row = jt + 4 * g + jj;
+      const float v = acc[jj];
+      const bool pass = row < j1 && v >= tau;
+      const uint64_t bm = __ballot(pass);
+      if (bm != 0ull) {
+        const uint64_t mc = bm & colmask;
+        if (pass) {
+          const int pos = cnt + __popcll(mc & below);
+          lds_write64(lds_addr(wbuf + col * TMB + pos), make_key(v, (uint32_t)row));
+        }
+        cnt += __popcll(mc);
+      }
+    }
+    // tau between compactions: the TM_M-th largest of a set of scores of DISTINCT rows (tm[],
+    // the same multiset in the 4 lanes of a column) is a lower bound of the running TM_M-th
+    // best.  The set starts as the first tile's 16 rows (if all are in range and finite: cnt),
+    // then each later tile's max replaces the set's min when larger (a tile max is a row of
+    // that tile: distinct).  Without it an empty buffer took ~TMB rows before its first
+    // compaction, and tau then lagged: 3-4 compactions per query and wave, all queries in
+    // the same tiles (nq = 16: 206 us for the 124 us stream).
+    if (t == 0) {
+      const bool full = cnt == TM_M;
+      float v16[16];
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
-        const int64_t row = jt + 16 * rb + 4 * g + jj;
-        const float v = acc[rb][jj];
-        const bool pass = row < j1 && v >= tau;
-        const uint64_t bm = __ballot(pass);
-        if (bm != 0ull) {
-          const uint64_t mc = bm & colmask;
-          if (pass) {
-            const int pos = cnt + __popcll(mc & below);
-            lds_write64(lds_addr(tbuf + col * TM_BUF + pos), make_key(v, (uint32_t)row));
-          }
-          cnt += __popcll(mc);
-        }
+        v16[jj] = acc[jj];
+        const auto x16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[jj]),
+                                                          __float_as_uint(acc[jj]), false, false);
+        v16[4 + jj] = __uint_as_float((g & 1) ? x16[0] : x16[1]);  // lane ^ 16
       }
-    const uint64_t need = __ballot(lane < 16 && cnt > TM_BUF - TR);
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const auto x32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v16[jj]),
+                                                          __float_as_uint(v16[jj]), false, false);
+        v16[8 + jj] = __uint_as_float(lane < 32 ? x32[1] : x32[0]);  // lane ^ 32
+      }
+      float mn = v16[0];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        tm[i] = full ? v16[i] : -__builtin_huge_valf();
+        mn = fminf(mn, v16[i]);
+      }
+      tmin = full ? mn : -__builtin_huge_valf();
+    } else {
+      float m = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3]));
+      const auto x16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m),
+                                                        false, false);
+      m = fmaxf(__uint_as_float(x16[0]), __uint_as_float(x16[1]));
+      const auto x32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m),
+                                                        false, false);
+      m = fmaxf(__uint_as_float(x32[0]), __uint_as_float(x32[1]));  // the column's tile max
+      if (m > tmin) {  // (NaN never)
+        bool done = false;
+        float mn = m;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const bool hit = !done && tm[i] == tmin;
+          tm[i] = hit ? m : tm[i];
+          done |= hit;
+          mn = fminf(mn, tm[i]);
+        }
+        tmin = mn;
+      }
+    }
+    tau = fmaxf(tau, qv ? tmin : tau);
+    const uint64_t need = __ballot(lane < 16 && cnt > TMB - 16);
     if (need != 0ull) {
       lds_wait<0>();
       uint64_t nd = need;
@@ -1901,16 +1968,17 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
         const int c = __builtin_ctzll(nd);
         nd &= nd - 1;
         compact(c);
+        if (TT_EXP_TM_STATS) ++st_compact;
       }
     }
   };
 
-  // wave 0, per tile t: issue ALL of tile t's fragment reads (RB x KS x 16 B per lane), run
-  // tile t-1's appends while they are in flight, one wait, then tile t's MFMA chain (its
-  // scores are appended in the next iteration: the LDS latency hides behind the append VALU)
-  f32x4 acc[RB];
+  // compute wave, per tile t: issue all of its row block's fragment reads (KS x 16 B per
+  // lane), run tile t-1's appends while they are in flight, one wait, then tile t's MFMA chain
+  // (its scores are appended in the next iteration: the LDS latency hides behind the appends)
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   for (int t = 0; t < TM_PD && t < n_tiles; ++t) issue(t);
-  if (w == 1 && blk < nq) {  // 2 eps of query blk for the final, while the first tiles land
+  if (w == TM_WAVES - 1 && blk < nq) {  // 2 eps of query blk for the final (not a compute wave)
     const float e = query_eps2_wave<EP>(q + (int64_t)blk * ldq, X, R, lane);
     if (lane == 0) eps2[blk] = e;
   }
@@ -1918,41 +1986,53 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
     wait_tiles(n_tiles - 1 - t < TM_PD - 1 ? n_tiles - 1 - t : TM_PD - 1);
     lds_barrier();  // tile t landed (every wave's pieces); every wave is done with tile t-1
     if (t + TM_PD < n_tiles) issue(t + TM_PD);  // into the slot of tile t-1
-    if (w == 0) {
+    if (cw) {
       const uint32_t so = (uint32_t)((t % TM_SLOTS) * TILE_B);
-      u32x4 fr[RB][KS];
+      u32x4 fr[KS];
       static_for<KS>([&](auto s_) __attribute__((always_inline)) {
         constexpr int S = decltype(s_)::value;
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb) fr[rb][S] = lds_read128<256 * (S / 4)>(lrd[rb][S % 4] + so);
+        fr[S] = lds_read128<256 * (S / 4)>(lrd[S % 4] + so);
       });
       if (t > 0) appends(acc, t - 1);
       lds_wait<0>();
-#pragma unroll
-      for (int rb = 0; rb < RB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      acc = f32x4{0.f, 0.f, 0.f, 0.f};
       static_for<KS>([&](auto s_) __attribute__((always_inline)) {
         constexpr int S = decltype(s_)::value;
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb) reg_tie(fr[rb][S]);
-#pragma unroll
-        for (int rb = 0; rb < RB; ++rb)
-          acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fr[rb][S]),
-                                                            qf[S], acc[rb], 0, 0, 0);
+        reg_tie(fr[S]);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fr[S]), qf[S],
+                                                      acc, 0, 0, 0);
       });
     }
   }
-  if (w == 0 && n_tiles > 0) appends(acc, n_tiles - 1);
+  if (cw && n_tiles > 0) appends(acc, n_tiles - 1);
   wait_vm<0>();
-  if (w == 0) {
-    lds_wait<0>();
-    for (int c = 0; c < nq; ++c) {
-      compact(c);
-      const int nc = __shfl(cnt, c, 64);
-      if (lane < nc) lists[((int64_t)c * G + blk) * TM_M + lane] = tbuf[c * TM_BUF + lane];
-      if (lane == 0) {
-        counts[(int64_t)c * G + blk] = nc;
-        ncs[c] = nc;
+  if (TT_EXP_TM_STATS) st_t1 = wall_clock64();
+  // end of the slab, per query (queries spread over the waves): the top TM_M of the CW
+  // buffers' keys together (wave_top16) -> tbuf[0][c], the slab's sorted list
+  __shared__ int ncw[CW][TM_NQ];
+  if (cw && lane < nq && g == 0) ncw[w][lane] = cnt;  // lanes 0..15: col = lane
+  lds_wait<0>();  // the appends' hand-issued LDS writes retire before the barrier
+  __syncthreads();
+  for (int c = w; c < nq; c += TM_WAVES) {
+    uint64_t key[CW * CPER];
+#pragma unroll
+    for (int wb = 0; wb < CW; ++wb) {
+      const int cc = ncw[wb][c];
+#pragma unroll
+      for (int r = 0; r < CPER; ++r) {
+        const int e = lane * CPER + r;
+        key[wb * CPER + r] = e < cc ? tbuf[(wb * TM_NQ + c) * TMB + e] : 0ull;
       }
+    }
+    int nc;
+    const uint64_t k = wave_top16<CW * CPER>(key, lane, tbuf + c * TMB, &nc);
+    if (lane < nc) {
+      tbuf[c * TMB + lane] = k;
+      lists[((int64_t)c * G + blk) * TM_M + lane] = k;
+    }
+    if (lane == 0) {
+      counts[(int64_t)c * G + blk] = nc;
+      ncs[c] = nc;
     }
   }
   // exact keys of the kept rows (every block in parallel, one 16-row exact16 pass per query
@@ -1962,7 +2042,7 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
   for (int c = w; c < nq; c += TM_WAVES) {
     const int nc = ncs[c], r16 = lane & 15, g4 = 4 * (lane >> 4);
     if (nc == 0) continue;
-    const uint64_t* tb = tbuf + c * TM_BUF;
+    const uint64_t* tb = tbuf + c * (TM_BUF / RB);
     const f32x4 acc =
         exact16<EP>(db, ld, key_row(tb[r16 < nc ? r16 : 0]), q + (int64_t)c * ldq, lane);
     if (r16 == 0) {
@@ -1972,6 +2052,13 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
           xkeys[((int64_t)c * G + blk) * TM_M + g4 + j] =
               acc[j] != acc[j] ? 0ull : make_key(acc[j], key_row(tb[g4 + j]));
     }
+  }
+  if (TT_EXP_TM_STATS) {
+    __syncthreads();
+    st_t2 = wall_clock64();
+    if ((blk == 0 || blk == 100) && cw && lane == 0)
+      printf("topm blk %d wave %d: compactions %d, stream %d ticks, tail %d ticks, cnt0 %d\n",
+             blk, w, st_compact, (int)(st_t1 - st_t0), (int)(st_t2 - st_t1), ncw[w][0]);
   }
 }
 
@@ -2622,7 +2709,7 @@ static FilterPlan plan_filter_uncached(int64_t n, int nq, int k, int ep) {
   for (int i = 0; i < nl; ++i) p.small = p.small && p.lv[i].n_slabs <= SM_THREADS;
   // single pass for the smallest batches: lists [nq][G][TM_M] and counts [nq][G] fit the
   // level workspace once max_slabs >= G (FL_CAP >= TM_M)
-  p.topm = nq <= TM_NQ && !topm_disabled() && device_cus() * TM_M <= TM_CAP &&
+  p.topm = nq <= TM_NQ_RUN && !topm_disabled() && device_cus() * TM_M <= TM_CAP &&
            device_cus() <= SM_THREADS;
   if (p.topm && p.max_slabs < device_cus()) p.max_slabs = device_cus();
   return p;
