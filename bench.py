@@ -147,8 +147,9 @@ def configs1(a, dev, rank):
                        "(MiniLM-L12 arch, seeded random weights, synthetic Zipf token ids, "
                        "L ~ U[16,128]) + exact top-100 over a 100k x 384 catalog",
            "texts": n_txt, "batch": BS}
-    res = {}
-    for prec, nb in (("bf16", len(batches)), ("f32", min(16, len(batches)))):
+    res, ys = {}, {}
+    for prec, nb in (("bf16", len(batches)), ("x3", min(64, len(batches))),
+                     ("f32", min(16, len(batches)))):
         enc = BertEncoder(sd, cfg, device=dev, prec=prec)
         pooled = torch.empty((BS, cfg["hidden"]), device=dev)
         e_enc = [torch.cuda.Event(enable_timing=True) for _ in range(2 * nb)]
@@ -208,30 +209,31 @@ def configs1(a, dev, rank):
         dt2 = time.perf_counter() - t0
         lens = [len(x) for x in seqs[:nb * BS]]
         fl = encoder_flops(lens)
-        peak = BF16_MFMA_PEAK_TFLOPS if prec == "bf16" else F32_MFMA_PEAK_TFLOPS
+        peak = F32_MFMA_PEAK_TFLOPS if prec == "f32" else BF16_MFMA_PEAK_TFLOPS
+        mf = 3.0 if prec == "x3" else 1.0  # x3: three bf16 MFMAs per product
         ntx = min(n_txt, nb * BS)
         res[prec] = {"texts_timed": ntx, "texts_per_s": ntx / min(dt, dt2),
                      "texts_per_s_two_streams": ntx / dt2, "texts_per_s_one_stream": ntx / dt,
                      "ms_per_batch": dt / nb * 1e3, "encode_ms_per_batch": enc_ms / nb,
                      "search_ms_per_batch": srch_ms / nb,
                      "encode_tflops": fl / (enc_ms * 1e-3) / 1e12,
-                     "encode_mfma_frac": fl / (enc_ms * 1e-3) / 1e12 / peak,
-                     "encode_mfma_frac_two_streams": fl / dt2 / 1e12 / peak,
+                     "encode_mfma_frac": mf * fl / (enc_ms * 1e-3) / 1e12 / peak,
+                     "encode_mfma_frac_two_streams": mf * fl / dt2 / 1e12 / peak,
                      "mfma_peak_tflops": peak,
                      "tokens_timed": int(sum(lens))}
-        if prec == "bf16":
-            y16 = step(0, False)[0].clone()
-        else:
-            y32 = step(0, False)[0]
+        if prec == "x3":
+            res[prec]["mfma_products_per_flop"] = 3
+        ys[prec] = step(0, False)[0].clone().detach()
         del enc
         torch.cuda.empty_cache()
-    # bf16 encoder vs the f32 (parity) encoder on the L2-normalised item embeddings
-    # (item_tower.py:209): worst cosine distance over the first batch
-    y16, y32 = y16.detach(), y32.detach()
-    cos = (y16 * y32).sum(dim=1)
-    res["bf16_vs_f32_item_cosine"] = {"min_cos": float(cos.min()),
-                                      "max_1_minus_cos": float((1 - cos).max()),
-                                      "max_abs_diff": float((y16 - y32).abs().max())}
+    # bf16 and x3 encoders vs the f32 (parity) encoder on the L2-normalised item embeddings
+    # (item_tower.py:209): worst cosine distance / element difference over the first batch
+    for prec in ("bf16", "x3"):
+        cos = (ys[prec] * ys["f32"]).sum(dim=1)
+        res[f"{prec}_vs_f32_item_cosine"] = {
+            "min_cos": float(cos.min()), "max_1_minus_cos": float((1 - cos).max()),
+            "max_abs_diff": float((ys[prec] - ys["f32"]).abs().max())}
+    res["x3_over_f32_texts_per_s"] = res["x3"]["texts_per_s"] / res["f32"]["texts_per_s"]
     out.update(res)
     out["value"] = res["bf16"]["texts_per_s"]
     out["unit"] = "texts/s (encode + top-100 per batch of 256)"

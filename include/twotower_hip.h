@@ -224,10 +224,14 @@ int tt_attn_agg_l2_f32_ws(const float* items, int64_t b, int32_t s, int32_t d, c
  * are concatenated row-wise into wqkv [3H, H] / bqkv [3H].  prec TT_PREC_F32 runs every GEMM
  * on v_mfma_f32_16x16x4_f32 (the parity path); TT_PREC_BF16 runs them on
  * v_mfma_f32_16x16x32_bf16 with f32 accumulation, f32 residual stream, LayerNorm, softmax and
- * pooling (the *_bf16 weight copies must be set).  out_pooled [n_seq, ld_out] f32.
+ * pooling (the *_bf16 weight copies must be set); TT_PREC_X3 keeps the f32 path's operands and
+ * splits them on the fly into bf16 hi + lo, each product as three bf16 MFMAs (hi.hi + lo.hi +
+ * hi.lo, f32 accumulate: ~2^-16 relative per product instead of bf16's 2^-8) -- the f32 path's
+ * precision class at bf16 MFMA rates.  out_pooled [n_seq, ld_out] f32.
  * --------------------------------------------------------------------------------- */
 #define TT_PREC_F32 0
 #define TT_PREC_BF16 1
+#define TT_PREC_X3 2
 #define TT_ACT_NONE 0
 #define TT_ACT_GELU 1 /* exact erf GELU (hidden_act="gelu") */
 #define TT_ACT_RELU 2
@@ -240,6 +244,9 @@ typedef struct tt_bert_layer {
   const float *w2, *b2;       /* [H, I], [H]     output.dense                    */
   const float *ln2_g, *ln2_b; /* [H]             output.LayerNorm                */
   const uint16_t *wqkv_bf16, *wo_bf16, *w1_bf16, *w2_bf16; /* bf16 images (TT_PREC_BF16) */
+  /* TT_PREC_X3, optional: pre-split images [N, 2K] (tt_x3_split_weights); NULL -> the f32
+   * weights are split on the fly */
+  const uint16_t *wqkv_x3, *wo_x3, *w1_x3, *w2_x3;
 } tt_bert_layer;
 
 typedef struct tt_bert_model {
@@ -265,6 +272,19 @@ int tt_bert_encode(const tt_bert_model* model, const int32_t* ids, const int32_t
 int tt_gemm_f32(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias,
                 const float* residual, int64_t ldr, float* C, int64_t ldc, uint16_t* C_bf16,
                 int64_t ldc16, int32_t M, int32_t N, int32_t K, int32_t act, void* stream);
+/* tt_gemm_x3: tt_gemm_f32's contract with the products on split-bf16 MFMA (TT_PREC_X3) */
+int tt_gemm_x3(const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias,
+                const float* residual, int64_t ldr, float* C, int64_t ldc, uint16_t* C_bf16,
+                int64_t ldc16, int32_t M, int32_t N, int32_t K, int32_t act, void* stream);
+/* tt_x3_split_weights: W [N, K] f32 -> out [N, 2K] bf16, per 32-k block 32 hi then 32 lo in
+ * the x3 GEMM's lane-slot order (K % 32 == 0).  tt_gemm_x3w: tt_gemm_x3 with W given as that
+ * pre-split image (ld_wx3 in bf16 elements): the weights' split is done once, not per tile. */
+int tt_x3_split_weights(const float* W, int64_t ldw, int32_t N, int32_t K, uint16_t* out,
+                        int64_t ld_out, void* stream);
+int tt_gemm_x3w(const float* A, int64_t lda, const uint16_t* Wx3, int64_t ld_wx3,
+                const float* bias, const float* residual, int64_t ldr, float* C, int64_t ldc,
+                uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N, int32_t K, int32_t act,
+                void* stream);
 int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
                  const float* bias, const float* residual, int64_t ldr, float* C, int64_t ldc,
                  uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N, int32_t K, int32_t act,

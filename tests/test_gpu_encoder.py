@@ -27,6 +27,8 @@ def _gemm(A, W, bias=None, res=None, act=0, prec="f32", want16=False):
     C16 = torch.empty((M, N), device="cuda", dtype=torch.bfloat16) if want16 else None
     if prec == "f32":
         fn, a, w = L.tt_gemm_f32, A, W
+    elif prec == "x3":
+        fn, a, w = L.tt_gemm_x3, A, W
     else:
         fn, a, w = L.tt_gemm_bf16, A.to(torch.bfloat16), W.to(torch.bfloat16)
     _lib.check(fn(a.data_ptr(), a.stride(0), w.data_ptr(), w.stride(0),
@@ -51,6 +53,57 @@ def test_gemm_f32_vs_torch(M, N, K, act):
     ref = {0: ref, 1: F.gelu(ref), 2: torch.relu(ref)}[act] + R.double()
     torch.testing.assert_close(C.double(), ref, rtol=1e-5, atol=2e-5)
     assert torch.equal(C16, C.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 128, 32), (77, 256, 512), (300, 1152, 384),
+                                   (1000, 384, 1536), (4097, 1536, 384)])
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_gemm_x3_vs_torch(M, N, K, act):
+    """Split-bf16 products (hi.hi + lo.hi + hi.lo, f32 accumulate): the f32 GEMM's tolerance
+    class -- 2^-16-relative products instead of bf16's 2^-8 (the bf16 test below needs its
+    reference computed on bf16-rounded operands; this one does not)."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + act + 7)
+    A = torch.randn((M, K), generator=g, device="cuda")
+    W = torch.randn((N, K), generator=g, device="cuda") / K ** 0.5
+    b = torch.randn(N, generator=g, device="cuda")
+    R = torch.randn((M, N), generator=g, device="cuda")
+    C, C16 = _gemm(A, W, b, R, act, "x3", want16=True)
+    ref = (A.double() @ W.double().T) + b.double()
+    ref = {0: ref, 1: F.gelu(ref), 2: torch.relu(ref)}[act] + R.double()
+    torch.testing.assert_close(C.double(), ref, rtol=1e-5, atol=5e-5)
+    assert torch.equal(C16, C.to(torch.bfloat16))
+    Cf, _ = _gemm(A, W, b, R, act, "f32")
+    assert (C - Cf).abs().max().item() < 5e-5  # next to the f32 MFMA path
+
+
+@pytest.mark.parametrize("M,N,K,act", [(1, 128, 32, 0), (300, 1152, 384, 0), (1000, 384, 1536, 0),
+                                       (4097, 1536, 384, 1), (77, 256, 512, 2)])
+def test_gemm_x3_presplit_weights_identical(M, N, K, act):
+    """tt_gemm_x3w (weights split once by tt_x3_split_weights, the encoder's x3 path) computes
+    the same split and the same MFMA sequence as tt_gemm_x3's on-the-fly split: equal bits."""
+    from twotower import _lib
+    from twotower.item_tower import x3_split_weights
+
+    g = torch.Generator(device="cuda").manual_seed(M + 2 * N + K + act)
+    A = torch.randn((M, K), generator=g, device="cuda")
+    W = torch.randn((N, K), generator=g, device="cuda") / K ** 0.5
+    b = torch.randn(N, generator=g, device="cuda")
+    R = torch.randn((M, N), generator=g, device="cuda")
+    C, _ = _gemm(A, W, b, R, act, "x3")
+    Wx = x3_split_weights(W)
+    assert Wx.shape == (N, 2 * K) and Wx.dtype == torch.bfloat16
+    C2 = torch.empty_like(C)
+    _lib.check(_lib.lib().tt_gemm_x3w(A.data_ptr(), A.stride(0), Wx.data_ptr(), Wx.stride(0),
+                                      b.data_ptr(), R.data_ptr(), R.stride(0), C2.data_ptr(),
+                                      C2.stride(0), None, 0, M, N, K, act, _lib.stream_ptr()),
+               "tt_gemm_x3w")
+    assert torch.equal(C2, C)
+    # the split itself: hi = bf16(w), lo = bf16(w - hi), per 32-k block in lane-slot order
+    kb, slot = 1 if K > 32 else 0, 13  # slot 13 = group 1, u = 5 -> k = 16 + 4 + 1
+    w = W[3 % N, 32 * kb + 21]
+    hi = w.to(torch.bfloat16)
+    assert Wx[3 % N, 64 * kb + slot] == hi
+    assert Wx[3 % N, 64 * kb + 32 + slot] == (w - hi.float()).to(torch.bfloat16)
 
 
 @pytest.mark.parametrize("M,N,K", [(5, 128, 64), (300, 1152, 384), (2049, 384, 1536)])
@@ -125,7 +178,7 @@ def test_layernorm_vs_torch():
 
 
 @pytest.mark.parametrize("lens", [[1], [7, 64, 128], [3, 200, 1, 512, 33], [31, 32, 33, 17]])
-@pytest.mark.parametrize("kind", ["scalar", "mfma_f32", "mfma_bf16", "bf16_in_out"])
+@pytest.mark.parametrize("kind", ["scalar", "mfma_f32", "mfma_x3", "mfma_bf16", "bf16_in_out"])
 def test_attention_varlen_vs_torch(lens, kind):
     from twotower import _lib
 
@@ -146,7 +199,8 @@ def test_attention_varlen_vs_torch(lens, kind):
                                         _lib.stream_ptr())
     else:
         rc = L.tt_attention_varlen(qkv.data_ptr(), 3 * H, cu.data_ptr(), len(lens), max(lens), H, nh,
-                                   _lib.TT_PREC_BF16 if kind == "mfma_bf16" else _lib.TT_PREC_F32,
+                                   {"mfma_bf16": _lib.TT_PREC_BF16, "mfma_x3": _lib.TT_PREC_X3}.get(
+                                       kind, _lib.TT_PREC_F32),
                                    out.data_ptr(), H, out16.data_ptr(), _lib.stream_ptr())
     _lib.check(rc, "attn")
     if kind == "bf16_in_out":
@@ -160,7 +214,8 @@ def test_attention_varlen_vs_torch(lens, kind):
         a, b = c[i], c[i + 1]
         q, k, v = (qkv[a:b, j * H:(j + 1) * H].view(b - a, nh, 32).transpose(0, 1) for j in range(3))
         ref[a:b] = (torch.softmax(q @ k.transpose(1, 2) / 32 ** 0.5, -1) @ v).transpose(0, 1).reshape(b - a, H)
-    tol = 1e-5 if kind in ("scalar", "mfma_f32") else 2e-2  # bf16 operands: 8-bit mantissa
+    # bf16 operands: 8-bit mantissa; x3 (split-bf16): ~16-bit products, the f32 class
+    tol = {"scalar": 1e-5, "mfma_f32": 1e-5, "mfma_x3": 3e-5}.get(kind, 2e-2)
     torch.testing.assert_close(out, ref, rtol=tol, atol=tol)
 
 
@@ -171,9 +226,12 @@ def _encoder(prec, cfg=mbg.CFG, seed=mbg.SEED):
     return BertEncoder(sd, cfg, prec=prec), sd
 
 
-def test_encoder_f32_vs_transformers_fixture(golden):
+@pytest.mark.parametrize("prec", ["f32", "x3"])
+def test_encoder_f32_vs_transformers_fixture(golden, prec):
+    """12-layer MiniLM-shape encoder vs the transformers.BertModel fixture: the f32 MFMA path
+    and the split-bf16 (x3) path under the same 5e-5 bar."""
     g = golden("bert.npz")
-    enc, _ = _encoder("f32")
+    enc, _ = _encoder(prec)
     ids = torch.from_numpy(g["ids"]).cuda()
     cu = torch.from_numpy(g["cu_seqlens"]).cuda()
     y = enc.encode_packed(ids, cu, int(np.diff(g["cu_seqlens"]).max()))
@@ -192,12 +250,13 @@ def test_encoder_bf16_close_to_f32(golden):
     assert (y16 - ref).abs().max() < 0.05 * ref.abs().max()
 
 
-def test_encoder_f32_vs_oracle_large_batch():
+@pytest.mark.parametrize("prec", ["f32", "x3"])
+def test_encoder_f32_vs_oracle_large_batch(prec):
     """256 ragged sequences (L in [16, 128]) -- the configs[1] encode batch -- vs the oracle."""
     from oracle import bert_ref
 
     cfg = dict(mbg.CFG, layers=2)
-    enc, sd = _encoder("f32", cfg, seed=21)
+    enc, sd = _encoder(prec, cfg, seed=21)
     rng = np.random.default_rng(5)
     seqs = [rng.integers(0, cfg["vocab"], rng.integers(16, 129)).tolist() for _ in range(256)]
     y = enc.encode_ids(seqs).cpu()
@@ -359,7 +418,7 @@ def test_gemm_ln_bf16_rejects_unsupported():
                              _lib.stream_ptr()) == _lib.TT_ERR_UNSUPPORTED
 
 
-@pytest.mark.parametrize("prec", ["f32", "bf16"])
+@pytest.mark.parametrize("prec", ["f32", "x3", "bf16"])
 def test_encode_batch_device_chunking_changes_nothing(prec):
     """ItemTower.encode_batch runs chunks of device_batch texts (>= batch_size): every output
     row depends on its own text only, so any chunking gives bit-identical rows."""

@@ -1,6 +1,6 @@
 """Item-tower encode throughput (configs[1]: batches of 256 texts, L ~ U[16, 128]).
 
-    python tools/bench_encoder.py [--prec bf16|f32] [--batches 20] [--batch 256]
+    python tools/bench_encoder.py [--prec bf16|x3|f32] [--batches 20] [--batch 256]
 
 Synthetic "Arabic-like" token ids (Zipf over a 30k-id sub-range, <s>=0 / </s>=2), seeded
 MiniLM-L12 weights.  Prints one JSON line: texts/s, ms per batch, achieved TFLOP/s.
@@ -40,7 +40,7 @@ def flops(seqs, cfg):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--prec", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--prec", default="bf16", choices=["bf16", "x3", "f32"])
     ap.add_argument("--batches", type=int, default=20)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--fixed-len", type=int, default=None)

@@ -249,7 +249,55 @@ __device__ __forceinline__ int gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, i
   return 0;
 }
 
-template <typename T>
+// Split-bf16 ("x3") operands: an f32 value a = hi + lo + r with hi = bf16(a), lo = bf16(a - hi)
+// (a - hi is exact in f32), |r| <= 2^-17 |a|.  Eight f32 (two 16-B LDS fragments) -> the hi
+// and lo bf16x8 MFMA operands: 4 v_cvt_pk_bf16_f32 + 8 unpacks + 8 subtracts + 4 packs.
+__device__ __forceinline__ void split_bf16x8(const u32x4& f0, const u32x4& f1, bf16x8e& hi,
+                                             bf16x8e& lo) {
+  const f32x4 a = __builtin_bit_cast(f32x4, f0), b = __builtin_bit_cast(f32x4, f1);
+  const u32x4 h = {pack_bf16_hw(a[0], a[1]), pack_bf16_hw(a[2], a[3]), pack_bf16_hw(b[0], b[1]),
+                   pack_bf16_hw(b[2], b[3])};
+  auto lo16 = [](uint32_t p) { return __uint_as_float(p << 16); };
+  auto hi16 = [](uint32_t p) { return __uint_as_float(p & 0xffff0000u); };
+  const u32x4 l = {pack_bf16_hw(a[0] - lo16(h[0]), a[1] - hi16(h[0])),
+                   pack_bf16_hw(a[2] - lo16(h[1]), a[3] - hi16(h[1])),
+                   pack_bf16_hw(b[0] - lo16(h[2]), b[1] - hi16(h[2])),
+                   pack_bf16_hw(b[2] - lo16(h[3]), b[3] - hi16(h[3]))};
+  hi = __builtin_bit_cast(bf16x8e, h);
+  lo = __builtin_bit_cast(bf16x8e, l);
+}
+
+// X3 (T = float only): the f32 data path (tiles, swizzle, epilogue) with the products on bf16
+// MFMA: per 32-k stage each lane's 8 f32 of a row (its two read steps' chunks) are split into
+// hi / lo bf16x8 and acc += W_hi A_hi + W_lo A_hi + W_hi A_lo (the lo.lo term, <= 2^-18
+// relative, dropped): 3 v_mfma_f32_16x16x32_bf16 instead of 8 v_mfma_f32_16x16x4_f32 per
+// 16x16 block and stage -- 16x the f32 MFMA rate, 3x the work.  The k -> lane assignment (the
+// chunks of both read steps) is the same for A and W, so each MFMA still pairs equal k.
+// Pre-split weights for X3M = 2: W [N, K] f32 -> Wx [N, 2K] bf16; per 32-k block of a row,
+// 32 hi then 32 lo, each in the GEMM lanes' slot order (slot 8 g + u <- k = 4 g + u for u < 4,
+// 16 + 4 g + (u - 4) for u >= 4: the f32 tile's chunks g and 4 + g).  Thread per 8 slots.
+__global__ __launch_bounds__(256) void k_x3_split_w(const float* __restrict__ W, int64_t ldw,
+                                                    int N, int K, uint16_t* __restrict__ out,
+                                                    int64_t ldo) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (row, 32-k block, group g)
+  const int nb = K / 32;
+  if (e >= (int64_t)N * nb * 4) return;
+  const int g = (int)(e & 3), kb = (int)((e >> 2) % nb), n = (int)((e >> 2) / nb);
+  const float* wr = W + (int64_t)n * ldw + 32 * kb;
+  const u32x4 f0 = *(const u32x4*)(wr + 4 * g), f1 = *(const u32x4*)(wr + 16 + 4 * g);
+  bf16x8e hi, lo;
+  split_bf16x8(f0, f1, hi, lo);
+  uint16_t* o = out + (int64_t)n * ldo + 64 * kb + 8 * g;
+  *(u32x4*)o = __builtin_bit_cast(u32x4, hi);
+  *(u32x4*)(o + 32) = __builtin_bit_cast(u32x4, lo);
+}
+
+// X3M = 2: W arrives pre-split (k_x3_split_w): each 32-k stage of a W row is 128 B = 32 hi
+// then 32 lo bf16 in the lanes' slot order, so the W tile's read step 0 / 1 chunks ARE the
+// lane's hi / lo operands -- only A is split in the loop (half the VALU of X3M = 1, which was
+// VALU-bound: 192 VALU beside 48 MFMAs per wave and stage).  W is passed as float* (the same
+// 128-B rows per 32 k), ldw in those 4-B units.
+template <typename T, int X3M = 0>
 __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_t lda,
                                                  const T* __restrict__ W, int64_t ldw,
                                                  const float* __restrict__ bias,
@@ -339,6 +387,33 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_
         av[s][i] = lds_read128<0>(sb + fa[i][s]);
         bv[s][i] = lds_read128<0>(sb + fb[i][s]);
       }
+    if constexpr (X3M != 0) {
+      static_assert(sizeof(T) == 4, "x3: f32 operands");
+      lds_wait<0>();
+      bf16x8e ahi[4], alo[4], bhi[4], blo[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        reg_tie(av[0][i]);
+        reg_tie(av[1][i]);
+        reg_tie(bv[0][i]);
+        reg_tie(bv[1][i]);
+        split_bf16x8(av[0][i], av[1][i], ahi[i], alo[i]);
+        if constexpr (X3M == 2) {
+          bhi[i] = __builtin_bit_cast(bf16x8e, bv[0][i]);
+          blo[i] = __builtin_bit_cast(bf16x8e, bv[1][i]);
+        } else {
+          split_bf16x8(bv[0][i], bv[1][i], bhi[i], blo[i]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bhi[j], ahi[i], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(blo[j], ahi[i], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bhi[j], alo[i], acc[i][j], 0, 0, 0);
+        }
+    } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       if (s == 0) lds_wait<8>();
@@ -364,6 +439,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_
           }
         }
     }
+    }
     enc_lds_barrier();
   }
 
@@ -380,15 +456,19 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_
 // DMA layout / swizzle / fragment reads / epilogue as k_gemm.
 constexpr int GB_BN = 128, GB_MAXN = 2048;
 
-template <int GB_BM, int GB_SLOTS, int ACT, bool BFO>
-__global__ __launch_bounds__(GB_BM * 2, 512 / (GB_BM * 2)) void k_gemm_big(const uint16_t* __restrict__ A, int64_t lda,
-                                                     const uint16_t* __restrict__ W, int64_t ldw,
+// T = float: the split-bf16 (x3) product of k_gemm<float, true> on this ring -- a stage is 32
+// f32 (the same 128-B LDS rows, so DMA, swizzle and fragment reads are unchanged), and the
+// stage's two read steps form one 8-f32 slot set per lane (split_bf16x8, 3 MFMAs per block).
+template <int GB_BM, int GB_SLOTS, int ACT, bool BFO, typename T = uint16_t>
+__global__ __launch_bounds__(GB_BM * 2, 512 / (GB_BM * 2)) void k_gemm_big(const T* __restrict__ A, int64_t lda,
+                                                     const T* __restrict__ W, int64_t ldw,
                                                      const float* __restrict__ bias,
                                                      const float* __restrict__ res, int64_t ldr,
                                                      float* __restrict__ C, int64_t ldc,
                                                      uint16_t* __restrict__ C16, int64_t ldc16,
                                                      int M, int N, int K, int act) {
-  constexpr int BK = 64, EPC = 8;
+  constexpr bool X3 = sizeof(T) == 4;
+  constexpr int BK = 128 / sizeof(T), EPC = 16 / sizeof(T);
   constexpr int GB_A_B = GB_BM * 128, GB_W_B = GB_BN * 128, GB_STAGE_B = GB_A_B + GB_W_B;
   constexpr int NW = GB_BM / 32;        // waves: (BM / 64) x 2 of 64 x 64
   constexpr int WP = 16 / NW;           // W pieces per wave and stage (A: 4)
@@ -516,6 +596,27 @@ __global__ __launch_bounds__(GB_BM * 2, 512 / (GB_BM * 2)) void k_gemm_big(const
           av[s][i] = lds_read128<0>(sb + fa[i][s]);
           bv[s][i] = lds_read128<0>(sb + fb[i][s]);
         }
+      if constexpr (X3) {
+        lds_wait<0>();
+        bf16x8e ahi[4], alo[4], bhi[4], blo[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          reg_tie(av[0][i]);
+          reg_tie(av[1][i]);
+          reg_tie(bv[0][i]);
+          reg_tie(bv[1][i]);
+          split_bf16x8(av[0][i], av[1][i], ahi[i], alo[i]);
+          split_bf16x8(bv[0][i], bv[1][i], bhi[i], blo[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bhi[j], ahi[i], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(blo[j], ahi[i], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bhi[j], alo[i], acc[i][j], 0, 0, 0);
+          }
+      } else {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         if (s == 0) lds_wait<8>();
@@ -533,9 +634,10 @@ __global__ __launch_bounds__(GB_BM * 2, 512 / (GB_BM * 2)) void k_gemm_big(const
                 __builtin_bit_cast(bf16x8e, bv[s][j]), __builtin_bit_cast(bf16x8e, av[s][i]),
                 acc[i][j], 0, 0, 0);
       }
+      }
     }
     if (TT_GEXP_NOSTORE != 1)
-      nst = gemm_wave_epilogue<true, ACT, BFO>(acc, (lt / n_tn) * GB_BM + 64 * wm, (lt % n_tn) * GB_BN + 64 * wn,
+      nst = gemm_wave_epilogue<!X3, ACT, BFO>(acc, (lt / n_tn) * GB_BM + 64 * wm, (lt % n_tn) * GB_BN + 64 * wn,
                                lane, M, N, bias, res, ldr, C, ldc, C16, ldc16, act,
                                lds_bias ? sbias : nullptr);
     else if (acc[0][0][0] == 123.456f && acc[3][3][3] == 1.5f) C[0] = acc[1][1][1];
@@ -1197,9 +1299,12 @@ __global__ __launch_bounds__(128) void k_attn(const float* __restrict__ qkv, int
 // cross-lane xors.  Keys stream in chunks of 32 with online (rescaled) softmax.
 //   BF = true : v_mfma_f32_16x16x32_bf16 (K, Q, V, P in bf16, f32 accumulate/softmax).
 //   BF = false: v_mfma_f32_16x16x4_f32 (everything f32: the parity path).
+//   X3 (BF = false): the f32 data path, each product on split-bf16 MFMA (split_bf16x8: hi.hi +
+//        lo.hi + hi.lo, 3 v_mfma_f32_16x16x32_bf16 per 8 f32 MFMAs); the 8 k-slots of a lane are
+//        the f32 path's two 4-wide groups (dims 4g.., 16 + 4g.. / keys kc + 4g.., kc + 16 + 4g..).
 // LDS: K [Lk][32] (rows padded to 144 B f32 / 80 B bf16) and V^T [32][vst] (vst = 128k + 4 f32
 // / 128k + 8 bf16 elements): both fragment reads are bank-conflict-free.
-template <bool BF, typename TI>
+template <bool BF, typename TI, bool X3 = false>
 __global__ __launch_bounds__(256) void k_attn32_mfma(const TI* __restrict__ qkv, int64_t ldq,
                                                      const int32_t* __restrict__ cu, int H,
                                                      int heads, float scale,
@@ -1215,9 +1320,37 @@ __global__ __launch_bounds__(256) void k_attn32_mfma(const TI* __restrict__ qkv,
   const int sq = lb / heads, h = lb % heads;
   const int t0 = cu[sq], L = cu[sq + 1] - t0;
   const int Lk = (L + 31) & ~31;
-  const int vst = ((Lk + 127) & ~127) + (BF ? 8 : 4);
+  const int vst = ((Lk + 127) & ~127) + (BF || X3 ? 8 : 4);
   char* Ks = sm;
   char* Vt = sm + (size_t)Lk * KROW;
+  // X3: operands split ONCE here (a K / V element feeds every query tile of the sequence), in
+  // bf16 hi | lo form, with the lane's 8 MFMA k-slots contiguous: dim (key-in-chunk) c sits at
+  // slot 8 ((c & 15) >> 2) + 4 (c >> 4) + (c & 3) -- slots 8g..8g+7 of lane group g are c =
+  // 4g..4g+3, 16+4g..16+4g+3, the f32 path's two groups.  K row: hi[32] then lo[32] (bf16);
+  // V^T: plane hi [32][vst] then plane lo [32][vst] (bf16).
+  uint16_t* Vhi = (uint16_t*)Vt;
+  uint16_t* Vlo = Vhi + (size_t)32 * vst;
+  if constexpr (X3) {
+    for (int e = tid; e < Lk * DH; e += 256) {
+      const int j = e / DH, c = e % DH;
+      float kv = 0.0f, vv = 0.0f;
+      if (j < L) {
+        const TI* row = qkv + (int64_t)(t0 + j) * ldq + h * DH + c;
+        kv = row[H];
+        vv = row[2 * H];
+      }
+      const int sc_ = 8 * ((c & 15) >> 2) + 4 * (c >> 4) + (c & 3);
+      const int jo = j & 31, sj = (j & ~31) + 8 * ((jo & 15) >> 2) + 4 * (jo >> 4) + (jo & 3);
+      const uint16_t kh = f32_to_bf16_rne(kv), vh = f32_to_bf16_rne(vv);
+      const uint16_t kl = f32_to_bf16_rne(kv - __uint_as_float((uint32_t)kh << 16));
+      const uint16_t vl = f32_to_bf16_rne(vv - __uint_as_float((uint32_t)vh << 16));
+      uint16_t* kr = (uint16_t*)(Ks + j * KROW);
+      kr[sc_] = kh;
+      kr[32 + sc_] = kl;
+      Vhi[(size_t)c * vst + sj] = vh;
+      Vlo[(size_t)c * vst + sj] = vl;
+    }
+  } else
   if constexpr (sizeof(TI) == 2) {
     // bf16 input: 16-B chunks (8 dims) of each K / V row -- one global load each (the head's
     // 64-B slice of a token row is 4 chunks); K rows copied whole, V transposed into V^T
@@ -1280,6 +1413,8 @@ __global__ __launch_bounds__(256) void k_attn32_mfma(const TI* __restrict__ qkv,
                  (uint32_t)f32_to_bf16_rne(x1[2]) | ((uint32_t)f32_to_bf16_rne(x1[3]) << 16)};
       qf = __builtin_bit_cast(bf16x8e, u);
     }
+    bf16x8e qhi, qlo;  // X3: the query's split operands
+    if (X3) split_bf16x8(__builtin_bit_cast(u32x4, qa), __builtin_bit_cast(u32x4, qb), qhi, qlo);
     float m = -__builtin_huge_valf(), lsum = 0.0f;
     f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
     for (int kc = 0; kc < Lk; kc += 32) {
@@ -1291,6 +1426,12 @@ __global__ __launch_bounds__(256) void k_attn32_mfma(const TI* __restrict__ qkv,
         if (BF) {
           const u32x4 kf = *(const u32x4*)(kr + 16 * g);
           z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8e, kf), qf, z, 0, 0, 0);
+        } else if (X3) {
+          const bf16x8e khi = __builtin_bit_cast(bf16x8e, *(const u32x4*)(kr + 16 * g));
+          const bf16x8e klo = __builtin_bit_cast(bf16x8e, *(const u32x4*)(kr + 64 + 16 * g));
+          z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(khi, qhi, z, 0, 0, 0);
+          z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(klo, qhi, z, 0, 0, 0);
+          z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(khi, qlo, z, 0, 0, 0);
         } else {  // slot g <-> dim 4g + u (u < 4), 16 + 4g + (u - 4) (u >= 4)
           const f32x4 ka = *(const f32x4*)(kr + 16 * g), kb = *(const f32x4*)(kr + 64 + 16 * g);
 #pragma unroll
@@ -1339,6 +1480,18 @@ __global__ __launch_bounds__(256) void k_attn32_mfma(const TI* __restrict__ qkv,
           u32x4 vu = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
           acc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8e, vu), pf,
                                                             acc[db], 0, 0, 0);
+        }
+      } else if (X3) {  // slots: keys kc + 4g + v (v < 4), kc + 16 + 4g + (v - 4)
+        bf16x8e phi, plo;
+        split_bf16x8(__builtin_bit_cast(u32x4, sc[0]), __builtin_bit_cast(u32x4, sc[1]), phi, plo);
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          const size_t vo = (size_t)(16 * db + ql) * vst + kc + 8 * g;
+          const bf16x8e vhi = __builtin_bit_cast(bf16x8e, *(const u32x4*)(Vhi + vo));
+          const bf16x8e vlo = __builtin_bit_cast(bf16x8e, *(const u32x4*)(Vlo + vo));
+          acc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vhi, phi, acc[db], 0, 0, 0);
+          acc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vlo, phi, acc[db], 0, 0, 0);
+          acc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vhi, plo, acc[db], 0, 0, 0);
         }
       } else {  // per 16-key block b and v: slot g <-> key kc + 16b + 4g + v
 #pragma unroll
@@ -1510,9 +1663,10 @@ __global__ __launch_bounds__(256 * HG) void k_attn32_bf16(
   }
 }
 
-size_t attn32_smem(int max_len, bool bf) {
+size_t attn32_smem(int max_len, bool bf, bool x3 = false) {
   const int Lk = (max_len + 31) & ~31;
-  const int vst = ((Lk + 127) & ~127) + (bf ? 8 : 4);
+  const int vst = ((Lk + 127) & ~127) + (bf || x3 ? 8 : 4);
+  // x3: K rows hi | lo (bf16, 144 B like f32), V^T as two bf16 planes (hi, lo)
   return (size_t)Lk * (32 * (bf ? 2 : 4) + 16) + (size_t)32 * vst * (bf ? 2 : 4);
 }
 
@@ -1595,10 +1749,26 @@ int gemm_big_variant() {  // TT_GEMM_BIG: 0 = 128x128 tiles only, 1 = 256x128 ri
 }
 }  // namespace
 
-extern "C" int tt_gemm_f32(const float* A, int64_t lda, const float* W, int64_t ldw,
-                           const float* bias, const float* residual, int64_t ldr, float* C,
-                           int64_t ldc, uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N,
-                           int32_t K, int32_t act, void* stream) {
+// x3 GEMMs take the persistent ring kernel from this many 256x128 tiles (TT_X3_BIG_MIN=d,
+// timing builds: d quarter-rounds of tiles per CU; 0 = never)
+// (default 0: the ring kernel measured slower for x3 -- 84.7 vs 76.2 us mean per GEMM over the
+// configs[1] encode; its 8 waves' on-the-fly splits are VALU-bound the same way)
+static int x3_big_min_tiles(int ncu) {
+  static const int d = env_switch("TT_X3_BIG_MIN", 0);
+  return d == 0 ? 1 << 30 : ncu * d / 4;
+}
+
+static int gemm_f32_impl(const float* A, int64_t lda, const float* W, int64_t ldw,
+                         const float* bias, const float* residual, int64_t ldr, float* C,
+                         int64_t ldc, uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N,
+                         int32_t K, int32_t act, void* stream, bool x3,
+                         const uint16_t* wx3 = nullptr, int64_t ldwx3 = 0) {
+  if (wx3) {  // pre-split W (k_x3_split_w): the same 128-B rows per 32 k, as float units
+    TT_REQUIRE(x3 && ldwx3 % 8 == 0 && ((uintptr_t)wx3 % 16) == 0,
+               "pre-split W: 16-B aligned rows, ld % 8 == 0");
+    W = (const float*)wx3;
+    ldw = ldwx3 / 2;
+  }
   TT_REQUIRE(M >= 0 && N >= 0 && K >= 0, "negative size");
   if (M == 0 || N == 0) return TT_OK;
   if (K % GemmElt<float>::BK != 0)
@@ -1608,9 +1778,65 @@ extern "C" int tt_gemm_f32(const float* A, int64_t lda, const float* W, int64_t 
              "A/W must be 16-B aligned with lda, ldw % 4 == 0");
   TT_REQUIRE(act >= 0 && act <= 2, "bad activation");
   const int nblk = ((M + GM_BM - 1) / GM_BM) * ((N + GM_BN - 1) / GM_BN);
-  hipLaunchKernelGGL(k_gemm<float>, dim3(nblk), dim3(256), 0, (hipStream_t)stream, A, lda, W, ldw,
-                     bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
-  return check_launch("tt_gemm_f32");
+  const int nbig = ((M + 255) / 256) * ((N + GB_BN - 1) / GB_BN), ncu = enc_device_cus();
+  if (x3 && !wx3 && nbig >= x3_big_min_tiles(ncu)) {
+    // the persistent 256x128 ring (3 slots, two stages ahead, one barrier per stage): the
+    // 128x128 two-stage kernel left the MFMA pipes ~75% idle on DMA latency
+    hipLaunchKernelGGL((k_gemm_big<256, 3, -1, false, float>), dim3(ncu), dim3(512), 0,
+                       (hipStream_t)stream, A, lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16,
+                       ldc16, M, N, K, act);
+    return check_launch("tt_gemm_x3(persistent)");
+  }
+  if (wx3)
+    hipLaunchKernelGGL((k_gemm<float, 2>), dim3(nblk), dim3(256), 0, (hipStream_t)stream, A,
+                       lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
+  else if (x3)
+    hipLaunchKernelGGL((k_gemm<float, 1>), dim3(nblk), dim3(256), 0, (hipStream_t)stream, A,
+                       lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
+  else
+    hipLaunchKernelGGL((k_gemm<float, 0>), dim3(nblk), dim3(256), 0, (hipStream_t)stream, A,
+                       lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
+  return check_launch(wx3 ? "tt_gemm_x3w" : x3 ? "tt_gemm_x3" : "tt_gemm_f32");
+}
+
+extern "C" int tt_gemm_f32(const float* A, int64_t lda, const float* W, int64_t ldw,
+                           const float* bias, const float* residual, int64_t ldr, float* C,
+                           int64_t ldc, uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N,
+                           int32_t K, int32_t act, void* stream) {
+  return gemm_f32_impl(A, lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act,
+                       stream, false);
+}
+
+extern "C" int tt_gemm_x3(const float* A, int64_t lda, const float* W, int64_t ldw,
+                          const float* bias, const float* residual, int64_t ldr, float* C,
+                          int64_t ldc, uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N,
+                          int32_t K, int32_t act, void* stream) {
+  return gemm_f32_impl(A, lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act,
+                       stream, true);
+}
+
+extern "C" int tt_x3_split_weights(const float* W, int64_t ldw, int32_t N, int32_t K,
+                                   uint16_t* out, int64_t ld_out, void* stream) {
+  TT_REQUIRE(N >= 0 && K >= 0, "negative size");
+  if (N == 0 || K == 0) return TT_OK;
+  if (K % 32 != 0) return fail(TT_ERR_UNSUPPORTED, "tt_x3_split_weights: need K % 32 == 0");
+  TT_REQUIRE(W && out, "null pointer");
+  TT_REQUIRE(ldw % 4 == 0 && ((uintptr_t)W % 16) == 0 && ld_out % 8 == 0 &&
+                 ((uintptr_t)out % 16) == 0 && ld_out >= 2 * (int64_t)K,
+             "W 16-B aligned rows (ldw % 4 == 0); out [N, >= 2K] 16-B aligned (ld % 8 == 0)");
+  const int64_t n = (int64_t)N * (K / 32) * 4;
+  hipLaunchKernelGGL(k_x3_split_w, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, W, ldw, N, K, out, ld_out);
+  return check_launch("tt_x3_split_weights");
+}
+
+extern "C" int tt_gemm_x3w(const float* A, int64_t lda, const uint16_t* Wx3, int64_t ldwx3,
+                           const float* bias, const float* residual, int64_t ldr, float* C,
+                           int64_t ldc, uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N,
+                           int32_t K, int32_t act, void* stream) {
+  TT_REQUIRE(Wx3 != nullptr, "null pointer");
+  return gemm_f32_impl(A, lda, nullptr, 0, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K,
+                       act, stream, true, Wx3, ldwx3);
 }
 
 extern "C" int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
@@ -1664,7 +1890,7 @@ extern "C" int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, i
     return launch(k_gemm_big<256, 3, -1, false>, ncu, 512);
   }
   const int nblk = ((M + GM_BM - 1) / GM_BM) * ((N + GM_BN - 1) / GM_BN);
-  hipLaunchKernelGGL(k_gemm<uint16_t>, dim3(nblk), dim3(256), 0, (hipStream_t)stream, A, lda, W,
+  hipLaunchKernelGGL((k_gemm<uint16_t, 0>), dim3(nblk), dim3(256), 0, (hipStream_t)stream, A, lda, W,
                      ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
   return check_launch("tt_gemm_bf16");
 }
@@ -1717,7 +1943,8 @@ extern "C" int tt_attention_varlen(const float* qkv, int64_t ld_qkv, const int32
                                    int32_t prec, float* out, int64_t ld_out, uint16_t* out_bf16,
                                    void* stream) {
   TT_REQUIRE(n_seq >= 0 && heads >= 1 && H % heads == 0, "bad n_seq / heads");
-  TT_REQUIRE(prec == TT_PREC_F32 || prec == TT_PREC_BF16, "bad precision");
+  TT_REQUIRE(prec == TT_PREC_F32 || prec == TT_PREC_BF16 || prec == TT_PREC_X3,
+             "bad precision");
   if (n_seq == 0) return TT_OK;
   TT_REQUIRE(max_len >= 1 && max_len <= 512, "max_len must be in [1, 512]");
   TT_REQUIRE(qkv && cu_seqlens && out, "null pointer");
@@ -1725,9 +1952,11 @@ extern "C" int tt_attention_varlen(const float* qkv, int64_t ld_qkv, const int32
                  ((uintptr_t)out % 16) == 0, "qkv/out must be 16-B aligned rows");
   if (H / heads != 32)
     return fail(TT_ERR_UNSUPPORTED, "tt_attention_varlen: MFMA path needs head dim 32");
-  const bool bf = prec == TT_PREC_BF16;
-  const size_t smem = attn32_smem(max_len, bf);
-  const void* fn = bf ? (const void*)k_attn32_mfma<true, float> : (const void*)k_attn32_mfma<false, float>;
+  const bool bf = prec == TT_PREC_BF16, x3 = prec == TT_PREC_X3;
+  const size_t smem = attn32_smem(max_len, bf, x3);
+  const void* fn = bf   ? (const void*)k_attn32_mfma<true, float>
+                   : x3 ? (const void*)k_attn32_mfma<false, float, true>
+                        : (const void*)k_attn32_mfma<false, float>;
   if (smem > 64 * 1024 &&
       hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "hipFuncSetAttribute(max dynamic LDS)");
@@ -1736,6 +1965,10 @@ extern "C" int tt_attention_varlen(const float* qkv, int64_t ld_qkv, const int32
   if (bf)
     hipLaunchKernelGGL((k_attn32_mfma<true, float>), grid, dim3(256), smem, (hipStream_t)stream, qkv,
                        ld_qkv, cu_seqlens, H, heads, scale, out, ld_out, out_bf16);
+  else if (x3)
+    hipLaunchKernelGGL((k_attn32_mfma<false, float, true>), grid, dim3(256), smem,
+                       (hipStream_t)stream, qkv, ld_qkv, cu_seqlens, H, heads, scale, out, ld_out,
+                       out_bf16);
   else
     hipLaunchKernelGGL((k_attn32_mfma<false, float>), grid, dim3(256), smem, (hipStream_t)stream, qkv,
                        ld_qkv, cu_seqlens, H, heads, scale, out, ld_out, out_bf16);
@@ -1865,13 +2098,21 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
                               float* out_pooled, int64_t ld_out, void* workspace,
                               int64_t workspace_bytes, void* stream) {
   TT_REQUIRE(m != nullptr, "model == NULL");
-  TT_REQUIRE(prec == TT_PREC_F32 || prec == TT_PREC_BF16, "bad precision");
+  TT_REQUIRE(prec == TT_PREC_F32 || prec == TT_PREC_BF16 || prec == TT_PREC_X3,
+             "bad precision");
   TT_REQUIRE(n_seq >= 0 && T >= n_seq, "need T >= n_seq >= 0 (no empty sequences)");
   if (n_seq == 0) return TT_OK;
   const int H = m->hidden, I = m->intermediate, NL = m->layers;
   TT_REQUIRE(H > 0 && H <= 1024 && I > 0 && NL >= 0 && m->heads > 0, "bad model dims");
   TT_REQUIRE(max_len <= m->max_positions, "max_len > max_position_embeddings");
-  const bool bf = prec == TT_PREC_BF16;
+  const bool bf = prec == TT_PREC_BF16, x3 = prec == TT_PREC_X3;
+  // the f32 path's GEMMs: f32 MFMA, or split-bf16 (x3) on the same f32 operands
+  auto gemm32 = [&](const float* A, int64_t lda, const float* W, int64_t ldw, const float* bias,
+                    const float* res, int64_t ldr, float* C, int64_t ldc, int32_t M, int32_t N,
+                    int32_t K, int32_t act, const uint16_t* wx3) {
+    return gemm_f32_impl(A, lda, W, ldw, bias, res, ldr, C, ldc, nullptr, 0, M, N, K, act,
+                         stream, x3, x3 ? wx3 : nullptr, 2 * (int64_t)K);
+  };
   // bf16 path at H = 384 with row tiles filling the chip: GEMM + LayerNorm fused (k_gemm_ln)
   const bool fuse_ln = bf && H == GL_H && I % 64 == 0 && !gemm_ln_disabled();
   EncWs w = enc_carve((char*)workspace, T, H, I, bf);
@@ -1892,8 +2133,8 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
     // Q|K|V = x Wqkv^T + b
     rc = bf ? tt_gemm_bf16(w.x16, H, L.wqkv_bf16, H, L.bqkv, nullptr, 0, nullptr, 3 * H, w.qkv16,
                            3 * H, (int)T, 3 * H, H, ACT_NONE, stream)
-            : tt_gemm_f32(w.x, H, L.wqkv, H, L.bqkv, nullptr, 0, w.qkv, 3 * H, nullptr, 0, (int)T,
-                          3 * H, H, ACT_NONE, stream);
+            : gemm32(w.x, H, L.wqkv, H, L.bqkv, nullptr, 0, w.qkv, 3 * H, (int)T, 3 * H, H,
+                     ACT_NONE, L.wqkv_x3);
     if (rc) return rc;
     if (bf && H / m->heads == 32)
       rc = tt_attention_varlen_bf16(w.qkv16, 3 * H, cu_seqlens, n_seq, max_len, H, m->heads,
@@ -1901,8 +2142,8 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
     else if (bf)
       return fail(TT_ERR_UNSUPPORTED, "tt_bert_encode: bf16 path needs head dim 32");
     else if (H / m->heads == 32)
-      rc = tt_attention_varlen(w.qkv, 3 * H, cu_seqlens, n_seq, max_len, H, m->heads, prec, w.ctx,
-                               H, nullptr, stream);
+      rc = tt_attention_varlen(w.qkv, 3 * H, cu_seqlens, n_seq, max_len, H, m->heads,
+                               x3 ? TT_PREC_X3 : TT_PREC_F32, w.ctx, H, nullptr, stream);
     else
       rc = tt_attention_varlen_f32(w.qkv, 3 * H, cu_seqlens, n_seq, max_len, H, m->heads, w.ctx,
                                    H, nullptr, stream);
@@ -1915,8 +2156,7 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
     } else {
       rc = bf ? tt_gemm_bf16(w.ctx16, H, L.wo_bf16, H, L.bo, w.x, H, w.y, H, nullptr, 0, (int)T, H,
                              H, ACT_NONE, stream)
-              : tt_gemm_f32(w.ctx, H, L.wo, H, L.bo, w.x, H, w.y, H, nullptr, 0, (int)T, H, H,
-                            ACT_NONE, stream);
+              : gemm32(w.ctx, H, L.wo, H, L.bo, w.x, H, w.y, H, (int)T, H, H, ACT_NONE, L.wo_x3);
       if (rc) return rc;
       rc = tt_layernorm_f32(w.y, H, L.ln1_g, L.ln1_b, m->ln_eps, w.x, H, bf ? w.x16 : nullptr, H,
                             T, H, stream);
@@ -1925,8 +2165,7 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
     // ff = GELU(x W1^T + b1) ; y = ff W2^T + b2 + x ; x = LN(y)
     rc = bf ? tt_gemm_bf16(w.x16, H, L.w1_bf16, H, L.b1, nullptr, 0, nullptr, I, w.ff16, I, (int)T,
                            I, H, ACT_GELU, stream)
-            : tt_gemm_f32(w.x, H, L.w1, H, L.b1, nullptr, 0, w.ff, I, nullptr, 0, (int)T, I, H,
-                          ACT_GELU, stream);
+            : gemm32(w.x, H, L.w1, H, L.b1, nullptr, 0, w.ff, I, (int)T, I, H, ACT_GELU, L.w1_x3);
     if (rc) return rc;
     if (fuse_ln) {
       rc = tt_gemm_ln_bf16(w.ff16, I, L.w2_bf16, I, L.b2, L.ln2_g, L.ln2_b, m->ln_eps, w.x, H,
@@ -1935,8 +2174,7 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
     } else {
       rc = bf ? tt_gemm_bf16(w.ff16, I, L.w2_bf16, I, L.b2, w.x, H, w.y, H, nullptr, 0, (int)T, H,
                              I, ACT_NONE, stream)
-              : tt_gemm_f32(w.ff, I, L.w2, I, L.b2, w.x, H, w.y, H, nullptr, 0, (int)T, H, I,
-                            ACT_NONE, stream);
+              : gemm32(w.ff, I, L.w2, I, L.b2, w.x, H, w.y, H, (int)T, H, I, ACT_NONE, L.w2_x3);
       if (rc) return rc;
       rc = tt_layernorm_f32(w.y, H, L.ln2_g, L.ln2_b, m->ln_eps, w.x, H, bf ? w.x16 : nullptr, H,
                             T, H, stream);

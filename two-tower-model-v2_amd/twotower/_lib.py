@@ -34,6 +34,7 @@ _i32 = ctypes.c_int32
 
 TT_PREC_F32 = 0
 TT_PREC_BF16 = 1
+TT_PREC_X3 = 2  # f32 operands, split-bf16 (hi + lo) MFMA products
 TT_ACT_NONE, TT_ACT_GELU, TT_ACT_RELU = 0, 1, 2
 
 
@@ -41,7 +42,7 @@ class BertLayer(ctypes.Structure):
     """tt_bert_layer (include/twotower_hip.h): device pointers of one BertLayer."""
     _fields_ = [(n, _vp) for n in (
         "wqkv", "bqkv", "wo", "bo", "ln1_g", "ln1_b", "w1", "b1", "w2", "b2", "ln2_g", "ln2_b",
-        "wqkv_bf16", "wo_bf16", "w1_bf16", "w2_bf16")]
+        "wqkv_bf16", "wo_bf16", "w1_bf16", "w2_bf16", "wqkv_x3", "wo_x3", "w1_x3", "w2_x3")]
 
 
 class BertModel(ctypes.Structure):
@@ -98,6 +99,11 @@ SIGNATURES = {
                                       _vp, _i64, _vp, _i64, _vp]),
     "tt_gemm_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64,
                                    _i32, _i32, _i32, _i32, _vp]),
+    "tt_gemm_x3": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64,
+                                  _i32, _i32, _i32, _i32, _vp]),
+    "tt_gemm_x3w": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64,
+                                   _i32, _i32, _i32, _i32, _vp]),
+    "tt_x3_split_weights": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp]),
     "tt_gemm_bf16": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64,
                                     _i32, _i32, _i32, _i32, _vp]),
     "tt_gemm_ln_bf16": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, ctypes.c_float, _vp,

@@ -84,16 +84,29 @@ def pack_sequences(seqs: Sequence[Sequence[int]], device=None):
             max(lens) if lens else 0)
 
 
+def x3_split_weights(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] f32 (device) -> the x3 GEMM's pre-split image [N, 2K] bf16 (tt_x3_split_weights)."""
+    N, K = w.shape
+    out = torch.empty((N, 2 * K), dtype=torch.bfloat16, device=w.device)
+    check(lib().tt_x3_split_weights(w.data_ptr(), w.stride(0), N, K, out.data_ptr(), out.stride(0),
+                                    stream_ptr()), "tt_x3_split_weights")
+    return out
+
+
 class BertEncoder:
     """Device-resident BertModel weights + the fused HIP forward (tt_bert_encode).
 
-    ``prec`` "f32": every GEMM on f32 MFMA (parity path); "bf16": GEMMs on bf16 MFMA with f32
-    accumulation and f32 residual stream / LayerNorm / softmax / pooling (throughput path)."""
+    ``prec`` "f32": every GEMM on f32 MFMA (parity path); "x3": the f32 path with each GEMM's
+    f32 operands split on the fly into bf16 hi + lo, products as three bf16 MFMAs (the parity
+    precision class at bf16 MFMA rates); "bf16": GEMMs on bf16 MFMA with f32 accumulation and
+    f32 residual stream / LayerNorm / softmax / pooling (throughput path)."""
+
+    _PREC = {"f32": _lib.TT_PREC_F32, "bf16": _lib.TT_PREC_BF16, "x3": _lib.TT_PREC_X3}
 
     def __init__(self, state_dict: Dict[str, torch.Tensor], cfg: Dict = MINILM_L12,
                  device=None, prec: str = "bf16"):
-        if prec not in ("f32", "bf16"):
-            raise ValueError("prec must be 'f32' or 'bf16'")
+        if prec not in self._PREC:
+            raise ValueError("prec must be 'f32', 'x3' or 'bf16'")
         self.cfg = dict(cfg)
         self.prec = prec
         self.device = device or _lib.device()
@@ -134,6 +147,9 @@ class BertEncoder:
             L.w2, L.b2 = ptr(w2), ptr(t(p + "output.dense.bias"))
             L.ln2_g = ptr(t(p + "output.LayerNorm.weight"))
             L.ln2_b = ptr(t(p + "output.LayerNorm.bias"))
+            if prec == "x3":  # the weights' hi / lo split once (tt_x3_split_weights)
+                L.wqkv_x3, L.wo_x3, L.w1_x3, L.w2_x3 = (ptr(x3_split_weights(x))
+                                                        for x in (wqkv, wo, w1, w2))
             if prec == "bf16":
                 L.wqkv_bf16 = ptr(wqkv.to(torch.bfloat16))
                 L.wo_bf16 = ptr(wo.to(torch.bfloat16))
@@ -151,8 +167,7 @@ class BertEncoder:
     def workspace_bytes(self, T: int) -> int:
         b = ctypes.c_int64(0)
         check(lib().tt_bert_workspace_bytes(T, self.hidden, self.cfg["intermediate"],
-                                            _lib.TT_PREC_BF16 if self.prec == "bf16" else
-                                            _lib.TT_PREC_F32, ctypes.byref(b)),
+                                            self._PREC[self.prec], ctypes.byref(b)),
               "tt_bert_workspace_bytes")
         return b.value
 
@@ -175,8 +190,7 @@ class BertEncoder:
             ws = self._ws[st] = torch.empty(need, dtype=torch.uint8, device=ids.device)
         check(lib().tt_bert_encode(ctypes.byref(self._model), ids.data_ptr(),
                                    cu_seqlens.data_ptr(), n, T, int(max_len),
-                                   _lib.TT_PREC_BF16 if self.prec == "bf16" else _lib.TT_PREC_F32,
-                                   out.data_ptr(), out.stride(0), ws.data_ptr(), ws.numel(), st),
+                                   self._PREC[self.prec], out.data_ptr(), out.stride(0), ws.data_ptr(), ws.numel(), st),
               "tt_bert_encode")
         return out
 
