@@ -59,7 +59,7 @@ def parse():
     p.add_argument("--cpu-batch", type=int, default=512, help="per repetition (median of 5)")
     p.add_argument("--mode-a-buyers", type=int, default=256,
                    help="Mode A sample per rank (history texts re-encoded); 0 disables")
-    p.add_argument("--mode-a-prec", choices=["bf16", "f32"], default="bf16")
+    p.add_argument("--mode-a-prec", choices=["bf16", "x3", "f32"], default="bf16")
     p.add_argument("--mode-a-steps", type=int, default=3)
     p.add_argument("--no-extra", action="store_true",
                    help="skip the configs[1] leg, the batch sweep and the f32 Mode A leg")
@@ -777,10 +777,13 @@ def main():
     if world == 1 and not a.no_extra:
         result["batch_sweep"] = batch_sweep(a, shard, shard16, hi - lo, E, K, bounds, dev)
         if a.mode_a_buyers > 0 and a.mode_a_prec == "bf16":
-            a32 = argparse.Namespace(**vars(a))
-            a32.mode_a_prec, a32.mode_a_steps = "f32", 1
-            m32, _ = mode_a(a32, dev, world, rank, lambda qall: local_search_k(qall), K, E)
-            result["mode_a_f32"] = m32
+            # Mode A at the parity precision class: the split-bf16 (x3) encoder, and one step
+            # of the f32 MFMA encoder beside it
+            for prec, steps in (("x3", a.mode_a_steps), ("f32", 1)):
+                a32 = argparse.Namespace(**vars(a))
+                a32.mode_a_prec, a32.mode_a_steps = prec, steps
+                m32, _ = mode_a(a32, dev, world, rank, lambda qall: local_search_k(qall), K, E)
+                result[f"mode_a_{prec}"] = m32
         result["configs1"] = configs1(a, dev, rank)
         torch.cuda.empty_cache()
         result["catalog_10m"] = catalog_10m(a, dev)

@@ -7,11 +7,11 @@ mkdir -p ../lib/variants ../build/variants
 rm -f ../lib/variants/lib_*.so
 for v in $VARIANTS; do
   name=${v%%:*}; defs=${v#*:}; defs=${defs//,/ }
-  for f in tt_filter tt_encoder; do
+  for f in ${EXP_FILES:-tt_filter tt_encoder tt_scan}; do
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -DTT_TIMING_BUILD $defs -x hip -c $f.hip -o ../build/variants/${f}_$name.o 2>/dev/null &
   done
   wait
-  others=$(ls ../build/*.o | grep -v "tt_filter\|tt_encoder")
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $others ../build/variants/tt_filter_$name.o ../build/variants/tt_encoder_$name.o -o ../lib/variants/lib_$name.so
+  others=$(ls ../build/*.o | grep -v "tt_filter\|tt_encoder\|tt_scan")
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $others ../build/variants/tt_filter_$name.o ../build/variants/tt_encoder_$name.o ../build/variants/tt_scan_$name.o -o ../lib/variants/lib_$name.so
 done
 ls ../lib/variants

@@ -464,13 +464,13 @@ static bool wide_k(int k) { return k > CfgNarrow::kKMax; }
 
 static int qpb_of(int k) { return wide_k(k) ? CfgWide::kQPB : CfgNarrow::kQPB; }
 
-static ScanPlan plan_scan(int64_t n, int nq, int k) {
+static ScanPlan plan_scan(int64_t n, int nq, int k, int par = 512) {
   ScanPlan p;
   const int qpb = qpb_of(k);
   p.qt = (nq + qpb - 1) / qpb;
-  // enough blocks to fill 256 CUs x 2, slabs no longer than SC_MAX_SLAB_ROWS
+  // enough blocks to fill 256 CUs x 2 (par), slabs no longer than SC_MAX_SLAB_ROWS
   int64_t s_min = (n + SC_MAX_SLAB_ROWS - 1) / SC_MAX_SLAB_ROWS;
-  int64_t s_par = (512 + p.qt - 1) / p.qt;
+  int64_t s_par = (par + p.qt - 1) / p.qt;
   int64_t s_rows = (n + 511) / 512;  // do not go below ~512 rows per slab
   int64_t s = s_par < s_rows ? s_par : s_rows;
   if (s < s_min) s = s_min;
@@ -532,6 +532,8 @@ static int scan_f32_impl(const float* db, int64_t n, int32_t d, int64_t ld_db,
   tt_scan_workspace_bytes(n, d, nq, k, &need);
   if (workspace_bytes < need || workspace == nullptr)
     return fail(TT_ERR_WORKSPACE, "tt_scan_topk_f32: workspace too small");
+  // (the fused one-tile fallback launched on every small search, usually exiting at once: 256
+  // or 128 instead of 512 slab blocks saved <= 2 us of that idle launch -- not adopted)
   const ScanPlan p = plan_scan(n, nq, k);
   const int64_t entries = (int64_t)nq * p.n_slabs * k;
   float* ws_s = (float*)workspace;

@@ -61,10 +61,11 @@ class EmbeddingEncoder:
 
     def __init__(self, model_path: Optional[str], config_path: Optional[str] = "configs/config.yaml",
                  device: Optional[str] = None, model: Optional[TwoTowerModel] = None,
-                 tokenizer=None, prec: str = "f32", text_encoder=None):
+                 tokenizer=None, prec: str = "x3", text_encoder=None):
         """reference :18-43.  ``config_path=None`` uses the reference's shipped config;
         ``model`` skips the checkpoint (an already-built TwoTowerModel); ``prec`` is the text
-        encoder's GEMM precision ("f32" = parity mode, "bf16" = throughput mode);
+        encoder's GEMM precision: "x3" (default: split-bf16 products, the f32 fixture tolerance
+        at 2x the f32 MFMA path's throughput), "f32" (f32 MFMA), "bf16" (throughput mode);
         ``text_encoder`` replaces the HIP MiniLM (any object with the SentenceTransformer
         surface ItemTower uses: ``encode``, ``get_sentence_embedding_dimension``)."""
         self.config = (load_config(config_path) if config_path is not None
@@ -81,7 +82,7 @@ class EmbeddingEncoder:
         self._table_rows: Optional[Dict[str, int]] = None
 
     # reference :45-130
-    def _load_model(self, model_path: str, tokenizer=None, prec: str = "f32",
+    def _load_model(self, model_path: str, tokenizer=None, prec: str = "x3",
                     text_encoder=None) -> TwoTowerModel:
         checkpoint = torch.load(model_path, map_location="cpu", weights_only=True)
         model_config = (checkpoint["config"]["model"] if "config" in checkpoint
