@@ -105,7 +105,7 @@ __device__ void merge_lists_block(uint64_t* buf, int& bcnt, uint32_t& th_key, in
                                   const int* __restrict__ in_c, int n_lists,
                                   int64_t list_stride_q, int64_t list_stride_l, int k_in, int k,
                                   int64_t row_base, float* out_s, int64_t* out_i,
-                                  const int* qsel);
+                                  const int* qsel, uint32_t thk_min = 0u);
 constexpr int MG_CAP = 8192;
 
 // Scan one (query tile, row slab) work item: query slots [qbase, qbase + kQPB) of [0, nq)
@@ -263,6 +263,7 @@ __global__ __launch_bounds__(64 * Cfg::kWaves, ((EP <= 384 && Cfg::kWaves > 1) ?
 // the batch plan (1.43-1.48 ms for 3 flagged queries of a 10k batch at 1M rows, round 2).
 // Blocks walk the items grid-stride; k_merge_fallback merges each slot's slab lists.
 constexpr int FB_GRID = 2048;  // one-wave blocks: 8 per CU (18.5 KB LDS each)
+constexpr int FB_MERGE_GRID = 256;  // k_merge_fallback blocks
 using CfgFb = ScanCfg<1, 192, 256>;
 struct FbPlan {
   int tiles, spt, rows;
@@ -282,6 +283,10 @@ __host__ __device__ inline FbPlan fb_plan(int64_t n, int nflag) {
   p.spt = (int)((n + r - 1) / r);
   return p;
 }
+// the split merge's partial lists (FB_MERGE_GRID x k of (f32 score, i64 row)) + counters
+static int64_t fb_merge_bytes(int k) {
+  return (int64_t)FB_MERGE_GRID * k * 12 + FB_MERGE_GRID * 4 + 256;
+}
 // list entries (of k) the fallback of up to nq flagged queries may write
 static int64_t fb_items_max(int64_t n, int nq) {
   const int64_t tmax = (nq + SC_QPW - 1) / SC_QPW;
@@ -294,10 +299,13 @@ template <int EP>
 __global__ __launch_bounds__(64, 2) void k_scan_fallback(
     const float* __restrict__ db, int64_t n, int64_t ld_db, const float* __restrict__ q,
     int64_t ld_q, int k, const int* __restrict__ qsel, const int* __restrict__ qsel_n,
-    float* __restrict__ ws_score, int* __restrict__ ws_row, int* __restrict__ ws_cnt) {
+    float* __restrict__ ws_score, int* __restrict__ ws_row, int* __restrict__ ws_cnt,
+    int* __restrict__ mg_done) {
   __shared__ __attribute__((aligned(16))) typename CfgFb::Smem sm;
   const int nq = *qsel_n;
   if (nq == 0) return;
+  if (blockIdx.x == 0)  // the merge's per-slot arrival counters (k_merge_fallback)
+    for (int i = threadIdx.x; i < FB_MERGE_GRID; i += blockDim.x) mg_done[i] = 0;
   const FbPlan p = fb_plan(n, nq);
   const int items = p.tiles * p.spt;
   for (int it = blockIdx.x; it < items; it += gridDim.x) {
@@ -349,15 +357,15 @@ __device__ void merge_lists_block(uint64_t* buf, int& bcnt, uint32_t& th_key, in
                                   const int* __restrict__ in_c, int n_lists,
                                   int64_t list_stride_q, int64_t list_stride_l, int k_in, int k,
                                   int64_t row_base, float* out_s, int64_t* out_i,
-                                  const int* qsel) {
+                                  const int* qsel, uint32_t thk_min) {
   const int64_t orow = qsel ? qsel[qid] : qid;
   const float* qs = in_s + (int64_t)qid * list_stride_q;
   const IdxT* qix = in_i + (int64_t)qid * list_stride_q;
   const int* qc = in_c ? in_c + (int64_t)qid * n_lists : nullptr;
 
-  if (threadIdx.x == 0) { bcnt = 0; th_key = 0u; }
+  if (threadIdx.x == 0) { bcnt = 0; th_key = thk_min; }
   __syncthreads();
-  // threshold from full lists
+  // threshold from full lists (or a caller's sound lower bound of the k-th best: thk_min)
   uint32_t tk = 0u;
   if (k <= k_in) {
     for (int j = threadIdx.x; j < n_lists; j += blockDim.x) {
@@ -438,21 +446,70 @@ __global__ __launch_bounds__(256) void k_merge_lists(const float* __restrict__ i
 }
 
 // Merge of the adaptive fallback's slab lists: block-strided over the flagged slots.
+// Merge of the adaptive fallback's slab lists.  A few flagged queries get up to ~2000 slabs
+// of k entries each (1953 x 100 at 1M rows): one block per query walked all ~195k entries
+// (+1.17 ms on a 10k batch with 3 flagged queries).  With fewer slots than blocks, each slot
+// gets bps = FB_MERGE_GRID / nq blocks, each merging a contiguous range of its slab lists into
+// a partial top-k (p_s / p_i, global rows); the last block of the slot to arrive (agent-scope
+// counter mg_done[slot], zeroed by k_scan_fallback) merges the bps partial lists.
 __global__ __launch_bounds__(256) void k_merge_fallback(const float* __restrict__ ws_score,
                                                         const int* __restrict__ ws_row,
                                                         const int* __restrict__ ws_cnt, int64_t n,
                                                         int k, int64_t row_base, float* out_s,
                                                         int64_t* out_i, const int* qsel,
-                                                        const int* qsel_n) {
+                                                        const int* qsel_n, float* p_s,
+                                                        int64_t* p_i, int* mg_done) {
   __shared__ uint64_t buf[MG_CAP];
   __shared__ int bcnt;
   __shared__ uint32_t th_key;
+  __shared__ int last;
   const int nq = *qsel_n;
   if (nq == 0) return;
   const int spt = fb_plan(n, nq).spt;
-  for (int slot = blockIdx.x; slot < nq; slot += gridDim.x)
-    merge_lists_block<int>(buf, bcnt, th_key, slot, ws_score, ws_row, ws_cnt, spt,
-                           (int64_t)spt * k, (int64_t)k, k, k, row_base, out_s, out_i, qsel);
+  const int bps = nq < (int)gridDim.x ? (int)gridDim.x / nq : 1;
+  if (bps == 1) {
+    for (int slot = blockIdx.x; slot < nq; slot += gridDim.x)
+      merge_lists_block<int>(buf, bcnt, th_key, slot, ws_score, ws_row, ws_cnt, spt,
+                             (int64_t)spt * k, (int64_t)k, k, k, row_base, out_s, out_i, qsel);
+    return;
+  }
+  const int slot = blockIdx.x / bps, part = blockIdx.x % bps;
+  if (slot >= nq) return;
+  // the slot's threshold over ALL its full lists (the k-th entry of any full list bounds the
+  // k-th best from below): each partial block then keeps only the few entries above it
+  // (with the partial's own lists only, ~k survivors per block had to be sorted)
+  __shared__ uint32_t thk_all;
+  if (threadIdx.x == 0) thk_all = 0u;
+  __syncthreads();
+  {
+    uint32_t tk = 0u;
+    const float* qs = ws_score + (int64_t)slot * spt * k;
+    const int* qr = ws_row + (int64_t)slot * spt * k;
+    const int* qc = ws_cnt + (int64_t)slot * spt;
+    for (int j = threadIdx.x; j < spt; j += blockDim.x)
+      if (qc[j] >= k && qr[(int64_t)j * k + k - 1] >= 0) {
+        const uint32_t fk = float_key(qs[(int64_t)j * k + k - 1]);
+        tk = fk > tk ? fk : tk;
+      }
+    atomicMax(&thk_all, tk);
+  }
+  __syncthreads();
+  const uint32_t thk = thk_all;
+  const int j0 = (int)((int64_t)part * spt / bps), j1 = (int)((int64_t)(part + 1) * spt / bps);
+  const int64_t qo = (int64_t)slot * spt * k + (int64_t)j0 * k;
+  float* ps = p_s + ((int64_t)slot * bps + part) * k;
+  int64_t* pi = p_i + ((int64_t)slot * bps + part) * k;
+  merge_lists_block<int>(buf, bcnt, th_key, 0, ws_score + qo, ws_row + qo,
+                         ws_cnt + (int64_t)slot * spt + j0, j1 - j0, 0, (int64_t)k, k, k, 0,
+                         ps, pi, nullptr, thk);
+  __threadfence();  // this block's partial list visible before it counts itself in
+  if (threadIdx.x == 0) last = atomicAdd(&mg_done[slot], 1) == bps - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();  // the other blocks' partial lists
+  merge_lists_block<int64_t>(buf, bcnt, th_key, slot, p_s + (int64_t)slot * bps * k,
+                             p_i + (int64_t)slot * bps * k, nullptr, bps, 0, (int64_t)k, k, k,
+                             row_base, out_s, out_i, qsel, thk);
 }
 
 // ----------------------------------------------------------------------------- host
@@ -505,7 +562,7 @@ extern "C" int tt_scan_workspace_bytes(int64_t n, int32_t d, int32_t nq, int32_t
   const int64_t entries = (int64_t)nq * p.n_slabs * k;
   int64_t b = entries * 8 + (int64_t)nq * p.n_slabs * 4;
   if (p.qt > 1 && k <= CfgFb::kKMax) {  // the adaptive fallback's lists (the same memory)
-    const int64_t fb = fb_items_max(n, nq) * SC_QPW * (8 * (int64_t)k + 4);
+    const int64_t fb = fb_items_max(n, nq) * SC_QPW * (8 * (int64_t)k + 4) + fb_merge_bytes(k);
     b = b > fb ? b : fb;
   }
   *bytes = (b + 255) / 256 * 256;
@@ -551,10 +608,15 @@ static int scan_f32_impl(const float* db, int64_t n, int32_t d, int64_t ld_db,
     float* fs = (float*)workspace;
     int* fr = (int*)(fs + fb_items_max(n, nq) * SC_QPW * k);
     int* fc = fr + fb_items_max(n, nq) * SC_QPW * k;
+    // the split merge's partials after the lists' counts (8-B aligned), then its counters
+    const int64_t fc_end = (int64_t)((char*)(fc + fb_items_max(n, nq) * SC_QPW) - (char*)workspace);
+    int64_t* pi = (int64_t*)((char*)workspace + (fc_end + 15) / 16 * 16);
+    float* ps = (float*)(pi + (int64_t)FB_MERGE_GRID * k);
+    int* mg = (int*)(ps + (int64_t)FB_MERGE_GRID * k);
 #define TT_FB_CASE(E)                                                                         \
   case E:                                                                                     \
     hipLaunchKernelGGL(k_scan_fallback<E>, dim3(FB_GRID), dim3(64), 0, st, db, n, ld_db, q,   \
-                       ld_q, k, qsel, qsel_n, fs, fr, fc);                                    \
+                       ld_q, k, qsel, qsel_n, fs, fr, fc, mg);                                \
     break;
     switch (ep) {
       TT_FB_CASE(64)
@@ -569,8 +631,8 @@ static int scan_f32_impl(const float* db, int64_t n, int32_t d, int64_t ld_db,
 #undef TT_FB_CASE
     int rc = check_launch("k_scan_fallback");
     if (rc) return rc;
-    hipLaunchKernelGGL(k_merge_fallback, dim3(256), dim3(256), 0, st, fs, fr, fc, n, k, row_base,
-                       out_score, out_idx, qsel, qsel_n);
+    hipLaunchKernelGGL(k_merge_fallback, dim3(FB_MERGE_GRID), dim3(256), 0, st, fs, fr, fc, n, k,
+                       row_base, out_score, out_idx, qsel, qsel_n, ps, pi, mg);
     return check_launch("k_merge_fallback");
   }
   const dim3 grid(p.qt, p.n_slabs);
