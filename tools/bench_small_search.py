@@ -46,6 +46,9 @@ def main():
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--nq", type=int, default=1)
     ap.add_argument("--reps", type=int, default=41)
+    ap.add_argument("--modeb", action="store_true",
+                    help="queries = L2-normalised means of 20 catalog rows (the bench's Mode B "
+                         "buyers) instead of iid")
     a = ap.parse_args()
     N, E, K, NQ = a.catalog, a.dim, a.k, a.nq
     ep = _lib.padded_dim(E)
@@ -56,12 +59,16 @@ def main():
     kernels.l2norm_rows(db, E, 0, out=db, out_bf16=db16)
     bounds = kernels.bf16_image_bounds(db, db16, E).tolist()
     q = torch.zeros((NQ, ep), device="cuda")
-    q[:, :E] = torch.randn((NQ, E), generator=g, device="cuda")
+    if a.modeb:
+        hist = torch.randint(0, N, (NQ, 20), generator=g, device="cuda")
+        q[:, :E] = db[hist, :E].mean(dim=1)
+    else:
+        q[:, :E] = torch.randn((NQ, E), generator=g, device="cuda")
     kernels.l2norm_rows(q, E, 0, out=q)
     stream = torch.cuda.current_stream()
     ws = torch.empty(kernels.filter_workspace_bytes(N, E, NQ, K), dtype=torch.uint8, device="cuda")
     ref = kernels.scan_topk_bf16(db, db16, N, E, q, K, bounds, workspace=ws)
-    res = {"catalog": N, "dim": E, "k": K, "nq": NQ}
+    res = {"catalog": N, "dim": E, "k": K, "nq": NQ, "queries": "modeb" if a.modeb else "iid"}
 
     def wrapper():
         return kernels.scan_topk_bf16(db, db16, N, E, q, K, bounds, workspace=ws)

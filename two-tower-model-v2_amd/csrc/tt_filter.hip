@@ -1382,7 +1382,9 @@ struct SmallLdsT {
   uint64_t key[CAP];   // the query's candidate keys (orderable score << 32 | ~row)
   int wred[SM_WAVES];
   uint32_t wmax[SM_WAVES];
-  int hist[3][256];    // radix select: pass p counts into hist[p % 3] (one barrier per pass)
+  // radix select: pass p counts into hist[p % 3] (one barrier per pass); 512 bins for the
+  // windowed first pass, 256 for the byte passes
+  __attribute__((aligned(16))) int hist[3][512];
 };
 using SmallLds = SmallLdsT<SM_CAP>;
 
@@ -1416,42 +1418,44 @@ __device__ int small_collect(const uint64_t* __restrict__ lists, const int* __re
   return total;
 }
 
-// One radix pass of a block-wide select: key j (act) is counted in bin (0..255, larger bin =
-// larger key); every wave then scans the histogram itself (no pick broadcast): lane l owns
-// bins 255 - 4 l (c0) down to 252 - 4 l (c3), so the inclusive prefix over lanes (DPP) counts
-// the keys in bins >= 252 - 4 l, and F = the first lane reaching r.  Returns the bin holding
-// the r-th largest key; r becomes its rank inside that bin.  `next` (the following pass's
-// histogram) is zeroed before the barrier.  Atomics land at distinct-ish bins (the callers'
-// bin maps spread the keys), so no wave aggregation.
-template <int PER, class BinF>
+// One radix pass of a block-wide select over NB bins (256 or 512): key j (act) is counted
+// in bin (larger bin = larger key); every wave then scans the histogram itself (no pick
+// broadcast): lane l owns the NB/64 bins from NB - 1 - (NB/64) l downwards, so the inclusive
+// prefix over lanes (DPP) counts the keys in bins >= the lane's lowest, and F = the first
+// lane reaching r.  Returns the bin holding the r-th largest key; r becomes its rank inside
+// that bin.  `next` (the following pass's histogram, NB entries) is zeroed before the
+// barrier.  The callers' bin maps spread the keys, so no wave aggregation of the atomics.
+template <int PER, int NB, class BinF>
 __device__ __forceinline__ int radix_pass(int* hist, int* next, BinF binof, int& r) {
+  constexpr int BPL = NB / 64;  // bins per lane
   const int tid = threadIdx.x, lane = tid & 63;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     uint32_t bin;
     if (binof(j, bin)) atomicAdd(&hist[bin], 1);
   }
-  if (next && tid < 256) next[tid] = 0;
+  if (next)
+    for (int i = tid; i < NB; i += blockDim.x) next[i] = 0;
   __syncthreads();
-  const int c0 = hist[255 - 4 * lane], c1 = hist[254 - 4 * lane], c2 = hist[253 - 4 * lane],
-            c3 = hist[252 - 4 * lane];
-  const int mine = c0 + c1 + c2 + c3;
+  int c[BPL];  // c[i] = bin NB - 1 - BPL lane - i
+  const int top = NB - 1 - BPL * lane;
+#pragma unroll
+  for (int i = 0; i < BPL; ++i) c[i] = hist[top - i];
+  int mine = 0;
+#pragma unroll
+  for (int i = 0; i < BPL; ++i) mine += c[i];
   const int incl = wave_incl_sum(mine);
   const int F = __builtin_ctzll(__ballot(incl >= r));
   int above = __builtin_amdgcn_readlane(incl - mine, F);
-  const int f0 = __builtin_amdgcn_readlane(c0, F), f1 = __builtin_amdgcn_readlane(c1, F),
-            f2 = __builtin_amdgcn_readlane(c2, F);
-  int bin = 252 - 4 * F;
-  if (above + f0 >= r) {
-    bin = 255 - 4 * F;
-  } else if (above + f0 + f1 >= r) {
-    bin = 254 - 4 * F;
-    above += f0;
-  } else if (above + f0 + f1 + f2 >= r) {
-    bin = 253 - 4 * F;
-    above += f0 + f1;
-  } else {
-    above += f0 + f1 + f2;
+  int bin = NB - BPL * (F + 1);  // the lane's lowest bin unless found earlier
+#pragma unroll
+  for (int i = 0; i < BPL - 1; ++i) {
+    const int ci = __builtin_amdgcn_readlane(c[i], F);
+    if (above + ci >= r) {
+      bin = NB - 1 - BPL * F - i;
+      break;
+    }
+    above += ci;
   }
   r -= above;
   return bin;
@@ -1461,30 +1465,33 @@ __device__ __forceinline__ int radix_pass(int* hist, int* next, BinF binof, int&
 // select.  Caller guarantees at least R nonzero keys.  ONE barrier per pass; pass p counts
 // into hist[p % 3], zeroed during pass p - 1 (after barrier p - 2, which every reader of that
 // buffer's previous use, pass p - 3, had passed).
-// hmax != 0 (the max nonzero h): a first pass over 16-bit prefixes in a window of 255 below
+// hmax != 0 (the max nonzero h): a first pass over 16-bit prefixes in a window of 511 below
 // hmax's -- the candidates' scores cluster (a fixed top byte puts nearly every key in one or
-// two bins, and serialised same-address atomics), while 255 prefix steps (2^-7 relative each)
-// spread them -- then the low two bytes: 3 passes.  The r-th key outside the window (bin 0 =
-// "255 or more below") -> the plain 4 passes of 8 bits.  (Four passes with wave-aggregated
-// atomics and four barriers each: 5.4 us of the one-buyer final.)
+// two bins, and serialised same-address atomics), while prefix steps (2^-7 relative each, 128
+// per octave) spread them; 511 steps cover 4 octaves of score below the maximum (255 did not
+// cover the bench's Mode B buyer whose best row scores 0.75 and its 100th 0.19: 256 steps,
+// so its select ran the plain 4 passes after the window: 10.2 us; 1023 steps: 4.7 us; 511:
+// 3.1 us, iid 2.9 us) -- then the low two bytes: 3 passes.  The r-th key outside the
+// window (bin 0) -> the plain 4 passes of 8 bits.  (Four passes with wave-aggregated atomics
+// and four barriers each: 5.4 us of the one-buyer final.)
 template <int PER, int CAP>
 __device__ uint32_t small_radix_select(const uint32_t (&h)[PER], int R, SmallLdsT<CAP>& s,
                                        uint32_t hmax = 0u) {
   const int tid = threadIdx.x;
-  if (tid < 256) s.hist[0][tid] = 0;
+  for (int i = tid; i < 512; i += blockDim.x) s.hist[0][i] = 0;
   __syncthreads();
   int r = R, pc = 0, shift = 24;
   uint32_t prefix = 0u, pmask = 0u;
   if (hmax != 0u) {
     const uint32_t top = hmax >> 16;
-    const int b = radix_pass<PER>(s.hist[0], s.hist[1], [&](int j, uint32_t& bin) {
+    const int b = radix_pass<PER, 512>(s.hist[0], s.hist[1], [&](int j, uint32_t& bin) {
       const uint32_t d = top - (h[j] >> 16);
-      bin = 255u - (d < 255u ? d : 255u);
+      bin = 511u - (d < 511u ? d : 511u);
       return h[j] != 0u;
     }, r);
     pc = 1;
     if (b > 0) {
-      prefix = (top - (uint32_t)(255 - b)) << 16;
+      prefix = (top - (uint32_t)(511 - b)) << 16;
       pmask = 0xffff0000u;
       shift = 8;
     } else {
@@ -1493,11 +1500,11 @@ __device__ uint32_t small_radix_select(const uint32_t (&h)[PER], int R, SmallLds
   }
 #pragma unroll 1
   for (; shift >= 0; shift -= 8, ++pc) {
-    const int b = radix_pass<PER>(s.hist[pc % 3], shift > 0 ? s.hist[(pc + 1) % 3] : nullptr,
-                                  [&](int j, uint32_t& bin) {
-                                    bin = (h[j] >> shift) & 255u;
-                                    return h[j] != 0u && (h[j] & pmask) == prefix;
-                                  }, r);
+    const int b = radix_pass<PER, 256>(s.hist[pc % 3], shift > 0 ? s.hist[(pc + 1) % 3] : nullptr,
+                                       [&](int j, uint32_t& bin) {
+                                         bin = (h[j] >> shift) & 255u;
+                                         return h[j] != 0u && (h[j] & pmask) == prefix;
+                                       }, r);
     prefix |= (uint32_t)b << shift;
     pmask |= 0xffu << shift;
   }
@@ -2177,9 +2184,9 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_topm(
   TT_FTS();
 #if TT_EXP_FINAL_TIMING
   if (qid == 0 && tid == 0)
-    printf("final_topm ticks: collect %d select %d band %d rank %d (nb %d)\n",
+    printf("final_topm ticks: collect %d select %d band %d rank %d (nb %d) max %.4f A %.4f n %d\n",
            (int)(ts[1] - ts[0]), (int)(ts[2] - ts[1]), (int)(ts[3] - ts[2]), (int)(ts[4] - ts[3]),
-           nb);
+           nb, key_float(hmax), A, n_keys);
 #endif
 #undef TT_FTS
 }
