@@ -2598,9 +2598,15 @@ static bool tmax_first_disabled() {  // TT_FILTER_TMAX_FIRST=0: full sample ladd
 }
 constexpr int64_t SW_CAP_TILES = SW_CAP - 64;  // first-level tiles per query, with margin
 #ifndef TT_SAMPLE_J_ADD
-#define TT_SAMPLE_J_ADD 12  // J = ceil(k / 8) + TT_SAMPLE_J_ADD (plan_filter)
+// J = ceil(k / 8) + TT_SAMPLE_J_ADD (plan_filter).  A query falls back when the stride-16
+// sample holds >= J of the catalog's top 99 (then a_J(sample) > A_k): at k = 100 that is
+// P(Bin(99, 1/16) >= J) = 1.1e-5 per query at J = 19, 7.1e-7 at 21, 1.5e-9 at 25, i.e.
+// 0.11 / 0.007 / 0.00001 fallbacks per 10k-query step.  A/B x3 on one box (tools/
+// bench_ab.sh): full level 5.48 / 5.53 / 5.57 ms, step 6.65 / 6.70 / 6.75 ms, 0 fallbacks;
+// J = 21 (a fallback costs ~0.47 ms, tt_scan.hip adaptive fallback; 1.4 ms in round 2).
+#define TT_SAMPLE_J_ADD 8
 #endif
-TT_CHECK_EXP(TT_SAMPLE_J_ADD != 12, "TT_SAMPLE_J_ADD");
+TT_CHECK_EXP(TT_SAMPLE_J_ADD != 8, "TT_SAMPLE_J_ADD");
 static int64_t ring_tr(int ep) {                 // rows per k_filter_ring tile
   return ep == 64 ? RingCfg<64>::TR : ep == 128 ? RingCfg<128>::TR : ep == 256 ? RingCfg<256>::TR
          : ep == 384 ? RingCfg<384>::TR : ep == 512 ? RingCfg<512>::TR : RingCfg<768>::TR;
@@ -2648,8 +2654,8 @@ static int64_t ring_slabs(int n_qt, int64_t n_sample, int64_t sl_min = 1) {
 
 static FilterPlan plan_filter_uncached(int64_t n, int nq, int k, int ep) {
   FilterPlan p;
-  // ~16*J full-catalog rows lie above a_J(stride-16 sample); J = k/8 + 12 keeps that count
-  // >= k with ~3.5 sigma margin on iid scores (fewer only under heavy clustering -> fallback)
+  // ~16*J full-catalog rows lie above a_J(stride-16 sample); J = k/8 + 8 keeps that count
+  // >= k except with probability P(Bin(k - 1, 1/16) >= J) (7e-7 at k = 100; TT_SAMPLE_J_ADD)
   p.J = (k + 7) / 8 + TT_SAMPLE_J_ADD;
   if (p.J > k) p.J = k;
   int64_t strides[8];
