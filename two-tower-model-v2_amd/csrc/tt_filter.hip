@@ -203,6 +203,17 @@ template <> struct RingCfg<256> { static constexpr int TR = 32, QB = 2; };
 #ifndef TT_RING_QB4
 #define TT_RING_QB4 0  // 4-wave blocks, 1 per CU, 64 queries per wave (half the LDS reads/flop)
 #endif
+#ifndef TT_RING_W4QB
+// One wave per SIMD (4-wave blocks, 1 per CU, up to 512 registers per lane): the batched full
+// level at E = 384 keeps TT_RING_W4QB 16-query blocks per wave (the other instantiations twice
+// their RingCfg blocks, so every level keeps its queries per block); 0 = two waves per SIMD.
+#define TT_RING_W4QB 0
+#endif
+#ifndef TT_RING_ASM
+// with TT_RING_W4QB: the <384, 1> MFMAs as inline asm with the query fragments (B) pinned in
+// AGPRs (the compiler-scheduled form moves them between AGPRs and VGPRs around every MFMA)
+#define TT_RING_ASM 0
+#endif
 template <> struct RingCfg<384> {
   static constexpr int TR = TT_RING_HALF ? 16 : 32, QB = TT_RING_QB4 ? 4 : 2;
 };
@@ -266,7 +277,8 @@ TT_CHECK_EXP(TT_EXP_NOSEL || TT_EXP_NOWRITE || TT_EXP_MAXONLY ||
                  TT_EXP_SEL_STOP || TT_EXP_SEL_TIMING || TT_EXP_FINAL_STOP ||
                  TT_EXP_FINAL_TIMING || TT_EXP_TM_STATS || TT_EXP_TM_SLOTS != 4,
              "TT_EXP_* (results wrong / printf / untested schedule)");
-TT_CHECK_EXP(TT_RING_HALF || TT_RING_QB4 || TT_EXP_NOIDLE || TT_EXP_PRIO ||
+TT_CHECK_EXP(TT_RING_HALF || TT_RING_QB4 || TT_RING_W4QB || TT_RING_ASM ||
+                 TT_RING_QB_WIDE != 1 || TT_RING_FD_WIDE || TT_EXP_NOIDLE || TT_EXP_PRIO ||
                  TT_RING_NT != 1 || TT_RR_STAGED != 1 || TT_RR_PF != 1 || TT_RR_NT,
              "a non-default ring/re-rank schedule (untested by the GPU suite)");
 #ifndef TT_RING_PD
@@ -274,7 +286,7 @@ TT_CHECK_EXP(TT_RING_HALF || TT_RING_QB4 || TT_EXP_NOIDLE || TT_EXP_PRIO ||
 #define TT_RING_PD 3
 #endif
 TT_CHECK_EXP(TT_RING_PD != 3, "TT_RING_PD");
-constexpr int RG_WAVES = (TT_RING_HALF || TT_RING_QB4) ? 4 : 8, RG_PD = TT_RING_PD,
+constexpr int RG_WAVES = (TT_RING_HALF || TT_RING_QB4 || TT_RING_W4QB) ? 4 : 8, RG_PD = TT_RING_PD,
               RG_SLOTS = RG_PD + 1;  // 3 in flight
 // Pool entries per wave: a query block's scan appends at most 16 x TR <= 512 (16 x 32 rows, all
 // passing); it starts with wn <= RG_WFLUSH, so its writes need no bounds check.
@@ -291,10 +303,19 @@ constexpr int RG_BLOCKS_PER_CU = TT_RING_HALF ? 2 : 1;
 // flight: 1.5x the compute per tile covers the same lead time): 6.26-6.33 -> 5.99-6.02 ms
 // (A/B x2, one box).  Small batches (LVL 2: one-buyer searches are HBM-bound and want 3 tiles
 // in flight) and sample levels keep two blocks per wave.
+#ifndef TT_RING_QB_WIDE
+#define TT_RING_QB_WIDE 1  // query blocks per wave of the batched full level at E = 512 / 768
+#endif
+#ifndef TT_RING_FD_WIDE
+#define TT_RING_FD_WIDE 0  // its fragment read-ahead (0: the generic rule)
+#endif
 template <int EP, int LVL>
 struct RingK {
-  static constexpr int QB = (EP == 384 && LVL == 1 && !TT_RING_HALF && !TT_RING_QB4)
-                                ? 3 : RingCfg<EP>::QB;
+  static constexpr int QB = TT_RING_W4QB ? (EP == 384 && LVL == 1 ? TT_RING_W4QB
+                                                                  : 2 * RingCfg<EP>::QB)
+                            : (EP == 384 && LVL == 1 && !TT_RING_HALF && !TT_RING_QB4)
+                                ? 3
+                            : (EP >= 512 && LVL == 1) ? TT_RING_QB_WIDE : RingCfg<EP>::QB;
   static constexpr int PD = QB == 3 ? 2 : RG_PD;
   static constexpr int SLOTS = PD + 1;
 };
@@ -412,7 +433,8 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   constexpr int PIECES = TILE_B / 1024, PPW = PIECES / RG_WAVES;
   constexpr int FM = (CPR >= 16 ? 16 : CPR) - 1;
   constexpr int RB = TR / 16;
-  constexpr int QSH = QPW <= 16 ? 4 : QPW <= 32 ? 5 : 6;  // pool entry: query bits
+  constexpr bool AMF = TT_RING_W4QB && TT_RING_ASM && EP == 384 && LVL == 1;
+  constexpr int QSH = QPW <= 16 ? 4 : QPW <= 32 ? 5 : QPW <= 64 ? 6 : 7;  // pool entry: query bits
   static_assert((1 << QSH) >= QPW, "queries per wave fit the pool entry's query bits");
   static_assert(PIECES % RG_WAVES == 0, "tile must split into whole 1-KiB pieces per wave");
   __shared__ __attribute__((aligned(16))) char smem[ring_smem<EP, LVL>()];
@@ -661,14 +683,15 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   // FD + 1 divides KS (the ring index is s % (FD + 1)); 2 steps ahead where registers are tight
   // (three query blocks per wave: 6 MFMAs per k-step already cover one step of read-ahead,
   // and the fragment registers of a second step would spill)
-  constexpr int FD = QB >= 3 ? 1 : (EP >= 384 && KS % 3 == 0) ? 2 : (KS >= 4 ? 3 : 1);
+  constexpr int FD = (EP >= 512 && LVL == 1 && TT_RING_FD_WIDE) ? TT_RING_FD_WIDE
+                     : QB >= 3 ? 1 : (EP >= 384 && KS % 3 == 0) ? 2 : (KS >= 4 ? 3 : 1);
   static_assert(RG_SLOTS >= 3, "ring depth");
   constexpr int S_MID = (KS - FD) / 2;
   // Candidate scan of tile t-1 in one piece per query block, spread between tile t's MFMAs:
   // block P at step S0 + P * KS / QB (batched full level 6.81 -> 6.65 ms against all blocks at
   // step 1; S0 = 2 vs 1: 6.72 -> 6.64 ms; finer pieces and other spacings measured slower).
   // Sample levels append their tile maxima at step 1.
-  constexpr int SP = KS / QB;
+  constexpr int SP = KS / QB > 0 ? KS / QB : 1;
   constexpr int S0 = LVL == 0 ? 1
                      : (QB > 1 && 2 + (QB - 1) * SP < KS) ? 2
                      : (QB > 1 && 1 + (QB - 1) * SP < KS) ? 1 : -1;  // -1: every block at step 1
@@ -753,8 +776,20 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
           for (int rb = 0; rb < RB; ++rb) {
             const bf16x8 a = __builtin_bit_cast(bf16x8, fr[s % (FD + 1)][rb]);
 #pragma unroll
-            for (int b = 0; b < QB; ++b)
-              acc[rb][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[b][s], acc[rb][b], 0, 0, 0);
+            for (int b = 0; b < QB; ++b) {
+              if constexpr (AMF) {
+                const u32x4 au = fr[s % (FD + 1)][rb];
+                if constexpr (s == 0)
+                  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0"
+                               : "=&v"(acc[rb][b]) : "v"(au), "a"(qf[b][s]));
+                else
+                  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+                               : "+v"(acc[rb][b]) : "v"(au), "a"(qf[b][s]));
+              } else {
+                acc[rb][b] =
+                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[b][s], acc[rb][b], 0, 0, 0);
+              }
+            }
           }
           if constexpr (s == 0) tile_max(accp, mx);  // VALU between this tile's MFMAs
           if constexpr (s == S_MID) {
@@ -784,6 +819,8 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
               if (mx[b] >= th[b]) asm volatile("" ::: "memory");
           }
         });
+        // (inline-asm MFMAs: the compiler does not see their results' VALU-read hazard)
+        if constexpr (AMF) asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
@@ -2710,8 +2747,8 @@ static FilterPlan plan_filter_uncached(int64_t n, int nq, int k, int ep) {
       sl = ring_slabs(L.n_qt, L.n_sample);
     }
     if (sl < 1) sl = 1;
-    // k_filter_ring's pool entries hold a row offset within the slab in 32 - 5 bits
-    if (!L.dense && sl < ((L.n_sample + (1 << 26) - 1) >> 26)) sl = (L.n_sample + (1 << 26) - 1) >> 26;
+    // k_filter_ring's pool entries hold a row offset within the slab in 32 - QSH bits (QSH <= 7)
+    if (!L.dense && sl < ((L.n_sample + (1 << 25) - 1) >> 25)) sl = (L.n_sample + (1 << 25) - 1) >> 25;
     int64_t r = (L.n_sample + sl - 1) / sl;
     r = (r + 63) / 64 * 64;
     L.rows_per_slab = (int)r;
