@@ -434,7 +434,7 @@ def mode_a(a, dev, world, rank, search_local, k, E):
             return cfg["hidden"]
 
     torch.manual_seed(0)
-    it = ItemTower(text_encoder=_Dim())
+    it = ItemTower(text_encoder=_Dim(), embedding_dim=E)  # the catalog's dim (--dim)
     it.initialize_categorical_embeddings([f"brand{i}" for i in range(50)],
                                          [f"cat{i}" for i in range(20)])
     it.to(dev).eval()

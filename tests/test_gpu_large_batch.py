@@ -99,10 +99,10 @@ def test_large_batch_duplicates_and_special_queries(K, oracle_mod):
     assert np.array_equal(gi[17], np.arange(k)) and not np.isin(777, gi).any()
 
 
-@pytest.mark.parametrize("d,k", [(128, 50), (768, 100)])
+@pytest.mark.parametrize("d,k", [(128, 50), (500, 64), (700, 128), (768, 100)])
 def test_large_batch_other_dims(K, oracle_mod, d, k):
-    """Other padded widths of the same instantiation family (E = 128 32-row tiles, E = 768
-    16-row tiles / one query block per wave)."""
+    """Other padded widths of the same instantiation family (E = 128 32-row tiles; E = 512 and
+    768 16-row tiles with two query blocks per wave, d = 500 / 700 zero-padded to them)."""
     rng = np.random.default_rng(d + 7)
     n, nq = 50_000, 2500
     x, q = _iid(oracle_mod, rng, n, nq, d)

@@ -277,8 +277,25 @@ TT_CHECK_EXP(TT_EXP_NOSEL || TT_EXP_NOWRITE || TT_EXP_MAXONLY ||
                  TT_EXP_SEL_STOP || TT_EXP_SEL_TIMING || TT_EXP_FINAL_STOP ||
                  TT_EXP_FINAL_TIMING || TT_EXP_TM_STATS || TT_EXP_TM_SLOTS != 4,
              "TT_EXP_* (results wrong / printf / untested schedule)");
+// The batched full level at E = 512 / 768 (configs[4]'s k_filter_ring<768, 1>) keeps TWO
+// 16-query blocks per wave (192 fragment registers at E = 768) with one k-step of fragment
+// read-ahead: each A fragment read from LDS feeds 2 MFMAs instead of 1.  2M x 768 x 10k
+// queries, A/B x2 on one box (tools/bench_ab.sh --dim 768): full level 28.95 / 29.18 ms (one
+// block, 2 steps ahead) -> 26.13 / 26.50 (two blocks, 2 ahead) -> 23.23 / 23.32 ms (two
+// blocks, 1 ahead) = 42% -> 53% of the bf16 peak; self-check bit-exact.  Two tiles in flight
+// (3-slot ring) instead of three: 22.54 / 22.55 -> 22.27 / 22.44 ms.
+#ifndef TT_RING_QB_WIDE
+#define TT_RING_QB_WIDE 2  // query blocks per wave of the batched full level at E = 512 / 768
+#endif
+#ifndef TT_RING_FD_WIDE
+#define TT_RING_FD_WIDE 1  // its fragment read-ahead (0: the generic rule)
+#endif
+#ifndef TT_RING_PD_WIDE
+#define TT_RING_PD_WIDE 2  // its ring tiles in flight (0: RG_PD)
+#endif
 TT_CHECK_EXP(TT_RING_HALF || TT_RING_QB4 || TT_RING_W4QB || TT_RING_ASM ||
-                 TT_RING_QB_WIDE != 1 || TT_RING_FD_WIDE || TT_EXP_NOIDLE || TT_EXP_PRIO ||
+                 TT_RING_QB_WIDE != 2 || TT_RING_FD_WIDE != 1 || TT_RING_PD_WIDE != 2 ||
+                 TT_EXP_NOIDLE || TT_EXP_PRIO ||
                  TT_RING_NT != 1 || TT_RR_STAGED != 1 || TT_RR_PF != 1 || TT_RR_NT,
              "a non-default ring/re-rank schedule (untested by the GPU suite)");
 #ifndef TT_RING_PD
@@ -303,12 +320,6 @@ constexpr int RG_BLOCKS_PER_CU = TT_RING_HALF ? 2 : 1;
 // flight: 1.5x the compute per tile covers the same lead time): 6.26-6.33 -> 5.99-6.02 ms
 // (A/B x2, one box).  Small batches (LVL 2: one-buyer searches are HBM-bound and want 3 tiles
 // in flight) and sample levels keep two blocks per wave.
-#ifndef TT_RING_QB_WIDE
-#define TT_RING_QB_WIDE 1  // query blocks per wave of the batched full level at E = 512 / 768
-#endif
-#ifndef TT_RING_FD_WIDE
-#define TT_RING_FD_WIDE 0  // its fragment read-ahead (0: the generic rule)
-#endif
 template <int EP, int LVL>
 struct RingK {
   static constexpr int QB = TT_RING_W4QB ? (EP == 384 && LVL == 1 ? TT_RING_W4QB
@@ -316,7 +327,7 @@ struct RingK {
                             : (EP == 384 && LVL == 1 && !TT_RING_HALF && !TT_RING_QB4)
                                 ? 3
                             : (EP >= 512 && LVL == 1) ? TT_RING_QB_WIDE : RingCfg<EP>::QB;
-  static constexpr int PD = QB == 3 ? 2 : RG_PD;
+  static constexpr int PD = QB == 3 ? 2 : (EP >= 512 && LVL == 1 && TT_RING_PD_WIDE) ? TT_RING_PD_WIDE : RG_PD;
   static constexpr int SLOTS = PD + 1;
 };
 template <int EP, int LVL = 0>
