@@ -283,7 +283,13 @@ TT_CHECK_EXP(TT_EXP_NOSEL || TT_EXP_NOWRITE || TT_EXP_MAXONLY ||
 // queries, A/B x2 on one box (tools/bench_ab.sh --dim 768): full level 28.95 / 29.18 ms (one
 // block, 2 steps ahead) -> 26.13 / 26.50 (two blocks, 2 ahead) -> 23.23 / 23.32 ms (two
 // blocks, 1 ahead) = 42% -> 53% of the bf16 peak; self-check bit-exact.  Two tiles in flight
-// (3-slot ring) instead of three: 22.54 / 22.55 -> 22.27 / 22.44 ms.
+// (3-slot ring) instead of three: 22.54 / 22.55 -> 22.27 / 22.44 ms.  The sample levels of a
+// large batch (LVL 3) at E >= 512 keep two blocks as well (10M x 768 step 120.7 / 120.9 ->
+// 118.1 / 118.1 ms, small batches unchanged; A/B x2 on one box).  Small batches (LVL 0 and 2, HBM-bound) keep ONE: with two, a 256-query
+// batch read the catalog once instead of twice (2M x 768: 1.11 -> 0.91 ms), but batches of
+// 16-64 ran 4-9% slower (one k-step of read-ahead leaves a lone live block's LDS latency
+// exposed; two steps spill; interleaving the blocks over the waves did not help) -- so the
+// levels have their own queries per block (ring_qpb_rt).
 #ifndef TT_RING_QB_WIDE
 #define TT_RING_QB_WIDE 2  // query blocks per wave of the batched full level at E = 512 / 768
 #endif
@@ -326,7 +332,8 @@ struct RingK {
                                                                   : 2 * RingCfg<EP>::QB)
                             : (EP == 384 && LVL == 1 && !TT_RING_HALF && !TT_RING_QB4)
                                 ? 3
-                            : (EP >= 512 && LVL == 1) ? TT_RING_QB_WIDE : RingCfg<EP>::QB;
+                            : (EP >= 512 && (LVL == 1 || LVL == 3)) ? TT_RING_QB_WIDE
+                                                                     : RingCfg<EP>::QB;
   static constexpr int PD = QB == 3 ? 2 : (EP >= 512 && LVL == 1 && TT_RING_PD_WIDE) ? TT_RING_PD_WIDE : RG_PD;
   static constexpr int SLOTS = PD + 1;
 };
@@ -336,6 +343,24 @@ template <int EP, int LVL>
 constexpr int ring_smem() {
   return RingK<EP, LVL>::SLOTS * RingCfg<EP>::TR * EP * 2 + RG_POOL * 8 +
          ring_qpb<EP, LVL>() * 4 + 16;
+}
+
+// queries per block of k_filter_ring<ep, lvl> (the host's plan must use the same shape), and
+// the instantiation a ring level runs: sample levels 0 (small batch) / 3 (large batch), the
+// full level 2 (small batch) / 1 (large batch, > RG_SMALL_NQ queries)
+template <int LVL>
+static int ring_qpb_ep(int ep) {
+  return ep == 64 ? ring_qpb<64, LVL>() : ep == 128 ? ring_qpb<128, LVL>()
+         : ep == 256 ? ring_qpb<256, LVL>() : ep == 384 ? ring_qpb<384, LVL>()
+         : ep == 512 ? ring_qpb<512, LVL>() : ring_qpb<768, LVL>();
+}
+static int ring_qpb_rt(int ep, int lvl) {
+  return lvl == 1 ? ring_qpb_ep<1>(ep) : lvl == 2 ? ring_qpb_ep<2>(ep)
+         : lvl == 3 ? ring_qpb_ep<3>(ep) : ring_qpb_ep<0>(ep);
+}
+constexpr int RG_SMALL_NQ_H = 2048;  // = RG_SMALL_NQ (declared with the kernel below)
+static int ring_lvl(bool tmax, int nq) {
+  return tmax ? (nq > RG_SMALL_NQ_H ? 3 : 0) : (nq > RG_SMALL_NQ_H ? 1 : 2);
 }
 
 // LDS ops of the ring kernel's append path, in inline asm: the compiler cannot prove they do
@@ -425,11 +450,13 @@ struct QueryInit {
   int* qsel_n;
 };
 
-// LVL: 0 = a sample level, 1 = the full-catalog (last) level of a large query batch
-// (> RG_SMALL_NQ queries), 2 = the full level of a small batch -- separate instantiations of
+// LVL: 0 = a sample level of a small batch, 3 = a sample level of a large batch, 1 = the
+// full-catalog (last) level of a large query batch (> RG_SMALL_NQ queries), 2 = the full level
+// of a small batch (ring_lvl) -- separate instantiations of
 // the same code so that profiles attribute the dominant launch (bench.py's roofline kernel,
 // 10k queries) on its own, apart from e.g. Mode A's 256-query searches.
 constexpr int RG_SMALL_NQ = 2048;
+static_assert(RG_SMALL_NQ == RG_SMALL_NQ_H, "one batch threshold");
 template <int EP, int LVL>
 __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring(
     const uint16_t* __restrict__ xb, int64_t ld, const float* __restrict__ q, int nq,
@@ -445,6 +472,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   constexpr int FM = (CPR >= 16 ? 16 : CPR) - 1;
   constexpr int RB = TR / 16;
   constexpr bool AMF = TT_RING_W4QB && TT_RING_ASM && EP == 384 && LVL == 1;
+  constexpr bool SAMPLE = LVL == 0 || LVL == 3;  // a strided sample level (tile-max appends)
   constexpr int QSH = QPW <= 16 ? 4 : QPW <= 32 ? 5 : QPW <= 64 ? 6 : 7;  // pool entry: query bits
   static_assert((1 << QSH) >= QPW, "queries per wave fit the pool entry's query bits");
   static_assert(PIECES % RG_WAVES == 0, "tile must split into whole 1-KiB pieces per wave");
@@ -517,7 +545,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   // pos ^ (r & FM) of that row, so row r's logical chunk c lives at position c ^ (r & FM).
   // Per lane the (row, column byte) of each piece is loop-invariant.
   // sample levels read every stride-th row; the full level (LVL 1, 2) is the catalog itself
-  const int64_t strd = LVL == 0 ? stride : 1;
+  const int64_t strd = SAMPLE ? stride : 1;
   const int64_t row_bytes = strd * ld * 2;
   // source = wave-uniform tile base (SGPRs) + the lane's 32-bit offset within the tile
   uint32_t voff[PPW];
@@ -694,7 +722,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   // FD + 1 divides KS (the ring index is s % (FD + 1)); 2 steps ahead where registers are tight
   // (three query blocks per wave: 6 MFMAs per k-step already cover one step of read-ahead,
   // and the fragment registers of a second step would spill)
-  constexpr int FD = (EP >= 512 && LVL == 1 && TT_RING_FD_WIDE) ? TT_RING_FD_WIDE
+  constexpr int FD = (EP >= 512 && (LVL == 1 || LVL == 3) && TT_RING_FD_WIDE) ? TT_RING_FD_WIDE
                      : QB >= 3 ? 1 : (EP >= 384 && KS % 3 == 0) ? 2 : (KS >= 4 ? 3 : 1);
   static_assert(RG_SLOTS >= 3, "ring depth");
   constexpr int S_MID = (KS - FD) / 2;
@@ -703,7 +731,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   // step 1; S0 = 2 vs 1: 6.72 -> 6.64 ms; finer pieces and other spacings measured slower).
   // Sample levels append their tile maxima at step 1.
   constexpr int SP = KS / QB > 0 ? KS / QB : 1;
-  constexpr int S0 = LVL == 0 ? 1
+  constexpr int S0 = SAMPLE ? 1
                      : (QB > 1 && 2 + (QB - 1) * SP < KS) ? 2
                      : (QB > 1 && 1 + (QB - 1) * SP < KS) ? 1 : -1;  // -1: every block at step 1
   static_assert(KS % (FD + 1) == 0 && S_MID < KS - FD, "fragment ring layout");
@@ -812,9 +840,9 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
             asm volatile("s_barrier" ::: "memory");
             if (t + RG_PD < n_tiles) issue(t + RG_PD);
           }
-          if constexpr (LVL == 0 || S0 < 0) {
+          if constexpr (SAMPLE || S0 < 0) {
             if constexpr (s == 1) {  // early: tile t-1's scores die before the peak
-              if constexpr (LVL == 0) {
+              if constexpr (SAMPLE) {
                 if (!TT_EXP_NOSEL) append_tmax(mx, t - 1, 0, QB);
               } else {
                 if (!TT_EXP_NOSEL) append(accp, mx, t - 1, 0, QB);
@@ -837,7 +865,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
 #pragma unroll
           for (int b = 0; b < QB; ++b) accp[rb][b] = acc[rb][b];
         // the slab's last tile (full level): rows past j1 are clamped DMA copies of row j1 - 1
-        if (LVL != 0 && j0 + (int64_t)(t + 1) * TR > j1) {
+        if (!SAMPLE && j0 + (int64_t)(t + 1) * TR > j1) {
           const int lim = (int)(j1 - (j0 + (int64_t)t * TR));
 #pragma unroll
           for (int rb = 0; rb < RB; ++rb)
@@ -853,7 +881,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   if (n_tiles > 0 && !TT_EXP_NOSEL) {
     float mx[QB];
     tile_max(accp, mx);
-    if constexpr (LVL == 0) append_tmax(mx, n_tiles - 1, 0, QB);
+    if constexpr (SAMPLE) append_tmax(mx, n_tiles - 1, 0, QB);
     else append(accp, mx, n_tiles - 1, 0, QB);
   }
   wait_vm<0>();
@@ -2731,15 +2759,7 @@ static FilterPlan plan_filter_uncached(int64_t n, int nq, int k, int ep) {
   p.max_slabs = 1;
   const int dense_qpb = FL_WAVES * 16 * (ep <= 384 ? 2 : 1);
   // queries per block of the ring instantiation a level will run (launch_level's rule)
-  auto ring_qpb_v = [&](bool tmax) {
-    if (!tmax && nq > RG_SMALL_NQ)
-      return ep == 64 ? ring_qpb<64, 1>() : ep == 128 ? ring_qpb<128, 1>()
-             : ep == 256 ? ring_qpb<256, 1>() : ep == 384 ? ring_qpb<384, 1>()
-             : ep == 512 ? ring_qpb<512, 1>() : ring_qpb<768, 1>();
-    return ep == 64 ? ring_qpb<64>() : ep == 128 ? ring_qpb<128>()
-           : ep == 256 ? ring_qpb<256>() : ep == 384 ? ring_qpb<384>()
-           : ep == 512 ? ring_qpb<512>() : ring_qpb<768>();
-  };
+  auto ring_qpb_v = [&](bool tmax) { return ring_qpb_rt(ep, ring_lvl(tmax, nq)); };
   for (int i = 0; i < nl; ++i) {
     Level& L = p.lv[i];
     L.stride = strides[nl - 1 - i];
@@ -2862,9 +2882,9 @@ static void launch_level(const Level& L, const uint16_t* xb, int64_t n, int64_t 
                        ld, q, nq, ldq, w.theta, L.stride, L.n_sample, L.rows_per_slab,
                        L.n_slabs, L.n_qt, w.lists, w.counts);
   } else {
-    auto kern = L.tmax            ? k_filter_ring<EP, 0>
-                : nq > RG_SMALL_NQ ? k_filter_ring<EP, 1>
-                                   : k_filter_ring<EP, 2>;
+    const int lvl = ring_lvl(L.tmax, nq);
+    auto kern = lvl == 3 ? k_filter_ring<EP, 3> : lvl == 0 ? k_filter_ring<EP, 0>
+                : lvl == 1 ? k_filter_ring<EP, 1> : k_filter_ring<EP, 2>;
     hipLaunchKernelGGL(kern, dim3(nblk), dim3(64 * RG_WAVES), 0, st, xb, ld, q, nq, ldq, w.theta,
                        L.stride, L.n_sample, L.rows_per_slab, L.n_slabs, L.n_qt, w.lists,
                        w.counts, qi);
@@ -3241,9 +3261,7 @@ extern "C" int tt_sharded_filter_begin(const uint16_t* sample_bf16, int64_t n_sa
     // ladder and its exact a_J -- one filter launch and one selection fewer per step.  Only
     // when the level's slabs fit the workspace carved for the generic plan.
     const int64_t TR = ring_tr(ep);
-    const int qpb = ep == 64 ? ring_qpb<64>() : ep == 128 ? ring_qpb<128>()
-                    : ep == 256 ? ring_qpb<256>() : ep == 384 ? ring_qpb<384>()
-                    : ep == 512 ? ring_qpb<512>() : ring_qpb<768>();
+    const int qpb = ring_qpb_rt(ep, ring_lvl(true, nq));
     if (n_sample > SEL_CAP / 2 && (n_sample + TR - 1) / TR <= SW_CAP_TILES && p.n_levels > 1) {
       Level L;
       L.stride = 1;
