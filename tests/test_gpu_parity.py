@@ -93,6 +93,8 @@ BF16_CASES = [c for c in SCAN_CASES if c[3] <= 128] + [
     (150000, 384, 3, 10),    # 585 slabs: ragged groups of 10 per lane
     (70000, 128, 2, 50),     # E = 128, 273 slabs
     (60000, 768, 33, 100),   # E = 768 (one query block per wave)
+    (60000, 768, 300, 100),  # E = 768 mid-size batch: two query blocks per wave (LVL 4)
+    (30000, 500, 129, 64),   # E = 512, one query past a 128-query tile
     (20000, 384, 300, 100),  # several query tiles
     (40000, 512, 9, 64),
     # small batches (block-per-query selection): ragged sizes, every E

@@ -289,7 +289,8 @@ TT_CHECK_EXP(TT_EXP_NOSEL || TT_EXP_NOWRITE || TT_EXP_MAXONLY ||
 // batch read the catalog once instead of twice (2M x 768: 1.11 -> 0.91 ms), but batches of
 // 16-64 ran 4-9% slower (one k-step of read-ahead leaves a lone live block's LDS latency
 // exposed; two steps spill; interleaving the blocks over the waves did not help) -- so the
-// levels have their own queries per block (ring_qpb_rt).
+// levels have their own queries per block (ring_qpb_rt), and batches past one 128-query tile
+// take the two-block full level (LVL 4) instead.
 #ifndef TT_RING_QB_WIDE
 #define TT_RING_QB_WIDE 2  // query blocks per wave of the batched full level at E = 512 / 768
 #endif
@@ -332,7 +333,7 @@ struct RingK {
                                                                   : 2 * RingCfg<EP>::QB)
                             : (EP == 384 && LVL == 1 && !TT_RING_HALF && !TT_RING_QB4)
                                 ? 3
-                            : (EP >= 512 && (LVL == 1 || LVL == 3)) ? TT_RING_QB_WIDE
+                            : (EP >= 512 && (LVL == 1 || LVL >= 3)) ? TT_RING_QB_WIDE
                                                                      : RingCfg<EP>::QB;
   static constexpr int PD = QB == 3 ? 2 : (EP >= 512 && LVL == 1 && TT_RING_PD_WIDE) ? TT_RING_PD_WIDE : RG_PD;
   static constexpr int SLOTS = PD + 1;
@@ -356,11 +357,13 @@ static int ring_qpb_ep(int ep) {
 }
 static int ring_qpb_rt(int ep, int lvl) {
   return lvl == 1 ? ring_qpb_ep<1>(ep) : lvl == 2 ? ring_qpb_ep<2>(ep)
-         : lvl == 3 ? ring_qpb_ep<3>(ep) : ring_qpb_ep<0>(ep);
+         : lvl == 3 ? ring_qpb_ep<3>(ep) : lvl == 4 ? ring_qpb_ep<4>(ep) : ring_qpb_ep<0>(ep);
 }
 constexpr int RG_SMALL_NQ_H = 2048;  // = RG_SMALL_NQ (declared with the kernel below)
-static int ring_lvl(bool tmax, int nq) {
-  return tmax ? (nq > RG_SMALL_NQ_H ? 3 : 0) : (nq > RG_SMALL_NQ_H ? 1 : 2);
+// 4 = the full level of a mid-size batch at E >= 512 (more than one 128-query tile of LVL 2)
+static int ring_lvl(bool tmax, int nq, int ep) {
+  if (tmax) return nq > RG_SMALL_NQ_H ? 3 : 0;
+  return nq > RG_SMALL_NQ_H ? 1 : (ep >= 512 && nq > ring_qpb_ep<2>(ep)) ? 4 : 2;
 }
 
 // LDS ops of the ring kernel's append path, in inline asm: the compiler cannot prove they do
@@ -452,7 +455,8 @@ struct QueryInit {
 
 // LVL: 0 = a sample level of a small batch, 3 = a sample level of a large batch, 1 = the
 // full-catalog (last) level of a large query batch (> RG_SMALL_NQ queries), 2 = the full level
-// of a small batch (ring_lvl) -- separate instantiations of
+// of a small batch, 4 = that of a mid-size batch at E >= 512 (ring_lvl) -- separate
+// instantiations of
 // the same code so that profiles attribute the dominant launch (bench.py's roofline kernel,
 // 10k queries) on its own, apart from e.g. Mode A's 256-query searches.
 constexpr int RG_SMALL_NQ = 2048;
@@ -583,7 +587,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
       }
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rs, (__attribute__((address_space(3))) void*)(slot + (w + RG_WAVES * pp) * 1024), 16,
-          off, 0, 0, ((TT_RING_NT >= 1 && LVL == 2) || TT_RING_NT >= 3) ? 2 : 0);
+          off, 0, 0, ((TT_RING_NT >= 1 && (LVL == 2 || LVL == 4)) || TT_RING_NT >= 3) ? 2 : 0);
     }
   };
   auto issue = [&](int t) __attribute__((always_inline)) {
@@ -722,7 +726,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   // FD + 1 divides KS (the ring index is s % (FD + 1)); 2 steps ahead where registers are tight
   // (three query blocks per wave: 6 MFMAs per k-step already cover one step of read-ahead,
   // and the fragment registers of a second step would spill)
-  constexpr int FD = (EP >= 512 && (LVL == 1 || LVL == 3) && TT_RING_FD_WIDE) ? TT_RING_FD_WIDE
+  constexpr int FD = (EP >= 512 && (LVL == 1 || LVL >= 3) && TT_RING_FD_WIDE) ? TT_RING_FD_WIDE
                      : QB >= 3 ? 1 : (EP >= 384 && KS % 3 == 0) ? 2 : (KS >= 4 ? 3 : 1);
   static_assert(RG_SLOTS >= 3, "ring depth");
   constexpr int S_MID = (KS - FD) / 2;
@@ -2759,7 +2763,7 @@ static FilterPlan plan_filter_uncached(int64_t n, int nq, int k, int ep) {
   p.max_slabs = 1;
   const int dense_qpb = FL_WAVES * 16 * (ep <= 384 ? 2 : 1);
   // queries per block of the ring instantiation a level will run (launch_level's rule)
-  auto ring_qpb_v = [&](bool tmax) { return ring_qpb_rt(ep, ring_lvl(tmax, nq)); };
+  auto ring_qpb_v = [&](bool tmax) { return ring_qpb_rt(ep, ring_lvl(tmax, nq, ep)); };
   for (int i = 0; i < nl; ++i) {
     Level& L = p.lv[i];
     L.stride = strides[nl - 1 - i];
@@ -2882,9 +2886,11 @@ static void launch_level(const Level& L, const uint16_t* xb, int64_t n, int64_t 
                        ld, q, nq, ldq, w.theta, L.stride, L.n_sample, L.rows_per_slab,
                        L.n_slabs, L.n_qt, w.lists, w.counts);
   } else {
-    const int lvl = ring_lvl(L.tmax, nq);
+    const int lvl = ring_lvl(L.tmax, nq, EP);
     auto kern = lvl == 3 ? k_filter_ring<EP, 3> : lvl == 0 ? k_filter_ring<EP, 0>
                 : lvl == 1 ? k_filter_ring<EP, 1> : k_filter_ring<EP, 2>;
+    if constexpr (EP >= 512)
+      if (lvl == 4) kern = k_filter_ring<EP, 4>;
     hipLaunchKernelGGL(kern, dim3(nblk), dim3(64 * RG_WAVES), 0, st, xb, ld, q, nq, ldq, w.theta,
                        L.stride, L.n_sample, L.rows_per_slab, L.n_slabs, L.n_qt, w.lists,
                        w.counts, qi);
@@ -3261,7 +3267,7 @@ extern "C" int tt_sharded_filter_begin(const uint16_t* sample_bf16, int64_t n_sa
     // ladder and its exact a_J -- one filter launch and one selection fewer per step.  Only
     // when the level's slabs fit the workspace carved for the generic plan.
     const int64_t TR = ring_tr(ep);
-    const int qpb = ring_qpb_rt(ep, ring_lvl(true, nq));
+    const int qpb = ring_qpb_rt(ep, ring_lvl(true, nq, ep));
     if (n_sample > SEL_CAP / 2 && (n_sample + TR - 1) / TR <= SW_CAP_TILES && p.n_levels > 1) {
       Level L;
       L.stride = 1;
