@@ -59,7 +59,9 @@ def parse():
     p.add_argument("--cpu-batch", type=int, default=512, help="per repetition (median of 5)")
     p.add_argument("--mode-a-buyers", type=int, default=256,
                    help="Mode A sample per rank (history texts re-encoded); 0 disables")
-    p.add_argument("--mode-a-prec", choices=["bf16", "x3", "f32"], default="bf16")
+    p.add_argument("--mode-a-prec", choices=["bf16", "x3", "f32"], default="x3",
+                   help="x3 (default): the reference's f32 precision class (split-bf16 "
+                        "products); bf16 is reported beside it as a throughput mode")
     p.add_argument("--mode-a-steps", type=int, default=3)
     p.add_argument("--no-extra", action="store_true",
                    help="skip the configs[1] leg, the batch sweep and the f32 Mode A leg")
@@ -110,8 +112,10 @@ def configs1(a, dev, rank):
     item_tower.py:213-243; then VectorDatabase.retrieve_batch, vector_db.py:171-209).
     One step = one batch of 256 product texts: MiniLM-L12 encode (HIP, packed varlen) +
     projection head + F.normalize -> q/(||q||+1e-8) -> exact top-100 of the 256 new item
-    embeddings over the 100k x 384 catalog.  bf16 encoder over all 100k texts (the whole
-    generate_embeddings pass); the f32 (parity) encoder on a 16-batch sample."""
+    embeddings over the 100k x 384 catalog.  The reported value is the x3 encoder (the
+    reference's f32 precision class: ItemTower's default) over all 100k texts (the whole
+    generate_embeddings pass); the bf16 encoder (throughput mode, below f32 precision) on a
+    64-batch sample and the f32-MFMA encoder on a 16-batch sample beside it."""
     from twotower.item_tower import MINILM_L12, BertEncoder, ItemTower, pack_sequences, \
         random_bert_state_dict
 
@@ -148,7 +152,7 @@ def configs1(a, dev, rank):
                        "L ~ U[16,128]) + exact top-100 over a 100k x 384 catalog",
            "texts": n_txt, "batch": BS}
     res, ys = {}, {}
-    for prec, nb in (("bf16", len(batches)), ("x3", min(64, len(batches))),
+    for prec, nb in (("x3", len(batches)), ("bf16", min(64, len(batches))),
                      ("f32", min(16, len(batches)))):
         enc = BertEncoder(sd, cfg, device=dev, prec=prec)
         pooled = torch.empty((BS, cfg["hidden"]), device=dev)
@@ -235,7 +239,8 @@ def configs1(a, dev, rank):
             "max_abs_diff": float((ys[prec] - ys["f32"]).abs().max())}
     res["x3_over_f32_texts_per_s"] = res["x3"]["texts_per_s"] / res["f32"]["texts_per_s"]
     out.update(res)
-    out["value"] = res["bf16"]["texts_per_s"]
+    out["value"] = res["x3"]["texts_per_s"]
+    out["value_prec"] = "x3 (f32 precision class; bf16 throughput mode under 'bf16')"
     out["unit"] = "texts/s (encode + top-100 per batch of 256)"
     return out
 
@@ -776,10 +781,10 @@ def main():
                                          K, E)
     if world == 1 and not a.no_extra:
         result["batch_sweep"] = batch_sweep(a, shard, shard16, hi - lo, E, K, bounds, dev)
-        if a.mode_a_buyers > 0 and a.mode_a_prec == "bf16":
-            # Mode A at the parity precision class: the split-bf16 (x3) encoder, and one step
-            # of the f32 MFMA encoder beside it
-            for prec, steps in (("x3", a.mode_a_steps), ("f32", 1)):
+        if a.mode_a_buyers > 0 and a.mode_a_prec == "x3":
+            # beside the parity-precision (x3) Mode A: the bf16 encoder (throughput mode, below
+            # the reference's f32 precision) and one step of the f32 MFMA encoder
+            for prec, steps in (("bf16", a.mode_a_steps), ("f32", 1)):
                 a32 = argparse.Namespace(**vars(a))
                 a32.mode_a_prec, a32.mode_a_steps = prec, steps
                 m32, _ = mode_a(a32, dev, world, rank, lambda qall: local_search_k(qall), K, E)

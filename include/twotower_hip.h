@@ -247,6 +247,13 @@ typedef struct tt_bert_layer {
   /* TT_PREC_X3, optional: pre-split images [N, 2K] (tt_x3_split_weights); NULL -> the f32
    * weights are split on the fly */
   const uint16_t *wqkv_x3, *wo_x3, *w1_x3, *w2_x3;
+  /* TT_PREC_X3 at H == 384 (head dim 32, I % 64 == 0), optional: K-concatenated images
+   * W' [N, 3K] bf16 = [bf16(W) | bf16(W - bf16(W)) | bf16(W)] (tt_x3c_weights).  When all four
+   * are set the encoder takes the x3c form: each GEMM is ONE bf16 GEMM over K' = 3K whose A
+   * operand is the [hi | lo] bf16 plane pair of the f32 activation (written so by its producer:
+   * embedding LayerNorm, attention, the fused GEMM + LayerNorm, the FFN1 GELU epilogue) -- the
+   * same three products hi.hi + hi.lo + lo.hi as TT_PREC_X3, on the persistent ring GEMMs. */
+  const uint16_t *wqkv_x3c, *wo_x3c, *w1_x3c, *w2_x3c;
 } tt_bert_layer;
 
 typedef struct tt_bert_model {
@@ -285,6 +292,23 @@ int tt_gemm_x3w(const float* A, int64_t lda, const uint16_t* Wx3, int64_t ld_wx3
                 const float* bias, const float* residual, int64_t ldr, float* C, int64_t ldc,
                 uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N, int32_t K, int32_t act,
                 void* stream);
+/* tt_x3c_weights: W [N, K] f32 -> out [N, 3K] bf16 = [hi | lo | hi], hi = bf16(W) (RNE),
+ * lo = bf16(W - hi) (the x3c GEMMs' W').  tt_gemm_x3c: C[M,N] = act(A . W^T + bias) + residual
+ * with A given as its split planes A2 [M, 2K] = [bf16(A) | bf16(A - bf16(A))] and W as W3 [N, 3K]
+ * (tt_x3c_weights): acc = A_hi.W_hi + A_hi.W_lo + A_lo.W_hi over K' = 3K on bf16 MFMA with f32
+ * accumulation.  Exactly one of C (f32) and C_split (the result's own planes [M, 2N], ld >= 2N,
+ * residual NULL) is written.  K % 64 == 0.  tt_gemm_ln_x3c: tt_gemm_ln_bf16 in that form
+ * (A2 [M, 2K], W3 [384, 3K]) writing x f32 and its planes x_split [M, 768]. */
+int tt_x3c_weights(const float* W, int64_t ldw, int32_t N, int32_t K, uint16_t* out,
+                   int64_t ld_out, void* stream);
+int tt_gemm_x3c(const uint16_t* A2, int64_t lda2, const uint16_t* W3, int64_t ldw3,
+                const float* bias, const float* residual, int64_t ldr, float* C, int64_t ldc,
+                uint16_t* C_split, int64_t ldc_split, int32_t M, int32_t N, int32_t K, int32_t act,
+                void* stream);
+int tt_gemm_ln_x3c(const uint16_t* A2, int64_t lda2, const uint16_t* W3, int64_t ldw3,
+                   const float* bias, const float* gamma, const float* beta, float eps, float* x,
+                   int64_t ldx, uint16_t* x_split, int64_t ldx_split, int32_t M, int32_t H,
+                   int32_t K, void* stream);
 int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
                  const float* bias, const float* residual, int64_t ldr, float* C, int64_t ldc,
                  uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N, int32_t K, int32_t act,

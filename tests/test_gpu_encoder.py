@@ -106,6 +106,91 @@ def test_gemm_x3_presplit_weights_identical(M, N, K, act):
     assert Wx[3 % N, 64 * kb + 32 + slot] == (w - hi.float()).to(torch.bfloat16)
 
 
+def _planes(x):
+    """f32 [M, K] -> the x3c A operand [M, 2K] bf16 = [bf16(x) | bf16(x - bf16(x))]."""
+    hi = x.to(torch.bfloat16)
+    return torch.cat([hi, (x - hi.float()).to(torch.bfloat16)], 1).contiguous()
+
+
+@pytest.mark.parametrize("M,N,K,act,split", [(1, 128, 64, 0, False), (77, 256, 512, 2, False),
+                                             (300, 1152, 384, 0, False), (300, 1536, 384, 1, True),
+                                             (18300, 1152, 384, 0, False),
+                                             (18300, 1536, 384, 1, True),
+                                             (70001, 1152, 384, 0, False),
+                                             (66000, 1536, 384, 1, True),
+                                             (50001, 1000, 384, 1, True),
+                                             (40000, 384, 1536, 0, False)])
+def test_gemm_x3c_vs_torch(M, N, K, act, split):
+    """K-concatenated split-bf16 GEMM (tt_gemm_x3c: A as [hi | lo] planes, W' = [hi | lo | hi],
+    one bf16 GEMM over 3K): the x3 tolerance vs the f64 product of the f32 operands, on the
+    128x128 kernel (small M), the 256x256 / 256x128 ring kernels (large M) and the split-plane
+    output (the FFN1 -> W2 form, checked by recombining hi + lo)."""
+    from twotower import _lib
+    from twotower.item_tower import x3c_weights
+
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K + act)
+    A = torch.randn((M, K), generator=g, device="cuda")
+    W = torch.randn((N, K), generator=g, device="cuda") / K ** 0.5
+    b = torch.randn(N, generator=g, device="cuda")
+    R = None if split else torch.randn((M, N), generator=g, device="cuda")
+    W3 = x3c_weights(W)
+    hi = W.to(torch.bfloat16)
+    assert torch.equal(W3[:, :K], hi) and torch.equal(W3[:, 2 * K:], hi)
+    assert torch.equal(W3[:, K:2 * K], (W - hi.float()).to(torch.bfloat16))
+    A2 = _planes(A)
+    if split:
+        C2 = torch.empty((M, 2 * N), device="cuda", dtype=torch.bfloat16)
+        _lib.check(_lib.lib().tt_gemm_x3c(A2.data_ptr(), A2.stride(0), W3.data_ptr(), W3.stride(0),
+                                          b.data_ptr(), None, 0, None, 0, C2.data_ptr(),
+                                          C2.stride(0), M, N, K, act, _lib.stream_ptr()), "x3c")
+        C = C2[:, :N].float() + C2[:, N:].float()
+        # the planes are a split of one f32 value: |lo| <= half a bf16 ulp of hi
+        hi, lo = C2[:, :N].float(), C2[:, N:].float()
+        assert bool((lo.abs() <= hi.abs() * 2.0 ** -8).all())
+    else:
+        C = torch.empty((M, N), device="cuda")
+        _lib.check(_lib.lib().tt_gemm_x3c(A2.data_ptr(), A2.stride(0), W3.data_ptr(), W3.stride(0),
+                                          b.data_ptr(), R.data_ptr(), R.stride(0), C.data_ptr(),
+                                          C.stride(0), None, 0, M, N, K, act, _lib.stream_ptr()),
+                   "x3c")
+    ref = (A.double() @ W.double().T) + b.double()
+    ref = {0: ref, 1: F.gelu(ref), 2: torch.relu(ref)}[act]
+    if R is not None:
+        ref = ref + R.double()
+    # split planes hold the f32 value to 2^-17 relative (the dropped remainder)
+    tol = 5e-5 if not split else 6e-5
+    torch.testing.assert_close(C.double(), ref, rtol=1e-5, atol=tol)
+
+
+@pytest.mark.parametrize("M,K", [(1, 384), (129, 1536), (18300, 384), (18300, 1536),
+                                 (70003, 1536)])
+def test_gemm_ln_x3c_vs_torch(M, K):
+    """Fused GEMM + LayerNorm in the x3c form (tt_gemm_ln_x3c): x = LN(A W^T + b + x) in place
+    with x's [hi | lo] planes, vs the f64 composition of the f32 operands."""
+    from twotower import _lib
+    from twotower.item_tower import x3c_weights
+
+    H = 384
+    g = torch.Generator(device="cuda").manual_seed(M + 5 * K)
+    A = torch.randn((M, K), generator=g, device="cuda")
+    W = torch.randn((H, K), generator=g, device="cuda") / K ** 0.5
+    b = torch.randn(H, generator=g, device="cuda")
+    gm = torch.randn(H, generator=g, device="cuda")
+    bt = torch.randn(H, generator=g, device="cuda")
+    x = torch.randn((M, H), generator=g, device="cuda") * 2 + 0.5
+    ref = F.layer_norm(A.double() @ W.double().T + b.double() + x.double(), (H,), gm.double(),
+                       bt.double(), 1e-12)
+    A2, W3 = _planes(A), x3c_weights(W)
+    xs = torch.empty((M, 2 * H), device="cuda", dtype=torch.bfloat16)
+    _lib.check(_lib.lib().tt_gemm_ln_x3c(A2.data_ptr(), A2.stride(0), W3.data_ptr(), W3.stride(0),
+                                         b.data_ptr(), gm.data_ptr(), bt.data_ptr(), 1e-12,
+                                         x.data_ptr(), H, xs.data_ptr(), 2 * H, M, H, K,
+                                         _lib.stream_ptr()), "gemm_ln_x3c")
+    torch.cuda.synchronize()
+    torch.testing.assert_close(x.double(), ref, rtol=2e-5, atol=5e-5)
+    assert torch.equal(xs, _planes(x))
+
+
 @pytest.mark.parametrize("M,N,K", [(5, 128, 64), (300, 1152, 384), (2049, 384, 1536)])
 def test_gemm_bf16_vs_torch(M, N, K):
     g = torch.Generator(device="cuda").manual_seed(M * 3 + N + K)
@@ -248,6 +333,18 @@ def test_encoder_bf16_close_to_f32(golden):
     cos = F.cosine_similarity(y16, ref, dim=1)
     assert cos.min() > 0.999, cos
     assert (y16 - ref).abs().max() < 0.05 * ref.abs().max()
+
+
+def test_encoder_x3_split_in_loop_path_non384_hidden():
+    """Hidden sizes other than 384 keep the x3 path with the split done in the GEMM loop
+    (k_gemm<float, 2>, the x3c form needs the fused H = 384 GEMM + LayerNorm): vs the f32 path."""
+    cfg = dict(vocab=300, hidden=256, layers=2, heads=8, intermediate=1024, max_positions=128,
+               type_vocab=2, ln_eps=1e-12)
+    rng = np.random.default_rng(3)
+    seqs = [rng.integers(0, 300, rng.integers(1, 100)).tolist() for _ in range(40)]
+    y3 = _encoder("x3", cfg, seed=4)[0].encode_ids(seqs)
+    yf = _encoder("f32", cfg, seed=4)[0].encode_ids(seqs)
+    assert (y3 - yf).abs().max().item() < 3e-5
 
 
 @pytest.mark.parametrize("prec", ["f32", "x3"])

@@ -133,24 +133,34 @@ __device__ __forceinline__ int enc_xcd_remap(int bid, int nblk) {
 // ACTC >= 0: the activation as a compile-time constant (no per-element branch); BFO: the
 // caller guarantees the bf16-only output form (C == NULL, res == NULL, C16 16-B aligned,
 // ldc16 % 8 == 0) -- the persistent kernel's specialisations.
-template <bool FAST, int ACTC = -1, bool BFO = false>
+// OM: output form.  0 = generic (C and / or C16, residual), 1 = BFO, 2 = SPLIT: the x3
+// encoder's split-bf16 planes (C == NULL, res == NULL): C16 row m holds hi = bf16(y) at column
+// n and lo = bf16(y - hi) at column N + n (ldc16 >= 2N, N % 8 == 0, 16-B aligned rows), i.e.
+// the A operand [hi | lo] of the next x3 GEMM (k_gemm_wide / k_gemm_ln with kx = N).
+// split_n > 0 selects the same planes at run time in the generic form (k_gemm's small-M path).
+template <bool FAST, int ACTC = -1, int OM = 0>
 __device__ __forceinline__ int gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, int nw0,
                                                    int lane, int M, int N,
                                                    const float* __restrict__ bias,
                                                    const float* __restrict__ res, int64_t ldr,
                                                    float* __restrict__ C, int64_t ldc,
                                                    uint16_t* __restrict__ C16, int64_t ldc16,
-                                                   int act, const float* lbias = nullptr) {
+                                                   int act, const float* lbias = nullptr,
+                                                   int split_n = 0) {
+  constexpr bool BFO = OM == 1, SPL = OM == 2;
   const int g = lane >> 4, rl = lane & 15;
   if constexpr (ACTC >= 0) act = ACTC;
-  if constexpr (BFO) {
+  if constexpr (BFO || SPL) {
     C = nullptr;
     res = nullptr;
   }
+  if constexpr (SPL) split_n = N;
   const bool vec = (N % 4) == 0 && (ldc % 4) == 0 && (!res || (ldr % 4) == 0) &&
                    (!C16 || (ldc16 % 4) == 0) && ((uintptr_t)bias % 16) == 0 &&
                    ((uintptr_t)res % 16) == 0 && ((uintptr_t)C % 16) == 0 &&
-                   ((uintptr_t)C16 % 8) == 0 && mw0 + 64 <= M && nw0 + 64 <= N;
+                   ((uintptr_t)C16 % 8) == 0 && mw0 + 64 <= M && nw0 + 64 <= N &&
+                   (!SPL || ((N % 8) == 0 && (ldc16 % 8) == 0 && ((uintptr_t)C16 % 16) == 0)) &&
+                   (SPL || split_n == 0);
   if (vec) {
     // full tile: every bias / residual load is issued before the first use, so their
     // latencies overlap (a load-use chain per 16x16 block serialises ~16 L2 round trips)
@@ -166,6 +176,45 @@ __device__ __forceinline__ int gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, i
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           rv[i][j] = *(const f32x4*)(res + (int64_t)(mw0 + 16 * i + rl) * ldr + nw0 + 16 * j + 4 * g);
+    }
+    if constexpr (SPL) {
+      // split planes: the BFO path's permlane16_swap pairing, once for hi and once for lo
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t m = mw0 + 16 * i + rl;
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          uint32_t ph[2][2], pl[2][2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int j = 2 * jp + h;
+            f32x4 y = acc[i][j] + bv[j];
+            if (FAST && act == ACT_GELU) {
+              gelu4_fast(y);
+            } else {
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                if (act == ACT_GELU) y[u] = gelu_erf(y[u]);
+                else if (act == ACT_RELU) y[u] = y[u] > 0.0f ? y[u] : 0.0f;
+              }
+            }
+            ph[h][0] = pack_bf16_hw(y[0], y[1]);
+            ph[h][1] = pack_bf16_hw(y[2], y[3]);
+            pl[h][0] = pack_bf16_hw(y[0] - __uint_as_float(ph[h][0] << 16),
+                                    y[1] - __uint_as_float(ph[h][0] & 0xffff0000u));
+            pl[h][1] = pack_bf16_hw(y[2] - __uint_as_float(ph[h][1] << 16),
+                                    y[3] - __uint_as_float(ph[h][1] & 0xffff0000u));
+          }
+          const auto s0 = __builtin_amdgcn_permlane16_swap(ph[0][0], ph[1][0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(ph[0][1], ph[1][1], false, false);
+          const auto t0 = __builtin_amdgcn_permlane16_swap(pl[0][0], pl[1][0], false, false);
+          const auto t1 = __builtin_amdgcn_permlane16_swap(pl[0][1], pl[1][1], false, false);
+          const int n = nw0 + 32 * jp + 16 * (g & 1) + 8 * (g >> 1);
+          *(u32x4*)(C16 + m * ldc16 + n) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+          *(u32x4*)(C16 + m * ldc16 + N + n) = u32x4{t0[0], t1[0], t0[1], t1[1]};
+        }
+      }
+      return 16;
     }
     if (BFO || (!C && (ldc16 % 8) == 0 && ((uintptr_t)C16 % 16) == 0)) {
       // bf16-only output: v_permlane16_swap pairs blocks j0 = 2 jp and j1 = 2 jp + 1 so that
@@ -242,7 +291,13 @@ __device__ __forceinline__ int gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, i
         else if (act == ACT_RELU) y = y > 0.0f ? y : 0.0f;
         if (res) y = y + res[(int64_t)m * ldr + n + u];
         if (C) C[(int64_t)m * ldc + n + u] = y;
-        if (C16) C16[(int64_t)m * ldc16 + n + u] = f32_to_bf16_rne(y);
+        if (C16) {
+          const uint16_t hv = f32_to_bf16_rne(y);
+          C16[(int64_t)m * ldc16 + n + u] = hv;
+          if (split_n > 0)
+            C16[(int64_t)m * ldc16 + split_n + n + u] =
+                f32_to_bf16_rne(y - __uint_as_float((uint32_t)hv << 16));
+        }
       }
     }
   }
@@ -292,11 +347,35 @@ __global__ __launch_bounds__(256) void k_x3_split_w(const float* __restrict__ W,
   *(u32x4*)(o + 32) = __builtin_bit_cast(u32x4, lo);
 }
 
+// x3c weights: W [N, K] f32 -> [N, 3K] bf16 = [hi | lo | hi] (see x3c_acol).  Thread per element.
+__global__ __launch_bounds__(256) void k_x3c_w(const float* __restrict__ W, int64_t ldw, int N,
+                                               int K, uint16_t* __restrict__ out, int64_t ldo) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)N * K) return;
+  const int n = (int)(e / K), k = (int)(e % K);
+  const float v = W[(int64_t)n * ldw + k];
+  const uint16_t hv = f32_to_bf16_rne(v);
+  const uint16_t lv = f32_to_bf16_rne(v - __uint_as_float((uint32_t)hv << 16));
+  uint16_t* o = out + (int64_t)n * ldo;
+  o[k] = hv;
+  o[K + k] = lv;
+  o[2 * K + k] = hv;
+}
+
 // X3M = 2: W arrives pre-split (k_x3_split_w): each 32-k stage of a W row is 128 B = 32 hi
 // then 32 lo bf16 in the lanes' slot order, so the W tile's read step 0 / 1 chunks ARE the
 // lane's hi / lo operands -- only A is split in the loop (half the VALU of X3M = 1, which was
 // VALU-bound: 192 VALU beside 48 MFMAs per wave and stage).  W is passed as float* (the same
 // 128-B rows per 32 k), ldw in those 4-B units.
+// K-concatenated split-bf16 ("x3c") GEMMs: A [M, 2K] = [hi | lo] bf16 planes (written so by
+// their producers), W' [N, 3K] = [W_hi | W_lo | W_hi] (prepared once), and the bf16 GEMM runs
+// over K' = 3K with A's k-column j read at j (j < K: hi . W_hi), j - K (K <= j < 2K: hi . W_lo)
+// and j - K (j >= 2K: lo . W_hi) -- the three products of the x3 split as ONE bf16 GEMM, on the
+// persistent ring kernels, with no split VALU in the loop.  kx = K (0: a plain GEMM).
+__device__ __forceinline__ int64_t x3c_acol(int64_t k0, int kx) {
+  return (kx > 0 && k0 >= kx) ? k0 - kx : k0;
+}
+
 template <typename T, int X3M = 0>
 __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_t lda,
                                                  const T* __restrict__ W, int64_t ldw,
@@ -304,7 +383,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_
                                                  const float* __restrict__ res, int64_t ldr,
                                                  float* __restrict__ C, int64_t ldc,
                                                  uint16_t* __restrict__ C16, int64_t ldc16,
-                                                 int M, int N, int K, int act) {
+                                                 int M, int N, int K, int act, int kx,
+                                                 int split_n) {
   constexpr int BK = GemmElt<T>::BK;
   constexpr int EPC = 16 / sizeof(T);  // elements per 16-B chunk
   __shared__ __attribute__((aligned(16))) char smem[2 * GM_STAGE_B];
@@ -334,12 +414,12 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_
   }
   auto issue = [&](int kt) {
     char* st = smem + (kt & 1) * GM_STAGE_B;
-    const int64_t k0 = (int64_t)kt * BK;
+    const int64_t k0 = (int64_t)kt * BK, ka = x3c_acol(k0, kx);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int p = w + 4 * j;
       __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(A + a_off[j] + k0),
+          (const __attribute__((address_space(1))) void*)(A + a_off[j] + ka),
           (__attribute__((address_space(3))) void*)(st + 1024 * p), 16, 0, 0);
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(W + w_off[j] + k0),
@@ -444,7 +524,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_
   }
 
   gemm_wave_epilogue<sizeof(T) == 2>(acc, m0 + 64 * wm, n0 + 64 * wn, lane, M, N, bias, res, ldr,
-                                     C, ldc, C16, ldc16, act);
+                                     C, ldc, C16, ldc16, act, nullptr, split_n);
 }
 
 // Large-M bf16 GEMM: persistent blocks (one per CU, 8 waves of 64x64 = 256x128 tiles), a
@@ -459,14 +539,14 @@ constexpr int GB_BN = 128, GB_MAXN = 2048;
 // T = float: the split-bf16 (x3) product of k_gemm<float, true> on this ring -- a stage is 32
 // f32 (the same 128-B LDS rows, so DMA, swizzle and fragment reads are unchanged), and the
 // stage's two read steps form one 8-f32 slot set per lane (split_bf16x8, 3 MFMAs per block).
-template <int GB_BM, int GB_SLOTS, int ACT, bool BFO, typename T = uint16_t>
+template <int GB_BM, int GB_SLOTS, int ACT, int BFO, typename T = uint16_t>
 __global__ __launch_bounds__(GB_BM * 2, 512 / (GB_BM * 2)) void k_gemm_big(const T* __restrict__ A, int64_t lda,
                                                      const T* __restrict__ W, int64_t ldw,
                                                      const float* __restrict__ bias,
                                                      const float* __restrict__ res, int64_t ldr,
                                                      float* __restrict__ C, int64_t ldc,
                                                      uint16_t* __restrict__ C16, int64_t ldc16,
-                                                     int M, int N, int K, int act) {
+                                                     int M, int N, int K, int act, int kx) {
   constexpr bool X3 = sizeof(T) == 4;
   constexpr int BK = 128 / sizeof(T), EPC = 16 / sizeof(T);
   constexpr int GB_A_B = GB_BM * 128, GB_W_B = GB_BN * 128, GB_STAGE_B = GB_A_B + GB_W_B;
@@ -520,11 +600,11 @@ __global__ __launch_bounds__(GB_BM * 2, 512 / (GB_BM * 2)) void k_gemm_big(const
   };
   auto issue = [&](const Offs& o, int kt, int gs) __attribute__((always_inline)) {
     char* st = smem + (gs % GB_SLOTS) * GB_STAGE_B;
-    const int64_t k0 = (int64_t)kt * BK;
+    const int64_t k0 = (int64_t)kt * BK, ka = x3c_acol(k0, kx);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(A + o.a[j] + k0),
+          (const __attribute__((address_space(1))) void*)(A + o.a[j] + ka),
           (__attribute__((address_space(3))) void*)(st + 1024 * (w + NW * j)), 16, 0, 0);
 #pragma unroll
     for (int j = 0; j < WP; ++j)
@@ -653,14 +733,14 @@ __global__ __launch_bounds__(GB_BM * 2, 512 / (GB_BM * 2)) void k_gemm_big(const
 #ifndef TT_GWEXP_NOEPI
 #define TT_GWEXP_NOEPI 0  // timing-only (results WRONG): k_gemm_wide without its epilogue
 #endif
-template <int ACT, bool BFO>
+template <int ACT, int BFO>
 __global__ __launch_bounds__(512, 1) void k_gemm_wide(const uint16_t* __restrict__ A, int64_t lda,
                                                       const uint16_t* __restrict__ W, int64_t ldw,
                                                       const float* __restrict__ bias,
                                                       const float* __restrict__ res, int64_t ldr,
                                                       float* __restrict__ C, int64_t ldc,
                                                       uint16_t* __restrict__ C16, int64_t ldc16,
-                                                      int M, int N, int K, int act) {
+                                                      int M, int N, int K, int act, int kx) {
   constexpr int BM = 256, BN = 256, BK = 64, EPC = 8, SLOTS = 2;
   constexpr int A_B = BM * 128, STAGE_B = A_B + BN * 128;
   __shared__ __attribute__((aligned(16))) char smem[SLOTS * STAGE_B];
@@ -700,11 +780,11 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wide(const uint16_t* __restrict
   };
   auto issue = [&](const Offs& o, int kt, int gs) __attribute__((always_inline)) {
     char* st = smem + (gs & 1) * STAGE_B;
-    const int64_t k0 = (int64_t)kt * BK;
+    const int64_t k0 = (int64_t)kt * BK, ka = x3c_acol(k0, kx);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(A + o.a[j] + k0),
+          (const __attribute__((address_space(1))) void*)(A + o.a[j] + ka),
           (__attribute__((address_space(3))) void*)(st + 1024 * (w + 8 * j)), 16, 0, 0);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -856,7 +936,9 @@ TT_CHECK_EXP(TT_GEXP_NOSTORE || TT_GWEXP_NOEPI || TT_GLEXP_NOW || TT_GLEXP_NOEPI
 
 // BM = 128 (8 waves of 64 x 96) or 96 (8 waves of 48 x 96: a batch of ~18k token rows is
 // 144 tiles of 128 on 256 CUs, 192 of 96 -- tt_gemm_ln_bf16 picks by rounds x tile cost).
-template <int BM>
+// SPL: the x3c encoder -- A and W are the K-concatenated split operands (kx = K / 3, see
+// x3c_acol) and x's bf16 copy is the [hi | lo] plane pair (X16 row: hi at n, lo at GL_H + n).
+template <int BM, bool SPL = false>
 __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__ A, int64_t lda,
                                                     const uint16_t* __restrict__ W, int64_t ldw,
                                                     const float* __restrict__ bias,
@@ -864,9 +946,11 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
                                                     const float* __restrict__ beta, float eps,
                                                     float* __restrict__ X, int64_t ldx,
                                                     uint16_t* __restrict__ X16, int64_t ldx16,
-                                                    int M, int K) {
+                                                    int M, int K, int kx) {
   constexpr int BK = 64, EPC = 8, MI = BM / 32, WR = BM / 2;  // 16-row blocks / rows per wave
-  constexpr int A_B = BM * 128, WBASE = GL_ASLOTS * A_B, STORES = MI * GL_NJ * 2;
+  constexpr int A_B = BM * 128, WBASE = GL_ASLOTS * A_B;
+  // stores per lane of a full tile's epilogue (vmcnt holds at most 63: a stronger wait is safe)
+  constexpr int STORES = MI * GL_NJ * (SPL ? 3 : 2) > 63 ? 63 : MI * GL_NJ * (SPL ? 3 : 2);
   static_assert(BM == 128 || BM == 96, "k_gemm_ln: BM");
   __shared__ __attribute__((aligned(16))) char smem[WBASE + GL_WSLOTS * GL_W_B];
   __shared__ float red[2][4][BM];  // [mean | var pass][wave column wn][tile row]
@@ -909,11 +993,11 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
   };
   auto issue_a = [&](const int64_t (&ao)[2], int kt, int t) __attribute__((always_inline)) {
     char* st = smem + (t % GL_ASLOTS) * A_B;
-    const int64_t k0 = (int64_t)kt * BK;
+    const int64_t k0 = (int64_t)kt * BK, ka = x3c_acol(k0, kx);
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(A + ao[j] + k0),
+          (const __attribute__((address_space(1))) void*)(A + ao[j] + ka),
           (__attribute__((address_space(3))) void*)(st + 1024 * apiece(j)), 16, 0,
           TT_GL_NT ? 2 : 0);
   };
@@ -1114,8 +1198,15 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
         for (int j = 0; j < GL_NJ; ++j) {
           const int n = nw0 + 16 * j;
           *(f32x4*)(X + m * ldx + n) = acc[i][j];
-          *(uint2*)(X16 + m * ldx16 + n) = uint2{pack_bf16_hw(acc[i][j][0], acc[i][j][1]),
-                                                  pack_bf16_hw(acc[i][j][2], acc[i][j][3])};
+          const uint2 hv = uint2{pack_bf16_hw(acc[i][j][0], acc[i][j][1]),
+                                 pack_bf16_hw(acc[i][j][2], acc[i][j][3])};
+          *(uint2*)(X16 + m * ldx16 + n) = hv;
+          if constexpr (SPL)
+            *(uint2*)(X16 + m * ldx16 + GL_H + n) =
+                uint2{pack_bf16_hw(acc[i][j][0] - __uint_as_float(hv.x << 16),
+                                   acc[i][j][1] - __uint_as_float(hv.x & 0xffff0000u)),
+                      pack_bf16_hw(acc[i][j][2] - __uint_as_float(hv.y << 16),
+                                   acc[i][j][3] - __uint_as_float(hv.y & 0xffff0000u))};
         }
       }
     } else {
@@ -1127,8 +1218,15 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
         for (int j = 0; j < GL_NJ; ++j) {
           const int n = nw0 + 16 * j;
           *(f32x4*)(X + m * ldx + n) = acc[i][j];
-          *(uint2*)(X16 + m * ldx16 + n) = uint2{pack_bf16_hw(acc[i][j][0], acc[i][j][1]),
-                                                  pack_bf16_hw(acc[i][j][2], acc[i][j][3])};
+          const uint2 hv = uint2{pack_bf16_hw(acc[i][j][0], acc[i][j][1]),
+                                 pack_bf16_hw(acc[i][j][2], acc[i][j][3])};
+          *(uint2*)(X16 + m * ldx16 + n) = hv;
+          if constexpr (SPL)
+            *(uint2*)(X16 + m * ldx16 + GL_H + n) =
+                uint2{pack_bf16_hw(acc[i][j][0] - __uint_as_float(hv.x << 16),
+                                   acc[i][j][1] - __uint_as_float(hv.x & 0xffff0000u)),
+                      pack_bf16_hw(acc[i][j][2] - __uint_as_float(hv.y << 16),
+                                   acc[i][j][3] - __uint_as_float(hv.y & 0xffff0000u))};
         }
       }
     }
@@ -1187,7 +1285,8 @@ __global__ __launch_bounds__(256) void k_embed_ln(const int32_t* __restrict__ id
                                                   const float* __restrict__ gamma,
                                                   const float* __restrict__ beta, float eps,
                                                   float* __restrict__ y, uint16_t* __restrict__ y16,
-                                                  int H) {
+                                                  int H, int split16) {
+  // split16: y16 rows are [hi | lo] planes (ld 2H) for the x3c encoder, else bf16 copies (ld H)
   // blocks (sequence, chunk of 4 tokens), wave per token (the position is t - cu[seq]; a
   // per-token binary search over cu was 13 dependent loads per token at 5k sequences).  Was a
   // block per sequence whose waves walked its tokens: at configs[1]'s 256 sequences that is
@@ -1226,7 +1325,11 @@ __global__ __launch_bounds__(256) void k_embed_ln(const int32_t* __restrict__ id
       if (e < H) {
         const float o = (v[i] - mean) * rstd * gamma[e] + beta[e];
         y[t * H + e] = o;
-        if (y16) y16[t * H + e] = f32_to_bf16_rne(o);
+        if (y16) {
+          const uint16_t hv = f32_to_bf16_rne(o);
+          y16[t * (split16 ? 2 * H : H) + e] = hv;
+          if (split16) y16[t * 2 * H + H + e] = f32_to_bf16_rne(o - __uint_as_float((uint32_t)hv << 16));
+        }
       }
     }
   }
@@ -1309,7 +1412,10 @@ __global__ __launch_bounds__(256) void k_attn32_mfma(const TI* __restrict__ qkv,
                                                      const int32_t* __restrict__ cu, int H,
                                                      int heads, float scale,
                                                      float* __restrict__ out, int64_t ldo,
-                                                     uint16_t* __restrict__ out16) {
+                                                     uint16_t* __restrict__ out16,
+                                                     int split16) {
+  // split16 (X3 only, out == NULL): out16 rows [hi | lo] (ldo = 2H, lo at column H + c), the
+  // A operand of the x3c Wo GEMM
   constexpr int DH = 32;
   constexpr int ES = BF ? 2 : 4;
   constexpr int KROW = DH * ES + 16;
@@ -1514,8 +1620,14 @@ __global__ __launch_bounds__(256) void k_attn32_mfma(const TI* __restrict__ qkv,
         if (out) *(f32x4*)(out + (int64_t)(t0 + q0 + ql) * ldo + h * DH + 16 * db + 4 * g) = o;
         if (out16) {  // 4 consecutive dims: one 8-B store
           uint16_t* o16 = out16 + (int64_t)(t0 + q0 + ql) * ldo + h * DH + 16 * db + 4 * g;
-          *(uint2*)o16 = uint2{(uint32_t)f32_to_bf16_rne(o[0]) | ((uint32_t)f32_to_bf16_rne(o[1]) << 16),
-                               (uint32_t)f32_to_bf16_rne(o[2]) | ((uint32_t)f32_to_bf16_rne(o[3]) << 16)};
+          const uint2 hv = uint2{(uint32_t)f32_to_bf16_rne(o[0]) | ((uint32_t)f32_to_bf16_rne(o[1]) << 16),
+                                 (uint32_t)f32_to_bf16_rne(o[2]) | ((uint32_t)f32_to_bf16_rne(o[3]) << 16)};
+          *(uint2*)o16 = hv;
+          if (X3 && split16)
+            *(uint2*)(o16 + H) = uint2{pack_bf16_hw(o[0] - __uint_as_float(hv.x << 16),
+                                                    o[1] - __uint_as_float(hv.x & 0xffff0000u)),
+                                       pack_bf16_hw(o[2] - __uint_as_float(hv.y << 16),
+                                                    o[3] - __uint_as_float(hv.y & 0xffff0000u))};
         }
       }
     }
@@ -1739,6 +1851,10 @@ bool gemm_wide_disabled() {  // TT_GEMM_WIDE=0: keep 256x128 tiles for the wide 
   static const bool off = env_switch("TT_GEMM_WIDE", 1) == 0;
   return off;
 }
+bool x3c_enabled() {  // TT_X3C=0: the x3 path's split-in-loop GEMMs (A/B timing, tests)
+  static const bool on = env_switch("TT_X3C", 1) != 0;
+  return on;
+}
 int gemm_big_variant() {  // TT_GEMM_BIG: 0 = 128x128 tiles only, 1 = 256x128 ring (default),
                           // 2 = 128x128 ring, two blocks per CU, 3 = 256x256 ring
   static const int v = [] {
@@ -1784,18 +1900,18 @@ static int gemm_f32_impl(const float* A, int64_t lda, const float* W, int64_t ld
     // 128x128 two-stage kernel left the MFMA pipes ~75% idle on DMA latency
     hipLaunchKernelGGL((k_gemm_big<256, 3, -1, false, float>), dim3(ncu), dim3(512), 0,
                        (hipStream_t)stream, A, lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16,
-                       ldc16, M, N, K, act);
+                       ldc16, M, N, K, act, 0);
     return check_launch("tt_gemm_x3(persistent)");
   }
   if (wx3)
     hipLaunchKernelGGL((k_gemm<float, 2>), dim3(nblk), dim3(256), 0, (hipStream_t)stream, A,
-                       lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
+                       lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act, 0, 0);
   else if (x3)
     hipLaunchKernelGGL((k_gemm<float, 1>), dim3(nblk), dim3(256), 0, (hipStream_t)stream, A,
-                       lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
+                       lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act, 0, 0);
   else
     hipLaunchKernelGGL((k_gemm<float, 0>), dim3(nblk), dim3(256), 0, (hipStream_t)stream, A,
-                       lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
+                       lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act, 0, 0);
   return check_launch(wx3 ? "tt_gemm_x3w" : x3 ? "tt_gemm_x3" : "tt_gemm_f32");
 }
 
@@ -1830,6 +1946,17 @@ extern "C" int tt_x3_split_weights(const float* W, int64_t ldw, int32_t N, int32
   return check_launch("tt_x3_split_weights");
 }
 
+extern "C" int tt_x3c_weights(const float* W, int64_t ldw, int32_t N, int32_t K, uint16_t* out,
+                              int64_t ld_out, void* stream) {
+  TT_REQUIRE(N >= 0 && K >= 0, "negative size");
+  if (N == 0 || K == 0) return TT_OK;
+  TT_REQUIRE(W && out && ldw >= K && ld_out >= 3 * (int64_t)K, "null pointer or ld too small");
+  const int64_t n = (int64_t)N * K;
+  hipLaunchKernelGGL(k_x3c_w, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, W, ldw, N, K, out, ld_out);
+  return check_launch("tt_x3c_weights");
+}
+
 extern "C" int tt_gemm_x3w(const float* A, int64_t lda, const uint16_t* Wx3, int64_t ldwx3,
                            const float* bias, const float* residual, int64_t ldr, float* C,
                            int64_t ldc, uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N,
@@ -1839,10 +1966,12 @@ extern "C" int tt_gemm_x3w(const float* A, int64_t lda, const uint16_t* Wx3, int
                        act, stream, true, Wx3, ldwx3);
 }
 
-extern "C" int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
-                            const float* bias, const float* residual, int64_t ldr, float* C,
-                            int64_t ldc, uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N,
-                            int32_t K, int32_t act, void* stream) {
+// bf16 GEMM dispatch.  kx > 0: the x3c form (x3c_acol; K = 3 kx, A [M, 2 kx] planes, W [N, 3 kx]);
+// split: C_bf16 receives [hi | lo] planes (C == NULL, residual == NULL, ldc16 >= 2N).
+static int gemm_bf16_impl(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
+                          const float* bias, const float* residual, int64_t ldr, float* C,
+                          int64_t ldc, uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N,
+                          int32_t K, int32_t act, void* stream, int32_t kx, bool split) {
   TT_REQUIRE(M >= 0 && N >= 0 && K >= 0, "negative size");
   if (M == 0 || N == 0) return TT_OK;
   if (K % GemmElt<uint16_t>::BK != 0)
@@ -1851,6 +1980,11 @@ extern "C" int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, i
   TT_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0,
              "A/W must be 16-B aligned with lda, ldw % 8 == 0");
   TT_REQUIRE(act >= 0 && act <= 2, "bad activation");
+  TT_REQUIRE(kx == 0 || (kx % 64 == 0 && K == 3 * kx && lda >= 2 * (int64_t)kx),
+             "x3c: K == 3 kx, kx % 64 == 0, A holds [hi | lo] (lda >= 2 kx)");
+  TT_REQUIRE(!split || (!C && !residual && C_bf16 && N % 8 == 0 && ldc16 >= 2 * (int64_t)N &&
+                        ldc16 % 8 == 0 && ((uintptr_t)C_bf16 % 16) == 0),
+             "split output: C_bf16 only, N % 8 == 0, ldc16 >= 2N (16-B aligned rows)");
   // large M: the persistent 256x128 ring kernel (one block per CU) once there are at least
   // two tiles per CU
   const int nbig = ((M + 255) / 256) * ((N + GB_BN - 1) / GB_BN);
@@ -1861,9 +1995,21 @@ extern "C" int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, i
     const bool bfo = !C && !residual && C_bf16 && ldc16 % 8 == 0 && ((uintptr_t)C_bf16 % 16) == 0;
     auto launch = [&](auto kern, int blocks, int threads) {
       hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, A, lda, W, ldw,
-                         bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
+                         bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act, kx);
       return check_launch("tt_gemm_bf16(persistent)");
     };
+    if (split) {  // x3c FFN1 (GELU) -> the W2 GEMM's [hi | lo] planes
+      const int64_t mt = (M + 255) / 256, ntw = mt * ((N + 255) / 256), ntn = mt * ((N + 127) / 128);
+      const bool narrow = ntw <= 2 * ncu && ((ntn + ncu - 1) / ncu) * 54 < ((ntw + ncu - 1) / ncu) * 100;
+      if (variant == 3 || (variant == 1 && N >= 1024 && !gemm_wide_disabled() && !narrow)) {
+        if (act == ACT_GELU) return launch(k_gemm_wide<ACT_GELU, 2>, ncu, 512);
+        if (act == ACT_NONE) return launch(k_gemm_wide<ACT_NONE, 2>, ncu, 512);
+        return launch(k_gemm_wide<ACT_RELU, 2>, ncu, 512);
+      }
+      if (act == ACT_GELU) return launch(k_gemm_big<256, 3, ACT_GELU, 2>, ncu, 512);
+      if (act == ACT_NONE) return launch(k_gemm_big<256, 3, ACT_NONE, 2>, ncu, 512);
+      return launch(k_gemm_big<256, 3, ACT_RELU, 2>, ncu, 512);
+    }
     // default: 256x256 tiles for the wide bf16-only GEMMs (QKV N = 1152, FFN1 N = 1536:
     // 534 / 747 us vs 586 / 824 us with 256x128 at 370k tokens), 256x128 otherwise
     // ... unless M is small enough that 256x256 tiles quantise badly onto the CUs (at most
@@ -1891,14 +2037,33 @@ extern "C" int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, i
   }
   const int nblk = ((M + GM_BM - 1) / GM_BM) * ((N + GM_BN - 1) / GM_BN);
   hipLaunchKernelGGL((k_gemm<uint16_t, 0>), dim3(nblk), dim3(256), 0, (hipStream_t)stream, A, lda, W,
-                     ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
+                     ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act, kx,
+                     split ? N : 0);
   return check_launch("tt_gemm_bf16");
 }
 
-extern "C" int tt_gemm_ln_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
-                               const float* bias, const float* gamma, const float* beta,
-                               float eps, float* x, int64_t ldx, uint16_t* x_bf16, int64_t ldx16,
-                               int32_t M, int32_t H, int32_t K, void* stream) {
+extern "C" int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
+                            const float* bias, const float* residual, int64_t ldr, float* C,
+                            int64_t ldc, uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N,
+                            int32_t K, int32_t act, void* stream) {
+  return gemm_bf16_impl(A, lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act,
+                        stream, 0, false);
+}
+
+extern "C" int tt_gemm_x3c(const uint16_t* A2, int64_t lda2, const uint16_t* W3, int64_t ldw3,
+                           const float* bias, const float* residual, int64_t ldr, float* C,
+                           int64_t ldc, uint16_t* C_split, int64_t ldc_split, int32_t M,
+                           int32_t N, int32_t K, int32_t act, void* stream) {
+  TT_REQUIRE(K > 0 && K % 64 == 0, "tt_gemm_x3c: need K % 64 == 0");
+  TT_REQUIRE((C != nullptr) != (C_split != nullptr), "tt_gemm_x3c: exactly one of C, C_split");
+  return gemm_bf16_impl(A2, lda2, W3, ldw3, bias, residual, ldr, C, ldc, C_split, ldc_split, M, N,
+                        3 * K, act, stream, K, C_split != nullptr);
+}
+
+static int gemm_ln_impl(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
+                        const float* bias, const float* gamma, const float* beta, float eps,
+                        float* x, int64_t ldx, uint16_t* x_bf16, int64_t ldx16, int32_t M,
+                        int32_t H, int32_t K, void* stream, int32_t kx) {
   TT_REQUIRE(M >= 0 && K >= 0, "negative size");
   if (M == 0) return TT_OK;
   if (H != GL_H) return fail(TT_ERR_UNSUPPORTED, "tt_gemm_ln_bf16: H must be 384");
@@ -1919,10 +2084,36 @@ extern "C" int tt_gemm_ln_bf16(const uint16_t* A, int64_t lda, const uint16_t* W
                    ((t96 + ncu - 1) / ncu) * (96 + 32) < ((t128 + ncu - 1) / ncu) * (128 + 32);
   const int ntiles = (int)(b96 ? t96 : t128);
   const int grid = ntiles < ncu ? ntiles : ncu;
+  if (kx > 0) {
+    TT_REQUIRE(kx % 64 == 0 && K == 3 * kx && lda >= 2 * (int64_t)kx && ldx16 >= 2 * GL_H &&
+                   ldx16 % 8 == 0,
+               "x3c gemm_ln: K == 3 kx, A [hi | lo] (lda >= 2 kx), x planes (ldx16 >= 768)");
+    hipLaunchKernelGGL((b96 ? k_gemm_ln<96, true> : k_gemm_ln<128, true>), dim3(grid), dim3(512), 0,
+                       (hipStream_t)stream, A, lda, W, ldw, bias, gamma, beta, eps, x, ldx,
+                       x_bf16, ldx16, M, K, kx);
+    return check_launch("tt_gemm_ln_x3c");
+  }
   hipLaunchKernelGGL(b96 ? k_gemm_ln<96> : k_gemm_ln<128>, dim3(grid), dim3(512), 0,
                      (hipStream_t)stream, A, lda, W, ldw, bias, gamma, beta, eps, x, ldx, x_bf16,
-                     ldx16, M, K);
+                     ldx16, M, K, 0);
   return check_launch("tt_gemm_ln_bf16");
+}
+
+extern "C" int tt_gemm_ln_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
+                               const float* bias, const float* gamma, const float* beta,
+                               float eps, float* x, int64_t ldx, uint16_t* x_bf16, int64_t ldx16,
+                               int32_t M, int32_t H, int32_t K, void* stream) {
+  return gemm_ln_impl(A, lda, W, ldw, bias, gamma, beta, eps, x, ldx, x_bf16, ldx16, M, H, K,
+                      stream, 0);
+}
+
+extern "C" int tt_gemm_ln_x3c(const uint16_t* A2, int64_t lda2, const uint16_t* W3, int64_t ldw3,
+                              const float* bias, const float* gamma, const float* beta, float eps,
+                              float* x, int64_t ldx, uint16_t* x_split, int64_t ldx_split,
+                              int32_t M, int32_t H, int32_t K, void* stream) {
+  TT_REQUIRE(K > 0 && K % 64 == 0, "tt_gemm_ln_x3c: need K % 64 == 0");
+  return gemm_ln_impl(A2, lda2, W3, ldw3, bias, gamma, beta, eps, x, ldx, x_split, ldx_split, M,
+                      H, 3 * K, stream, K);
 }
 
 extern "C" int tt_layernorm_f32(const float* x, int64_t ldx, const float* gamma,
@@ -1938,16 +2129,18 @@ extern "C" int tt_layernorm_f32(const float* x, int64_t ldx, const float* gamma,
   return check_launch("tt_layernorm_f32");
 }
 
-extern "C" int tt_attention_varlen(const float* qkv, int64_t ld_qkv, const int32_t* cu_seqlens,
-                                   int32_t n_seq, int32_t max_len, int32_t H, int32_t heads,
-                                   int32_t prec, float* out, int64_t ld_out, uint16_t* out_bf16,
-                                   void* stream) {
+static int attention_varlen_impl(const float* qkv, int64_t ld_qkv, const int32_t* cu_seqlens,
+                                 int32_t n_seq, int32_t max_len, int32_t H, int32_t heads,
+                                 int32_t prec, float* out, int64_t ld_out, uint16_t* out_bf16,
+                                 void* stream, int split16) {
   TT_REQUIRE(n_seq >= 0 && heads >= 1 && H % heads == 0, "bad n_seq / heads");
   TT_REQUIRE(prec == TT_PREC_F32 || prec == TT_PREC_BF16 || prec == TT_PREC_X3,
              "bad precision");
   if (n_seq == 0) return TT_OK;
   TT_REQUIRE(max_len >= 1 && max_len <= 512, "max_len must be in [1, 512]");
-  TT_REQUIRE(qkv && cu_seqlens && out, "null pointer");
+  TT_REQUIRE(qkv && cu_seqlens && (out || (split16 && out_bf16)), "null pointer");
+  TT_REQUIRE(!split16 || (prec == TT_PREC_X3 && !out && ld_out >= 2 * (int64_t)H),
+             "split context planes: x3 only, out_bf16 [T, >= 2H]");
   TT_REQUIRE(ld_qkv % 4 == 0 && ld_out % 4 == 0 && H % 4 == 0 && ((uintptr_t)qkv % 16) == 0 &&
                  ((uintptr_t)out % 16) == 0, "qkv/out must be 16-B aligned rows");
   if (H / heads != 32)
@@ -1964,15 +2157,23 @@ extern "C" int tt_attention_varlen(const float* qkv, int64_t ld_qkv, const int32
   const dim3 grid((unsigned)(n_seq * heads));
   if (bf)
     hipLaunchKernelGGL((k_attn32_mfma<true, float>), grid, dim3(256), smem, (hipStream_t)stream, qkv,
-                       ld_qkv, cu_seqlens, H, heads, scale, out, ld_out, out_bf16);
+                       ld_qkv, cu_seqlens, H, heads, scale, out, ld_out, out_bf16, 0);
   else if (x3)
     hipLaunchKernelGGL((k_attn32_mfma<false, float, true>), grid, dim3(256), smem,
                        (hipStream_t)stream, qkv, ld_qkv, cu_seqlens, H, heads, scale, out, ld_out,
-                       out_bf16);
+                       out_bf16, split16);
   else
     hipLaunchKernelGGL((k_attn32_mfma<false, float>), grid, dim3(256), smem, (hipStream_t)stream, qkv,
-                       ld_qkv, cu_seqlens, H, heads, scale, out, ld_out, out_bf16);
+                       ld_qkv, cu_seqlens, H, heads, scale, out, ld_out, out_bf16, 0);
   return check_launch("tt_attention_varlen");
+}
+
+extern "C" int tt_attention_varlen(const float* qkv, int64_t ld_qkv, const int32_t* cu_seqlens,
+                                   int32_t n_seq, int32_t max_len, int32_t H, int32_t heads,
+                                   int32_t prec, float* out, int64_t ld_out, uint16_t* out_bf16,
+                                   void* stream) {
+  return attention_varlen_impl(qkv, ld_qkv, cu_seqlens, n_seq, max_len, H, heads, prec, out,
+                               ld_out, out_bf16, stream, 0);
 }
 
 extern "C" int tt_attention_varlen_bf16(const uint16_t* qkv, int64_t ld_qkv,
@@ -2014,7 +2215,7 @@ extern "C" int tt_attention_varlen_bf16(const uint16_t* qkv, int64_t ld_qkv,
     return fail(TT_ERR_LAUNCH, "hipFuncSetAttribute(max dynamic LDS)");
   hipLaunchKernelGGL((k_attn32_mfma<true, uint16_t>), dim3((unsigned)(n_seq * heads)), dim3(256),
                      smem, (hipStream_t)stream, qkv, ld_qkv, cu_seqlens, H, heads,
-                     1.0f / sqrtf(32.0f), out, ld_out, out_bf16);
+                     1.0f / sqrtf(32.0f), out, ld_out, out_bf16, 0);
   return check_launch("tt_attention_varlen_bf16");
 }
 
@@ -2115,15 +2316,55 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
   };
   // bf16 path at H = 384 with row tiles filling the chip: GEMM + LayerNorm fused (k_gemm_ln)
   const bool fuse_ln = bf && H == GL_H && I % 64 == 0 && !gemm_ln_disabled();
+  // x3 at H = 384 with K-concatenated weights (wqkv_x3c ...): the x3c form -- every GEMM one
+  // bf16 GEMM over K' = 3K on the persistent kernels, Wo / W2 fused with their LayerNorm, the
+  // activations the GEMMs read written as [hi | lo] bf16 planes by their producers
+  bool x3c = x3 && H == GL_H && I % 64 == 0 && H / m->heads == 32 && !gemm_ln_disabled() &&
+             x3c_enabled();
+  for (int l = 0; x3c && l < NL; ++l)
+    x3c = m->layer[l].wqkv_x3c && m->layer[l].wo_x3c && m->layer[l].w1_x3c && m->layer[l].w2_x3c;
   EncWs w = enc_carve((char*)workspace, T, H, I, bf);
   if (!workspace || workspace_bytes < (int64_t)w.total)
     return fail(TT_ERR_WORKSPACE, "tt_bert_encode: workspace too small");
   hipStream_t st = (hipStream_t)stream;
+  if (x3c) {
+    // planes alias the f32 path's buffers (same bytes: [T, 2H] bf16 == [T, H] f32)
+    uint16_t* xs = (uint16_t*)w.y;
+    uint16_t* cs = (uint16_t*)w.ctx;
+    uint16_t* fs = (uint16_t*)w.ff;
+    const unsigned chunks = (unsigned)(max_len > 4 ? (max_len + 3) / 4 : 1);
+    hipLaunchKernelGGL(k_embed_ln, dim3((unsigned)n_seq, chunks), dim3(256), 0, st, ids,
+                       cu_seqlens, n_seq, T, m->word_emb, m->vocab, m->pos_emb, m->type_emb,
+                       m->emb_ln_g, m->emb_ln_b, m->ln_eps, w.x, xs, H, 1);
+    int rc = check_launch("k_embed_ln");
+    if (rc) return rc;
+    for (int l = 0; l < NL; ++l) {
+      const tt_bert_layer& L = m->layer[l];
+      rc = gemm_bf16_impl(xs, 2 * H, L.wqkv_x3c, 3 * H, L.bqkv, nullptr, 0, w.qkv, 3 * H, nullptr,
+                          0, (int)T, 3 * H, 3 * H, ACT_NONE, stream, H, false);
+      if (rc) return rc;
+      rc = attention_varlen_impl(w.qkv, 3 * H, cu_seqlens, n_seq, max_len, H, m->heads,
+                                 TT_PREC_X3, nullptr, 2 * H, cs, stream, 1);
+      if (rc) return rc;
+      rc = gemm_ln_impl(cs, 2 * H, L.wo_x3c, 3 * H, L.bo, L.ln1_g, L.ln1_b, m->ln_eps, w.x, H, xs,
+                        2 * H, (int)T, H, 3 * H, stream, H);
+      if (rc) return rc;
+      rc = gemm_bf16_impl(xs, 2 * H, L.w1_x3c, 3 * H, L.b1, nullptr, 0, nullptr, 0, fs, 2 * I,
+                          (int)T, I, 3 * H, ACT_GELU, stream, H, true);
+      if (rc) return rc;
+      rc = gemm_ln_impl(fs, 2 * I, L.w2_x3c, 3 * I, L.b2, L.ln2_g, L.ln2_b, m->ln_eps, w.x, H, xs,
+                        2 * H, (int)T, H, 3 * I, stream, I);
+      if (rc) return rc;
+    }
+    hipLaunchKernelGGL(k_mean_pool, dim3((unsigned)n_seq), dim3(256), 0, st, w.x, (int64_t)H,
+                       cu_seqlens, H, out_pooled, ld_out);
+    return check_launch("k_mean_pool");
+  }
   {
     const unsigned chunks = (unsigned)(max_len > 4 ? (max_len + 3) / 4 : 1);
     hipLaunchKernelGGL(k_embed_ln, dim3((unsigned)n_seq, chunks), dim3(256), 0, st, ids,
                        cu_seqlens, n_seq, T, m->word_emb, m->vocab, m->pos_emb, m->type_emb,
-                       m->emb_ln_g, m->emb_ln_b, m->ln_eps, w.x, bf ? w.x16 : nullptr, H);
+                       m->emb_ln_g, m->emb_ln_b, m->ln_eps, w.x, bf ? w.x16 : nullptr, H, 0);
     int rc = check_launch("k_embed_ln");
     if (rc) return rc;
   }

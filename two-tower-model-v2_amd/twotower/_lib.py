@@ -42,7 +42,8 @@ class BertLayer(ctypes.Structure):
     """tt_bert_layer (include/twotower_hip.h): device pointers of one BertLayer."""
     _fields_ = [(n, _vp) for n in (
         "wqkv", "bqkv", "wo", "bo", "ln1_g", "ln1_b", "w1", "b1", "w2", "b2", "ln2_g", "ln2_b",
-        "wqkv_bf16", "wo_bf16", "w1_bf16", "w2_bf16", "wqkv_x3", "wo_x3", "w1_x3", "w2_x3")]
+        "wqkv_bf16", "wo_bf16", "w1_bf16", "w2_bf16", "wqkv_x3", "wo_x3", "w1_x3", "w2_x3",
+        "wqkv_x3c", "wo_x3c", "w1_x3c", "w2_x3c")]
 
 
 class BertModel(ctypes.Structure):
@@ -104,6 +105,11 @@ SIGNATURES = {
     "tt_gemm_x3w": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64,
                                    _i32, _i32, _i32, _i32, _vp]),
     "tt_x3_split_weights": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp]),
+    "tt_x3c_weights": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp]),
+    "tt_gemm_x3c": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64,
+                                   _i32, _i32, _i32, _i32, _vp]),
+    "tt_gemm_ln_x3c": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, ctypes.c_float, _vp,
+                                       _i64, _vp, _i64, _i32, _i32, _i32, _vp]),
     "tt_gemm_bf16": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64,
                                     _i32, _i32, _i32, _i32, _vp]),
     "tt_gemm_ln_bf16": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, ctypes.c_float, _vp,

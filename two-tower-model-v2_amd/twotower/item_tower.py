@@ -93,6 +93,16 @@ def x3_split_weights(w: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def x3c_weights(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] f32 (device) -> the x3c GEMM's K-concatenated image [N, 3K] bf16 =
+    [bf16(W) | bf16(W - bf16(W)) | bf16(W)] (tt_x3c_weights)."""
+    N, K = w.shape
+    out = torch.empty((N, 3 * K), dtype=torch.bfloat16, device=w.device)
+    check(lib().tt_x3c_weights(w.data_ptr(), w.stride(0), N, K, out.data_ptr(), out.stride(0),
+                               stream_ptr()), "tt_x3c_weights")
+    return out
+
+
 class BertEncoder:
     """Device-resident BertModel weights + the fused HIP forward (tt_bert_encode).
 
@@ -104,7 +114,7 @@ class BertEncoder:
     _PREC = {"f32": _lib.TT_PREC_F32, "bf16": _lib.TT_PREC_BF16, "x3": _lib.TT_PREC_X3}
 
     def __init__(self, state_dict: Dict[str, torch.Tensor], cfg: Dict = MINILM_L12,
-                 device=None, prec: str = "bf16"):
+                 device=None, prec: str = "x3"):
         if prec not in self._PREC:
             raise ValueError("prec must be 'f32', 'x3' or 'bf16'")
         self.cfg = dict(cfg)
@@ -147,9 +157,12 @@ class BertEncoder:
             L.w2, L.b2 = ptr(w2), ptr(t(p + "output.dense.bias"))
             L.ln2_g = ptr(t(p + "output.LayerNorm.weight"))
             L.ln2_b = ptr(t(p + "output.LayerNorm.bias"))
-            if prec == "x3":  # the weights' hi / lo split once (tt_x3_split_weights)
+            if prec == "x3":  # the weights' hi / lo split once (tt_x3_split_weights), and
+                # their K-concatenated form for the x3c GEMMs (H = 384: tt_bert_encode's x3c path)
                 L.wqkv_x3, L.wo_x3, L.w1_x3, L.w2_x3 = (ptr(x3_split_weights(x))
                                                         for x in (wqkv, wo, w1, w2))
+                L.wqkv_x3c, L.wo_x3c, L.w1_x3c, L.w2_x3c = (ptr(x3c_weights(x))
+                                                            for x in (wqkv, wo, w1, w2))
             if prec == "bf16":
                 L.wqkv_bf16 = ptr(wqkv.to(torch.bfloat16))
                 L.wo_bf16 = ptr(wo.to(torch.bfloat16))
@@ -241,7 +254,7 @@ class ItemTower(nn.Module):
                  categorical_embedding_dim: int = 64, projection_hidden_dim: int = 256,
                  freeze_text_encoder: bool = True, text_encoder=None, tokenizer=None,
                  encoder_state_dict: Optional[Dict[str, torch.Tensor]] = None,
-                 encoder_cfg: Dict = MINILM_L12, prec: str = "bf16", seed: int = 0):
+                 encoder_cfg: Dict = MINILM_L12, prec: str = "x3", seed: int = 0):
         super().__init__()
         self.embedding_dim = embedding_dim
         self.use_categorical_features = use_categorical_features
