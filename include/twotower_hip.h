@@ -154,6 +154,13 @@ int tt_sharded_fallback_offset(int64_t n, int32_t d, int32_t nq, int32_t k, int6
  * per query.  sharded = 0: tt_scan_topk_bf16f32's workspace; 1: the full/finish workspace. */
 int tt_filter_workspace_layout(int64_t n, int32_t d, int32_t nq, int32_t k, int32_t sharded,
                                int64_t* offsets);
+/* Test hook (fault injection for the bounds checks of decoded candidate rows): the NEXT
+ * tt_scan_topk_bf16f32 call on this host thread corrupts query `query`'s best candidate key
+ * on the device so that its row decodes to 0xffffffff -- where = 1: a band key between the
+ * full level's selection and k_rerank (the large-batch path); where = 2: an exact key between
+ * k_filter_topm and k_final_topm (the nq <= 4 single pass).  The kernels must then never read
+ * that row and flag the query for the exact fallback.  where = 0 clears.  One-shot. */
+int tt_debug_plant_bad_row(int32_t where, int32_t query);
 int tt_sharded_filter_begin(const uint16_t* sample_bf16, int64_t n_sample, int32_t d, int64_t ld,
                             const float* q, int32_t nq, int64_t ld_q, int32_t k, float* stats,
                             void* workspace, int64_t workspace_bytes, void* stream);

@@ -20,6 +20,7 @@ for p in (ROOT, PKG, os.path.join(ROOT, "tests", "golden")):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); parity tests")
     config.addinivalue_line("markers", "slow: long-running (full-size) case")
+    config.addinivalue_line("markers", "perf: wall-clock guard on a GPU (not part of -m gpu)")
 
 
 def pytest_collection_modifyitems(config, items):
@@ -32,7 +33,7 @@ def pytest_collection_modifyitems(config, items):
         return
     skip = pytest.mark.skip(reason="no HIP device in this container")
     for item in items:
-        if "gpu" in item.keywords:
+        if "gpu" in item.keywords or "perf" in item.keywords:
             item.add_marker(skip)
 
 

@@ -191,34 +191,6 @@ def test_configs2_flagged_queries_fallback_bit_exact(K, oracle_mod, n_picked):
 
 
 @pytest.mark.slow
-def test_configs2_few_flagged_queries_fallback_cost(K):
-    """Cost guard (a performance property, kept apart from the parity tests above): 3 flagged
-    queries of a 10k batch add < 20% to the search (median of 7 each way).  Round 2's fallback
-    ran them as one 64-query f32 tile over the catalog: 1.43-1.48 ms on a ~6.9 ms search."""
-    n, d, k = 1_000_000, 384, 100
-    x, x16, q, q2, picked = _flagged_scenario(K, 3)
-    ws = torch.empty(K.filter_workspace_bytes(n, d, q.shape[0], k), dtype=torch.uint8,
-                     device="cuda")
-    bnd = bounds(K, x, x16, d)
-
-    def timed(qq, reps=7):
-        t = []
-        for _ in range(reps):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            K.scan_topk_bf16(x, x16, n, d, qq, k, bnd, workspace=ws)
-            e1.record()
-            torch.cuda.synchronize()
-            t.append(e0.elapsed_time(e1))
-        return sorted(t)[reps // 2]
-
-    timed(q, 2)
-    t_fb, t_none = timed(q), timed(q2)
-    print(f"search with 3 flagged queries {t_fb:.3f} ms, none flagged {t_none:.3f} ms")
-    assert t_fb < 1.2 * t_none
-
-
-@pytest.mark.slow
 def test_sharded_protocol_large_batch_w8(K, oracle_mod):
     """The W = 8 staged sharded filter with W.B = 4096 queries per rank launch (> 2048: the
     per-shard full level is the large-batch instantiation), 1M rows: merged results bit-exact

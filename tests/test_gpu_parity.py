@@ -86,6 +86,24 @@ def test_scan_bit_exact_vs_oracle(K, oracle_mod, n, d, nq, k):
     assert np.array_equal(s, rs)
 
 
+@pytest.mark.parametrize("n,d,nq,k", [(20000, 384, 3, 1025), (5000, 128, 2, 5000),
+                                      (3000, 768, 5, 2999)])
+def test_scan_large_k_bit_exact_vs_oracle(K, oracle_mod, n, d, nq, k):
+    """k > 1024 (faiss takes any k <= ntotal): every canonical score by the f32 MFMA GEMM, a
+    stable sort -- bit-exact ids and scores vs the oracle; a NaN row is never returned."""
+    rng = np.random.default_rng(n + k)
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
+    x[7] = np.nan
+    x[11] = x[12]  # an exact tie: the lower row first
+    q = oracle_mod.l2norm_rows(rng.standard_normal((nq, d)).astype(np.float32), 0)
+    s, i = K.scan_topk_large(dev_rows(x), n, d, dev_rows(q), k, row_base=5)
+    s, i = s.cpu().numpy(), i.cpu().numpy()
+    rs, ri = oracle_mod.scan_topk(x, q, k, row_base=5)
+    assert np.array_equal(i, ri)
+    assert np.array_equal(s, rs)
+    assert not np.any(i == 7 + 5)
+
+
 BF16_CASES = [c for c in SCAN_CASES if c[3] <= 128] + [
     (2049, 384, 5, 128),     # two filter levels, k at the filter's maximum
     (300000, 384, 40, 100),  # tile-max first level at stride 16; 1024 full-level slabs
@@ -598,6 +616,38 @@ def test_sharded_finish_corrupt_band_row_falls_back(K, oracle_mod):
     rs, ri = oracle_mod.scan_topk(x, q, k)
     assert np.array_equal(mi, ri) and np.array_equal(ms, rs)
     assert fb[0] >= 1 and "q" in planted
+
+
+@pytest.mark.parametrize("where,n,nq", [(1, 100000, 300), (1, 300000, 2100), (2, 100000, 1),
+                                         (2, 1000000, 3)])
+def test_bf16_filter_corrupt_key_falls_back(K, oracle_mod, where, n, nq):
+    """Bounds check of decoded candidate rows on the single-GPU paths (tt_debug_plant_bad_row
+    corrupts one query's best candidate key on the device so that its row decodes to
+    0xffffffff): where 1 = a band key between the full level and k_rerank (the large-batch
+    path), 2 = an exact key between k_filter_topm and k_final_topm (the one-buyer single pass).
+    The row is never read: the query takes the exact f32 fallback, every result stays
+    bit-exact, nothing faults; the hook is one-shot (the next call takes no fallback)."""
+    from twotower import _lib
+
+    rng = np.random.default_rng(n + nq + where)
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, 384)).astype(np.float32), 0)
+    q = oracle_mod.l2norm_rows(rng.standard_normal((nq, 384)).astype(np.float32), 0)
+    db, qd = dev_rows(x), dev_rows(q)
+    db16 = db.to(torch.bfloat16)
+    b = bounds(K, db, db16, 384)
+    k = 100
+    ws = torch.empty(K.filter_workspace_bytes(n, 384, nq, k), dtype=torch.uint8, device="cuda")
+    sub = np.unique(np.linspace(0, nq - 1, min(nq, 64)).round().astype(int))
+    qi = int(sub[len(sub) // 2])
+    rs, ri = oracle_mod.scan_topk(x, q[sub], k)
+    for planted in (True, False):
+        if planted:
+            _lib.check(_lib.lib().tt_debug_plant_bad_row(where, qi), "plant")
+        s, i = K.scan_topk_bf16(db, db16, n, 384, qd, k, b, workspace=ws)
+        fb = K.filter_fallback_count(ws, n, 384, nq, k)
+        assert np.array_equal(i.cpu().numpy()[sub], ri)
+        assert np.array_equal(s.cpu().numpy()[sub], rs)
+        assert fb == (1 if planted else 0), (planted, fb)
 
 
 @pytest.mark.parametrize("E,S", [(384, 20), (768, 20), (768, 100)])

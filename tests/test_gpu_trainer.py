@@ -210,3 +210,19 @@ def test_trainer_epochs_reference_batches(tmp_path, aggregation):
     for k in tr.step.m:
         assert torch.equal(tr2.step.m[k], tr.step.m[k]) and torch.equal(tr2.step.v[k], tr.step.v[k])
     assert all(torch.equal(v.cpu(), ref[k].cpu()) for k, v in model2.state_dict().items())
+    # resume INTO train(): it continues at the checkpoint's next epoch -- the saved epochs are
+    # not re-run and later checkpoints keep the epoch / Adam step numbering
+    tr3 = Trainer(_model(aggregation=aggregation, seed=9), train, val, config_path=str(cp),
+                  pad_to_batch_max=True)
+    tr3.set_product_metadata(meta)
+    tr3.load_checkpoint(tmp_path / "checkpoint_epoch_2.pt")
+    t_ck = tr3.step.t
+    assert tr3.start_epoch == 2 and t_ck == 3 * 4 + 2 * 4
+    calls = []
+    run_epoch = tr3.train_epoch
+    tr3.train_epoch = lambda: (calls.append(tr3.current_epoch), run_epoch())[1]
+    tr3.train()
+    assert calls == [2, 3] and tr3.step.t == t_ck + 2 * len(train)
+    ck4 = torch.load(tmp_path / "checkpoint_epoch_4.pt", weights_only=True)
+    assert ck4["epoch"] == 3
+    assert {int(float(e["step"])) for e in ck4["optimizer_state_dict"]["state"].values()} == {7 * 4}

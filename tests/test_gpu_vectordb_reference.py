@@ -142,3 +142,45 @@ def test_retrieve_endpoint_matches_reference_server(golden):
             if gp["product_id"] == rp["product_id"]:
                 assert {k: v for k, v in gp.items() if k != "score"} == \
                        {k: v for k, v in rp.items() if k != "score"}
+
+
+def test_retrieve_serving_path_threads_and_device_path_agree():
+    """VectorDatabase.retrieve / retrieve_batch run the prepared serving path
+    (FlatIPIndex.search_host: bound PreparedSearch, pinned staging, device normalisation).
+    Results equal the device path (normalize_queries + search) bit for bit, and four threads
+    calling retrieve concurrently on one index get the same answers as one thread."""
+    import threading
+
+    import torch
+
+    from twotower import VectorDatabase
+
+    rng = np.random.default_rng(11)
+    n, d, k = 20000, 384, 100
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    ids = [f"p{i}" for i in range(n)]
+    vdb = VectorDatabase(d)
+    vdb.build_index(x, ids)
+    q = rng.standard_normal((64, d)).astype(np.float32)
+    s_dev, i_dev = vdb.search(torch.from_numpy(q).cuda(), k)
+    s_dev, i_dev = s_dev.cpu().numpy(), i_dev.cpu().numpy()
+    want = [[(ids[j], float(s)) for j, s in zip(i_dev[b], s_dev[b])] for b in range(len(q))]
+    assert vdb.retrieve_batch(q, k=k) == want
+    assert [vdb.retrieve(q[b], k=k) for b in range(len(q))] == want
+    got, errs = [None] * len(q), []
+
+    def work(t):
+        try:
+            for b in range(t, len(q), 4):
+                for _ in range(3):
+                    got[b] = vdb.retrieve(q[b], k=k)
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs and got == want
+    assert vdb.retrieve(q[0], k=n + 5)[:k] == want[0]  # k clamp (:159): all rows, same head

@@ -3096,6 +3096,49 @@ int filter_finish(const FilterWs& w, const float* db, int64_t n, int32_t d, int6
 }
 }  // namespace
 
+// ---- fault injection for the decoded-row bounds checks (tests only, tt_debug_plant_bad_row)
+namespace {
+thread_local int g_plant_where = 0, g_plant_query = 0;
+
+// one wave: the largest key of keys[0..n) gets row ~0 (low word 0); xk != nullptr: the key of
+// the same slot in xk (the single pass's exact keys) instead.  keys[j] valid for j < n only.
+__global__ void k_debug_plant(uint64_t* keys, uint64_t* xk, const int* counts, int n_lists,
+                              int list_cap) {
+  const int lane = threadIdx.x;
+  uint64_t best = 0ull;
+  int64_t at = -1;
+  for (int b = 0; b < n_lists; ++b) {
+    const int c = counts[b];
+    for (int j = lane; j < c && j < list_cap; j += 64) {
+      const int64_t o = (int64_t)b * list_cap + j;
+      if (keys[o] > best) {
+        best = keys[o];
+        at = o;
+      }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t ob = __shfl_xor(best, o, 64);
+    const int64_t oa = __shfl_xor(at, o, 64);
+    if (ob > best) {
+      best = ob;
+      at = oa;
+    }
+  }
+  if (lane == 0 && at >= 0) {
+    uint64_t* t = xk ? xk : keys;
+    if (t[at] != 0ull) t[at] &= 0xffffffff00000000ull;
+  }
+}
+}  // namespace
+
+extern "C" int tt_debug_plant_bad_row(int32_t where, int32_t query) {
+  TT_REQUIRE(where >= 0 && where <= 2 && query >= 0, "bad arguments");
+  g_plant_where = where;
+  g_plant_query = query;
+  return TT_OK;
+}
+
 extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n,
                                     int32_t d, int64_t ld_db, int64_t row_base, const float* q,
                                     int32_t nq, int64_t ld_q, int32_t k, float x_norm_max,
@@ -3139,6 +3182,14 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
     if ((rc = check_launch("k_filter_topm"))) return rc;
     if (ev_stop && hipEventRecord((hipEvent_t)ev_stop, st) != hipSuccess)
       return fail(TT_ERR_LAUNCH, "hipEventRecord(stop)");
+    if (g_plant_where == 2 && g_plant_query < nq) {  // test hook: corrupt an exact key
+      hipLaunchKernelGGL(k_debug_plant, dim3(1), dim3(64), 0, st,
+                         w.lists + (int64_t)g_plant_query * G * TM_M,
+                         xkeys + (int64_t)g_plant_query * G * TM_M,
+                         w.counts + (int64_t)g_plant_query * G, G, TM_M);
+      g_plant_where = 0;
+      if ((rc = check_launch("k_debug_plant"))) return rc;
+    }
     switch (ep) {
 #define TT_TF(E)                                                                              \
   case E:                                                                                     \
@@ -3190,6 +3241,13 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
     if ((rc = check_launch("k_final_small"))) return rc;
     return scan_f32_select_fused(db, n, d, ld_db, row_base, q, nq, ld_q, k, w.qsel, w.qsel_n,
                                  w.done, out_score, out_idx, w.scan_ws, w.scan_ws_bytes, st);
+  }
+  if (g_plant_where == 1 && g_plant_query < nq) {  // test hook: corrupt a band key
+    hipLaunchKernelGGL(k_debug_plant, dim3(1), dim3(64), 0, st,
+                       w.band + (int64_t)g_plant_query * BAND_CAP, (uint64_t*)nullptr,
+                       w.band_n + g_plant_query, 1, BAND_CAP);
+    g_plant_where = 0;
+    if ((rc = check_launch("k_debug_plant"))) return rc;
   }
   return filter_finish(w, db, n, d, ld_db, row_base, q, nq, ld_q, k, ep, out_score, out_idx, st);
 }

@@ -105,6 +105,7 @@ SIGNATURES = {
     "tt_gemm_x3w": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64,
                                    _i32, _i32, _i32, _i32, _vp]),
     "tt_x3_split_weights": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp]),
+    "tt_debug_plant_bad_row": (ctypes.c_int, [_i32, _i32]),
     "tt_x3c_weights": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp]),
     "tt_gemm_x3c": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64,
                                    _i32, _i32, _i32, _i32, _vp]),
@@ -199,3 +200,29 @@ def padded_dim(d: int) -> int:
     if ep < 0:
         raise RuntimeError(f"embedding dim {d} unsupported by the scan kernel (max 768)")
     return ep
+
+
+class StreamWorkspaces:
+    """Device scratch buffers keyed by the current HIP stream, least-recently-used first out
+    (at most ``maxsize`` kept).  Kernels on one stream are ordered, so a workspace per stream
+    never races; an evicted buffer returns to torch's caching allocator, whose blocks are
+    reused on the stream that freed them only, so in-flight work on it stays safe."""
+
+    def __init__(self, maxsize: int = 4):
+        import collections
+
+        self._d = collections.OrderedDict()
+        self.maxsize = maxsize
+
+    def get(self, need: int, device) -> "torch.Tensor":
+        st = stream_ptr()
+        ws = self._d.pop(st, None)
+        if ws is None or ws.numel() < need:
+            ws = torch.empty(max(need, 1), dtype=torch.uint8, device=device)
+        self._d[st] = ws
+        while len(self._d) > self.maxsize:
+            self._d.popitem(last=False)
+        return ws
+
+    def __len__(self) -> int:
+        return len(self._d)

@@ -171,7 +171,8 @@ class BertEncoder:
         m.layer = ctypes.cast(layers, ctypes.POINTER(_lib.BertLayer))
         self._layers = layers
         self._model = m
-        self._ws = {}  # per HIP stream: encodes may run concurrently on several streams
+        # per HIP stream (encodes may run concurrently on several streams), bounded LRU
+        self._ws = _lib.StreamWorkspaces(4)
 
     @property
     def hidden(self) -> int:
@@ -198,9 +199,7 @@ class BertEncoder:
             raise ValueError(f"sequence longer than max_position_embeddings ({max_len})")
         need = self.workspace_bytes(T)
         st = stream_ptr()
-        ws = self._ws.get(st)
-        if ws is None or ws.numel() < need:
-            ws = self._ws[st] = torch.empty(need, dtype=torch.uint8, device=ids.device)
+        ws = self._ws.get(need, ids.device)
         check(lib().tt_bert_encode(ctypes.byref(self._model), ids.data_ptr(),
                                    cu_seqlens.data_ptr(), n, T, int(max_len),
                                    self._PREC[self.prec], out.data_ptr(), out.stride(0), ws.data_ptr(), ws.numel(), st),

@@ -57,6 +57,7 @@ class Trainer:
                                       prec=prec)
         self.optimizer = self.step  # Adam lives in the fused step (moments resident in HBM)
         self.current_epoch = 0
+        self.start_epoch = 0  # first epoch train() runs (load_checkpoint: saved epoch + 1)
         self.best_val_loss = float("inf")
         self.checkpoint_dir = Path(tc["checkpoint_dir"])
         self.product_metadata = None
@@ -181,14 +182,16 @@ class Trainer:
         if "optimizer_state_dict" in ck:
             self.step.load_optimizer_state_dict(self.model, ck["optimizer_state_dict"])
         self.current_epoch = int(ck.get("epoch", 0)) + 1
+        self.start_epoch = self.current_epoch  # train() continues from here
         self.best_val_loss = float(ck.get("best_val_loss", float("inf")))
         return ck
 
-    # reference :354-378
+    # reference :354-378 (a resumed Trainer continues at start_epoch: the checkpoint's epochs
+    # are not re-run, and the epoch labels of later checkpoints continue from it)
     def train(self):
         num_epochs = self.config["training"]["num_epochs"]
         save_every = self.config["training"]["save_every_n_epochs"]
-        for epoch in range(num_epochs):
+        for epoch in range(self.start_epoch, num_epochs):
             self.current_epoch = epoch
             train_loss = self.train_epoch()
             print(f"Epoch {epoch + 1}/{num_epochs} - Train Loss: {train_loss:.4f}")

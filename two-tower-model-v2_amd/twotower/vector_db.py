@@ -43,12 +43,15 @@ class FlatIPIndex:
         self._bounds_dev = torch.zeros(2, dtype=torch.float32, device=self.device)
         self.bounds = (0.0, 0.0)
         self.ntotal = 0
-        self._ws = None
-        self._prepared = {}  # (nq, k, ntotal, xb ptr) -> kernels.PreparedSearch (host search)
-        # the prepared searches and the workspace are shared state: host searches from
-        # several threads are serialised (faiss' search is re-entrant; the reference's /retrieve
-        # runs on one event-loop thread, server.py:212-244)
-        self._lock = threading.Lock()
+        self._ws = _lib.StreamWorkspaces(4)  # search_device's workspace, one per HIP stream
+        # host searches (the /retrieve path): per (nq, k, index state, stream) a bound
+        # kernels.PreparedSearch (k <= 128, nq <= 256) with its device query buffer and pinned
+        # host staging, so one buyer costs one H2D copy, the search launches and one D2H copy
+        self._prepared = {}
+        # shared state (prepared searches, staging buffers, workspaces) is guarded by one lock:
+        # faiss' search is re-entrant, and the reference's /retrieve may be called from several
+        # threads (server.py:212-244)
+        self._lock = threading.RLock()
 
     def _append(self, rows: torch.Tensor, rows16: torch.Tensor) -> None:
         if rows.shape[0]:  # build-time statistic over the new rows (max-combined)
@@ -90,40 +93,59 @@ class FlatIPIndex:
         if k < 1:
             raise RuntimeError("Error: 'k > 0' failed")  # faiss' own assertion text
         use_bf16 = method == "bf16" or (method == "auto" and k <= kernels.FILTER_KMAX)
+        if k > kernels.SCAN_KMAX:  # faiss takes any k: the exact all-scores edge path
+            return kernels.scan_topk_large(self.xb, self.ntotal, self.d, q, k,
+                                           row_base=self.row_base)
         if use_bf16:
             need = kernels.filter_workspace_bytes(self.ntotal, self.d, q.shape[0], k)
         else:
             need = kernels.scan_workspace_bytes(self.ntotal, self.d, q.shape[0], k)
-        if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
-        if use_bf16:
-            return kernels.scan_topk_bf16(self.xb, self.xb16, self.ntotal, self.d, q, k,
-                                          self.bounds, row_base=self.row_base,
-                                          workspace=self._ws)
-        return kernels.scan_topk(self.xb, self.ntotal, self.d, q, k, row_base=self.row_base,
-                                 workspace=self._ws)
+        with self._lock:  # the workspace cache is shared; the outputs are fresh per call
+            ws = self._ws.get(need, self.device)
+            if use_bf16:
+                return kernels.scan_topk_bf16(self.xb, self.xb16, self.ntotal, self.d, q, k,
+                                              self.bounds, row_base=self.row_base, workspace=ws)
+            return kernels.scan_topk(self.xb, self.ntotal, self.d, q, k,
+                                     row_base=self.row_base, workspace=ws)
+
+    def search_host(self, x: np.ndarray, k: int, normalize: bool = False):
+        """Host float32 [nq, d] queries -> host (D [nq,k] f32, I [nq,k] i64).  normalize=True
+        first applies the reference's q/(||q||+1e-8) on the device (vector_db.py:152-153,
+        189-190).  The serving path of VectorDatabase.retrieve / retrieve_batch."""
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        if x.ndim != 2 or x.shape[1] != self.d:
+            raise ValueError(f"search: expected [nq, {self.d}] float32 queries")
+        nq = x.shape[0]
+        with self._lock:  # staging buffers / prepared outputs are reused until copied out
+            key = (nq, k, self.ntotal, self.xb.data_ptr(), _lib.stream_ptr())
+            ent = self._prepared.get(key)
+            if ent is None:
+                if len(self._prepared) >= 8:
+                    self._prepared.clear()
+                pin = torch.cuda.is_available()
+                q = torch.zeros((nq, self.ep), dtype=torch.float32, device=self.device)
+                qh = torch.empty((nq, self.d), dtype=torch.float32, pin_memory=pin)
+                outh = (torch.empty((nq, k), dtype=torch.float32, pin_memory=pin),
+                        torch.empty((nq, k), dtype=torch.int64, pin_memory=pin))
+                ps = None
+                if 1 <= nq <= 256 and 1 <= k <= min(self.ntotal, kernels.FILTER_KMAX):
+                    ps = kernels.PreparedSearch(self.xb, self.xb16, self.ntotal, self.d, nq, k,
+                                                self.bounds, self.row_base)
+                ent = self._prepared[key] = (q, qh, outh, ps)
+            q, qh, outh, ps = ent
+            qh.numpy()[...] = x
+            q[:, : self.d].copy_(qh, non_blocking=True)
+            if normalize:
+                kernels.l2norm_rows(q, self.d, _lib.TT_NORM_ADD_EPS, out=q)
+            s, i = ps(q) if ps is not None else self.search_device(q, k)
+            outh[0].copy_(s, non_blocking=True)
+            outh[1].copy_(i, non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+            return outh[0].numpy().copy(), outh[1].numpy().copy()
 
     def search(self, x: np.ndarray, k: int):
         """faiss signature: float32 [nq, d] host queries -> (D [nq,k] f32, I [nq,k] i64) host."""
-        x = np.ascontiguousarray(x, dtype=np.float32)
-        q = torch.zeros((x.shape[0], self.ep), dtype=torch.float32, device=self.device)
-        q[:, : self.d].copy_(torch.from_numpy(x))
-        nq = x.shape[0]
-        with self._lock:  # outputs / workspace are reused: copied out before the next call
-            if 1 <= nq <= 256 and 1 <= k <= min(self.ntotal, kernels.FILTER_KMAX):
-                # the /retrieve pattern (one buyer per call): arguments, outputs and workspace
-                # are bound once per (nq, k, index state); results copied out before returning
-                key = (nq, k, self.ntotal, self.xb.data_ptr())
-                ps = self._prepared.get(key)
-                if ps is None:
-                    self._prepared.clear()
-                    ps = self._prepared[key] = kernels.PreparedSearch(
-                        self.xb, self.xb16, self.ntotal, self.d, nq, k, self.bounds,
-                        self.row_base)
-                s, i = ps(q)
-            else:
-                s, i = self.search_device(q, k)
-            return s.cpu().numpy(), i.cpu().numpy()
+        return self.search_host(x, k, normalize=False)
 
     def reconstruct(self, i: int) -> np.ndarray:
         return self.xb[i, : self.d].cpu().numpy()
@@ -235,18 +257,16 @@ class VectorDatabase:
         return self.index.search_device(q, k)
 
     def _search_host(self, query_embeddings: np.ndarray, k: int):
+        """Host queries -> host (scores, rows) through the index's prepared serving path
+        (FlatIPIndex.search_host: one H2D copy, the device normalisation, the search, one D2H
+        copy per call)."""
         x = np.ascontiguousarray(query_embeddings)
+        k = min(k, self.index.ntotal)  # reference :159 / :196
         if x.dtype != np.float32:
             # reference normalises in the input dtype, then casts (:189-193): do the same
             norms = np.linalg.norm(x, axis=1, keepdims=True)
-            x = (x / (norms + 1e-8)).astype(np.float32)
-            normalized = True
-        else:
-            normalized = False
-        q = torch.zeros((x.shape[0], self.index.ep), dtype=torch.float32, device=self.index.device)
-        q[:, : self.embedding_dim].copy_(torch.from_numpy(x))
-        s, i = self.search(q, k, normalized=normalized)
-        return s.cpu().numpy(), i.cpu().numpy()
+            return self.index.search_host((x / (norms + 1e-8)).astype(np.float32), k)
+        return self.index.search_host(x, k, normalize=True)
 
     def _to_results(self, scores: np.ndarray, indices: np.ndarray):
         out = []
