@@ -475,6 +475,31 @@ def test_gemm_bf16_only_output_and_misaligned_bias():
     assert torch.equal(only16, C16)
 
 
+@pytest.mark.parametrize("M,N,act", [(70001, 1152, 0), (65536, 1536, 1), (40000, 1280, 1),
+                                     (18340, 1536, 1)])
+def test_gemm_bf16_only_output_phase_pipelined(M, N, act):
+    """The bf16-only output at large M (k_gemm_pp, the phase-pipelined 256x256 persistent
+    kernel; ragged M and N tiles) equals the generic-output kernel's bf16 copy bit for bit --
+    the same MFMA k order, the same epilogue rounding -- and stays within the bf16 bar."""
+    from twotower import _lib
+
+    K = 384
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    A = torch.randn((M, K), generator=g, device="cuda")
+    W = torch.randn((N, K), generator=g, device="cuda") / K ** 0.5
+    b = torch.randn(N, generator=g, device="cuda")
+    C, C16 = _gemm(A, W, b, None, act, "bf16", want16=True)
+    only16 = torch.empty((M, N), device="cuda", dtype=torch.bfloat16)
+    a16, w16 = A.to(torch.bfloat16), W.to(torch.bfloat16)
+    _lib.check(_lib.lib().tt_gemm_bf16(a16.data_ptr(), K, w16.data_ptr(), K, b.data_ptr(), None,
+                                       0, None, N, only16.data_ptr(), N, M, N, K, act,
+                                       _lib.stream_ptr()), "gemm")
+    assert torch.equal(only16, C16)
+    ref = a16.double() @ w16.double().T + b.double()
+    ref = F.gelu(ref) if act == 1 else ref
+    torch.testing.assert_close(only16.double(), ref, rtol=1e-2, atol=1e-2)
+
+
 @pytest.mark.parametrize("M,K", [(1, 384), (127, 384), (129, 1536), (5000, 384),
                                  (70003, 1536), (65536, 384)])
 def test_gemm_ln_bf16_vs_torch(M, K):

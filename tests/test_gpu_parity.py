@@ -104,6 +104,31 @@ def test_scan_large_k_bit_exact_vs_oracle(K, oracle_mod, n, d, nq, k):
     assert not np.any(i == 7 + 5)
 
 
+@pytest.mark.parametrize("d,k", [(1000, 100), (1024, 10), (1536, 1100)])
+def test_vector_db_dims_above_768_bit_exact(K, oracle_mod, d, k):
+    """Embedding dims past the scan kernels' 768 (the reference accepts any embedding_dim,
+    vector_db.py:13,48): VectorDatabase builds, normalises and retrieves through the generic
+    exact path (f32 MFMA GEMM scores + key top-k) -- ids and scores bit-exact vs the oracle,
+    through retrieve_batch, retrieve and the device search."""
+    from twotower import VectorDatabase
+
+    rng = np.random.default_rng(d + k)
+    n, nq = 5000, 6
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    q = rng.standard_normal((nq, d)).astype(np.float32)
+    ids = [f"p{i}" for i in range(n)]
+    vdb = VectorDatabase(d)
+    vdb.build_index(x, ids)
+    assert vdb.index.ep % 64 == 0 and vdb.index.ep >= d and not vdb.index.scan_dim
+    xn = oracle_mod.vector_db_normalize(x)
+    assert np.array_equal(vdb.index.xb[:, :d].cpu().numpy(), xn)
+    rs, ri = oracle_mod.scan_topk(xn, oracle_mod.vector_db_normalize(q), k)
+    res = vdb.retrieve_batch(q, k=k)
+    assert [[p for p, _ in r] for r in res] == [[ids[j] for j in row] for row in ri]
+    assert np.array_equal(np.array([[sc for _, sc in r] for r in res], np.float32), rs)
+    assert vdb.retrieve(q[2], k=k) == res[2]
+
+
 BF16_CASES = [c for c in SCAN_CASES if c[3] <= 128] + [
     (2049, 384, 5, 128),     # two filter levels, k at the filter's maximum
     (300000, 384, 40, 100),  # tile-max first level at stride 16; 1024 full-level slabs
@@ -650,7 +675,7 @@ def test_bf16_filter_corrupt_key_falls_back(K, oracle_mod, where, n, nq):
         assert fb == (1 if planted else 0), (planted, fb)
 
 
-@pytest.mark.parametrize("E,S", [(384, 20), (768, 20), (768, 100)])
+@pytest.mark.parametrize("E,S", [(384, 20), (768, 20), (768, 100), (1024, 20)])
 def test_attn_agg_batched_gemm_form_vs_oracle(K, oracle_mod, E, S):
     """tt_attn_agg_l2_f32_ws (the batched form: first MLP layer on the f32 MFMA GEMM, then the
     per-buyer softmax / weighted sum / F.normalize) vs the C oracle and the one-kernel form:

@@ -1,0 +1,80 @@
+"""GEMM microbenchmark at the encoder's shapes, bf16 and x3c, for A/B between GEMM variants
+(TT_GEMM_PP=0/1 in the environment; run the variants alternately, several times).
+
+    python tools/bench_gemm_pp.py [--M 370761,18340] [--iters 20]
+Prints one JSON line: per shape ms and TFLOP/s (x3c counted as 3 products).
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "two-tower-model-v2_amd"))
+
+import torch  # noqa: E402
+
+from twotower import _lib  # noqa: E402
+from twotower.item_tower import x3c_weights  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", default="370761,18340")
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    L = _lib.lib()
+    out = {"pp": os.environ.get("TT_GEMM_PP", "1")}
+    for M in (int(v) for v in a.M.split(",")):
+        for (kind, N, K, act) in (("bf16", 1152, 384, 0), ("bf16", 1536, 384, 1),
+                                  ("x3c", 1152, 384, 0), ("x3c", 1536, 384, 1)):
+            g = torch.Generator(device="cuda").manual_seed(1)
+            Af = torch.randn(M, K, device="cuda", generator=g)
+            Wf = torch.randn(N, K, device="cuda", generator=g) / K ** 0.5
+            b = torch.randn(N, device="cuda", generator=g)
+            if kind == "bf16":
+                A, W = Af.to(torch.bfloat16), Wf.to(torch.bfloat16)
+                C16 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+
+                def run():
+                    _lib.check(L.tt_gemm_bf16(A.data_ptr(), K, W.data_ptr(), K, b.data_ptr(), None,
+                                              0, None, N, C16.data_ptr(), N, M, N, K, act,
+                                              _lib.stream_ptr()), "gemm")
+                fl = 2.0 * M * N * K
+            else:
+                hi = Af.to(torch.bfloat16)
+                A2 = torch.cat([hi, (Af - hi.float()).to(torch.bfloat16)], 1).contiguous()
+                W3 = x3c_weights(Wf)
+                if act == 0:  # the QKV form: f32 out
+                    C = torch.empty(M, N, device="cuda")
+
+                    def run():
+                        _lib.check(L.tt_gemm_x3c(A2.data_ptr(), 2 * K, W3.data_ptr(), 3 * K,
+                                                 b.data_ptr(), None, 0, C.data_ptr(), N, None, 0,
+                                                 M, N, K, act, _lib.stream_ptr()), "x3c")
+                else:  # the FFN1 form: GELU, split planes out
+                    C2 = torch.empty(M, 2 * N, device="cuda", dtype=torch.bfloat16)
+
+                    def run():
+                        _lib.check(L.tt_gemm_x3c(A2.data_ptr(), 2 * K, W3.data_ptr(), 3 * K,
+                                                 b.data_ptr(), None, 0, None, 0, C2.data_ptr(),
+                                                 2 * N, M, N, K, act, _lib.stream_ptr()), "x3c")
+                fl = 3 * 2.0 * M * N * K
+            for _ in range(3):
+                run()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / a.iters
+            out[f"{kind}_M{M}_N{N}_act{act}"] = {"us": round(ms * 1e3, 1),
+                                                  "tflops": round(fl / (ms * 1e-3) / 1e12, 1)}
+            del Af, Wf
+            torch.cuda.empty_cache()
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -196,10 +196,19 @@ def stream_ptr() -> int:
 
 
 def padded_dim(d: int) -> int:
+    """Row length of the device catalog / query layout: tt_padded_dim(d) (64 ... 768, the scan
+    and bf16-filter kernels' instantiations), or for d > 768 the next multiple of 64 -- rows
+    that only the generic exact path (kernels.scan_topk_large: f32 MFMA GEMM + key top-k)
+    searches.  The reference accepts any embedding_dim (vector_db.py:13,48)."""
+    if int(d) < 1:
+        raise ValueError(f"embedding dim must be >= 1, got {d}")
     ep = lib().tt_padded_dim(int(d))
-    if ep < 0:
-        raise RuntimeError(f"embedding dim {d} unsupported by the scan kernel (max 768)")
-    return ep
+    return ep if ep > 0 else (int(d) + 63) // 64 * 64
+
+
+def scan_kernel_dim(d: int) -> bool:
+    """True when the scan / bf16-filter kernels take dimension d (<= 768)."""
+    return lib().tt_padded_dim(int(d)) > 0
 
 
 class StreamWorkspaces:

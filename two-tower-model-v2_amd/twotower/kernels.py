@@ -84,35 +84,45 @@ SCAN_KMAX = 1024  # tt_scan_topk_f32's largest k; larger k: scan_topk_large
 
 
 def scan_topk_large(db: torch.Tensor, n: int, d: int, q: torch.Tensor, k: int, row_base: int = 0,
-                    chunk_elems: int = 1 << 28):
-    """Exact top-k for k > SCAN_KMAX (faiss' IndexFlatIP takes any k <= ntotal; the reference's
-    /retrieve caps k at 1000, server.py:46, but VectorDatabase.retrieve does not): every score
-    by tt_gemm_f32 -- the f32 MFMA GEMM whose k order IS the canonical fma order of the scan
-    (DESIGN section 2), so the scores are the scan's bits -- then a stable descending sort
-    (ties to the lower row).  NaN scores are never returned: their slots read (-inf, -1) at
-    the end of the list, as in the scan.  Queries are processed in chunks of at most
-    chunk_elems scores.  An edge path (k > 1024), not the serving path."""
+                    chunk_elems: int = 1 << 27):
+    """Generic exact top-k: any k (faiss' IndexFlatIP takes any k <= ntotal; the reference's
+    /retrieve caps k at 1000, server.py:46, VectorDatabase.retrieve does not) and any dimension
+    (rows past 768 dims, which the scan kernels do not instantiate; vector_db.py:13,48 accept
+    any embedding_dim).  Every score by tt_gemm_f32 -- the f32 MFMA GEMM whose k order IS the
+    canonical fma order of the scan, so the scores are the scan's bits --
+    then a top-k over 64-bit keys (orderable(score) << 32 | ~row: score descending, ties to
+    the lower row, exactly the scan's order).  NaN scores are never returned: their slots read
+    (-inf, -1) at the end of the list, as in the scan.  Queries in chunks of at most
+    chunk_elems scores.  Not the serving path (k <= 128, d <= 768 take the bf16 filter)."""
     _check_2d(db, "db")
     _check_2d(q, "q")
     nq, ep = q.shape[0], db.shape[1]
-    if not (1 <= k <= n <= db.shape[0]) or q.shape[1] != ep:
-        raise ValueError(f"scan_topk_large: need 1 <= k ({k}) <= n ({n}), q [nq, {ep}]")
+    if not (1 <= k <= n <= db.shape[0]) or q.shape[1] != ep or ep % 32 != 0:
+        raise ValueError(f"scan_topk_large: need 1 <= k ({k}) <= n ({n}), q [nq, {ep}], "
+                         "row length % 32 == 0")
     out_s = torch.empty((nq, k), dtype=_f32, device=q.device)
     out_i = torch.empty((nq, k), dtype=torch.int64, device=q.device)
     step = max(1, min(nq, chunk_elems // max(n, 1)))
+    rows = torch.arange(n, device=q.device, dtype=torch.int64)
+    low = 0xFFFFFFFF - rows  # ~row in the low word: ties -> the lower row first
     for a in range(0, nq, step):
         b = min(nq, a + step)
         sc = torch.empty((b - a, n), dtype=_f32, device=q.device)
         check(lib().tt_gemm_f32(_ptr(q[a:b]), q.stride(0), _ptr(db), db.stride(0), None, None, 0,
                                 _ptr(sc), sc.stride(0), None, 0, b - a, n, ep, 0, stream_ptr()),
               "tt_gemm_f32")
+        bits = sc.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+        # orderable: negative floats flipped, positive with the sign bit set; NaN -> 0 (last)
+        orderable = torch.where(bits >= 0x80000000, 0xFFFFFFFF - bits, bits + 0x80000000)
         nan = torch.isnan(sc)
-        sc.masked_fill_(nan, float("-inf"))
-        s, i = torch.sort(sc, dim=1, descending=True, stable=True)
-        s, i = s[:, :k], i[:, :k]
-        bad = torch.gather(nan, 1, i)
-        out_s[a:b] = s.masked_fill(bad, float("-inf"))
-        out_i[a:b] = (i + row_base).masked_fill(bad, -1)
+        orderable = orderable.masked_fill(nan, 0)
+        key = ((orderable - 0x80000000) << 32) | low  # signed: the order of (orderable, ~row)
+        top = torch.topk(key, k, dim=1, largest=True, sorted=True).values
+        r = 0xFFFFFFFF - (top & 0xFFFFFFFF)
+        bad = torch.gather(nan, 1, r)
+        out_s[a:b] = torch.gather(sc, 1, r).masked_fill(bad, float("-inf"))
+        out_i[a:b] = (r + row_base).masked_fill(bad, -1)
+        del sc, bits, orderable, key
     return out_s, out_i
 
 

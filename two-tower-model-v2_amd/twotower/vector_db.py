@@ -36,6 +36,7 @@ class FlatIPIndex:
         self.d = int(d)
         self.row_base = int(row_base)  # global id of local row 0 (catalog row shard)
         self.ep = _lib.padded_dim(self.d)
+        self.scan_dim = _lib.scan_kernel_dim(self.d)  # d <= 768: the scan / bf16 filter
         self.device = device or _lib.device()
         self.xb = torch.zeros((0, self.ep), dtype=torch.float32, device=self.device)
         self.xb16 = torch.zeros((0, self.ep), dtype=torch.bfloat16, device=self.device)
@@ -93,7 +94,8 @@ class FlatIPIndex:
         if k < 1:
             raise RuntimeError("Error: 'k > 0' failed")  # faiss' own assertion text
         use_bf16 = method == "bf16" or (method == "auto" and k <= kernels.FILTER_KMAX)
-        if k > kernels.SCAN_KMAX:  # faiss takes any k: the exact all-scores edge path
+        if k > kernels.SCAN_KMAX or not self.scan_dim:
+            # faiss takes any k and any d: the generic exact path (GEMM scores + key top-k)
             return kernels.scan_topk_large(self.xb, self.ntotal, self.d, q, k,
                                            row_base=self.row_base)
         if use_bf16:
@@ -128,7 +130,8 @@ class FlatIPIndex:
                 outh = (torch.empty((nq, k), dtype=torch.float32, pin_memory=pin),
                         torch.empty((nq, k), dtype=torch.int64, pin_memory=pin))
                 ps = None
-                if 1 <= nq <= 256 and 1 <= k <= min(self.ntotal, kernels.FILTER_KMAX):
+                if (self.scan_dim and 1 <= nq <= 256
+                        and 1 <= k <= min(self.ntotal, kernels.FILTER_KMAX)):
                     ps = kernels.PreparedSearch(self.xb, self.xb16, self.ntotal, self.d, nq, k,
                                                 self.bounds, self.row_base)
                 ent = self._prepared[key] = (q, qh, outh, ps)
