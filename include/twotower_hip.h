@@ -316,6 +316,13 @@ int tt_gemm_ln_x3c(const uint16_t* A2, int64_t lda2, const uint16_t* W3, int64_t
                    const float* bias, const float* gamma, const float* beta, float eps, float* x,
                    int64_t ldx, uint16_t* x_split, int64_t ldx_split, int32_t M, int32_t H,
                    int32_t K, void* stream);
+/* tt_attention_varlen_x3c: the x3c encoder's attention -- qkv2 [T, ld >= 6H] bf16 rows
+ * [Q K V hi | Q K V lo] (the QKV GEMM's split planes, lo at column 3H), every product as
+ * three bf16 MFMAs (hi.hi + lo.hi + hi.lo), f32 softmax; context out2 [T, ld >= 2H] as its
+ * own planes (hi | lo at column H).  Head dim 32, max_len <= 512. */
+int tt_attention_varlen_x3c(const uint16_t* qkv2, int64_t ld_qkv2, const int32_t* cu_seqlens,
+                            int32_t n_seq, int32_t max_len, int32_t H, int32_t heads,
+                            uint16_t* out2, int64_t ld_out2, void* stream);
 int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
                  const float* bias, const float* residual, int64_t ldr, float* C, int64_t ldc,
                  uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N, int32_t K, int32_t act,

@@ -304,6 +304,32 @@ def test_attention_varlen_vs_torch(lens, kind):
     torch.testing.assert_close(out, ref, rtol=tol, atol=tol)
 
 
+@pytest.mark.parametrize("lens", [[1], [7, 64, 128], [3, 200, 1, 512, 33], [31, 32, 33, 17]])
+def test_attention_x3c_planes_vs_torch(lens):
+    """tt_attention_varlen_x3c (the x3c encoder's attention: QKV as split-bf16 planes in, the
+    context's planes out, three MFMAs per product): the x3 tolerance of the f32 attention."""
+    from twotower import _lib
+
+    H, nh = 384, 12
+    T = sum(lens)
+    g = torch.Generator(device="cuda").manual_seed(sum(lens))
+    qkv = torch.randn((T, 3 * H), device="cuda", generator=g)
+    cu = torch.tensor(np.concatenate([[0], np.cumsum(lens)]), dtype=torch.int32, device="cuda")
+    out2 = torch.empty((T, 2 * H), device="cuda", dtype=torch.bfloat16)
+    _lib.check(_lib.lib().tt_attention_varlen_x3c(_planes(qkv).data_ptr(), 6 * H, cu.data_ptr(),
+                                                  len(lens), max(lens), H, nh, out2.data_ptr(),
+                                                  2 * H, _lib.stream_ptr()), "attn_x3c")
+    out = out2[:, :H].float() + out2[:, H:].float()
+    ref = torch.empty((T, H), device="cuda", dtype=torch.float64)
+    c = cu.tolist()
+    for i in range(len(lens)):
+        a, b = c[i], c[i + 1]
+        q, k, v = (qkv[a:b, j * H:(j + 1) * H].double().view(b - a, nh, 32).transpose(0, 1)
+                   for j in range(3))
+        ref[a:b] = (torch.softmax(q @ k.transpose(1, 2) / 32 ** 0.5, -1) @ v).transpose(0, 1).reshape(b - a, H)
+    torch.testing.assert_close(out.double(), ref, rtol=3e-5, atol=3e-5)
+
+
 def _encoder(prec, cfg=mbg.CFG, seed=mbg.SEED):
     from twotower.item_tower import BertEncoder, random_bert_state_dict
 

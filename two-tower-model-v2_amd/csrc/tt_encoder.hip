@@ -949,6 +949,12 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wide(const uint16_t* __restrict
 #ifndef TT_GPP_PRIO
 #define TT_GPP_PRIO 1  // s_setprio(1) around each phase's MFMAs
 #endif
+#ifndef TT_GPP_BAR
+// barriers per K-tile: 4 (every phase) or 2 (phases 1 and 3: enough for the DMA schedule --
+// every restage is issued after a barrier that follows the lgkmcnt retiring the buffer's
+// last reads, and phase 3's barrier follows the vmcnt retiring the next K-tile)
+#define TT_GPP_BAR 4
+#endif
 template <int ACT, int OM>
 __global__ __launch_bounds__(512, 1) void k_gemm_pp(const uint16_t* __restrict__ A, int64_t lda,
                                                     const uint16_t* __restrict__ W, int64_t ldw,
@@ -1075,7 +1081,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_pp(const uint16_t* __restrict__
         if (gi + 2 < total) enc_wait_vm<3>();
         else enc_wait_vm<0>();
       }
-      __builtin_amdgcn_s_barrier();
+      if (TT_GPP_BAR == 4 || p == 1 || p == 3) __builtin_amdgcn_s_barrier();
       if (p == 0) {
         const uint32_t pa0 = sb + fa[0], pa1 = sb + fa[1];
         av[0][0] = lds_read128<0>(pa0);
@@ -1177,8 +1183,12 @@ constexpr int GL_W_B = GL_H * 128;
 TT_CHECK_EXP(TT_GEXP_NOSTORE || TT_GWEXP_NOEPI || TT_GLEXP_NOW || TT_GLEXP_NOEPI || TT_GL_NT,
              "TT_G*EXP_* / TT_GL_NT (results wrong or untested)");
 
-// BM = 128 (8 waves of 64 x 96) or 96 (8 waves of 48 x 96: a batch of ~18k token rows is
-// 144 tiles of 128 on 256 CUs, 192 of 96 -- tt_gemm_ln_bf16 picks by rounds x tile cost).
+// BM = 128 (8 waves as 2 (M) x 4 (N) of 64 x 96), 96 (2 x 4 of 48 x 96) or 80 (1 (M) x 8 (N)
+// of 80 x 48): a batch of ~18k token rows is 144 tiles of 128 on 256 CUs, 192 of 96, 230 of 80
+// -- tt_gemm_ln_bf16 picks by rounds x tile cost.  The LayerNorm statistics are reduced in a
+// layout-independent order (each row's 384 columns as 8 partial sums of 48 columns, each
+// partial summed over its lanes, the 8 combined by a fixed tree), so a row's bits do not
+// depend on the tile height the batch size selected.
 // SPL: the x3c encoder -- A and W are the K-concatenated split operands (kx = K / 3, see
 // x3c_acol) and x's bf16 copy is the [hi | lo] plane pair (X16 row: hi at n, lo at GL_H + n).
 template <int BM, bool SPL = false>
@@ -1190,13 +1200,19 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
                                                     float* __restrict__ X, int64_t ldx,
                                                     uint16_t* __restrict__ X16, int64_t ldx16,
                                                     int M, int K, int kx) {
-  constexpr int BK = 64, EPC = 8, MI = BM / 32, WR = BM / 2;  // 16-row blocks / rows per wave
+  static_assert(BM == 128 || BM == 96 || BM == 80, "k_gemm_ln: BM");
+  constexpr int WM_N = BM == 80 ? 1 : 2;     // waves along M
+  constexpr int WN_N = 8 / WM_N;             // waves along N
+  constexpr int NJ = (GL_H / 16) / WN_N;     // 16-column blocks per wave (6 or 3)
+  constexpr int HJ = 3;                      // blocks per 48-column partial
+  constexpr int NP = NJ / HJ;                // partials per wave (2 or 1)
+  constexpr int BK = 64, EPC = 8, WR = BM / WM_N, MI = WR / 16;  // rows per wave / 16-row blocks
   constexpr int A_B = BM * 128, WBASE = GL_ASLOTS * A_B;
+  constexpr int APIECES = BM / 8;            // 1-KB A pieces per stage (10, 12 or 16)
   // stores per lane of a full tile's epilogue (vmcnt holds at most 63: a stronger wait is safe)
-  constexpr int STORES = MI * GL_NJ * (SPL ? 3 : 2) > 63 ? 63 : MI * GL_NJ * (SPL ? 3 : 2);
-  static_assert(BM == 128 || BM == 96, "k_gemm_ln: BM");
+  constexpr int STORES = MI * NJ * (SPL ? 3 : 2) > 63 ? 63 : MI * NJ * (SPL ? 3 : 2);
   __shared__ __attribute__((aligned(16))) char smem[WBASE + GL_WSLOTS * GL_W_B];
-  __shared__ float red[2][4][BM];  // [mean | var pass][wave column wn][tile row]
+  __shared__ float red[2][8][BM];  // [mean | var pass][48-column partial][tile row]
   __shared__ __attribute__((aligned(16))) float prm[3][GL_H];  // bias, gamma, beta
   const int tid = threadIdx.x, lane = tid & 63;
   for (int e = tid; e < GL_H; e += 512) {
@@ -1205,24 +1221,24 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
     prm[2][e] = beta[e];
   }  // visible after the first stage's barrier
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 2, wn = w & 3;
+  const int wm = w / WN_N, wn = w % WN_N;
   const int ntiles = (M + BM - 1) / BM;
   const int nk = K / BK;
   auto tile_of = [&](int r) { return enc_xcd_remap(blockIdx.x + r * gridDim.x, ntiles); };
   const int n_mine = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
   if (n_mine <= 0) return;
 
-  // DMA: A = BM / 8 pieces of 8 rows x 128 B, W = 48 pieces; wave w issues A pieces w + 8j
-  // (j < 2; at BM = 96 pieces 12..15 fold onto 8..11, written twice with the same bytes, so
-  // every wave issues 2 and the vmcnt accounting is uniform) and W pieces w + 8j (j < 6);
-  // chunk swizzle as k_gemm.
+  // DMA: A = APIECES pieces of 8 rows x 128 B, W = 48 pieces; wave w issues A pieces w + 8j
+  // (j < 2; pieces past APIECES fold back onto earlier ones, written twice with the same
+  // bytes, so every wave issues 2 and the vmcnt accounting is uniform) and W pieces w + 8j
+  // (j < 6); chunk swizzle as k_gemm.
   // W piece w + 8j = rows 64 j + 8 w + (lane >> 3): a per-lane 32-bit offset (the swizzle
   // (row >> 1) & 7 does not depend on j) plus the uniform base W + 64 j ldw
   const int w_row0 = 8 * w + (lane >> 3);
   const int w_lane = w_row0 * (int)ldw + ((lane & 7) ^ ((w_row0 >> 1) & 7)) * EPC;
   auto apiece = [&](int j) {
     const int pc = w + 8 * j;
-    return pc < BM / 8 ? pc : pc - 4;
+    return pc < APIECES ? pc : pc - (16 - APIECES);
   };
   auto a_offsets = [&](int lt, int64_t (&ao)[2]) __attribute__((always_inline)) {
 #pragma unroll
@@ -1254,15 +1270,15 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
           (__attribute__((address_space(3))) void*)(st + 1024 * (w + 8 * j)), 16, 0, 0);
   };
 
-  // fragment rows WR wm + 16 i + rl (A) / 96 wn + 16 j + rl (W): the swizzle (row >> 1) & 7
-  // = (rl >> 1) & 7 is the same for every i, j, so block i / j is an immediate offset
+  // fragment rows WR wm + 16 i + rl (A) / 16 NJ wn + 16 j + rl (W): the swizzle (row >> 1) & 7
+  // = (rl >> 1) & 7 is the same for every i, j, so block i / j is 2048 B further
   const int g = lane >> 4, rl = lane & 15;
   uint32_t fa[2], fb[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const int c = (4 * s + g) ^ ((rl >> 1) & 7);
     fa[s] = (WR * wm + rl) * 128 + 16 * c;
-    fb[s] = (96 * wn + rl) * 128 + 16 * c;
+    fb[s] = (16 * NJ * wn + rl) * 128 + 16 * c;
   }
 
   // the block's stages t = r * nk + kt in one sequence: A(t) issued at stage t - 2, W(t) at
@@ -1289,11 +1305,11 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
   const float inv_h = 1.0f / (float)GL_H;
   for (int r = 0; r < n_mine; ++r) {
     const int m0 = tile_of(r) * BM;
-    f32x4 acc[MI][GL_NJ];
+    f32x4 acc[MI][NJ];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < GL_NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int kt = 0; kt < nk; ++kt) {
       // younger than this stage's W pieces: A(t + 1) (2 per lane, if issued) and, at a tile's
       // first stage, the previous epilogue's residual loads and STORES stores (a ragged
@@ -1313,40 +1329,26 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
       issue_next_a();
       const uint32_t sa = lds_addr(smem) + (uint32_t)((t % GL_ASLOTS) * A_B);
       const uint32_t sw = lds_addr(smem) + (uint32_t)(WBASE + (t % GL_WSLOTS) * GL_W_B);
-      // fragment reads of both k-halves issued up front (2 (MI + 6); the LDS counter holds 15:
-      // the last five of s = 1 go out once s = 0 has landed), s = 1 lands under s = 0's MFMAs
-      u32x4 av[2][MI], bv[2][GL_NJ];
-      const uint32_t pa0 = sa + fa[0], pb0 = sw + fb[0], pa1 = sa + fa[1], pb1 = sw + fb[1];
-      av[0][0] = lds_read128<0>(pa0);
-      av[0][1] = lds_read128<2048>(pa0);
-      av[0][2] = lds_read128<4096>(pa0);
-      if constexpr (MI > 3) av[0][3] = lds_read128<6144>(pa0);
-      bv[0][0] = lds_read128<0>(pb0);
-      bv[0][1] = lds_read128<2048>(pb0);
-      bv[0][2] = lds_read128<4096>(pb0);
-      bv[0][3] = lds_read128<6144>(pb0);
-      bv[0][4] = lds_read128<8192>(pb0);
-      bv[0][5] = lds_read128<10240>(pb0);
-      av[1][0] = lds_read128<0>(pa1);
-      av[1][1] = lds_read128<2048>(pa1);
-      av[1][2] = lds_read128<4096>(pa1);
-      if constexpr (MI > 3) av[1][3] = lds_read128<6144>(pa1);
-      bv[1][0] = lds_read128<0>(pb1);
-      lds_wait<MI + 1>();  // s = 0's MI + 6 reads have landed
-      bv[1][1] = lds_read128<2048>(pb1);
-      bv[1][2] = lds_read128<4096>(pb1);
-      bv[1][3] = lds_read128<6144>(pb1);
-      bv[1][4] = lds_read128<8192>(pb1);
-      bv[1][5] = lds_read128<10240>(pb1);
+      // fragment reads of both k-halves issued up front; s = 1 lands under s = 0's MFMAs
+      u32x4 av[2][MI], bv[2][NJ];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        if (s == 1) lds_wait<0>();
+        const uint32_t pa = sa + fa[s], pb = sw + fb[s];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) av[s][i] = lds_read128<0>(pa + 2048 * i);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bv[s][j] = lds_read128<0>(pb + 2048 * j);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        if (s == 0) lds_wait<(MI + NJ) < 15 ? MI + NJ : 15>();
+        else lds_wait<0>();
 #pragma unroll
         for (int i = 0; i < MI; ++i) reg_tie(av[s][i]);
 #pragma unroll
-        for (int j = 0; j < GL_NJ; ++j) reg_tie(bv[s][j]);
+        for (int j = 0; j < NJ; ++j) reg_tie(bv[s][j]);
 #pragma unroll
-        for (int j = 0; j < GL_NJ; ++j)
+        for (int j = 0; j < NJ; ++j)
 #pragma unroll
           for (int i = 0; i < MI; ++i)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
@@ -1361,71 +1363,87 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < GL_NJ; ++j) t += (acc[i][j][0] + acc[i][j][1]) + (acc[i][j][2] + acc[i][j][3]);
+        for (int j = 0; j < NJ; ++j) t += (acc[i][j][0] + acc[i][j][1]) + (acc[i][j][2] + acc[i][j][3]);
       if (t == 1.2345f) X[0] = t;
       prev_full = false;
       continue;
     }
     // ---- epilogue: y = acc + bias + x ; x = LayerNorm(y) (biased variance, two passes).
-    // Residual rows are loaded one 16-row block ahead (6 x 16 B per lane in flight while the
-    // previous block is summed); bias / gamma / beta come from LDS.
+    // Residual rows are loaded one 16-row block ahead (NJ x 16 B per lane in flight while the
+    // previous block is summed); bias / gamma / beta come from LDS.  Statistics: per row, 8
+    // partials of 48 columns (a wave's HJ blocks, lane-summed), combined by a fixed tree.
     const bool full = m0 + BM <= M;
-    const int nw0 = 96 * wn + 4 * g;
+    const int nw0 = 16 * NJ * wn + 4 * g;
     const float* xr0 = X + (int64_t)(m0 + WR * wm + rl) * ldx + nw0;
     auto xrow = [&](int i) __attribute__((always_inline)) {
       const int m = m0 + WR * wm + 16 * i + rl;
       return X + (int64_t)(m < M ? m : M - 1) * ldx + nw0;  // rows past M: clamped reads
     };
+    auto tree8 = [](const float* r) __attribute__((always_inline)) {
+      return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    };
     float mean[MI], rstd[MI];
     {
-      f32x4 rv[2][GL_NJ];
+      f32x4 rv[2][NJ];
       const float* p0 = full ? xr0 : xrow(0);
 #pragma unroll
-      for (int j = 0; j < GL_NJ; ++j) rv[0][j] = *(const f32x4*)(p0 + 16 * j);
+      for (int j = 0; j < NJ; ++j) rv[0][j] = *(const f32x4*)(p0 + 16 * j);
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         if (i + 1 < MI) {
           const float* p1 = full ? xr0 + (int64_t)(16 * (i + 1)) * ldx : xrow(i + 1);
 #pragma unroll
-          for (int j = 0; j < GL_NJ; ++j) rv[(i + 1) & 1][j] = *(const f32x4*)(p1 + 16 * j);
+          for (int j = 0; j < NJ; ++j) rv[(i + 1) & 1][j] = *(const f32x4*)(p1 + 16 * j);
         }
-        float s = 0.0f;
 #pragma unroll
-        for (int j = 0; j < GL_NJ; ++j) {
-          acc[i][j] += rv[i & 1][j] + *(const f32x4*)(&prm[0][nw0 + 16 * j]);
-          s += (acc[i][j][0] + acc[i][j][1]) + (acc[i][j][2] + acc[i][j][3]);
+        for (int p = 0; p < NP; ++p) {
+          float sp = 0.0f;
+#pragma unroll
+          for (int jj = 0; jj < HJ; ++jj) {
+            const int j = HJ * p + jj;
+            acc[i][j] += rv[i & 1][j] + *(const f32x4*)(&prm[0][nw0 + 16 * j]);
+            sp += (acc[i][j][0] + acc[i][j][1]) + (acc[i][j][2] + acc[i][j][3]);
+          }
+          sp += __shfl_xor(sp, 16, 64);
+          sp += __shfl_xor(sp, 32, 64);
+          if (g == 0) red[0][NP * wn + p][WR * wm + 16 * i + rl] = sp;
         }
-        s += __shfl_xor(s, 16, 64);
-        s += __shfl_xor(s, 32, 64);
-        if (g == 0) red[0][wn][WR * wm + 16 * i + rl] = s;
       }
     }
     enc_lds_barrier();
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int row = WR * wm + 16 * i + rl;
-      mean[i] = ((red[0][0][row] + red[0][1][row]) + (red[0][2][row] + red[0][3][row])) * inv_h;
-      float q = 0.0f;
+      float rr[8];
 #pragma unroll
-      for (int j = 0; j < GL_NJ; ++j)
+      for (int c = 0; c < 8; ++c) rr[c] = red[0][c][row];
+      mean[i] = tree8(rr) * inv_h;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float d = acc[i][j][u] - mean[i];
-          q = fmaf(d, d, q);
-        }
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
-      if (g == 0) red[1][wn][row] = q;
+      for (int p = 0; p < NP; ++p) {
+        float q = 0.0f;
+#pragma unroll
+        for (int jj = 0; jj < HJ; ++jj)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float d = acc[i][HJ * p + jj][u] - mean[i];
+            q = fmaf(d, d, q);
+          }
+        q += __shfl_xor(q, 16, 64);
+        q += __shfl_xor(q, 32, 64);
+        if (g == 0) red[1][NP * wn + p][row] = q;
+      }
     }
     enc_lds_barrier();
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int row = WR * wm + 16 * i + rl;
-      const float q = (red[1][0][row] + red[1][1][row]) + (red[1][2][row] + red[1][3][row]);
-      rstd[i] = 1.0f / sqrtf(q * inv_h + eps);
+      float rr[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) rr[c] = red[1][c][row];
+      rstd[i] = 1.0f / sqrtf(tree8(rr) * inv_h + eps);
     }
 #pragma unroll
-    for (int j = 0; j < GL_NJ; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const int n = nw0 + 16 * j;
       const f32x4 gm = *(const f32x4*)(&prm[1][n]), bt = *(const f32x4*)(&prm[2][n]);
 #pragma unroll
@@ -1433,44 +1451,23 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
 #pragma unroll
         for (int u = 0; u < 4; ++u) acc[i][j][u] = (acc[i][j][u] - mean[i]) * rstd[i] * gm[u] + bt[u];
     }
-    if (full) {
 #pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int64_t m = m0 + WR * wm + 16 * i + rl;
+    for (int i = 0; i < MI; ++i) {
+      const int64_t m = m0 + WR * wm + 16 * i + rl;
+      if (!full && m >= M) continue;
 #pragma unroll
-        for (int j = 0; j < GL_NJ; ++j) {
-          const int n = nw0 + 16 * j;
-          *(f32x4*)(X + m * ldx + n) = acc[i][j];
-          const uint2 hv = uint2{pack_bf16_hw(acc[i][j][0], acc[i][j][1]),
-                                 pack_bf16_hw(acc[i][j][2], acc[i][j][3])};
-          *(uint2*)(X16 + m * ldx16 + n) = hv;
-          if constexpr (SPL)
-            *(uint2*)(X16 + m * ldx16 + GL_H + n) =
-                uint2{pack_bf16_hw(acc[i][j][0] - __uint_as_float(hv.x << 16),
-                                   acc[i][j][1] - __uint_as_float(hv.x & 0xffff0000u)),
-                      pack_bf16_hw(acc[i][j][2] - __uint_as_float(hv.y << 16),
-                                   acc[i][j][3] - __uint_as_float(hv.y & 0xffff0000u))};
-        }
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int64_t m = m0 + WR * wm + 16 * i + rl;
-        if (m >= M) continue;
-#pragma unroll
-        for (int j = 0; j < GL_NJ; ++j) {
-          const int n = nw0 + 16 * j;
-          *(f32x4*)(X + m * ldx + n) = acc[i][j];
-          const uint2 hv = uint2{pack_bf16_hw(acc[i][j][0], acc[i][j][1]),
-                                 pack_bf16_hw(acc[i][j][2], acc[i][j][3])};
-          *(uint2*)(X16 + m * ldx16 + n) = hv;
-          if constexpr (SPL)
-            *(uint2*)(X16 + m * ldx16 + GL_H + n) =
-                uint2{pack_bf16_hw(acc[i][j][0] - __uint_as_float(hv.x << 16),
-                                   acc[i][j][1] - __uint_as_float(hv.x & 0xffff0000u)),
-                      pack_bf16_hw(acc[i][j][2] - __uint_as_float(hv.y << 16),
-                                   acc[i][j][3] - __uint_as_float(hv.y & 0xffff0000u))};
-        }
+      for (int j = 0; j < NJ; ++j) {
+        const int n = nw0 + 16 * j;
+        *(f32x4*)(X + m * ldx + n) = acc[i][j];
+        const uint2 hv = uint2{pack_bf16_hw(acc[i][j][0], acc[i][j][1]),
+                               pack_bf16_hw(acc[i][j][2], acc[i][j][3])};
+        *(uint2*)(X16 + m * ldx16 + n) = hv;
+        if constexpr (SPL)
+          *(uint2*)(X16 + m * ldx16 + GL_H + n) =
+              uint2{pack_bf16_hw(acc[i][j][0] - __uint_as_float(hv.x << 16),
+                                 acc[i][j][1] - __uint_as_float(hv.x & 0xffff0000u)),
+                    pack_bf16_hw(acc[i][j][2] - __uint_as_float(hv.y << 16),
+                                 acc[i][j][3] - __uint_as_float(hv.y & 0xffff0000u))};
       }
     }
     prev_full = full;
@@ -2018,6 +2015,162 @@ __global__ __launch_bounds__(256 * HG) void k_attn32_bf16(
   }
 }
 
+// x3c attention: the fast kernel's structure (K / V^T staged with 16-B loads, HG heads of a
+// sequence per block, two passes over the keys) on split-bf16 operands.  qkv arrives as the
+// QKV GEMM's [hi | lo] planes (row: Q K V hi, then Q K V lo at column lo_off = 3H); each
+// product is three bf16 MFMAs (hi.hi + lo.hi + hi.lo, as k_attn32_mfma<X3>): S = K Q^T and
+// O^T = V^T P^T with P split in registers.  Pass 1 finds each query's row maximum from the
+// hi.hi scores only (an offset for exp2's range; the softmax is exact for any offset), pass 2
+// the full scores, exp2 and P.V.  The context goes out as the Wo GEMM's [hi | lo] planes.
+// LDS per head: K rows hi | lo (144 B) and V^T as two bf16 planes.
+template <int HG>
+__global__ __launch_bounds__(256 * HG) void k_attn32_x3(
+    const uint16_t* __restrict__ qkv, int64_t ldq, int lo_off, const int32_t* __restrict__ cu,
+    int H, int heads, float scale, uint16_t* __restrict__ out16, int64_t ldo) {
+  constexpr int DH = 32, KROW = 2 * DH * 2 + 16;
+  constexpr int WPH = 4, NT = 64 * HG * WPH;
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int hh = w / WPH, wsub = w % WPH;
+  const int g = lane >> 4, ql = lane & 15;
+  const int groups = heads / HG;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int sq = lb / groups, h0 = (lb % groups) * HG, h = h0 + hh;
+  const int t0 = cu[sq], L = cu[sq + 1] - t0;
+  const int Lk = (L + 31) & ~31;
+  const int vst = ((Lk + 127) & ~127) + 8;  // V^T row stride (bf16 elements)
+  const size_t vplane = (size_t)32 * vst * 2;
+  const size_t per_head = (size_t)Lk * KROW + 2 * vplane;
+  char* Ks = sm + hh * per_head;
+  char* Vt = Ks + (size_t)Lk * KROW;
+  auto load_q = [&](int q0_, u32x4& qh, u32x4& qlo) __attribute__((always_inline)) {
+    const int qr = q0_ + ql < L ? q0_ + ql : L - 1;
+    const uint16_t* qp = qkv + (int64_t)(t0 + qr) * ldq + h * DH + 8 * g;
+    qh = *(const u32x4*)qp;
+    qlo = *(const u32x4*)(qp + lo_off);
+  };
+  u32x4 qnh, qnl;
+  load_q(16 * wsub < L ? 16 * wsub : 0, qnh, qnl);
+  // item e = (key pair p, plane pl, head hs, 8-dim chunk c8), chunk fastest
+  for (int e = tid; e < (Lk / 2) * 8 * HG; e += NT) {
+    const int cc = e % (8 * HG), hs = (cc >> 2) % HG, pl = cc / (4 * HG);
+    const int p = e / (8 * HG), c8 = 8 * (cc & 3), j = 2 * p;
+    char* Ks_ = sm + hs * per_head;
+    char* Vp = Ks_ + (size_t)Lk * KROW + pl * vplane;
+    u32x4 k0 = {0u, 0u, 0u, 0u}, k1 = k0, v0 = k0, v1 = k0;
+    const uint16_t* row = qkv + (int64_t)(t0 + j) * ldq + (pl ? lo_off : 0) + (h0 + hs) * DH + c8;
+    if (j < L) {
+      k0 = *(const u32x4*)(row + H);
+      v0 = *(const u32x4*)(row + 2 * H);
+    }
+    if (j + 1 < L) {
+      k1 = *(const u32x4*)(row + ldq + H);
+      v1 = *(const u32x4*)(row + ldq + 2 * H);
+    }
+    *(u32x4*)(Ks_ + j * KROW + pl * 64 + c8 * 2) = k0;
+    *(u32x4*)(Ks_ + (j + 1) * KROW + pl * 64 + c8 * 2) = k1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t a = (v0[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+      const uint32_t b = (v1[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+      *(uint32_t*)(Vp + ((size_t)(c8 + i) * vst + j) * 2) = a | (b << 16);
+    }
+  }
+  __syncthreads();
+  const float sl2 = scale * 1.4426950408889634f;  // scores in log2 units
+  for (int q0 = 16 * wsub; q0 < L; q0 += 16 * WPH) {
+    const bf16x8e qh = __builtin_bit_cast(bf16x8e, qnh), qlo = __builtin_bit_cast(bf16x8e, qnl);
+    if (q0 + 16 * WPH < L) load_q(q0 + 16 * WPH, qnh, qnl);
+    auto mask = [&](int kc, f32x4 (&sc)[2]) __attribute__((always_inline)) {
+      if (kc + 32 > L) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            if (kc + 16 * b + 4 * g + v >= L) sc[b][v] = -__builtin_huge_valf();
+      }
+    };
+    // pass 1: row maximum of the hi.hi scores (sc[b][v] = key kc + 16b + 4g + v, query ql)
+    float m = -__builtin_huge_valf();
+    for (int kc = 0; kc < Lk; kc += 32) {
+      f32x4 sc[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const u32x4 kf = *(const u32x4*)(Ks + (kc + 16 * b + ql) * KROW + 16 * g);
+        sc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8e, kf), qh,
+                                                        f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      }
+      mask(kc, sc);
+      m = fmaxf(m, fmaxf(fmaxf(fmaxf(sc[0][0], sc[0][1]), fmaxf(sc[0][2], sc[0][3])),
+                         fmaxf(fmaxf(sc[1][0], sc[1][1]), fmaxf(sc[1][2], sc[1][3]))));
+    }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    const float m2 = m * sl2;
+    float lpart = 0.0f;
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    for (int kc = 0; kc < Lk; kc += 32) {
+      f32x4 sc[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const char* kr = Ks + (kc + 16 * b + ql) * KROW + 16 * g;
+        const bf16x8e kh = __builtin_bit_cast(bf16x8e, *(const u32x4*)kr);
+        const bf16x8e kl = __builtin_bit_cast(bf16x8e, *(const u32x4*)(kr + 64));
+        f32x4 z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kh, qh, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kl, qh, z, 0, 0, 0);
+        sc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kh, qlo, z, 0, 0, 0);
+      }
+      mask(kc, sc);
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          sc[b][v] = __builtin_amdgcn_exp2f(fmaf(sc[b][v], sl2, -m2));
+          lpart += sc[b][v];
+        }
+      // P^T slots: j < 4 <-> key kc + 4g + j, j >= 4 <-> kc + 16 + 4g + (j - 4); split hi | lo
+      bf16x8e ph, plo;
+      split_bf16x8(__builtin_bit_cast(u32x4, sc[0]), __builtin_bit_cast(u32x4, sc[1]), ph, plo);
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const char* vr = Vt + ((size_t)(16 * db + ql) * vst + kc + 4 * g) * 2;
+        const uint64_t a0 = *(const uint64_t*)vr, a1 = *(const uint64_t*)(vr + 32);
+        const uint64_t b0 = *(const uint64_t*)(vr + vplane), b1 = *(const uint64_t*)(vr + vplane + 32);
+        const bf16x8e vh = __builtin_bit_cast(
+            bf16x8e, u32x4{(uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32)});
+        const bf16x8e vl = __builtin_bit_cast(
+            bf16x8e, u32x4{(uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1, (uint32_t)(b1 >> 32)});
+        acc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh, ph, acc[db], 0, 0, 0);
+        acc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vl, ph, acc[db], 0, 0, 0);
+        acc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh, plo, acc[db], 0, 0, 0);
+      }
+    }
+    float lsum = lpart + __shfl_xor(lpart, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    // acc[db][v] = O^T[dim 16 db + 4 g + v][query q0 + ql] -> the context's hi | lo planes
+    if (q0 + ql < L) {
+      const float inv = 1.0f / lsum;
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const f32x4 o = acc[db] * inv;
+        uint16_t* o16 = out16 + (int64_t)(t0 + q0 + ql) * ldo + h * DH + 16 * db + 4 * g;
+        const uint2 hv = uint2{pack_bf16_hw(o[0], o[1]), pack_bf16_hw(o[2], o[3])};
+        *(uint2*)o16 = hv;
+        *(uint2*)(o16 + H) = uint2{pack_bf16_hw(o[0] - __uint_as_float(hv.x << 16),
+                                                o[1] - __uint_as_float(hv.x & 0xffff0000u)),
+                                   pack_bf16_hw(o[2] - __uint_as_float(hv.y << 16),
+                                                o[3] - __uint_as_float(hv.y & 0xffff0000u))};
+      }
+    }
+  }
+}
+
+size_t attn32_x3_smem(int max_len) {
+  const int Lk = (max_len + 31) & ~31;
+  const int vst = ((Lk + 127) & ~127) + 8;
+  return (size_t)Lk * (2 * 32 * 2 + 16) + 2 * (size_t)32 * vst * 2;
+}
+
 size_t attn32_smem(int max_len, bool bf, bool x3 = false) {
   const int Lk = (max_len + 31) & ~31;
   const int vst = ((Lk + 127) & ~127) + (bf || x3 ? 8 : 4);
@@ -2337,23 +2490,32 @@ static int gemm_ln_impl(const uint16_t* A, int64_t lda, const uint16_t* W, int64
   // only when strictly cheaper -- a configs[1] batch (~18k rows: 144 tiles of 128 = one
   // 56%-full round, 192 of 96); at Mode A's 365k rows 128 and 96 tie and 128 stays
   const int ncu = enc_device_cus();
-  const int64_t t128 = (M + 127) / 128, t96 = (M + 95) / 96;
-  const bool b96 = gemm_ln96_enabled() &&
-                   ((t96 + ncu - 1) / ncu) * (96 + 32) < ((t128 + ncu - 1) / ncu) * (128 + 32);
-  const int ntiles = (int)(b96 ? t96 : t128);
+  // cost of a tile height: rounds (ceil(tiles / CUs)) x (BM + ~32 rows of fixed cost); the
+  // smallest cost wins, ties to the taller tile
+  int bm = 128;
+  int64_t best = ((M + 127) / 128 + ncu - 1) / ncu * (128 + 32);
+  if (gemm_ln96_enabled())
+    for (int c : {96, 80}) {
+      const int64_t cost = (((M + c - 1) / c) + ncu - 1) / ncu * (c + 32);
+      if (cost < best) {
+        best = cost;
+        bm = c;
+      }
+    }
+  const int ntiles = (int)((M + bm - 1) / bm);
   const int grid = ntiles < ncu ? ntiles : ncu;
   if (kx > 0) {
     TT_REQUIRE(kx % 64 == 0 && K == 3 * kx && lda >= 2 * (int64_t)kx && ldx16 >= 2 * GL_H &&
                    ldx16 % 8 == 0,
                "x3c gemm_ln: K == 3 kx, A [hi | lo] (lda >= 2 kx), x planes (ldx16 >= 768)");
-    hipLaunchKernelGGL((b96 ? k_gemm_ln<96, true> : k_gemm_ln<128, true>), dim3(grid), dim3(512), 0,
-                       (hipStream_t)stream, A, lda, W, ldw, bias, gamma, beta, eps, x, ldx,
-                       x_bf16, ldx16, M, K, kx);
+    auto kern = bm == 80 ? k_gemm_ln<80, true> : bm == 96 ? k_gemm_ln<96, true> : k_gemm_ln<128, true>;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, (hipStream_t)stream, A, lda, W, ldw, bias,
+                       gamma, beta, eps, x, ldx, x_bf16, ldx16, M, K, kx);
     return check_launch("tt_gemm_ln_x3c");
   }
-  hipLaunchKernelGGL(b96 ? k_gemm_ln<96> : k_gemm_ln<128>, dim3(grid), dim3(512), 0,
-                     (hipStream_t)stream, A, lda, W, ldw, bias, gamma, beta, eps, x, ldx, x_bf16,
-                     ldx16, M, K, 0);
+  auto kern = bm == 80 ? k_gemm_ln<80> : bm == 96 ? k_gemm_ln<96> : k_gemm_ln<128>;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, (hipStream_t)stream, A, lda, W, ldw, bias,
+                     gamma, beta, eps, x, ldx, x_bf16, ldx16, M, K, 0);
   return check_launch("tt_gemm_ln_bf16");
 }
 
@@ -2424,6 +2586,42 @@ static int attention_varlen_impl(const float* qkv, int64_t ld_qkv, const int32_t
     hipLaunchKernelGGL((k_attn32_mfma<false, float>), grid, dim3(256), smem, (hipStream_t)stream, qkv,
                        ld_qkv, cu_seqlens, H, heads, scale, out, ld_out, out_bf16, 0);
   return check_launch("tt_attention_varlen");
+}
+
+// x3c attention over the QKV planes (k_attn32_x3): qkv2 [T, ld] bf16 rows [Q K V hi | Q K V lo]
+// (lo at column 3H), context planes out2 [T, ld_out >= 2H] (hi | lo at column H)
+extern "C" int tt_attention_varlen_x3c(const uint16_t* qkv2, int64_t ld_qkv2,
+                                       const int32_t* cu_seqlens, int32_t n_seq, int32_t max_len,
+                                       int32_t H, int32_t heads, uint16_t* out2, int64_t ld_out2,
+                                       void* stream) {
+  TT_REQUIRE(n_seq >= 0 && heads >= 1 && H % heads == 0, "bad n_seq / heads");
+  if (n_seq == 0) return TT_OK;
+  TT_REQUIRE(max_len >= 1 && max_len <= 512, "max_len must be in [1, 512]");
+  TT_REQUIRE(qkv2 && cu_seqlens && out2, "null pointer");
+  if (H / heads != 32)
+    return fail(TT_ERR_UNSUPPORTED, "tt_attention_varlen_x3c: head dim must be 32");
+  TT_REQUIRE(ld_qkv2 >= 6 * (int64_t)H && ld_qkv2 % 8 == 0 && H % 8 == 0 &&
+                 ld_out2 >= 2 * (int64_t)H && ld_out2 % 4 == 0 && ((uintptr_t)qkv2 % 16) == 0 &&
+                 ((uintptr_t)out2 % 8) == 0,
+             "qkv planes [T, >= 6H] 16-B aligned rows; context planes [T, >= 2H]");
+  const size_t smem = attn32_x3_smem(max_len);
+  const bool h2 = heads % 2 == 0 && 2 * smem <= 160 * 1024;
+  const void* fb = h2 ? (const void*)k_attn32_x3<2> : (const void*)k_attn32_x3<1>;
+  const size_t sm = h2 ? 2 * smem : smem;
+  if (sm > 160 * 1024) return fail(TT_ERR_UNSUPPORTED, "attention K/V exceed LDS");
+  if (sm > 64 * 1024 &&
+      hipFuncSetAttribute(fb, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm) != hipSuccess)
+    return fail(TT_ERR_LAUNCH, "hipFuncSetAttribute(max dynamic LDS)");
+  const float scale = 1.0f / sqrtf(32.0f);
+  if (h2)
+    hipLaunchKernelGGL(k_attn32_x3<2>, dim3((unsigned)(n_seq * heads / 2)), dim3(512), sm,
+                       (hipStream_t)stream, qkv2, ld_qkv2, 3 * H, cu_seqlens, H, heads, scale,
+                       out2, ld_out2);
+  else
+    hipLaunchKernelGGL(k_attn32_x3<1>, dim3((unsigned)(n_seq * heads)), dim3(256), sm,
+                       (hipStream_t)stream, qkv2, ld_qkv2, 3 * H, cu_seqlens, H, heads, scale,
+                       out2, ld_out2);
+  return check_launch("tt_attention_varlen_x3c");
 }
 
 extern "C" int tt_attention_varlen(const float* qkv, int64_t ld_qkv, const int32_t* cu_seqlens,
@@ -2598,11 +2796,12 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
     if (rc) return rc;
     for (int l = 0; l < NL; ++l) {
       const tt_bert_layer& L = m->layer[l];
-      rc = gemm_bf16_impl(xs, 2 * H, L.wqkv_x3c, 3 * H, L.bqkv, nullptr, 0, w.qkv, 3 * H, nullptr,
-                          0, (int)T, 3 * H, 3 * H, ACT_NONE, stream, H, false);
+      uint16_t* qs = (uint16_t*)w.qkv;  // [T, 6H] planes in the f32 path's [T, 3H] buffer
+      rc = gemm_bf16_impl(xs, 2 * H, L.wqkv_x3c, 3 * H, L.bqkv, nullptr, 0, nullptr, 0, qs, 6 * H,
+                          (int)T, 3 * H, 3 * H, ACT_NONE, stream, H, true);
       if (rc) return rc;
-      rc = attention_varlen_impl(w.qkv, 3 * H, cu_seqlens, n_seq, max_len, H, m->heads,
-                                 TT_PREC_X3, nullptr, 2 * H, cs, stream, 1);
+      rc = tt_attention_varlen_x3c(qs, 6 * H, cu_seqlens, n_seq, max_len, H, m->heads, cs, 2 * H,
+                                   stream);
       if (rc) return rc;
       rc = gemm_ln_impl(cs, 2 * H, L.wo_x3c, 3 * H, L.bo, L.ln1_g, L.ln1_b, m->ln_eps, w.x, H, xs,
                         2 * H, (int)T, H, 3 * H, stream, H);

@@ -106,6 +106,8 @@ SIGNATURES = {
                                    _i32, _i32, _i32, _i32, _vp]),
     "tt_x3_split_weights": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp]),
     "tt_debug_plant_bad_row": (ctypes.c_int, [_i32, _i32]),
+    "tt_attention_varlen_x3c": (ctypes.c_int, [_vp, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _i64,
+                                               _vp]),
     "tt_x3c_weights": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp]),
     "tt_gemm_x3c": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64,
                                    _i32, _i32, _i32, _i32, _vp]),
