@@ -251,6 +251,9 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #ifndef TT_EXP_PRIO
 #define TT_EXP_PRIO 0  // s_setprio 1 for waves 4-7 (static priority for the younger half)
 #endif
+#ifndef TT_RING_EARLY
+#define TT_RING_EARLY 1  // k_filter_ring: first ring DMAs before the query loads (0: after)
+#endif
 #ifndef TT_RING_NT
 // Non-temporal (aux = 2) ring DMA.  1 (default): the small-batch full level (LVL 2: one query
 // tile, so every catalog byte is read exactly once) -- one-buyer full level 0.139 -> 0.124 ms
@@ -466,7 +469,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
     const uint16_t* __restrict__ xb, int64_t ld, const float* __restrict__ q, int nq,
     int64_t ldq, const float* __restrict__ theta, int64_t stride, int64_t n_sample,
     int rows_per_slab, int n_slabs, int n_qt, uint64_t* __restrict__ lists,
-    int* __restrict__ counts, QueryInit qinit) {
+    int* __restrict__ counts, QueryInit qinit, const uint16_t* __restrict__ q16) {
   constexpr int TR = RingCfg<EP>::TR, QB = RingK<EP, LVL>::QB;
   constexpr int RG_PD = RingK<EP, LVL>::PD, RG_SLOTS = RingK<EP, LVL>::SLOTS;
   constexpr int KS = EP / 32, QPW = 16 * QB, QPB = RG_WAVES * QPW;
@@ -495,50 +498,6 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
 
   bf16x8 qf[QB][KS];
   float th[QB];
-  const bool init = qinit.eps2 != nullptr;  // first level: theta = -inf, query state set here
-#pragma unroll
-  for (int b = 0; b < QB; ++b) {
-    const int qi = qbase + 16 * b + col;
-    const bool v = qi < nq;
-    th[b] = !v ? __builtin_huge_valf() : init ? -__builtin_huge_valf() : theta[qi];
-    const float* qp = q + (int64_t)(v ? qi : 0) * ldq + 8 * g;
-    float sq = 0.0f, st = 0.0f, sr = 0.0f;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const f32x4 v0 = *(const f32x4*)(qp + 32 * s);
-      const f32x4 v1 = *(const f32x4*)(qp + 32 * s + 4);
-      u32x4 u = {pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]), pack_bf16x2(v1[0], v1[1]),
-                 pack_bf16x2(v1[2], v1[3])};
-      qf[b][s] = __builtin_bit_cast(bf16x8, u);
-      if (init && slab == 0) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float x = i < 4 ? v0[i] : v1[i - 4];
-          const uint32_t h = (u[i >> 1] >> (16 * (i & 1))) & 0xffffu;
-          const float xt = __uint_as_float(h << 16);
-          sq = fmaf(x, x, sq);
-          st = fmaf(xt, xt, st);
-          sr = fmaf(x - xt, x - xt, sr);
-        }
-      }
-    }
-    if (init && slab == 0) {  // lanes col, col+16, col+32, col+48 hold the query's 4 parts
-      sq += __shfl_xor(sq, 16, 64);
-      st += __shfl_xor(st, 16, 64);
-      sr += __shfl_xor(sr, 16, 64);
-      sq += __shfl_xor(sq, 32, 64);
-      st += __shfl_xor(st, 32, 64);
-      sr += __shfl_xor(sr, 32, 64);
-      if (v && g == 0) {
-        qinit.eps2[qi] = query_eps2<EP>(sq, st, sr, qinit.X, qinit.R);
-        qinit.aref[qi] = -__builtin_huge_valf();
-        qinit.flags[qi] = 0;
-        qinit.qsel_n[1 + qi] = 0;  // done[qi] (FilterWs layout)
-        if (qi == 0) *qinit.qsel_n = 0;
-      }
-    }
-  }
-  for (int i = tid; i < QPB; i += 64 * RG_WAVES) qcnt[i] = 0;
 
   const int64_t j0 = (int64_t)slab * rows_per_slab;
   const int64_t j1 = (j0 + rows_per_slab < n_sample) ? j0 + rows_per_slab : n_sample;
@@ -594,6 +553,69 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
     if (j0 + (int64_t)(t + 1) * TR > j1) issue_t(t, std::true_type{});
     else issue_t(t, std::false_type{});
   };
+  // the ring's first tiles go out BEFORE the queries are loaded (TT_RING_EARLY): the query
+  // loads' latency and the first tiles' DMA latency overlap instead of adding up per block
+  if (TT_RING_EARLY)
+    for (int t = 0; t < RG_PD && t < n_tiles; ++t) issue(t);
+  // this wave's queries as bf16 B-fragments (+ the first level's per-query state)
+  const bool init = qinit.eps2 != nullptr;  // first level: theta = -inf, query state set here
+  if (q16 != nullptr && !init) {
+    // the bf16 query image (k_query_eps wrote it with this conversion): half the bytes of the
+    // f32 rows and no branch between the loads, so all QB x KS fragment loads are in flight at
+    // once (the f32 path's per-step conversion + first-level branch serialised them)
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      const int qi = qbase + 16 * b + col;
+      const bool v = qi < nq;
+      th[b] = !v ? __builtin_huge_valf() : theta[qi];
+      const uint16_t* qp = q16 + (int64_t)(v ? qi : 0) * EP + 8 * g;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) qf[b][s] = *(const bf16x8*)(qp + 32 * s);
+    }
+  } else
+#pragma unroll
+  for (int b = 0; b < QB; ++b) {
+    const int qi = qbase + 16 * b + col;
+    const bool v = qi < nq;
+    th[b] = !v ? __builtin_huge_valf() : init ? -__builtin_huge_valf() : theta[qi];
+    const float* qp = q + (int64_t)(v ? qi : 0) * ldq + 8 * g;
+    float sq = 0.0f, st = 0.0f, sr = 0.0f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const f32x4 v0 = *(const f32x4*)(qp + 32 * s);
+      const f32x4 v1 = *(const f32x4*)(qp + 32 * s + 4);
+      u32x4 u = {pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]), pack_bf16x2(v1[0], v1[1]),
+                 pack_bf16x2(v1[2], v1[3])};
+      qf[b][s] = __builtin_bit_cast(bf16x8, u);
+      if (init && slab == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float x = i < 4 ? v0[i] : v1[i - 4];
+          const uint32_t h = (u[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+          const float xt = __uint_as_float(h << 16);
+          sq = fmaf(x, x, sq);
+          st = fmaf(xt, xt, st);
+          sr = fmaf(x - xt, x - xt, sr);
+        }
+      }
+    }
+    if (init && slab == 0) {  // lanes col, col+16, col+32, col+48 hold the query's 4 parts
+      sq += __shfl_xor(sq, 16, 64);
+      st += __shfl_xor(st, 16, 64);
+      sr += __shfl_xor(sr, 16, 64);
+      sq += __shfl_xor(sq, 32, 64);
+      st += __shfl_xor(st, 32, 64);
+      sr += __shfl_xor(sr, 32, 64);
+      if (v && g == 0) {
+        qinit.eps2[qi] = query_eps2<EP>(sq, st, sr, qinit.X, qinit.R);
+        qinit.aref[qi] = -__builtin_huge_valf();
+        qinit.flags[qi] = 0;
+        qinit.qsel_n[1 + qi] = 0;  // done[qi] (FilterWs layout)
+        if (qi == 0) *qinit.qsel_n = 0;
+      }
+    }
+  }
+  for (int i = tid; i < QPB; i += 64 * RG_WAVES) qcnt[i] = 0;
   // Candidate pool: each wave owns RG_WPOOL 8-byte entries and the counters of its own queries,
   // so appends need no atomics and no cross-wave synchronisation; the pool position `wn` is a
   // wave-uniform (scalar) count.  Entry = (orderable score << 32) | (row offset in the slab's
@@ -739,7 +761,8 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
                      : (QB > 1 && 2 + (QB - 1) * SP < KS) ? 2
                      : (QB > 1 && 1 + (QB - 1) * SP < KS) ? 1 : -1;  // -1: every block at step 1
   static_assert(KS % (FD + 1) == 0 && S_MID < KS - FD, "fragment ring layout");
-  for (int t = 0; t < RG_PD && t < n_tiles; ++t) issue(t);
+  if (!TT_RING_EARLY)
+    for (int t = 0; t < RG_PD && t < n_tiles; ++t) issue(t);
   wait_tiles(n_tiles - 1 < RG_PD - 1 ? n_tiles - 1 : RG_PD - 1);
   lds_barrier();  // tile 0 landed; counters initialised
   // A wave without a single real query only moves its share of the ring DMA, in lockstep with
@@ -2626,9 +2649,19 @@ __global__ __launch_bounds__(256) void k_query_eps(const float* __restrict__ q, 
                                                    float* __restrict__ theta,
                                                    float* __restrict__ aref,
                                                    int* __restrict__ flags,
-                                                   int* __restrict__ qsel_n) {
+                                                   int* __restrict__ qsel_n,
+                                                   uint16_t* __restrict__ q16) {
   const int qi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (qi >= nq) return;
+  if (q16) {  // the bf16 image the ring levels load (the conversion k_filter_ring's f32 path does)
+    const float* qr = q + (int64_t)qi * ldq;
+    for (int c = lane; c < EP / 8; c += 64) {
+      const f32x4 v0 = *(const f32x4*)(qr + 8 * c), v1 = *(const f32x4*)(qr + 8 * c + 4);
+      *(u32x4*)(q16 + (int64_t)qi * EP + 8 * c) =
+          u32x4{pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]), pack_bf16x2(v1[0], v1[1]),
+                pack_bf16x2(v1[2], v1[3])};
+    }
+  }
   if (lane == 0) {  // filter state of query qi
     theta[qi] = -__builtin_huge_valf();
     aref[qi] = -__builtin_huge_valf();
@@ -2667,6 +2700,10 @@ struct FilterPlan {
 static bool select_reg_disabled() {  // TT_SELECT_REG=0: LDS-staged k_select_wave (timing builds)
   static const bool off = env_switch("TT_SELECT_REG", 1) == 0;
   return off;
+}
+static bool q16_enabled() {  // TT_FILTER_Q16=0: ring levels load f32 queries (timing builds)
+  static const bool on = env_switch("TT_FILTER_Q16", 1) != 0;
+  return on;
 }
 static bool topm_disabled() {  // TT_FILTER_TOPM=0: the multi-level small path (timing builds)
   static const bool off = env_switch("TT_FILTER_TOPM", 1) == 0;
@@ -2839,6 +2876,8 @@ struct FilterWs {
   int* done;
   void* scan_ws;
   int64_t scan_ws_bytes;
+  uint16_t* q16;     // [nq][ep] bf16 query image (k_query_eps), for the ring levels
+  bool q16_valid;    // written by this search's k_query_eps
   int64_t total;
 };
 
@@ -2871,6 +2910,8 @@ static FilterWs carve(void* base, const FilterPlan& p, int64_t n, int d, int nq,
   tt_scan_workspace_bytes(n, d, nq, k, &sb);
   w.scan_ws_bytes = sb;
   w.scan_ws = take(sb);
+  w.q16 = (uint16_t*)take((int64_t)nq * tt_padded_dim(d) * 2);
+  w.q16_valid = false;
   w.total = off;
   return w;
 }
@@ -2893,7 +2934,7 @@ static void launch_level(const Level& L, const uint16_t* xb, int64_t n, int64_t 
       if (lvl == 4) kern = k_filter_ring<EP, 4>;
     hipLaunchKernelGGL(kern, dim3(nblk), dim3(64 * RG_WAVES), 0, st, xb, ld, q, nq, ldq, w.theta,
                        L.stride, L.n_sample, L.rows_per_slab, L.n_slabs, L.n_qt, w.lists,
-                       w.counts, qi);
+                       w.counts, qi, w.q16_valid ? (const uint16_t*)w.q16 : nullptr);
   }
 }
 
@@ -2996,9 +3037,9 @@ int filter_setup(const float* db, const uint16_t* db_bf16, int64_t n, int32_t d,
 
 // Per-query state (eps2, theta, aref, flags, qsel_n).  fold != nullptr and a ring first level
 // (the tmax-first plan): that launch initialises it (*fold filled in, no launch here).
-int filter_init(const FilterWs& w, const float* q, int nq, int64_t ld_q, int ep, float x_norm_max,
+int filter_init(FilterWs& w, const float* q, int nq, int64_t ld_q, int ep, float x_norm_max,
                 float x_resid_max, hipStream_t st, const FilterPlan* p = nullptr,
-                QueryInit* fold = nullptr) {
+                QueryInit* fold = nullptr, bool want_q16 = false) {
   TT_REQUIRE(x_norm_max >= 0.0f && x_resid_max >= 0.0f,
              "x_norm_max / x_resid_max must be >= 0 (tt_bf16_image_bounds)");
   if (fold) *fold = QueryInit{0.0f, 0.0f, nullptr, nullptr, nullptr, nullptr};
@@ -3012,11 +3053,13 @@ int filter_init(const FilterWs& w, const float* q, int nq, int64_t ld_q, int ep,
 #define TT_QE(E)                                                                              \
   case E:                                                                                     \
     hipLaunchKernelGGL(k_query_eps<E>, dim3(eps_grid), dim3(256), 0, st, q, nq, ld_q,         \
-                       x_norm_max, x_resid_max, w.eps2, w.theta, w.aref, w.flags, w.qsel_n); \
+                       x_norm_max, x_resid_max, w.eps2, w.theta, w.aref, w.flags, w.qsel_n,  \
+                       want_q16 ? w.q16 : nullptr);                                          \
     break;
     TT_QE(64) TT_QE(128) TT_QE(256) TT_QE(384) TT_QE(512) TT_QE(768)
 #undef TT_QE
   }
+  w.q16_valid = want_q16;
   return check_launch("filter_init");
 }
 
@@ -3205,7 +3248,13 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
                                  w.done, out_score, out_idx, w.scan_ws, w.scan_ws_bytes, st);
   }
   QueryInit qinit;
-  if ((rc = filter_init(w, q, nq, ld_q, ep, x_norm_max, x_resid_max, st, &p, &qinit))) return rc;
+  // large batches: k_query_eps (one launch) writes the per-query state AND the bf16 query
+  // image the ring levels load; smaller ones fold the state into the first level (no launch)
+  const bool q16 = nq > RG_SMALL_NQ && q16_enabled();
+  if ((rc = filter_init(w, q, nq, ld_q, ep, x_norm_max, x_resid_max, st, &p, q16 ? nullptr : &qinit,
+                        q16)))
+    return rc;
+  if (q16) qinit = QueryInit{0.0f, 0.0f, nullptr, nullptr, nullptr, nullptr};
   // small batches: block-per-query selection (k_select_small) and a fused selection +
   // f32-MFMA re-rank of the full level (k_final_small)
   const bool small = p.small;
@@ -3345,7 +3394,9 @@ extern "C" int tt_sharded_filter_begin(const uint16_t* sample_bf16, int64_t n_sa
     }
   }
   hipStream_t st = (hipStream_t)stream;
-  if ((rc = filter_init(w, q, nq, ld_q, ep, 0.0f, 0.0f, st))) return rc;
+  if ((rc = filter_init(w, q, nq, ld_q, ep, 0.0f, 0.0f, st, nullptr, nullptr,
+                        nq > RG_SMALL_NQ && q16_enabled())))
+    return rc;
   for (int li = 0; li < p.n_levels; ++li) {
     const bool last = li == p.n_levels - 1;
     if ((rc = filter_level(p, w, li, 0, sample_bf16, n_sample, ld, q, nq, ld_q, k, ep, st, nullptr,
@@ -3373,7 +3424,9 @@ extern "C" int tt_sharded_filter_full(const uint16_t* db_bf16, int64_t n, int32_
                          &ep, &p, &w);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
-  if ((rc = filter_init(w, q, nq, ld_q, ep, x_norm_max, x_resid_max, st))) return rc;
+  if ((rc = filter_init(w, q, nq, ld_q, ep, x_norm_max, x_resid_max, st, nullptr, nullptr,
+                        nq > RG_SMALL_NQ && q16_enabled())))
+    return rc;
   hipLaunchKernelGGL(k_stats_theta, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, stats,
                      w.eps2, nq, w.aref, w.theta);
   if ((rc = check_launch("k_stats_theta"))) return rc;
