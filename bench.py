@@ -238,6 +238,37 @@ def configs1(a, dev, rank):
             "min_cos": float(cos.min()), "max_1_minus_cos": float((1 - cos).max()),
             "max_abs_diff": float((ys[prec] - ys["f32"]).abs().max())}
     res["x3_over_f32_texts_per_s"] = res["x3"]["texts_per_s"] / res["f32"]["texts_per_s"]
+    # the same 100k texts through the chunking the drop-in API runs: ItemTower.encode_batch(
+    # texts, batch_size=256) encodes device chunks of device_batch = 4096 texts (same results
+    # row for row, tests/test_gpu_encoder.py), then the top-100 of every 256 new embeddings
+    # (pre-tokenized ids: the tokenizer is host-side and out of scope)
+    DB = ItemTower.device_batch
+    enc = BertEncoder(sd, cfg, device=dev, prec="x3")
+    chunks = [pack_sequences(seqs[i:i + DB], dev) for i in range(0, n_txt, DB)]
+    pooled = torch.empty((DB, cfg["hidden"]), device=dev)
+
+    def chunk_step(c):
+        ids, cu, mx = chunks[c]
+        nt = cu.numel() - 1
+        enc.encode_packed(ids, cu, mx, out=pooled[:nt])
+        y = it.head(pooled[:nt], bid[c * DB:c * DB + nt], cid[c * DB:c * DB + nt], use_cat=True)
+        for j in range(0, nt, BS):
+            nb_ = min(BS, nt - j)
+            kernels.l2norm_rows(y[j:j + nb_], E, _lib.TT_NORM_ADD_EPS, out=qn[:nb_])
+            kernels.scan_topk_bf16(cat, cat16, 100_000, E, qn[:nb_], K, bnd, workspace=ws)
+
+    chunk_step(0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for c in range(len(chunks)):
+        chunk_step(c)
+    torch.cuda.synchronize()
+    dtc = time.perf_counter() - t0
+    res["x3_api_chunks"] = {
+        "texts_per_s": n_txt / dtc, "device_batch": DB, "texts": n_txt,
+        "is": ("ItemTower.encode_batch(texts, batch_size=256)'s device chunking (4096 texts per "
+               "encoder call, x3) + exact top-100 per 256 new embeddings")}
+    del enc
     out.update(res)
     out["value"] = res["x3"]["texts_per_s"]
     out["value_prec"] = "x3 (f32 precision class; bf16 throughput mode under 'bf16')"
@@ -300,8 +331,28 @@ def batch_sweep(a, shard, shard16, n, E, K, bounds, dev):
                        "bf16_pass_frac_end_to_end": 2.0 * n * ep / (t * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                        "full_level_frac": 2.0 * n * ep / (l_ * 1e-3) / 1e9 / HBM_PEAK_GBPS}
         del ws
+    # k in (128, 1000] (the /retrieve cap, server.py:46): the exact f32 scan, nq = 1, k = 1000
+    q = torch.zeros((1, ep), device=dev)
+    q[:, :E] = torch.randn((1, E), generator=g, device=dev)
+    kernels.l2norm_rows(q, E, _lib.TT_NORM_ADD_EPS, out=q)
+    k2 = 1000
+    ws = torch.empty(kernels.scan_workspace_bytes(n, E, 1, k2), dtype=torch.uint8, device=dev)
+    for _ in range(3):
+        kernels.scan_topk(shard, n, E, q, k2, workspace=ws)
+    tk = []
+    for _ in range(21):
+        torch.cuda.synchronize()
+        ev[2].record(stream)
+        kernels.scan_topk(shard, n, E, q, k2, workspace=ws)
+        ev[3].record(stream)
+        torch.cuda.synchronize()
+        tk.append(ev[2].elapsed_time(ev[3]))
+    t = float(np.median(tk))
+    k1000 = {"nq": 1, "k": k2, "ms_per_search": t, "kernel": "k_scan_topk_f32 (exact f32 scan)",
+             "f32_pass_bytes": 4.0 * n * ep,
+             "f32_pass_frac_end_to_end": 4.0 * n * ep / (t * 1e-3) / 1e9 / HBM_PEAK_GBPS}
     return {"catalog": f"{n} x {E}", "k": K, "timing": "median of 21 synchronised calls",
-            "by_batch": res}
+            "by_batch": res, "k1000_nq1": k1000}
 
 
 def catalog_10m(a, dev, nq=10_000, n=10_000_000):
