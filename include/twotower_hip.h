@@ -254,13 +254,14 @@ typedef struct tt_bert_layer {
   /* TT_PREC_X3, optional: pre-split images [N, 2K] (tt_x3_split_weights); NULL -> the f32
    * weights are split on the fly */
   const uint16_t *wqkv_x3, *wo_x3, *w1_x3, *w2_x3;
-  /* TT_PREC_X3 at H == 384 (head dim 32, I % 64 == 0), optional: K-concatenated images
-   * W' [N, 3K] bf16 = [bf16(W) | bf16(W - bf16(W)) | bf16(W)] (tt_x3c_weights).  When all four
-   * are set the encoder takes the x3c form: each GEMM is ONE bf16 GEMM over K' = 3K whose A
-   * operand is the [hi | lo] bf16 plane pair of the f32 activation (written so by its producer:
-   * embedding LayerNorm, attention, the fused GEMM + LayerNorm, the FFN1 GELU epilogue) -- the
-   * same three products hi.hi + hi.lo + lo.hi as TT_PREC_X3, on the persistent ring GEMMs. */
-  const uint16_t *wqkv_x3c, *wo_x3c, *w1_x3c, *w2_x3c;
+  /* TT_PREC_X3 at H == 384 (head dim 32, I % 64 == 0), optional: x3i images W' [N, 2K] bf16
+   * (tt_x3i_weights: per 32 k, 32 hi = bf16(W) then 32 lo = bf16(W - hi)).  When all four are
+   * set the encoder takes the x3i form: every GEMM runs on the bf16 MFMA kernels with both
+   * operands x3i interleaved -- per 32 k the three products hi.hi + lo.hi + hi.lo of
+   * TT_PREC_X3, no split in the GEMM loop -- and every producer (embedding LayerNorm,
+   * attention, the fused GEMM + LayerNorm, the QKV / FFN1 epilogues) writes its activation
+   * x3i interleaved. */
+  const uint16_t *wqkv_x3i, *wo_x3i, *w1_x3i, *w2_x3i;
 } tt_bert_layer;
 
 typedef struct tt_bert_model {
@@ -299,28 +300,25 @@ int tt_gemm_x3w(const float* A, int64_t lda, const uint16_t* Wx3, int64_t ld_wx3
                 const float* bias, const float* residual, int64_t ldr, float* C, int64_t ldc,
                 uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N, int32_t K, int32_t act,
                 void* stream);
-/* tt_x3c_weights: W [N, K] f32 -> out [N, 3K] bf16 = [hi | lo | hi], hi = bf16(W) (RNE),
- * lo = bf16(W - hi) (the x3c GEMMs' W').  tt_gemm_x3c: C[M,N] = act(A . W^T + bias) + residual
- * with A given as its split planes A2 [M, 2K] = [bf16(A) | bf16(A - bf16(A))] and W as W3 [N, 3K]
- * (tt_x3c_weights): acc = A_hi.W_hi + A_hi.W_lo + A_lo.W_hi over K' = 3K on bf16 MFMA with f32
- * accumulation.  Exactly one of C (f32) and C_split (the result's own planes [M, 2N], ld >= 2N,
- * residual NULL) is written.  K % 64 == 0.  tt_gemm_ln_x3c: tt_gemm_ln_bf16 in that form
- * (A2 [M, 2K], W3 [384, 3K]) writing x f32 and its planes x_split [M, 768]. */
-int tt_x3c_weights(const float* W, int64_t ldw, int32_t N, int32_t K, uint16_t* out,
+/* Split-bf16 interleaved rows ("x3i"): an f32 row v of length K (K % 32 == 0) as 2K bf16,
+ * per 32 elements first hi = bf16(v) (round to nearest even) then lo = bf16(v - hi).
+ * tt_x3i_weights: W [N, K] f32 -> out [N, 2K] x3i.  tt_gemm_x3i: the x3 product
+ * act(A . W^T + bias) with A2 [M, 2K] and W2 [N, 2K] x3i rows (acc = A_hi.W_hi + A_hi.W_lo +
+ * A_lo.W_hi on bf16 MFMA, f32 accumulation), written as x3i rows C2 [M, 2N] (N % 32 == 0).
+ * tt_gemm_ln_x3i: tt_gemm_ln_bf16 in that form (A2 [M, 2K], W2 [384, 2K]) writing x f32 and
+ * its x3i rows x2 [M, 768].  tt_attention_varlen_x3i: the encoder's attention over x3i QKV
+ * rows qkv2 [T, >= 6H] (a head's Q / K / V = 32-blocks h / heads + h / 2 heads + h), every
+ * product as three bf16 MFMAs, f32 softmax; context out2 [T, >= 2H] x3i.  Head dim 32. */
+int tt_x3i_weights(const float* W, int64_t ldw, int32_t N, int32_t K, uint16_t* out,
                    int64_t ld_out, void* stream);
-int tt_gemm_x3c(const uint16_t* A2, int64_t lda2, const uint16_t* W3, int64_t ldw3,
-                const float* bias, const float* residual, int64_t ldr, float* C, int64_t ldc,
-                uint16_t* C_split, int64_t ldc_split, int32_t M, int32_t N, int32_t K, int32_t act,
-                void* stream);
-int tt_gemm_ln_x3c(const uint16_t* A2, int64_t lda2, const uint16_t* W3, int64_t ldw3,
+int tt_gemm_x3i(const uint16_t* A2, int64_t lda2, const uint16_t* W2, int64_t ldw2,
+                const float* bias, uint16_t* C2, int64_t ldc2, int32_t M, int32_t N, int32_t K,
+                int32_t act, void* stream);
+int tt_gemm_ln_x3i(const uint16_t* A2, int64_t lda2, const uint16_t* W2, int64_t ldw2,
                    const float* bias, const float* gamma, const float* beta, float eps, float* x,
-                   int64_t ldx, uint16_t* x_split, int64_t ldx_split, int32_t M, int32_t H,
-                   int32_t K, void* stream);
-/* tt_attention_varlen_x3c: the x3c encoder's attention -- qkv2 [T, ld >= 6H] bf16 rows
- * [Q K V hi | Q K V lo] (the QKV GEMM's split planes, lo at column 3H), every product as
- * three bf16 MFMAs (hi.hi + lo.hi + hi.lo), f32 softmax; context out2 [T, ld >= 2H] as its
- * own planes (hi | lo at column H).  Head dim 32, max_len <= 512. */
-int tt_attention_varlen_x3c(const uint16_t* qkv2, int64_t ld_qkv2, const int32_t* cu_seqlens,
+                   int64_t ldx, uint16_t* x2, int64_t ldx2, int32_t M, int32_t H, int32_t K,
+                   void* stream);
+int tt_attention_varlen_x3i(const uint16_t* qkv2, int64_t ld_qkv2, const int32_t* cu_seqlens,
                             int32_t n_seq, int32_t max_len, int32_t H, int32_t heads,
                             uint16_t* out2, int64_t ld_out2, void* stream);
 int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,

@@ -106,69 +106,61 @@ def test_gemm_x3_presplit_weights_identical(M, N, K, act):
     assert Wx[3 % N, 64 * kb + 32 + slot] == (w - hi.float()).to(torch.bfloat16)
 
 
-def _planes(x):
-    """f32 [M, K] -> the x3c A operand [M, 2K] bf16 = [bf16(x) | bf16(x - bf16(x))]."""
+def _x3i(x):
+    """f32 [M, K] -> x3i interleaved rows [M, 2K] bf16: per 32 columns, bf16(x) then
+    bf16(x - bf16(x)) (the x3 encoder's operand format, tt_x3i_weights)."""
+    M, K = x.shape
     hi = x.to(torch.bfloat16)
-    return torch.cat([hi, (x - hi.float()).to(torch.bfloat16)], 1).contiguous()
+    lo = (x - hi.float()).to(torch.bfloat16)
+    return torch.stack([hi.view(M, K // 32, 32), lo.view(M, K // 32, 32)], 2).reshape(M, 2 * K)
 
 
-@pytest.mark.parametrize("M,N,K,act,split", [(1, 128, 64, 0, False), (77, 256, 512, 2, False),
-                                             (300, 1152, 384, 0, False), (300, 1536, 384, 1, True),
-                                             (18300, 1152, 384, 0, False),
-                                             (18300, 1536, 384, 1, True),
-                                             (70001, 1152, 384, 0, False),
-                                             (66000, 1536, 384, 1, True),
-                                             (50001, 1000, 384, 1, True),
-                                             (40000, 384, 1536, 0, False)])
-def test_gemm_x3c_vs_torch(M, N, K, act, split):
-    """K-concatenated split-bf16 GEMM (tt_gemm_x3c: A as [hi | lo] planes, W' = [hi | lo | hi],
-    one bf16 GEMM over 3K): the x3 tolerance vs the f64 product of the f32 operands, on the
-    128x128 kernel (small M), the 256x256 / 256x128 ring kernels (large M) and the split-plane
-    output (the FFN1 -> W2 form, checked by recombining hi + lo)."""
+def _x3i_value(y2):
+    """x3i rows [M, 2N] -> (hi, lo) [M, N] as float."""
+    M, N2 = y2.shape
+    v = y2.view(M, N2 // 64, 2, 32).float()
+    return v[:, :, 0].reshape(M, N2 // 2), v[:, :, 1].reshape(M, N2 // 2)
+
+
+@pytest.mark.parametrize("M,N,K,act", [(1, 128, 64, 0), (77, 256, 512, 2), (300, 1152, 384, 0),
+                                       (300, 1536, 384, 1), (18300, 1152, 384, 0),
+                                       (18300, 1536, 384, 1), (70001, 1152, 384, 0),
+                                       (66000, 1536, 384, 1), (50001, 1024, 384, 1),
+                                       (40000, 384, 1536, 0)])
+def test_gemm_x3i_vs_torch(M, N, K, act):
+    """The x3 encoder's GEMM (tt_gemm_x3i: A and W as x3i interleaved split-bf16 rows, three
+    bf16 MFMAs per 32 k on the bf16 kernels, result written x3i): the x3 tolerance vs the f64
+    product of the f32 operands -- the 128x128 kernel (small M), the 256x256 / 256x128 ring
+    kernels (large M) -- with the result's hi + lo recombined."""
     from twotower import _lib
-    from twotower.item_tower import x3c_weights
+    from twotower.item_tower import x3i_weights
 
     g = torch.Generator(device="cuda").manual_seed(M + 3 * N + K + act)
     A = torch.randn((M, K), generator=g, device="cuda")
     W = torch.randn((N, K), generator=g, device="cuda") / K ** 0.5
     b = torch.randn(N, generator=g, device="cuda")
-    R = None if split else torch.randn((M, N), generator=g, device="cuda")
-    W3 = x3c_weights(W)
-    hi = W.to(torch.bfloat16)
-    assert torch.equal(W3[:, :K], hi) and torch.equal(W3[:, 2 * K:], hi)
-    assert torch.equal(W3[:, K:2 * K], (W - hi.float()).to(torch.bfloat16))
-    A2 = _planes(A)
-    if split:
-        C2 = torch.empty((M, 2 * N), device="cuda", dtype=torch.bfloat16)
-        _lib.check(_lib.lib().tt_gemm_x3c(A2.data_ptr(), A2.stride(0), W3.data_ptr(), W3.stride(0),
-                                          b.data_ptr(), None, 0, None, 0, C2.data_ptr(),
-                                          C2.stride(0), M, N, K, act, _lib.stream_ptr()), "x3c")
-        C = C2[:, :N].float() + C2[:, N:].float()
-        # the planes are a split of one f32 value: |lo| <= half a bf16 ulp of hi
-        hi, lo = C2[:, :N].float(), C2[:, N:].float()
-        assert bool((lo.abs() <= hi.abs() * 2.0 ** -8).all())
-    else:
-        C = torch.empty((M, N), device="cuda")
-        _lib.check(_lib.lib().tt_gemm_x3c(A2.data_ptr(), A2.stride(0), W3.data_ptr(), W3.stride(0),
-                                          b.data_ptr(), R.data_ptr(), R.stride(0), C.data_ptr(),
-                                          C.stride(0), None, 0, M, N, K, act, _lib.stream_ptr()),
-                   "x3c")
+    W2 = x3i_weights(W)
+    assert torch.equal(W2, _x3i(W))
+    A2 = _x3i(A)
+    C2 = torch.empty((M, 2 * N), device="cuda", dtype=torch.bfloat16)
+    _lib.check(_lib.lib().tt_gemm_x3i(A2.data_ptr(), A2.stride(0), W2.data_ptr(), W2.stride(0),
+                                      b.data_ptr(), C2.data_ptr(), C2.stride(0), M, N, K, act,
+                                      _lib.stream_ptr()), "x3i")
+    hi, lo = _x3i_value(C2)
+    assert bool((lo.abs() <= hi.abs() * 2.0 ** -8).all())  # |lo| <= half a bf16 ulp of hi
+    C = hi + lo
     ref = (A.double() @ W.double().T) + b.double()
     ref = {0: ref, 1: F.gelu(ref), 2: torch.relu(ref)}[act]
-    if R is not None:
-        ref = ref + R.double()
-    # split planes hold the f32 value to 2^-17 relative (the dropped remainder)
-    tol = 5e-5 if not split else 6e-5
-    torch.testing.assert_close(C.double(), ref, rtol=1e-5, atol=tol)
+    torch.testing.assert_close(C.double(), ref, rtol=1e-5, atol=6e-5)
 
 
-@pytest.mark.parametrize("M,K", [(1, 384), (129, 1536), (18300, 384), (18300, 1536),
+@pytest.mark.parametrize("M,K", [(1, 384), (129, 1536), (5000, 384), (18300, 384), (18300, 1536),
                                  (70003, 1536)])
-def test_gemm_ln_x3c_vs_torch(M, K):
-    """Fused GEMM + LayerNorm in the x3c form (tt_gemm_ln_x3c): x = LN(A W^T + b + x) in place
-    with x's [hi | lo] planes, vs the f64 composition of the f32 operands."""
+def test_gemm_ln_x3i_vs_torch(M, K):
+    """Fused GEMM + LayerNorm in the x3i form (tt_gemm_ln_x3i): x = LN(A W^T + b + x) in place
+    with x's x3i rows, vs the f64 composition of the f32 operands (80 / 96 / 128-row tiles)."""
     from twotower import _lib
-    from twotower.item_tower import x3c_weights
+    from twotower.item_tower import x3i_weights
 
     H = 384
     g = torch.Generator(device="cuda").manual_seed(M + 5 * K)
@@ -180,15 +172,15 @@ def test_gemm_ln_x3c_vs_torch(M, K):
     x = torch.randn((M, H), generator=g, device="cuda") * 2 + 0.5
     ref = F.layer_norm(A.double() @ W.double().T + b.double() + x.double(), (H,), gm.double(),
                        bt.double(), 1e-12)
-    A2, W3 = _planes(A), x3c_weights(W)
+    A2, W2 = _x3i(A), x3i_weights(W)
     xs = torch.empty((M, 2 * H), device="cuda", dtype=torch.bfloat16)
-    _lib.check(_lib.lib().tt_gemm_ln_x3c(A2.data_ptr(), A2.stride(0), W3.data_ptr(), W3.stride(0),
+    _lib.check(_lib.lib().tt_gemm_ln_x3i(A2.data_ptr(), A2.stride(0), W2.data_ptr(), W2.stride(0),
                                          b.data_ptr(), gm.data_ptr(), bt.data_ptr(), 1e-12,
                                          x.data_ptr(), H, xs.data_ptr(), 2 * H, M, H, K,
-                                         _lib.stream_ptr()), "gemm_ln_x3c")
+                                         _lib.stream_ptr()), "gemm_ln_x3i")
     torch.cuda.synchronize()
     torch.testing.assert_close(x.double(), ref, rtol=2e-5, atol=5e-5)
-    assert torch.equal(xs, _planes(x))
+    assert torch.equal(xs, _x3i(x))
 
 
 @pytest.mark.parametrize("M,N,K", [(5, 128, 64), (300, 1152, 384), (2049, 384, 1536)])
@@ -305,9 +297,9 @@ def test_attention_varlen_vs_torch(lens, kind):
 
 
 @pytest.mark.parametrize("lens", [[1], [7, 64, 128], [3, 200, 1, 512, 33], [31, 32, 33, 17]])
-def test_attention_x3c_planes_vs_torch(lens):
-    """tt_attention_varlen_x3c (the x3c encoder's attention: QKV as split-bf16 planes in, the
-    context's planes out, three MFMAs per product): the x3 tolerance of the f32 attention."""
+def test_attention_x3i_vs_torch(lens):
+    """tt_attention_varlen_x3i (the x3 encoder's attention: QKV as x3i split-bf16 rows in, the
+    context x3i out, three MFMAs per product): the x3 tolerance of the f32 attention."""
     from twotower import _lib
 
     H, nh = 384, 12
@@ -316,10 +308,11 @@ def test_attention_x3c_planes_vs_torch(lens):
     qkv = torch.randn((T, 3 * H), device="cuda", generator=g)
     cu = torch.tensor(np.concatenate([[0], np.cumsum(lens)]), dtype=torch.int32, device="cuda")
     out2 = torch.empty((T, 2 * H), device="cuda", dtype=torch.bfloat16)
-    _lib.check(_lib.lib().tt_attention_varlen_x3c(_planes(qkv).data_ptr(), 6 * H, cu.data_ptr(),
+    _lib.check(_lib.lib().tt_attention_varlen_x3i(_x3i(qkv).data_ptr(), 6 * H, cu.data_ptr(),
                                                   len(lens), max(lens), H, nh, out2.data_ptr(),
-                                                  2 * H, _lib.stream_ptr()), "attn_x3c")
-    out = out2[:, :H].float() + out2[:, H:].float()
+                                                  2 * H, _lib.stream_ptr()), "attn_x3i")
+    hi, lo = _x3i_value(out2)
+    out = hi + lo
     ref = torch.empty((T, H), device="cuda", dtype=torch.float64)
     c = cu.tolist()
     for i in range(len(lens)):
@@ -363,7 +356,7 @@ def test_encoder_bf16_close_to_f32(golden):
 
 def test_encoder_x3_split_in_loop_path_non384_hidden():
     """Hidden sizes other than 384 keep the x3 path with the split done in the GEMM loop
-    (k_gemm<float, 2>, the x3c form needs the fused H = 384 GEMM + LayerNorm): vs the f32 path."""
+    (k_gemm<float, 2>; the x3i form needs the fused H = 384 GEMM + LayerNorm): vs the f32 path."""
     cfg = dict(vocab=300, hidden=256, layers=2, heads=8, intermediate=1024, max_positions=128,
                type_vocab=2, ln_eps=1e-12)
     rng = np.random.default_rng(3)

@@ -135,12 +135,18 @@ __device__ __forceinline__ int enc_xcd_remap(int bid, int nblk) {
 // ACTC >= 0: the activation as a compile-time constant (no per-element branch); BFO: the
 // caller guarantees the bf16-only output form (C == NULL, res == NULL, C16 16-B aligned,
 // ldc16 % 8 == 0) -- the persistent kernel's specialisations.
+// Split-bf16 interleaved rows ("x3i"), the x3 encoder's activation / weight format: a row of N
+// f32 values is 2N bf16, per 32 columns first their hi = bf16(v) then their lo = bf16(v - hi).
+// A 128-B LDS row of a GEMM stage is then one 32-k block's hi (chunks 0-3) and lo (4-7): the
+// bf16 kernels' two k-halves become the hi and lo operands of the same 32 k.
+__device__ __forceinline__ int x3i_col(int n) { return 64 * (n >> 5) + (n & 31); }
+
 // OM: output form.  0 = generic (C and / or C16, residual), 1 = BFO, 3 = f32 C only (no
-// residual, no C16: the x3c QKV GEMM, whose consumer splits its operands itself), 2 = SPLIT: the x3
-// encoder's split-bf16 planes (C == NULL, res == NULL): C16 row m holds hi = bf16(y) at column
-// n and lo = bf16(y - hi) at column N + n (ldc16 >= 2N, N % 8 == 0, 16-B aligned rows), i.e.
-// the A operand [hi | lo] of the next x3 GEMM (k_gemm_wide / k_gemm_ln with kx = N).
-// split_n > 0 selects the same planes at run time in the generic form (k_gemm's small-M path).
+// residual, no C16), 2 = SPLIT: the x3 encoder's split-bf16 interleaved rows (C == NULL,
+// res == NULL): C16 row m holds, per 32 columns, hi = bf16(y) then lo = bf16(y - hi)
+// (x3i_col; ldc16 >= 2N, N % 32 == 0, 16-B aligned rows), i.e. the A operand of the next x3
+// GEMM.  split_n > 0 selects the same form at run time in the generic epilogue (k_gemm's
+// small-M path).
 template <bool FAST, int ACTC = -1, int OM = 0>
 __device__ __forceinline__ int gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, int nw0,
                                                    int lane, int M, int N,
@@ -166,7 +172,7 @@ __device__ __forceinline__ int gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, i
                    (!C16 || (ldc16 % 4) == 0) && ((uintptr_t)bias % 16) == 0 &&
                    ((uintptr_t)res % 16) == 0 && ((uintptr_t)C % 16) == 0 &&
                    ((uintptr_t)C16 % 8) == 0 && mw0 + 64 <= M && nw0 + 64 <= N &&
-                   (!SPL || ((N % 8) == 0 && (ldc16 % 8) == 0 && ((uintptr_t)C16 % 16) == 0)) &&
+                   (!SPL || ((N % 32) == 0 && (ldc16 % 8) == 0 && ((uintptr_t)C16 % 16) == 0)) &&
                    (SPL || split_n == 0);
   if (vec) {
     // full tile: every bias / residual load is issued before the first use, so their
@@ -234,9 +240,10 @@ __device__ __forceinline__ int gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, i
           const auto s1 = __builtin_amdgcn_permlane16_swap(ph[0][1], ph[1][1], false, false);
           const auto t0 = __builtin_amdgcn_permlane16_swap(pl[0][0], pl[1][0], false, false);
           const auto t1 = __builtin_amdgcn_permlane16_swap(pl[0][1], pl[1][1], false, false);
-          const int n = nw0 + 32 * jp + 16 * (g & 1) + 8 * (g >> 1);
-          *(u32x4*)(C16 + m * ldc16 + n) = u32x4{s0[0], s1[0], s0[1], s1[1]};
-          *(u32x4*)(C16 + m * ldc16 + N + n) = u32x4{t0[0], t1[0], t0[1], t1[1]};
+          const int n = nw0 + 32 * jp + 16 * (g & 1) + 8 * (g >> 1);  // 8 columns, one 32-block
+          uint16_t* o = C16 + m * ldc16 + x3i_col(n);
+          *(u32x4*)o = u32x4{s0[0], s1[0], s0[1], s1[1]};
+          *(u32x4*)(o + 32) = u32x4{t0[0], t1[0], t0[1], t1[1]};
         }
       }
       return 16;
@@ -318,10 +325,13 @@ __device__ __forceinline__ int gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, i
         if (C) C[(int64_t)m * ldc + n + u] = y;
         if (C16) {
           const uint16_t hv = f32_to_bf16_rne(y);
-          C16[(int64_t)m * ldc16 + n + u] = hv;
-          if (split_n > 0)
-            C16[(int64_t)m * ldc16 + split_n + n + u] =
-                f32_to_bf16_rne(y - __uint_as_float((uint32_t)hv << 16));
+          if (split_n > 0) {
+            uint16_t* o = C16 + (int64_t)m * ldc16 + x3i_col(n + u);
+            o[0] = hv;
+            o[32] = f32_to_bf16_rne(y - __uint_as_float((uint32_t)hv << 16));
+          } else {
+            C16[(int64_t)m * ldc16 + n + u] = hv;
+          }
         }
       }
     }
@@ -372,19 +382,17 @@ __global__ __launch_bounds__(256) void k_x3_split_w(const float* __restrict__ W,
   *(u32x4*)(o + 32) = __builtin_bit_cast(u32x4, lo);
 }
 
-// x3c weights: W [N, K] f32 -> [N, 3K] bf16 = [hi | lo | hi] (see x3c_acol).  Thread per element.
-__global__ __launch_bounds__(256) void k_x3c_w(const float* __restrict__ W, int64_t ldw, int N,
+// x3i weights: W [N, K] f32 -> [N, 2K] bf16 interleaved (x3i_col).  Thread per element.
+__global__ __launch_bounds__(256) void k_x3i_w(const float* __restrict__ W, int64_t ldw, int N,
                                                int K, uint16_t* __restrict__ out, int64_t ldo) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= (int64_t)N * K) return;
   const int n = (int)(e / K), k = (int)(e % K);
   const float v = W[(int64_t)n * ldw + k];
   const uint16_t hv = f32_to_bf16_rne(v);
-  const uint16_t lv = f32_to_bf16_rne(v - __uint_as_float((uint32_t)hv << 16));
-  uint16_t* o = out + (int64_t)n * ldo;
-  o[k] = hv;
-  o[K + k] = lv;
-  o[2 * K + k] = hv;
+  uint16_t* o = out + (int64_t)n * ldo + x3i_col(k);
+  o[0] = hv;
+  o[32] = f32_to_bf16_rne(v - __uint_as_float((uint32_t)hv << 16));
 }
 
 // X3M = 2: W arrives pre-split (k_x3_split_w): each 32-k stage of a W row is 128 B = 32 hi
@@ -392,24 +400,17 @@ __global__ __launch_bounds__(256) void k_x3c_w(const float* __restrict__ W, int6
 // lane's hi / lo operands -- only A is split in the loop (half the VALU of X3M = 1, which was
 // VALU-bound: 192 VALU beside 48 MFMAs per wave and stage).  W is passed as float* (the same
 // 128-B rows per 32 k), ldw in those 4-B units.
-// K-concatenated split-bf16 ("x3c") GEMMs: A [M, 2K] = [hi | lo] bf16 planes (written so by
-// their producers), W' [N, 3K] = [W_hi | W_lo | W_hi] (prepared once), and the bf16 GEMM runs
-// over K' = 3K with A's k-column j read at j (j < K: hi . W_hi), j - K (K <= j < 2K: hi . W_lo)
-// and j - K (j >= 2K: lo . W_hi) -- the three products of the x3 split as ONE bf16 GEMM, on the
-// persistent ring kernels, with no split VALU in the loop.  kx = K (0: a plain GEMM).
-__device__ __forceinline__ int64_t x3c_acol(int64_t k0, int kx) {
-  return (kx > 0 && k0 >= kx) ? k0 - kx : k0;
-}
-
-template <typename T, int X3M = 0>
+// X3I (T = bf16): the stage's A and W rows are x3i interleaved (K here = 2 x the product's K):
+// per 32 k, acc += W_hi A_hi + W_lo A_hi + W_hi A_lo -- the split-bf16 (x3) product with the
+// bf16 kernels' data path and no split VALU (the producers wrote the operands split).
+template <typename T, int X3M = 0, bool X3I = false>
 __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_t lda,
                                                  const T* __restrict__ W, int64_t ldw,
                                                  const float* __restrict__ bias,
                                                  const float* __restrict__ res, int64_t ldr,
                                                  float* __restrict__ C, int64_t ldc,
                                                  uint16_t* __restrict__ C16, int64_t ldc16,
-                                                 int M, int N, int K, int act, int kx,
-                                                 int split_n) {
+                                                 int M, int N, int K, int act, int split_n) {
   constexpr int BK = GemmElt<T>::BK;
   constexpr int EPC = 16 / sizeof(T);  // elements per 16-B chunk
   __shared__ __attribute__((aligned(16))) char smem[2 * GM_STAGE_B];
@@ -439,7 +440,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_
   }
   auto issue = [&](int kt) {
     char* st = smem + (kt & 1) * GM_STAGE_B;
-    const int64_t k0 = (int64_t)kt * BK, ka = x3c_acol(k0, kx);
+    const int64_t k0 = (int64_t)kt * BK, ka = k0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int p = w + 4 * j;
@@ -518,6 +519,26 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const T* __restrict__ A, int64_
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(blo[j], ahi[i], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bhi[j], alo[i], acc[i][j], 0, 0, 0);
         }
+    } else if constexpr (X3I) {
+      static_assert(sizeof(T) == 2, "x3i: bf16 operands");
+      lds_wait<0>();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        reg_tie(av[0][i]);
+        reg_tie(av[1][i]);
+        reg_tie(bv[0][i]);
+        reg_tie(bv[1][i]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bf16x8e ah = __builtin_bit_cast(bf16x8e, av[0][i]), al = __builtin_bit_cast(bf16x8e, av[1][i]);
+          const bf16x8e bh = __builtin_bit_cast(bf16x8e, bv[0][j]), bl = __builtin_bit_cast(bf16x8e, bv[1][j]);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al, acc[i][j], 0, 0, 0);
+        }
     } else {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -564,14 +585,14 @@ constexpr int GB_BN = 128, GB_MAXN = 2048;
 // T = float: the split-bf16 (x3) product of k_gemm<float, true> on this ring -- a stage is 32
 // f32 (the same 128-B LDS rows, so DMA, swizzle and fragment reads are unchanged), and the
 // stage's two read steps form one 8-f32 slot set per lane (split_bf16x8, 3 MFMAs per block).
-template <int GB_BM, int GB_SLOTS, int ACT, int BFO, typename T = uint16_t>
+template <int GB_BM, int GB_SLOTS, int ACT, int BFO, typename T = uint16_t, bool X3I = false>
 __global__ __launch_bounds__(GB_BM * 2, 512 / (GB_BM * 2)) void k_gemm_big(const T* __restrict__ A, int64_t lda,
                                                      const T* __restrict__ W, int64_t ldw,
                                                      const float* __restrict__ bias,
                                                      const float* __restrict__ res, int64_t ldr,
                                                      float* __restrict__ C, int64_t ldc,
                                                      uint16_t* __restrict__ C16, int64_t ldc16,
-                                                     int M, int N, int K, int act, int kx) {
+                                                     int M, int N, int K, int act) {
   constexpr bool X3 = sizeof(T) == 4;
   constexpr int BK = 128 / sizeof(T), EPC = 16 / sizeof(T);
   constexpr int GB_A_B = GB_BM * 128, GB_W_B = GB_BN * 128, GB_STAGE_B = GB_A_B + GB_W_B;
@@ -625,7 +646,7 @@ __global__ __launch_bounds__(GB_BM * 2, 512 / (GB_BM * 2)) void k_gemm_big(const
   };
   auto issue = [&](const Offs& o, int kt, int gs) __attribute__((always_inline)) {
     char* st = smem + (gs % GB_SLOTS) * GB_STAGE_B;
-    const int64_t k0 = (int64_t)kt * BK, ka = x3c_acol(k0, kx);
+    const int64_t k0 = (int64_t)kt * BK, ka = k0;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       __builtin_amdgcn_global_load_lds(
@@ -721,6 +742,25 @@ __global__ __launch_bounds__(GB_BM * 2, 512 / (GB_BM * 2)) void k_gemm_big(const
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(blo[j], ahi[i], acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bhi[j], alo[i], acc[i][j], 0, 0, 0);
           }
+      } else if constexpr (X3I) {
+        lds_wait<0>();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          reg_tie(av[0][i]);
+          reg_tie(av[1][i]);
+          reg_tie(bv[0][i]);
+          reg_tie(bv[1][i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const bf16x8e ah = __builtin_bit_cast(bf16x8e, av[0][i]), al = __builtin_bit_cast(bf16x8e, av[1][i]);
+            const bf16x8e bh = __builtin_bit_cast(bf16x8e, bv[0][j]), bl = __builtin_bit_cast(bf16x8e, bv[1][j]);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, ah, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl, ah, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bh, al, acc[i][j], 0, 0, 0);
+          }
       } else {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -758,14 +798,14 @@ __global__ __launch_bounds__(GB_BM * 2, 512 / (GB_BM * 2)) void k_gemm_big(const
 #ifndef TT_GWEXP_NOEPI
 #define TT_GWEXP_NOEPI 0  // timing-only (results WRONG): k_gemm_wide without its epilogue
 #endif
-template <int ACT, int BFO>
+template <int ACT, int BFO, bool X3I = false>
 __global__ __launch_bounds__(512, 1) void k_gemm_wide(const uint16_t* __restrict__ A, int64_t lda,
                                                       const uint16_t* __restrict__ W, int64_t ldw,
                                                       const float* __restrict__ bias,
                                                       const float* __restrict__ res, int64_t ldr,
                                                       float* __restrict__ C, int64_t ldc,
                                                       uint16_t* __restrict__ C16, int64_t ldc16,
-                                                      int M, int N, int K, int act, int kx) {
+                                                      int M, int N, int K, int act) {
   constexpr int BM = 256, BN = 256, BK = 64, EPC = 8, SLOTS = 2;
   constexpr int A_B = BM * 128, STAGE_B = A_B + BN * 128;
   __shared__ __attribute__((aligned(16))) char smem[SLOTS * STAGE_B];
@@ -805,7 +845,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wide(const uint16_t* __restrict
   };
   auto issue = [&](const Offs& o, int kt, int gs) __attribute__((always_inline)) {
     char* st = smem + (gs & 1) * STAGE_B;
-    const int64_t k0 = (int64_t)kt * BK, ka = x3c_acol(k0, kx);
+    const int64_t k0 = (int64_t)kt * BK, ka = k0;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       __builtin_amdgcn_global_load_lds(
@@ -861,6 +901,55 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wide(const uint16_t* __restrict
       enc_lds_barrier();  // stage visible to all; the other slot is free again
       issue_next();
       const uint32_t sb = lds_addr(smem) + (uint32_t)(((gs + kt) & 1) * STAGE_B);
+      if constexpr (X3I) {
+        // x3i: the stage's hi (k-half 0) and lo (k-half 1) of the same 32 k; A's 8 fragments
+        // stay for the stage, W's 8 per 64-column half
+        u32x4 av[2][4];
+        const uint32_t pa0 = sb + fa[0], pa1 = sb + fa[1];
+        av[0][0] = lds_read128<0>(pa0);
+        av[0][1] = lds_read128<2048>(pa0);
+        av[0][2] = lds_read128<4096>(pa0);
+        av[0][3] = lds_read128<6144>(pa0);
+        av[1][0] = lds_read128<0>(pa1);
+        av[1][1] = lds_read128<2048>(pa1);
+        av[1][2] = lds_read128<4096>(pa1);
+        av[1][3] = lds_read128<6144>(pa1);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t pb0 = sb + fb[0] + 8192 * h, pb1 = sb + fb[1] + 8192 * h;
+          u32x4 bh[4], bl[4];
+          bh[0] = lds_read128<0>(pb0);
+          bh[1] = lds_read128<2048>(pb0);
+          bh[2] = lds_read128<4096>(pb0);
+          bh[3] = lds_read128<6144>(pb0);
+          bl[0] = lds_read128<0>(pb1);
+          bl[1] = lds_read128<2048>(pb1);
+          bl[2] = lds_read128<4096>(pb1);
+          bl[3] = lds_read128<6144>(pb1);
+          lds_wait<0>();
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            reg_tie(av[0][i]);
+            reg_tie(av[1][i]);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            reg_tie(bh[j]);
+            reg_tie(bl[j]);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const bf16x8e ah = __builtin_bit_cast(bf16x8e, av[0][i]), al = __builtin_bit_cast(bf16x8e, av[1][i]);
+              const bf16x8e wh = __builtin_bit_cast(bf16x8e, bh[j]), wl = __builtin_bit_cast(bf16x8e, bl[j]);
+              acc[h][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, ah, acc[h][i][j], 0, 0, 0);
+              acc[h][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, ah, acc[h][i][j], 0, 0, 0);
+              acc[h][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, al, acc[h][i][j], 0, 0, 0);
+            }
+        }
+        continue;
+      }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const uint32_t pa = sb + fa[s], pb = sb + fb[s];
@@ -945,7 +1034,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wide(const uint16_t* __restrict
 //     restaged >= 2 phases after its last read, so one barrier per phase orders both RAW and
 //     WAR.  The DMA sequence runs across output tiles (persistent blocks), so the epilogue of a
 //     tile overlaps the next tile's first loads.
-// kx: the x3c K-concatenation (x3c_acol).  OM / ACT: as k_gemm_wide.
+// OM / ACT: as k_gemm_wide.
 #ifndef TT_GPP_PRIO
 #define TT_GPP_PRIO 1  // s_setprio(1) around each phase's MFMAs
 #endif
@@ -962,7 +1051,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_pp(const uint16_t* __restrict__
                                                     const float* __restrict__ res, int64_t ldr,
                                                     float* __restrict__ C, int64_t ldc,
                                                     uint16_t* __restrict__ C16, int64_t ldc16,
-                                                    int M, int N, int K, int act, int kx) {
+                                                    int M, int N, int K, int act) {
   constexpr int BM = 256, BN = 256, BK = 64, EPC = 8;
   constexpr int HB = 128 * 128;              // half-tile buffer: 128 rows x 128 B
   constexpr int SET_B = 4 * HB;              // one K-tile: A0 A1 B0 B1
@@ -995,7 +1084,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_pp(const uint16_t* __restrict__
     const int r = gi / nk, kt = gi - r * nk;
     const int lt = tile_of(r);
     const int m0 = (lt / n_tn) * BM + 128 * h;
-    const int64_t ka = x3c_acol((int64_t)kt * BK, kx);
+    const int64_t ka = (int64_t)kt * BK;
     char* dst = smem + (gi & 1) * SET_B + h * HB;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -1189,8 +1278,8 @@ TT_CHECK_EXP(TT_GEXP_NOSTORE || TT_GWEXP_NOEPI || TT_GLEXP_NOW || TT_GLEXP_NOEPI
 // layout-independent order (each row's 384 columns as 8 partial sums of 48 columns, each
 // partial summed over its lanes, the 8 combined by a fixed tree), so a row's bits do not
 // depend on the tile height the batch size selected.
-// SPL: the x3c encoder -- A and W are the K-concatenated split operands (kx = K / 3, see
-// x3c_acol) and x's bf16 copy is the [hi | lo] plane pair (X16 row: hi at n, lo at GL_H + n).
+// SPL: the x3 encoder -- A and W are x3i interleaved rows (K = 2 x the product's K; per 32 k
+// the three split-bf16 products, as k_gemm<X3I>) and x's bf16 copy is written interleaved too.
 template <int BM, bool SPL = false>
 __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__ A, int64_t lda,
                                                     const uint16_t* __restrict__ W, int64_t ldw,
@@ -1199,7 +1288,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
                                                     const float* __restrict__ beta, float eps,
                                                     float* __restrict__ X, int64_t ldx,
                                                     uint16_t* __restrict__ X16, int64_t ldx16,
-                                                    int M, int K, int kx) {
+                                                    int M, int K) {
   static_assert(BM == 128 || BM == 96 || BM == 80, "k_gemm_ln: BM");
   constexpr int WM_N = BM == 80 ? 1 : 2;     // waves along M
   constexpr int WN_N = 8 / WM_N;             // waves along N
@@ -1252,7 +1341,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
   };
   auto issue_a = [&](const int64_t (&ao)[2], int kt, int t) __attribute__((always_inline)) {
     char* st = smem + (t % GL_ASLOTS) * A_B;
-    const int64_t k0 = (int64_t)kt * BK, ka = x3c_acol(k0, kx);
+    const int64_t k0 = (int64_t)kt * BK, ka = k0;
 #pragma unroll
     for (int j = 0; j < 2; ++j)
       __builtin_amdgcn_global_load_lds(
@@ -1339,6 +1428,26 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
 #pragma unroll
         for (int j = 0; j < NJ; ++j) bv[s][j] = lds_read128<0>(pb + 2048 * j);
       }
+      if constexpr (SPL) {  // x3i: hi (k-half 0) and lo (k-half 1) of the same 32 k
+        lds_wait<0>();
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+#pragma unroll
+          for (int i = 0; i < MI; ++i) reg_tie(av[s][i]);
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) reg_tie(bv[s][j]);
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const bf16x8e ah = __builtin_bit_cast(bf16x8e, av[0][i]), al = __builtin_bit_cast(bf16x8e, av[1][i]);
+            const bf16x8e wh = __builtin_bit_cast(bf16x8e, bv[0][j]), wl = __builtin_bit_cast(bf16x8e, bv[1][j]);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, ah, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, ah, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, al, acc[i][j], 0, 0, 0);
+          }
+      } else {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         if (s == 0) lds_wait<(MI + NJ) < 15 ? MI + NJ : 15>();
@@ -1354,6 +1463,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                 __builtin_bit_cast(bf16x8e, bv[s][j]), __builtin_bit_cast(bf16x8e, av[s][i]),
                 acc[i][j], 0, 0, 0);
+      }
       }
     }
     gs += nk;
@@ -1461,13 +1571,17 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
         *(f32x4*)(X + m * ldx + n) = acc[i][j];
         const uint2 hv = uint2{pack_bf16_hw(acc[i][j][0], acc[i][j][1]),
                                pack_bf16_hw(acc[i][j][2], acc[i][j][3])};
-        *(uint2*)(X16 + m * ldx16 + n) = hv;
-        if constexpr (SPL)
-          *(uint2*)(X16 + m * ldx16 + GL_H + n) =
+        if constexpr (SPL) {
+          uint16_t* o = X16 + m * ldx16 + x3i_col(n);
+          *(uint2*)o = hv;
+          *(uint2*)(o + 32) =
               uint2{pack_bf16_hw(acc[i][j][0] - __uint_as_float(hv.x << 16),
                                  acc[i][j][1] - __uint_as_float(hv.x & 0xffff0000u)),
                     pack_bf16_hw(acc[i][j][2] - __uint_as_float(hv.y << 16),
                                  acc[i][j][3] - __uint_as_float(hv.y & 0xffff0000u))};
+        } else {
+          *(uint2*)(X16 + m * ldx16 + n) = hv;
+        }
       }
     }
     prev_full = full;
@@ -1526,7 +1640,7 @@ __global__ __launch_bounds__(256) void k_embed_ln(const int32_t* __restrict__ id
                                                   const float* __restrict__ beta, float eps,
                                                   float* __restrict__ y, uint16_t* __restrict__ y16,
                                                   int H, int split16) {
-  // split16: y16 rows are [hi | lo] planes (ld 2H) for the x3c encoder, else bf16 copies (ld H)
+  // split16: y16 rows are x3i interleaved (ld 2H) for the x3 encoder, else bf16 copies (ld H)
   // blocks (sequence, chunk of 4 tokens), wave per token (the position is t - cu[seq]; a
   // per-token binary search over cu was 13 dependent loads per token at 5k sequences).  Was a
   // block per sequence whose waves walked its tokens: at configs[1]'s 256 sequences that is
@@ -1567,8 +1681,13 @@ __global__ __launch_bounds__(256) void k_embed_ln(const int32_t* __restrict__ id
         y[t * H + e] = o;
         if (y16) {
           const uint16_t hv = f32_to_bf16_rne(o);
-          y16[t * (split16 ? 2 * H : H) + e] = hv;
-          if (split16) y16[t * 2 * H + H + e] = f32_to_bf16_rne(o - __uint_as_float((uint32_t)hv << 16));
+          if (split16) {
+            uint16_t* d = y16 + t * 2 * H + x3i_col(e);
+            d[0] = hv;
+            d[32] = f32_to_bf16_rne(o - __uint_as_float((uint32_t)hv << 16));
+          } else {
+            y16[t * H + e] = hv;
+          }
         }
       }
     }
@@ -1655,7 +1774,7 @@ __global__ __launch_bounds__(256) void k_attn32_mfma(const TI* __restrict__ qkv,
                                                      uint16_t* __restrict__ out16,
                                                      int split16) {
   // split16 (X3 only, out == NULL): out16 rows [hi | lo] (ldo = 2H, lo at column H + c), the
-  // A operand of the x3c Wo GEMM
+  // A operand of a Wo GEMM over [hi | lo] planes
   constexpr int DH = 32;
   constexpr int ES = BF ? 2 : 4;
   constexpr int KROW = DH * ES + 16;
@@ -2015,17 +2134,18 @@ __global__ __launch_bounds__(256 * HG) void k_attn32_bf16(
   }
 }
 
-// x3c attention: the fast kernel's structure (K / V^T staged with 16-B loads, HG heads of a
+// x3 attention: the fast kernel's structure (K / V^T staged with 16-B loads, HG heads of a
 // sequence per block, two passes over the keys) on split-bf16 operands.  qkv arrives as the
-// QKV GEMM's [hi | lo] planes (row: Q K V hi, then Q K V lo at column lo_off = 3H); each
-// product is three bf16 MFMAs (hi.hi + lo.hi + hi.lo, as k_attn32_mfma<X3>): S = K Q^T and
-// O^T = V^T P^T with P split in registers.  Pass 1 finds each query's row maximum from the
-// hi.hi scores only (an offset for exp2's range; the softmax is exact for any offset), pass 2
-// the full scores, exp2 and P.V.  The context goes out as the Wo GEMM's [hi | lo] planes.
+// QKV GEMM's x3i interleaved rows (a head's 32 dims = one 32-block: 64 B hi then 64 B lo;
+// Q of head h is block h, K block heads + h, V block 2 heads + h); each product is three
+// bf16 MFMAs (hi.hi + lo.hi + hi.lo, as k_attn32_mfma<X3>): S = K Q^T and O^T = V^T P^T with
+// P split in registers.  Pass 1 finds each query's row maximum from the hi.hi scores only (an
+// offset for exp2's range; the softmax is exact for any offset), pass 2 the full scores, exp2
+// and P.V.  The context goes out x3i interleaved (the Wo GEMM's A).
 // LDS per head: K rows hi | lo (144 B) and V^T as two bf16 planes.
 template <int HG>
 __global__ __launch_bounds__(256 * HG) void k_attn32_x3(
-    const uint16_t* __restrict__ qkv, int64_t ldq, int lo_off, const int32_t* __restrict__ cu,
+    const uint16_t* __restrict__ qkv, int64_t ldq, const int32_t* __restrict__ cu,
     int H, int heads, float scale, uint16_t* __restrict__ out16, int64_t ldo) {
   constexpr int DH = 32, KROW = 2 * DH * 2 + 16;
   constexpr int WPH = 4, NT = 64 * HG * WPH;
@@ -2045,9 +2165,9 @@ __global__ __launch_bounds__(256 * HG) void k_attn32_x3(
   char* Vt = Ks + (size_t)Lk * KROW;
   auto load_q = [&](int q0_, u32x4& qh, u32x4& qlo) __attribute__((always_inline)) {
     const int qr = q0_ + ql < L ? q0_ + ql : L - 1;
-    const uint16_t* qp = qkv + (int64_t)(t0 + qr) * ldq + h * DH + 8 * g;
+    const uint16_t* qp = qkv + (int64_t)(t0 + qr) * ldq + 64 * h + 8 * g;
     qh = *(const u32x4*)qp;
-    qlo = *(const u32x4*)(qp + lo_off);
+    qlo = *(const u32x4*)(qp + 32);
   };
   u32x4 qnh, qnl;
   load_q(16 * wsub < L ? 16 * wsub : 0, qnh, qnl);
@@ -2058,14 +2178,14 @@ __global__ __launch_bounds__(256 * HG) void k_attn32_x3(
     char* Ks_ = sm + hs * per_head;
     char* Vp = Ks_ + (size_t)Lk * KROW + pl * vplane;
     u32x4 k0 = {0u, 0u, 0u, 0u}, k1 = k0, v0 = k0, v1 = k0;
-    const uint16_t* row = qkv + (int64_t)(t0 + j) * ldq + (pl ? lo_off : 0) + (h0 + hs) * DH + c8;
+    const uint16_t* row = qkv + (int64_t)(t0 + j) * ldq + 64 * (h0 + hs) + 32 * pl + c8;
     if (j < L) {
-      k0 = *(const u32x4*)(row + H);
-      v0 = *(const u32x4*)(row + 2 * H);
+      k0 = *(const u32x4*)(row + 2 * H);
+      v0 = *(const u32x4*)(row + 4 * H);
     }
     if (j + 1 < L) {
-      k1 = *(const u32x4*)(row + ldq + H);
-      v1 = *(const u32x4*)(row + ldq + 2 * H);
+      k1 = *(const u32x4*)(row + ldq + 2 * H);
+      v1 = *(const u32x4*)(row + ldq + 4 * H);
     }
     *(u32x4*)(Ks_ + j * KROW + pl * 64 + c8 * 2) = k0;
     *(u32x4*)(Ks_ + (j + 1) * KROW + pl * 64 + c8 * 2) = k1;
@@ -2147,16 +2267,16 @@ __global__ __launch_bounds__(256 * HG) void k_attn32_x3(
     }
     float lsum = lpart + __shfl_xor(lpart, 16, 64);
     lsum += __shfl_xor(lsum, 32, 64);
-    // acc[db][v] = O^T[dim 16 db + 4 g + v][query q0 + ql] -> the context's hi | lo planes
+    // acc[db][v] = O^T[dim 16 db + 4 g + v][query q0 + ql] -> the context, x3i interleaved
     if (q0 + ql < L) {
       const float inv = 1.0f / lsum;
 #pragma unroll
       for (int db = 0; db < 2; ++db) {
         const f32x4 o = acc[db] * inv;
-        uint16_t* o16 = out16 + (int64_t)(t0 + q0 + ql) * ldo + h * DH + 16 * db + 4 * g;
+        uint16_t* o16 = out16 + (int64_t)(t0 + q0 + ql) * ldo + 64 * h + 16 * db + 4 * g;
         const uint2 hv = uint2{pack_bf16_hw(o[0], o[1]), pack_bf16_hw(o[2], o[3])};
         *(uint2*)o16 = hv;
-        *(uint2*)(o16 + H) = uint2{pack_bf16_hw(o[0] - __uint_as_float(hv.x << 16),
+        *(uint2*)(o16 + 32) = uint2{pack_bf16_hw(o[0] - __uint_as_float(hv.x << 16),
                                                 o[1] - __uint_as_float(hv.x & 0xffff0000u)),
                                    pack_bf16_hw(o[2] - __uint_as_float(hv.y << 16),
                                                 o[3] - __uint_as_float(hv.y & 0xffff0000u))};
@@ -2251,7 +2371,7 @@ bool gemm_pp_enabled() {  // TT_GEMM_PP=1: k_gemm_pp for the 256x256 tiles (timi
   static const bool on = env_switch("TT_GEMM_PP", 0) != 0;
   return on;
 }
-bool x3c_enabled() {  // TT_X3C=0: the x3 path's split-in-loop GEMMs (A/B timing, tests)
+bool x3c_enabled() {  // TT_X3C=0: the x3 path's split-in-loop GEMMs (timing builds: A/B)
   static const bool on = env_switch("TT_X3C", 1) != 0;
   return on;
 }
@@ -2300,18 +2420,18 @@ static int gemm_f32_impl(const float* A, int64_t lda, const float* W, int64_t ld
     // 128x128 two-stage kernel left the MFMA pipes ~75% idle on DMA latency
     hipLaunchKernelGGL((k_gemm_big<256, 3, -1, false, float>), dim3(ncu), dim3(512), 0,
                        (hipStream_t)stream, A, lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16,
-                       ldc16, M, N, K, act, 0);
+                       ldc16, M, N, K, act);
     return check_launch("tt_gemm_x3(persistent)");
   }
   if (wx3)
     hipLaunchKernelGGL((k_gemm<float, 2>), dim3(nblk), dim3(256), 0, (hipStream_t)stream, A,
-                       lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act, 0, 0);
+                       lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act, 0);
   else if (x3)
     hipLaunchKernelGGL((k_gemm<float, 1>), dim3(nblk), dim3(256), 0, (hipStream_t)stream, A,
-                       lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act, 0, 0);
+                       lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act, 0);
   else
     hipLaunchKernelGGL((k_gemm<float, 0>), dim3(nblk), dim3(256), 0, (hipStream_t)stream, A,
-                       lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act, 0, 0);
+                       lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act, 0);
   return check_launch(wx3 ? "tt_gemm_x3w" : x3 ? "tt_gemm_x3" : "tt_gemm_f32");
 }
 
@@ -2346,15 +2466,16 @@ extern "C" int tt_x3_split_weights(const float* W, int64_t ldw, int32_t N, int32
   return check_launch("tt_x3_split_weights");
 }
 
-extern "C" int tt_x3c_weights(const float* W, int64_t ldw, int32_t N, int32_t K, uint16_t* out,
+extern "C" int tt_x3i_weights(const float* W, int64_t ldw, int32_t N, int32_t K, uint16_t* out,
                               int64_t ld_out, void* stream) {
   TT_REQUIRE(N >= 0 && K >= 0, "negative size");
   if (N == 0 || K == 0) return TT_OK;
-  TT_REQUIRE(W && out && ldw >= K && ld_out >= 3 * (int64_t)K, "null pointer or ld too small");
+  if (K % 32 != 0) return fail(TT_ERR_UNSUPPORTED, "tt_x3i_weights: need K % 32 == 0");
+  TT_REQUIRE(W && out && ldw >= K && ld_out >= 2 * (int64_t)K, "null pointer or ld too small");
   const int64_t n = (int64_t)N * K;
-  hipLaunchKernelGGL(k_x3c_w, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+  hipLaunchKernelGGL(k_x3i_w, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, W, ldw, N, K, out, ld_out);
-  return check_launch("tt_x3c_weights");
+  return check_launch("tt_x3i_weights");
 }
 
 extern "C" int tt_gemm_x3w(const float* A, int64_t lda, const uint16_t* Wx3, int64_t ldwx3,
@@ -2366,12 +2487,13 @@ extern "C" int tt_gemm_x3w(const float* A, int64_t lda, const uint16_t* Wx3, int
                        act, stream, true, Wx3, ldwx3);
 }
 
-// bf16 GEMM dispatch.  kx > 0: the x3c form (x3c_acol; K = 3 kx, A [M, 2 kx] planes, W [N, 3 kx]);
-// split: C_bf16 receives [hi | lo] planes (C == NULL, residual == NULL, ldc16 >= 2N).
+// bf16 GEMM dispatch.  x3i: A [M, K] and W [N, K] are x3i interleaved rows (K = 2 x the
+// product's K; k_gemm*<..., X3I>), and the result goes out split (x3i interleaved C_bf16 [M, 2N],
+// C == NULL, residual == NULL).  split without x3i is not offered.
 static int gemm_bf16_impl(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
                           const float* bias, const float* residual, int64_t ldr, float* C,
                           int64_t ldc, uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N,
-                          int32_t K, int32_t act, void* stream, int32_t kx, bool split) {
+                          int32_t K, int32_t act, void* stream, bool x3i) {
   TT_REQUIRE(M >= 0 && N >= 0 && K >= 0, "negative size");
   if (M == 0 || N == 0) return TT_OK;
   if (K % GemmElt<uint16_t>::BK != 0)
@@ -2380,11 +2502,9 @@ static int gemm_bf16_impl(const uint16_t* A, int64_t lda, const uint16_t* W, int
   TT_REQUIRE(lda % 8 == 0 && ldw % 8 == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)W % 16) == 0,
              "A/W must be 16-B aligned with lda, ldw % 8 == 0");
   TT_REQUIRE(act >= 0 && act <= 2, "bad activation");
-  TT_REQUIRE(kx == 0 || (kx % 64 == 0 && K == 3 * kx && lda >= 2 * (int64_t)kx),
-             "x3c: K == 3 kx, kx % 64 == 0, A holds [hi | lo] (lda >= 2 kx)");
-  TT_REQUIRE(!split || (!C && !residual && C_bf16 && N % 8 == 0 && ldc16 >= 2 * (int64_t)N &&
-                        ldc16 % 8 == 0 && ((uintptr_t)C_bf16 % 16) == 0),
-             "split output: C_bf16 only, N % 8 == 0, ldc16 >= 2N (16-B aligned rows)");
+  TT_REQUIRE(!x3i || (!C && !residual && C_bf16 && N % 32 == 0 && ldc16 >= 2 * (int64_t)N &&
+                      ldc16 % 8 == 0 && ((uintptr_t)C_bf16 % 16) == 0),
+             "x3i output: C_bf16 only, N % 32 == 0, ldc16 >= 2N (16-B aligned rows)");
   // large M: the persistent 256x128 ring kernel (one block per CU) once there are at least
   // two tiles per CU
   const int nbig = ((M + 255) / 256) * ((N + GB_BN - 1) / GB_BN);
@@ -2395,44 +2515,39 @@ static int gemm_bf16_impl(const uint16_t* A, int64_t lda, const uint16_t* W, int
     const bool bfo = !C && !residual && C_bf16 && ldc16 % 8 == 0 && ((uintptr_t)C_bf16 % 16) == 0;
     auto launch = [&](auto kern, int blocks, int threads) {
       hipLaunchKernelGGL(kern, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, A, lda, W, ldw,
-                         bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act, kx);
+                         bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
       return check_launch("tt_gemm_bf16(persistent)");
     };
     const bool pp = gemm_pp_enabled();
-    if (split) {  // x3c FFN1 (GELU) -> the W2 GEMM's [hi | lo] planes
-      const int64_t mt = (M + 255) / 256, ntw = mt * ((N + 255) / 256), ntn = mt * ((N + 127) / 128);
-      const bool narrow = ntw <= 2 * ncu && ((ntn + ncu - 1) / ncu) * 54 < ((ntw + ncu - 1) / ncu) * 100;
-      if (variant == 3 || (variant == 1 && N >= 1024 && !gemm_wide_disabled() && !narrow)) {
-        if (pp && act == ACT_GELU) return launch(k_gemm_pp<ACT_GELU, 2>, ncu, 512);
-        if (pp && act == ACT_NONE) return launch(k_gemm_pp<ACT_NONE, 2>, ncu, 512);
-        if (act == ACT_GELU) return launch(k_gemm_wide<ACT_GELU, 2>, ncu, 512);
-        if (act == ACT_NONE) return launch(k_gemm_wide<ACT_NONE, 2>, ncu, 512);
-        return launch(k_gemm_wide<ACT_RELU, 2>, ncu, 512);
-      }
-      if (act == ACT_GELU) return launch(k_gemm_big<256, 3, ACT_GELU, 2>, ncu, 512);
-      if (act == ACT_NONE) return launch(k_gemm_big<256, 3, ACT_NONE, 2>, ncu, 512);
-      return launch(k_gemm_big<256, 3, ACT_RELU, 2>, ncu, 512);
-    }
-    // default: 256x256 tiles for the wide bf16-only GEMMs (QKV N = 1152, FFN1 N = 1536:
-    // 534 / 747 us vs 586 / 824 us with 256x128 at 370k tokens), 256x128 otherwise
-    // ... unless M is small enough that 256x256 tiles quantise badly onto the CUs (at most
-    // two rounds): rounds x tile cost with a 256x128 tile at 0.54 of a 256x256 one.
-    // configs[1]'s QKV (~18k rows, N = 1152): 360 wide tiles = 2 rounds vs 648 narrow = 3 x
-    // 0.54 (41.7 -> ~33 us); FFN1 (N = 1536) and the Mode A shapes (28+ rounds, where the
-    // wide tile measured faster: 546 vs 586 us QKV) stay wide.
+    // default: 256x256 tiles for the wide GEMMs (QKV N = 1152, FFN1 N = 1536: 534 / 747 us vs
+    // 586 / 824 us with 256x128 at 370k tokens, bf16), 256x128 otherwise ... unless M is small
+    // enough that 256x256 tiles quantise badly onto the CUs (at most two rounds): rounds x tile
+    // cost with a 256x128 tile at 0.54 of a 256x256 one.  configs[1]'s QKV (~18k rows,
+    // N = 1152): 360 wide tiles = 2 rounds vs 648 narrow = 3 x 0.54 (41.7 -> ~33 us); FFN1
+    // (N = 1536) and the Mode A shapes (28+ rounds, where the wide tile measured faster: 546
+    // vs 586 us QKV) stay wide.
     const int64_t mt = (M + 255) / 256, ntw = mt * ((N + 255) / 256), ntn = mt * ((N + 127) / 128);
     const bool narrow_pays =
         ntw <= 2 * ncu && ((ntn + ncu - 1) / ncu) * 54 < ((ntw + ncu - 1) / ncu) * 100;
-    if (pp && (variant == 3 || (variant == 1 && N >= 1024 && !gemm_wide_disabled() &&
-                                !narrow_pays))) {  // 256x256, phase-pipelined
+    const bool wide = variant == 3 || (variant == 1 && N >= 1024 && !gemm_wide_disabled() &&
+                                       !narrow_pays);
+    if (x3i) {  // the x3 encoder's QKV (no activation) / FFN1 (GELU), split output
+      if (wide) {
+        if (act == ACT_GELU) return launch(k_gemm_wide<ACT_GELU, 2, true>, ncu, 512);
+        if (act == ACT_NONE) return launch(k_gemm_wide<ACT_NONE, 2, true>, ncu, 512);
+        return launch(k_gemm_wide<ACT_RELU, 2, true>, ncu, 512);
+      }
+      if (act == ACT_GELU) return launch(k_gemm_big<256, 3, ACT_GELU, 2, uint16_t, true>, ncu, 512);
+      if (act == ACT_NONE) return launch(k_gemm_big<256, 3, ACT_NONE, 2, uint16_t, true>, ncu, 512);
+      return launch(k_gemm_big<256, 3, ACT_RELU, 2, uint16_t, true>, ncu, 512);
+    }
+    if (pp && wide) {  // 256x256, phase-pipelined (timing builds: TT_GEMM_PP=1)
       if (bfo && act == ACT_NONE) return launch(k_gemm_pp<ACT_NONE, 1>, ncu, 512);
       if (bfo && act == ACT_GELU) return launch(k_gemm_pp<ACT_GELU, 1>, ncu, 512);
       const bool fo = C && !C_bf16 && !residual && ldc % 4 == 0 && ((uintptr_t)C % 16) == 0;
       if (fo && act == ACT_NONE) return launch(k_gemm_pp<ACT_NONE, 3>, ncu, 512);
       // other output forms: the 256x128 ring below (the generic 256x256 epilogue spills)
-    } else
-    if (variant == 3 ||
-        (variant == 1 && bfo && N >= 1024 && !gemm_wide_disabled() && !narrow_pays)) {  // 256x256
+    } else if (variant == 3 || (wide && bfo)) {  // 256x256
       if (bfo && act == ACT_NONE) return launch(k_gemm_wide<ACT_NONE, true>, ncu, 512);
       if (bfo && act == ACT_GELU) return launch(k_gemm_wide<ACT_GELU, true>, ncu, 512);
       return launch(k_gemm_wide<-1, false>, ncu, 512);
@@ -2447,9 +2562,13 @@ static int gemm_bf16_impl(const uint16_t* A, int64_t lda, const uint16_t* W, int
     return launch(k_gemm_big<256, 3, -1, false>, ncu, 512);
   }
   const int nblk = ((M + GM_BM - 1) / GM_BM) * ((N + GM_BN - 1) / GM_BN);
-  hipLaunchKernelGGL((k_gemm<uint16_t, 0>), dim3(nblk), dim3(256), 0, (hipStream_t)stream, A, lda, W,
-                     ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act, kx,
-                     split ? N : 0);
+  if (x3i)
+    hipLaunchKernelGGL((k_gemm<uint16_t, 0, true>), dim3(nblk), dim3(256), 0, (hipStream_t)stream,
+                       A, lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act,
+                       N);
+  else
+    hipLaunchKernelGGL((k_gemm<uint16_t, 0>), dim3(nblk), dim3(256), 0, (hipStream_t)stream, A, lda,
+                       W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act, 0);
   return check_launch("tt_gemm_bf16");
 }
 
@@ -2458,23 +2577,21 @@ extern "C" int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, i
                             int64_t ldc, uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N,
                             int32_t K, int32_t act, void* stream) {
   return gemm_bf16_impl(A, lda, W, ldw, bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act,
-                        stream, 0, false);
+                        stream, false);
 }
 
-extern "C" int tt_gemm_x3c(const uint16_t* A2, int64_t lda2, const uint16_t* W3, int64_t ldw3,
-                           const float* bias, const float* residual, int64_t ldr, float* C,
-                           int64_t ldc, uint16_t* C_split, int64_t ldc_split, int32_t M,
-                           int32_t N, int32_t K, int32_t act, void* stream) {
-  TT_REQUIRE(K > 0 && K % 64 == 0, "tt_gemm_x3c: need K % 64 == 0");
-  TT_REQUIRE((C != nullptr) != (C_split != nullptr), "tt_gemm_x3c: exactly one of C, C_split");
-  return gemm_bf16_impl(A2, lda2, W3, ldw3, bias, residual, ldr, C, ldc, C_split, ldc_split, M, N,
-                        3 * K, act, stream, K, C_split != nullptr);
+extern "C" int tt_gemm_x3i(const uint16_t* A2, int64_t lda2, const uint16_t* W2, int64_t ldw2,
+                           const float* bias, uint16_t* C2, int64_t ldc2, int32_t M, int32_t N,
+                           int32_t K, int32_t act, void* stream) {
+  TT_REQUIRE(K > 0 && K % 32 == 0, "tt_gemm_x3i: need K % 32 == 0");
+  return gemm_bf16_impl(A2, lda2, W2, ldw2, bias, nullptr, 0, nullptr, 0, C2, ldc2, M, N, 2 * K,
+                        act, stream, true);
 }
 
 static int gemm_ln_impl(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
                         const float* bias, const float* gamma, const float* beta, float eps,
                         float* x, int64_t ldx, uint16_t* x_bf16, int64_t ldx16, int32_t M,
-                        int32_t H, int32_t K, void* stream, int32_t kx) {
+                        int32_t H, int32_t K, void* stream, bool x3i) {
   TT_REQUIRE(M >= 0 && K >= 0, "negative size");
   if (M == 0) return TT_OK;
   if (H != GL_H) return fail(TT_ERR_UNSUPPORTED, "tt_gemm_ln_bf16: H must be 384");
@@ -2486,9 +2603,6 @@ static int gemm_ln_impl(const uint16_t* A, int64_t lda, const uint16_t* W, int64
                  ((uintptr_t)x_bf16 % 8) == 0 && ((uintptr_t)bias % 16) == 0 &&
                  ((uintptr_t)gamma % 16) == 0 && ((uintptr_t)beta % 16) == 0,
              "x / bias / gamma / beta must be 16-B aligned (x_bf16 8-B), ldx, ldx16 % 4 == 0");
-  // row-tile height: rounds (ceil(tiles / CUs)) x (BM + ~32 rows of fixed cost per tile); 96
-  // only when strictly cheaper -- a configs[1] batch (~18k rows: 144 tiles of 128 = one
-  // 56%-full round, 192 of 96); at Mode A's 365k rows 128 and 96 tie and 128 stays
   const int ncu = enc_device_cus();
   // cost of a tile height: rounds (ceil(tiles / CUs)) x (BM + ~32 rows of fixed cost); the
   // smallest cost wins, ties to the taller tile
@@ -2504,18 +2618,16 @@ static int gemm_ln_impl(const uint16_t* A, int64_t lda, const uint16_t* W, int64
     }
   const int ntiles = (int)((M + bm - 1) / bm);
   const int grid = ntiles < ncu ? ntiles : ncu;
-  if (kx > 0) {
-    TT_REQUIRE(kx % 64 == 0 && K == 3 * kx && lda >= 2 * (int64_t)kx && ldx16 >= 2 * GL_H &&
-                   ldx16 % 8 == 0,
-               "x3c gemm_ln: K == 3 kx, A [hi | lo] (lda >= 2 kx), x planes (ldx16 >= 768)");
+  if (x3i) {
+    TT_REQUIRE(ldx16 >= 2 * GL_H && ldx16 % 8 == 0, "x3i gemm_ln: x rows x3i interleaved (ldx16 >= 768)");
     auto kern = bm == 80 ? k_gemm_ln<80, true> : bm == 96 ? k_gemm_ln<96, true> : k_gemm_ln<128, true>;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, (hipStream_t)stream, A, lda, W, ldw, bias,
-                       gamma, beta, eps, x, ldx, x_bf16, ldx16, M, K, kx);
-    return check_launch("tt_gemm_ln_x3c");
+                       gamma, beta, eps, x, ldx, x_bf16, ldx16, M, K);
+    return check_launch("tt_gemm_ln_x3i");
   }
   auto kern = bm == 80 ? k_gemm_ln<80> : bm == 96 ? k_gemm_ln<96> : k_gemm_ln<128>;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, (hipStream_t)stream, A, lda, W, ldw, bias,
-                     gamma, beta, eps, x, ldx, x_bf16, ldx16, M, K, 0);
+                     gamma, beta, eps, x, ldx, x_bf16, ldx16, M, K);
   return check_launch("tt_gemm_ln_bf16");
 }
 
@@ -2524,16 +2636,16 @@ extern "C" int tt_gemm_ln_bf16(const uint16_t* A, int64_t lda, const uint16_t* W
                                float eps, float* x, int64_t ldx, uint16_t* x_bf16, int64_t ldx16,
                                int32_t M, int32_t H, int32_t K, void* stream) {
   return gemm_ln_impl(A, lda, W, ldw, bias, gamma, beta, eps, x, ldx, x_bf16, ldx16, M, H, K,
-                      stream, 0);
+                      stream, false);
 }
 
-extern "C" int tt_gemm_ln_x3c(const uint16_t* A2, int64_t lda2, const uint16_t* W3, int64_t ldw3,
+extern "C" int tt_gemm_ln_x3i(const uint16_t* A2, int64_t lda2, const uint16_t* W2, int64_t ldw2,
                               const float* bias, const float* gamma, const float* beta, float eps,
-                              float* x, int64_t ldx, uint16_t* x_split, int64_t ldx_split,
-                              int32_t M, int32_t H, int32_t K, void* stream) {
-  TT_REQUIRE(K > 0 && K % 64 == 0, "tt_gemm_ln_x3c: need K % 64 == 0");
-  return gemm_ln_impl(A2, lda2, W3, ldw3, bias, gamma, beta, eps, x, ldx, x_split, ldx_split, M,
-                      H, 3 * K, stream, K);
+                              float* x, int64_t ldx, uint16_t* x2, int64_t ldx2, int32_t M,
+                              int32_t H, int32_t K, void* stream) {
+  TT_REQUIRE(K > 0 && K % 32 == 0, "tt_gemm_ln_x3i: need K % 32 == 0");
+  return gemm_ln_impl(A2, lda2, W2, ldw2, bias, gamma, beta, eps, x, ldx, x2, ldx2, M, H, 2 * K,
+                      stream, true);
 }
 
 extern "C" int tt_layernorm_f32(const float* x, int64_t ldx, const float* gamma,
@@ -2588,9 +2700,9 @@ static int attention_varlen_impl(const float* qkv, int64_t ld_qkv, const int32_t
   return check_launch("tt_attention_varlen");
 }
 
-// x3c attention over the QKV planes (k_attn32_x3): qkv2 [T, ld] bf16 rows [Q K V hi | Q K V lo]
-// (lo at column 3H), context planes out2 [T, ld_out >= 2H] (hi | lo at column H)
-extern "C" int tt_attention_varlen_x3c(const uint16_t* qkv2, int64_t ld_qkv2,
+// x3 attention over x3i interleaved QKV rows (k_attn32_x3): qkv2 [T, ld >= 6H] bf16, context
+// out2 [T, ld_out >= 2H] x3i interleaved
+extern "C" int tt_attention_varlen_x3i(const uint16_t* qkv2, int64_t ld_qkv2,
                                        const int32_t* cu_seqlens, int32_t n_seq, int32_t max_len,
                                        int32_t H, int32_t heads, uint16_t* out2, int64_t ld_out2,
                                        void* stream) {
@@ -2599,11 +2711,11 @@ extern "C" int tt_attention_varlen_x3c(const uint16_t* qkv2, int64_t ld_qkv2,
   TT_REQUIRE(max_len >= 1 && max_len <= 512, "max_len must be in [1, 512]");
   TT_REQUIRE(qkv2 && cu_seqlens && out2, "null pointer");
   if (H / heads != 32)
-    return fail(TT_ERR_UNSUPPORTED, "tt_attention_varlen_x3c: head dim must be 32");
+    return fail(TT_ERR_UNSUPPORTED, "tt_attention_varlen_x3i: head dim must be 32");
   TT_REQUIRE(ld_qkv2 >= 6 * (int64_t)H && ld_qkv2 % 8 == 0 && H % 8 == 0 &&
                  ld_out2 >= 2 * (int64_t)H && ld_out2 % 4 == 0 && ((uintptr_t)qkv2 % 16) == 0 &&
                  ((uintptr_t)out2 % 8) == 0,
-             "qkv planes [T, >= 6H] 16-B aligned rows; context planes [T, >= 2H]");
+             "qkv x3i rows [T, >= 6H] 16-B aligned; context x3i rows [T, >= 2H]");
   const size_t smem = attn32_x3_smem(max_len);
   const bool h2 = heads % 2 == 0 && 2 * smem <= 160 * 1024;
   const void* fb = h2 ? (const void*)k_attn32_x3<2> : (const void*)k_attn32_x3<1>;
@@ -2615,13 +2727,13 @@ extern "C" int tt_attention_varlen_x3c(const uint16_t* qkv2, int64_t ld_qkv2,
   const float scale = 1.0f / sqrtf(32.0f);
   if (h2)
     hipLaunchKernelGGL(k_attn32_x3<2>, dim3((unsigned)(n_seq * heads / 2)), dim3(512), sm,
-                       (hipStream_t)stream, qkv2, ld_qkv2, 3 * H, cu_seqlens, H, heads, scale,
-                       out2, ld_out2);
+                       (hipStream_t)stream, qkv2, ld_qkv2, cu_seqlens, H, heads, scale, out2,
+                       ld_out2);
   else
     hipLaunchKernelGGL(k_attn32_x3<1>, dim3((unsigned)(n_seq * heads)), dim3(256), sm,
-                       (hipStream_t)stream, qkv2, ld_qkv2, 3 * H, cu_seqlens, H, heads, scale,
-                       out2, ld_out2);
-  return check_launch("tt_attention_varlen_x3c");
+                       (hipStream_t)stream, qkv2, ld_qkv2, cu_seqlens, H, heads, scale, out2,
+                       ld_out2);
+  return check_launch("tt_attention_varlen_x3i");
 }
 
 extern "C" int tt_attention_varlen(const float* qkv, int64_t ld_qkv, const int32_t* cu_seqlens,
@@ -2772,19 +2884,20 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
   };
   // bf16 path at H = 384 with row tiles filling the chip: GEMM + LayerNorm fused (k_gemm_ln)
   const bool fuse_ln = bf && H == GL_H && I % 64 == 0 && !gemm_ln_disabled();
-  // x3 at H = 384 with K-concatenated weights (wqkv_x3c ...): the x3c form -- every GEMM one
-  // bf16 GEMM over K' = 3K on the persistent kernels, Wo / W2 fused with their LayerNorm, the
-  // activations the GEMMs read written as [hi | lo] bf16 planes by their producers
-  bool x3c = x3 && H == GL_H && I % 64 == 0 && H / m->heads == 32 && !gemm_ln_disabled() &&
-             x3c_enabled();
-  for (int l = 0; x3c && l < NL; ++l)
-    x3c = m->layer[l].wqkv_x3c && m->layer[l].wo_x3c && m->layer[l].w1_x3c && m->layer[l].w2_x3c;
+  // x3 at H = 384 with x3i weights (wqkv_x3i ...): every GEMM runs on the bf16 kernels with
+  // x3i interleaved operands (three MFMAs per 32 k, no split VALU), Wo / W2 fused with their
+  // LayerNorm; the producers (embedding LayerNorm, GEMM epilogues, attention) write their
+  // outputs x3i interleaved
+  bool x3fast = x3 && H == GL_H && I % 64 == 0 && H / m->heads == 32 && !gemm_ln_disabled() &&
+                x3c_enabled();
+  for (int l = 0; x3fast && l < NL; ++l)
+    x3fast = m->layer[l].wqkv_x3i && m->layer[l].wo_x3i && m->layer[l].w1_x3i && m->layer[l].w2_x3i;
   EncWs w = enc_carve((char*)workspace, T, H, I, bf);
   if (!workspace || workspace_bytes < (int64_t)w.total)
     return fail(TT_ERR_WORKSPACE, "tt_bert_encode: workspace too small");
   hipStream_t st = (hipStream_t)stream;
-  if (x3c) {
-    // planes alias the f32 path's buffers (same bytes: [T, 2H] bf16 == [T, H] f32)
+  if (x3fast) {
+    // x3i rows alias the f32 path's buffers (same bytes: [T, 2H] bf16 == [T, H] f32)
     uint16_t* xs = (uint16_t*)w.y;
     uint16_t* cs = (uint16_t*)w.ctx;
     uint16_t* fs = (uint16_t*)w.ff;
@@ -2796,21 +2909,21 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
     if (rc) return rc;
     for (int l = 0; l < NL; ++l) {
       const tt_bert_layer& L = m->layer[l];
-      uint16_t* qs = (uint16_t*)w.qkv;  // [T, 6H] planes in the f32 path's [T, 3H] buffer
-      rc = gemm_bf16_impl(xs, 2 * H, L.wqkv_x3c, 3 * H, L.bqkv, nullptr, 0, nullptr, 0, qs, 6 * H,
-                          (int)T, 3 * H, 3 * H, ACT_NONE, stream, H, true);
+      uint16_t* qs = (uint16_t*)w.qkv;  // [T, 6H] x3i rows in the f32 path's [T, 3H] buffer
+      rc = gemm_bf16_impl(xs, 2 * H, L.wqkv_x3i, 2 * H, L.bqkv, nullptr, 0, nullptr, 0, qs, 6 * H,
+                          (int)T, 3 * H, 2 * H, ACT_NONE, stream, true);
       if (rc) return rc;
-      rc = tt_attention_varlen_x3c(qs, 6 * H, cu_seqlens, n_seq, max_len, H, m->heads, cs, 2 * H,
+      rc = tt_attention_varlen_x3i(qs, 6 * H, cu_seqlens, n_seq, max_len, H, m->heads, cs, 2 * H,
                                    stream);
       if (rc) return rc;
-      rc = gemm_ln_impl(cs, 2 * H, L.wo_x3c, 3 * H, L.bo, L.ln1_g, L.ln1_b, m->ln_eps, w.x, H, xs,
-                        2 * H, (int)T, H, 3 * H, stream, H);
+      rc = gemm_ln_impl(cs, 2 * H, L.wo_x3i, 2 * H, L.bo, L.ln1_g, L.ln1_b, m->ln_eps, w.x, H, xs,
+                        2 * H, (int)T, H, 2 * H, stream, true);
       if (rc) return rc;
-      rc = gemm_bf16_impl(xs, 2 * H, L.w1_x3c, 3 * H, L.b1, nullptr, 0, nullptr, 0, fs, 2 * I,
-                          (int)T, I, 3 * H, ACT_GELU, stream, H, true);
+      rc = gemm_bf16_impl(xs, 2 * H, L.w1_x3i, 2 * H, L.b1, nullptr, 0, nullptr, 0, fs, 2 * I,
+                          (int)T, I, 2 * H, ACT_GELU, stream, true);
       if (rc) return rc;
-      rc = gemm_ln_impl(fs, 2 * I, L.w2_x3c, 3 * I, L.b2, L.ln2_g, L.ln2_b, m->ln_eps, w.x, H, xs,
-                        2 * H, (int)T, H, 3 * I, stream, I);
+      rc = gemm_ln_impl(fs, 2 * I, L.w2_x3i, 2 * I, L.b2, L.ln2_g, L.ln2_b, m->ln_eps, w.x, H, xs,
+                        2 * H, (int)T, H, 2 * I, stream, true);
       if (rc) return rc;
     }
     hipLaunchKernelGGL(k_mean_pool, dim3((unsigned)n_seq), dim3(256), 0, st, w.x, (int64_t)H,

@@ -43,7 +43,7 @@ class BertLayer(ctypes.Structure):
     _fields_ = [(n, _vp) for n in (
         "wqkv", "bqkv", "wo", "bo", "ln1_g", "ln1_b", "w1", "b1", "w2", "b2", "ln2_g", "ln2_b",
         "wqkv_bf16", "wo_bf16", "w1_bf16", "w2_bf16", "wqkv_x3", "wo_x3", "w1_x3", "w2_x3",
-        "wqkv_x3c", "wo_x3c", "w1_x3c", "w2_x3c")]
+        "wqkv_x3i", "wo_x3i", "w1_x3i", "w2_x3i")]
 
 
 class BertModel(ctypes.Structure):
@@ -106,12 +106,12 @@ SIGNATURES = {
                                    _i32, _i32, _i32, _i32, _vp]),
     "tt_x3_split_weights": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp]),
     "tt_debug_plant_bad_row": (ctypes.c_int, [_i32, _i32]),
-    "tt_attention_varlen_x3c": (ctypes.c_int, [_vp, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _i64,
+    "tt_attention_varlen_x3i": (ctypes.c_int, [_vp, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _i64,
                                                _vp]),
-    "tt_x3c_weights": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp]),
-    "tt_gemm_x3c": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64,
-                                   _i32, _i32, _i32, _i32, _vp]),
-    "tt_gemm_ln_x3c": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, ctypes.c_float, _vp,
+    "tt_x3i_weights": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp]),
+    "tt_gemm_x3i": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _i32, _i32, _i32, _i32,
+                                   _vp]),
+    "tt_gemm_ln_x3i": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, ctypes.c_float, _vp,
                                        _i64, _vp, _i64, _i32, _i32, _i32, _vp]),
     "tt_gemm_bf16": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _i64, _vp, _i64,
                                     _i32, _i32, _i32, _i32, _vp]),

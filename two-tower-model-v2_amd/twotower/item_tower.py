@@ -93,13 +93,13 @@ def x3_split_weights(w: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def x3c_weights(w: torch.Tensor) -> torch.Tensor:
-    """[N, K] f32 (device) -> the x3c GEMM's K-concatenated image [N, 3K] bf16 =
-    [bf16(W) | bf16(W - bf16(W)) | bf16(W)] (tt_x3c_weights)."""
+def x3i_weights(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] f32 (device) -> the x3 encoder's x3i image [N, 2K] bf16: per 32 k, 32 hi =
+    bf16(W) then 32 lo = bf16(W - hi) (tt_x3i_weights)."""
     N, K = w.shape
-    out = torch.empty((N, 3 * K), dtype=torch.bfloat16, device=w.device)
-    check(lib().tt_x3c_weights(w.data_ptr(), w.stride(0), N, K, out.data_ptr(), out.stride(0),
-                               stream_ptr()), "tt_x3c_weights")
+    out = torch.empty((N, 2 * K), dtype=torch.bfloat16, device=w.device)
+    check(lib().tt_x3i_weights(w.data_ptr(), w.stride(0), N, K, out.data_ptr(), out.stride(0),
+                               stream_ptr()), "tt_x3i_weights")
     return out
 
 
@@ -158,10 +158,11 @@ class BertEncoder:
             L.ln2_g = ptr(t(p + "output.LayerNorm.weight"))
             L.ln2_b = ptr(t(p + "output.LayerNorm.bias"))
             if prec == "x3":  # the weights' hi / lo split once (tt_x3_split_weights), and
-                # their K-concatenated form for the x3c GEMMs (H = 384: tt_bert_encode's x3c path)
+                # their x3i interleaved form for the bf16 GEMM kernels (H = 384: tt_bert_encode's
+                # x3i path)
                 L.wqkv_x3, L.wo_x3, L.w1_x3, L.w2_x3 = (ptr(x3_split_weights(x))
                                                         for x in (wqkv, wo, w1, w2))
-                L.wqkv_x3c, L.wo_x3c, L.w1_x3c, L.w2_x3c = (ptr(x3c_weights(x))
+                L.wqkv_x3i, L.wo_x3i, L.w1_x3i, L.w2_x3i = (ptr(x3i_weights(x))
                                                             for x in (wqkv, wo, w1, w2))
             if prec == "bf16":
                 L.wqkv_bf16 = ptr(wqkv.to(torch.bfloat16))
