@@ -141,8 +141,8 @@ __device__ __forceinline__ int enc_xcd_remap(int bid, int nblk) {
 // bf16 kernels' two k-halves become the hi and lo operands of the same 32 k.
 __device__ __forceinline__ int x3i_col(int n) { return 64 * (n >> 5) + (n & 31); }
 
-// OM: output form.  0 = generic (C and / or C16, residual), 1 = BFO, 3 = f32 C only (no
-// residual, no C16), 2 = SPLIT: the x3 encoder's split-bf16 interleaved rows (C == NULL,
+// OM: output form.  0 = generic (C and / or C16, residual), 1 = BFO, 2 = SPLIT: the x3
+// encoder's split-bf16 interleaved rows (C == NULL,
 // res == NULL): C16 row m holds, per 32 columns, hi = bf16(y) then lo = bf16(y - hi)
 // (x3i_col; ldc16 >= 2N, N % 32 == 0, 16-B aligned rows), i.e. the A operand of the next x3
 // GEMM.  split_n > 0 selects the same form at run time in the generic epilogue (k_gemm's
@@ -156,15 +156,11 @@ __device__ __forceinline__ int gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, i
                                                    uint16_t* __restrict__ C16, int64_t ldc16,
                                                    int act, const float* lbias = nullptr,
                                                    int split_n = 0) {
-  constexpr bool BFO = OM == 1, SPL = OM == 2, FO = OM == 3;
+  constexpr bool BFO = OM == 1, SPL = OM == 2;
   const int g = lane >> 4, rl = lane & 15;
   if constexpr (ACTC >= 0) act = ACTC;
   if constexpr (BFO || SPL) {
     C = nullptr;
-    res = nullptr;
-  }
-  if constexpr (FO) {
-    C16 = nullptr;
     res = nullptr;
   }
   if constexpr (SPL) split_n = N;
@@ -189,24 +185,6 @@ __device__ __forceinline__ int gemm_wave_epilogue(f32x4 (&acc)[4][4], int mw0, i
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           rv[i][j] = *(const f32x4*)(res + (int64_t)(mw0 + 16 * i + rl) * ldr + nw0 + 16 * j + 4 * g);
-    }
-    if constexpr (FO) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t m = mw0 + 16 * i + rl;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          f32x4 y = acc[i][j] + bv[j];
-          if (act == ACT_GELU) {
-            gelu4_fast(y);
-          } else if (act == ACT_RELU) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) y[u] = y[u] > 0.0f ? y[u] : 0.0f;
-          }
-          *(f32x4*)(C + m * ldc + nw0 + 16 * j + 4 * g) = y;
-        }
-      }
-      return 16;
     }
     if constexpr (SPL) {
       // split planes: the BFO path's permlane16_swap pairing, once for hi and once for lo
@@ -1014,230 +992,6 @@ __global__ __launch_bounds__(512, 1) void k_gemm_wide(const uint16_t* __restrict
     }
     gs += nk;
   }
-}
-
-// Phase-pipelined persistent GEMM (k_gemm_pp): the 256 x 256 tile of k_gemm_wide with its
-// global -> LDS DMA decoupled from the k-stages (the guide's 256^2 phase template, adapted):
-//   * 8 waves as 4 (M) x 2 (N) of 64 x 128; a K-tile (BK = 64) is four PHASES of 16 MFMAs per
-//     wave: phase p multiplies the wave's 4 M-blocks by N-blocks 2p, 2p + 1 over both k-halves.
-//     A fragments (8 ds_read_b128) are read once per K-tile in phase 0 and stay in registers;
-//     B fragments (4 reads) are read per phase.  One raw s_barrier per phase.
-//   * LDS: two buffer sets (K-tile parity) of [A rows 0-127 | A rows 128-255 | B rows 0-127 |
-//     B rows 128-255] x 128 B rows (XOR-swizzled chunks, as k_gemm) = 128 KB, plus the bias;
-//     ONE __shared__ array (a second one can make hipcc drain vmcnt before LDS reads).
-//   * Because A is consumed in phase 0, its halves are free two phases later: the A of K-tile
-//     g + 2 is issued in phases 2 / 3 of K-tile g (4-5 phases of flight for the HBM-streamed
-//     operand); B (the L2-resident weights) is refilled in quarters as each 32-row slice is
-//     read: quarter q of K-tile g + 2 in phase q + 2 of g (q < 2) or q - 2 of g + 1.  The only
-//     wait is one counted vmcnt(3) per K-tile (phase 3 of g + 1 retires K-tile g + 2's data;
-//     phase 2's three younger DMAs stay in flight across the barrier).  Every buffer is
-//     restaged >= 2 phases after its last read, so one barrier per phase orders both RAW and
-//     WAR.  The DMA sequence runs across output tiles (persistent blocks), so the epilogue of a
-//     tile overlaps the next tile's first loads.
-// OM / ACT: as k_gemm_wide.
-#ifndef TT_GPP_PRIO
-#define TT_GPP_PRIO 1  // s_setprio(1) around each phase's MFMAs
-#endif
-#ifndef TT_GPP_BAR
-// barriers per K-tile: 4 (every phase) or 2 (phases 1 and 3: enough for the DMA schedule --
-// every restage is issued after a barrier that follows the lgkmcnt retiring the buffer's
-// last reads, and phase 3's barrier follows the vmcnt retiring the next K-tile)
-#define TT_GPP_BAR 4
-#endif
-template <int ACT, int OM>
-__global__ __launch_bounds__(512, 1) void k_gemm_pp(const uint16_t* __restrict__ A, int64_t lda,
-                                                    const uint16_t* __restrict__ W, int64_t ldw,
-                                                    const float* __restrict__ bias,
-                                                    const float* __restrict__ res, int64_t ldr,
-                                                    float* __restrict__ C, int64_t ldc,
-                                                    uint16_t* __restrict__ C16, int64_t ldc16,
-                                                    int M, int N, int K, int act) {
-  constexpr int BM = 256, BN = 256, BK = 64, EPC = 8;
-  constexpr int HB = 128 * 128;              // half-tile buffer: 128 rows x 128 B
-  constexpr int SET_B = 4 * HB;              // one K-tile: A0 A1 B0 B1
-  constexpr int BIAS_OFF = 2 * SET_B;        // float bias[GB_MAXN] after the two sets
-  __shared__ __attribute__((aligned(16))) char smem[2 * SET_B + GB_MAXN * 4];
-  float* sbias = (float*)(smem + BIAS_OFF);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const bool lds_bias = bias && N <= GB_MAXN && ((uintptr_t)bias % 16) == 0;
-  if (lds_bias)
-    for (int e = tid; e < N; e += 512) sbias[e] = bias[e];
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 1, wn = w & 1;
-  const int n_tn = (N + BN - 1) / BN;
-  const int ntiles = ((M + BM - 1) / BM) * n_tn;
-  const int nk = K / BK;
-  const int n_mine = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-  if (n_mine <= 0) return;
-  const int total = n_mine * nk;  // K-tiles of this block, one sequence over its output tiles
-  auto tile_of = [&](int r) { return enc_xcd_remap(blockIdx.x + r * gridDim.x, ntiles); };
-
-  // ---- DMA: per-lane pieces.  A half h: rows 128 h + 64 j + 8 w + (lane >> 3), j = 0, 1 (two
-  // glds per lane); B quarter q: rows 128 (w >> 2) + 32 q + 8 (w & 3) + (lane >> 3) (one glds).
-  // Chunk swizzle (row >> 1) & 7 of the row within its 128-row buffer, as the reads below.
-  const int arow = 8 * w + (lane >> 3);                    // + 64 j within the half
-  const int achunk = ((lane & 7) ^ ((arow >> 1) & 7)) * EPC;
-  const int brow = 8 * (w & 3) + (lane >> 3);              // + 32 q within the half
-  const int bchunk = ((lane & 7) ^ ((brow >> 1) & 7)) * EPC;
-  const uint32_t sm0 = lds_addr(smem);
-  auto issue_a = [&](int h, int gi) __attribute__((always_inline)) {
-    const int r = gi / nk, kt = gi - r * nk;
-    const int lt = tile_of(r);
-    const int m0 = (lt / n_tn) * BM + 128 * h;
-    const int64_t ka = (int64_t)kt * BK;
-    char* dst = smem + (gi & 1) * SET_B + h * HB;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      int am = m0 + 64 * j + arow;
-      am = am < M ? am : M - 1;
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(A + (int64_t)am * lda + achunk + ka),
-          (__attribute__((address_space(3))) void*)(dst + (64 * j + 8 * w) * 128), 16, 0, 0);
-    }
-  };
-  auto issue_b = [&](int q, int gi) __attribute__((always_inline)) {
-    const int r = gi / nk, kt = gi - r * nk;
-    const int lt = tile_of(r);
-    int wr = (lt % n_tn) * BN + 128 * (w >> 2) + 32 * q + brow;
-    wr = wr < N ? wr : N - 1;  // rows past N: clamped loads, no stores
-    char* dst = smem + (gi & 1) * SET_B + 2 * HB + (w >> 2) * HB + (32 * q + 8 * (w & 3)) * 128;
-    __builtin_amdgcn_global_load_lds(
-        (const __attribute__((address_space(1))) void*)(W + (int64_t)wr * ldw + bchunk +
-                                                         (int64_t)kt * BK),
-        (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-  };
-
-  // ---- fragment reads: A rows 64 wm + 16 i + rl of the tile = half wm >> 1, row
-  // 64 (wm & 1) + 16 i + rl; B rows 128 wn + 16 j + rl = half wn, row 16 j + rl.  The swizzle
-  // (row >> 1) & 7 = (rl >> 1) & 7 for every i, j: blocks are ds_read immediates (2048 B).
-  const int g = lane >> 4, rl = lane & 15;
-  uint32_t fa[2], fb[2];
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int c = (4 * s + g) ^ ((rl >> 1) & 7);
-    fa[s] = (uint32_t)((wm >> 1) * HB + (64 * (wm & 1) + rl) * 128 + 16 * c);
-    fb[s] = (uint32_t)(2 * HB + wn * HB + rl * 128 + 16 * c);
-  }
-
-  // ---- prologue: K-tile 0 whole, K-tile 1 except its last two B quarters (issued in phases
-  // 0 / 1 of K-tile 0, as in the steady state)
-  issue_a(0, 0);
-  issue_a(1, 0);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) issue_b(q, 0);
-  if (total > 1) {
-    issue_a(0, 1);
-    issue_b(0, 1);
-    issue_a(1, 1);
-    issue_b(1, 1);
-    enc_wait_vm<6>();
-  } else {
-    enc_wait_vm<0>();
-  }
-  __builtin_amdgcn_s_barrier();
-
-  f32x4 acc[2][4][4];  // [column half][M-block i][N-block j within the half]
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // fragment registers: B read ONE phase ahead (its LDS latency runs under the previous
-  // phase's MFMAs; two register sets by phase parity), A read once per K-tile at phase 0 (a
-  // second A set does not fit beside the 128 accumulator VGPRs)
-  u32x4 av[2][4], bv[2][2][2];  // av[k-half][M-block], bv[phase parity][k-half][N-block]
-#define TT_GPP_READ_B(PAR, SB, P)                                                           \
-  do {                                                                                      \
-    const uint32_t pb0_ = (SB) + fb[0] + 4096 * (P), pb1_ = (SB) + fb[1] + 4096 * (P);      \
-    bv[PAR][0][0] = lds_read128<0>(pb0_);                                                   \
-    bv[PAR][0][1] = lds_read128<2048>(pb0_);                                                \
-    bv[PAR][1][0] = lds_read128<0>(pb1_);                                                   \
-    bv[PAR][1][1] = lds_read128<2048>(pb1_);                                                \
-  } while (0)
-  TT_GPP_READ_B(0, sm0, 0);  // K-tile 0, phase 0
-
-  for (int gi = 0; gi < total; ++gi) {
-    const uint32_t sb = sm0 + (uint32_t)((gi & 1) * SET_B);
-    const uint32_t sb_next = sm0 + (uint32_t)(((gi + 1) & 1) * SET_B);
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      // phase p: [phase 3: the wait retiring K-tile gi + 1] barrier, [phase 0: this K-tile's
-      // A fragments], the NEXT phase's B fragments, this phase's DMA, the wait for this
-      // phase's fragments, 16 MFMAs
-      if (p == 3) {
-        if (gi + 2 < total) enc_wait_vm<3>();
-        else enc_wait_vm<0>();
-      }
-      if (TT_GPP_BAR == 4 || p == 1 || p == 3) __builtin_amdgcn_s_barrier();
-      if (p == 0) {
-        const uint32_t pa0 = sb + fa[0], pa1 = sb + fa[1];
-        av[0][0] = lds_read128<0>(pa0);
-        av[0][1] = lds_read128<2048>(pa0);
-        av[0][2] = lds_read128<4096>(pa0);
-        av[0][3] = lds_read128<6144>(pa0);
-        av[1][0] = lds_read128<0>(pa1);
-        av[1][1] = lds_read128<2048>(pa1);
-        av[1][2] = lds_read128<4096>(pa1);
-        av[1][3] = lds_read128<6144>(pa1);
-      }
-      const bool more = p < 3 || gi + 1 < total;
-      if (p < 3) TT_GPP_READ_B((p + 1) & 1, sb, p + 1);
-      else if (more) TT_GPP_READ_B(0, sb_next, 0);
-      if (p == 0 && gi + 1 < total) issue_b(2, gi + 1);
-      if (p == 1 && gi + 1 < total) issue_b(3, gi + 1);
-      if (p == 2 && gi + 2 < total) {
-        issue_a(0, gi + 2);
-        issue_b(0, gi + 2);
-      }
-      if (p == 3 && gi + 2 < total) {
-        issue_a(1, gi + 2);
-        issue_b(1, gi + 2);
-      }
-      // LDS ops younger than this phase's fragments: the 4 B reads just issued for the next
-      if (more) lds_wait<4>();
-      else lds_wait<0>();
-      if (p == 0) {
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) reg_tie(av[s2][i]);
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) reg_tie(bv[p & 1][s2][j]);
-      if (TT_GPP_PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            f32x4& a = acc[p >> 1][i][2 * (p & 1) + j];
-            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                __builtin_bit_cast(bf16x8e, bv[p & 1][s2][j]),
-                __builtin_bit_cast(bf16x8e, av[s2][i]), a, 0, 0, 0);
-          }
-      if (TT_GPP_PRIO) __builtin_amdgcn_s_setprio(0);
-    }
-    const int r = gi / nk;
-    if (gi - r * nk == nk - 1) {  // last K-tile of output tile r: epilogue, then a fresh tile
-      const int lt = tile_of(r);
-      const int m0 = (lt / n_tn) * BM + 64 * wm, n0 = (lt % n_tn) * BN + 128 * wn;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        gemm_wave_epilogue<true, ACT, OM>(acc[h], m0, n0 + 64 * h, lane, M, N, bias, res, ldr, C,
-                                          ldc, C16, ldc16, act, lds_bias ? sbias : nullptr);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-  }
-#undef TT_GPP_READ_B
 }
 
 // Fused GEMM + LayerNorm for the two H-wide GEMMs of a BERT layer (bf16 path):
@@ -2367,10 +2121,6 @@ bool gemm_wide_disabled() {  // TT_GEMM_WIDE=0: keep 256x128 tiles for the wide 
   static const bool off = env_switch("TT_GEMM_WIDE", 1) == 0;
   return off;
 }
-bool gemm_pp_enabled() {  // TT_GEMM_PP=1: k_gemm_pp for the 256x256 tiles (timing builds: A/B)
-  static const bool on = env_switch("TT_GEMM_PP", 0) != 0;
-  return on;
-}
 bool x3c_enabled() {  // TT_X3C=0: the x3 path's split-in-loop GEMMs (timing builds: A/B)
   static const bool on = env_switch("TT_X3C", 1) != 0;
   return on;
@@ -2518,7 +2268,6 @@ static int gemm_bf16_impl(const uint16_t* A, int64_t lda, const uint16_t* W, int
                          bias, residual, ldr, C, ldc, C_bf16, ldc16, M, N, K, act);
       return check_launch("tt_gemm_bf16(persistent)");
     };
-    const bool pp = gemm_pp_enabled();
     // default: 256x256 tiles for the wide GEMMs (QKV N = 1152, FFN1 N = 1536: 534 / 747 us vs
     // 586 / 824 us with 256x128 at 370k tokens, bf16), 256x128 otherwise ... unless M is small
     // enough that 256x256 tiles quantise badly onto the CUs (at most two rounds): rounds x tile
@@ -2541,13 +2290,7 @@ static int gemm_bf16_impl(const uint16_t* A, int64_t lda, const uint16_t* W, int
       if (act == ACT_NONE) return launch(k_gemm_big<256, 3, ACT_NONE, 2, uint16_t, true>, ncu, 512);
       return launch(k_gemm_big<256, 3, ACT_RELU, 2, uint16_t, true>, ncu, 512);
     }
-    if (pp && wide) {  // 256x256, phase-pipelined (timing builds: TT_GEMM_PP=1)
-      if (bfo && act == ACT_NONE) return launch(k_gemm_pp<ACT_NONE, 1>, ncu, 512);
-      if (bfo && act == ACT_GELU) return launch(k_gemm_pp<ACT_GELU, 1>, ncu, 512);
-      const bool fo = C && !C_bf16 && !residual && ldc % 4 == 0 && ((uintptr_t)C % 16) == 0;
-      if (fo && act == ACT_NONE) return launch(k_gemm_pp<ACT_NONE, 3>, ncu, 512);
-      // other output forms: the 256x128 ring below (the generic 256x256 epilogue spills)
-    } else if (variant == 3 || (wide && bfo)) {  // 256x256
+    if (variant == 3 || (wide && bfo)) {  // 256x256
       if (bfo && act == ACT_NONE) return launch(k_gemm_wide<ACT_NONE, true>, ncu, 512);
       if (bfo && act == ACT_GELU) return launch(k_gemm_wide<ACT_GELU, true>, ncu, 512);
       return launch(k_gemm_wide<-1, false>, ncu, 512);
