@@ -226,3 +226,15 @@ def test_trainer_epochs_reference_batches(tmp_path, aggregation):
     ck4 = torch.load(tmp_path / "checkpoint_epoch_4.pt", weights_only=True)
     assert ck4["epoch"] == 3
     assert {int(float(e["step"])) for e in ck4["optimizer_state_dict"]["state"].values()} == {7 * 4}
+    # a state dict indexed over a different parameter list (the reference's Adam state puts
+    # the frozen SentenceTransformer parameters first) is refused, not silently ignored
+    shifted = {"state": {int(i) + 200: e for i, e in osd["state"].items()},
+               "param_groups": osd["param_groups"]}
+    with pytest.raises(ValueError, match="different parameter"):
+        tr2.step.load_optimizer_state_dict(model2, shifted)
+    first = sorted(osd["state"])[0]
+    wrong = {"state": {first: dict(osd["state"][first], exp_avg=torch.zeros(3),
+                                   exp_avg_sq=torch.zeros(3))},
+             "param_groups": osd["param_groups"]}
+    with pytest.raises(ValueError, match="different parameter"):
+        tr2.step.load_optimizer_state_dict(model2, wrong)

@@ -280,17 +280,36 @@ class TwoTowerTrainStep:
 
     def load_optimizer_state_dict(self, model, sd: Dict) -> None:
         """Restore Adam's step count and moments from optimizer_state_dict's format (or a
-        torch.optim.Adam state dict over model.parameters())."""
+        torch.optim.Adam state dict over THIS model's model.parameters()).
+
+        Compatibility is with this module's own parameter order: the reference's Adam state
+        indexes the SentenceTransformer's ~200 frozen parameters first (item_tower.py:38,
+        trainer.py:49-50), so its indices do not line up here.  A state dict whose entries do
+        not match the trained parameters' shapes, or none of whose entries lands on a trained
+        parameter, raises instead of silently leaving Adam at step 0."""
         pos = {p.data_ptr(): i for i, p in enumerate(model.parameters())}
         st = sd["state"]
         steps = set()
+        matched = 0
         for k, p in self.params.items():
-            e = st.get(pos[p.data_ptr()])
+            i = pos[p.data_ptr()]
+            e = st.get(i)
             if e is None:
                 continue
-            self.m[k].copy_(torch.as_tensor(e["exp_avg"]).view_as(self.m[k]))
-            self.v[k].copy_(torch.as_tensor(e["exp_avg_sq"]).view_as(self.v[k]))
+            ea, es = torch.as_tensor(e["exp_avg"]), torch.as_tensor(e["exp_avg_sq"])
+            if ea.numel() != self.m[k].numel() or es.numel() != self.v[k].numel():
+                raise ValueError(
+                    f"optimizer state entry {i} holds {tuple(ea.shape)} moments, parameter {k} "
+                    f"needs {tuple(self.m[k].shape)}: the state dict indexes a different parameter "
+                    "list (e.g. a reference checkpoint, whose frozen text-encoder parameters come "
+                    "first)")
+            self.m[k].copy_(ea.view_as(self.m[k]))
+            self.v[k].copy_(es.view_as(self.v[k]))
             steps.add(int(float(e["step"])))
+            matched += 1
+        if st and matched == 0:
+            raise ValueError("no optimizer state entry matches a trained parameter: the state dict "
+                             "indexes a different parameter list")
         if len(steps) > 1:
             raise ValueError(f"inconsistent Adam step counts in the state dict: {sorted(steps)}")
         self.t = steps.pop() if steps else 0
