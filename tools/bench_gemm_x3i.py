@@ -1,8 +1,9 @@
-"""GEMM microbenchmark at the encoder's shapes, bf16 and x3c, for A/B between GEMM variants
-(TT_GEMM_PP=0/1 in the environment; run the variants alternately, several times).
+"""GEMM microbenchmark at the encoder's QKV / FFN1 shapes, bf16 and x3i (split-bf16 operands
+interleaved per 32 k), for A/B between GEMM variants built with tools/exp_build2.sh (run the
+variants alternately, several times).
 
-    python tools/bench_gemm_pp.py [--M 370761,18340] [--iters 20]
-Prints one JSON line: per shape ms and TFLOP/s (x3c counted as 3 products).
+    python tools/bench_gemm_x3i.py [--M 370761,18340] [--iters 20]
+Prints one JSON line: per shape us and TFLOP/s (x3i counted as 3 products).
 """
 import argparse
 import json
@@ -15,7 +16,7 @@ sys.path.insert(0, os.path.join(ROOT, "two-tower-model-v2_amd"))
 import torch  # noqa: E402
 
 from twotower import _lib  # noqa: E402
-from twotower.item_tower import x3c_weights  # noqa: E402
+from twotower.item_tower import x3i_weights  # noqa: E402
 
 
 def main():
@@ -24,10 +25,10 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     a = ap.parse_args()
     L = _lib.lib()
-    out = {"pp": os.environ.get("TT_GEMM_PP", "1")}
+    out = {"lib": os.environ.get("TWOTOWER_HIP_LIB", "in-tree")}
     for M in (int(v) for v in a.M.split(",")):
         for (kind, N, K, act) in (("bf16", 1152, 384, 0), ("bf16", 1536, 384, 1),
-                                  ("x3c", 1152, 384, 0), ("x3c", 1536, 384, 1)):
+                                  ("x3i", 1152, 384, 0), ("x3i", 1536, 384, 1)):
             g = torch.Generator(device="cuda").manual_seed(1)
             Af = torch.randn(M, K, device="cuda", generator=g)
             Wf = torch.randn(N, K, device="cuda", generator=g) / K ** 0.5
@@ -42,23 +43,13 @@ def main():
                                               _lib.stream_ptr()), "gemm")
                 fl = 2.0 * M * N * K
             else:
-                hi = Af.to(torch.bfloat16)
-                A2 = torch.cat([hi, (Af - hi.float()).to(torch.bfloat16)], 1).contiguous()
-                W3 = x3c_weights(Wf)
-                if act == 0:  # the QKV form: f32 out
-                    C = torch.empty(M, N, device="cuda")
+                A2, W2 = x3i_weights(Af), x3i_weights(Wf)
+                C2 = torch.empty(M, 2 * N, device="cuda", dtype=torch.bfloat16)
 
-                    def run():
-                        _lib.check(L.tt_gemm_x3c(A2.data_ptr(), 2 * K, W3.data_ptr(), 3 * K,
-                                                 b.data_ptr(), None, 0, C.data_ptr(), N, None, 0,
-                                                 M, N, K, act, _lib.stream_ptr()), "x3c")
-                else:  # the FFN1 form: GELU, split planes out
-                    C2 = torch.empty(M, 2 * N, device="cuda", dtype=torch.bfloat16)
-
-                    def run():
-                        _lib.check(L.tt_gemm_x3c(A2.data_ptr(), 2 * K, W3.data_ptr(), 3 * K,
-                                                 b.data_ptr(), None, 0, None, 0, C2.data_ptr(),
-                                                 2 * N, M, N, K, act, _lib.stream_ptr()), "x3c")
+                def run():
+                    _lib.check(L.tt_gemm_x3i(A2.data_ptr(), 2 * K, W2.data_ptr(), 2 * K,
+                                             b.data_ptr(), C2.data_ptr(), 2 * N, M, N, K, act,
+                                             _lib.stream_ptr()), "x3i")
                 fl = 3 * 2.0 * M * N * K
             for _ in range(3):
                 run()

@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU box: PMC passes over the x3c / bf16 GEMM microbenchmark at Mode A M (separate passes,
+# GPU box: PMC passes over the x3i / bf16 GEMM microbenchmark at Mode A M (separate passes,
 # one counter group each, under their own time limits).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -10,7 +10,7 @@ for ctrs in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY
             "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VMEM SQ_INSTS_VALU SQ_INSTS_SALU" \
             "FETCH_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $ctrs --kernel-trace -d gpurun_out/pmcg_$i -o run --output-format csv -- python tools/bench_gemm_pp.py --M 370761 --iters 2 > gpurun_out/pmcg_$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/pmcg_$i.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $ctrs --kernel-trace -d gpurun_out/pmcg_$i -o run --output-format csv -- python tools/bench_gemm_x3i.py --M 370761 --iters 2 > gpurun_out/pmcg_$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/pmcg_$i.log; exit 1; }
 done
 python tools/pmc_table.py gpurun_out/pmcg_*/run_counter_collection.csv > gpurun_out/pmcg_table.txt
 head -80 gpurun_out/pmcg_table.txt
