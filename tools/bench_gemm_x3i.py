@@ -28,7 +28,8 @@ def main():
     out = {"lib": os.environ.get("TWOTOWER_HIP_LIB", "in-tree")}
     for M in (int(v) for v in a.M.split(",")):
         for (kind, N, K, act) in (("bf16", 1152, 384, 0), ("bf16", 1536, 384, 1),
-                                  ("x3i", 1152, 384, 0), ("x3i", 1536, 384, 1)):
+                                  ("x3i", 1152, 384, 0), ("x3i", 1536, 384, 1),
+                                  ("x3i_ln", 384, 384, 0), ("x3i_ln", 384, 1536, 0)):
             g = torch.Generator(device="cuda").manual_seed(1)
             Af = torch.randn(M, K, device="cuda", generator=g)
             Wf = torch.randn(N, K, device="cuda", generator=g) / K ** 0.5
@@ -42,6 +43,19 @@ def main():
                                               0, None, N, C16.data_ptr(), N, M, N, K, act,
                                               _lib.stream_ptr()), "gemm")
                 fl = 2.0 * M * N * K
+            elif kind == "x3i_ln":  # BertSelfOutput / BertOutput: x = LN(A.W^T + b + x)
+                A2, W2 = x3i_weights(Af), x3i_weights(Wf)
+                X = torch.randn(M, N, device="cuda", generator=g)
+                X2 = torch.empty(M, 2 * N, device="cuda", dtype=torch.bfloat16)
+                gm = torch.rand(N, device="cuda", generator=g) + 0.5
+                bt = torch.randn(N, device="cuda", generator=g)
+
+                def run():
+                    _lib.check(L.tt_gemm_ln_x3i(A2.data_ptr(), 2 * K, W2.data_ptr(), 2 * K,
+                                                b.data_ptr(), gm.data_ptr(), bt.data_ptr(), 1e-12,
+                                                X.data_ptr(), N, X2.data_ptr(), 2 * N, M, N, K,
+                                                _lib.stream_ptr()), "x3i_ln")
+                fl = 3 * 2.0 * M * N * K
             else:
                 A2, W2 = x3i_weights(Af), x3i_weights(Wf)
                 C2 = torch.empty(M, 2 * N, device="cuda", dtype=torch.bfloat16)

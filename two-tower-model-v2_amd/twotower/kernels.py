@@ -397,7 +397,12 @@ def attn_agg_l2(items, w, W1, b1, W2, b2, out=None, fused: bool = None):
     """BuyerTower.attention_aggregation + F.normalize (buyer_tower.py:70-101).  Batches of
     >= ATTN_WS_MIN_ROWS history rows take the two-stage form (first MLP layer as an f32 MFMA
     GEMM, tt_attn_agg_l2_f32_ws); smaller ones (e.g. one /retrieve buyer) the one-kernel form.
-    fused=True/False forces one of them."""
+    fused=True/False forces one of them.  The two forms sum the first MLP layer's dot products
+    in different orders, so the same buyer's embedding can differ in the last bits (measured
+    <= 1e-6) between a call with >= 256 history rows (batch encode) and a smaller one (one
+    /retrieve buyer); near-tied items may then swap ranks between the two.  Both are within the
+    reference-fixture tolerance (2e-6); pass the same ``fused`` everywhere when identical bits
+    across batch sizes matter."""
     require_device(items, "item_embeddings")
     if items.dim() != 3 or w.shape != items.shape[:2]:
         raise ValueError("attn_agg_l2: items [B,S,E] and weights [B,S] required")
