@@ -74,7 +74,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / a.iters
-            out[f"{kind}_M{M}_N{N}_act{act}"] = {"us": round(ms * 1e3, 1),
+            out[f"{kind}_M{M}_N{N}_K{K}_act{act}"] = {"us": round(ms * 1e3, 1),
                                                   "tflops": round(fl / (ms * 1e-3) / 1e12, 1)}
             del Af, Wf
             torch.cuda.empty_cache()

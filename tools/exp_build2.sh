@@ -11,7 +11,12 @@ for v in $VARIANTS; do
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -DTT_TIMING_BUILD $defs -x hip -c $f.hip -o ../build/variants/${f}_$name.o 2>/dev/null &
   done
   wait
-  others=$(ls ../build/*.o | grep -v "tt_filter\|tt_encoder\|tt_scan")
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $others ../build/variants/tt_filter_$name.o ../build/variants/tt_encoder_$name.o ../build/variants/tt_scan_$name.o -o ../lib/variants/lib_$name.so
+  objs=""
+  others=$(ls ../build/*.o)
+  for f in ${EXP_FILES:-tt_filter tt_encoder tt_scan}; do
+    others=$(echo "$others" | grep -v "/$f\.")
+    objs="$objs ../build/variants/${f}_$name.o"
+  done
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $others $objs -o ../lib/variants/lib_$name.so
 done
 ls ../lib/variants
