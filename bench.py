@@ -331,26 +331,45 @@ def batch_sweep(a, shard, shard16, n, E, K, bounds, dev):
                        "bf16_pass_frac_end_to_end": 2.0 * n * ep / (t * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                        "full_level_frac": 2.0 * n * ep / (l_ * 1e-3) / 1e9 / HBM_PEAK_GBPS}
         del ws
-    # k in (128, 1000] (the /retrieve cap, server.py:46): the exact f32 scan, nq = 1, k = 1000
-    q = torch.zeros((1, ep), device=dev)
-    q[:, :E] = torch.randn((1, E), generator=g, device=dev)
-    kernels.l2norm_rows(q, E, _lib.TT_NORM_ADD_EPS, out=q)
+    # k in (128, 1000] (the /retrieve cap, server.py:46): nq = 1, 32 at k = 1000 through the
+    # scores-then-radix-select path the index takes for k > 128 (FlatIPIndex.search_device),
+    # the per-slab-list scan beside it at nq = 1
     k2 = 1000
-    ws = torch.empty(kernels.scan_workspace_bytes(n, E, 1, k2), dtype=torch.uint8, device=dev)
-    for _ in range(3):
-        kernels.scan_topk(shard, n, E, q, k2, workspace=ws)
-    tk = []
-    for _ in range(21):
-        torch.cuda.synchronize()
-        ev[2].record(stream)
-        kernels.scan_topk(shard, n, E, q, k2, workspace=ws)
-        ev[3].record(stream)
-        torch.cuda.synchronize()
-        tk.append(ev[2].elapsed_time(ev[3]))
-    t = float(np.median(tk))
-    k1000 = {"nq": 1, "k": k2, "ms_per_search": t, "kernel": "k_scan_topk_f32 (exact f32 scan)",
-             "f32_pass_bytes": 4.0 * n * ep,
-             "f32_pass_frac_end_to_end": 4.0 * n * ep / (t * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+
+    def time_k(fn, reps=21):
+        for _ in range(3):
+            fn()
+        tk = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            ev[2].record(stream)
+            fn()
+            ev[3].record(stream)
+            torch.cuda.synchronize()
+            tk.append(ev[2].elapsed_time(ev[3]))
+        return float(np.median(tk))
+
+    k1000 = {}
+    for nq_ in (1, 32):
+        q = torch.zeros((nq_, ep), device=dev)
+        q[:, :E] = torch.randn((nq_, E), generator=g, device=dev)
+        kernels.l2norm_rows(q, E, _lib.TT_NORM_ADD_EPS, out=q)
+        ws = torch.empty(kernels.select_workspace_bytes(n, nq_, k2), dtype=torch.uint8,
+                         device=dev)
+        t = time_k(lambda: kernels.scan_topk_select(shard, n, E, q, k2, workspace=ws))
+        k1000[f"nq{nq_}"] = {
+            "nq": nq_, "k": k2, "ms_per_search": t,
+            "kernel": "tt_scan_topk_select_f32 (exact f32 scores + radix select)",
+            "f32_pass_bytes": 4.0 * n * ep,
+            "f32_pass_frac_end_to_end": 4.0 * n * ep / (t * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+        if nq_ == 1:
+            ws2 = torch.empty(kernels.scan_workspace_bytes(n, E, 1, k2), dtype=torch.uint8,
+                              device=dev)
+            k1000["nq1"]["per_slab_list_scan_ms"] = time_k(
+                lambda: kernels.scan_topk(shard, n, E, q, k2, workspace=ws2), reps=5)
+            del ws2
+        del ws
+    k1000.update(k1000.pop("nq1"))  # nq = 1 at the top level (the driver's key), nq = 32 nested
     return {"catalog": f"{n} x {E}", "k": K, "timing": "median of 21 synchronised calls",
             "by_batch": res, "k1000_nq1": k1000}
 

@@ -95,6 +95,19 @@ int tt_scan_topk_f32_select(const float* db, int64_t n, int32_t d, int64_t ld_db
                             float* out_score, int64_t* out_idx, void* workspace,
                             int64_t workspace_bytes, void* stream);
 
+/* Same results as tt_scan_topk_f32 (bit-identical scores and order) for any 1 <= k <= 1024,
+ * by scores-then-select: every canonical f32 score is written once (the scan's scoring loop)
+ * and each query's k-th largest (score, ~row) key is found by a radix select over its score
+ * row, then the k keys above it are sorted.  The large-k path (faiss.IndexFlatIP.search with
+ * k up to 1000: server.py:46, vector_db.py:160,196): the scan's per-slab top-k lists cost
+ * ~24-29 ms per search at k = 1000 over 1M rows.  Workspace: tt_select_workspace_bytes (the
+ * score rows of up to 64 queries at a time: 256 MB at 1M rows). */
+int tt_select_workspace_bytes(int64_t n, int32_t nq, int32_t k, int64_t* bytes);
+int tt_scan_topk_select_f32(const float* db, int64_t n, int32_t d, int64_t ld_db,
+                            int64_t row_base, const float* q, int32_t nq, int64_t ld_q,
+                            int32_t k, float* out_score, int64_t* out_idx, void* workspace,
+                            int64_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------------
  * Same results as tt_scan_topk_f32 (bit-identical: canonical f32 scores, same order), found
  * through a bf16 MFMA filter over db_bf16 (the bf16 image of db, e.g. from tt_l2norm_rows_f32)

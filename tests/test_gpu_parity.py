@@ -104,6 +104,55 @@ def test_scan_large_k_bit_exact_vs_oracle(K, oracle_mod, n, d, nq, k):
     assert not np.any(i == 7 + 5)
 
 
+@pytest.mark.parametrize("n,d,nq,k", [(3000, 384, 1, 129), (20000, 384, 5, 500),
+                                      (20000, 768, 17, 1000), (4096, 64, 70, 1024),
+                                      (1024, 128, 3, 1024), (50000, 384, 2, 1000)])
+def test_scan_select_bit_exact_vs_oracle(K, oracle_mod, n, d, nq, k):
+    """128 < k <= 1024 (the /retrieve cap is 1000, server.py:46): scores-then-radix-select,
+    bit-exact ids and scores vs the oracle and vs the per-slab-list scan -- one query tile
+    (rows split over waves), several (shared rows), k == n, a NaN row never returned, exact
+    ties (lower row first, also where the k-th score itself is tied), a NaN query (all slots
+    (-inf, -1))."""
+    rng = np.random.default_rng(n + d + k)
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
+    x[7] = np.nan
+    x[11] = x[12]  # an exact tie
+    q = oracle_mod.l2norm_rows(rng.standard_normal((nq, d)).astype(np.float32), 0)
+    # the k-th best of query 0 tied with a later duplicate row: the tie at the threshold
+    # must be resolved by the row word (lower row in, higher row out)
+    s0 = x @ q[0]
+    order = np.argsort(-np.where(np.isnan(s0), -np.inf, s0), kind="stable")
+    if k < n - 2:
+        x[order[k + 1]] = x[order[k - 1]]
+    if nq > 2:
+        q[2] = np.nan
+    dx, dq = dev_rows(x), dev_rows(q)
+    s, i = K.scan_topk_select(dx, n, d, dq, k, row_base=3)
+    s, i = s.cpu().numpy(), i.cpu().numpy()
+    rs, ri = oracle_mod.scan_topk(x, q, k, row_base=3)
+    assert np.array_equal(i, ri)
+    assert np.array_equal(s, rs)
+    assert not np.any(i == 7 + 3)
+    ss, si = K.scan_topk(dx, n, d, dq, k, row_base=3)
+    assert np.array_equal(si.cpu().numpy(), i) and np.array_equal(ss.cpu().numpy(), s)
+
+
+def test_scan_select_query_chunks_bit_exact(K, oracle_mod):
+    """More queries than one chunk of score rows (the chunk is sized by a 256 MB budget: 64
+    queries at 1M rows) -- chunks reuse the workspace, results bit-exact vs the scan."""
+    rng = np.random.default_rng(5)
+    n, d, nq, k = 1_000_000, 128, 80, 300
+    x = torch.from_numpy(oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0))
+    q = oracle_mod.l2norm_rows(rng.standard_normal((nq, d)).astype(np.float32), 0)
+    dx, dq = dev_rows(x.numpy()), dev_rows(q)
+    s, i = K.scan_topk_select(dx, n, d, dq, k)
+    ss, si = K.scan_topk(dx, n, d, dq, k)
+    assert torch.equal(i, si) and torch.equal(s, ss)
+    sub = [0, 63, 64, 79]
+    rs, ri = oracle_mod.scan_topk(x.numpy(), q[sub], k)
+    assert np.array_equal(i.cpu().numpy()[sub], ri)
+
+
 @pytest.mark.parametrize("d,k", [(1000, 100), (1024, 10), (1536, 1100)])
 def test_vector_db_dims_above_768_bit_exact(K, oracle_mod, d, k):
     """Embedding dims past the scan kernels' 768 (the reference accepts any embedding_dim,

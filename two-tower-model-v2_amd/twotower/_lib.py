@@ -67,6 +67,9 @@ SIGNATURES = {
                                               _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
     "tt_scan_topk_f32_select": (ctypes.c_int, [_vp, _i64, _i32, _i64, _i64, _vp, _i32, _i64,
                                                _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "tt_select_workspace_bytes": (ctypes.c_int, [_i64, _i32, _i32, ctypes.POINTER(_i64)]),
+    "tt_scan_topk_select_f32": (ctypes.c_int, [_vp, _i64, _i32, _i64, _i64, _vp, _i32, _i64,
+                                               _i32, _vp, _vp, _vp, _i64, _vp]),
     "tt_filter_workspace_bytes": (ctypes.c_int, [_i64, _i32, _i32, _i32,
                                                  ctypes.POINTER(_i64)]),
     "tt_filter_fallback_offset": (ctypes.c_int, [_i64, _i32, _i32, _i32,

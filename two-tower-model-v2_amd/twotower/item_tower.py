@@ -80,8 +80,11 @@ def pack_sequences(seqs: Sequence[Sequence[int]], device=None):
     cu[1:] = np.cumsum(lens)
     flat = np.fromiter((t for s in seqs for t in s), dtype=np.int32, count=int(cu[-1]))
     dev = device or _lib.device()
-    return (torch.from_numpy(flat).to(dev), torch.from_numpy(cu).to(dev),
-            max(lens) if lens else 0)
+    # pinned + non-blocking: a pageable copy waits for the stream, so the host could not pack
+    # the next batch while this one is encoded
+    up = (lambda a: torch.from_numpy(a).pin_memory().to(dev, non_blocking=True)) \
+        if torch.device(dev).type == "cuda" else (lambda a: torch.from_numpy(a).to(dev))
+    return up(flat), up(cu), max(lens) if lens else 0
 
 
 def x3_split_weights(w: torch.Tensor) -> torch.Tensor:
@@ -246,6 +249,18 @@ class _HipTextEncoder:
         return self.encoder.encode_ids(self.tokenizer(texts))
 
 
+def _device_ids(v, dev):
+    """Categorical ids -> int32 on ``dev`` without stalling the host: a device tensor is used
+    as is, a host list goes through pinned memory with a non-blocking copy (torch.tensor(...,
+    device=dev) is a synchronous copy that waits for the stream, so the host could not queue
+    the next batch's launches while this one runs)."""
+    if v is None:
+        return None
+    if isinstance(v, torch.Tensor):
+        return v.to(dev, torch.int32, non_blocking=True).contiguous()
+    return torch.tensor(v, dtype=torch.int32).pin_memory().to(dev, non_blocking=True)
+
+
 class ItemTower(nn.Module):
     """Mirror of reference ``ItemTower`` (src/models/item_tower.py:10-243)."""
 
@@ -357,8 +372,7 @@ class ItemTower(nn.Module):
         if use_cat:
             bt = self.brand_embedding.weight.detach().to(dev, torch.float32).contiguous()
             ct = self.category_embedding.weight.detach().to(dev, torch.float32).contiguous()
-            bi = torch.tensor(brand_ids, dtype=torch.int32, device=dev) if brand_ids is not None else None
-            ci = torch.tensor(cat_ids, dtype=torch.int32, device=dev) if cat_ids is not None else None
+            bi, ci = _device_ids(brand_ids, dev), _device_ids(cat_ids, dev)
             check(lib().tt_item_concat(te.data_ptr(), te.stride(0), Ht,
                                        bi.data_ptr() if bi is not None else None,
                                        bt.data_ptr() if bi is not None else None,

@@ -89,8 +89,9 @@ class FlatIPIndex:
     def search_device(self, q: torch.Tensor, k: int, method: str = "auto"):
         """q: [nq, ep] normalised device rows -> (scores [nq,k], labels [nq,k]) on device.
 
-        method "auto": bf16 filter + exact f32 re-rank for k <= 128, else the f32 scan;
-        "f32" / "bf16" force one.  Both give bit-identical results."""
+        method "auto": bf16 filter + exact f32 re-rank for k <= 128, else exact f32 scores +
+        radix select (k <= 1024); "f32" / "bf16" force the f32 scan / the filter.  All give
+        bit-identical results."""
         if k < 1:
             raise RuntimeError("Error: 'k > 0' failed")  # faiss' own assertion text
         use_bf16 = method == "bf16" or (method == "auto" and k <= kernels.FILTER_KMAX)
@@ -98,8 +99,11 @@ class FlatIPIndex:
             # faiss takes any k and any d: the generic exact path (GEMM scores + key top-k)
             return kernels.scan_topk_large(self.xb, self.ntotal, self.d, q, k,
                                            row_base=self.row_base)
+        use_select = method == "auto" and k > kernels.FILTER_KMAX
         if use_bf16:
             need = kernels.filter_workspace_bytes(self.ntotal, self.d, q.shape[0], k)
+        elif use_select:
+            need = kernels.select_workspace_bytes(self.ntotal, q.shape[0], k)
         else:
             need = kernels.scan_workspace_bytes(self.ntotal, self.d, q.shape[0], k)
         with self._lock:  # the workspace cache is shared; the outputs are fresh per call
@@ -107,6 +111,9 @@ class FlatIPIndex:
             if use_bf16:
                 return kernels.scan_topk_bf16(self.xb, self.xb16, self.ntotal, self.d, q, k,
                                               self.bounds, row_base=self.row_base, workspace=ws)
+            if use_select:
+                return kernels.scan_topk_select(self.xb, self.ntotal, self.d, q, k,
+                                                row_base=self.row_base, workspace=ws)
             return kernels.scan_topk(self.xb, self.ntotal, self.d, q, k,
                                      row_base=self.row_base, workspace=ws)
 
