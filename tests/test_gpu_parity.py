@@ -137,6 +137,26 @@ def test_scan_select_bit_exact_vs_oracle(K, oracle_mod, n, d, nq, k):
     assert np.array_equal(si.cpu().numpy(), i) and np.array_equal(ss.cpu().numpy(), s)
 
 
+@pytest.mark.parametrize("k", [1000, 129])
+def test_scan_select_heavy_duplicates_tail(K, oracle_mod, k):
+    """3000 identical rows at the top score (more than SL_CAP keys share the k-th key's
+    bucket after two digits): the per-query tail resolves the remaining digits on the row word
+    -- the lowest rows win, bit-exact vs the oracle; a second query without duplicates in the
+    same call takes the short path."""
+    rng = np.random.default_rng(k)
+    n, d = 20000, 128
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
+    q = oracle_mod.l2norm_rows(rng.standard_normal((2, d)).astype(np.float32), 0)
+    x[100:3100] = q[0]  # score ~1.0 for query 0, 3000 exact ties
+    dx, dq = dev_rows(x), dev_rows(q)
+    s, i = K.scan_topk_select(dx, n, d, dq, k)
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
+    assert np.array_equal(ri[0], np.arange(100, 100 + k))
+    s1, i1 = K.scan_topk_select(dx, n, d, dq[:1], k)  # one query: the fused first histogram
+    assert np.array_equal(i1.cpu().numpy(), ri[:1]) and np.array_equal(s1.cpu().numpy(), rs[:1])
+
+
 def test_scan_select_query_chunks_bit_exact(K, oracle_mod):
     """More queries than one chunk of score rows (the chunk is sized by a 256 MB budget: 64
     queries at 1M rows) -- chunks reuse the workspace, results bit-exact vs the scan."""

@@ -7,22 +7,26 @@
 // of a 1M-row catalog.  Here every exact f32 score is written once (the scan's MFMA scoring
 // loop: the canonical fma order, so the scores are the scan's bits) and each query's k-th
 // largest 64-bit key -- float_key(score) << 32 | ~row, the scan's order: score descending,
-// ties to the lower row, NaN last -- is found by an MSB-first radix select over its score row
-// (11/11/10-bit digits of the score word, then of the row word only when the k-th score is
-// tied and not all of its ties are needed).  The keys >= it are exactly the top k; one wave
-// sorts them.  Launches per query chunk: init, scores, up to 6 x (histogram, digit), collect,
-// sort -- each histogram / collect pass re-reads the chunk's score rows (4 B per row and
-// query, L2 / MALL resident at 1M rows), the catalog is read once per 64-query tile.
+// ties to the lower row, NaN last -- is located by an MSB-first radix select over its score row
+// (11/11/10-bit digits of the score word, then of the row word): a digit ends the search once
+// the keys at or above its bucket number at most SL_CAP (usually the second digit: a 22-bit
+// bucket holds a handful of keys), and those keys -- the top k and the rest of the bucket --
+// are collected and sorted by one wave.  Launches per query chunk: init, scores (+ the first
+// histogram for a single query), 2 x (histogram, digit), the tail (digits 3-6 for heavy
+// duplicates; exits at once otherwise), collect, sort.  Each histogram / collect pass re-reads
+// the chunk's score rows (4 B per row and query, L2 / MALL resident at 1M rows); the catalog is
+// read once per 64-query tile.
 #include "tt_common.hpp"
 
 namespace tt {
 
 constexpr int SL_BINS = 2048;
 constexpr int SL_KMAX = 1024;
+constexpr int SL_CAP = 2048;                         // candidates collected and sorted per query
 constexpr int SL_CHUNK = 8192;                       // score rows per histogram / collect block
 constexpr int64_t SL_SCORE_BUDGET = 256ll << 20;     // bytes of score rows per query chunk
 constexpr int SL_QT = 16;                            // queries per wave (MFMA N)
-constexpr int SL_ROWS = 32;                          // rows per wave step
+constexpr int SL_ROWS = 32;                          // slab rows: a multiple of this
 __constant__ const int kSlShift[6] = {53, 42, 32, 21, 10, 0};
 __constant__ const int kSlWidth[6] = {11, 11, 10, 11, 11, 10};
 
@@ -42,16 +46,36 @@ __device__ __forceinline__ uint64_t sel_key(float s, int64_t row) {
 // ---------------------------------------------------------------------------- scores
 // Exact f32 scores of query rows [qbase, qbase + 16 * (SHARE ? 4 : 1)) for catalog rows
 // [s0, s1): the scan's scoring loop (tt_scan.hip scan_tile: query dims 16t + 4g .. + 3 in the
-// MFMA B operand, two 16-row blocks per step), so score[q][r] has the scan's bits.  SHARE
+// MFMA B operand, the same MFMA sequence per accumulator), so score[q][r] has the scan's bits.  SHARE
 // (more than 16 queries): the block's 4 waves own 16 queries each and stream the same rows;
 // otherwise one 16-query tile whose rows the 4 waves split.
-template <int EP, bool SHARE>
+// Rows per wave step: one 16-row MFMA block when the waves split the rows (a step's 24 loads
+// all in flight beside the 96 query VGPRs: 0.57 -> 0.43 ms per k = 1000 search at nq = 1, 1M
+// rows), two when they share them (nq = 32: 1.09 vs 1.17 ms with one).
+// H0 (one query, rows split): the first digit's histogram is counted here from the scores in
+// registers (LDS, flushed once per block) instead of by a pass over the score row.
+#ifndef TT_SEL_RMIN
+#define TT_SEL_RMIN 1024  // smallest slab (rows) when one query tile's waves split the rows (2048: 0.39 ms per nq = 1 search, 1024: 0.35)
+#endif
+#ifndef TT_SEL_NT
+#define TT_SEL_NT 0  // catalog row loads non-temporal
+#endif
+template <int EP, bool SHARE, bool H0 = false>
 __global__ __launch_bounds__(256, EP <= 384 ? 2 : 1) void k_sel_scores(
     const float* __restrict__ db, int64_t n, int64_t ld_db, const float* __restrict__ q, int nq,
-    int64_t ld_q, int rows_per_slab, float* __restrict__ scores, int64_t ld_s) {
+    int64_t ld_q, int rows_per_slab, float* __restrict__ scores, int64_t ld_s,
+    uint32_t* __restrict__ hist0) {
+  static_assert(!(H0 && SHARE), "H0: rows split over the waves, one query");
+  constexpr int RB = SHARE ? 2 : 1, ROWS = 16 * RB;
+  __shared__ uint32_t lh[H0 ? SL_BINS : 1];
+  if constexpr (H0) {
+    for (int b = threadIdx.x; b < SL_BINS; b += 256) lh[b] = 0u;
+    __syncthreads();
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ql = lane & 15, g = lane >> 4;
-  const int qbase = blockIdx.y * (SHARE ? 4 * SL_QT : SL_QT) + (SHARE ? w * SL_QT : 0);
+  const int nw = blockDim.x >> 6;  // SHARE: one wave per 16 queries of the block's tile
+  const int qbase = blockIdx.y * (SHARE ? nw * SL_QT : SL_QT) + (SHARE ? w * SL_QT : 0);
   if (qbase >= nq) return;  // whole wave idle (uniform)
   const int qi = qbase + ql;
   const bool qvalid = qi < nq;
@@ -67,42 +91,56 @@ __global__ __launch_bounds__(256, EP <= 384 ? 2 : 1) void k_sel_scores(
   const int64_t s0 = (int64_t)blockIdx.x * rows_per_slab;
   const int64_t s1 = s0 + rows_per_slab < n ? s0 + rows_per_slab : n;
   float* srow = scores + (int64_t)(qvalid ? qi : 0) * ld_s;
-  const int64_t first = SHARE ? s0 : s0 + (int64_t)SL_ROWS * w;
-  const int64_t stride = SHARE ? SL_ROWS : 4 * SL_ROWS;
+  const int64_t first = SHARE ? s0 : s0 + (int64_t)ROWS * w;
+  const int64_t stride = SHARE ? ROWS : 4 * ROWS;
   for (int64_t rb = first; rb < s1; rb += stride) {
-    const int64_t ra = (rb + ql < n) ? rb + ql : n - 1;
-    const int64_t rc = (rb + 16 + ql < n) ? rb + 16 + ql : n - 1;
-    const float* pa = db + ra * ld_db + 4 * g;
-    const float* pc = db + rc * ld_db + 4 * g;
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    const float* pa[RB];
+#pragma unroll
+    for (int b = 0; b < RB; ++b) {
+      const int64_t r = (rb + 16 * b + ql < n) ? rb + 16 * b + ql : n - 1;
+      pa[b] = db + r * ld_db + 4 * g;
+    }
+    f32x4 acc[RB];
+#pragma unroll
+    for (int b = 0; b < RB; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < EP / 16; ++t) {
-      const f32x4 a0 = *(const f32x4*)(pa + 16 * t);
-      const f32x4 a1 = *(const f32x4*)(pc + 16 * t);
-      const f32x4 b = qf[t];
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[0], b[0], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[0], b[0], acc1, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[1], b[1], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[1], b[1], acc1, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[2], b[2], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[2], b[2], acc1, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[3], b[3], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[3], b[3], acc1, 0, 0, 0);
-    }
-    // D[row 4g + j][query ql]: acc0 -> rows rb + 4g + j, acc1 -> rows rb + 16 + 4g + j
-    if (qvalid) {
-      const int64_t r0 = rb + 4 * g, r1 = rb + 16 + 4 * g;
-      if (r1 + 3 < s1) {
-        *(f32x4*)(srow + r0) = acc0;
-        *(f32x4*)(srow + r1) = acc1;
-      } else {
+      f32x4 a[RB];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (r0 + j < s1) srow[r0 + j] = acc0[j];
-          if (r1 + j < s1) srow[r1 + j] = acc1[j];
+      for (int b = 0; b < RB; ++b)
+        a[b] = TT_SEL_NT ? __builtin_nontemporal_load((const f32x4*)(pa[b] + 16 * t))
+                         : *(const f32x4*)(pa[b] + 16 * t);
+      const f32x4 bq = qf[t];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int b = 0; b < RB; ++b)
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[b][u], bq[u], acc[b], 0, 0, 0);
+    }
+    // D[row 4g + j][query ql] of block b -> score row rb + 16 b + 4g + j
+    if (qvalid) {
+#pragma unroll
+      for (int b = 0; b < RB; ++b) {
+        const int64_t r0 = rb + 16 * b + 4 * g;
+        if (r0 + 3 < s1) {
+          *(f32x4*)(srow + r0) = acc[b];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (r0 + j < s1) srow[r0 + j] = acc[b][j];
+        }
+        if constexpr (H0) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (r0 + j < s1) atomicAdd(&lh[float_key(acc[b][j]) >> 21], 1u);
         }
       }
     }
+  }
+  if constexpr (H0) {
+    __syncthreads();
+    for (int b = threadIdx.x; b < SL_BINS; b += 256)
+      if (lh[b]) atomicAdd(&hist0[b], lh[b]);
   }
 }
 
@@ -139,6 +177,7 @@ __global__ __launch_bounds__(256) void k_sel_hist(const float* __restrict__ scor
   const float* sr = scores + (int64_t)qq * ld_s;
   const int64_t r0 = (int64_t)blockIdx.x * SL_CHUNK;
   const int64_t r1 = r0 + SL_CHUNK < n ? r0 + SL_CHUNK : n;
+#pragma unroll 8
   for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
     const uint64_t key = sel_key(sr[r], r);
     if (hs >= 64 || (key >> hs) == s.prefix) atomicAdd(&lh[(uint32_t)(key >> shift) & mask], 1u);
@@ -151,24 +190,20 @@ __global__ __launch_bounds__(256) void k_sel_hist(const float* __restrict__ scor
 
 // Pass p digit: the bin d holding the krem-th largest key among those sharing the prefix
 // (bins above d hold fewer than krem keys, with d at least krem); the histogram is cleared for
-// the next pass.  When bin d holds exactly krem keys all of them are in the top k: done, and
-// every key >= (prefix . d) << shift is selected.
-__global__ __launch_bounds__(256) void k_sel_digit(int p, SelState* __restrict__ st,
-                                                   uint32_t* __restrict__ hist) {
-  __shared__ uint32_t part[256];
-  const int qq = blockIdx.x, t = threadIdx.x;
-  const SelState s = st[qq];
-  if (s.done) return;  // uniform
-  uint32_t* gh = hist + (int64_t)qq * SL_BINS;
+// the next pass.  When the keys in bin d and above number at most SL_CAP -- (k - krem) of them
+// above the bin -- they are all collected: done, threshold (prefix . d) << shift.
+__device__ void sel_digit(int p, int k, const SelState& s, SelState* __restrict__ sto,
+                          uint32_t* h8base, uint32_t* part) {
+  const int t = threadIdx.x;
   uint32_t h[8];
   uint32_t sum = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    h[i] = gh[8 * t + i];
+    h[i] = h8base[8 * t + i];
     sum += h[i];
   }
 #pragma unroll
-  for (int i = 0; i < 8; ++i) gh[8 * t + i] = 0u;
+  for (int i = 0; i < 8; ++i) h8base[8 * t + i] = 0u;
   part[t] = sum;
   __syncthreads();
   // keys in bins above this thread's: the threads t' > t (suffix sum; 256 adds, done once)
@@ -182,75 +217,155 @@ __global__ __launch_bounds__(256) void k_sel_digit(int p, SelState* __restrict__
       SelState o = s;
       o.prefix = (s.prefix << width) | (uint64_t)(8 * t + i);
       o.krem = (int)(krem - above);
-      if (h[i] == krem - above || p == 5) {
+      // stop when the keys to collect fit the sort of the next power of two >= k (first
+      // digit on), or SL_CAP (from the second digit on: the tail only for heavy duplicates)
+      const uint32_t tot = (uint32_t)(k - s.krem) + above + h[i];
+      uint32_t kp = 64;
+      while (kp < (uint32_t)k) kp <<= 1;
+      if (tot <= kp || (p >= 1 && tot <= (uint32_t)SL_CAP) || p == 5) {
         o.done = 1;
         o.thr = o.prefix << shift;
       }
-      st[qq] = o;
+      *sto = o;
     }
     above += h[i];
   }
 }
 
-// Keys >= thr (exactly k of them) -> the query's candidate list (wave-aggregated slots).
+__global__ __launch_bounds__(256) void k_sel_digit(int p, int k, SelState* __restrict__ st,
+                                                   uint32_t* __restrict__ hist) {
+  __shared__ uint32_t part[256];
+  const int qq = blockIdx.x;
+  const SelState s = st[qq];
+  if (s.done) return;  // uniform
+  sel_digit(p, k, s, st + qq, hist + (int64_t)qq * SL_BINS, part);
+}
+
+// Passes 2 .. 5 for a query whose first two digits left more than SL_CAP keys at or above the
+// k-th key's bucket (thousands of keys sharing 22 bits of the score: exact duplicates): one
+// block per query histograms the whole score row per pass in LDS.  Exits at once otherwise.
+__global__ __launch_bounds__(256) void k_sel_tail(const float* __restrict__ scores, int64_t ld_s,
+                                                  int64_t n, int k, SelState* __restrict__ st) {
+  __shared__ uint32_t lh[SL_BINS];
+  __shared__ uint32_t part[256];
+  const int qq = blockIdx.x;
+  if (st[qq].done) return;  // uniform
+  const float* sr = scores + (int64_t)qq * ld_s;
+  for (int b = threadIdx.x; b < SL_BINS; b += 256) lh[b] = 0u;
+  for (int p = 2; p < 6; ++p) {
+    __syncthreads();
+    const SelState s = st[qq];
+    if (s.done) return;  // uniform
+    const int shift = kSlShift[p], width = kSlWidth[p], hs = shift + width;
+    const uint32_t mask = (1u << width) - 1u;
+    for (int64_t r = threadIdx.x; r < n; r += 256) {
+      const uint64_t key = sel_key(sr[r], r);
+      if ((key >> hs) == s.prefix) atomicAdd(&lh[(uint32_t)(key >> shift) & mask], 1u);
+    }
+    __syncthreads();
+    sel_digit(p, k, s, st + qq, lh, part);  // clears lh for the next pass
+    __threadfence_block();
+  }
+}
+
+// Keys >= thr (k .. SL_CAP of them) -> the query's candidate list: gathered per block in LDS,
+// then one global atomic per block reserves its slots (an atomic per taking wave on the one
+// counter serialised ~1k atomics from every CU: 19 us at k = 1000, 1M rows).
 __global__ __launch_bounds__(256) void k_sel_collect(const float* __restrict__ scores,
                                                      int64_t ld_s, int64_t n,
                                                      SelState* __restrict__ st,
                                                      uint64_t* __restrict__ cand) {
-  const int qq = blockIdx.y, lane = threadIdx.x & 63;
+  __shared__ uint64_t lbuf[SL_CAP];
+  __shared__ int lcnt, lbase;
+  const int qq = blockIdx.y;
+  if (threadIdx.x == 0) lcnt = 0;
+  __syncthreads();
   const uint64_t thr = st[qq].thr;
   const float* sr = scores + (int64_t)qq * ld_s;
   const int64_t r0 = (int64_t)blockIdx.x * SL_CHUNK;
   const int64_t r1 = r0 + SL_CHUNK < n ? r0 + SL_CHUNK : n;
-  uint64_t* cq = cand + (int64_t)qq * SL_KMAX;
-  // every lane runs the same trip count (ballots need the whole wave)
-  for (int64_t rw = r0 + (threadIdx.x & ~63); rw < r1; rw += 256) {
-    const int64_t r = rw + lane;
-    const uint64_t key = r < r1 ? sel_key(sr[r], r) : 0ull;
-    const bool take = r < r1 && key >= thr;
-    const uint64_t m = __ballot(take);
-    if (m) {
-      int base = 0;
-      if (lane == 0) base = atomicAdd(&st[qq].ncand, __popcll(m));
-      base = __shfl(base, 0, 64);
-      if (take) {
-        const int slot = base + __popcll(m & ((1ull << lane) - 1ull));
-        if (slot < SL_KMAX) cq[slot] = key;  // bounds: never more than k by construction
+#pragma unroll 8
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += 256) {
+    const uint64_t key = sel_key(sr[r], r);
+    if (key >= thr) {
+      const int slot = atomicAdd(&lcnt, 1);
+      if (slot < SL_CAP) lbuf[slot] = key;  // bounds: at most SL_CAP keys >= thr in all
+    }
+  }
+  __syncthreads();
+  const int c = lcnt < SL_CAP ? lcnt : SL_CAP;
+  if (c == 0) return;  // uniform
+  if (threadIdx.x == 0) lbase = atomicAdd(&st[qq].ncand, c);
+  __syncthreads();
+  uint64_t* cq = cand + (int64_t)qq * SL_CAP;
+  for (int e = threadIdx.x; e < c; e += 256)
+    if (lbase + e < SL_CAP) cq[lbase + e] = lbuf[e];
+}
+
+// One block per query: the candidate keys (k .. SL_CAP, unique) are cut into 4 runs, one per
+// wave, each sorted descending in registers (bitonic_desc: DPP exchanges for most stages);
+// a key's final position is its index in its run plus, for each other run, the number of
+// keys above it there (binary search of that run in LDS) -- the first k positions are written
+// as (score, row).  NaN scores (key word 0) read (-inf, -1), as in the scan.  (A bitonic
+// network over all keys in LDS: 21 us at k = 1000; one wave sorting 2048 keys: 51 us.)
+template <int PER>
+__device__ __forceinline__ void sel_sort_runs(const uint64_t* __restrict__ cq, int c, int k,
+                                              uint64_t* ks, int64_t row_base, float* os,
+                                              int64_t* oi) {
+  constexpr int R = 64 * PER;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  uint64_t key[PER];
+#pragma unroll
+  for (int r = 0; r < PER; ++r) {
+    const int e = w * R + lane * PER + r;
+    key[r] = e < c ? cq[e] : 0ull;
+  }
+  bitonic_desc<PER>(key, lane);
+#pragma unroll
+  for (int r = 0; r < PER; ++r) ks[w * R + lane * PER + r] = key[r];
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < PER; ++r) {
+    const uint64_t x = key[r];
+    if (x == 0ull) continue;  // padding (every real key is nonzero: its row word is ~row)
+    int rank = lane * PER + r;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      if (v == w) continue;
+      const uint64_t* run = ks + v * R;
+      int lo = 0, hi = R;  // keys of run v above x: the first index holding a key < x
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (run[mid] > x) lo = mid + 1;
+        else hi = mid;
       }
+      rank += lo;
+    }
+    if (rank < k) {
+      const uint32_t hi32 = (uint32_t)(x >> 32);
+      os[rank] = hi32 != 0u ? key_float(hi32) : -__builtin_huge_valf();
+      oi[rank] = hi32 != 0u ? row_base + (int64_t)key_row(x) : -1;
     }
   }
 }
 
-// One wave per query: sort the k candidate keys (descending) and write (score, row).  NaN
-// scores (key word 0) read (-inf, -1), as in the scan.
-__global__ __launch_bounds__(64) void k_sel_sort(const SelState* __restrict__ st,
-                                                 const uint64_t* __restrict__ cand, int k,
-                                                 int64_t row_base, float* __restrict__ out_s,
-                                                 int64_t* __restrict__ out_i, int64_t q0) {
-  constexpr int PER = SL_KMAX / 64;
-  const int qq = blockIdx.x, lane = threadIdx.x;
+__global__ __launch_bounds__(256) void k_sel_sort(const SelState* __restrict__ st,
+                                                  const uint64_t* __restrict__ cand, int k,
+                                                  int64_t row_base, float* __restrict__ out_s,
+                                                  int64_t* __restrict__ out_i, int64_t q0) {
+  __shared__ uint64_t ks[SL_CAP];
+  const int qq = blockIdx.x;
   int c = st[qq].ncand;
-  c = c < SL_KMAX ? c : SL_KMAX;
-  const uint64_t* cq = cand + (int64_t)qq * SL_KMAX;
-  uint64_t key[PER];
-#pragma unroll
-  for (int r = 0; r < PER; ++r) {
-    const int e = lane * PER + r;
-    key[r] = e < c ? cq[e] : 0ull;
-  }
-  bitonic_desc<PER>(key, lane);
+  c = c < SL_CAP ? c : SL_CAP;
   float* os = out_s + (q0 + qq) * (int64_t)k;
   int64_t* oi = out_i + (q0 + qq) * (int64_t)k;
-#pragma unroll
-  for (int r = 0; r < PER; ++r) {
-    const int e = lane * PER + r;
-    if (e < k) {
-      const uint32_t hi = (uint32_t)(key[r] >> 32);
-      const bool ok = hi != 0u && e < c;
-      os[e] = ok ? key_float(hi) : -__builtin_huge_valf();
-      oi[e] = ok ? row_base + (int64_t)key_row(key[r]) : -1;
-    }
+  for (int e = c + threadIdx.x; e < k; e += 256) {  // never taken: the collect gathers >= k
+    os[e] = -__builtin_huge_valf();
+    oi[e] = -1;
   }
+  const uint64_t* cq = cand + (int64_t)qq * SL_CAP;
+  if (c <= 4 * 256) sel_sort_runs<4>(cq, c, k, ks, row_base, os, oi);
+  else sel_sort_runs<8>(cq, c, k, ks, row_base, os, oi);
 }
 
 static int sel_pad_dim(int d) {
@@ -283,7 +398,7 @@ extern "C" int tt_select_workspace_bytes(int64_t n, int32_t nq, int32_t k, int64
   TT_REQUIRE(n >= 1 && nq >= 1 && k >= 1, "n, nq, k must be >= 1");
   const SelPlan p = plan_select(n, nq);
   const int64_t b = (int64_t)p.qc * p.ld_s * 4 + (int64_t)p.qc * SL_BINS * 4 +
-                    (int64_t)p.qc * (int64_t)sizeof(SelState) + (int64_t)p.qc * SL_KMAX * 8;
+                    (int64_t)p.qc * (int64_t)sizeof(SelState) + (int64_t)p.qc * SL_CAP * 8;
   *bytes = (b + 4 * 256 + 255) / 256 * 256;
   return TT_OK;
 }
@@ -324,21 +439,30 @@ extern "C" int tt_scan_topk_select_f32(const float* db, int64_t n, int32_t d, in
     int rc = check_launch("k_sel_init");
     if (rc) return rc;
     const bool share = qn > SL_QT;
-    const int qtiles = share ? (qn + 4 * SL_QT - 1) / (4 * SL_QT) : 1;
-    // row slabs: >= 2 blocks per CU over the query tiles, slabs of >= 2048 rows
-    int64_t slabs = (1024 + qtiles - 1) / qtiles;
+    // SHARE: blocks of one wave per 16 queries (up to 4): a 32-query chunk runs 2-wave blocks,
+    // more of them per CU, instead of 4-wave blocks with 2 waves idle
+    const int swaves = share ? ((qn + SL_QT - 1) / SL_QT < 4 ? (qn + SL_QT - 1) / SL_QT : 4) : 4;
+    const int qtiles = share ? (qn + swaves * SL_QT - 1) / (swaves * SL_QT) : 1;
+    // row slabs: ~2k blocks' worth of waves over the query tiles; >= 512 rows per wave (split
+    // waves: a 2048-row slab is 512 rows per wave; shared: every wave streams the whole slab)
+    int64_t slabs = ((share ? 2048 : 1024) + qtiles - 1) / qtiles;
     int64_t rps = (n + slabs - 1) / slabs;
-    rps = rps < 2048 ? 2048 : (rps + SL_ROWS - 1) / SL_ROWS * SL_ROWS;
+    const int64_t rmin = share ? 512 : TT_SEL_RMIN;
+    rps = rps < rmin ? rmin : (rps + SL_ROWS - 1) / SL_ROWS * SL_ROWS;
     slabs = (n + rps - 1) / rps;
     const dim3 grid((unsigned)slabs, (unsigned)qtiles);
+    const bool h0 = !share && qn == 1;
 #define TT_SEL_CASE(E)                                                                          \
   case E:                                                                                       \
     if (share)                                                                                  \
-      hipLaunchKernelGGL((k_sel_scores<E, true>), grid, dim3(256), 0, s, db, n, ld_db, qp, qn,  \
-                         ld_q, (int)rps, scores, p.ld_s);                                       \
+      hipLaunchKernelGGL((k_sel_scores<E, true>), grid, dim3(64 * swaves), 0, s, db, n, ld_db,  \
+                         qp, qn, ld_q, (int)rps, scores, p.ld_s, hist);                         \
+    else if (h0)                                                                                \
+      hipLaunchKernelGGL((k_sel_scores<E, false, true>), grid, dim3(256), 0, s, db, n, ld_db,   \
+                         qp, qn, ld_q, (int)rps, scores, p.ld_s, hist);                         \
     else                                                                                        \
       hipLaunchKernelGGL((k_sel_scores<E, false>), grid, dim3(256), 0, s, db, n, ld_db, qp, qn, \
-                         ld_q, (int)rps, scores, p.ld_s);                                       \
+                         ld_q, (int)rps, scores, p.ld_s, hist);                                 \
     break;
     switch (ep) {
       TT_SEL_CASE(64)
@@ -353,20 +477,27 @@ extern "C" int tt_scan_topk_select_f32(const float* db, int64_t n, int32_t d, in
 #undef TT_SEL_CASE
     rc = check_launch("k_sel_scores");
     if (rc) return rc;
-    for (int pass = 0; pass < 6; ++pass) {
-      hipLaunchKernelGGL(k_sel_hist, dim3(nchunk, qn), dim3(256), 0, s, scores, p.ld_s, n, pass,
-                         st, hist);
-      rc = check_launch("k_sel_hist");
-      if (rc) return rc;
-      hipLaunchKernelGGL(k_sel_digit, dim3(qn), dim3(256), 0, s, pass, st, hist);
+    // two digits on the chip (the second almost always leaves <= SL_CAP keys at or above the
+    // k-th key's bucket), the rest -- duplicates -- in the per-query tail
+    for (int pass = 0; pass < 2; ++pass) {
+      if (!(pass == 0 && h0)) {
+        hipLaunchKernelGGL(k_sel_hist, dim3(nchunk, qn), dim3(256), 0, s, scores, p.ld_s, n,
+                           pass, st, hist);
+        rc = check_launch("k_sel_hist");
+        if (rc) return rc;
+      }
+      hipLaunchKernelGGL(k_sel_digit, dim3(qn), dim3(256), 0, s, pass, k, st, hist);
       rc = check_launch("k_sel_digit");
       if (rc) return rc;
     }
+    hipLaunchKernelGGL(k_sel_tail, dim3(qn), dim3(256), 0, s, scores, p.ld_s, n, k, st);
+    rc = check_launch("k_sel_tail");
+    if (rc) return rc;
     hipLaunchKernelGGL(k_sel_collect, dim3(nchunk, qn), dim3(256), 0, s, scores, p.ld_s, n, st,
                        cand);
     rc = check_launch("k_sel_collect");
     if (rc) return rc;
-    hipLaunchKernelGGL(k_sel_sort, dim3(qn), dim3(64), 0, s, st, cand, k, row_base, out_score,
+    hipLaunchKernelGGL(k_sel_sort, dim3(qn), dim3(256), 0, s, st, cand, k, row_base, out_score,
                        out_idx, (int64_t)q0);
     rc = check_launch("k_sel_sort");
     if (rc) return rc;
