@@ -106,6 +106,7 @@ def encoder_flops(lens, E_out=384):
     return float((L * (42.47e6 + 18432.0 * L)).sum() + 0.46e6 * len(L))
 
 
+@torch.no_grad()  # inference, as ItemTower.encode_batch runs it
 def configs1(a, dev, rank):
     """BASELINE.json configs[1]: 100k products x 384-d, item-tower encode at batch 256 +
     brute-force top-100 (scripts/generate_embeddings.py:52 -> ItemTower.encode_batch,
@@ -155,6 +156,7 @@ def configs1(a, dev, rank):
     for prec, nb in (("x3", len(batches)), ("bf16", min(64, len(batches))),
                      ("f32", min(16, len(batches)))):
         enc = BertEncoder(sd, cfg, device=dev, prec=prec)
+        it.head_prec = "f32" if prec == "f32" else "x3"  # ItemTower's choice with this encoder
         pooled = torch.empty((BS, cfg["hidden"]), device=dev)
         e_enc = [torch.cuda.Event(enable_timing=True) for _ in range(2 * nb)]
         e_srch = [torch.cuda.Event(enable_timing=True) for _ in range(nb)]
@@ -244,6 +246,7 @@ def configs1(a, dev, rank):
     # (pre-tokenized ids: the tokenizer is host-side and out of scope)
     DB = ItemTower.device_batch
     enc = BertEncoder(sd, cfg, device=dev, prec="x3")
+    it.head_prec = "x3"
     chunks = [pack_sequences(seqs[i:i + DB], dev) for i in range(0, n_txt, DB)]
     pooled = torch.empty((DB, cfg["hidden"]), device=dev)
 
@@ -544,6 +547,7 @@ def single_buyer_api(a, dev, shard, shard16, n, E, K, bounds, table, hist, w, re
             "api_e2e_is": "Mode B encode of one buyer (device) + .cpu() + VectorDatabase.retrieve"}
 
 
+@torch.no_grad()  # inference, as ItemTower.encode_batch runs it
 def mode_a(a, dev, world, rank, search_local, k, E):
     """Mode A: EmbeddingEncoder.encode_buyer as written (src/inference/encoder.py:286-303):
     each buyer's S history texts are re-encoded by the item tower (MiniLM encoder on HIP,
@@ -562,6 +566,7 @@ def mode_a(a, dev, world, rank, search_local, k, E):
 
     torch.manual_seed(0)
     it = ItemTower(text_encoder=_Dim(), embedding_dim=E)  # the catalog's dim (--dim)
+    it.head_prec = "f32" if a.mode_a_prec == "f32" else "x3"  # as with the HIP text encoder
     it.initialize_categorical_embeddings([f"brand{i}" for i in range(50)],
                                          [f"cat{i}" for i in range(20)])
     it.to(dev).eval()

@@ -290,6 +290,11 @@ class ItemTower(nn.Module):
                                         nn.Dropout(0.1),
                                         nn.Linear(projection_hidden_dim, embedding_dim))
         self._categorical_vocabs = {"brand": set(), "category": set()}
+        # precision of the projection head's two GEMMs at inference: "x3" (split-bf16 products,
+        # k_gemm<float, 1>: the f32 precision class at 16x the f32 MFMA rate -- a batch of 256
+        # is 4 tiles, 47 + 27 us on f32 MFMA) with the x3 encoder, else "f32"
+        enc = getattr(self.text_encoder, "encoder", None)
+        self.head_prec = "x3" if getattr(enc, "prec", None) == "x3" else "f32"
 
     # reference :68-98
     def initialize_categorical_embeddings(self, brand_vocab: Optional[List[str]] = None,
@@ -391,18 +396,19 @@ class ItemTower(nn.Module):
             raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({B}x{width} and "
                                f"{w0.shape[1]}x{hdim})")
         h = torch.empty((B, hdim), dtype=torch.float32, device=dev)
-        check(lib().tt_gemm_f32(x.data_ptr(), x.stride(0), w0.data_ptr(), w0.stride(0),
-                                b0.data_ptr(), None, 0, h.data_ptr(), h.stride(0), None, 0, B, hdim,
-                                width, _lib.TT_ACT_RELU, stream_ptr()), "projection.0")
+        gemm = lib().tt_gemm_x3 if self.head_prec == "x3" else lib().tt_gemm_f32
+        check(gemm(x.data_ptr(), x.stride(0), w0.data_ptr(), w0.stride(0), b0.data_ptr(), None, 0,
+                   h.data_ptr(), h.stride(0), None, 0, B, hdim, width, _lib.TT_ACT_RELU,
+                   stream_ptr()), "projection.0")
         if self.training and self.projection[2].p > 0:  # nn.Dropout (:61) in train mode
             from .train import apply_dropout, dropout_keep
 
             p = self.projection[2].p
             apply_dropout(h, dropout_keep(h.shape, p, dev), p)
         y = torch.empty((B, E), dtype=torch.float32, device=dev)
-        check(lib().tt_gemm_f32(h.data_ptr(), h.stride(0), w3.data_ptr(), w3.stride(0),
-                                b3.data_ptr(), None, 0, y.data_ptr(), y.stride(0), None, 0, B, E,
-                                hdim, _lib.TT_ACT_NONE, stream_ptr()), "projection.3")
+        check(gemm(h.data_ptr(), h.stride(0), w3.data_ptr(), w3.stride(0), b3.data_ptr(), None, 0,
+                   y.data_ptr(), y.stride(0), None, 0, B, E, hdim, _lib.TT_ACT_NONE,
+                   stream_ptr()), "projection.3")
         return kernels.l2norm_rows(y, E, _lib.TT_NORM_MAX_EPS, out=y)
 
     # reference :174-211

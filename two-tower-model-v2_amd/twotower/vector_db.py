@@ -281,12 +281,12 @@ class VectorDatabase:
     def _to_results(self, scores: np.ndarray, indices: np.ndarray):
         out = []
         n = len(self.product_ids)
-        for query_scores, query_indices in zip(scores, indices):
-            res = []
-            for idx, score in zip(query_indices, query_scores):
-                if idx < n:  # reference :165 (note: -1 would pass, as in the reference)
-                    res.append((self.product_ids[idx], float(score)))
-            out.append(res)
+        ids = self.product_ids
+        # Python ints / floats first (.tolist()): per-element numpy scalars made a k = 1000
+        # response cost ~0.25 ms of host time; float(np.float32 x) == the list's float of x
+        for query_scores, query_indices in zip(scores.tolist(), indices.tolist()):
+            out.append([(ids[idx], score) for idx, score in zip(query_indices, query_scores)
+                        if idx < n])  # reference :165 (note: -1 would pass, as in the reference)
         return out
 
     def retrieve(self, query_embedding: np.ndarray, k: int = 10) -> List[Tuple[str, float]]:
