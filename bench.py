@@ -598,12 +598,43 @@ def mode_a(a, dev, world, rank, search_local, k, E):
     if world > 1:
         dist.barrier()
     dt = (time.perf_counter() - t0) / a.mode_a_steps
+    dt1 = dt2 = dt
+    if world == 1:
+        # consecutive steps (independent batches of 256 buyers) two in flight on alternating
+        # streams, each with its own encoder workspace / outputs / exchange, as configs[1]
+        streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+        slots = [(torch.empty_like(pooled), TopkExchange(B, _lib.padded_dim(E), k, device=dev))
+                 for _ in streams]
+
+        def step2(j):
+            pooled_s, ex_s = slots[j % 2]
+            enc.encode_packed(ids, cu, mx, out=pooled_s)
+            items = it.head(pooled_s, bid, cid, use_cat=True)
+            q = kernels.weighted_avg_l2(items.view(B, S, E), w)
+            qn = torch.zeros((B, _lib.padded_dim(E)), device=dev)
+            kernels.l2norm_rows(q, E, _lib.TT_NORM_ADD_EPS, out=qn)
+            return ex_s.search(qn, search_local, kernels.merge_topk)
+
+        for j in range(2):
+            with torch.cuda.stream(streams[j % 2]):
+                step2(j)
+        torch.cuda.synchronize()
+        n2 = max(4, 2 * a.mode_a_steps)
+        t0 = time.perf_counter()
+        for j in range(n2):
+            with torch.cuda.stream(streams[j % 2]):
+                step2(j)
+        torch.cuda.synchronize()
+        dt2 = (time.perf_counter() - t0) / n2
+        dt = min(dt1, dt2)
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
     tokens = int(ids.numel())
     res = {"value": world * B / dt, "unit": "buyers/s", "ms_per_step": dt * 1e3,
+           "buyers_per_s_one_stream": world * B / dt1,
+           "buyers_per_s_two_streams": world * B / dt2,
            "buyers_per_rank": B, "texts_per_step_per_rank": B * S,
            "tokens_per_step_per_rank": tokens, "encoder_prec": a.mode_a_prec,
            "texts_per_s": world * B * S / dt,
