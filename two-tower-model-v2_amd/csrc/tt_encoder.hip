@@ -1448,6 +1448,131 @@ __global__ __launch_bounds__(256) void k_embed_ln(const int32_t* __restrict__ id
   }
 }
 
+// k_embed_ln for H % 4 == 0, H <= 256 NV: a wave embeds FOUR tokens of its sequence at once
+// with 16-B loads and stores (all 4 x NV row gathers in flight after the 4 id loads), blocks of
+// (sequence, 16 tokens).  The one-token-per-wave form waited 72% of its wave cycles on the
+// dependent id -> row gather (727 us per 370k-token Mode A step).  Per element the same
+// (word + type) + position sum; the LayerNorm statistics reduce 4 contiguous elements per lane
+// and then across lanes.  x3i output: a lane's 4 columns lie in one 32-column block.
+template <int NV>
+__global__ __launch_bounds__(256) void k_embed_ln4(const int32_t* __restrict__ ids,
+                                                   const int32_t* __restrict__ cu, int n_seq,
+                                                   int64_t T, const float* __restrict__ word,
+                                                   int vocab, const float* __restrict__ pos,
+                                                   const float* __restrict__ type0,
+                                                   const float* __restrict__ gamma,
+                                                   const float* __restrict__ beta, float eps,
+                                                   float* __restrict__ y, uint16_t* __restrict__ y16,
+                                                   int H, int split16) {
+  constexpr int TPW = 4;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t t0 = cu[blockIdx.x], t1 = cu[blockIdx.x + 1];
+  const int H4 = H >> 2;
+  const float inv_h = 1.0f / (float)H;
+  for (int64_t tb = t0 + (int64_t)TPW * (4 * (int64_t)blockIdx.y + w); tb < t1;
+       tb += (int64_t)TPW * 4 * gridDim.y) {
+    int id[TPW];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      const int v = tb + j < t1 ? ids[tb + j] : 0;
+      id[j] = (v >= 0 && v < vocab) ? v : 0;
+    }
+    f32x4 v[TPW][NV];
+    float sm[TPW];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      const int p = tb + j < t1 ? (int)(tb + j - t0) : 0;
+      const float* wr = word + (int64_t)id[j] * H;
+      const float* pr = pos + (int64_t)p * H;
+      sm[j] = 0.0f;
+#pragma unroll
+      for (int c = 0; c < NV; ++c) {
+        const int e4 = lane + 64 * c;
+        if (e4 < H4) {
+          const f32x4 wv = *(const f32x4*)(wr + 4 * e4), tv = *(const f32x4*)(type0 + 4 * e4);
+          const f32x4 pv = *(const f32x4*)(pr + 4 * e4);
+          v[j][c] = (wv + tv) + pv;
+          sm[j] += (v[j][c][0] + v[j][c][1]) + (v[j][c][2] + v[j][c][3]);
+        } else {
+          v[j][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TPW; ++j)
+      for (int o = 32; o > 0; o >>= 1) sm[j] += __shfl_xor(sm[j], o, 64);
+    float q[TPW];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      const float mean = sm[j] * inv_h;
+      q[j] = 0.0f;
+#pragma unroll
+      for (int c = 0; c < NV; ++c)
+        if (lane + 64 * c < H4)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float d = v[j][c][u] - mean;
+            q[j] = fmaf(d, d, q[j]);
+          }
+    }
+#pragma unroll
+    for (int j = 0; j < TPW; ++j)
+      for (int o = 32; o > 0; o >>= 1) q[j] += __shfl_xor(q[j], o, 64);
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+      const int64_t t = tb + j;
+      if (t >= t1) continue;
+      const float mean = sm[j] * inv_h;
+      const float rstd = 1.0f / sqrtf(q[j] * inv_h + eps);
+#pragma unroll
+      for (int c = 0; c < NV; ++c) {
+        const int e4 = lane + 64 * c;
+        if (e4 >= H4) continue;
+        const f32x4 gm = *(const f32x4*)(gamma + 4 * e4), bt = *(const f32x4*)(beta + 4 * e4);
+        f32x4 o;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[u] = (v[j][c][u] - mean) * rstd * gm[u] + bt[u];
+        *(f32x4*)(y + t * H + 4 * e4) = o;
+        if (y16) {
+          const uint2 hv = uint2{pack_bf16_hw(o[0], o[1]), pack_bf16_hw(o[2], o[3])};
+          if (split16) {
+            uint16_t* d = y16 + t * 2 * H + x3i_col(4 * e4);
+            *(uint2*)d = hv;
+            *(uint2*)(d + 32) = uint2{pack_bf16_hw(o[0] - __uint_as_float(hv.x << 16),
+                                                   o[1] - __uint_as_float(hv.x & 0xffff0000u)),
+                                      pack_bf16_hw(o[2] - __uint_as_float(hv.y << 16),
+                                                   o[3] - __uint_as_float(hv.y & 0xffff0000u))};
+          } else {
+            *(uint2*)(y16 + t * H + 4 * e4) = hv;
+          }
+        }
+      }
+    }
+  }
+}
+
+// host: the embedding LayerNorm launch (k_embed_ln4 when H % 4 == 0 and H <= 1024)
+static int embed_ln_launch(const tt_bert_model* m, const int32_t* ids, const int32_t* cu,
+                           int n_seq, int64_t T, int max_len, float* x, uint16_t* x16, int H,
+                           int split16, hipStream_t st) {
+  if (H % 4 == 0 && H <= 1024 && ((uintptr_t)m->word_emb % 16) == 0 &&
+      ((uintptr_t)m->pos_emb % 16) == 0 && ((uintptr_t)m->type_emb % 16) == 0 &&
+      ((uintptr_t)m->emb_ln_g % 16) == 0 && ((uintptr_t)m->emb_ln_b % 16) == 0 &&
+      ((uintptr_t)x % 16) == 0 && ((uintptr_t)x16 % 8) == 0) {
+    const unsigned chunks = (unsigned)(max_len > 16 ? (max_len + 15) / 16 : 1);
+    auto kern = H <= 256 ? k_embed_ln4<1> : H <= 512 ? k_embed_ln4<2> : k_embed_ln4<4>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)n_seq, chunks), dim3(256), 0, st, ids, cu, n_seq, T,
+                       m->word_emb, m->vocab, m->pos_emb, m->type_emb, m->emb_ln_g, m->emb_ln_b,
+                       m->ln_eps, x, x16, H, split16);
+    return check_launch("k_embed_ln4");
+  }
+  const unsigned chunks = (unsigned)(max_len > 4 ? (max_len + 3) / 4 : 1);
+  hipLaunchKernelGGL(k_embed_ln, dim3((unsigned)n_seq, chunks), dim3(256), 0, st, ids, cu, n_seq,
+                     T, m->word_emb, m->vocab, m->pos_emb, m->type_emb, m->emb_ln_g, m->emb_ln_b,
+                     m->ln_eps, x, x16, H, split16);
+  return check_launch("k_embed_ln");
+}
+
 // Multi-head self-attention over packed sequences.  qkv: [T, 3H] (Q | K | V, head h at
 // columns h*DH within each third).  Block per (sequence, head); K and V of the head live in
 // LDS; thread = query row.  softmax(q.k / sqrt(DH)) . v, keys restricted to the sequence.
@@ -2644,11 +2769,7 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
     uint16_t* xs = (uint16_t*)w.y;
     uint16_t* cs = (uint16_t*)w.ctx;
     uint16_t* fs = (uint16_t*)w.ff;
-    const unsigned chunks = (unsigned)(max_len > 4 ? (max_len + 3) / 4 : 1);
-    hipLaunchKernelGGL(k_embed_ln, dim3((unsigned)n_seq, chunks), dim3(256), 0, st, ids,
-                       cu_seqlens, n_seq, T, m->word_emb, m->vocab, m->pos_emb, m->type_emb,
-                       m->emb_ln_g, m->emb_ln_b, m->ln_eps, w.x, xs, H, 1);
-    int rc = check_launch("k_embed_ln");
+    int rc = embed_ln_launch(m, ids, cu_seqlens, n_seq, T, max_len, w.x, xs, H, 1, st);
     if (rc) return rc;
     for (int l = 0; l < NL; ++l) {
       const tt_bert_layer& L = m->layer[l];
@@ -2674,11 +2795,8 @@ extern "C" int tt_bert_encode(const tt_bert_model* m, const int32_t* ids, const 
     return check_launch("k_mean_pool");
   }
   {
-    const unsigned chunks = (unsigned)(max_len > 4 ? (max_len + 3) / 4 : 1);
-    hipLaunchKernelGGL(k_embed_ln, dim3((unsigned)n_seq, chunks), dim3(256), 0, st, ids,
-                       cu_seqlens, n_seq, T, m->word_emb, m->vocab, m->pos_emb, m->type_emb,
-                       m->emb_ln_g, m->emb_ln_b, m->ln_eps, w.x, bf ? w.x16 : nullptr, H, 0);
-    int rc = check_launch("k_embed_ln");
+    int rc = embed_ln_launch(m, ids, cu_seqlens, n_seq, T, max_len, w.x, bf ? w.x16 : nullptr, H,
+                             0, st);
     if (rc) return rc;
   }
   for (int l = 0; l < NL; ++l) {
