@@ -2072,7 +2072,12 @@ __global__ __launch_bounds__(256 * HG) void k_attn32_x3(
     for (int i = 0; i < 8; ++i) {
       const uint32_t a = (v0[i >> 1] >> (16 * (i & 1))) & 0xffffu;
       const uint32_t b = (v1[i >> 1] >> (16 * (i & 1))) & 0xffffu;
-      *(uint32_t*)(Vp + ((size_t)(c8 + i) * vst + j) * 2) = a | (b << 16);
+      // V^T column swizzle: the 16 lanes of a key pair write rows 8 apart of 4 planes -- one
+      // bank (67% of the kernel's LDS cycles were conflicts) -- unless the pair's column is
+      // XORed by 4 x (row group, plane); XOR by multiples of 4 keeps the readers' 4-key
+      // groups contiguous and inside the row (< vst).  Encode -0.7% (B 256) / -0.8% (B 5120).
+      const int jw = j ^ (4 * ((c8 >> 3) + 4 * (hs + HG * pl)));
+      *(uint32_t*)(Vp + ((size_t)(c8 + i) * vst + jw) * 2) = a | (b << 16);
     }
   }
   __syncthreads();
@@ -2132,9 +2137,15 @@ __global__ __launch_bounds__(256 * HG) void k_attn32_x3(
       split_bf16x8(__builtin_bit_cast(u32x4, sc[0]), __builtin_bit_cast(u32x4, sc[1]), ph, plo);
 #pragma unroll
       for (int db = 0; db < 2; ++db) {
-        const char* vr = Vt + ((size_t)(16 * db + ql) * vst + kc + 4 * g) * 2;
-        const uint64_t a0 = *(const uint64_t*)vr, a1 = *(const uint64_t*)(vr + 32);
-        const uint64_t b0 = *(const uint64_t*)(vr + vplane), b1 = *(const uint64_t*)(vr + vplane + 32);
+        const int d = 16 * db + ql;
+        const char* vrow = Vt + (size_t)d * vst * 2;
+        // hi / lo plane columns under the staging's swizzle
+        const int sh = 4 * (((d >> 3) & 3) + 4 * hh), sl = sh + 16 * HG;
+        const int c0 = (kc + 4 * g) ^ sh, c1 = (kc + 16 + 4 * g) ^ sh;
+        const int e0 = (kc + 4 * g) ^ sl, e1 = (kc + 16 + 4 * g) ^ sl;
+        const uint64_t a0 = *(const uint64_t*)(vrow + c0 * 2), a1 = *(const uint64_t*)(vrow + c1 * 2);
+        const uint64_t b0 = *(const uint64_t*)(vrow + vplane + e0 * 2),
+                       b1 = *(const uint64_t*)(vrow + vplane + e1 * 2);
         const bf16x8e vh = __builtin_bit_cast(
             bf16x8e, u32x4{(uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)a1, (uint32_t)(a1 >> 32)});
         const bf16x8e vl = __builtin_bit_cast(
