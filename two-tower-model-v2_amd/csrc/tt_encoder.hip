@@ -1042,7 +1042,7 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
                                                     const float* __restrict__ beta, float eps,
                                                     float* __restrict__ X, int64_t ldx,
                                                     uint16_t* __restrict__ X16, int64_t ldx16,
-                                                    int M, int K) {
+                                                    int M, int K, int st16) {
   static_assert(BM == 128 || BM == 96 || BM == 80, "k_gemm_ln: BM");
   constexpr int WM_N = BM == 80 ? 1 : 2;     // waves along M
   constexpr int WN_N = 8 / WM_N;             // waves along N
@@ -1319,10 +1319,49 @@ __global__ __launch_bounds__(512, 1) void k_gemm_ln(const uint16_t* __restrict__
     for (int i = 0; i < MI; ++i) {
       const int64_t m = m0 + WR * wm + 16 * i + rl;
       if (!full && m >= M) continue;
+      // x16: blocks j = 2 jp, 2 jp + 1 re-paired by v_permlane16_swap so each lane holds 8
+      // consecutive columns -> 16-B stores (hi and lo each for x3i), a full 128-B x3i line per
+      // row and block pair.  Single blocks' 8-B stores (32-B pieces of a line from 4 separate
+      // instructions) made the x16 copy cost as much as the rest of the epilogue: Wo+LN at
+      // 370k rows 709 -> 449 us without them, the f32 x stores ~free.
+      int jbeg = 0;
+      if (st16) {
+#pragma unroll
+        for (int jp = 0; jp < NJ / 2; ++jp) {
+          uint32_t ph[2][2], pw[2][2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const f32x4 y = acc[i][2 * jp + h];
+            ph[h][0] = pack_bf16_hw(y[0], y[1]);
+            ph[h][1] = pack_bf16_hw(y[2], y[3]);
+            if constexpr (SPL) {
+              pw[h][0] = pack_bf16_hw(y[0] - __uint_as_float(ph[h][0] << 16),
+                                      y[1] - __uint_as_float(ph[h][0] & 0xffff0000u));
+              pw[h][1] = pack_bf16_hw(y[2] - __uint_as_float(ph[h][1] << 16),
+                                      y[3] - __uint_as_float(ph[h][1] & 0xffff0000u));
+            }
+          }
+          const auto s0 = __builtin_amdgcn_permlane16_swap(ph[0][0], ph[1][0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(ph[0][1], ph[1][1], false, false);
+          const int n = 16 * NJ * wn + 32 * jp + 16 * (g & 1) + 8 * (g >> 1);
+          if constexpr (SPL) {
+            const auto t0 = __builtin_amdgcn_permlane16_swap(pw[0][0], pw[1][0], false, false);
+            const auto t1 = __builtin_amdgcn_permlane16_swap(pw[0][1], pw[1][1], false, false);
+            uint16_t* o = X16 + m * ldx16 + x3i_col(n);
+            *(u32x4*)o = u32x4{s0[0], s1[0], s0[1], s1[1]};
+            *(u32x4*)(o + 32) = u32x4{t0[0], t1[0], t0[1], t1[1]};
+          } else {
+            *(u32x4*)(X16 + m * ldx16 + n) = u32x4{s0[0], s1[0], s0[1], s1[1]};
+          }
+        }
+        jbeg = NJ / 2 * 2;
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) *(f32x4*)(X + m * ldx + nw0 + 16 * j) = acc[i][j];
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
+        if (j < jbeg) continue;
         const int n = nw0 + 16 * j;
-        *(f32x4*)(X + m * ldx + n) = acc[i][j];
         const uint2 hv = uint2{pack_bf16_hw(acc[i][j][0], acc[i][j][1]),
                                pack_bf16_hw(acc[i][j][2], acc[i][j][3])};
         if constexpr (SPL) {
@@ -2497,16 +2536,18 @@ static int gemm_ln_impl(const uint16_t* A, int64_t lda, const uint16_t* W, int64
     }
   const int ntiles = (int)((M + bm - 1) / bm);
   const int grid = ntiles < ncu ? ntiles : ncu;
+  // 16-B x16 stores (block pairs) when the copy's rows allow them
+  const int st16 = ((uintptr_t)x_bf16 % 16) == 0 && ldx16 % 8 == 0;
   if (x3i) {
     TT_REQUIRE(ldx16 >= 2 * GL_H && ldx16 % 8 == 0, "x3i gemm_ln: x rows x3i interleaved (ldx16 >= 768)");
     auto kern = bm == 80 ? k_gemm_ln<80, true> : bm == 96 ? k_gemm_ln<96, true> : k_gemm_ln<128, true>;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, (hipStream_t)stream, A, lda, W, ldw, bias,
-                       gamma, beta, eps, x, ldx, x_bf16, ldx16, M, K);
+                       gamma, beta, eps, x, ldx, x_bf16, ldx16, M, K, st16);
     return check_launch("tt_gemm_ln_x3i");
   }
   auto kern = bm == 80 ? k_gemm_ln<80> : bm == 96 ? k_gemm_ln<96> : k_gemm_ln<128>;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), 0, (hipStream_t)stream, A, lda, W, ldw, bias,
-                     gamma, beta, eps, x, ldx, x_bf16, ldx16, M, K);
+                     gamma, beta, eps, x, ldx, x_bf16, ldx16, M, K, st16);
   return check_launch("tt_gemm_ln_bf16");
 }
 
