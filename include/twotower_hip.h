@@ -321,7 +321,8 @@ int tt_gemm_x3w(const float* A, int64_t lda, const uint16_t* Wx3, int64_t ld_wx3
  * tt_gemm_ln_x3i: tt_gemm_ln_bf16 in that form (A2 [M, 2K], W2 [384, 2K]) writing x f32 and
  * its x3i rows x2 [M, 768].  tt_attention_varlen_x3i: the encoder's attention over x3i QKV
  * rows qkv2 [T, >= 6H] (a head's Q / K / V = 32-blocks h / heads + h / 2 heads + h), every
- * product as three bf16 MFMAs, f32 softmax; context out2 [T, >= 2H] x3i.  Head dim 32. */
+ * product as three bf16 MFMAs, f32 softmax; context out2 [T, >= 2H] x3i (16-B aligned rows,
+ * ld_out2 % 8 == 0).  Head dim 32. */
 int tt_x3i_weights(const float* W, int64_t ldw, int32_t N, int32_t K, uint16_t* out,
                    int64_t ld_out, void* stream);
 int tt_gemm_x3i(const uint16_t* A2, int64_t lda2, const uint16_t* W2, int64_t ldw2,

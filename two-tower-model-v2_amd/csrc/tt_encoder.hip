@@ -2197,19 +2197,29 @@ __global__ __launch_bounds__(256 * HG) void k_attn32_x3(
     float lsum = lpart + __shfl_xor(lpart, 16, 64);
     lsum += __shfl_xor(lsum, 32, 64);
     // acc[db][v] = O^T[dim 16 db + 4 g + v][query q0 + ql] -> the context, x3i interleaved
-    if (q0 + ql < L) {
-      const float inv = 1.0f / lsum;
+    // the two 16-dim blocks re-paired by v_permlane16_swap (partners share ql, so they are
+    // valid together): lane g then holds dims 16 (g & 1) + 8 (g >> 1) .. + 7 -> one 16-B hi
+    // and one 16-B lo store, a full 128-B x3i line per query row (was 8-B pieces)
+    const float inv = 1.0f / lsum;
+    uint32_t ph[2][2], pw[2][2];
 #pragma unroll
-      for (int db = 0; db < 2; ++db) {
-        const f32x4 o = acc[db] * inv;
-        uint16_t* o16 = out16 + (int64_t)(t0 + q0 + ql) * ldo + 64 * h + 16 * db + 4 * g;
-        const uint2 hv = uint2{pack_bf16_hw(o[0], o[1]), pack_bf16_hw(o[2], o[3])};
-        *(uint2*)o16 = hv;
-        *(uint2*)(o16 + 32) = uint2{pack_bf16_hw(o[0] - __uint_as_float(hv.x << 16),
-                                                o[1] - __uint_as_float(hv.x & 0xffff0000u)),
-                                   pack_bf16_hw(o[2] - __uint_as_float(hv.y << 16),
-                                                o[3] - __uint_as_float(hv.y & 0xffff0000u))};
-      }
+    for (int db = 0; db < 2; ++db) {
+      const f32x4 o = acc[db] * inv;
+      ph[db][0] = pack_bf16_hw(o[0], o[1]);
+      ph[db][1] = pack_bf16_hw(o[2], o[3]);
+      pw[db][0] = pack_bf16_hw(o[0] - __uint_as_float(ph[db][0] << 16),
+                               o[1] - __uint_as_float(ph[db][0] & 0xffff0000u));
+      pw[db][1] = pack_bf16_hw(o[2] - __uint_as_float(ph[db][1] << 16),
+                               o[3] - __uint_as_float(ph[db][1] & 0xffff0000u));
+    }
+    const auto s0 = __builtin_amdgcn_permlane16_swap(ph[0][0], ph[1][0], false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(ph[0][1], ph[1][1], false, false);
+    const auto u0 = __builtin_amdgcn_permlane16_swap(pw[0][0], pw[1][0], false, false);
+    const auto u1 = __builtin_amdgcn_permlane16_swap(pw[0][1], pw[1][1], false, false);
+    if (q0 + ql < L) {
+      uint16_t* o16 = out16 + (int64_t)(t0 + q0 + ql) * ldo + 64 * h + 16 * (g & 1) + 8 * (g >> 1);
+      *(u32x4*)o16 = u32x4{s0[0], s1[0], s0[1], s1[1]};
+      *(u32x4*)(o16 + 32) = u32x4{u0[0], u1[0], u0[1], u1[1]};
     }
   }
 }
@@ -2633,9 +2643,9 @@ extern "C" int tt_attention_varlen_x3i(const uint16_t* qkv2, int64_t ld_qkv2,
   if (H / heads != 32)
     return fail(TT_ERR_UNSUPPORTED, "tt_attention_varlen_x3i: head dim must be 32");
   TT_REQUIRE(ld_qkv2 >= 6 * (int64_t)H && ld_qkv2 % 8 == 0 && H % 8 == 0 &&
-                 ld_out2 >= 2 * (int64_t)H && ld_out2 % 4 == 0 && ((uintptr_t)qkv2 % 16) == 0 &&
-                 ((uintptr_t)out2 % 8) == 0,
-             "qkv x3i rows [T, >= 6H] 16-B aligned; context x3i rows [T, >= 2H]");
+                 ld_out2 >= 2 * (int64_t)H && ld_out2 % 8 == 0 && ((uintptr_t)qkv2 % 16) == 0 &&
+                 ((uintptr_t)out2 % 16) == 0,
+             "qkv x3i rows [T, >= 6H] 16-B aligned; context x3i rows [T, >= 2H] 16-B aligned");
   const size_t smem = attn32_x3_smem(max_len);
   const bool h2 = heads % 2 == 0 && 2 * smem <= 160 * 1024;
   const void* fb = h2 ? (const void*)k_attn32_x3<2> : (const void*)k_attn32_x3<1>;
