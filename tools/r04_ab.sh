@@ -20,5 +20,5 @@ for rep in 1 2; do
   done
 done
 TWOTOWER_HIP_LIB=$V/lib_n.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ab -o run \
-  --output-format csv -- python tools/bench_encoder.py --prec x3 --batch 256 --batches 20 > gpurun_out/prof_ab.log 2>&1 || exit 1
+  --output-format csv -- python tools/bench_encoder.py --prec x3 --batch ${PROF_B:-256} --batches ${PROF_NB:-20} > gpurun_out/prof_ab.log 2>&1 || exit 1
 echo done
