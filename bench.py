@@ -492,6 +492,133 @@ def catalog_10m_768(a, dev, nq=10_000, n=10_000_000):
             "hbm_resident_gb": (x.numel() * 4 + x16.numel() * 2) / 1e9}
 
 
+def train_step_leg(a, dev, steps=20, B=512, N=4, S=20, E=768):
+    """configs[4]'s training step (BASELINE.json configs[4]; trainer.py:161-243 with
+    forward_simplified, two_tower.py:155-218, InfoNCELoss, losses.py:20-79, Adam): item-tower
+    projection head on the positive / 4 negative text embeddings, buyer-tower attention
+    aggregation over S = 20 history rows, InfoNCE (in-batch + explicit negatives, tau 0.07),
+    backward, Adam -- twotower.train.TwoTowerTrainStep, every GEMM on HIP MFMA, in bf16 (GEMM
+    operands) and f32.  Reports ms per step, the MFMA fraction of the matching dense peak, and
+    the bf16 step's loss / gradient deviation from the f32 step on the same weights and batch.
+    Synthetic batch (random-normal text and history embeddings, event-mix weights), random-init
+    weights; projection Dropout active (train mode) in the timed steps, off for the deviation."""
+    import copy
+
+    from twotower.buyer_tower import BuyerTower
+    from twotower.item_tower import ItemTower
+    from twotower.train import TwoTowerTrainStep
+
+    class _Dim:
+        def get_sentence_embedding_dimension(self):
+            return 384
+
+    torch.manual_seed(0)
+    it0 = ItemTower(embedding_dim=E, text_encoder=_Dim())
+    it0.initialize_categorical_embeddings([f"b{i}" for i in range(500)],
+                                          [f"c{i}" for i in range(50)])
+    bt0 = BuyerTower(E, "attention")
+    g = torch.Generator(device=dev).manual_seed(17)
+    items = torch.randn((B, S, E), generator=g, device=dev)
+    w = event_mix(g, (B, S), dev)
+    pos = torch.randn((B, 384), generator=g, device=dev)
+    neg = torch.randn((B, N, 384), generator=g, device=dev)
+    pb, pc = (torch.randint(0, m, (B,), generator=g, device=dev, dtype=torch.int32)
+              for m in (501, 51))
+    nb, nc = (torch.randint(0, m, (B, N), generator=g, device=dev, dtype=torch.int32)
+              for m in (501, 51))
+    batch = (items, w, pos, neg, pb, pc, nb, nc)
+    # flops per step: head forward 2 B(1+N)(512*256 + 256 E), attention MLP 2 B S E 128,
+    # in-batch logits 2 B B E; backward ~2x forward
+    flops = 3.0 * (2 * B * (1 + N) * (512 * 256 + 256 * E) + 2 * B * S * E * 128 + 2 * B * B * E)
+    stream = torch.cuda.current_stream()
+    out = {"workload": f"configs[4] training step: B={B}, {N} negatives, S={S} history rows, "
+                       f"E={E}, attention aggregation, InfoNCE tau 0.07, Adam",
+           "flops_per_step": flops}
+    grads = {}
+    for prec in ("bf16", "f32"):
+        it, bt = copy.deepcopy(it0).to(dev), copy.deepcopy(bt0).to(dev)
+        st = TwoTowerTrainStep(it, bt, lr=1e-4, prec=prec)
+        it.eval()  # deviation: same weights, same batch, no dropout
+        loss, gr = st.forward_backward(*batch)
+        grads[prec] = (float(loss), {k: v.detach().clone() for k, v in gr.items()})
+        it.train()  # as under the reference Trainer (model.train(), trainer.py:167)
+        for _ in range(3):
+            st.step(*batch)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        torch.cuda.synchronize()
+        ev[0].record(stream)
+        for _ in range(steps):
+            st.step(*batch)
+        ev[1].record(stream)
+        torch.cuda.synchronize()
+        ms = ev[0].elapsed_time(ev[1]) / steps
+        peak = BF16_MFMA_PEAK_TFLOPS if prec == "bf16" else F32_MFMA_PEAK_TFLOPS
+        out[prec] = {"ms_per_step": ms, "samples_per_s": B / (ms * 1e-3),
+                     "tflops": flops / (ms * 1e-3) / 1e12,
+                     "mfma_frac": flops / (ms * 1e-3) / 1e12 / peak, "mfma_peak_tflops": peak,
+                     "loss_after": float(st.last_loss)}
+        del st, it, bt
+    l16, g16 = grads["bf16"]
+    l32, g32 = grads["f32"]
+    out["bf16_vs_f32"] = {
+        "loss_abs_diff": abs(l16 - l32), "loss_f32": l32,
+        "grad_max_rel_l2": max(float((g16[k] - g32[k]).norm() / g32[k].norm().clamp_min(1e-30))
+                               for k in g32),
+        "is": "one forward+backward on identical weights and batch, dropout off"}
+    return out
+
+
+def _sig(v, n=4):
+    return float(f"{v:.{n}g}") if isinstance(v, float) else v
+
+
+def summary(result):
+    """Compact digest of every headline number, printed LAST in the JSON line so a reader
+    that keeps only the line's tail (the driver) sees all of them."""
+    s = {"value": _sig(result["value"]), "ms_per_step": _sig(result["ms_per_step"]),
+         "filter_frac": _sig(result["roofline"]["frac"]),
+         "filter_ms": _sig(result["roofline"]["kernel_ms"]),
+         "search_minus_filter_ms": _sig(result["roofline"]["search_ms"]
+                                        - result["roofline"]["kernel_ms"]),
+         "fallbacks": result["roofline"]["fallback_queries_last_step"],
+         "self_check_bad": result["self_check"]["mismatched_queries"]}
+    ma = result.get("mode_a")
+    if ma:
+        s["mode_a_buyers_per_s"] = _sig(ma["value"])
+        s["mode_a_prec"] = ma["encoder_prec"]
+        if "cpu_baseline" in ma:
+            s["mode_a_cpu_buyers_per_s"] = _sig(ma["cpu_baseline"]["value"])
+    sb = result.get("single_buyer_search")
+    if sb:
+        s["one_buyer_ms"] = _sig(sb["ms_per_search"])
+        s["one_buyer_api_ms"] = _sig(sb["api_ms_per_call"])
+        s["one_buyer_api_e2e_ms"] = _sig(sb["api_e2e_ms_per_buyer"])
+        s["one_buyer_api_k1000_ms"] = _sig(sb["api_k1000_ms_per_call"])
+        s["api_calls_per_s_1_vs_4_threads"] = [_sig(sb["api_calls_per_s_1_thread"]),
+                                               _sig(sb["api_calls_per_s_4_threads"])]
+    bs = result.get("batch_sweep", {}).get("by_batch", {})
+    if bs:
+        s["batch_ms"] = {b: _sig(v["ms_per_search"]) for b, v in bs.items()}
+    if "configs1" in result:
+        s["configs1_texts_per_s"] = _sig(result["configs1"]["value"])
+    if "catalog_10m" in result:
+        s["catalog_10m_queries_per_s"] = _sig(result["catalog_10m"]["queries_per_s"])
+    if "catalog_10m_768" in result:
+        c = result["catalog_10m_768"]
+        s["catalog_10m_768_buyers_per_s"] = _sig(c["buyers_per_s"])
+        s["catalog_10m_768_frac"] = _sig(c["full_level_frac_bf16_peak"])
+    if "train_step" in result:
+        t = result["train_step"]
+        s["train_ms"] = {p: _sig(t[p]["ms_per_step"]) for p in ("bf16", "f32")}
+        s["train_mfma_frac"] = {p: _sig(t[p]["mfma_frac"]) for p in ("bf16", "f32")}
+        s["train_bf16_grad_rel"] = _sig(t["bf16_vs_f32"]["grad_max_rel_l2"])
+    cb = result.get("cpu_baseline")
+    if cb:
+        s["cpu_buyers_per_s"] = _sig(cb["value"])
+        s["cpu_cores"] = cb.get("cores")
+    return s
+
+
 CPU_MODE_A_BUYERS = 32
 
 
@@ -539,7 +666,27 @@ def single_buyer_api(a, dev, shard, shard16, n, E, K, bounds, table, hist, w, re
         res_k = vdb.retrieve(q_np, k=1000)
         api_k.append((time.perf_counter() - t0) * 1e3)
     assert len(res_k) == 1000
+    # concurrent callers (the reference's /retrieve under a threaded server): 4 threads, each
+    # call on its own serving slot's stream, vs the same calls from one thread
+    import threading
+
+    def calls(n_calls, t_off=0):
+        for c in range(n_calls):
+            vdb.retrieve(q_np, k=K)
+
+    calls(20)
+    t0 = time.perf_counter()
+    calls(200)
+    one = 200 / (time.perf_counter() - t0)
+    th = [threading.Thread(target=calls, args=(50,)) for _ in range(4)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    four = 200 / (time.perf_counter() - t0)
     return {"api_ms_per_call": statistics.median(api),
+            "api_calls_per_s_1_thread": one, "api_calls_per_s_4_threads": four,
             "api_k1000_ms_per_call": statistics.median(api_k),
             "api_ms_per_call_is": ("VectorDatabase.retrieve(host numpy query, k) -> list of "
                                    "(product_id, score), host to host, median of 21"),
@@ -956,6 +1103,8 @@ def main():
         torch.cuda.empty_cache()
         result["catalog_10m_768"] = catalog_10m_768(a, dev)
         torch.cuda.empty_cache()
+        result["train_step"] = train_step_leg(a, dev)
+        torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         sys.path.insert(0, ROOT)
         from oracle import cpu_baseline
@@ -987,6 +1136,7 @@ def main():
             result["mode_a"]["gpu_over_cpu_single"] = (
                 result["mode_a"]["value"] / result["mode_a"]["cpu_baseline"]["value"])
     if rank == 0:
+        result["summary"] = summary(result)  # last: the line's tail carries every headline
         print(json.dumps(result))
     if world > 1:
         dist.destroy_process_group()

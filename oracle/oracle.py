@@ -148,6 +148,28 @@ def vector_db_normalize(x: np.ndarray) -> np.ndarray:
     return (x / (norms + 1e-8)).astype(np.float32)
 
 
+def weighted_avg_l2_f64(items: np.ndarray, w: np.ndarray) -> np.ndarray:
+    """BuyerTower.weighted_average in float64 (buyer_tower.py:43-68): w / (sum w + 1e-8),
+    weighted sum over the history, F.normalize (x / max(||x||, 1e-12))."""
+    items = np.asarray(items, np.float64)
+    w = np.asarray(w, np.float64)[..., None]
+    z = (items * (w / (w.sum(axis=1, keepdims=True) + 1e-8))).sum(axis=1)
+    return z / np.maximum(np.linalg.norm(z, axis=1, keepdims=True), 1e-12)
+
+
+def attn_agg_l2_f64(items, w, W1, b1, W2, b2) -> np.ndarray:
+    """BuyerTower.attention_aggregation in float64 (buyer_tower.py:70-101, MLP :32-36):
+    scores = Linear(ReLU(Linear(x))) * w, softmax over the history, weighted sum, F.normalize."""
+    items = np.asarray(items, np.float64)
+    f = lambda a: np.asarray(a, np.float64)  # noqa: E731
+    h = np.maximum(items @ f(W1).T + f(b1), 0.0)
+    a = (h @ f(W2).T + f(b2))[..., 0] * f(w)
+    a = np.exp(a - a.max(axis=1, keepdims=True))
+    a /= a.sum(axis=1, keepdims=True)
+    z = (items * a[..., None]).sum(axis=1)
+    return z / np.maximum(np.linalg.norm(z, axis=1, keepdims=True), 1e-12)
+
+
 def flatip_search_f64(db: np.ndarray, q: np.ndarray, k: int):
     """fp64 restatement of IndexFlatIP.search: scores desc, ties -> lower row."""
     s = np.asarray(q, np.float64) @ np.asarray(db, np.float64).T

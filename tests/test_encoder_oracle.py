@@ -31,6 +31,21 @@ def test_bert_oracle_vs_transformers_fixture(golden):
     np.testing.assert_allclose(y.numpy(), g["pooled"], rtol=0, atol=2e-5)
 
 
+def test_bert_oracle_f64_vs_transformers_f64_fixture(golden):
+    """The float64 restatement (the envelope the GPU encoder tests measure against) equals
+    transformers.BertModel run in float64 on the same weights; and the reference's own f32
+    arithmetic sits within the stored f32_vs_f64_max of it."""
+    from oracle import bert_ref
+
+    g = golden("bert.npz")
+    with torch.no_grad():
+        y = bert_ref.bert_mean_pool(_sd(), mbg.CFG, torch.from_numpy(g["ids"]), g["cu_seqlens"],
+                                    dtype=torch.float64)
+    np.testing.assert_allclose(y.numpy(), g["pooled64"], rtol=0, atol=1e-11)
+    dev = np.abs(g["pooled"].astype(np.float64) - g["pooled64"]).max()
+    assert dev == pytest.approx(float(g["f32_vs_f64_max"]), rel=1e-12) and 1e-7 < dev < 1e-5
+
+
 def test_bert_oracle_vs_transformers_live():
     transformers = pytest.importorskip("transformers")
     from oracle import bert_ref

@@ -60,15 +60,16 @@ def _checkpoint(tmp_path, aggregation, with_vocab=True, seed=3):
     return path, enc_sd, sd, it
 
 
-def _oracle_items(enc, enc_sd, sd, pids, meta):
+def _oracle_items(enc, enc_sd, sd, pids, meta, dtype=torch.float32):
     from oracle import bert_ref
 
     it = enc.model.item_tower
     texts = [meta.get(p, {}).get("text", "") for p in pids]
     seqs = it.text_encoder.tokenizer([t if t and t.strip() else " " for t in texts])
     cu = np.concatenate([[0], np.cumsum([len(s) for s in seqs])])
-    te = bert_ref.bert_mean_pool(enc_sd, CFG, torch.tensor([t for s in seqs for t in s]), cu)
-    head = {k[len("item_tower."):]: v for k, v in sd.items()
+    te = bert_ref.bert_mean_pool(enc_sd, CFG, torch.tensor([t for s in seqs for t in s]), cu,
+                                 dtype=dtype)
+    head = {k[len("item_tower."):]: v.to(dtype) for k, v in sd.items()
             if k.startswith("item_tower.") and "text_encoder" not in k}
     bid = [it.brand_vocab.get(meta[p].get("brand"), 0) if meta.get(p, {}).get("brand") else 0
            for p in pids]
@@ -77,20 +78,25 @@ def _oracle_items(enc, enc_sd, sd, pids, meta):
     return bert_ref.item_head(te, head, bid, cid)
 
 
+@pytest.mark.parametrize("prec", ["f32", "x3"])
 @pytest.mark.parametrize("aggregation", ["weighted_avg", "attention"])
-def test_encode_items_and_buyer_vs_oracle(tmp_path, oracle_mod, aggregation):
+def test_encode_items_and_buyer_vs_oracle(tmp_path, oracle_mod, aggregation, prec):
+    """encode_items / encode_buyer (f32 and the default x3 encoder) vs the float64 composition
+    (bert_ref in float64 -> head in float64 -> float64 buyer aggregation): unit rows within 2e-6,
+    the bar of the f32 head against the reference ItemTower fixture."""
+    from oracle import oracle as O
     from twotower.encoder import EmbeddingEncoder
 
     path, enc_sd, sd, _ = _checkpoint(tmp_path, aggregation)
-    enc = EmbeddingEncoder(str(path), config_path=None)
+    enc = EmbeddingEncoder(str(path), config_path=None, prec=prec)
     meta = _metadata()
     with pytest.raises(ValueError, match="Product metadata must be set"):
         enc.encode_items(["p0"])
     enc.set_product_metadata(meta)
     pids = list(meta)
     y = enc.encode_items(pids, batch_size=7)
-    ref = _oracle_items(enc, enc_sd, sd, pids, meta).numpy()
-    np.testing.assert_allclose(y, ref, rtol=0, atol=5e-5)
+    ref = _oracle_items(enc, enc_sd, sd, pids, meta, torch.float64).numpy()
+    np.testing.assert_allclose(y, ref, rtol=0, atol=2e-6)
 
     # encode_buyer: timestamps sort, event weights (aliases, unknown -> 1), unknown product
     inter = [{"product_id": "p3", "event_type": "purchase", "timestamp": "2024-01-03"},
@@ -100,17 +106,17 @@ def test_encode_items_and_buyer_vs_oracle(tmp_path, oracle_mod, aggregation):
     b = enc.encode_buyer(inter)
     order = ["p1", "p7", "p3", "nope"]
     w = np.array([[1, 5, 10, 1]], np.float32)
-    items = _oracle_items(enc, enc_sd, sd, order, meta).numpy()[None]
+    items = _oracle_items(enc, enc_sd, sd, order, meta, torch.float64).numpy()[None]
     if aggregation == "weighted_avg":
-        rb = oracle_mod.weighted_avg_l2(items, w)
+        rb = O.weighted_avg_l2_f64(items, w)
     else:
         a = {k: v.numpy() for k, v in sd.items() if k.startswith("buyer_tower.attention")}
-        rb = oracle_mod.attn_agg_l2(items, w, a["buyer_tower.attention.0.weight"],
-                                    a["buyer_tower.attention.0.bias"],
-                                    a["buyer_tower.attention.2.weight"],
-                                    a["buyer_tower.attention.2.bias"])
+        rb = O.attn_agg_l2_f64(items, w, a["buyer_tower.attention.0.weight"],
+                               a["buyer_tower.attention.0.bias"],
+                               a["buyer_tower.attention.2.weight"],
+                               a["buyer_tower.attention.2.bias"])
     assert b.shape == (384,)
-    np.testing.assert_allclose(b, rb[0], rtol=0, atol=5e-5)
+    np.testing.assert_allclose(b, rb[0], rtol=0, atol=2e-6)
 
 
 def test_history_truncation_and_missing_timestamp(tmp_path):

@@ -744,6 +744,29 @@ def test_bf16_filter_corrupt_key_falls_back(K, oracle_mod, where, n, nq):
         assert fb == (1 if planted else 0), (planted, fb)
 
 
+def test_plant_hook_disarmed_by_a_call_on_another_path(K, oracle_mod):
+    """The hook armed for the single pass (where 2) but spent on a call that takes the
+    multi-level path (nq > 4) is disarmed by that call: a later one-buyer search takes no
+    fallback (an armed hook must not outlive the call it was meant for)."""
+    from twotower import _lib
+
+    rng = np.random.default_rng(77)
+    n, k = 100000, 100
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, 384)).astype(np.float32), 0)
+    q = oracle_mod.l2norm_rows(rng.standard_normal((40, 384)).astype(np.float32), 0)
+    db, qd = dev_rows(x), dev_rows(q)
+    db16 = db.to(torch.bfloat16)
+    b = bounds(K, db, db16, 384)
+    ws = torch.empty(K.filter_workspace_bytes(n, 384, 40, k), dtype=torch.uint8, device="cuda")
+    _lib.check(_lib.lib().tt_debug_plant_bad_row(2, 0), "plant")
+    K.scan_topk_bf16(db, db16, n, 384, qd, k, b, workspace=ws)      # multi-level path
+    assert K.filter_fallback_count(ws, n, 384, 40, k) == 0
+    s, i = K.scan_topk_bf16(db, db16, n, 384, qd[:1], k, b, workspace=ws)  # single pass
+    assert K.filter_fallback_count(ws, n, 384, 1, k) == 0
+    rs, ri = oracle_mod.scan_topk(x, q[:1], k)
+    assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
+
+
 @pytest.mark.parametrize("E,S", [(384, 20), (768, 20), (768, 100), (1024, 20)])
 def test_attn_agg_batched_gemm_form_vs_oracle(K, oracle_mod, E, S):
     """tt_attn_agg_l2_f32_ws (the batched form: first MLP layer on the f32 MFMA GEMM, then the

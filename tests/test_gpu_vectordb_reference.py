@@ -145,8 +145,8 @@ def test_retrieve_endpoint_matches_reference_server(golden):
 
 
 def test_retrieve_serving_path_threads_and_device_path_agree():
-    """VectorDatabase.retrieve / retrieve_batch run the prepared serving path
-    (FlatIPIndex.search_host: bound PreparedSearch, pinned staging, device normalisation).
+    """VectorDatabase.retrieve / retrieve_batch run the serving path (FlatIPIndex.search_host:
+    a serving slot's own stream, pinned staging, device normalisation).
     Results equal the device path (normalize_queries + search) bit for bit, and four threads
     calling retrieve concurrently on one index get the same answers as one thread."""
     import threading
@@ -184,3 +184,56 @@ def test_retrieve_serving_path_threads_and_device_path_agree():
         t.join()
     assert not errs and got == want
     assert vdb.retrieve(q[0], k=n + 5)[:k] == want[0]  # k clamp (:159): all rows, same head
+
+
+def test_retrieve_per_request_k_no_reallocation_and_threads():
+    """/retrieve takes any k in 1..1000 per request (server.py:46).  Cycling k over 20 values x
+    50 calls (k <= 128: the bf16 filter; k > 128: scores + radix select) reuses the serving
+    slot's buffers: no allocation after the first pass, and every answer equals the device
+    path's bit for bit.  Four threads cycling k concurrently (each call on its own slot's
+    stream, the index lock not held across the kernels) get the same answers."""
+    import threading
+
+    import torch
+
+    from twotower import VectorDatabase
+
+    rng = np.random.default_rng(12)
+    n, d = 30000, 384
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    ids = [f"p{i}" for i in range(n)]
+    vdb = VectorDatabase(d)
+    vdb.build_index(x, ids)
+    ks = [1, 2, 5, 10, 16, 20, 33, 50, 64, 99, 100, 127, 128, 129, 200, 256, 500, 512, 999, 1000]
+    q = rng.standard_normal((8, d)).astype(np.float32)
+    want = {}
+    for k in ks:
+        s_dev, i_dev = vdb.search(torch.from_numpy(q).cuda(), k)
+        s_dev, i_dev = s_dev.cpu().numpy(), i_dev.cpu().numpy()
+        want[k] = [[(ids[j], float(v)) for j, v in zip(i_dev[b], s_dev[b])] for b in range(len(q))]
+    for k in ks:  # warm-up pass
+        assert vdb.retrieve(q[0], k=k) == want[k][0]
+    warm = vdb.index.allocations
+    for c in range(50):
+        for j, k in enumerate(ks):
+            b = (c + j) % len(q)
+            assert vdb.retrieve(q[b], k=k) == want[k][b], (c, k)
+    assert vdb.index.allocations == warm, (warm, vdb.index.allocations)
+    errs = []
+
+    def work(t):
+        try:
+            for c in range(10):
+                for j, k in enumerate(ks):
+                    b = (t + c + j) % len(q)
+                    if vdb.retrieve(q[b], k=k) != want[k][b]:
+                        errs.append((t, c, k))
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs[:5]

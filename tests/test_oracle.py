@@ -103,6 +103,22 @@ def test_oracle_attention_vs_reference(oracle_mod, golden, case):
     np.testing.assert_allclose(got, g[case], rtol=0, atol=2e-6)
 
 
+@pytest.mark.parametrize("case", list(gi.BUYER_CASES))
+def test_oracle_buyer_f64_vs_reference(golden, case):
+    """The float64 buyer restatements (the Mode A / encode_buyer envelope tests' reference)
+    against the reference BuyerTower's own float32 outputs: within its f32 rounding."""
+    from oracle import oracle as O
+
+    g = golden("buyer.npz")
+    spec = gi.BUYER_CASES[case]
+    items, w = gi.buyer_inputs(spec)
+    if spec["method"] == "weighted_avg":
+        got = O.weighted_avg_l2_f64(items, w)
+    else:
+        got = O.attn_agg_l2_f64(items, w, *gi.attn_weights(spec))
+    np.testing.assert_allclose(got, g[case], rtol=0, atol=1e-6)
+
+
 def test_oracle_gather_equals_dense(oracle_mod):
     rng = np.random.default_rng(5)
     table = rng.standard_normal((500, 384)).astype(np.float32)

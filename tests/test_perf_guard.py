@@ -43,3 +43,39 @@ def test_configs2_few_flagged_queries_fallback_cost(K):
     t_fb, t_none = timed(q), timed(q2)
     print(f"search with 3 flagged queries {t_fb:.3f} ms, none flagged {t_none:.3f} ms")
     assert t_fb < 1.2 * t_none
+
+
+def test_retrieve_four_threads_beat_one():
+    """Aggregate /retrieve throughput with 4 concurrent callers exceeds one caller's: each call
+    runs on its own serving slot's stream and the index lock is not held across the kernels or
+    the stream synchronisation (FlatIPIndex.search_host)."""
+    import threading
+    import time
+
+    import numpy as np
+
+    from twotower import VectorDatabase
+
+    rng = np.random.default_rng(5)
+    n, d = 1_000_000, 384
+    vdb = VectorDatabase(d)
+    vdb.build_index(rng.standard_normal((n, d)).astype(np.float32), list(range(n)))
+    q = rng.standard_normal(d).astype(np.float32)
+
+    def calls(m):
+        for _ in range(m):
+            vdb.retrieve(q, k=100)
+
+    calls(20)
+    t0 = time.perf_counter()
+    calls(200)
+    one = 200 / (time.perf_counter() - t0)
+    th = [threading.Thread(target=calls, args=(50,)) for _ in range(4)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    four = 200 / (time.perf_counter() - t0)
+    print(f"/retrieve calls/s: 1 thread {one:.0f}, 4 threads {four:.0f}")
+    assert four > one

@@ -3182,12 +3182,12 @@ extern "C" int tt_debug_plant_bad_row(int32_t where, int32_t query) {
   return TT_OK;
 }
 
-extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n,
-                                    int32_t d, int64_t ld_db, int64_t row_base, const float* q,
-                                    int32_t nq, int64_t ld_q, int32_t k, float x_norm_max,
-                                    float x_resid_max, float* out_score, int64_t* out_idx,
-                                    void* workspace, int64_t workspace_bytes, void* stream,
-                                    void* ev_start, void* ev_stop) {
+namespace {
+int scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n, int32_t d,
+                      int64_t ld_db, int64_t row_base, const float* q, int32_t nq, int64_t ld_q,
+                      int32_t k, float x_norm_max, float x_resid_max, float* out_score,
+                      int64_t* out_idx, void* workspace, int64_t workspace_bytes, void* stream,
+                      void* ev_start, void* ev_stop) {
   TT_REQUIRE(nq >= 0, "nq < 0");
   if (nq == 0) return TT_OK;
   int ep;
@@ -3299,6 +3299,22 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
     if ((rc = check_launch("k_debug_plant"))) return rc;
   }
   return filter_finish(w, db, n, d, ld_db, row_base, q, nq, ld_q, k, ep, out_score, out_idx, st);
+}
+}  // namespace
+
+extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n,
+                                    int32_t d, int64_t ld_db, int64_t row_base, const float* q,
+                                    int32_t nq, int64_t ld_q, int32_t k, float x_norm_max,
+                                    float x_resid_max, float* out_score, int64_t* out_idx,
+                                    void* workspace, int64_t workspace_bytes, void* stream,
+                                    void* ev_start, void* ev_stop) {
+  const int rc = scan_topk_bf16f32(db, db_bf16, n, d, ld_db, row_base, q, nq, ld_q, k, x_norm_max,
+                                   x_resid_max, out_score, out_idx, workspace, workspace_bytes,
+                                   stream, ev_start, ev_stop);
+  // the test hook is armed for ONE call: disarmed whichever path (or early return) the call took,
+  // so it can never corrupt a later search on this thread
+  g_plant_where = 0;
+  return rc;
 }
 
 // ------------------------------------------------------------------ sharded (multi-GPU)

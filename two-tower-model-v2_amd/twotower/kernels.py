@@ -114,7 +114,7 @@ SCAN_KMAX = 1024  # tt_scan_topk_f32's / tt_scan_topk_select_f32's largest k; la
 
 
 def scan_topk_large(db: torch.Tensor, n: int, d: int, q: torch.Tensor, k: int, row_base: int = 0,
-                    chunk_elems: int = 1 << 27):
+                    chunk_elems: int = 1 << 25):
     """Generic exact top-k: any k (faiss' IndexFlatIP takes any k <= ntotal; the reference's
     /retrieve caps k at 1000, server.py:46, VectorDatabase.retrieve does not) and any dimension
     (rows past 768 dims, which the scan kernels do not instantiate; vector_db.py:13,48 accept
@@ -123,7 +123,8 @@ def scan_topk_large(db: torch.Tensor, n: int, d: int, q: torch.Tensor, k: int, r
     then a top-k over 64-bit keys (orderable(score) << 32 | ~row: score descending, ties to
     the lower row, exactly the scan's order).  NaN scores are never returned: their slots read
     (-inf, -1) at the end of the list, as in the scan.  Queries in chunks of at most
-    chunk_elems scores.  Not the serving path (k <= 128, d <= 768 take the bf16 filter)."""
+    chunk_elems scores: a chunk holds its f32 scores plus ~4 int64 temporaries of the same
+    shape (bits, orderable, key, the where result), ~36 B per score -- 1.2 GB at 2^25.  Not the serving path (k <= 128, d <= 768 take the bf16 filter)."""
     _check_2d(db, "db")
     _check_2d(q, "q")
     nq, ep = q.shape[0], db.shape[1]

@@ -12,6 +12,8 @@ fma order), sorted descending, ties to the lower row.
 """
 from __future__ import annotations
 
+import collections
+import ctypes
 import json
 import struct
 import threading
@@ -45,24 +47,31 @@ class FlatIPIndex:
         self.bounds = (0.0, 0.0)
         self.ntotal = 0
         self._ws = _lib.StreamWorkspaces(4)  # search_device's workspace, one per HIP stream
-        # host searches (the /retrieve path): per (nq, k, index state, stream) a bound
-        # kernels.PreparedSearch (k <= 128, nq <= 256) with its device query buffer and pinned
-        # host staging, so one buyer costs one H2D copy, the search launches and one D2H copy
-        self._prepared = {}
-        # shared state (prepared searches, staging buffers, workspaces) is guarded by one lock:
-        # faiss' search is re-entrant, and the reference's /retrieve may be called from several
-        # threads (server.py:212-244)
+        # host searches (the /retrieve path, FlatIPIndex.search_host): serving slots, each with
+        # its own HIP stream, device query / output buffers, pinned host staging and filter
+        # workspace, checked out by ONE call at a time and grown only when a call needs more,
+        # so any k in 1..1000 per request (server.py:46) reuses them, and concurrent callers
+        # run on separate streams; pooled per nq bucket (power of two), least recently used out
+        self._slots = collections.OrderedDict()  # nq bucket -> [free _ServingSlot, ...]
+        self.max_slots = 16
+        self.allocations = 0  # serving-slot buffer (re)allocations: a test / ops counter
+        # the slot pool and the catalog state are guarded by one lock, held only to check a
+        # slot out / in and to read the catalog state: faiss' search is re-entrant, and the
+        # reference's /retrieve may be called from several threads (server.py:212-244)
         self._lock = threading.RLock()
 
     def _append(self, rows: torch.Tensor, rows16: torch.Tensor) -> None:
+        # bounds first: they only grow (max-combined), so a search snapshot taken between the
+        # two updates pairs larger bounds with the old rows -- conservative, still exact
         if rows.shape[0]:  # build-time statistic over the new rows (max-combined)
             kernels.bf16_image_bounds(rows, rows16, self.d, out2=self._bounds_dev)
             self.bounds = tuple(self._bounds_dev.tolist())
         if self.ntotal:
             rows = torch.cat([self.xb[: self.ntotal], rows])
             rows16 = torch.cat([self.xb16[: self.ntotal], rows16])
-        self.xb, self.xb16 = rows, rows16
-        self.ntotal = rows.shape[0]
+        with self._lock:  # searches read (xb, xb16, ntotal, bounds) as one snapshot
+            self.xb, self.xb16 = rows, rows16
+            self.ntotal = rows.shape[0]
 
     # faiss-style add of ALREADY-normalised float32 rows (host or device)
     def add(self, x) -> None:
@@ -117,41 +126,51 @@ class FlatIPIndex:
             return kernels.scan_topk(self.xb, self.ntotal, self.d, q, k,
                                      row_base=self.row_base, workspace=ws)
 
+    def _checkout(self, nq: int) -> "_ServingSlot":
+        bucket = 1 << max(0, (nq - 1).bit_length())
+        with self._lock:
+            free = self._slots.get(bucket)
+            if free:
+                self._slots.move_to_end(bucket)
+                return free.pop()
+        return _ServingSlot(self, bucket)
+
+    def _checkin(self, slot: "_ServingSlot") -> None:
+        with self._lock:
+            self._slots.setdefault(slot.bucket, []).append(slot)
+            self._slots.move_to_end(slot.bucket)
+            while sum(len(v) for v in self._slots.values()) > self.max_slots:
+                b, v = next(iter(self._slots.items()))
+                v.pop(0)
+                if not v:
+                    del self._slots[b]
+
     def search_host(self, x: np.ndarray, k: int, normalize: bool = False):
         """Host float32 [nq, d] queries -> host (D [nq,k] f32, I [nq,k] i64).  normalize=True
         first applies the reference's q/(||q||+1e-8) on the device (vector_db.py:152-153,
-        189-190).  The serving path of VectorDatabase.retrieve / retrieve_batch."""
+        189-190).  The serving path of VectorDatabase.retrieve / retrieve_batch: one H2D copy,
+        the device normalisation, the search, one D2H copy, on a serving slot's own stream; the
+        index lock is held only to check the slot out and to read the catalog state, not across
+        the kernels or the stream synchronisation."""
         x = np.ascontiguousarray(x, dtype=np.float32)
         if x.ndim != 2 or x.shape[1] != self.d:
             raise ValueError(f"search: expected [nq, {self.d}] float32 queries")
         nq = x.shape[0]
-        with self._lock:  # staging buffers / prepared outputs are reused until copied out
-            key = (nq, k, self.ntotal, self.xb.data_ptr(), _lib.stream_ptr())
-            ent = self._prepared.get(key)
-            if ent is None:
-                if len(self._prepared) >= 8:
-                    self._prepared.clear()
-                pin = torch.cuda.is_available()
-                q = torch.zeros((nq, self.ep), dtype=torch.float32, device=self.device)
-                qh = torch.empty((nq, self.d), dtype=torch.float32, pin_memory=pin)
-                outh = (torch.empty((nq, k), dtype=torch.float32, pin_memory=pin),
-                        torch.empty((nq, k), dtype=torch.int64, pin_memory=pin))
-                ps = None
-                if (self.scan_dim and 1 <= nq <= 256
-                        and 1 <= k <= min(self.ntotal, kernels.FILTER_KMAX)):
-                    ps = kernels.PreparedSearch(self.xb, self.xb16, self.ntotal, self.d, nq, k,
-                                                self.bounds, self.row_base)
-                ent = self._prepared[key] = (q, qh, outh, ps)
-            q, qh, outh, ps = ent
-            qh.numpy()[...] = x
-            q[:, : self.d].copy_(qh, non_blocking=True)
+        with self._lock:  # one consistent catalog state for this call
+            state = (self.xb, self.xb16, self.ntotal, self.bounds)
+        if nq == 0 or not (1 <= k <= state[2]):
+            q = torch.zeros((nq, self.ep), dtype=torch.float32, device=self.device)
+            q[:, : self.d] = torch.from_numpy(x).to(self.device)
             if normalize:
                 kernels.l2norm_rows(q, self.d, _lib.TT_NORM_ADD_EPS, out=q)
-            s, i = ps(q) if ps is not None else self.search_device(q, k)
-            outh[0].copy_(s, non_blocking=True)
-            outh[1].copy_(i, non_blocking=True)
+            s, i = self.search_device(q, k)
             torch.cuda.current_stream().synchronize()
-            return outh[0].numpy().copy(), outh[1].numpy().copy()
+            return s.cpu().numpy(), i.cpu().numpy()
+        slot = self._checkout(nq)
+        try:
+            return slot.run(x, k, normalize, state)
+        finally:
+            self._checkin(slot)
 
     def search(self, x: np.ndarray, k: int):
         """faiss signature: float32 [nq, d] host queries -> (D [nq,k] f32, I [nq,k] i64) host."""
@@ -159,6 +178,91 @@ class FlatIPIndex:
 
     def reconstruct(self, i: int) -> np.ndarray:
         return self.xb[i, : self.d].cpu().numpy()
+
+
+class _ServingSlot:
+    """One in-flight host search's device state (FlatIPIndex.search_host): a HIP stream, the
+    device query rows [bucket, ep], flat device / pinned host outputs, pinned query staging and
+    one workspace for the bf16 filter (k <= 128) and the radix-select path (k <= 1024).  Every
+    buffer grows to the largest (nq, k) it has served and is then reused, so a client mixing k
+    values causes no allocation after warm-up.  Used by one call at a time (checked out)."""
+
+    KCAP = 1024  # outputs sized for the /retrieve cap (k <= 1000, server.py:46) up front
+
+    def __init__(self, index: FlatIPIndex, bucket: int):
+        self.ix, self.bucket = index, bucket
+        dev = index.device
+        self.stream = torch.cuda.Stream(device=dev)
+        pin = torch.cuda.is_available()
+        self.q = torch.zeros((bucket, index.ep), dtype=torch.float32, device=dev)
+        self.qh = torch.empty((bucket, index.d), dtype=torch.float32, pin_memory=pin)
+        kc = self.KCAP if bucket <= 256 else 128
+        self._outs(kc, pin)
+        self.ws = torch.empty(0, dtype=torch.uint8, device=dev)
+        self.ws_need = {}  # (n, nq, k, kind) -> workspace bytes (memoised size queries)
+        index.allocations += 1
+
+    def _outs(self, kc: int, pin: bool) -> None:
+        dev = self.ix.device
+        self.kc = kc
+        self.s = torch.empty(self.bucket * kc, dtype=torch.float32, device=dev)
+        self.i = torch.empty(self.bucket * kc, dtype=torch.int64, device=dev)
+        self.sh = torch.empty(self.bucket * kc, dtype=torch.float32, pin_memory=pin)
+        self.ih = torch.empty(self.bucket * kc, dtype=torch.int64, pin_memory=pin)
+
+    def _workspace(self, n: int, nq: int, k: int, kind: str) -> torch.Tensor:
+        key = (n, nq, k, kind)
+        need = self.ws_need.get(key)
+        if need is None:
+            need = (kernels.filter_workspace_bytes(n, self.ix.d, nq, k) if kind == "bf16"
+                    else kernels.select_workspace_bytes(n, nq, k))
+            if len(self.ws_need) > 256:
+                self.ws_need.clear()
+            self.ws_need[key] = need
+        if self.ws.numel() < need:
+            self.ws = torch.empty(need, dtype=torch.uint8, device=self.ix.device)
+            self.ix.allocations += 1
+        return self.ws
+
+    def run(self, x: np.ndarray, k: int, normalize: bool, state):
+        ix = self.ix
+        xb, xb16, n, bounds = state
+        nq, d = x.shape
+        if k > self.kc:
+            self._outs(k, torch.cuda.is_available())
+            ix.allocations += 1
+        q = self.q[:nq]
+        # ordered after the caller's stream (e.g. an add() whose kernels may still run there)
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream):
+            self.qh[:nq].numpy()[...] = x
+            q[:, :d].copy_(self.qh[:nq], non_blocking=True)
+            if normalize:
+                kernels.l2norm_rows(q, d, _lib.TT_NORM_ADD_EPS, out=q)
+            s, i = self.s[: nq * k].view(nq, k), self.i[: nq * k].view(nq, k)
+            st = self.stream.cuda_stream
+            if ix.scan_dim and k <= kernels.FILTER_KMAX:
+                ws = self._workspace(n, nq, k, "bf16")
+                check = _lib.lib().tt_scan_topk_bf16f32(
+                    ctypes.c_void_p(xb.data_ptr()), ctypes.c_void_p(xb16.data_ptr()), n, d,
+                    xb.stride(0), ix.row_base, ctypes.c_void_p(q.data_ptr()), nq, q.stride(0),
+                    k, ctypes.c_float(bounds[0]), ctypes.c_float(bounds[1]),
+                    ctypes.c_void_p(s.data_ptr()), ctypes.c_void_p(i.data_ptr()),
+                    ctypes.c_void_p(ws.data_ptr()), ws.numel(), ctypes.c_void_p(st), None, None)
+                _lib.check(check, "tt_scan_topk_bf16f32")
+            elif ix.scan_dim and k <= kernels.SCAN_KMAX:
+                ws = self._workspace(n, nq, k, "select")
+                kernels.scan_topk_select(xb, n, d, q, k, row_base=ix.row_base, workspace=ws,
+                                         out=(s, i))
+            else:  # k > 1024 or d > 768: the generic exact path (allocates; not the serving k)
+                s2, i2 = kernels.scan_topk_large(xb, n, d, q, k, row_base=ix.row_base)
+                s.copy_(s2)
+                i.copy_(i2)
+            sh, ih = self.sh[: nq * k], self.ih[: nq * k]
+            sh.copy_(s.view(-1), non_blocking=True)
+            ih.copy_(i.view(-1), non_blocking=True)
+        self.stream.synchronize()
+        return sh.numpy().reshape(nq, k).copy(), ih.numpy().reshape(nq, k).copy()
 
 
 # ------------------------------------------------------------------ index file format
