@@ -273,12 +273,25 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #ifndef TT_RR_NT
 #define TT_RR_NT 0  // k_rerank: band rows loaded non-temporal (A/B: re-rank 0.65 -> 1.75 ms)
 #endif
+#ifndef TT_RR_ONEPHASE
+#define TT_RR_ONEPHASE 0  // k_rerank: score the whole band in one phase (A/B)
+#endif
 #ifndef TT_EXP_MAXONLY
 #define TT_EXP_MAXONLY 0  // per-block max + ballot only (no per-slot scan)
 #endif
+#ifndef TT_EXP_BLKTIME
+// timing only: k_filter_ring<EP, 1> records per block (start, end wall clock, hardware id,
+// XCC id, logical block) into g_blktime (tt_debug_blktimes): the launch's per-CU timeline
+#define TT_EXP_BLKTIME 0
+#endif
+#if TT_EXP_BLKTIME
+constexpr int BLKTIME_MAX = 8192;
+__device__ unsigned long long g_blktime[BLKTIME_MAX * 4];
+#endif
 TT_CHECK_EXP(TT_EXP_NOSEL || TT_EXP_NOWRITE || TT_EXP_MAXONLY ||
                  TT_EXP_SEL_STOP || TT_EXP_SEL_TIMING || TT_EXP_FINAL_STOP ||
-                 TT_EXP_FINAL_TIMING || TT_EXP_TM_STATS || TT_EXP_TM_SLOTS != 4,
+                 TT_EXP_FINAL_TIMING || TT_EXP_TM_STATS || TT_EXP_TM_SLOTS != 4 ||
+                 TT_EXP_BLKTIME,
              "TT_EXP_* (results wrong / printf / untested schedule)");
 // The batched full level at E = 512 / 768 (configs[4]'s k_filter_ring<768, 1>) keeps TWO
 // 16-query blocks per wave (192 fragment registers at E = 768) with one k-step of fragment
@@ -306,7 +319,8 @@ TT_CHECK_EXP(TT_EXP_NOSEL || TT_EXP_NOWRITE || TT_EXP_MAXONLY ||
 TT_CHECK_EXP(TT_RING_HALF || TT_RING_QB4 || TT_RING_W4QB || TT_RING_ASM ||
                  TT_RING_QB_WIDE != 2 || TT_RING_FD_WIDE != 1 || TT_RING_PD_WIDE != 2 ||
                  TT_EXP_NOIDLE || TT_EXP_PRIO ||
-                 TT_RING_NT != 1 || TT_RR_STAGED != 1 || TT_RR_PF != 1 || TT_RR_NT,
+                 TT_RING_NT != 1 || TT_RR_STAGED != 1 || TT_RR_PF != 1 || TT_RR_NT ||
+                 TT_RR_ONEPHASE,
              "a non-default ring/re-rank schedule (untested by the GPU suite)");
 #ifndef TT_RING_PD
 // ring tiles in flight; 4 (5 slots, the pool's flush mark lowered to fit LDS): 6.33 -> 6.49 ms
@@ -495,6 +509,25 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   const int lb = xcd_remap(blockIdx.x, gridDim.x);
   const int slab = lb / n_qt, qt = lb % n_qt;
   const int qbase = qt * QPB + w * QPW;
+#if TT_EXP_BLKTIME
+  const unsigned long long blk_t0 = wall_clock64();
+  struct BlkTimeEnd {  // end stamp when the block's last wave leaves (any return path)
+    unsigned long long t0;
+    int lb;
+    __device__ ~BlkTimeEnd() {
+      if (LVL != 1 || blockIdx.x >= BLKTIME_MAX) return;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        unsigned long long* o = g_blktime + 4 * blockIdx.x;
+        o[0] = t0;
+        o[1] = wall_clock64();
+        o[2] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+        o[3] = ((unsigned long long)(unsigned)lb << 32) |
+               (unsigned)__builtin_amdgcn_s_getreg((3 << 11) | 20);            // XCC_ID
+      }
+    }
+  } blk_end{blk_t0, lb};
+#endif
 
   bf16x8 qf[QB][KS];
   float th[QB];
@@ -1055,7 +1088,7 @@ __global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict_
                                                      int mode, float* __restrict__ theta_out,
                                                      float* __restrict__ aref,
                                                      uint64_t* __restrict__ band,
-                                                     int* __restrict__ band_n,
+                                                     int* __restrict__ band_n, int* __restrict__ band_p1,
                                                      int* __restrict__ flags, int* qsel,
                                                      int* qsel_n, int nq,
                                                      const float* __restrict__ stats,
@@ -1216,6 +1249,7 @@ __global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict_
   if (lane == 0) {
     if (nb > BAND_CAP) flag_query(qid, flags, qsel, qsel_n);
     else band_n[qid] = nb;
+    band_p1[qid] = -1;  // unordered band: k_rerank scores it in one phase
   }
 }
 
@@ -1232,7 +1266,7 @@ __global__ __launch_bounds__(256) void k_select_reg(const uint64_t* __restrict__
                                                     int mode, float* __restrict__ theta_out,
                                                     float* __restrict__ aref,
                                                     uint64_t* __restrict__ band,
-                                                    int* __restrict__ band_n,
+                                                    int* __restrict__ band_n, int* __restrict__ band_p1,
                                                     int* __restrict__ flags, int* qsel,
                                                     int* qsel_n, int nq,
                                                     const float* __restrict__ stats,
@@ -1440,16 +1474,24 @@ __global__ __launch_bounds__(256) void k_select_reg(const uint64_t* __restrict__
   const float thr = A - eps2[qid];
   int nb = 0;
   uint64_t* qb = band + (int64_t)qid * BAND_CAP;
+  // the band in two parts: first the rows with a >= A_k (the k largest a, plus ties: P1), then
+  // the other rows with a >= A_k - 2 eps; k_rerank scores P1 first and keeps from the rest only
+  // rows that can still reach the k-th exact score (two-phase re-rank)
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    if (i < ni) {
-      const bool in = lane + 64 * i < total && key_float(hv[i]) >= thr;
-      const uint64_t bm = __ballot(in);
-      const int pos = nb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
-                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
-      if (in && pos < BAND_CAP) qb[pos] = ((uint64_t)hv[i] << 32) | lo[i];
-      nb += __popcll(bm);
+  for (int part = 0; part < 2; ++part) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      if (i < ni) {
+        const bool in = lane + 64 * i < total &&
+                        (part == 0 ? hv[i] >= T : hv[i] < T && key_float(hv[i]) >= thr);
+        const uint64_t bm = __ballot(in);
+        const int pos = nb + (int)__builtin_amdgcn_mbcnt_hi(
+                                 (uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+        if (in && pos < BAND_CAP) qb[pos] = ((uint64_t)hv[i] << 32) | lo[i];
+        nb += __popcll(bm);
+      }
     }
+    if (part == 0 && lane == 0) band_p1[qid] = nb;
   }
 #if TT_EXP_SEL_TIMING
   tstamp[ntst++] = wall_clock64();
@@ -2315,15 +2357,22 @@ __global__ void k_probe_cut(const int* __restrict__ pcount, const float* __restr
 }
 
 // --------------------------------------------------------------------------- rerank
+// Two-phase re-rank (band_p1 >= 0: k_select_reg stored the band's P1 = {a >= A_k}, k rows plus
+// ties, first).  Phase 1 scores P1 exactly; s1 = their smallest exact score is a lower bound of
+// the final k-th score s_k (P1 holds >= k rows).  A row of the rest of the band can only enter
+// the top k if s >= s_k >= s1, and s <= a + eps, so phase 2 scores only the rows with
+// a + eps >= s1 (a + eps < s1 means s < s1 <= s_k: strictly below, ties included).  In practice
+// s1 ~ A_k, so phase 2 keeps the rows within ~eps of A_k instead of 2 eps: ~180 -> ~135 exact
+// rows per query at 1M x 384 (tools/band_analysis.py), a quarter less HBM gather.
 template <int EP>
 __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, int64_t ld,
                                                 const float* __restrict__ q, int64_t ldq,
                                                 const uint64_t* __restrict__ band,
-                                                const int* __restrict__ band_n, int* flags,
+                                                const int* __restrict__ band_n,
+                                                const int* __restrict__ band_p1,
+                                                const float* __restrict__ eps2, int* flags,
                                                 int* qsel, int* qsel_n, int64_t n_rows, int k,
-                                                int64_t row_base,
-                                                const float* __restrict__ cut,
-                                                float* __restrict__ out_s,
+                                                int64_t row_base, float* __restrict__ out_s,
                                                 int64_t* __restrict__ out_i) {
   __shared__ uint64_t buf[BAND_CAP];
   // A decoded candidate row >= n_rows (a corrupted list or band entry) is never read: the row
@@ -2331,39 +2380,34 @@ __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, in
   bool bad_row = false;
   __shared__ __attribute__((aligned(16))) float qs[EP];
   __shared__ int nkeep;
+  __shared__ unsigned long long kmin;
   const int qid = blockIdx.x;
   if (flags[qid]) return;  // served by the exact fallback
-  int nb = band_n[qid];
+  const int nb = band_n[qid];
+  const int p1 = band_p1 != nullptr ? band_p1[qid] : -1;
   const uint64_t* qband = band + (int64_t)qid * BAND_CAP;
   for (int i = threadIdx.x; i < EP; i += blockDim.x) qs[i] = q[(int64_t)qid * ldq + i];
-  if (cut) {  // sharded: keep band rows with a >= cut[q] (unordered; sorted below)
-    const float c = cut[qid];
-    if (threadIdx.x == 0) nkeep = 0;
-    __syncthreads();
-    for (int e = threadIdx.x; e < nb; e += blockDim.x) {
-      const uint64_t key = qband[e];
-      if (key_float((uint32_t)(key >> 32)) >= c) buf[atomicAdd(&nkeep, 1)] = key;
-    }
-    __syncthreads();
-    nb = nkeep;
-    qband = buf;
+  if (threadIdx.x == 0) {
+    nkeep = 0;
+    kmin = ~0ull;
   }
   __syncthreads();
+  // exact keys of src[0 .. cnt) into dst[0 .. cnt) (dst may alias src element for element)
 #if TT_RR_STAGED
-  // Each wave takes 64 band rows at a time and fetches them 64 dimensions (256 B per row) per
+  // Each wave takes 64 rows at a time and fetches them 64 dimensions (256 B per row) per
   // chunk: 16 lanes per row, 4 rows per wave-instruction, 16 instructions in flight (the next
   // chunk is loaded while this one is summed).  The chunk goes through a wave-private LDS
   // stage (16-B pieces XOR-swizzled by row: conflict-free writes and reads), and lane j then
   // runs row j's canonical FMA chain over those 64 dimensions -- the same order as below.
   // (Thread-per-row loads put 64 rows into every wave-instruction.)
-  {
-    __shared__ __attribute__((aligned(16))) char stage[4][64 * 256];
+  __shared__ __attribute__((aligned(16))) char stage[4][64 * 256];
+  auto score = [&](const uint64_t* src, uint64_t* dst, int cnt) __attribute__((always_inline)) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     char* st = stage[w];
     const int sub = lane >> 4, piece = lane & 15;
-    for (int e0 = 64 * w; e0 < nb; e0 += 256) {
+    for (int e0 = 64 * w; e0 < cnt; e0 += 256) {
       const int ej = e0 + lane;
-      uint32_t rj = key_row(qband[ej < nb ? ej : e0]);
+      uint32_t rj = key_row(src[ej < cnt ? ej : e0]);
       if ((int64_t)rj >= n_rows) {
         bad_row = true;
         rj = 0;
@@ -2425,52 +2469,70 @@ __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, in
         }
       }
       asm volatile("" ::: "memory");
-      if (ej < nb) buf[ej] = acc != acc ? 0ull : make_key(acc, rj);
+      if (ej < cnt) dst[ej] = acc != acc ? 0ull : make_key(acc, rj);
     }
-  }
+  };
 #else
-  for (int e = threadIdx.x; e < nb; e += blockDim.x) {
-    uint32_t r = key_row(qband[e]);
-    if ((int64_t)r >= n_rows) {
-      bad_row = true;
-      r = 0;
-    }
-    const f32x4* xr = (const f32x4*)(db + (int64_t)r * ld);
-    float acc = 0.0f;
-#pragma unroll 4
-    for (int t = 0; t < EP / 16; ++t) {
-#if TT_RR_NT
-      const f32x4 x0 = __builtin_nontemporal_load(xr + 4 * t + 0),
-                  x1 = __builtin_nontemporal_load(xr + 4 * t + 1),
-                  x2 = __builtin_nontemporal_load(xr + 4 * t + 2),
-                  x3 = __builtin_nontemporal_load(xr + 4 * t + 3);
-#else
-      const f32x4 x0 = xr[4 * t + 0], x1 = xr[4 * t + 1], x2 = xr[4 * t + 2], x3 = xr[4 * t + 3];
-#endif
-      const float* qt = qs + 16 * t;
-      // canonical order: for i: for g: d = 16t + 4g + i
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        acc = fmaf(x0[i], qt[0 + i], acc);
-        acc = fmaf(x1[i], qt[4 + i], acc);
-        acc = fmaf(x2[i], qt[8 + i], acc);
-        acc = fmaf(x3[i], qt[12 + i], acc);
+  auto score = [&](const uint64_t* src, uint64_t* dst, int cnt) __attribute__((always_inline)) {
+    for (int e = threadIdx.x; e < cnt; e += blockDim.x) {
+      uint32_t r = key_row(src[e]);
+      if ((int64_t)r >= n_rows) {
+        bad_row = true;
+        r = 0;
       }
+      const f32x4* xr = (const f32x4*)(db + (int64_t)r * ld);
+      float acc = 0.0f;
+#pragma unroll 4
+      for (int t = 0; t < EP / 16; ++t) {
+        const f32x4 x0 = xr[4 * t + 0], x1 = xr[4 * t + 1], x2 = xr[4 * t + 2], x3 = xr[4 * t + 3];
+        const float* qt = qs + 16 * t;
+        // canonical order: for i: for g: d = 16t + 4g + i
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc = fmaf(x0[i], qt[0 + i], acc);
+          acc = fmaf(x1[i], qt[4 + i], acc);
+          acc = fmaf(x2[i], qt[8 + i], acc);
+          acc = fmaf(x3[i], qt[12 + i], acc);
+        }
+      }
+      dst[e] = acc != acc ? 0ull : make_key(acc, r);
     }
-    buf[e] = acc != acc ? 0ull : make_key(acc, r);
-  }
+  };
 #endif
+  int nsc = nb;  // rows scored into buf[0 .. nsc)
+  if (p1 >= 0 && p1 <= nb && !TT_RR_ONEPHASE) {
+    score(qband, buf, p1);  // phase 1: P1
+    __syncthreads();
+    // s1 = the smallest exact P1 key (a NaN score keys 0: then s1 = -inf, all rows stay)
+    unsigned long long m = ~0ull;
+    for (int i = threadIdx.x; i < p1; i += blockDim.x) m = min(m, (unsigned long long)buf[i]);
+    for (int o = 32; o > 0; o >>= 1) m = min(m, (unsigned long long)__shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) atomicMin(&kmin, m);
+    __syncthreads();
+    const float s1 = kmin == 0ull || kmin == ~0ull ? -__builtin_huge_valf() : key_score(kmin);
+    const float eps = 0.5f * eps2[qid];  // eps2 = 2 eps (x1.001)
+    // phase 2: the rest of the band, rows with a + eps >= s1, compacted after P1
+    for (int e = p1 + threadIdx.x; e < nb; e += blockDim.x) {
+      const uint64_t key = qband[e];
+      if (key_float((uint32_t)(key >> 32)) + eps >= s1) buf[p1 + atomicAdd(&nkeep, 1)] = key;
+    }
+    __syncthreads();
+    nsc = p1 + nkeep;
+    score(buf + p1, buf + p1, nsc - p1);
+  } else {
+    score(qband, buf, nb);
+  }
   if (__syncthreads_or(bad_row)) {
     if (threadIdx.x == 0) flag_query(qid, flags, qsel, qsel_n);
     return;
   }
-  const int np = pow2_at_least(nb);
-  for (int i = nb + threadIdx.x; i < np; i += blockDim.x) buf[i] = 0ull;
+  const int np = pow2_at_least(nsc);
+  for (int i = nsc + threadIdx.x; i < np; i += blockDim.x) buf[i] = 0ull;
   block_sort_desc(buf, np);
   for (int i = threadIdx.x; i < k; i += blockDim.x) {
     float s = -__builtin_huge_valf();
     int64_t ix = -1;
-    if (i < nb && buf[i] != 0ull) {
+    if (i < nsc && buf[i] != 0ull) {
       s = key_score(buf[i]);
       ix = row_base + (int64_t)key_row(buf[i]);
     }
@@ -2870,6 +2932,7 @@ struct FilterWs {
   float* cut;
   uint64_t* band;
   int* band_n;
+  int* band_p1;  // rows of the band with a >= A_k, stored first (k_select_reg); -1: unordered
   int* flags;  // flags[nq], qsel[nq], qsel_n[1], done[nq] are contiguous: the per-query
   int* qsel;   // init zeroes flags[qi] and qsel_n[1 + qi] (= done[qi], the fused fallback
   int* qsel_n; // merge's per-tile arrival counter)
@@ -2901,6 +2964,7 @@ static FilterWs carve(void* base, const FilterPlan& p, int64_t n, int d, int nq,
   w.cut = (float*)take((int64_t)nq * 4);
   w.band = (uint64_t*)take((int64_t)nq * BAND_CAP * 8);
   w.band_n = (int*)take((int64_t)nq * 4);
+  w.band_p1 = (int*)take((int64_t)nq * 4);
   int* fl = (int*)take(((int64_t)3 * nq + 1) * 4);
   w.flags = fl;
   w.qsel = fl + nq;
@@ -3096,8 +3160,8 @@ int filter_level(const FilterPlan& p, const FilterWs& w, int li, int mode, const
              : L.n_slabs <= 64 * SR_GMAX ? k_select_reg<true>
                                     : k_select_wave;
   hipLaunchKernelGGL(sel, dim3((nq + 3) / 4), dim3(256), 0, st, w.lists, w.counts,
-                     L.n_slabs, k, p.J, w.eps2, mode, w.theta, w.aref, w.band, w.band_n, w.flags,
-                     w.qsel, w.qsel_n, nq, stats, pcount, smax_out, fin);
+                     L.n_slabs, k, p.J, w.eps2, mode, w.theta, w.aref, w.band, w.band_n,
+                     w.band_p1, w.flags, w.qsel, w.qsel_n, nq, stats, pcount, smax_out, fin);
   return check_launch("k_select");
 }
 
@@ -3125,8 +3189,8 @@ int filter_finish(const FilterWs& w, const float* db, int64_t n, int32_t d, int6
                          row_base, cut, out_score, out_idx);                                  \
     else                                                                                      \
       hipLaunchKernelGGL(k_rerank<E>, dim3(nq), dim3(256), 0, st, db, ld_db, q, ld_q, w.band, \
-                         w.band_n, w.flags, w.qsel, w.qsel_n, n, k, row_base, cut, out_score, \
-                         out_idx);                                                            \
+                         w.band_n, w.band_p1, w.eps2, w.flags, w.qsel, w.qsel_n, n, k,        \
+                         row_base, out_score, out_idx);                                       \
     break;
     TT_RR(64) TT_RR(128) TT_RR(256) TT_RR(384) TT_RR(512) TT_RR(768)
 #undef TT_RR
@@ -3174,6 +3238,13 @@ __global__ void k_debug_plant(uint64_t* keys, uint64_t* xk, const int* counts, i
   }
 }
 }  // namespace
+
+#if TT_EXP_BLKTIME
+extern "C" int tt_debug_blktimes(void* host, int32_t n) {  // timing builds only
+  if (n > BLKTIME_MAX) n = BLKTIME_MAX;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_blktime), (size_t)n * 32) == hipSuccess ? n : -1;
+}
+#endif
 
 extern "C" int tt_debug_plant_bad_row(int32_t where, int32_t query) {
   TT_REQUIRE(where >= 0 && where <= 2 && query >= 0, "bad arguments");
