@@ -274,7 +274,11 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 #define TT_RR_NT 0  // k_rerank: band rows loaded non-temporal (A/B: re-rank 0.65 -> 1.75 ms)
 #endif
 #ifndef TT_RR_ONEPHASE
-#define TT_RR_ONEPHASE 0  // k_rerank: score the whole band in one phase (A/B)
+// k_rerank scores the whole band in one phase (default).  The two-phase form (0: P1 first, then
+// only the rows of the rest that can still reach s1) gathers ~25% fewer rows but adds a
+// dependent gather + barrier per query block: in-process A/B (tools/ab_inproc.py, 16 reps,
+// configs[2]) search minus full level 1.108 -> 1.186 ms -- slower, kept as a switch.
+#define TT_RR_ONEPHASE 1
 #endif
 #ifndef TT_EXP_MAXONLY
 #define TT_EXP_MAXONLY 0  // per-block max + ballot only (no per-slot scan)
@@ -320,7 +324,7 @@ TT_CHECK_EXP(TT_RING_HALF || TT_RING_QB4 || TT_RING_W4QB || TT_RING_ASM ||
                  TT_RING_QB_WIDE != 2 || TT_RING_FD_WIDE != 1 || TT_RING_PD_WIDE != 2 ||
                  TT_EXP_NOIDLE || TT_EXP_PRIO ||
                  TT_RING_NT != 1 || TT_RR_STAGED != 1 || TT_RR_PF != 1 || TT_RR_NT ||
-                 TT_RR_ONEPHASE,
+                 !TT_RR_ONEPHASE,
              "a non-default ring/re-rank schedule (untested by the GPU suite)");
 #ifndef TT_RING_PD
 // ring tiles in flight; 4 (5 slots, the pool's flush mark lowered to fit LDS): 6.33 -> 6.49 ms
@@ -458,6 +462,24 @@ __device__ __forceinline__ float query_eps2_wave(const float* __restrict__ qr, f
   }
   return query_eps2<EP>(sq, st, sr, X, R);
 }
+
+// Threshold of the batched full level from the last sample level's a_J (= aref) and 2 eps:
+// every row of the exact top k has a >= s_k - eps, so the level must keep {a >= s_k - eps}.
+// It keeps {a >= aref - 1.25 eps} and k_rerank certifies afterwards, from exact scores, that
+// s_k >= aref - eps / 8 (the k-th exact score of the band is a lower bound of s_k): then
+// s_k - eps >= aref - 1.125 eps > theta (the eps / 8 gap dwarfs the f32 rounding of these
+// expressions).  A query that does not certify takes the exact fallback.  In practice s_k is
+// far above aref (aref ~ the 336th row, s_k the 100th), so nothing falls back, and the level
+// keeps ~484 instead of ~592 candidates per query at 1M x 384 (aref - 2 eps until round 4;
+// tools/band_analysis.py restates the count).
+#ifndef TT_FULL_THETA_2EPS
+#define TT_FULL_THETA_2EPS 0  // timing builds: the round-4 threshold aref - 2 eps (A/B)
+#endif
+TT_CHECK_EXP(TT_FULL_THETA_2EPS, "TT_FULL_THETA_2EPS");
+__device__ __forceinline__ float full_theta(float aref, float eps2) {
+  return aref - (TT_FULL_THETA_2EPS ? 1.0f : 0.625f) * eps2;
+}
+__device__ __forceinline__ float full_cert(float aref, float eps2) { return aref - 0.0625f * eps2; }
 
 // Per-query filter state, initialised by the first level of a search (k_query_eps's work,
 // folded into that launch): eps2 from the catalog bounds X, R; aref = -inf; flags = 0;
@@ -1221,8 +1243,8 @@ __global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict_
       for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
       if (lane == 0) smax_out[qid] = key_float(m);
     }
-    if (lane == 0) {  // fin: the next level is the full one -> its threshold A - 2 eps
-      theta_out[qid] = fin ? A - eps2[qid] : A;
+    if (lane == 0) {  // fin: the next level is the full one -> its threshold (full_theta)
+      theta_out[qid] = fin ? full_theta(A, eps2[qid]) : A;
       aref[qid] = A;
     }
     return;
@@ -1461,8 +1483,8 @@ __global__ __launch_bounds__(256) void k_select_reg(const uint64_t* __restrict__
       for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
       if (lane == 0) smax_out[qid] = key_float(m);
     }
-    if (lane == 0) {  // fin: the next level is the full one -> its threshold A - 2 eps
-      theta_out[qid] = fin ? A - eps2[qid] : A;
+    if (lane == 0) {  // fin: the next level is the full one -> its threshold (full_theta)
+      theta_out[qid] = fin ? full_theta(A, eps2[qid]) : A;
       aref[qid] = A;
     }
     return;
@@ -2370,7 +2392,8 @@ __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, in
                                                 const uint64_t* __restrict__ band,
                                                 const int* __restrict__ band_n,
                                                 const int* __restrict__ band_p1,
-                                                const float* __restrict__ eps2, int* flags,
+                                                const float* __restrict__ eps2,
+                                                const float* __restrict__ aref, int* flags,
                                                 int* qsel, int* qsel_n, int64_t n_rows, int k,
                                                 int64_t row_base, float* __restrict__ out_s,
                                                 int64_t* __restrict__ out_i) {
@@ -2529,6 +2552,17 @@ __global__ __launch_bounds__(256) void k_rerank(const float* __restrict__ db, in
   const int np = pow2_at_least(nsc);
   for (int i = nsc + threadIdx.x; i < np; i += blockDim.x) buf[i] = 0ull;
   block_sort_desc(buf, np);
+  // certification of the full level's threshold (full_theta): the k-th exact score of the
+  // scored rows is a lower bound of the query's s_k; below full_cert(aref) the level may have
+  // dropped a band row -> exact fallback (a NaN exact score in the top k: also the fallback)
+  if (aref != nullptr) {
+    const bool ok = nsc >= k && buf[k - 1] != 0ull &&
+                    key_score(buf[k - 1]) >= full_cert(aref[qid], eps2[qid]);
+    if (!ok) {
+      if (threadIdx.x == 0) flag_query(qid, flags, qsel, qsel_n);
+      return;
+    }
+  }
   for (int i = threadIdx.x; i < k; i += blockDim.x) {
     float s = -__builtin_huge_valf();
     int64_t ix = -1;
@@ -3189,7 +3223,7 @@ int filter_finish(const FilterWs& w, const float* db, int64_t n, int32_t d, int6
                          row_base, cut, out_score, out_idx);                                  \
     else                                                                                      \
       hipLaunchKernelGGL(k_rerank<E>, dim3(nq), dim3(256), 0, st, db, ld_db, q, ld_q, w.band, \
-                         w.band_n, w.band_p1, w.eps2, w.flags, w.qsel, w.qsel_n, n, k,        \
+                         w.band_n, w.band_p1, w.eps2, w.aref, w.flags, w.qsel, w.qsel_n, n, k,\
                          row_base, out_score, out_idx);                                       \
     break;
     TT_RR(64) TT_RR(128) TT_RR(256) TT_RR(384) TT_RR(512) TT_RR(768)
