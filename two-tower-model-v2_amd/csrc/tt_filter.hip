@@ -505,7 +505,8 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
     const uint16_t* __restrict__ xb, int64_t ld, const float* __restrict__ q, int nq,
     int64_t ldq, const float* __restrict__ theta, int64_t stride, int64_t n_sample,
     int rows_per_slab, int n_slabs, int n_qt, uint64_t* __restrict__ lists,
-    int* __restrict__ counts, QueryInit qinit, const uint16_t* __restrict__ q16) {
+    int* __restrict__ counts, QueryInit qinit, const uint16_t* __restrict__ q16,
+    int n_slabs_p, int rows_p) {
   constexpr int TR = RingCfg<EP>::TR, QB = RingK<EP, LVL>::QB;
   constexpr int RG_PD = RingK<EP, LVL>::PD, RG_SLOTS = RingK<EP, LVL>::SLOTS;
   constexpr int KS = EP / 32, QPW = 16 * QB, QPB = RG_WAVES * QPW;
@@ -528,8 +529,35 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (TT_EXP_PRIO && w >= RG_WAVES / 2) __builtin_amdgcn_s_setprio(1);  // younger half (guide)
   const int col = lane & 15, g = lane >> 4;
-  const int lb = xcd_remap(blockIdx.x, gridDim.x);
-  const int slab = lb / n_qt, qt = lb % n_qt;
+  // Block -> (slab, query tile).  Uniform plan: XCD-contiguous ranges of (slab, tile) units,
+  // the n_qt tiles of a slab adjacent (they share the slab's rows in L2).  Balanced plan
+  // (n_slabs_p > 0, plan_balance): the last query tile is partial (e.g. 10k queries = 26 x 384
+  // + 16) and costs about half a full block per row, so it has its own, coarser slabs
+  // (n_slabs_p of rows_p rows, sized so its blocks cost about what a full block costs) and the
+  // launch is exactly whole rounds of blocks; each XCD runs its share of the full tiles' units
+  // first, then its share of the partial tile's.
+  int slab, qt;
+  int64_t rps = rows_per_slab;
+  if (n_slabs_p > 0) {
+    const int nfull = (n_qt - 1) * n_slabs, nblk = (int)gridDim.x;
+    const int x = (int)blockIdx.x % 8, local = (int)blockIdx.x / 8;
+    const int qf = nfull / 8, rf = nfull % 8, qb8 = nblk / 8, rb8 = nblk % 8;
+    const int fx0 = x * qf + (x < rf ? x : rf), nfx = qf + (x < rf ? 1 : 0);
+    const int px0 = x * qb8 + (x < rb8 ? x : rb8) - fx0;  // partial units of the XCDs before x
+    if (local < nfx) {
+      slab = (fx0 + local) / (n_qt - 1);
+      qt = (fx0 + local) % (n_qt - 1);
+    } else {
+      slab = px0 + (local - nfx);
+      qt = n_qt - 1;
+      rps = rows_p;
+    }
+  } else {
+    const int lb0 = xcd_remap(blockIdx.x, gridDim.x);
+    slab = lb0 / n_qt;
+    qt = lb0 % n_qt;
+  }
+  const int lb = slab * n_qt + qt;
   const int qbase = qt * QPB + w * QPW;
 #if TT_EXP_BLKTIME
   const unsigned long long blk_t0 = wall_clock64();
@@ -554,8 +582,8 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   bf16x8 qf[QB][KS];
   float th[QB];
 
-  const int64_t j0 = (int64_t)slab * rows_per_slab;
-  const int64_t j1 = (j0 + rows_per_slab < n_sample) ? j0 + rows_per_slab : n_sample;
+  const int64_t j0 = (int64_t)slab * rps;
+  const int64_t j1 = (j0 + rps < n_sample) ? j0 + rps : n_sample;
   const int n_tiles = j0 < j1 ? (int)((j1 - j0 + TR - 1) / TR) : 0;
 
   // DMA of tile t into ring slot t % RG_SLOTS: piece p of the tile = LDS bytes [1024p, +1024),
@@ -975,6 +1003,11 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
       const uint32_t c = (uint32_t)qcnt[w * QPW + i];
       counts[(int64_t)qi * n_slabs + slab] =
           c > (uint32_t)FL_CAP ? FL_CAP + 1 : (int)c;
+      // balanced plan: the partial tile's queries have n_slabs_p slabs, their lists keep the
+      // n_slabs stride -- the slots past n_slabs_p read as empty
+      if (n_slabs_p > 0 && qt == n_qt - 1)
+        for (int s2 = slab + n_slabs_p; s2 < n_slabs; s2 += n_slabs_p)
+          counts[(int64_t)qi * n_slabs + s2] = 0;
     }
   }
 }
@@ -2778,6 +2811,7 @@ __global__ void k_sub_arr(float* x, const float* y, int n) {
 struct Level {
   int64_t stride, n_sample;
   int rows_per_slab, n_slabs, n_qt;
+  int n_slabs_p = 0, rows_p = 0;  // balanced plan of a partial last query tile (plan_balance)
   bool dense;
   bool tmax;  // appends tile maxima (k_filter_ring<EP, 0>): every level sampled at stride > 1
 };
@@ -2865,6 +2899,63 @@ static int64_t ring_slabs(int n_qt, int64_t n_sample, int64_t sl_min = 1) {
   return best;
 }
 
+// Balanced plan of the batched full level when its last query tile is partial (10k queries =
+// 26 tiles of 384 + 16): a block of that tile streams its slab with ~1 of 8 waves computing and
+// costs ~0.53 of a full block per row (round-5 block timeline, tools/blktime.py: 620 vs 1160
+// us), so with uniform slabs the launch's CUs ran 4 or 5 full blocks plus or minus a cheap one
+// -- 4.5% of the launch's CU time idle, most of it a ragged tail.  Here the full tiles take
+// s_f slabs and the partial tile s_p ~ c_p s_f coarser ones, with (n_qt - 1) s_f + s_p = whole
+// rounds of the chip, so every CU runs the same number of blocks of about the same cost.
+// Taken when its rounds x (rows + 96) model beats the uniform plan's.
+#ifndef TT_FILTER_BALANCE_DEFAULT
+#define TT_FILTER_BALANCE_DEFAULT 1  // 0: uniform slabs unless TT_FILTER_BALANCE=1 (A/B builds)
+#endif
+TT_CHECK_EXP(TT_FILTER_BALANCE_DEFAULT != 1, "TT_FILTER_BALANCE_DEFAULT");
+static bool balance_disabled() {  // TT_FILTER_BALANCE=0: uniform slabs
+  static const bool off = env_switch("TT_FILTER_BALANCE", TT_FILTER_BALANCE_DEFAULT) == 0;
+  return off;
+}
+static void plan_balance(Level& L, int nq, int qpb) {
+  if (balance_disabled() || L.n_qt < 2) return;
+  const int ncu = device_cus() * RG_BLOCKS_PER_CU;
+  const double f = (double)(nq - (L.n_qt - 1) * qpb) / qpb;  // partial tile's share of queries
+  const double cp = 0.5 + 0.5 * f;                              // its cost per row, vs a full tile
+  if (f >= 1.0) return;
+  const int64_t rounds_u = ((int64_t)L.n_qt * L.n_slabs + ncu - 1) / ncu;
+  const double cost_u = (double)rounds_u * (L.rows_per_slab + 96);
+  double best = cost_u;
+  int bf = 0, bp = 0, rf_best = 0, rp_best = 0;
+  for (int64_t R = 1; R <= 64; ++R) {
+    const int64_t blocks = R * ncu;
+    int64_t sf = (int64_t)((double)blocks / (L.n_qt - 1 + cp));
+    for (; sf >= 1; --sf) {
+      int64_t rf = ((L.n_sample + sf - 1) / sf + 63) / 64 * 64;
+      const int64_t sf2 = (L.n_sample + rf - 1) / rf;
+      const int64_t sp = blocks - (int64_t)(L.n_qt - 1) * sf2;
+      if (sp < 16 || sp > sf2) continue;
+      const int64_t rp = ((L.n_sample + sp - 1) / sp + 63) / 64 * 64;
+      const int64_t sp2 = (L.n_sample + rp - 1) / rp;
+      if (sp2 < 16 || rp >= (1 << 25) || rf >= (1 << 25)) continue;
+      const double cost = (double)R * ((rf > cp * rp ? rf : cp * rp) + 96);
+      if (cost < best * 0.999) {
+        best = cost;
+        bf = (int)sf2;
+        bp = (int)sp2;
+        rf_best = (int)rf;
+        rp_best = (int)rp;
+      }
+      break;
+    }
+    if (R * ncu > 4 * (int64_t)L.n_qt * L.n_slabs) break;
+  }
+  if (bf > 0) {
+    L.n_slabs = bf;
+    L.rows_per_slab = rf_best;
+    L.n_slabs_p = bp;
+    L.rows_p = rp_best;
+  }
+}
+
 static FilterPlan plan_filter_uncached(int64_t n, int nq, int k, int ep) {
   FilterPlan p;
   // ~16*J full-catalog rows lie above a_J(stride-16 sample); J = k/8 + 8 keeps that count
@@ -2921,6 +3012,7 @@ static FilterPlan plan_filter_uncached(int64_t n, int nq, int k, int ep) {
     r = (r + 63) / 64 * 64;
     L.rows_per_slab = (int)r;
     L.n_slabs = (int)((L.n_sample + r - 1) / r);
+    if (i == nl - 1 && !L.dense && ring_lvl(false, nq, ep) == 1) plan_balance(L, nq, qpb);
     if (L.n_slabs > p.max_slabs) p.max_slabs = L.n_slabs;
   }
   p.small = nq <= SM_NQ && !select_reg_disabled();
@@ -3030,9 +3122,11 @@ static void launch_level(const Level& L, const uint16_t* xb, int64_t n, int64_t 
                 : lvl == 1 ? k_filter_ring<EP, 1> : k_filter_ring<EP, 2>;
     if constexpr (EP >= 512)
       if (lvl == 4) kern = k_filter_ring<EP, 4>;
-    hipLaunchKernelGGL(kern, dim3(nblk), dim3(64 * RG_WAVES), 0, st, xb, ld, q, nq, ldq, w.theta,
+    const int nb = L.n_slabs_p > 0 ? (L.n_qt - 1) * L.n_slabs + L.n_slabs_p : nblk;
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(64 * RG_WAVES), 0, st, xb, ld, q, nq, ldq, w.theta,
                        L.stride, L.n_sample, L.rows_per_slab, L.n_slabs, L.n_qt, w.lists,
-                       w.counts, qi, w.q16_valid ? (const uint16_t*)w.q16 : nullptr);
+                       w.counts, qi, w.q16_valid ? (const uint16_t*)w.q16 : nullptr,
+                       L.n_slabs_p, L.rows_p);
   }
 }
 
