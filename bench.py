@@ -679,14 +679,17 @@ def single_buyer_api(a, dev, shard, shard16, n, E, K, bounds, table, hist, w, re
     calls(200)
     one = 200 / (time.perf_counter() - t0)
     th = [threading.Thread(target=calls, args=(50,)) for _ in range(4)]
+    st0 = list(idx.coalesce_stats)
     t0 = time.perf_counter()
     for t in th:
         t.start()
     for t in th:
         t.join()
     four = 200 / (time.perf_counter() - t0)
+    nb, nr = (idx.coalesce_stats[0] - st0[0], idx.coalesce_stats[1] - st0[1])
     return {"api_ms_per_call": statistics.median(api),
             "api_calls_per_s_1_thread": one, "api_calls_per_s_4_threads": four,
+            "api_4_threads_mean_batch": nr / max(nb, 1),
             "api_k1000_ms_per_call": statistics.median(api_k),
             "api_ms_per_call_is": ("VectorDatabase.retrieve(host numpy query, k) -> list of "
                                    "(product_id, score), host to host, median of 21"),

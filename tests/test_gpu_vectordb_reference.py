@@ -237,3 +237,49 @@ def test_retrieve_per_request_k_no_reallocation_and_threads():
     for t in th:
         t.join()
     assert not errs, errs[:5]
+
+
+def test_retrieve_coalesces_concurrent_requests_bit_identical():
+    """Concurrent single-query retrieve calls are served as batched searches (FlatIPIndex
+    request coalescing): 6 threads x 40 calls with per-request k (filter and select paths)
+    get exactly the single-request answers; the coalescing counters account for every call."""
+    import threading
+
+    import torch
+
+    from twotower import VectorDatabase
+
+    rng = np.random.default_rng(13)
+    n, d = 50000, 384
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    ids = [f"p{i}" for i in range(n)]
+    vdb = VectorDatabase(d)
+    vdb.build_index(x, ids)
+    q = rng.standard_normal((12, d)).astype(np.float32)
+    ks = [1, 7, 50, 100, 128, 129, 300, 1000]
+    want = {}
+    for k in ks:
+        s_dev, i_dev = vdb.search(torch.from_numpy(q).cuda(), k)
+        s_dev, i_dev = s_dev.cpu().numpy(), i_dev.cpu().numpy()
+        want[k] = [[(ids[j], float(v)) for j, v in zip(i_dev[b], s_dev[b])] for b in range(len(q))]
+    errs = []
+    st0 = list(vdb.index.coalesce_stats)
+
+    def work(t):
+        try:
+            for c in range(40):
+                k, b = ks[(t + c) % len(ks)], (3 * t + c) % len(q)
+                if vdb.retrieve(q[b], k=k) != want[k][b]:
+                    errs.append((t, c, k, b))
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs[:5]
+    nb, nr = (vdb.index.coalesce_stats[0] - st0[0], vdb.index.coalesce_stats[1] - st0[1])
+    assert nr == 240 and 1 <= nb <= 240
+    print(f"coalesced 240 requests into {nb} searches")

@@ -59,6 +59,11 @@ class FlatIPIndex:
         # slot out / in and to read the catalog state: faiss' search is re-entrant, and the
         # reference's /retrieve may be called from several threads (server.py:212-244)
         self._lock = threading.RLock()
+        self.coalesce = True  # batch concurrent single-query host searches (search_host)
+        self._qlock = threading.Lock()
+        self._queue = []
+        self._leading = False
+        self.coalesce_stats = [0, 0]  # [batches run, requests served] by the coalescing path
 
     def _append(self, rows: torch.Tensor, rows16: torch.Tensor) -> None:
         # bounds first: they only grow (max-combined), so a search snapshot taken between the
@@ -166,11 +171,86 @@ class FlatIPIndex:
             s, i = self.search_device(q, k)
             torch.cuda.current_stream().synchronize()
             return s.cpu().numpy(), i.cpu().numpy()
-        slot = self._checkout(nq)
+        if nq == 1 and self.coalesce:
+            return self._coalesced(x, k, normalize)
+        return self._run_batch(x, k, normalize, state)
+
+    def _run_batch(self, x: np.ndarray, k: int, normalize: bool, state=None):
+        if state is None:
+            with self._lock:
+                state = (self.xb, self.xb16, self.ntotal, self.bounds)
+        slot = self._checkout(x.shape[0])
         try:
             return slot.run(x, k, normalize, state)
         finally:
             self._checkin(slot)
+
+    # ---- request coalescing (concurrent one-query callers, e.g. /retrieve under a threaded
+    # server): while one search is in flight, arriving single-query requests queue up; the
+    # thread that leads runs the queue's requests as ONE batched search (up to COALESCE_MAX
+    # queries of the same search path -- k <= 128: the bf16 filter, k <= 1024: scores + select
+    # -- at the batch's largest k; a request gets the first k entries of its row, which are its
+    # own exact top k: the lists are sorted by (score desc, row asc)), then hands the lead to
+    # the next waiting thread.  One caller alone is a batch of one.
+    COALESCE_MAX = 8
+
+    def _path(self, k: int) -> int:
+        return 0 if k <= kernels.FILTER_KMAX else 1 if k <= kernels.SCAN_KMAX else 2
+
+    def _coalesced(self, x: np.ndarray, k: int, normalize: bool):
+        req = _Request(x, k, normalize)
+        with self._qlock:
+            self._queue.append(req)
+            lead = not self._leading
+            if lead:
+                self._leading = True
+        if not lead:
+            req.event.wait()
+            if not req.finished:  # handed the lead: this thread serves the queue now
+                self._serve(req)
+        else:
+            self._serve(req)
+        if req.error is not None:
+            raise req.error
+        return req.result
+
+    def _serve(self, me: "_Request") -> None:
+        while True:
+            with self._qlock:
+                head = self._queue[0]
+                cls = (head.normalize, self._path(head.k))
+                batch, rest = [], []
+                for r in self._queue:
+                    if len(batch) < self.COALESCE_MAX and (r.normalize, self._path(r.k)) == cls:
+                        batch.append(r)
+                    else:
+                        rest.append(r)
+                self._queue[:] = rest
+            kk = max(r.k for r in batch)
+            self.coalesce_stats[0] += 1
+            self.coalesce_stats[1] += len(batch)
+            try:
+                with self._lock:
+                    state = (self.xb, self.xb16, self.ntotal, self.bounds)
+                kk = min(kk, state[2])
+                xs = np.concatenate([r.x for r in batch]) if len(batch) > 1 else batch[0].x
+                s, i = self._run_batch(xs, kk, head.normalize, state)
+                for j, r in enumerate(batch):
+                    r.result = (s[j:j + 1, :r.k], i[j:j + 1, :r.k])
+            except Exception as e:  # every request of the failed batch sees the error
+                for r in batch:
+                    r.error = e
+            for r in batch:
+                r.finished = True
+                if r is not me:
+                    r.event.set()
+            with self._qlock:
+                if me.finished:
+                    if self._queue:  # hand the lead to the oldest waiting request's thread
+                        self._queue[0].event.set()
+                    else:
+                        self._leading = False
+                    return
 
     def search(self, x: np.ndarray, k: int):
         """faiss signature: float32 [nq, d] host queries -> (D [nq,k] f32, I [nq,k] i64) host."""
@@ -178,6 +258,36 @@ class FlatIPIndex:
 
     def reconstruct(self, i: int) -> np.ndarray:
         return self.xb[i, : self.d].cpu().numpy()
+
+
+_HIP = None
+
+
+def _hip():
+    """The HIP runtime torch already loaded (ctypes): the serving slot's async copies."""
+    global _HIP
+    if _HIP is None:
+        h = ctypes.CDLL("libamdhip64.so")
+        h.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                     ctypes.c_int, ctypes.c_void_p]
+        h.hipMemcpy2DAsync.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                       ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
+                                       ctypes.c_int, ctypes.c_void_p]
+        h.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+        _HIP = h
+    return _HIP
+
+
+class _Request:
+    """One queued single-query host search (FlatIPIndex._coalesced)."""
+
+    __slots__ = ("x", "k", "normalize", "event", "result", "error", "finished")
+
+    def __init__(self, x, k, normalize):
+        self.x, self.k, self.normalize = x, k, normalize
+        self.event = threading.Event()
+        self.result = self.error = None
+        self.finished = False
 
 
 class _ServingSlot:
@@ -200,6 +310,11 @@ class _ServingSlot:
         self._outs(kc, pin)
         self.ws = torch.empty(0, dtype=torch.uint8, device=dev)
         self.ws_need = {}  # (n, nq, k, kind) -> workspace bytes (memoised size queries)
+        self.synced = None  # catalog state this slot's stream is ordered after
+        self.fn = _lib.lib().tt_scan_topk_bf16f32
+        self.norm_fn = _lib.lib().tt_l2norm_rows_f32
+        self.qh_np = self.qh.numpy()
+        self.args, self.args_key = None, None
         index.allocations += 1
 
     def _outs(self, kc: int, pin: bool) -> None:
@@ -209,6 +324,7 @@ class _ServingSlot:
         self.i = torch.empty(self.bucket * kc, dtype=torch.int64, device=dev)
         self.sh = torch.empty(self.bucket * kc, dtype=torch.float32, pin_memory=pin)
         self.ih = torch.empty(self.bucket * kc, dtype=torch.int64, pin_memory=pin)
+        self.sh_np, self.ih_np = self.sh.numpy(), self.ih.numpy()
 
     def _workspace(self, n: int, nq: int, k: int, kind: str) -> torch.Tensor:
         key = (n, nq, k, kind)
@@ -224,6 +340,52 @@ class _ServingSlot:
             self.ix.allocations += 1
         return self.ws
 
+    def _fast(self, x: np.ndarray, k: int, normalize: bool, state, skey):
+        """The bf16-filter search (k <= 128, d <= 768) with no torch op per call: the staging
+        copies, the normalisation, the search and the result copies are C calls on this slot's
+        stream (hipMemcpy*Async, tt_l2norm_rows_f32, tt_scan_topk_bf16f32), the arguments bound
+        once per (catalog state, nq, k); the stream synchronisation releases the GIL (ctypes),
+        so other serving threads run their host work meanwhile.  ~25% less host time per call
+        than the torch-op form."""
+        ix = self.ix
+        xb, xb16, n, bounds = state
+        nq, d = x.shape
+        ws = self._workspace(n, nq, k, "bf16")
+        akey = (skey, nq, k, ws.data_ptr(), self.s.data_ptr(), bounds, normalize)
+        if akey != self.args_key:  # the C arguments, bound once per (state, nq, k)
+            vp = ctypes.c_void_p
+            qp, st = vp(self.q.data_ptr()), vp(self.stream.cuda_stream)
+            self.args = (
+                vp(xb.data_ptr()), vp(xb16.data_ptr()), n, d, xb.stride(0), ix.row_base, qp, nq,
+                self.q.stride(0), k, ctypes.c_float(bounds[0]), ctypes.c_float(bounds[1]),
+                vp(self.s.data_ptr()), vp(self.i.data_ptr()), vp(ws.data_ptr()), ws.numel(), st,
+                None, None)
+            self.h2d = (qp, ctypes.c_size_t(self.q.stride(0) * 4), vp(self.qh.data_ptr()),
+                        ctypes.c_size_t(d * 4), ctypes.c_size_t(d * 4), ctypes.c_size_t(nq), 1, st)
+            self.norm = ((qp, nq, d, self.q.stride(0), qp, self.q.stride(0), None,
+                          _lib.TT_NORM_ADD_EPS, st) if normalize else None)
+            self.d2h = ((vp(self.sh.data_ptr()), vp(self.s.data_ptr()), ctypes.c_size_t(nq * k * 4),
+                         2, st),
+                        (vp(self.ih.data_ptr()), vp(self.i.data_ptr()), ctypes.c_size_t(nq * k * 8),
+                         2, st))
+            self.args_key = akey
+        self.qh_np[:nq] = x
+        hip = _hip()
+        if hip.hipMemcpy2DAsync(*self.h2d):
+            raise RuntimeError("hipMemcpy2DAsync (queries) failed")
+        if self.norm is not None:
+            _lib.check(self.norm_fn(*self.norm), "tt_l2norm_rows_f32")
+        rc = self.fn(*self.args)
+        if rc:
+            _lib.check(rc, "tt_scan_topk_bf16f32")
+        for a in self.d2h:
+            if hip.hipMemcpyAsync(*a):
+                raise RuntimeError("hipMemcpyAsync (results) failed")
+        if hip.hipStreamSynchronize(self.args[16]):
+            raise RuntimeError("hipStreamSynchronize failed")
+        return (self.sh_np[: nq * k].reshape(nq, k).copy(),
+                self.ih_np[: nq * k].reshape(nq, k).copy())
+
     def run(self, x: np.ndarray, k: int, normalize: bool, state):
         ix = self.ix
         xb, xb16, n, bounds = state
@@ -232,8 +394,15 @@ class _ServingSlot:
             self._outs(k, torch.cuda.is_available())
             ix.allocations += 1
         q = self.q[:nq]
-        # ordered after the caller's stream (e.g. an add() whose kernels may still run there)
-        self.stream.wait_stream(torch.cuda.current_stream())
+        # ordered after the caller's stream once per catalog state (an add() whose kernels may
+        # still run there); later calls on the same state need no cross-stream wait
+        skey = (xb.data_ptr(), xb16.data_ptr(), n)
+        if skey != self.synced:
+            self.stream.wait_stream(torch.cuda.current_stream())
+            self.synced = skey
+        if ix.scan_dim and k <= kernels.FILTER_KMAX and k <= self.kc:
+            return self._fast(x, k, normalize, state, skey)
+        self.args_key = None  # the torch-op path below rebinds its own arguments
         with torch.cuda.stream(self.stream):
             self.qh[:nq].numpy()[...] = x
             q[:, :d].copy_(self.qh[:nq], non_blocking=True)
@@ -243,13 +412,19 @@ class _ServingSlot:
             st = self.stream.cuda_stream
             if ix.scan_dim and k <= kernels.FILTER_KMAX:
                 ws = self._workspace(n, nq, k, "bf16")
-                check = _lib.lib().tt_scan_topk_bf16f32(
-                    ctypes.c_void_p(xb.data_ptr()), ctypes.c_void_p(xb16.data_ptr()), n, d,
-                    xb.stride(0), ix.row_base, ctypes.c_void_p(q.data_ptr()), nq, q.stride(0),
-                    k, ctypes.c_float(bounds[0]), ctypes.c_float(bounds[1]),
-                    ctypes.c_void_p(s.data_ptr()), ctypes.c_void_p(i.data_ptr()),
-                    ctypes.c_void_p(ws.data_ptr()), ws.numel(), ctypes.c_void_p(st), None, None)
-                _lib.check(check, "tt_scan_topk_bf16f32")
+                akey = (skey, nq, k, ws.data_ptr(), s.data_ptr(), bounds)
+                if akey != self.args_key:  # the C arguments, bound once per (state, nq, k)
+                    self.args = (
+                        ctypes.c_void_p(xb.data_ptr()), ctypes.c_void_p(xb16.data_ptr()), n, d,
+                        xb.stride(0), ix.row_base, ctypes.c_void_p(q.data_ptr()), nq,
+                        q.stride(0), k, ctypes.c_float(bounds[0]), ctypes.c_float(bounds[1]),
+                        ctypes.c_void_p(s.data_ptr()), ctypes.c_void_p(i.data_ptr()),
+                        ctypes.c_void_p(ws.data_ptr()), ws.numel(), ctypes.c_void_p(st), None,
+                        None)
+                    self.args_key = akey
+                rc = self.fn(*self.args)
+                if rc:
+                    _lib.check(rc, "tt_scan_topk_bf16f32")
             elif ix.scan_dim and k <= kernels.SCAN_KMAX:
                 ws = self._workspace(n, nq, k, "select")
                 kernels.scan_topk_select(xb, n, d, q, k, row_base=ix.row_base, workspace=ws,
