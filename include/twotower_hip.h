@@ -133,6 +133,24 @@ int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n, in
                          void* ev_start, void* ev_stop);
 
 /* ---------------------------------------------------------------------------------
+ * Same results as tt_scan_topk_f32 for the one-buyer serving call (nq <= 4, padded dim 384
+ * or 768, k <= 128; src/api/server.py:241-244 -> vector_db.py:160 retrieve): one streaming pass
+ * over an INT8 image of the catalog (tt_i8_image: half the bytes of the bf16 image), a
+ * per-(query, slab) top-16 on v_mfma_i32_16x16x64_i8 with the exact f32 scores of the kept
+ * rows, and a final that certifies the exact top k with a rigorous bound (a slab's dropped rows
+ * score at most its 16th approximate score + eps, eps from x_norm_max, x_resid_max, s_max = the
+ * image's bounds).  Uncertified queries take the exact f32 fallback in a following launch.
+ * Workspace: tt_filter_workspace_bytes (same n, d, nq, k).  Returns TT_ERR_UNSUPPORTED outside
+ * that shape (callers then use tt_scan_topk_bf16f32).
+ * --------------------------------------------------------------------------------- */
+int tt_scan_topk_i8f32(const float* db, const int8_t* db_i8, const float* tile_scales,
+                       int64_t n, int32_t d, int64_t ld_db, int64_t ld_i8, int64_t row_base,
+                       const float* q, int32_t nq, int64_t ld_q, int32_t k, float x_norm_max,
+                       float x_resid_max, float s_max, float* out_score, int64_t* out_idx,
+                       void* workspace, int64_t workspace_bytes, void* stream, void* ev_start,
+                       void* ev_stop);
+
+/* ---------------------------------------------------------------------------------
  * Row-sharded (multi-GPU) form of tt_scan_topk_bf16f32 (faiss IndexFlatIP.search,
  * vector_db.py:160,197, over a catalog split by rows across ranks).
  * Every rank holds its shard [row_base, row_base + n) in f32 and bf16, plus the GLOBAL
@@ -192,6 +210,12 @@ int tt_sharded_filter_finish(const float* db, const uint16_t* db_bf16, int64_t n
  * (atomically, so successive add() batches accumulate; the caller zero-fills out2 once)
  * out2[0] >= max_r ||x_r|| and out2[1] >= max_r ||x_r - x_bf16_r||  (out2: 2 device floats).
  * NaN rows are skipped. */
+/* The int8 image of a normalised catalog for tt_scan_topk_i8f32: per 64-row tile one scale
+ * s = max |x| / 127 (tile_scales[ceil(n / 64)]), codes rint(x / s) in [-127, 127] into
+ * codes [n, ld_codes] int8 (padding columns zero); out3 (device, 3 floats, max-combined like
+ * tt_bf16_image_bounds; zero it first) >= (max ||x_r||, max ||x_r - s n_r||, max s ||n_r||). */
+int tt_i8_image(const float* x, int64_t n, int32_t d, int64_t ld, int8_t* codes,
+                int64_t ld_codes, float* tile_scales, float* out3, void* stream);
 int tt_bf16_image_bounds(const float* x, const uint16_t* x_bf16, int64_t n, int32_t d,
                          int64_t ld, float* out2, void* stream);
 

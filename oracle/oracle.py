@@ -148,6 +148,38 @@ def vector_db_normalize(x: np.ndarray) -> np.ndarray:
     return (x / (norms + 1e-8)).astype(np.float32)
 
 
+def i8_image(x: np.ndarray):
+    """numpy restatement of tt_i8_image (test infrastructure): per 64-row tile s = max|x| / 127
+    over finite values (float32 division), codes rint(x / s) clamped to [-127, 127] (0 where
+    s == 0 or x is not finite); bounds (max ||x||, max ||x - s n||, max s ||n||) in float64 over
+    rows without a non-finite value."""
+    x = np.asarray(x, np.float32)
+    n, d = x.shape
+    codes = np.zeros((n, d), np.int8)
+    scales = np.zeros((n + 63) // 64, np.float32)
+    bx = br = bs = 0.0
+    fin = np.isfinite(x)
+    for t in range(scales.size):
+        blk, f = x[64 * t:64 * t + 64], fin[64 * t:64 * t + 64]
+        m = np.float32(np.abs(np.where(f, blk, 0)).max()) if blk.size else np.float32(0)
+        s = np.float32(m / np.float32(127.0))
+        scales[t] = s
+        if s > 0:
+            with np.errstate(invalid="ignore", divide="ignore"):
+                c = np.clip(np.rint(np.where(f, blk, 0) / s), -127, 127)
+            c = np.where(f, c, 0).astype(np.int8)
+        else:
+            c = np.zeros(blk.shape, np.int8)
+        codes[64 * t:64 * t + 64] = c
+        ok = f.all(axis=1)
+        if ok.any():
+            b64, c64 = blk[ok].astype(np.float64), c[ok].astype(np.float64)
+            bx = max(bx, float(np.sqrt((b64 ** 2).sum(1)).max()))
+            br = max(br, float(np.sqrt(((b64 - float(s) * c64) ** 2).sum(1)).max()))
+            bs = max(bs, float(s) * float(np.sqrt((c64 ** 2).sum(1)).max()))
+    return codes, scales, (bx, br, bs)
+
+
 def weighted_avg_l2_f64(items: np.ndarray, w: np.ndarray) -> np.ndarray:
     """BuyerTower.weighted_average in float64 (buyer_tower.py:43-68): w / (sum w + 1e-8),
     weighted sum over the history, F.normalize (x / max(||x||, 1e-12))."""

@@ -1,0 +1,141 @@
+"""The int8 single pass for one-buyer searches (tt_i8_image + tt_scan_topk_i8f32,
+DESIGN 4.1c): the image against its numpy restatement, and the search bit-exact against the
+canonical f32 oracle -- the bound and the exact-score certification make it exact; a query the
+final cannot certify takes the exact f32 fallback (clustered and adversarial cases below)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def K():
+    from twotower import kernels
+
+    return kernels
+
+
+def dev_rows(x, ep=None):
+    from twotower import _lib
+
+    x = np.ascontiguousarray(x, np.float32)
+    ep = ep or _lib.padded_dim(x.shape[1])
+    t = torch.zeros((x.shape[0], ep), dtype=torch.float32, device="cuda")
+    t[:, : x.shape[1]] = torch.from_numpy(x).cuda()
+    return t
+
+
+@pytest.mark.parametrize("n,d", [(1000, 384), (129, 700), (64, 384), (5, 768)])
+def test_i8_image_vs_numpy(K, oracle_mod, n, d):
+    from oracle import oracle as O
+
+    rng = np.random.default_rng(n + d)
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
+    x[3 % n] = 0.0  # a zero row (its tile scale stays that of the other rows)
+    if n >= 64:
+        x[64:] *= 0.5  # tiles of different magnitude
+    db = dev_rows(x)
+    codes, scales, b3 = K.i8_image(db, d)
+    c_ref, s_ref, b_ref = O.i8_image(x)
+    assert np.array_equal(scales.cpu().numpy(), s_ref)
+    got = codes.cpu().numpy()
+    assert np.array_equal(got[:, :d], c_ref) and np.all(got[:, d:] == 0)
+    b = b3.cpu().numpy().astype(np.float64)
+    for i in range(3):  # upper bounds, tight to f64 rounding + the x1.000001 margin
+        assert b_ref[i] <= b[i] <= b_ref[i] * 1.00001 + 1e-30, (i, b[i], b_ref[i])
+
+
+def _i8_search(K, db, x16_ref, n, d, q, k):
+    codes, scales, b3 = K.i8_image(db, d)
+    return K.scan_topk_i8(db, codes, scales, n, d, q, k, b3.tolist())
+
+
+@pytest.mark.parametrize("n,d,nq,k", [(100_000, 384, 1, 100), (300_001, 384, 4, 128),
+                                      (1000, 384, 2, 10), (50_000, 700, 3, 100),
+                                      (70_000, 768, 1, 1), (257, 384, 1, 128),
+                                      (1_000_000, 384, 1, 100)])
+def test_scan_topk_i8_bit_exact_vs_oracle(K, oracle_mod, n, d, nq, k):
+    rng = np.random.default_rng(n + nq + k)
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
+    q = oracle_mod.l2norm_rows(rng.standard_normal((nq, d)).astype(np.float32), 0)
+    db, qd = dev_rows(x), dev_rows(q)
+    s, i = _i8_search(K, db, None, n, d, qd, k)
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    assert np.array_equal(i.cpu().numpy(), ri)
+    assert np.array_equal(s.cpu().numpy(), rs)
+
+
+def test_scan_topk_i8_mode_b_buyers_no_fallback(K, oracle_mod):
+    """Mode B buyers (weighted averages of 20 catalog rows, as bench.py's) over 1M x 384: every
+    result bit-exact, and the certification holds (no query falls back)."""
+    n, d, k = 1_000_000, 384, 100
+    rng = np.random.default_rng(5)
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
+    db = dev_rows(x)
+    codes, scales, b3 = K.i8_image(db, d)
+    ws = torch.empty(K.filter_workspace_bytes(n, d, 4, k), dtype=torch.uint8, device="cuda")
+    fb = 0
+    for rep in range(4):
+        h = rng.integers(0, n, (4, 20))
+        w = np.where(rng.random((4, 20)) < 0.75, 1.0, 5.0).astype(np.float32)
+        q = oracle_mod.l2norm_rows(oracle_mod.weighted_avg_l2(x[h], w), 0)
+        s, i = K.scan_topk_i8(db, codes, scales, n, d, dev_rows(q), k, b3.tolist(), workspace=ws)
+        fb += K.filter_fallback_count(ws, n, d, 4, k)
+        rs, ri = oracle_mod.scan_topk(x, q, k)
+        assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
+    assert fb == 0, fb
+
+
+def test_scan_topk_i8_clustered_slab_falls_back_exactly(K, oracle_mod):
+    """400 near-copies of the query inside one slab: that slab's 16th approximate score is far
+    above the 100th exact score, so the final cannot certify and the exact fallback serves the
+    query -- bit-exact either way; duplicates tie to the lower row."""
+    n, d, k = 200_000, 384, 100
+    rng = np.random.default_rng(9)
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    q = rng.standard_normal((1, d)).astype(np.float32)
+    x[1000:1400] = q + 0.05 * rng.standard_normal((400, d)).astype(np.float32)
+    x[5000] = x[1001]  # an exact duplicate
+    x = oracle_mod.l2norm_rows(x, 0)
+    q = oracle_mod.l2norm_rows(q, 0)
+    db = dev_rows(x)
+    codes, scales, b3 = K.i8_image(db, d)
+    ws = torch.empty(K.filter_workspace_bytes(n, d, 1, k), dtype=torch.uint8, device="cuda")
+    s, i = K.scan_topk_i8(db, codes, scales, n, d, dev_rows(q), k, b3.tolist(), workspace=ws)
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
+    assert K.filter_fallback_count(ws, n, d, 1, k) == 1
+
+
+def test_scan_topk_i8_nan_row_and_nan_query(K, oracle_mod):
+    n, d, k = 20_000, 384, 50
+    rng = np.random.default_rng(4)
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
+    x[77, 5] = np.nan  # a NaN row: never returned
+    q = oracle_mod.l2norm_rows(rng.standard_normal((2, d)).astype(np.float32), 0)
+    q[1, 0] = np.nan  # a NaN query: every slot (-inf, -1)
+    db = dev_rows(x)
+    s, i = _i8_search(K, db, None, n, d, dev_rows(q), k)
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    assert np.array_equal(i.cpu().numpy(), ri)
+    assert np.array_equal(s.cpu().numpy(), rs)
+
+
+def test_retrieve_one_buyer_takes_the_i8_pass(K):
+    """VectorDatabase.retrieve (the serving path) at d = 384 builds the int8 image with the
+    index and serves one-buyer calls through it: same answers as the bf16 path."""
+    from twotower import VectorDatabase
+
+    rng = np.random.default_rng(21)
+    n, d, k = 60_000, 384, 100
+    vdb = VectorDatabase(d)
+    vdb.build_index(rng.standard_normal((n, d)).astype(np.float32), [f"p{j}" for j in range(n)])
+    assert vdb.index.i8 is not None
+    q = rng.standard_normal((3, d)).astype(np.float32)
+    qd = vdb.normalize_queries(torch.from_numpy(q).cuda())
+    s16, i16 = vdb.index.search_device(qd, k, method="bf16")
+    for b in range(3):
+        got = vdb.retrieve(q[b], k=k)
+        assert [p for p, _ in got] == [f"p{j}" for j in i16[b].tolist()]
+        assert [v for _, v in got] == s16[b].tolist()

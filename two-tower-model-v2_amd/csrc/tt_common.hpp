@@ -53,6 +53,13 @@ inline int env_switch(const char*, int dflt) { return dflt; }
 
 // ----------------------------------------------------------------------------- device utils
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// a float >= v (v >= 0, finite): rounding UP of an f64 bound
+__device__ __forceinline__ float f64_up(double v) {
+  const float f = (float)v;
+  return (double)f >= v ? f : __uint_as_float(__float_as_uint(f) + 1u);
+}
 
 // XCD-aware block id: blocks b and b+8 run on the same XCD (observed placement, speed only).
 // Give every XCD a contiguous range of logical ids so that blocks sharing data (the slabs of

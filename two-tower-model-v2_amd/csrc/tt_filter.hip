@@ -557,7 +557,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
     slab = lb0 / n_qt;
     qt = lb0 % n_qt;
   }
-  const int lb = slab * n_qt + qt;
+  [[maybe_unused]] const int lb = slab * n_qt + qt;
   const int qbase = qt * QPB + w * QPW;
 #if TT_EXP_BLKTIME
   const unsigned long long blk_t0 = wall_clock64();
@@ -2391,6 +2391,448 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_topm(
 #undef TT_FTS
 }
 
+// ------------------------------------------------------ single pass on the int8 image (nq <= 4)
+// The one-buyer search reads the whole catalog image once, so its time is that image's bytes
+// (bf16: 768 MB at 1M x 384, ~124 us at 6.2 TB/s).  An int8 image (tt_i8_image: 64-row tiles
+// of codes n and one scale s) halves them.  The bound is looser than bf16's but still a
+// rigorous one: with the query coded per query as t m (t = max |q| / 127, m = rint(q / t)),
+//   |x.q - s t (n.m)| <= ||x - s n|| ||q|| + s ||n|| ||q - t m||
+// and a = fl(fl(n.m) fl(s t)) (n.m exact in i32 and in f32: |n.m| <= 384 * 127^2 < 2^24) adds
+// at most 2^-23 s ||n|| t ||m||, the canonical f32 chain at most E 2^-24 X ||q||:
+//   eps = 1.001 (R ||q|| + S ||q - t m|| + 2^-23 S (||q|| + ||q - t m||) + 1.01 E 2^-24 X ||q||)
+// with X, R, S the image's bounds (max ||x||, max ||x - s n||, max s ||n||; ~1, 0.0136, 1.003 on
+// unit rows): eps ~0.02 (bf16: ~0.004).
+// The stream, the per-(query, slab) streaming top-16 and the exact keys of the kept rows are
+// k_filter_topm's, on v_mfma_i32_16x16x64_i8 (64-row tiles: 24 KB, the bf16 ring's tile size).
+// The final certifies with exact scores instead of a band: a row a slab dropped has a <= tau_b
+// (the slab list's 16th approximate score), so its exact score s <= tau_b + eps.  If
+// max_b tau_b + eps < S_k, the k-th best EXACT score among the kept rows, no dropped row can
+// reach the top k, which is then the kept rows' exact top k.  Otherwise the query takes the
+// exact fallback.  (One eps instead of the band's two: on iid and Mode B queries the margin
+// S_k - max tau - eps is 0.015-0.03, tools/i8_sim in DESIGN 4.1c.)
+constexpr int I8_MAXTILES = 1024;  // 64-row scale tiles per block (rows_per_blk <= 65536)
+#ifndef TT_I8_SLOTS
+#define TT_I8_SLOTS 4  // ring slots of the int8 single pass (tiles in flight + 1)
+#endif
+TT_CHECK_EXP(TT_I8_SLOTS != 4, "TT_I8_SLOTS");
+#ifndef TT_I8_SWZ
+#define TT_I8_SWZ 1  // 0: XOR swizzle by r & 7 (2-way bank conflicts at E = 384), 1: by (r >> 1) & 7
+#endif
+TT_CHECK_EXP(TT_I8_SWZ != 1, "TT_I8_SWZ");
+#ifndef TT_I8_EXP_NOCOMP
+#define TT_I8_EXP_NOCOMP 0  // timing only (results WRONG): the int8 stream without compute
+#endif
+TT_CHECK_EXP(TT_I8_EXP_NOCOMP, "TT_I8_EXP_NOCOMP");
+// 16-B chunk swizzle of an int8 tile row r (XOR of the chunk index within aligned groups of
+// 8 / 16 chunks): the 16 rows a ds_read_b128 lane group reads must land in 16 different
+// 16-B bank groups.  E = 384: 24 chunks per row, 24 = 8 mod 16, so rows r and r + 1 are 8
+// bank groups apart -- XOR by (r >> 1) & 7 spreads each row pair over the other 8 (r & 7 put
+// rows r and r + 8 on one bank group).  E = 768: 48 chunks = 0 mod 16: XOR by r & 15.
+template <int EP>
+__device__ __forceinline__ int i8_swz(int r) {
+  return EP == 768 ? (r & 15) : TT_I8_SWZ ? ((r >> 1) & 7) : (r & 7);
+}
+
+template <int EP>
+__global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
+    const int8_t* __restrict__ xc, int64_t ldc, const float* __restrict__ scales, int64_t n,
+    const float* __restrict__ q, int nq, int64_t ldq, int rows_per_blk,
+    const float* __restrict__ db, int64_t ld, float X, float R, float S,
+    float* __restrict__ eps1, uint64_t* __restrict__ lists, uint64_t* __restrict__ xkeys,
+    int* __restrict__ counts, int* __restrict__ flags, int* __restrict__ qsel_n) {
+  static_assert(EP == 384 || EP == 768, "int8 single pass: E = 384 or 768");
+  constexpr int TR = 24576 / EP, KS = EP / 64, CPR = EP / 16, RB = TR / 16;
+  constexpr int TILE_B = TR * EP, PIECES = TILE_B / 1024, PPW = PIECES / TM_WAVES;
+  constexpr int SLOTS = TT_I8_SLOTS, PD = SLOTS - 1;
+  static_assert(PIECES % TM_WAVES == 0 && CPR % 16 == 8 * (EP == 384), "tile layout");
+  __shared__ __attribute__((aligned(16))) char smem[SLOTS * TILE_B + TM_NQ * TM_BUF * 8];
+  __shared__ int ncs[TM_NQ];
+  __shared__ float ssc[I8_MAXTILES];
+  char* ring = smem;
+  uint64_t* tbuf = (uint64_t*)(smem + SLOTS * TILE_B);  // [TM_NQ][TM_BUF]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int G = gridDim.x, blk = blockIdx.x;
+  if (blk == 0 && tid < nq) {  // per-query fallback state (FilterWs: flags, qsel, qsel_n, done)
+    flags[tid] = 0;
+    qsel_n[1 + tid] = 0;
+    if (tid == 0) *qsel_n = 0;
+  }
+  const int64_t j0 = (int64_t)blk * rows_per_blk;  // rows_per_blk: a multiple of 64
+  const int64_t j1 = (j0 + rows_per_blk < n) ? j0 + rows_per_blk : n;
+  const int n_tiles = j0 < j1 ? (int)((j1 - j0 + TR - 1) / TR) : 0;
+  for (int i = tid; i < (rows_per_blk >> 6); i += 64 * TM_WAVES) {
+    const int64_t st = (j0 >> 6) + i;
+    ssc[i] = st < ((n + 63) >> 6) ? scales[st] : 0.0f;
+  }
+
+  constexpr int CW = RB, TMB = TM_BUF / CW, CPER = TMB / 64;
+  static_assert(TMB % 64 == 0 && TMB >= 2 * TM_M && CW <= TM_WAVES, "top-m buffer shape");
+  const bool cw = w < CW && !TT_I8_EXP_NOCOMP;
+  uint64_t* wbuf = tbuf + (cw ? w : 0) * TM_NQ * TMB;
+  u32x4 qf[KS];
+  const bool qv = col < nq;
+  float tq = 0.0f;  // the query's code scale t
+  float tau = qv ? -__builtin_huge_valf() : __builtin_huge_valf();
+  int cnt = 0;
+  float tm[16], tmin = -__builtin_huge_valf();
+  if (cw) {
+    // the query (column col) coded as t m: lanes (g, col) hold chunks 4s + g, i.e. dims
+    // 64 s + 16 g .. + 15 -- the same chunk of every row the MFMA pairs them with
+    const float* qp = q + (int64_t)(qv ? col : 0) * ldq + 16 * g;
+    float mx = 0.0f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const f32x4 v = *(const f32x4*)(qp + 64 * s + 4 * u);
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    tq = mx / 127.0f;
+    double sq = 0.0, sd = 0.0;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      uint32_t wd[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const f32x4 v = *(const f32x4*)(qp + 64 * s + 4 * u);
+        uint32_t pk = 0u;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          int c = 0;
+          if (tq > 0.0f) {
+            c = (int)rintf(v[b] / tq);
+            c = c > 127 ? 127 : c < -127 ? -127 : c;
+          }
+          const double e = (double)v[b] - (double)tq * (double)c;
+          sq += (double)v[b] * (double)v[b];
+          sd += e * e;
+          pk |= ((uint32_t)(c & 0xff)) << (8 * b);
+        }
+        wd[u] = pk;
+      }
+      qf[s] = u32x4{wd[0], wd[1], wd[2], wd[3]};
+    }
+    sq += __shfl_xor(sq, 16, 64);
+    sd += __shfl_xor(sd, 16, 64);
+    sq += __shfl_xor(sq, 32, 64);
+    sd += __shfl_xor(sd, 32, 64);
+    if (blk == 0 && w == 0 && g == 0 && qv) {
+      const double nq2 = sqrt(sq) * 1.000001, nd = sqrt(sd) * 1.000001;
+      const double e = 1.001 * ((double)R * nq2 + (double)S * nd +
+                                1.1920928955078125e-07 * (double)S * (nq2 + nd) +
+                                1.01 * EP * 5.9604644775390625e-08 * (double)X * nq2);
+      eps1[col] = e == e ? f64_up(e) : __builtin_huge_valf();
+    }
+  }
+  wait_vm<0>();  // the query / scale loads and init stores retire before the ring's counted waits
+
+  const int64_t tile_bytes = ldc * TR;
+  const char* slab_base = (const char*)xc + j0 * ldc;
+  uint32_t voff[PPW];
+#pragma unroll
+  for (int pp = 0; pp < PPW; ++pp) {
+    const int P = (w + TM_WAVES * pp) * 64 + lane;
+    const int r = P / CPR;
+    voff[pp] = (uint32_t)(r * ldc) + 16u * (uint32_t)((P % CPR) ^ i8_swz<EP>(r));
+  }
+  auto issue = [&](int t) __attribute__((always_inline)) {
+    char* slot = ring + (t % SLOTS) * TILE_B;
+    const int64_t jt = j0 + (int64_t)t * TR;
+    const bool clamp = jt + TR > j1;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(slab_base + (int64_t)t * tile_bytes), 0, (int)tile_bytes, 0x00020000);
+#pragma unroll
+    for (int pp = 0; pp < PPW; ++pp) {
+      uint32_t off = voff[pp];
+      if (clamp) {  // rows past the slab end read a copy of its last row (masked below)
+        const int P = (w + TM_WAVES * pp) * 64 + lane;
+        const int r = P / CPR;
+        int64_t j = jt + r;
+        j = j < j1 ? j : j1 - 1;
+        off = (uint32_t)((j - jt) * ldc) + 16u * (uint32_t)((P % CPR) ^ i8_swz<EP>(r));
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(slot + (w + TM_WAVES * pp) * 1024), 16,
+          off, 0, 0, 2);
+    }
+  };
+  auto wait_tiles = [&](int younger) __attribute__((always_inline)) {
+    static_assert(PD <= 4, "wait_tiles covers up to 3 younger tiles");
+    if (younger >= 3) wait_vm<3 * PPW>();
+    else if (younger == 2) wait_vm<2 * PPW>();
+    else if (younger == 1) wait_vm<PPW>();
+    else wait_vm<0>();
+  };
+  uint32_t lrd[4];
+  {
+    const int r = 16 * (cw ? w : 0) + col, f = i8_swz<EP>(r), h = f >> 2;
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+      lrd[v] = lds_addr(ring) + 16 * (r * CPR + (g ^ (f & 3))) + 64 * (v ^ h);
+  }
+  static_assert(TM_M == 16, "wave_top16 keeps 16");
+  auto compact = [&](int c) __attribute__((always_inline)) {
+    uint64_t* b = wbuf + c * TMB;
+    const int cc = __shfl(cnt, c, 64);
+    uint64_t key[CPER];
+#pragma unroll
+    for (int r = 0; r < CPER; ++r) {
+      const int e = lane * CPER + r;
+      key[r] = e < cc ? b[e] : 0ull;
+    }
+    int nc;
+    const uint64_t k = wave_top16<CPER>(key, lane, b, &nc);
+    if (lane < nc) b[lane] = k;
+    const uint32_t hk = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(k >> 32), TM_M - 1);
+    if (col == c) {
+      cnt = nc;
+      if (nc == TM_M) tau = fmaxf(tau, key_float(hk));
+    }
+    wave_sync();
+  };
+  // appends and the tile-max bound of tau: k_filter_topm's (the scores arrive as f32 here)
+  auto appends = [&](const f32x4& acc, int t) __attribute__((always_inline)) {
+    const int64_t jt = j0 + (int64_t)t * TR + 16 * w;
+    const uint64_t colmask = 0x0001000100010001ull << col;
+    const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int64_t row = jt + 4 * g + jj;
+      const float v = acc[jj];
+      const bool pass = row < j1 && v >= tau;
+      const uint64_t bm = __ballot(pass);
+      if (bm != 0ull) {
+        const uint64_t mc = bm & colmask;
+        if (pass) {
+          const int pos = cnt + __popcll(mc & below);
+          lds_write64(lds_addr(wbuf + col * TMB + pos), make_key(v, (uint32_t)row));
+        }
+        cnt += __popcll(mc);
+      }
+    }
+    if (t == 0) {
+      const bool full = cnt == TM_M;
+      float v16[16];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        v16[jj] = acc[jj];
+        const auto x16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[jj]),
+                                                          __float_as_uint(acc[jj]), false, false);
+        v16[4 + jj] = __uint_as_float((g & 1) ? x16[0] : x16[1]);
+      }
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const auto x32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v16[jj]),
+                                                          __float_as_uint(v16[jj]), false, false);
+        v16[8 + jj] = __uint_as_float(lane < 32 ? x32[1] : x32[0]);
+      }
+      float mn = v16[0];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        tm[i] = full ? v16[i] : -__builtin_huge_valf();
+        mn = fminf(mn, v16[i]);
+      }
+      tmin = full ? mn : -__builtin_huge_valf();
+    } else {
+      float m = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3]));
+      const auto x16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m),
+                                                        false, false);
+      m = fmaxf(__uint_as_float(x16[0]), __uint_as_float(x16[1]));
+      const auto x32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m),
+                                                        false, false);
+      m = fmaxf(__uint_as_float(x32[0]), __uint_as_float(x32[1]));
+      if (m > tmin) {
+        bool done = false;
+        float mn = m;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const bool hit = !done && tm[i] == tmin;
+          tm[i] = hit ? m : tm[i];
+          done |= hit;
+          mn = fminf(mn, tm[i]);
+        }
+        tmin = mn;
+      }
+    }
+    tau = fmaxf(tau, qv ? tmin : tau);
+    const uint64_t need = __ballot(lane < 16 && cnt > TMB - 16);
+    if (need != 0ull) {
+      lds_wait<0>();
+      uint64_t nd = need;
+      while (nd) {
+        const int c = __builtin_ctzll(nd);
+        nd &= nd - 1;
+        compact(c);
+      }
+    }
+  };
+
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < PD && t < n_tiles; ++t) issue(t);
+  for (int t = 0; t < n_tiles; ++t) {
+    wait_tiles(n_tiles - 1 - t < PD - 1 ? n_tiles - 1 - t : PD - 1);
+    lds_barrier();  // tile t landed (every wave's pieces); every wave is done with tile t-1
+    if (t + PD < n_tiles) issue(t + PD);
+    if (cw) {
+      const uint32_t so = (uint32_t)((t % SLOTS) * TILE_B);
+      u32x4 fr[KS];
+      static_for<KS>([&](auto s_) __attribute__((always_inline)) {
+        constexpr int Sx = decltype(s_)::value;
+        fr[Sx] = lds_read128<256 * (Sx / 4)>(lrd[Sx % 4] + so);
+      });
+      // the tile's scale (its 64-row scale tile) x the query's t: one product per lane
+      const float st = ssc[(int)(((int64_t)t * TR) >> 6)] * tq;
+      if (t > 0) appends(acc, t - 1);
+      lds_wait<0>();
+      i32x4 ai = {0, 0, 0, 0};
+      static_for<KS>([&](auto s_) __attribute__((always_inline)) {
+        constexpr int Sx = decltype(s_)::value;
+        reg_tie(fr[Sx]);
+        ai = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, fr[Sx]),
+                                                   __builtin_bit_cast(i32x4, qf[Sx]), ai, 0, 0,
+                                                   0);
+      });
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) acc[jj] = (float)ai[jj] * st;
+    }
+  }
+  if (cw && n_tiles > 0) appends(acc, n_tiles - 1);
+  wait_vm<0>();
+  __shared__ int ncw[CW][TM_NQ];
+  if (cw && lane < nq && g == 0) ncw[w][lane] = cnt;
+  lds_wait<0>();
+  __syncthreads();
+  for (int c = w; c < nq; c += TM_WAVES) {
+    uint64_t key[CW * CPER];
+#pragma unroll
+    for (int wb = 0; wb < CW; ++wb) {
+      const int cc = ncw[wb][c];
+#pragma unroll
+      for (int r = 0; r < CPER; ++r) {
+        const int e = lane * CPER + r;
+        key[wb * CPER + r] = e < cc ? tbuf[(wb * TM_NQ + c) * TMB + e] : 0ull;
+      }
+    }
+    int nc;
+    const uint64_t k = wave_top16<CW * CPER>(key, lane, tbuf + c * TMB, &nc);
+    if (lane < nc) {
+      tbuf[c * TMB + lane] = k;
+      lists[((int64_t)c * G + blk) * TM_M + lane] = k;
+    }
+    if (lane == 0) {
+      counts[(int64_t)c * G + blk] = nc;
+      ncs[c] = nc;
+    }
+  }
+  __syncthreads();
+  for (int c = w; c < nq; c += TM_WAVES) {
+    const int nc = ncs[c], r16 = lane & 15, g4 = 4 * (lane >> 4);
+    if (nc == 0) continue;
+    const uint64_t* tb = tbuf + c * TMB;
+    const f32x4 ex =
+        exact16<EP>(db, ld, key_row(tb[r16 < nc ? r16 : 0]), q + (int64_t)c * ldq, lane);
+    if (r16 == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (g4 + j < nc)
+          xkeys[((int64_t)c * G + blk) * TM_M + g4 + j] =
+              ex[j] != ex[j] ? 0ull : make_key(ex[j], key_row(tb[g4 + j]));
+    }
+  }
+}
+
+// Final of the int8 single pass, one block per query: the union U of the G slab lists' exact
+// keys; S_k = the k-th best exact score of U (radix select on the exact keys); certified when
+// every full list's tau_b (its 16th approximate score) has tau_b + eps < S_k (see above);
+// then U's keys with score >= S_k are ranked into the output (ties at S_k by row).
+template <int EP>
+__global__ __launch_bounds__(SM_THREADS) void k_final_topm_i8(
+    const uint64_t* __restrict__ lists, const uint64_t* __restrict__ xkeys,
+    const int* __restrict__ counts, int G, int k, const float* __restrict__ eps1,
+    int* __restrict__ flags, int* qsel, int* qsel_n, int64_t n_rows, int64_t row_base,
+    float* __restrict__ out_s, int64_t* __restrict__ out_i) {
+  constexpr int PER = TM_CAP / SM_THREADS;
+  __shared__ SmallLdsT<1> s;
+  __shared__ BandLds<EP> bl;
+  __shared__ uint32_t taus[SM_WAVES];
+  const int qid = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t h[PER];
+  uint64_t xk[PER];
+  {
+    int cj[PER];
+    uint64_t kk[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int e = tid + j * SM_THREADS, b = e / TM_M;
+      const int64_t o = ((int64_t)qid * G + (b < G ? b : 0)) * TM_M + e % TM_M;
+      cj[j] = b < G ? counts[(int64_t)qid * G + b] : 0;
+      kk[j] = lists[o];
+      xk[j] = xkeys[o];
+    }
+    int mine = 0;
+    uint32_t tmax = 0u, hm = 0u;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = (tid + j * SM_THREADS) % TM_M;
+      const bool ok = i < cj[j];
+      if (!ok) xk[j] = 0ull;
+      h[j] = (uint32_t)(xk[j] >> 32);  // exact score (0: no key, or a NaN exact score)
+      if (ok && i == TM_M - 1) tmax = tmax > (uint32_t)(kk[j] >> 32) ? tmax : (uint32_t)(kk[j] >> 32);
+      mine += h[j] != 0u;
+      hm = hm > h[j] ? hm : h[j];
+    }
+    mine = wave_sum(mine);
+    tmax = wave_max_u32(tmax);
+    hm = wave_max_u32(hm);
+    if (lane == 0) {
+      s.wred[w] = mine;
+      s.wmax[w] = hm;
+      taus[w] = tmax;
+    }
+  }
+  __syncthreads();
+  int n_keys = 0;
+  uint32_t tau_max = 0u, hmax = 0u;
+#pragma unroll
+  for (int i = 0; i < SM_WAVES; ++i) {
+    n_keys += s.wred[i];
+    tau_max = tau_max > taus[i] ? tau_max : taus[i];
+    hmax = hmax > s.wmax[i] ? hmax : s.wmax[i];
+  }
+  if (n_keys < k) {  // (NaN query / rows, or too few kept rows) -> exact fallback
+    if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
+  const float Sk = key_float(small_radix_select(h, k, s, hmax));
+  // certification: a row dropped by slab b has exact score <= tau_b + eps (strictly below S_k)
+  if (tau_max != 0u && !(key_float(tau_max) + eps1[qid] < Sk)) {
+    if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
+  int pos;
+  const int nb = band_positions<EP>(h, Sk, bl, &pos);
+  if (nb > BAND_CAP) {
+    if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
+  bool bad_row = false;
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if (h[j] != 0u && key_float(h[j]) >= Sk) {
+      bad_row |= (int64_t)key_row(xk[j]) >= n_rows;
+      bl.sbuf[pos++] = xk[j];
+    }
+  if (__syncthreads_or(bad_row)) {
+    if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
+    return;
+  }
+  band_rank_out<EP>(bl, nb, qid, k, row_base, out_s, out_i);
+}
+
 // sharded finish: pcount[q][i] = #rows over ALL shards with a >= t_i (all-reduced SUM).
 // pcount[q][0] < k: the sample threshold did not certify -> exact fallback on every shard
 // (identical decision on all ranks).  Else A_k >= t* = the highest probe with >= k rows, so
@@ -3514,6 +3956,64 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
   // so it can never corrupt a later search on this thread
   g_plant_where = 0;
   return rc;
+}
+
+extern "C" int tt_scan_topk_i8f32(const float* db, const int8_t* db_i8, const float* tile_scales,
+                                  int64_t n, int32_t d, int64_t ld_db, int64_t ld_i8,
+                                  int64_t row_base, const float* q, int32_t nq, int64_t ld_q,
+                                  int32_t k, float x_norm_max, float x_resid_max, float s_max,
+                                  float* out_score, int64_t* out_idx, void* workspace,
+                                  int64_t workspace_bytes, void* stream, void* ev_start,
+                                  void* ev_stop) {
+  TT_REQUIRE(nq >= 0, "nq < 0");
+  if (nq == 0) return TT_OK;
+  TT_REQUIRE(db != nullptr && db_i8 != nullptr && tile_scales != nullptr && out_score &&
+                 out_idx, "null pointer");
+  const int ep = tt_padded_dim(d);
+  if (ep != 384 && ep != 768) return fail(TT_ERR_UNSUPPORTED, "int8 single pass: E 384 / 768");
+  if (nq > TM_NQ_RUN) return fail(TT_ERR_UNSUPPORTED, "int8 single pass: nq <= 4");
+  TT_REQUIRE(ld_i8 >= ep && ld_i8 % 16 == 0 && ((uintptr_t)db_i8 % 16) == 0,
+             "int8 image: ld_i8 >= tt_padded_dim(d), multiple of 16, 16-B aligned");
+  TT_REQUIRE(x_norm_max >= 0.0f && x_resid_max >= 0.0f && s_max >= 0.0f,
+             "bounds must be >= 0 (tt_i8_image)");
+  int epx;
+  FilterPlan p;
+  FilterWs w;
+  int rc = filter_setup(db, (const uint16_t*)db_i8, n, d, ld_db, q, nq, ld_q, k, workspace,
+                        workspace_bytes, &epx, &p, &w);
+  if (rc) return rc;
+  if (!p.topm) return fail(TT_ERR_UNSUPPORTED, "int8 single pass: not a single-pass plan");
+  const int G = device_cus();
+  TT_REQUIRE(p.max_slabs >= G, "topm plan: list region smaller than one list per CU");
+  const int64_t rpb = ((n + G - 1) / G + 63) / 64 * 64;
+  if (rpb / 64 > I8_MAXTILES) return fail(TT_ERR_UNSUPPORTED, "int8 single pass: n too large");
+  if (ld_i8 * (24576 / ep) > 0x7fffffffLL) return fail(TT_ERR_UNSUPPORTED, "int8: row too long");
+  hipStream_t st = (hipStream_t)stream;
+  uint64_t* xkeys = w.lists + (int64_t)nq * G * TM_M;
+  if (ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
+    return fail(TT_ERR_LAUNCH, "hipEventRecord(start)");
+  if (ep == 384)
+    hipLaunchKernelGGL(k_filter_topm_i8<384>, dim3(G), dim3(64 * TM_WAVES), 0, st, db_i8, ld_i8,
+                       tile_scales, n, q, nq, ld_q, (int)rpb, db, ld_db, x_norm_max, x_resid_max,
+                       s_max, w.eps2, w.lists, xkeys, w.counts, w.flags, w.qsel_n);
+  else
+    hipLaunchKernelGGL(k_filter_topm_i8<768>, dim3(G), dim3(64 * TM_WAVES), 0, st, db_i8, ld_i8,
+                       tile_scales, n, q, nq, ld_q, (int)rpb, db, ld_db, x_norm_max, x_resid_max,
+                       s_max, w.eps2, w.lists, xkeys, w.counts, w.flags, w.qsel_n);
+  if ((rc = check_launch("k_filter_topm_i8"))) return rc;
+  if (ev_stop && hipEventRecord((hipEvent_t)ev_stop, st) != hipSuccess)
+    return fail(TT_ERR_LAUNCH, "hipEventRecord(stop)");
+  if (ep == 384)
+    hipLaunchKernelGGL(k_final_topm_i8<384>, dim3(nq), dim3(SM_THREADS), 0, st, w.lists, xkeys,
+                       w.counts, G, k, w.eps2, w.flags, w.qsel, w.qsel_n, n, row_base, out_score,
+                       out_idx);
+  else
+    hipLaunchKernelGGL(k_final_topm_i8<768>, dim3(nq), dim3(SM_THREADS), 0, st, w.lists, xkeys,
+                       w.counts, G, k, w.eps2, w.flags, w.qsel, w.qsel_n, n, row_base, out_score,
+                       out_idx);
+  if ((rc = check_launch("k_final_topm_i8"))) return rc;
+  return scan_f32_select_fused(db, n, d, ld_db, row_base, q, nq, ld_q, k, w.qsel, w.qsel_n,
+                               w.done, out_score, out_idx, w.scan_ws, w.scan_ws_bytes, st);
 }
 
 // ------------------------------------------------------------------ sharded (multi-GPU)

@@ -117,7 +117,90 @@ __global__ __launch_bounds__(256) void k_bf16_bounds(const float* __restrict__ x
     atomicMax((unsigned int*)&out2[1], __float_as_uint(br));
   }
 }
+// int8 image of the catalog for the single-pass small-batch filter (tt_scan_topk_i8f32):
+// per 64-row tile one scale s = max |x| / 127 over the tile's finite values, codes
+// n = rint(x / s) in [-127, 127] (0 where s == 0 or x is not finite), padding columns zero.
+// Bounds (max-combined into out3, every one rounded UP, accumulated in f64; rows with a
+// non-finite value are skipped -- their scores are NaN and never returned):
+//   out3[0] >= max_r ||x_r||, out3[1] >= max_r ||x_r - s n_r||, out3[2] >= max_r s ||n_r||.
+// One block per tile: pass 1 the tile maximum, pass 2 one wave per row.
+__global__ __launch_bounds__(256) void k_i8_image(const float* __restrict__ x, int64_t n, int d,
+                                                  int64_t ld, int8_t* __restrict__ codes,
+                                                  int64_t ldc, float* __restrict__ scales,
+                                                  float* out3) {
+  __shared__ float wmax[4];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  const int nr = n - r0 < 64 ? (int)(n - r0) : 64;
+  float m = 0.0f;
+  for (int r = w; r < nr; r += 4) {
+    const float* xr = x + (r0 + r) * ld;
+    for (int i = lane; i < d; i += 64) {
+      const float a = fabsf(xr[i]);
+      if (a <= 3.4e38f) m = fmaxf(m, a);  // finite values only
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if (lane == 0) wmax[w] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+  const float s = m / 127.0f;
+  if (threadIdx.x == 0) scales[blockIdx.x] = s;
+  double bx = 0.0, br = 0.0, bs = 0.0;
+  for (int r = w; r < nr; r += 4) {
+    const float* xr = x + (r0 + r) * ld;
+    int8_t* cr = codes + (r0 + r) * ldc;
+    double sx = 0.0, sr = 0.0, sn = 0.0;
+    bool fin = true;
+    for (int i = lane; i < ldc; i += 64) {
+      int c = 0;
+      if (i < d) {
+        const float v = xr[i];
+        fin &= fabsf(v) <= 3.4e38f;
+        if (s > 0.0f && fabsf(v) <= 3.4e38f) {
+          c = (int)rintf(v / s);
+          c = c > 127 ? 127 : c < -127 ? -127 : c;
+        }
+        const double e = (double)v - (double)s * (double)c;
+        sx += (double)v * (double)v;
+        sr += e * e;
+        sn += (double)c * (double)c;
+      }
+      cr[i] = (int8_t)c;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      sx += __shfl_xor(sx, o, 64);
+      sr += __shfl_xor(sr, o, 64);
+      sn += __shfl_xor(sn, o, 64);
+    }
+    if (__ballot(!fin) == 0ull) {
+      bx = fmax(bx, sx);
+      br = fmax(br, sr);
+      bs = fmax(bs, (double)s * (double)s * sn);
+    }
+  }
+  if (lane == 0) {
+    // sqrt in f64 of sums of f64 squares (relative error ~1e-15), then rounded up, x1.000001
+    atomicMax((unsigned int*)&out3[0], __float_as_uint(f64_up(sqrt(bx) * 1.000001)));
+    atomicMax((unsigned int*)&out3[1], __float_as_uint(f64_up(sqrt(br) * 1.000001)));
+    atomicMax((unsigned int*)&out3[2], __float_as_uint(f64_up(sqrt(bs) * 1.000001)));
+  }
+}
 }  // namespace tt
+
+extern "C" int tt_i8_image(const float* x, int64_t n, int32_t d, int64_t ld, int8_t* codes,
+                           int64_t ld_codes, float* tile_scales, float* out3, void* stream) {
+  using namespace tt;
+  TT_REQUIRE(n >= 0 && d >= 1 && ld >= d && ld_codes >= d, "need n >= 0, 1 <= d <= ld, ld_codes");
+  TT_REQUIRE(out3 != nullptr, "out3 == NULL");
+  if (n == 0) return TT_OK;
+  TT_REQUIRE(x != nullptr && codes != nullptr && tile_scales != nullptr, "null pointer");
+  const int64_t tiles = (n + 63) / 64;
+  TT_REQUIRE(tiles < (1ll << 31), "too many rows");
+  hipLaunchKernelGGL(k_i8_image, dim3((unsigned)tiles), dim3(256), 0, (hipStream_t)stream, x, n,
+                     d, ld, codes, ld_codes, tile_scales, out3);
+  return check_launch("tt_i8_image");
+}
 
 extern "C" int tt_bf16_image_bounds(const float* x, const uint16_t* x_bf16, int64_t n,
                                     int32_t d, int64_t ld, float* out2, void* stream) {

@@ -89,6 +89,10 @@ SIGNATURES = {
     "tt_sharded_filter_finish": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _i64, _vp, _i32,
                                                 _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
     "tt_bf16_image_bounds": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _vp, _vp]),
+    "tt_i8_image": (ctypes.c_int, [_vp, _i64, _i32, _i64, _vp, _i64, _vp, _vp, _vp]),
+    "tt_scan_topk_i8f32": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _i64, _i64, _i64, _vp, _i32,
+                                          _i64, _i32, ctypes.c_float, ctypes.c_float,
+                                          ctypes.c_float, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
     "tt_topk_merge_f32": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp]),
     "tt_weighted_avg_l2_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _i64, _vp]),
     "tt_gather_weighted_avg_l2_f32": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp, _i64,

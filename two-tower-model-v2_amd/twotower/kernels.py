@@ -231,6 +231,57 @@ def scan_topk_bf16(db: torch.Tensor, db16: torch.Tensor, n: int, d: int, q: torc
     return out
 
 
+I8_DIMS = (384, 768)  # padded dims of the int8 single pass (tt_scan_topk_i8f32)
+I8_NQ_MAX = 4
+
+
+def i8_image(x: torch.Tensor, d: int, out3: torch.Tensor = None):
+    """The int8 image of a normalised catalog x [n, ep] f32 (tt_i8_image): codes [n, ep] int8,
+    per-64-row-tile scales [ceil(n / 64)] f32 and the bounds (max ||x||, max ||x - s n||,
+    max s ||n||) max-combined into out3 (device [3] f32)."""
+    _check_2d(x, "x")
+    n, ep = x.shape
+    codes = torch.empty((n, ep), dtype=torch.int8, device=x.device)
+    scales = torch.empty(max((n + 63) // 64, 1), dtype=_f32, device=x.device)
+    if out3 is None:
+        out3 = torch.zeros(3, dtype=_f32, device=x.device)
+    check(lib().tt_i8_image(_ptr(x), n, d, x.stride(0), _ptr(codes), codes.stride(0),
+                            _ptr(scales), _ptr(out3), stream_ptr()), "tt_i8_image")
+    return codes, scales, out3
+
+
+def scan_topk_i8(db: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, n: int, d: int,
+                 q: torch.Tensor, k: int, bounds3, row_base: int = 0,
+                 workspace: torch.Tensor = None, out=None, events=(None, None)):
+    """Exact top-k (bit-identical to scan_topk) for nq <= 4 through the int8 single pass
+    (tt_scan_topk_i8f32): padded dim 384 / 768, k <= 128.  bounds3 = i8_image's out3 as host
+    floats."""
+    _check_2d(db, "db")
+    _check_2d(q, "q")
+    if codes.dtype != torch.int8 or codes.dim() != 2 or codes.shape[0] < n:
+        raise ValueError("codes must be the int8 image [n, ep] of db (i8_image)")
+    nq = q.shape[0]
+    if not (1 <= k <= min(n, FILTER_KMAX)) or nq > I8_NQ_MAX:
+        raise ValueError(f"scan_topk_i8: need 1 <= k ({k}) <= min(n, 128) and nq <= 4")
+    if out is None:
+        out = (torch.empty((nq, k), dtype=_f32, device=q.device),
+               torch.empty((nq, k), dtype=torch.int64, device=q.device))
+    if nq == 0:
+        return out
+    need = filter_workspace_bytes(n, d, nq, k)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=q.device)
+    X, R, S = (float(v) for v in bounds3)
+    e0, e1 = events
+    check(lib().tt_scan_topk_i8f32(
+        _ptr(db), _ptr(codes), _ptr(scales), n, d, db.stride(0), codes.stride(0), row_base,
+        _ptr(q), nq, q.stride(0), k, ctypes.c_float(X), ctypes.c_float(R), ctypes.c_float(S),
+        _ptr(out[0]), _ptr(out[1]), _ptr(workspace), workspace.numel(), stream_ptr(),
+        e0.cuda_event if e0 is not None else None, e1.cuda_event if e1 is not None else None),
+        "tt_scan_topk_i8f32")
+    return out
+
+
 class PreparedSearch:
     """scan_topk_bf16 for a fixed (catalog, nq, k): validation, workspace, output buffers and
     the C arguments are set up once, so a call is one ctypes call (the serving pattern: the
@@ -239,7 +290,9 @@ class PreparedSearch:
     Returns the same (scores, ids) tensors on every call (overwritten in place)."""
 
     def __init__(self, db: torch.Tensor, db16: torch.Tensor, n: int, d: int, nq: int, k: int,
-                 bounds, row_base: int = 0):
+                 bounds, row_base: int = 0, i8=None):
+        """i8 = (codes, scales, bounds3) from i8_image: nq <= 4 at padded dim 384 / 768 then
+        runs the int8 single pass (tt_scan_topk_i8f32, same results)."""
         _check_2d(db, "db")
         _check_2d(db16, "db16", torch.bfloat16)
         if db16.shape[0] < n or db16.stride(0) != db.stride(0):
@@ -257,6 +310,16 @@ class PreparedSearch:
         self._head = (_ptr(db), _ptr(db16), n, d, db.stride(0), row_base)
         self._tail = (k, ctypes.c_float(x_norm_max), ctypes.c_float(x_resid_max),
                       _ptr(self.out[0]), _ptr(self.out[1]), _ptr(self.ws), self.ws.numel())
+        self.i8 = i8 is not None and nq <= I8_NQ_MAX and self.ld_q in I8_DIMS
+        if self.i8:
+            codes, scales, b3 = i8
+            X, R, S = (float(v) for v in b3)
+            self._keep = (codes, scales)
+            self._fn = lib().tt_scan_topk_i8f32
+            self._head = (_ptr(db), _ptr(codes), _ptr(scales), n, d, db.stride(0),
+                          codes.stride(0), row_base)
+            self._tail = (k, ctypes.c_float(X), ctypes.c_float(R), ctypes.c_float(S),
+                          _ptr(self.out[0]), _ptr(self.out[1]), _ptr(self.ws), self.ws.numel())
 
     def __call__(self, q: torch.Tensor):
         if (q.shape != (self.nq, self.ld_q) or q.dtype != _f32 or q.device != self.db.device

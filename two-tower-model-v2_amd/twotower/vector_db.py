@@ -46,6 +46,7 @@ class FlatIPIndex:
         self._bounds_dev = torch.zeros(2, dtype=torch.float32, device=self.device)
         self.bounds = (0.0, 0.0)
         self.ntotal = 0
+        self.i8 = None  # int8 image (codes, tile scales, bounds) for nq <= 4 searches
         self._ws = _lib.StreamWorkspaces(4)  # search_device's workspace, one per HIP stream
         # host searches (the /retrieve path, FlatIPIndex.search_host): serving slots, each with
         # its own HIP stream, device query / output buffers, pinned host staging and filter
@@ -74,9 +75,25 @@ class FlatIPIndex:
         if self.ntotal:
             rows = torch.cat([self.xb[: self.ntotal], rows])
             rows16 = torch.cat([self.xb16[: self.ntotal], rows16])
-        with self._lock:  # searches read (xb, xb16, ntotal, bounds) as one snapshot
+        i8 = self._i8_image(rows)
+        with self._lock:  # searches read (xb, xb16, ntotal, bounds, i8) as one snapshot
             self.xb, self.xb16 = rows, rows16
             self.ntotal = rows.shape[0]
+            self.i8 = i8
+
+    def _i8_image(self, rows: torch.Tensor):
+        """(codes, tile scales, bounds) of the int8 single pass for one-buyer searches
+        (kernels.i8_image; padded dims 384 / 768), or None."""
+        if self.ep not in kernels.I8_DIMS or rows.shape[0] == 0:
+            return None
+        codes, scales, b3 = kernels.i8_image(rows, self.d)
+        return codes, scales, tuple(b3.tolist())
+
+    def build_i8(self) -> None:
+        """(Re)build the int8 image of the current rows (for an index whose xb was set
+        directly rather than through add)."""
+        with self._lock:
+            self.i8 = self._i8_image(self.xb[: self.ntotal])
 
     # faiss-style add of ALREADY-normalised float32 rows (host or device)
     def add(self, x) -> None:
@@ -103,9 +120,9 @@ class FlatIPIndex:
     def search_device(self, q: torch.Tensor, k: int, method: str = "auto"):
         """q: [nq, ep] normalised device rows -> (scores [nq,k], labels [nq,k]) on device.
 
-        method "auto": bf16 filter + exact f32 re-rank for k <= 128, else exact f32 scores +
-        radix select (k <= 1024); "f32" / "bf16" force the f32 scan / the filter.  All give
-        bit-identical results."""
+        method "auto": bf16 filter + exact f32 re-rank for k <= 128 (nq <= 4 at padded dim 384 /
+        768: the int8 single pass), else exact f32 scores + radix select (k <= 1024); "f32" /
+        "bf16" force the f32 scan / the bf16 filter.  All give bit-identical results."""
         if k < 1:
             raise RuntimeError("Error: 'k > 0' failed")  # faiss' own assertion text
         use_bf16 = method == "bf16" or (method == "auto" and k <= kernels.FILTER_KMAX)
@@ -122,6 +139,11 @@ class FlatIPIndex:
             need = kernels.scan_workspace_bytes(self.ntotal, self.d, q.shape[0], k)
         with self._lock:  # the workspace cache is shared; the outputs are fresh per call
             ws = self._ws.get(need, self.device)
+            if (use_bf16 and method == "auto" and self.i8 is not None
+                    and q.shape[0] <= kernels.I8_NQ_MAX):  # one-buyer calls: the int8 pass
+                codes, scales, b3 = self.i8
+                return kernels.scan_topk_i8(self.xb, codes, scales, self.ntotal, self.d, q, k, b3,
+                                            row_base=self.row_base, workspace=ws)
             if use_bf16:
                 return kernels.scan_topk_bf16(self.xb, self.xb16, self.ntotal, self.d, q, k,
                                               self.bounds, row_base=self.row_base, workspace=ws)
@@ -162,7 +184,7 @@ class FlatIPIndex:
             raise ValueError(f"search: expected [nq, {self.d}] float32 queries")
         nq = x.shape[0]
         with self._lock:  # one consistent catalog state for this call
-            state = (self.xb, self.xb16, self.ntotal, self.bounds)
+            state = (self.xb, self.xb16, self.ntotal, self.bounds, self.i8)
         if nq == 0 or not (1 <= k <= state[2]):
             q = torch.zeros((nq, self.ep), dtype=torch.float32, device=self.device)
             q[:, : self.d] = torch.from_numpy(x).to(self.device)
@@ -178,7 +200,7 @@ class FlatIPIndex:
     def _run_batch(self, x: np.ndarray, k: int, normalize: bool, state=None):
         if state is None:
             with self._lock:
-                state = (self.xb, self.xb16, self.ntotal, self.bounds)
+                state = (self.xb, self.xb16, self.ntotal, self.bounds, self.i8)
         slot = self._checkout(x.shape[0])
         try:
             return slot.run(x, k, normalize, state)
@@ -231,7 +253,7 @@ class FlatIPIndex:
             self.coalesce_stats[1] += len(batch)
             try:
                 with self._lock:
-                    state = (self.xb, self.xb16, self.ntotal, self.bounds)
+                    state = (self.xb, self.xb16, self.ntotal, self.bounds, self.i8)
                 kk = min(kk, state[2])
                 xs = np.concatenate([r.x for r in batch]) if len(batch) > 1 else batch[0].x
                 s, i = self._run_batch(xs, kk, head.normalize, state)
@@ -348,18 +370,30 @@ class _ServingSlot:
         so other serving threads run their host work meanwhile.  ~25% less host time per call
         than the torch-op form."""
         ix = self.ix
-        xb, xb16, n, bounds = state
+        xb, xb16, n, bounds, i8 = state
         nq, d = x.shape
         ws = self._workspace(n, nq, k, "bf16")
-        akey = (skey, nq, k, ws.data_ptr(), self.s.data_ptr(), bounds, normalize)
+        use8 = i8 is not None and nq <= kernels.I8_NQ_MAX
+        akey = (skey, nq, k, ws.data_ptr(), self.s.data_ptr(), bounds, normalize, use8)
         if akey != self.args_key:  # the C arguments, bound once per (state, nq, k)
             vp = ctypes.c_void_p
             qp, st = vp(self.q.data_ptr()), vp(self.stream.cuda_stream)
-            self.args = (
-                vp(xb.data_ptr()), vp(xb16.data_ptr()), n, d, xb.stride(0), ix.row_base, qp, nq,
-                self.q.stride(0), k, ctypes.c_float(bounds[0]), ctypes.c_float(bounds[1]),
-                vp(self.s.data_ptr()), vp(self.i.data_ptr()), vp(ws.data_ptr()), ws.numel(), st,
-                None, None)
+            if use8:  # the int8 single pass (one-buyer /retrieve calls, nq <= 4)
+                codes, scales, (X, R, S) = i8
+                self.fn = _lib.lib().tt_scan_topk_i8f32
+                self.args = (
+                    vp(xb.data_ptr()), vp(codes.data_ptr()), vp(scales.data_ptr()), n, d,
+                    xb.stride(0), codes.stride(0), ix.row_base, qp, nq, self.q.stride(0), k,
+                    ctypes.c_float(X), ctypes.c_float(R), ctypes.c_float(S),
+                    vp(self.s.data_ptr()), vp(self.i.data_ptr()), vp(ws.data_ptr()), ws.numel(),
+                    st, None, None)
+            else:
+                self.fn = _lib.lib().tt_scan_topk_bf16f32
+                self.args = (
+                    vp(xb.data_ptr()), vp(xb16.data_ptr()), n, d, xb.stride(0), ix.row_base, qp,
+                    nq, self.q.stride(0), k, ctypes.c_float(bounds[0]),
+                    ctypes.c_float(bounds[1]), vp(self.s.data_ptr()), vp(self.i.data_ptr()),
+                    vp(ws.data_ptr()), ws.numel(), st, None, None)
             self.h2d = (qp, ctypes.c_size_t(self.q.stride(0) * 4), vp(self.qh.data_ptr()),
                         ctypes.c_size_t(d * 4), ctypes.c_size_t(d * 4), ctypes.c_size_t(nq), 1, st)
             self.norm = ((qp, nq, d, self.q.stride(0), qp, self.q.stride(0), None,
@@ -377,18 +411,18 @@ class _ServingSlot:
             _lib.check(self.norm_fn(*self.norm), "tt_l2norm_rows_f32")
         rc = self.fn(*self.args)
         if rc:
-            _lib.check(rc, "tt_scan_topk_bf16f32")
+            _lib.check(rc, "tt_scan_topk_i8f32" if use8 else "tt_scan_topk_bf16f32")
         for a in self.d2h:
             if hip.hipMemcpyAsync(*a):
                 raise RuntimeError("hipMemcpyAsync (results) failed")
-        if hip.hipStreamSynchronize(self.args[16]):
+        if hip.hipStreamSynchronize(self.args[-3]):
             raise RuntimeError("hipStreamSynchronize failed")
         return (self.sh_np[: nq * k].reshape(nq, k).copy(),
                 self.ih_np[: nq * k].reshape(nq, k).copy())
 
     def run(self, x: np.ndarray, k: int, normalize: bool, state):
         ix = self.ix
-        xb, xb16, n, bounds = state
+        xb, xb16, n, bounds, _ = state
         nq, d = x.shape
         if k > self.kc:
             self._outs(k, torch.cuda.is_available())
