@@ -279,7 +279,7 @@ def configs1(a, dev, rank):
     return out
 
 
-def batch_sweep(a, shard, shard16, n, E, K, bounds, dev):
+def batch_sweep(a, shard, shard16, n, E, K, bounds, dev, i8=None):
     """SURVEY.md 8(d) query-batch sweep over the 1M x 384 catalog (vector_db.py:160,197):
     end-to-end search time per call (every launch of tt_scan_topk_bf16f32, queries resident;
     kernels.PreparedSearch as the serving path calls it, the per-call wrapper beside it) and
@@ -311,27 +311,41 @@ def batch_sweep(a, shard, shard16, n, E, K, bounds, dev):
             tot.append(ev[2].elapsed_time(ev[3]))
             lvl.append(ev[0].elapsed_time(ev[1]))
         tw, l_ = float(np.median(tot)), float(np.median(lvl))
-        # end to end through the serving path (one PreparedSearch call per batch)
-        ps = kernels.PreparedSearch(shard, shard16, n, E, B, K, bounds)
-        for _ in range(3):
-            ps(q)
-        prep = []
-        for _ in range(21):
-            torch.cuda.synchronize()
-            ev[2].record(stream)
-            ps(q)
-            ev[3].record(stream)
-            torch.cuda.synchronize()
-            prep.append(ev[2].elapsed_time(ev[3]))
-        del ps
-        t = float(np.median(prep))
-        # bytes the search actually streams: the bf16 image once (the full level; the sample
-        # level, selection and re-rank add ~5% and are not counted), so frac <= 1
-        res[str(B)] = {"ms_per_search": t, "queries_per_s": B / (t * 1e-3),
+        # end to end through the serving path (one PreparedSearch call per batch; nq <= 4 takes
+        # the int8 single pass when the catalog has its image, same results)
+        def prepared(i8_):
+            ps = kernels.PreparedSearch(shard, shard16, n, E, B, K, bounds, i8=i8_)
+            for _ in range(3):
+                ps(q)
+            prep = []
+            for _ in range(21):
+                torch.cuda.synchronize()
+                ev[2].record(stream)
+                ps(q)
+                ev[3].record(stream)
+                torch.cuda.synchronize()
+                prep.append(ev[2].elapsed_time(ev[3]))
+            return float(np.median(prep)), ps.i8, (ps.out[0].clone(), ps.out[1].clone())
+
+        t16, _, o16 = prepared(None)
+        t, extra = t16, {}
+        if i8 is not None and B <= kernels.I8_NQ_MAX:
+            t8, used, o8 = prepared(i8)
+            if used:
+                assert torch.equal(o8[0], o16[0]) and torch.equal(o8[1], o16[1])
+                b8 = float(n * ep + 4 * ((n + 63) // 64))  # codes + tile scales, read once
+                t = t8
+                extra = {"pass": "int8 single pass (bit-identical to the bf16 pass)",
+                         "bf16_pass_ms_per_search": t16, "int8_pass_bytes": b8,
+                         "int8_pass_frac_end_to_end": b8 / (t8 * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+        # bytes the bf16 pass streams: the bf16 image once (the full level; the sample level,
+        # selection and re-rank add ~5% and are not counted), so frac <= 1
+        res[str(B)] = {"ms_per_search": t, "queries_per_s": B / (t * 1e-3), **extra,
                        "wrapper_ms_per_search": tw, "full_level_ms": l_,
                        "bf16_pass_bytes": 2.0 * n * ep,
-                       "bf16_pass_gbps_end_to_end": 2.0 * n * ep / (t * 1e-3) / 1e9,
-                       "bf16_pass_frac_end_to_end": 2.0 * n * ep / (t * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                       "bf16_pass_gbps_end_to_end": 2.0 * n * ep / (t16 * 1e-3) / 1e9,
+                       "bf16_pass_frac_end_to_end":
+                           2.0 * n * ep / (t16 * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                        "full_level_frac": 2.0 * n * ep / (l_ * 1e-3) / 1e9 / HBM_PEAK_GBPS}
         del ws
     # k in (128, 1000] (the /retrieve cap, server.py:46): nq = 1, 32 at k = 1000 through the
@@ -594,6 +608,9 @@ def summary(result):
     sb = result.get("single_buyer_search")
     if sb:
         s["one_buyer_ms"] = _sig(sb["ms_per_search"])
+        if "bf16_pass_ms_per_search" in sb:
+            s["one_buyer_bf16_pass_ms"] = _sig(sb["bf16_pass_ms_per_search"])
+            s["one_buyer_int8_stream_frac"] = _sig(sb["int8_stream_frac"])
         s["one_buyer_api_ms"] = _sig(sb["api_ms_per_call"])
         s["one_buyer_api_e2e_ms"] = _sig(sb["api_e2e_ms_per_buyer"])
         s["one_buyer_api_k1000_ms"] = _sig(sb["api_k1000_ms_per_call"])
@@ -637,6 +654,7 @@ def single_buyer_api(a, dev, shard, shard16, n, E, K, bounds, table, hist, w, re
     idx = FlatIPIndex(E, device=dev)
     idx.xb, idx.xb16, idx.ntotal = shard, shard16, n
     idx.bounds = tuple(bounds)
+    idx.build_i8()
     vdb = VectorDatabase(E)
     vdb.index = idx
     vdb.product_ids = [f"product_{i}" for i in range(n)]
@@ -1062,23 +1080,57 @@ def main():
             tot.append(ev[2].elapsed_time(ev[3]))
             lvl.append(ev[0].elapsed_time(ev[1]))
         lvl_ms = statistics.median(lvl)
+        # the int8 single pass the serving path takes for nq <= 4 (tt_scan_topk_i8f32, same
+        # results): its image is built once per catalog, like the bf16 one
+        i8 = kernels.i8_image(shard, E) if ep in kernels.I8_DIMS else None
+        i8_lvl = []
+        if i8 is not None:
+            for r in range(n1 + 3):
+                kernels.scan_topk_i8(shard, i8[0], i8[1], hi - lo, E, q1, K, i8[2].tolist(),
+                                     row_base=lo, workspace=ws1, events=(ev[0], ev[1]))
+                torch.cuda.synchronize()
+                if r >= 3:
+                    i8_lvl.append(ev[0].elapsed_time(ev[1]))
+            i8_fb = kernels.filter_fallback_count(ws1, hi - lo, E, 1, K)
+
         # the device search as the serving path binds it (kernels.PreparedSearch: one C call per
         # buyer, outputs / workspace bound once); median of 21 synchronised calls
-        ps = kernels.PreparedSearch(shard, shard16, hi - lo, E, 1, K, bounds, row_base=lo)
-        for _ in range(3):
-            ps(q1)
-        prep = []
-        for _ in range(n1):
-            ev[2].record(stream)
-            ps(q1)
-            ev[3].record(stream)
-            torch.cuda.synchronize()
-            prep.append(ev[2].elapsed_time(ev[3]))
-        del ps
+        def prepared(i8_):
+            ps = kernels.PreparedSearch(shard, shard16, hi - lo, E, 1, K, bounds, row_base=lo,
+                                        i8=i8_)
+            for _ in range(3):
+                ps(q1)
+            prep = []
+            for _ in range(n1):
+                ev[2].record(stream)
+                ps(q1)
+                ev[3].record(stream)
+                torch.cuda.synchronize()
+                prep.append(ev[2].elapsed_time(ev[3]))
+            o = (ps.out[0].clone(), ps.out[1].clone())
+            return statistics.median(prep), o
+
+        bf16_ms, o16 = prepared(None)
+        one_ms, o1 = prepared(i8) if i8 is not None else (bf16_ms, o16)
+        assert torch.equal(o1[0], o16[0]) and torch.equal(o1[1], o16[1]), "int8 != bf16 pass"
         api = single_buyer_api(a, dev, shard, shard16, hi - lo, E, K, bounds, table, hist, w)
+        i8_info = {}
+        if i8 is not None:
+            i8_ms = statistics.median(i8_lvl)
+            i8_bytes = float((hi - lo) * ep + 4 * ((hi - lo + 63) // 64))
+            i8_info = {"bf16_pass_ms_per_search": bf16_ms, "int8_stream_ms": i8_ms,
+                       "int8_stream_bytes": i8_bytes,
+                       "int8_stream_gbps": i8_bytes / (i8_ms * 1e-3) / 1e9,
+                       "int8_stream_frac": i8_bytes / (i8_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                       "int8_fallback_queries": int(i8_fb),
+                       "int8_same_as_bf16_pass": True}
         result["single_buyer_search"] = {
-            "nq": 1, "ms_per_search": statistics.median(prep),
-            "ms_per_search_is": "kernels.PreparedSearch device call (no host copies)",
+            "nq": 1, "ms_per_search": one_ms,
+            "ms_per_search_is": ("kernels.PreparedSearch device call (no host copies); the int8 "
+                                 "single pass (nq <= 4), bit-identical to the bf16 pass"
+                                 if i8 is not None else
+                                 "kernels.PreparedSearch device call (no host copies)"),
+            **i8_info,
             **api,
             "timing": "median of 21 synchronised calls, HIP events on the launch stream",
             "wrapper_ms_per_search": statistics.median(tot), "full_level_ms": lvl_ms,
@@ -1094,7 +1146,8 @@ def main():
         result["mode_a"], cpu_a = mode_a(a, dev, world, rank, lambda qall: local_search_k(qall),
                                          K, E)
     if world == 1 and not a.no_extra:
-        result["batch_sweep"] = batch_sweep(a, shard, shard16, hi - lo, E, K, bounds, dev)
+        result["batch_sweep"] = batch_sweep(a, shard, shard16, hi - lo, E, K, bounds, dev,
+                                            i8=i8 if a.method == "bf16" else None)
         if a.mode_a_buyers > 0 and a.mode_a_prec == "x3":
             # beside the parity-precision (x3) Mode A: the bf16 encoder (throughput mode, below
             # the reference's f32 precision) and one step of the f32 MFMA encoder

@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out/r05o
+for nq in 1 4; do
+NQ=$nq TWOTOWER_HIP_LIB=$PWD/two-tower-model-v2_amd/lib/variants/lib_clk.so timeout -k 10 120 python -u tools/i8clk.py > gpurun_out/r05o/clk_nq$nq.json 2>gpurun_out/r05o/clk.err || exit 1
+python -c "import json; print(json.dumps(json.load(open('gpurun_out/r05o/clk_nq$nq.json'))))"
+done

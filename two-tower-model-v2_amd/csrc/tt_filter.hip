@@ -1962,6 +1962,24 @@ constexpr int TM_M = 16;      // rows kept per (query, slab)
 constexpr int TM_BUF = 256;   // candidate buffer per query, split over the compute waves
 constexpr int TM_SLOTS = TT_EXP_TM_SLOTS, TM_PD = TM_SLOTS - 1;  // ring slots, tiles in flight
 constexpr int TM_WAVES = 8;
+#ifndef TT_TM_ANYB
+#define TT_TM_ANYB 1  // 1: one ballot per tile skips a wave's appends when no row passes tau
+#endif
+TT_CHECK_EXP(TT_TM_ANYB != 1, "TT_TM_ANYB");
+#ifndef TT_TM_BIGBUF16
+#define TT_TM_BIGBUF16 0  // 1: k_filter_topm's buffers hold TM_NQ_RUN queries, as the int8 pass's
+#endif
+TT_CHECK_EXP(TT_TM_BIGBUF16 != 0, "TT_TM_BIGBUF16");
+// queries the single passes' candidate buffers hold.  They run for nq <= TM_NQ_RUN only, so the
+// TM_NQ x TM_BUF keys of LDS can give each of those queries 4x the buffer: the int8 pass (4
+// compute waves, 64 keys each per query otherwise) then compacts ~0 instead of 2.5 (nq = 1) /
+// 9.7 (nq = 4) times per wave and slab -- nq 1 / 2 / 4: 0.094 / 0.104 / 0.129 -> 0.092 / 0.093 /
+// 0.094 ms per search; the bf16 pass (2 compute waves, 128 keys each) gains at nq = 4 (0.156 ->
+// 0.150) but loses at nq = 1 (0.141 -> 0.145), so it keeps the 16-query layout
+template <bool I8>
+constexpr int tm_qb() {
+  return (I8 || TT_TM_BIGBUF16) ? TM_NQ_RUN : TM_NQ;
+}
 constexpr int TM_CAP = 4096;  // final: keys per query (G x TM_M, G <= 256)
 
 template <int EP>
@@ -2001,15 +2019,27 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
   // one wave scoring the whole tile: 131 vs 122 us for the same stream without that work).
   // Each holds the query fragments (bf16 B operands, 16 queries) and its own per-query top-m
   // buffers tbuf[w][c][TMB].
-  constexpr int CW = RB, TMB = TM_BUF / CW, CPER = TMB / 64;
+  constexpr int TM_QB = tm_qb<false>(), CW = RB, TMB = TM_NQ * TM_BUF / TM_QB / CW;
+  constexpr int CPER = TMB / 64;
   static_assert(TMB % 64 == 0 && TMB >= 2 * TM_M && CW <= TM_WAVES, "top-m buffer shape");
   const bool cw = w < CW;
-  uint64_t* wbuf = tbuf + (cw ? w : 0) * TM_NQ * TMB;
+  uint64_t* wbuf = tbuf + (cw ? w : 0) * TM_QB * TMB;  // [TM_QB][TMB] per compute wave
   bf16x8 qf[KS];
   const bool qv = col < nq;
   float tau = qv ? -__builtin_huge_valf() : __builtin_huge_valf();
   int cnt = 0;  // appended keys of query `col` (same in the 4 lanes of a column)
-  float tm[16], tmin = -__builtin_huge_valf();  // tile-max bound of tau (appends)
+  // tile-max bound of tau (appends): the 16 largest of the set, ascending (tm[0] = the 16th)
+  float tm[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) tm[i] = -__builtin_huge_valf();
+  // insert m: clamp(m, tm[i], tm[i + 1]) per entry = the sorted 16 largest of the set plus m
+  // (one v_med3 each, branch-free; a no-op when m <= tm[0]); NaN enters as -inf
+  auto tm_insert = [&](float m) __attribute__((always_inline)) {
+    m = m == m ? m : -__builtin_huge_valf();
+#pragma unroll
+    for (int i = 0; i < 15; ++i) tm[i] = __builtin_amdgcn_fmed3f(tm[i], m, tm[i + 1]);
+    tm[15] = fmaxf(tm[15], m);
+  };
   int st_compact = 0;
   uint64_t st_t0 = TT_EXP_TM_STATS ? wall_clock64() : 0, st_t1 = 0, st_t2 = 0;
   if (cw) {
@@ -2096,34 +2126,43 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
   // appends of tile t's scores (lane: rows jt + 16 w + 4 g + jj of query col): a >= tau
   // (NaN never passes); positions within a column by ballot (no atomics): the 4 lanes of a
   // column hold cnt.  Then the compactions the buffers need.
-  auto appends = [&](const f32x4& acc, int t) __attribute__((always_inline)) {
+  auto appends = [&](f32x4 acc, int t) __attribute__((always_inline)) {
     const int64_t jt = j0 + (int64_t)t * TR + 16 * w;
     const uint64_t colmask = 0x0001000100010001ull << col;
     const uint64_t below = (1ull << lane) - 1ull;
+    if (jt + 16 > j1) {  // (wave-uniform) the slab's last tile: rows past its end score -inf
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int64_t row = jt + 4 * g + jj;
-      const float v = acc[jj];
-      const bool pass = row < j1 && v >= tau;
-      const uint64_t bm = __ballot(pass);
-      if (bm != 0ull) {
-        const uint64_t mc = bm & colmask;
-        if (pass) {
-          const int pos = cnt + __popcll(mc & below);
-          lds_write64(lds_addr(wbuf + col * TMB + pos), make_key(v, (uint32_t)row));
+      for (int jj = 0; jj < 4; ++jj)
+        if (jt + 4 * g + jj >= j1) acc[jj] = -__builtin_huge_valf();
+    }
+    // late in the slab tau has risen past nearly every row: one ballot skips the four
+    const bool any = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])) >= tau;
+    if (!TT_TM_ANYB || __ballot(any) != 0ull) {
+      const int lr0 = t * TR + 16 * w + 4 * g, nloc = (int)(j1 - j0);  // slab-local rows
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const float v = acc[jj];
+        const bool pass = lr0 + jj < nloc && v >= tau;
+        const uint64_t bm = __ballot(pass);
+        if (bm != 0ull) {
+          const uint64_t mc = bm & colmask;
+          if (pass) {
+            const int pos = cnt + __popcll(mc & below);
+            lds_write64(lds_addr(wbuf + col * TMB + pos),
+                        make_key(v, (uint32_t)(j0 + lr0 + jj)));
+          }
+          cnt += __popcll(mc);
         }
-        cnt += __popcll(mc);
       }
     }
     // tau between compactions: the TM_M-th largest of a set of scores of DISTINCT rows (tm[],
     // the same multiset in the 4 lanes of a column) is a lower bound of the running TM_M-th
-    // best.  The set starts as the first tile's 16 rows (if all are in range and finite: cnt),
-    // then each later tile's max replaces the set's min when larger (a tile max is a row of
-    // that tile: distinct).  Without it an empty buffer took ~TMB rows before its first
-    // compaction, and tau then lagged: 3-4 compactions per query and wave, all queries in
-    // the same tiles (nq = 16: 206 us for the 124 us stream).
-    if (t == 0) {
-      const bool full = cnt == TM_M;
+    // best.  The set: the first tile's 16 rows, then each later tile's max (a row of that
+    // tile: distinct); rows past the slab end and NaNs enter as -inf.  Without it an empty
+    // buffer took ~TMB rows before its first compaction, and tau then lagged: 3-4 compactions
+    // per query and wave, all queries in the same tiles (nq = 16: 206 us for the 124 us
+    // stream).
+    if (t == 0) {  // the first tile's 16 rows (every lane of the column gathers all 16)
       float v16[16];
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
@@ -2138,13 +2177,8 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
                                                           __float_as_uint(v16[jj]), false, false);
         v16[8 + jj] = __uint_as_float(lane < 32 ? x32[1] : x32[0]);  // lane ^ 32
       }
-      float mn = v16[0];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        tm[i] = full ? v16[i] : -__builtin_huge_valf();
-        mn = fminf(mn, v16[i]);
-      }
-      tmin = full ? mn : -__builtin_huge_valf();
+      for (int i = 0; i < 16; ++i) tm_insert(v16[i]);
     } else {
       float m = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3]));
       const auto x16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m),
@@ -2152,21 +2186,9 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
       m = fmaxf(__uint_as_float(x16[0]), __uint_as_float(x16[1]));
       const auto x32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m),
                                                         false, false);
-      m = fmaxf(__uint_as_float(x32[0]), __uint_as_float(x32[1]));  // the column's tile max
-      if (m > tmin) {  // (NaN never)
-        bool done = false;
-        float mn = m;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const bool hit = !done && tm[i] == tmin;
-          tm[i] = hit ? m : tm[i];
-          done |= hit;
-          mn = fminf(mn, tm[i]);
-        }
-        tmin = mn;
-      }
+      tm_insert(fmaxf(__uint_as_float(x32[0]), __uint_as_float(x32[1])));  // the tile max
     }
-    tau = fmaxf(tau, qv ? tmin : tau);
+    tau = fmaxf(tau, qv ? tm[0] : tau);
     const uint64_t need = __ballot(lane < 16 && cnt > TMB - 16);
     if (need != 0ull) {
       lds_wait<0>();
@@ -2228,7 +2250,7 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
 #pragma unroll
       for (int r = 0; r < CPER; ++r) {
         const int e = lane * CPER + r;
-        key[wb * CPER + r] = e < cc ? tbuf[(wb * TM_NQ + c) * TMB + e] : 0ull;
+        key[wb * CPER + r] = e < cc ? tbuf[(wb * TM_QB + c) * TMB + e] : 0ull;
       }
     }
     int nc;
@@ -2249,7 +2271,7 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
   for (int c = w; c < nq; c += TM_WAVES) {
     const int nc = ncs[c], r16 = lane & 15, g4 = 4 * (lane >> 4);
     if (nc == 0) continue;
-    const uint64_t* tb = tbuf + c * (TM_BUF / RB);
+    const uint64_t* tb = tbuf + c * TMB;
     const f32x4 acc =
         exact16<EP>(db, ld, key_row(tb[r16 < nc ? r16 : 0]), q + (int64_t)c * ldq, lane);
     if (r16 == 0) {
@@ -2419,10 +2441,35 @@ TT_CHECK_EXP(TT_I8_SLOTS != 4, "TT_I8_SLOTS");
 #define TT_I8_SWZ 1  // 0: XOR swizzle by r & 7 (2-way bank conflicts at E = 384), 1: by (r >> 1) & 7
 #endif
 TT_CHECK_EXP(TT_I8_SWZ != 1, "TT_I8_SWZ");
+#ifndef TT_I8_DMAW
+#define TT_I8_DMAW 1  // 1: only the waves that run no MFMA issue the ring's DMA (0: all waves)
+#endif
+TT_CHECK_EXP(TT_I8_DMAW != 1, "TT_I8_DMAW");
 #ifndef TT_I8_EXP_NOCOMP
 #define TT_I8_EXP_NOCOMP 0  // timing only (results WRONG): the int8 stream without compute
 #endif
 TT_CHECK_EXP(TT_I8_EXP_NOCOMP, "TT_I8_EXP_NOCOMP");
+#ifndef TT_I8_EXP_PART
+#define TT_I8_EXP_PART 0  // timing only (results WRONG): 1 no appends, 2 no LDS reads, 3 no MFMA
+#endif
+TT_CHECK_EXP(TT_I8_EXP_PART, "TT_I8_EXP_PART");
+#ifndef TT_I8_EXP_CLK
+#define TT_I8_EXP_CLK 0  // timing only: per-wave cycle split of the int8 stream's tile loop
+#endif
+TT_CHECK_EXP(TT_I8_EXP_CLK, "TT_I8_EXP_CLK");
+#if TT_I8_EXP_CLK
+__device__ unsigned long long g_i8clk[256 * TM_WAVES * 8];
+#define I8CLK(i)                                               \
+  do {                                                         \
+    const unsigned long long c1_ = __builtin_amdgcn_s_memtime(); \
+    ck[i] += c1_ - c0_;                                        \
+    c0_ = c1_;                                                 \
+  } while (0)
+#else
+#define I8CLK(i) \
+  do {           \
+  } while (0)
+#endif
 // 16-B chunk swizzle of an int8 tile row r (XOR of the chunk index within aligned groups of
 // 8 / 16 chunks): the 16 rows a ds_read_b128 lane group reads must land in 16 different
 // 16-B bank groups.  E = 384: 24 chunks per row, 24 = 8 mod 16, so rows r and r + 1 are 8
@@ -2442,9 +2489,14 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
     int* __restrict__ counts, int* __restrict__ flags, int* __restrict__ qsel_n) {
   static_assert(EP == 384 || EP == 768, "int8 single pass: E = 384 or 768");
   constexpr int TR = 24576 / EP, KS = EP / 64, CPR = EP / 16, RB = TR / 16;
-  constexpr int TILE_B = TR * EP, PIECES = TILE_B / 1024, PPW = PIECES / TM_WAVES;
+  // the ring's 1-KB DMA pieces per tile, issued by DW waves (PPW each): with TT_I8_DMAW the
+  // TM_WAVES - RB waves that run no MFMA, so the compute waves' per-tile path carries no
+  // address arithmetic or memory-pipe stalls and needs no vmcnt wait (the barrier after the
+  // issuing waves' waits orders every piece)
+  constexpr int DW = TT_I8_DMAW ? TM_WAVES - RB : TM_WAVES, DW0 = TM_WAVES - DW;
+  constexpr int TILE_B = TR * EP, PIECES = TILE_B / 1024, PPW = PIECES / DW;
   constexpr int SLOTS = TT_I8_SLOTS, PD = SLOTS - 1;
-  static_assert(PIECES % TM_WAVES == 0 && CPR % 16 == 8 * (EP == 384), "tile layout");
+  static_assert(PIECES % DW == 0 && CPR % 16 == 8 * (EP == 384), "tile layout");
   __shared__ __attribute__((aligned(16))) char smem[SLOTS * TILE_B + TM_NQ * TM_BUF * 8];
   __shared__ int ncs[TM_NQ];
   __shared__ float ssc[I8_MAXTILES];
@@ -2467,16 +2519,28 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
     ssc[i] = st < ((n + 63) >> 6) ? scales[st] : 0.0f;
   }
 
-  constexpr int CW = RB, TMB = TM_BUF / CW, CPER = TMB / 64;
+  constexpr int TM_QB = tm_qb<true>(), CW = RB, TMB = TM_NQ * TM_BUF / TM_QB / CW;
+  constexpr int CPER = TMB / 64;
   static_assert(TMB % 64 == 0 && TMB >= 2 * TM_M && CW <= TM_WAVES, "top-m buffer shape");
   const bool cw = w < CW && !TT_I8_EXP_NOCOMP;
-  uint64_t* wbuf = tbuf + (cw ? w : 0) * TM_NQ * TMB;
+  uint64_t* wbuf = tbuf + (cw ? w : 0) * TM_QB * TMB;  // [TM_QB][TMB] per compute wave
   u32x4 qf[KS];
   const bool qv = col < nq;
   float tq = 0.0f;  // the query's code scale t
   float tau = qv ? -__builtin_huge_valf() : __builtin_huge_valf();
   int cnt = 0;
-  float tm[16], tmin = -__builtin_huge_valf();
+  // tile-max bound of tau (appends): the 16 largest of the set, ascending (tm[0] = the 16th)
+  float tm[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) tm[i] = -__builtin_huge_valf();
+  // insert m: clamp(m, tm[i], tm[i + 1]) per entry = the sorted 16 largest of the set plus m
+  // (one v_med3 each, branch-free; a no-op when m <= tm[0]); NaN enters as -inf
+  auto tm_insert = [&](float m) __attribute__((always_inline)) {
+    m = m == m ? m : -__builtin_huge_valf();
+#pragma unroll
+    for (int i = 0; i < 15; ++i) tm[i] = __builtin_amdgcn_fmed3f(tm[i], m, tm[i + 1]);
+    tm[15] = fmaxf(tm[15], m);
+  };
   if (cw) {
     // the query (column col) coded as t m: lanes (g, col) hold chunks 4s + g, i.e. dims
     // 64 s + 16 g .. + 15 -- the same chunk of every row the MFMA pairs them with
@@ -2532,14 +2596,17 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
 
   const int64_t tile_bytes = ldc * TR;
   const char* slab_base = (const char*)xc + j0 * ldc;
+  const bool dmaw = w >= DW0;
+  const int dw = dmaw ? w - DW0 : 0;
   uint32_t voff[PPW];
 #pragma unroll
   for (int pp = 0; pp < PPW; ++pp) {
-    const int P = (w + TM_WAVES * pp) * 64 + lane;
+    const int P = (dw + DW * pp) * 64 + lane;
     const int r = P / CPR;
     voff[pp] = (uint32_t)(r * ldc) + 16u * (uint32_t)((P % CPR) ^ i8_swz<EP>(r));
   }
   auto issue = [&](int t) __attribute__((always_inline)) {
+    if (!dmaw) return;
     char* slot = ring + (t % SLOTS) * TILE_B;
     const int64_t jt = j0 + (int64_t)t * TR;
     const bool clamp = jt + TR > j1;
@@ -2549,19 +2616,20 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
     for (int pp = 0; pp < PPW; ++pp) {
       uint32_t off = voff[pp];
       if (clamp) {  // rows past the slab end read a copy of its last row (masked below)
-        const int P = (w + TM_WAVES * pp) * 64 + lane;
+        const int P = (dw + DW * pp) * 64 + lane;
         const int r = P / CPR;
         int64_t j = jt + r;
         j = j < j1 ? j : j1 - 1;
         off = (uint32_t)((j - jt) * ldc) + 16u * (uint32_t)((P % CPR) ^ i8_swz<EP>(r));
       }
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs, (__attribute__((address_space(3))) void*)(slot + (w + TM_WAVES * pp) * 1024), 16,
+          rs, (__attribute__((address_space(3))) void*)(slot + (dw + DW * pp) * 1024), 16,
           off, 0, 0, 2);
     }
   };
   auto wait_tiles = [&](int younger) __attribute__((always_inline)) {
     static_assert(PD <= 4, "wait_tiles covers up to 3 younger tiles");
+    if (!dmaw) return;  // issued nothing: the barrier after the issuing waves' waits orders it
     if (younger >= 3) wait_vm<3 * PPW>();
     else if (younger == 2) wait_vm<2 * PPW>();
     else if (younger == 1) wait_vm<PPW>();
@@ -2575,6 +2643,9 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
       lrd[v] = lds_addr(ring) + 16 * (r * CPR + (g ^ (f & 3))) + 64 * (v ^ h);
   }
   static_assert(TM_M == 16, "wave_top16 keeps 16");
+#if TT_I8_EXP_CLK
+  unsigned long long n_any = 0, n_cmp = 0;
+#endif
   auto compact = [&](int c) __attribute__((always_inline)) {
     uint64_t* b = wbuf + c * TMB;
     const int cc = __shfl(cnt, c, 64);
@@ -2595,48 +2666,55 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
     wave_sync();
   };
   // appends and the tile-max bound of tau: k_filter_topm's (the scores arrive as f32 here)
-  auto appends = [&](const f32x4& acc, int t) __attribute__((always_inline)) {
+  auto appends = [&](f32x4 acc, int t) __attribute__((always_inline)) {
     const int64_t jt = j0 + (int64_t)t * TR + 16 * w;
     const uint64_t colmask = 0x0001000100010001ull << col;
     const uint64_t below = (1ull << lane) - 1ull;
+    if (jt + 16 > j1) {  // (wave-uniform) the slab's last tile: rows past its end score -inf
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      const int64_t row = jt + 4 * g + jj;
-      const float v = acc[jj];
-      const bool pass = row < j1 && v >= tau;
-      const uint64_t bm = __ballot(pass);
-      if (bm != 0ull) {
-        const uint64_t mc = bm & colmask;
-        if (pass) {
-          const int pos = cnt + __popcll(mc & below);
-          lds_write64(lds_addr(wbuf + col * TMB + pos), make_key(v, (uint32_t)row));
+      for (int jj = 0; jj < 4; ++jj)
+        if (jt + 4 * g + jj >= j1) acc[jj] = -__builtin_huge_valf();
+    }
+    // late in the slab tau has risen past nearly every row: one ballot skips the four
+    const bool any = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])) >= tau;
+    if (!TT_TM_ANYB || __ballot(any) != 0ull) {
+#if TT_I8_EXP_CLK
+      ++n_any;
+#endif
+      const int lr0 = t * TR + 16 * w + 4 * g, nloc = (int)(j1 - j0);  // slab-local rows
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const float v = acc[jj];
+        const bool pass = lr0 + jj < nloc && v >= tau;
+        const uint64_t bm = __ballot(pass);
+        if (bm != 0ull) {
+          const uint64_t mc = bm & colmask;
+          if (pass) {
+            const int pos = cnt + __popcll(mc & below);
+            lds_write64(lds_addr(wbuf + col * TMB + pos),
+                        make_key(v, (uint32_t)(j0 + lr0 + jj)));
+          }
+          cnt += __popcll(mc);
         }
-        cnt += __popcll(mc);
       }
     }
-    if (t == 0) {
-      const bool full = cnt == TM_M;
+    if (t == 0) {  // the first tile's 16 rows (every lane of the column gathers all 16)
       float v16[16];
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         v16[jj] = acc[jj];
         const auto x16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[jj]),
                                                           __float_as_uint(acc[jj]), false, false);
-        v16[4 + jj] = __uint_as_float((g & 1) ? x16[0] : x16[1]);
+        v16[4 + jj] = __uint_as_float((g & 1) ? x16[0] : x16[1]);  // lane ^ 16
       }
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         const auto x32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v16[jj]),
                                                           __float_as_uint(v16[jj]), false, false);
-        v16[8 + jj] = __uint_as_float(lane < 32 ? x32[1] : x32[0]);
+        v16[8 + jj] = __uint_as_float(lane < 32 ? x32[1] : x32[0]);  // lane ^ 32
       }
-      float mn = v16[0];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        tm[i] = full ? v16[i] : -__builtin_huge_valf();
-        mn = fminf(mn, v16[i]);
-      }
-      tmin = full ? mn : -__builtin_huge_valf();
+      for (int i = 0; i < 16; ++i) tm_insert(v16[i]);
     } else {
       float m = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3]));
       const auto x16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m),
@@ -2644,21 +2722,9 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
       m = fmaxf(__uint_as_float(x16[0]), __uint_as_float(x16[1]));
       const auto x32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m),
                                                         false, false);
-      m = fmaxf(__uint_as_float(x32[0]), __uint_as_float(x32[1]));
-      if (m > tmin) {
-        bool done = false;
-        float mn = m;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const bool hit = !done && tm[i] == tmin;
-          tm[i] = hit ? m : tm[i];
-          done |= hit;
-          mn = fminf(mn, tm[i]);
-        }
-        tmin = mn;
-      }
+      tm_insert(fmaxf(__uint_as_float(x32[0]), __uint_as_float(x32[1])));  // the tile max
     }
-    tau = fmaxf(tau, qv ? tmin : tau);
+    tau = fmaxf(tau, qv ? tm[0] : tau);
     const uint64_t need = __ballot(lane < 16 && cnt > TMB - 16);
     if (need != 0ull) {
       lds_wait<0>();
@@ -2667,43 +2733,75 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
         const int c = __builtin_ctzll(nd);
         nd &= nd - 1;
         compact(c);
+#if TT_I8_EXP_CLK
+        ++n_cmp;
+#endif
       }
     }
   };
 
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#if TT_I8_EXP_CLK
+  unsigned long long ck[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long c0_ = __builtin_amdgcn_s_memtime();
+  const unsigned long long cstart = c0_;
+#endif
   for (int t = 0; t < PD && t < n_tiles; ++t) issue(t);
   for (int t = 0; t < n_tiles; ++t) {
     wait_tiles(n_tiles - 1 - t < PD - 1 ? n_tiles - 1 - t : PD - 1);
+    I8CLK(0);
     lds_barrier();  // tile t landed (every wave's pieces); every wave is done with tile t-1
+    I8CLK(1);
     if (t + PD < n_tiles) issue(t + PD);
+    I8CLK(2);
     if (cw) {
       const uint32_t so = (uint32_t)((t % SLOTS) * TILE_B);
       u32x4 fr[KS];
       static_for<KS>([&](auto s_) __attribute__((always_inline)) {
         constexpr int Sx = decltype(s_)::value;
-        fr[Sx] = lds_read128<256 * (Sx / 4)>(lrd[Sx % 4] + so);
+        if (TT_I8_EXP_PART == 2)
+          fr[Sx] = qf[Sx] ^ (uint32_t)t;
+        else
+          fr[Sx] = lds_read128<256 * (Sx / 4)>(lrd[Sx % 4] + so);
       });
       // the tile's scale (its 64-row scale tile) x the query's t: one product per lane
       const float st = ssc[(int)(((int64_t)t * TR) >> 6)] * tq;
-      if (t > 0) appends(acc, t - 1);
+      I8CLK(6);
+      if (t > 0 && TT_I8_EXP_PART != 1) appends(acc, t - 1);
+      I8CLK(3);
       lds_wait<0>();
+      I8CLK(4);
       i32x4 ai = {0, 0, 0, 0};
       static_for<KS>([&](auto s_) __attribute__((always_inline)) {
         constexpr int Sx = decltype(s_)::value;
         reg_tie(fr[Sx]);
-        ai = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, fr[Sx]),
-                                                   __builtin_bit_cast(i32x4, qf[Sx]), ai, 0, 0,
-                                                   0);
+        if (TT_I8_EXP_PART == 3)
+          ai += __builtin_bit_cast(i32x4, fr[Sx]);
+        else
+          ai = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, fr[Sx]),
+                                                     __builtin_bit_cast(i32x4, qf[Sx]), ai, 0, 0,
+                                                     0);
       });
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) acc[jj] = (float)ai[jj] * st;
+      I8CLK(5);
     }
   }
+#if TT_I8_EXP_CLK
+  if (lane == 0 && blk < 256) {
+    ck[8] = __builtin_amdgcn_s_memtime() - cstart;
+    ck[7] = (unsigned long long)n_tiles;
+    ck[3] += ck[6] << 32;  // 3: appends (low word), reads (high word)
+    ck[4] += n_any << 32;  // tiles whose appends ran / compactions (high words)
+    ck[5] += n_cmp << 32;
+    ck[6] = ck[8];
+    for (int i = 0; i < 8; ++i) g_i8clk[(blk * TM_WAVES + w) * 8 + i] = ck[i];
+  }
+#endif
   if (cw && n_tiles > 0) appends(acc, n_tiles - 1);
   wait_vm<0>();
   __shared__ int ncw[CW][TM_NQ];
-  if (cw && lane < nq && g == 0) ncw[w][lane] = cnt;
+  if (w < CW && lane < nq && g == 0) ncw[w][lane] = cnt;  // (0 when TT_I8_EXP_NOCOMP)
   lds_wait<0>();
   __syncthreads();
   for (int c = w; c < nq; c += TM_WAVES) {
@@ -2714,7 +2812,7 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
 #pragma unroll
       for (int r = 0; r < CPER; ++r) {
         const int e = lane * CPER + r;
-        key[wb * CPER + r] = e < cc ? tbuf[(wb * TM_NQ + c) * TMB + e] : 0ull;
+        key[wb * CPER + r] = e < cc ? tbuf[(wb * TM_QB + c) * TMB + e] : 0ull;
       }
     }
     int nc;
@@ -3813,6 +3911,12 @@ __global__ void k_debug_plant(uint64_t* keys, uint64_t* xk, const int* counts, i
 extern "C" int tt_debug_blktimes(void* host, int32_t n) {  // timing builds only
   if (n > BLKTIME_MAX) n = BLKTIME_MAX;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_blktime), (size_t)n * 32) == hipSuccess ? n : -1;
+}
+#endif
+
+#if TT_I8_EXP_CLK
+extern "C" int tt_debug_i8clk(void* host) {  // timing builds only: [256][TM_WAVES][8] u64
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_i8clk), sizeof(g_i8clk)) == hipSuccess ? 0 : -1;
 }
 #endif
 

@@ -215,6 +215,11 @@ class FlatIPIndex:
     # own exact top k: the lists are sorted by (score desc, row asc)), then hands the lead to
     # the next waiting thread.  One caller alone is a batch of one.
     COALESCE_MAX = 8
+    # a leader whose own request is answered may go on serving the queue for up to LEAD_EXTRA
+    # more batches before handing the lead over (no thread wake-up between two batches); 0:
+    # measured slower at 2 and 4 (tools/bench_api.py: 4 threads 7.7k calls/s at 0, 7.2-7.4k
+    # at 2 / 4 -- fewer requests per batch while the leader's own caller waits)
+    LEAD_EXTRA = 0
 
     def _path(self, k: int) -> int:
         return 0 if k <= kernels.FILTER_KMAX else 1 if k <= kernels.SCAN_KMAX else 2
@@ -237,6 +242,7 @@ class FlatIPIndex:
         return req.result
 
     def _serve(self, me: "_Request") -> None:
+        extra = 0
         while True:
             with self._qlock:
                 head = self._queue[0]
@@ -268,11 +274,13 @@ class FlatIPIndex:
                     r.event.set()
             with self._qlock:
                 if me.finished:
-                    if self._queue:  # hand the lead to the oldest waiting request's thread
-                        self._queue[0].event.set()
-                    else:
+                    if not self._queue:
                         self._leading = False
-                    return
+                        return
+                    if extra >= self.LEAD_EXTRA:  # hand the lead to the oldest waiting thread
+                        self._queue[0].event.set()
+                        return
+                    extra += 1
 
     def search(self, x: np.ndarray, k: int):
         """faiss signature: float32 [nq, d] host queries -> (D [nq,k] f32, I [nq,k] i64) host."""
@@ -337,6 +345,7 @@ class _ServingSlot:
         self.norm_fn = _lib.lib().tt_l2norm_rows_f32
         self.qh_np = self.qh.numpy()
         self.args, self.args_key = None, None
+        self.bound = collections.OrderedDict()  # akey -> bound C arguments (a few nq / k)
         index.allocations += 1
 
     def _outs(self, kc: int, pin: bool) -> None:
@@ -375,6 +384,10 @@ class _ServingSlot:
         ws = self._workspace(n, nq, k, "bf16")
         use8 = i8 is not None and nq <= kernels.I8_NQ_MAX
         akey = (skey, nq, k, ws.data_ptr(), self.s.data_ptr(), bounds, normalize, use8)
+        if akey != self.args_key and akey in self.bound:  # coalesced batches vary nq
+            self.fn, self.args, self.h2d, self.norm, self.d2h = self.bound[akey]
+            self.bound.move_to_end(akey)
+            self.args_key = akey
         if akey != self.args_key:  # the C arguments, bound once per (state, nq, k)
             vp = ctypes.c_void_p
             qp, st = vp(self.q.data_ptr()), vp(self.stream.cuda_stream)
@@ -403,6 +416,9 @@ class _ServingSlot:
                         (vp(self.ih.data_ptr()), vp(self.i.data_ptr()), ctypes.c_size_t(nq * k * 8),
                          2, st))
             self.args_key = akey
+            self.bound[akey] = (self.fn, self.args, self.h2d, self.norm, self.d2h)
+            if len(self.bound) > 8:
+                self.bound.popitem(last=False)
         self.qh_np[:nq] = x
         hip = _hip()
         if hip.hipMemcpy2DAsync(*self.h2d):
@@ -422,7 +438,7 @@ class _ServingSlot:
 
     def run(self, x: np.ndarray, k: int, normalize: bool, state):
         ix = self.ix
-        xb, xb16, n, bounds, _ = state
+        xb, xb16, n, _, _ = state
         nq, d = x.shape
         if k > self.kc:
             self._outs(k, torch.cuda.is_available())
@@ -436,30 +452,14 @@ class _ServingSlot:
             self.synced = skey
         if ix.scan_dim and k <= kernels.FILTER_KMAX and k <= self.kc:
             return self._fast(x, k, normalize, state, skey)
-        self.args_key = None  # the torch-op path below rebinds its own arguments
         with torch.cuda.stream(self.stream):
             self.qh[:nq].numpy()[...] = x
             q[:, :d].copy_(self.qh[:nq], non_blocking=True)
             if normalize:
                 kernels.l2norm_rows(q, d, _lib.TT_NORM_ADD_EPS, out=q)
             s, i = self.s[: nq * k].view(nq, k), self.i[: nq * k].view(nq, k)
-            st = self.stream.cuda_stream
-            if ix.scan_dim and k <= kernels.FILTER_KMAX:
-                ws = self._workspace(n, nq, k, "bf16")
-                akey = (skey, nq, k, ws.data_ptr(), s.data_ptr(), bounds)
-                if akey != self.args_key:  # the C arguments, bound once per (state, nq, k)
-                    self.args = (
-                        ctypes.c_void_p(xb.data_ptr()), ctypes.c_void_p(xb16.data_ptr()), n, d,
-                        xb.stride(0), ix.row_base, ctypes.c_void_p(q.data_ptr()), nq,
-                        q.stride(0), k, ctypes.c_float(bounds[0]), ctypes.c_float(bounds[1]),
-                        ctypes.c_void_p(s.data_ptr()), ctypes.c_void_p(i.data_ptr()),
-                        ctypes.c_void_p(ws.data_ptr()), ws.numel(), ctypes.c_void_p(st), None,
-                        None)
-                    self.args_key = akey
-                rc = self.fn(*self.args)
-                if rc:
-                    _lib.check(rc, "tt_scan_topk_bf16f32")
-            elif ix.scan_dim and k <= kernels.SCAN_KMAX:
+            # (k <= 128 at a scan dim always took _fast above: outputs grow to k first)
+            if ix.scan_dim and k <= kernels.SCAN_KMAX:
                 ws = self._workspace(n, nq, k, "select")
                 kernels.scan_topk_select(xb, n, d, q, k, row_base=ix.row_base, workspace=ws,
                                          out=(s, i))
