@@ -1,4 +1,4 @@
-"""One-buyer / small-batch latency: bf16 single pass vs the int8 single pass (1M x 384, k=100),
+"""One-buyer / small-batch latency (env NQS = batch sizes, default 1,2,4): bf16 single pass vs the int8 single pass (1M x 384, k=100),
 kernels.PreparedSearch device calls, median of 51 synchronised calls (HIP events), plus the
 stream kernel alone (ev_start/ev_stop around k_filter_topm / k_filter_topm_i8)."""
 import json
@@ -30,13 +30,16 @@ def main():
     st = torch.cuda.current_stream()
     for e in ev:
         e.record(st)
-    for nq in (1, 2, 4):
+    kernels.I8_NQ_MAX = int(os.environ.get("I8MAX", kernels.I8_NQ_MAX))  # timing builds only
+    for nq in (int(v) for v in os.environ.get("NQS", "1,2,4").split(",")):
         q = torch.zeros((nq, ep), device=dev)
         q[:, :E] = torch.randn((nq, E), generator=g, device=dev)
         kernels.l2norm_rows(q, E, _lib.TT_NORM_ADD_EPS, out=q)
         res = {}
         ref = None
         for name, i8 in (("bf16", None), ("i8", (codes, scales, b3))):
+            if name == "i8" and nq > kernels.I8_NQ_MAX:
+                continue
             ps = kernels.PreparedSearch(x, x16, N, E, nq, K, bnd, i8=i8)
             assert ps.i8 == (name == "i8")
             for _ in range(5):

@@ -1957,7 +1957,11 @@ constexpr int TM_NQ = 16;     // queries per MFMA query block (the buffers' quer
 // grow with the query count, and from 8 queries on the multi-level path is as fast (one-buyer
 // latency, topm vs multi-level, ms: nq 1 0.139 / 0.181, 2 0.145 / 0.195, 4 0.158 / 0.184,
 // 8 0.188 / 0.186, 16 0.225 / 0.189)
-constexpr int TM_NQ_RUN = 4;
+#ifndef TT_EXP_TM_NQ_RUN
+#define TT_EXP_TM_NQ_RUN 4  // timing builds: the single passes for larger batches
+#endif
+TT_CHECK_EXP(TT_EXP_TM_NQ_RUN != 4, "TT_EXP_TM_NQ_RUN");
+constexpr int TM_NQ_RUN = TT_EXP_TM_NQ_RUN;
 constexpr int TM_M = 16;      // rows kept per (query, slab)
 constexpr int TM_BUF = 256;   // candidate buffer per query, split over the compute waves
 constexpr int TM_SLOTS = TT_EXP_TM_SLOTS, TM_PD = TM_SLOTS - 1;  // ring slots, tiles in flight
@@ -1980,6 +1984,14 @@ template <bool I8>
 constexpr int tm_qb() {
   return (I8 || TT_TM_BIGBUF16) ? TM_NQ_RUN : TM_NQ;
 }
+#ifndef TT_TM_PREFIX
+#define TT_TM_PREFIX 1  // 1: appends place a lane's 4 rows by one column prefix (0: per-row ballots)
+#endif
+TT_CHECK_EXP(TT_TM_PREFIX != 1, "TT_TM_PREFIX");
+#ifndef TT_TM_SHTAU
+#define TT_TM_SHTAU 1  // 1: the compute waves of a block share their tau bounds (max)
+#endif
+TT_CHECK_EXP(TT_TM_SHTAU != 1, "TT_TM_SHTAU");
 constexpr int TM_CAP = 4096;  // final: keys per query (G x TM_M, G <= 256)
 
 template <int EP>
@@ -2026,6 +2038,11 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
   uint64_t* wbuf = tbuf + (cw ? w : 0) * TM_QB * TMB;  // [TM_QB][TMB] per compute wave
   bf16x8 qf[KS];
   const bool qv = col < nq;
+  // tau bounds shared by the block's compute waves: a row below ANY wave's tau (each a lower
+  // bound of the 16th best of distinct rows of this slab) is below the slab's 16th best, so
+  // every wave may drop it -- each wave's appends follow the block's max
+  __shared__ __attribute__((aligned(16))) float tau_sh[TM_NQ_RUN][4];
+  if (TT_TM_SHTAU && w < 4 && lane < TM_NQ_RUN) tau_sh[lane][w] = -__builtin_huge_valf();
   float tau = qv ? -__builtin_huge_valf() : __builtin_huge_valf();
   int cnt = 0;  // appended keys of query `col` (same in the 4 lanes of a column)
   // tile-max bound of tau (appends): the 16 largest of the set, ascending (tm[0] = the 16th)
@@ -2039,6 +2056,13 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
 #pragma unroll
     for (int i = 0; i < 15; ++i) tm[i] = __builtin_amdgcn_fmed3f(tm[i], m, tm[i + 1]);
     tm[15] = fmaxf(tm[15], m);
+  };
+  // the block's shared tau for this lane's query (issued before the tile's fragment reads:
+  // LDS reads complete in order)
+  auto read_shtau = [&]() __attribute__((always_inline)) {
+    if (!TT_TM_SHTAU) return -__builtin_huge_valf();
+    const f32x4 v = *(const f32x4*)&tau_sh[col < TM_NQ_RUN ? col : 0][0];
+    return fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
   };
   int st_compact = 0;
   uint64_t st_t0 = TT_EXP_TM_STATS ? wall_clock64() : 0, st_t1 = 0, st_t2 = 0;
@@ -2126,8 +2150,9 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
   // appends of tile t's scores (lane: rows jt + 16 w + 4 g + jj of query col): a >= tau
   // (NaN never passes); positions within a column by ballot (no atomics): the 4 lanes of a
   // column hold cnt.  Then the compactions the buffers need.
-  auto appends = [&](f32x4 acc, int t) __attribute__((always_inline)) {
+  auto appends = [&](f32x4 acc, int t, float shtau) __attribute__((always_inline)) {
     const int64_t jt = j0 + (int64_t)t * TR + 16 * w;
+    if (TT_TM_SHTAU && qv) tau = fmaxf(tau, shtau);
     const uint64_t colmask = 0x0001000100010001ull << col;
     const uint64_t below = (1ull << lane) - 1ull;
     if (jt + 16 > j1) {  // (wave-uniform) the slab's last tile: rows past its end score -inf
@@ -2139,19 +2164,47 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
     const bool any = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])) >= tau;
     if (!TT_TM_ANYB || __ballot(any) != 0ull) {
       const int lr0 = t * TR + 16 * w + 4 * g, nloc = (int)(j1 - j0);  // slab-local rows
+      if (TT_TM_PREFIX) {
+        // one pass for the lane's 4 rows: its pass count, the exclusive prefix over the
+        // column's 4 lanes (lane ^ 16, lane ^ 32 partners) and the column's total
+        bool pass[4];
+        int np = 0;
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const float v = acc[jj];
-        const bool pass = lr0 + jj < nloc && v >= tau;
-        const uint64_t bm = __ballot(pass);
-        if (bm != 0ull) {
-          const uint64_t mc = bm & colmask;
-          if (pass) {
-            const int pos = cnt + __popcll(mc & below);
+        for (int jj = 0; jj < 4; ++jj) {
+          pass[jj] = lr0 + jj < nloc && acc[jj] >= tau;
+          np += pass[jj] ? 1 : 0;
+        }
+        const auto x16 = __builtin_amdgcn_permlane16_swap((uint32_t)np, (uint32_t)np, false,
+                                                          false);
+        const int b = (int)((g & 1) ? x16[0] : x16[1]);  // lane ^ 16
+        const int s2 = np + b;
+        const auto x32 = __builtin_amdgcn_permlane32_swap((uint32_t)s2, (uint32_t)s2, false,
+                                                          false);
+        const int s2x = (int)(lane < 32 ? x32[1] : x32[0]);  // lane ^ 32
+        int pos = cnt + ((g & 1) ? b : 0) + ((g & 2) ? s2x : 0);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          if (pass[jj]) {
             lds_write64(lds_addr(wbuf + col * TMB + pos),
-                        make_key(v, (uint32_t)(j0 + lr0 + jj)));
+                        make_key(acc[jj], (uint32_t)(j0 + lr0 + jj)));
+            ++pos;
           }
-          cnt += __popcll(mc);
+        cnt += s2 + s2x;
+      } else {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const float v = acc[jj];
+          const bool pass = lr0 + jj < nloc && v >= tau;
+          const uint64_t bm = __ballot(pass);
+          if (bm != 0ull) {
+            const uint64_t mc = bm & colmask;
+            if (pass) {
+              const int pos = cnt + __popcll(mc & below);
+              lds_write64(lds_addr(wbuf + col * TMB + pos),
+                          make_key(v, (uint32_t)(j0 + lr0 + jj)));
+            }
+            cnt += __popcll(mc);
+          }
         }
       }
     }
@@ -2200,6 +2253,7 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
         if (TT_EXP_TM_STATS) ++st_compact;
       }
     }
+    if (TT_TM_SHTAU && qv && g == 0) tau_sh[col][w] = tau;  // published for the other waves
   };
 
   // compute wave, per tile t: issue all of its row block's fragment reads (KS x 16 B per
@@ -2216,13 +2270,14 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
     lds_barrier();  // tile t landed (every wave's pieces); every wave is done with tile t-1
     if (t + TM_PD < n_tiles) issue(t + TM_PD);  // into the slot of tile t-1
     if (cw) {
+      const float shtau = read_shtau();
       const uint32_t so = (uint32_t)((t % TM_SLOTS) * TILE_B);
       u32x4 fr[KS];
       static_for<KS>([&](auto s_) __attribute__((always_inline)) {
         constexpr int S = decltype(s_)::value;
         fr[S] = lds_read128<256 * (S / 4)>(lrd[S % 4] + so);
       });
-      if (t > 0) appends(acc, t - 1);
+      if (t > 0) appends(acc, t - 1, shtau);
       lds_wait<0>();
       acc = f32x4{0.f, 0.f, 0.f, 0.f};
       static_for<KS>([&](auto s_) __attribute__((always_inline)) {
@@ -2233,7 +2288,7 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
       });
     }
   }
-  if (cw && n_tiles > 0) appends(acc, n_tiles - 1);
+  if (cw && n_tiles > 0) appends(acc, n_tiles - 1, read_shtau());
   wait_vm<0>();
   if (TT_EXP_TM_STATS) st_t1 = wall_clock64();
   // end of the slab, per query (queries spread over the waves): the top TM_M of the CW
@@ -2526,6 +2581,11 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
   uint64_t* wbuf = tbuf + (cw ? w : 0) * TM_QB * TMB;  // [TM_QB][TMB] per compute wave
   u32x4 qf[KS];
   const bool qv = col < nq;
+  // tau bounds shared by the block's compute waves: a row below ANY wave's tau (each a lower
+  // bound of the 16th best of distinct rows of this slab) is below the slab's 16th best, so
+  // every wave may drop it -- each wave's appends follow the block's max
+  __shared__ __attribute__((aligned(16))) float tau_sh[TM_NQ_RUN][4];
+  if (TT_TM_SHTAU && w < 4 && lane < TM_NQ_RUN) tau_sh[lane][w] = -__builtin_huge_valf();
   float tq = 0.0f;  // the query's code scale t
   float tau = qv ? -__builtin_huge_valf() : __builtin_huge_valf();
   int cnt = 0;
@@ -2540,6 +2600,13 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
 #pragma unroll
     for (int i = 0; i < 15; ++i) tm[i] = __builtin_amdgcn_fmed3f(tm[i], m, tm[i + 1]);
     tm[15] = fmaxf(tm[15], m);
+  };
+  // the block's shared tau for this lane's query (issued before the tile's fragment reads:
+  // LDS reads complete in order)
+  auto read_shtau = [&]() __attribute__((always_inline)) {
+    if (!TT_TM_SHTAU) return -__builtin_huge_valf();
+    const f32x4 v = *(const f32x4*)&tau_sh[col < TM_NQ_RUN ? col : 0][0];
+    return fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
   };
   if (cw) {
     // the query (column col) coded as t m: lanes (g, col) hold chunks 4s + g, i.e. dims
@@ -2666,8 +2733,9 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
     wave_sync();
   };
   // appends and the tile-max bound of tau: k_filter_topm's (the scores arrive as f32 here)
-  auto appends = [&](f32x4 acc, int t) __attribute__((always_inline)) {
+  auto appends = [&](f32x4 acc, int t, float shtau) __attribute__((always_inline)) {
     const int64_t jt = j0 + (int64_t)t * TR + 16 * w;
+    if (TT_TM_SHTAU && qv) tau = fmaxf(tau, shtau);
     const uint64_t colmask = 0x0001000100010001ull << col;
     const uint64_t below = (1ull << lane) - 1ull;
     if (jt + 16 > j1) {  // (wave-uniform) the slab's last tile: rows past its end score -inf
@@ -2682,19 +2750,47 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
       ++n_any;
 #endif
       const int lr0 = t * TR + 16 * w + 4 * g, nloc = (int)(j1 - j0);  // slab-local rows
+      if (TT_TM_PREFIX) {
+        // one pass for the lane's 4 rows: its pass count, the exclusive prefix over the
+        // column's 4 lanes (lane ^ 16, lane ^ 32 partners) and the column's total
+        bool pass[4];
+        int np = 0;
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        const float v = acc[jj];
-        const bool pass = lr0 + jj < nloc && v >= tau;
-        const uint64_t bm = __ballot(pass);
-        if (bm != 0ull) {
-          const uint64_t mc = bm & colmask;
-          if (pass) {
-            const int pos = cnt + __popcll(mc & below);
+        for (int jj = 0; jj < 4; ++jj) {
+          pass[jj] = lr0 + jj < nloc && acc[jj] >= tau;
+          np += pass[jj] ? 1 : 0;
+        }
+        const auto x16 = __builtin_amdgcn_permlane16_swap((uint32_t)np, (uint32_t)np, false,
+                                                          false);
+        const int b = (int)((g & 1) ? x16[0] : x16[1]);  // lane ^ 16
+        const int s2 = np + b;
+        const auto x32 = __builtin_amdgcn_permlane32_swap((uint32_t)s2, (uint32_t)s2, false,
+                                                          false);
+        const int s2x = (int)(lane < 32 ? x32[1] : x32[0]);  // lane ^ 32
+        int pos = cnt + ((g & 1) ? b : 0) + ((g & 2) ? s2x : 0);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          if (pass[jj]) {
             lds_write64(lds_addr(wbuf + col * TMB + pos),
-                        make_key(v, (uint32_t)(j0 + lr0 + jj)));
+                        make_key(acc[jj], (uint32_t)(j0 + lr0 + jj)));
+            ++pos;
           }
-          cnt += __popcll(mc);
+        cnt += s2 + s2x;
+      } else {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const float v = acc[jj];
+          const bool pass = lr0 + jj < nloc && v >= tau;
+          const uint64_t bm = __ballot(pass);
+          if (bm != 0ull) {
+            const uint64_t mc = bm & colmask;
+            if (pass) {
+              const int pos = cnt + __popcll(mc & below);
+              lds_write64(lds_addr(wbuf + col * TMB + pos),
+                          make_key(v, (uint32_t)(j0 + lr0 + jj)));
+            }
+            cnt += __popcll(mc);
+          }
         }
       }
     }
@@ -2738,6 +2834,7 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
 #endif
       }
     }
+    if (TT_TM_SHTAU && qv && g == 0) tau_sh[col][w] = tau;  // published for the other waves
   };
 
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -2755,6 +2852,7 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
     if (t + PD < n_tiles) issue(t + PD);
     I8CLK(2);
     if (cw) {
+      const float shtau = read_shtau();
       const uint32_t so = (uint32_t)((t % SLOTS) * TILE_B);
       u32x4 fr[KS];
       static_for<KS>([&](auto s_) __attribute__((always_inline)) {
@@ -2767,7 +2865,7 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
       // the tile's scale (its 64-row scale tile) x the query's t: one product per lane
       const float st = ssc[(int)(((int64_t)t * TR) >> 6)] * tq;
       I8CLK(6);
-      if (t > 0 && TT_I8_EXP_PART != 1) appends(acc, t - 1);
+      if (t > 0 && TT_I8_EXP_PART != 1) appends(acc, t - 1, shtau);
       I8CLK(3);
       lds_wait<0>();
       I8CLK(4);
@@ -2798,7 +2896,7 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
     for (int i = 0; i < 8; ++i) g_i8clk[(blk * TM_WAVES + w) * 8 + i] = ck[i];
   }
 #endif
-  if (cw && n_tiles > 0) appends(acc, n_tiles - 1);
+  if (cw && n_tiles > 0) appends(acc, n_tiles - 1, read_shtau());
   wait_vm<0>();
   __shared__ int ncw[CW][TM_NQ];
   if (w < CW && lane < nq && g == 0) ncw[w][lane] = cnt;  // (0 when TT_I8_EXP_NOCOMP)
@@ -4075,7 +4173,7 @@ extern "C" int tt_scan_topk_i8f32(const float* db, const int8_t* db_i8, const fl
                  out_idx, "null pointer");
   const int ep = tt_padded_dim(d);
   if (ep != 384 && ep != 768) return fail(TT_ERR_UNSUPPORTED, "int8 single pass: E 384 / 768");
-  if (nq > TM_NQ_RUN) return fail(TT_ERR_UNSUPPORTED, "int8 single pass: nq <= 4");
+  if (nq > TM_NQ_RUN) return fail(TT_ERR_UNSUPPORTED, "int8 single pass: nq <= TM_NQ_RUN (4)");
   TT_REQUIRE(ld_i8 >= ep && ld_i8 % 16 == 0 && ((uintptr_t)db_i8 % 16) == 0,
              "int8 image: ld_i8 >= tt_padded_dim(d), multiple of 16, 16-B aligned");
   TT_REQUIRE(x_norm_max >= 0.0f && x_resid_max >= 0.0f && s_max >= 0.0f,
