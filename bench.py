@@ -311,7 +311,7 @@ def batch_sweep(a, shard, shard16, n, E, K, bounds, dev, i8=None):
             tot.append(ev[2].elapsed_time(ev[3]))
             lvl.append(ev[0].elapsed_time(ev[1]))
         tw, l_ = float(np.median(tot)), float(np.median(lvl))
-        # end to end through the serving path (one PreparedSearch call per batch; nq <= 4 takes
+        # end to end through the serving path (one PreparedSearch call per batch; nq <= 8 takes
         # the int8 single pass when the catalog has its image, same results)
         def prepared(i8_):
             ps = kernels.PreparedSearch(shard, shard16, n, E, B, K, bounds, i8=i8_)
@@ -1080,7 +1080,7 @@ def main():
             tot.append(ev[2].elapsed_time(ev[3]))
             lvl.append(ev[0].elapsed_time(ev[1]))
         lvl_ms = statistics.median(lvl)
-        # the int8 single pass the serving path takes for nq <= 4 (tt_scan_topk_i8f32, same
+        # the int8 single pass the serving path takes for nq <= 8 (tt_scan_topk_i8f32, same
         # results): its image is built once per catalog, like the bf16 one
         i8 = kernels.i8_image(shard, E) if ep in kernels.I8_DIMS else None
         i8_lvl = []
@@ -1127,7 +1127,7 @@ def main():
         result["single_buyer_search"] = {
             "nq": 1, "ms_per_search": one_ms,
             "ms_per_search_is": ("kernels.PreparedSearch device call (no host copies); the int8 "
-                                 "single pass (nq <= 4), bit-identical to the bf16 pass"
+                                 "single pass (nq <= 8), bit-identical to the bf16 pass"
                                  if i8 is not None else
                                  "kernels.PreparedSearch device call (no host copies)"),
             **i8_info,

@@ -133,7 +133,7 @@ int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n, in
                          void* ev_start, void* ev_stop);
 
 /* ---------------------------------------------------------------------------------
- * Same results as tt_scan_topk_f32 for the one-buyer serving call (nq <= 4, padded dim 384
+ * Same results as tt_scan_topk_f32 for the one-buyer serving call (nq <= 8, padded dim 384
  * or 768, k <= 128; src/api/server.py:241-244 -> vector_db.py:160 retrieve): one streaming pass
  * over an INT8 image of the catalog (tt_i8_image: half the bytes of the bf16 image), a
  * per-(query, slab) top-16 on v_mfma_i32_16x16x64_i8 with the exact f32 scores of the kept

@@ -54,7 +54,9 @@ def _i8_search(K, db, x16_ref, n, d, q, k):
 @pytest.mark.parametrize("n,d,nq,k", [(100_000, 384, 1, 100), (300_001, 384, 4, 128),
                                       (1000, 384, 2, 10), (50_000, 700, 3, 100),
                                       (70_000, 768, 1, 1), (257, 384, 1, 128),
-                                      (1_000_000, 384, 1, 100)])
+                                      (1_000_000, 384, 1, 100), (200_000, 384, 5, 100),
+                                      (1_000_000, 384, 8, 100), (30_001, 700, 7, 64),
+                                      (100_000, 768, 8, 128)])
 def test_scan_topk_i8_bit_exact_vs_oracle(K, oracle_mod, n, d, nq, k):
     rng = np.random.default_rng(n + nq + k)
     x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
@@ -74,14 +76,14 @@ def test_scan_topk_i8_mode_b_buyers_no_fallback(K, oracle_mod):
     x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
     db = dev_rows(x)
     codes, scales, b3 = K.i8_image(db, d)
-    ws = torch.empty(K.filter_workspace_bytes(n, d, 4, k), dtype=torch.uint8, device="cuda")
+    ws = torch.empty(K.filter_workspace_bytes(n, d, 8, k), dtype=torch.uint8, device="cuda")
     fb = 0
-    for rep in range(4):
-        h = rng.integers(0, n, (4, 20))
-        w = np.where(rng.random((4, 20)) < 0.75, 1.0, 5.0).astype(np.float32)
+    for rep, nq in enumerate((4, 4, 1, 8, 8)):  # both buffer layouts (4 and 8 queries)
+        h = rng.integers(0, n, (nq, 20))
+        w = np.where(rng.random((nq, 20)) < 0.75, 1.0, 5.0).astype(np.float32)
         q = oracle_mod.l2norm_rows(oracle_mod.weighted_avg_l2(x[h], w), 0)
         s, i = K.scan_topk_i8(db, codes, scales, n, d, dev_rows(q), k, b3.tolist(), workspace=ws)
-        fb += K.filter_fallback_count(ws, n, d, 4, k)
+        fb += K.filter_fallback_count(ws, n, d, nq, k)
         rs, ri = oracle_mod.scan_topk(x, q, k)
         assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
     assert fb == 0, fb
@@ -139,3 +141,28 @@ def test_retrieve_one_buyer_takes_the_i8_pass(K):
         got = vdb.retrieve(q[b], k=k)
         assert [p for p, _ in got] == [f"p{j}" for j in i16[b].tolist()]
         assert [v for _, v in got] == s16[b].tolist()
+
+
+def test_i8_abi_rejects_more_than_8_queries(K):
+    """The ABI's batch limit (nq <= 8, the 8-query buffer layout): nq = 9 is refused with
+    TT_ERR_UNSUPPORTED before any launch, and the Python wrapper raises."""
+    import ctypes
+
+    from twotower import _lib
+
+    n, d, k = 4096, 384, 10
+    db = torch.randn((n, d), device="cuda")
+    K.l2norm_rows(db, d, _lib.TT_NORM_ADD_EPS, out=db)
+    codes, scales, b3 = K.i8_image(db, d)
+    q = torch.randn((9, d), device="cuda")
+    with pytest.raises(ValueError):
+        K.scan_topk_i8(db, codes, scales, n, d, q, k, b3.tolist())
+    ws = torch.empty(K.filter_workspace_bytes(n, d, 9, k), dtype=torch.uint8, device="cuda")
+    out_s = torch.empty((9, k), device="cuda")
+    out_i = torch.empty((9, k), dtype=torch.int64, device="cuda")
+    X, R, S = (ctypes.c_float(v) for v in b3.tolist())
+    rc = _lib.lib().tt_scan_topk_i8f32(
+        db.data_ptr(), codes.data_ptr(), scales.data_ptr(), n, d, db.stride(0), codes.stride(0),
+        0, q.data_ptr(), 9, q.stride(0), k, X, R, S, out_s.data_ptr(), out_i.data_ptr(),
+        ws.data_ptr(), ws.numel(), None, None, None)
+    assert rc == _lib.TT_ERR_UNSUPPORTED

@@ -1962,6 +1962,10 @@ constexpr int TM_NQ = 16;     // queries per MFMA query block (the buffers' quer
 #endif
 TT_CHECK_EXP(TT_EXP_TM_NQ_RUN != 4, "TT_EXP_TM_NQ_RUN");
 constexpr int TM_NQ_RUN = TT_EXP_TM_NQ_RUN;
+// the int8 single pass (k_filter_topm_i8) runs up to 8 queries: its candidate buffers are laid
+// out for 4 (nq <= 4) or 8 queries (the kernel's QB), and 5-8 queries still beat the multi-level bf16
+// path (1M x 384, nq = 8: 0.128 vs 0.185 ms; 16: 0.249 vs 0.183, so 16 stays multi-level)
+constexpr int TM_NQ_I8 = TM_NQ_RUN > 8 ? TM_NQ_RUN : 8;
 constexpr int TM_M = 16;      // rows kept per (query, slab)
 constexpr int TM_BUF = 256;   // candidate buffer per query, split over the compute waves
 constexpr int TM_SLOTS = TT_EXP_TM_SLOTS, TM_PD = TM_SLOTS - 1;  // ring slots, tiles in flight
@@ -1980,10 +1984,7 @@ TT_CHECK_EXP(TT_TM_BIGBUF16 != 0, "TT_TM_BIGBUF16");
 // 9.7 (nq = 4) times per wave and slab -- nq 1 / 2 / 4: 0.094 / 0.104 / 0.129 -> 0.092 / 0.093 /
 // 0.094 ms per search; the bf16 pass (2 compute waves, 128 keys each) gains at nq = 4 (0.156 ->
 // 0.150) but loses at nq = 1 (0.141 -> 0.145), so it keeps the 16-query layout
-template <bool I8>
-constexpr int tm_qb() {
-  return (I8 || TT_TM_BIGBUF16) ? TM_NQ_RUN : TM_NQ;
-}
+constexpr int tm_qb16() { return TT_TM_BIGBUF16 ? TM_NQ_RUN : TM_NQ; }
 #ifndef TT_TM_PREFIX
 #define TT_TM_PREFIX 1  // 1: appends place a lane's 4 rows by one column prefix (0: per-row ballots)
 #endif
@@ -2031,7 +2032,7 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm(
   // one wave scoring the whole tile: 131 vs 122 us for the same stream without that work).
   // Each holds the query fragments (bf16 B operands, 16 queries) and its own per-query top-m
   // buffers tbuf[w][c][TMB].
-  constexpr int TM_QB = tm_qb<false>(), CW = RB, TMB = TM_NQ * TM_BUF / TM_QB / CW;
+  constexpr int TM_QB = tm_qb16(), CW = RB, TMB = TM_NQ * TM_BUF / TM_QB / CW;
   constexpr int CPER = TMB / 64;
   static_assert(TMB % 64 == 0 && TMB >= 2 * TM_M && CW <= TM_WAVES, "top-m buffer shape");
   const bool cw = w < CW;
@@ -2468,7 +2469,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_topm(
 #undef TT_FTS
 }
 
-// ------------------------------------------------------ single pass on the int8 image (nq <= 4)
+// ------------------------------------------------------ single pass on the int8 image (nq <= 8)
 // The one-buyer search reads the whole catalog image once, so its time is that image's bytes
 // (bf16: 768 MB at 1M x 384, ~124 us at 6.2 TB/s).  An int8 image (tt_i8_image: 64-row tiles
 // of codes n and one scale s) halves them.  The bound is looser than bf16's but still a
@@ -2535,7 +2536,7 @@ __device__ __forceinline__ int i8_swz(int r) {
   return EP == 768 ? (r & 15) : TT_I8_SWZ ? ((r >> 1) & 7) : (r & 7);
 }
 
-template <int EP>
+template <int EP, int QB>
 __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
     const int8_t* __restrict__ xc, int64_t ldc, const float* __restrict__ scales, int64_t n,
     const float* __restrict__ q, int nq, int64_t ldq, int rows_per_blk,
@@ -2574,7 +2575,7 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
     ssc[i] = st < ((n + 63) >> 6) ? scales[st] : 0.0f;
   }
 
-  constexpr int TM_QB = tm_qb<true>(), CW = RB, TMB = TM_NQ * TM_BUF / TM_QB / CW;
+  constexpr int TM_QB = QB, CW = RB, TMB = TM_NQ * TM_BUF / TM_QB / CW;
   constexpr int CPER = TMB / 64;
   static_assert(TMB % 64 == 0 && TMB >= 2 * TM_M && CW <= TM_WAVES, "top-m buffer shape");
   const bool cw = w < CW && !TT_I8_EXP_NOCOMP;
@@ -2584,8 +2585,8 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
   // tau bounds shared by the block's compute waves: a row below ANY wave's tau (each a lower
   // bound of the 16th best of distinct rows of this slab) is below the slab's 16th best, so
   // every wave may drop it -- each wave's appends follow the block's max
-  __shared__ __attribute__((aligned(16))) float tau_sh[TM_NQ_RUN][4];
-  if (TT_TM_SHTAU && w < 4 && lane < TM_NQ_RUN) tau_sh[lane][w] = -__builtin_huge_valf();
+  __shared__ __attribute__((aligned(16))) float tau_sh[QB][4];
+  if (TT_TM_SHTAU && w < 4 && lane < QB) tau_sh[lane][w] = -__builtin_huge_valf();
   float tq = 0.0f;  // the query's code scale t
   float tau = qv ? -__builtin_huge_valf() : __builtin_huge_valf();
   int cnt = 0;
@@ -2605,7 +2606,7 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
   // LDS reads complete in order)
   auto read_shtau = [&]() __attribute__((always_inline)) {
     if (!TT_TM_SHTAU) return -__builtin_huge_valf();
-    const f32x4 v = *(const f32x4*)&tau_sh[col < TM_NQ_RUN ? col : 0][0];
+    const f32x4 v = *(const f32x4*)&tau_sh[col < QB ? col : 0][0];
     return fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
   };
   if (cw) {
@@ -3657,7 +3658,8 @@ static FilterPlan plan_filter_uncached(int64_t n, int nq, int k, int ep) {
   for (int i = 0; i < nl; ++i) p.small = p.small && p.lv[i].n_slabs <= SM_THREADS;
   // single pass for the smallest batches: lists [nq][G][TM_M] and counts [nq][G] fit the
   // level workspace once max_slabs >= G (FL_CAP >= TM_M)
-  p.topm = nq <= TM_NQ_RUN && !topm_disabled() && device_cus() * TM_M <= TM_CAP &&
+  // (the bf16 single pass runs for nq <= TM_NQ_RUN; the int8 one up to TM_NQ_I8)
+  p.topm = nq <= TM_NQ_I8 && !topm_disabled() && device_cus() * TM_M <= TM_CAP &&
            device_cus() <= SM_THREADS;
   if (p.topm && p.max_slabs < device_cus()) p.max_slabs = device_cus();
   return p;
@@ -4040,7 +4042,7 @@ int scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n, int32
                         &p, &w);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
-  if (p.topm) {  // single pass: stream + per-slab top-m, final, exact fallback
+  if (p.topm && nq <= TM_NQ_RUN) {  // single pass: stream + per-slab top-m, final, fallback
     TT_REQUIRE(db != nullptr && out_score && out_idx, "null pointer");
     TT_REQUIRE(x_norm_max >= 0.0f && x_resid_max >= 0.0f,
                "x_norm_max / x_resid_max must be >= 0 (tt_bf16_image_bounds)");
@@ -4173,7 +4175,7 @@ extern "C" int tt_scan_topk_i8f32(const float* db, const int8_t* db_i8, const fl
                  out_idx, "null pointer");
   const int ep = tt_padded_dim(d);
   if (ep != 384 && ep != 768) return fail(TT_ERR_UNSUPPORTED, "int8 single pass: E 384 / 768");
-  if (nq > TM_NQ_RUN) return fail(TT_ERR_UNSUPPORTED, "int8 single pass: nq <= TM_NQ_RUN (4)");
+  if (nq > TM_NQ_I8) return fail(TT_ERR_UNSUPPORTED, "int8 single pass: nq <= 8");
   TT_REQUIRE(ld_i8 >= ep && ld_i8 % 16 == 0 && ((uintptr_t)db_i8 % 16) == 0,
              "int8 image: ld_i8 >= tt_padded_dim(d), multiple of 16, 16-B aligned");
   TT_REQUIRE(x_norm_max >= 0.0f && x_resid_max >= 0.0f && s_max >= 0.0f,
@@ -4194,14 +4196,12 @@ extern "C" int tt_scan_topk_i8f32(const float* db, const int8_t* db_i8, const fl
   uint64_t* xkeys = w.lists + (int64_t)nq * G * TM_M;
   if (ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "hipEventRecord(start)");
-  if (ep == 384)
-    hipLaunchKernelGGL(k_filter_topm_i8<384>, dim3(G), dim3(64 * TM_WAVES), 0, st, db_i8, ld_i8,
-                       tile_scales, n, q, nq, ld_q, (int)rpb, db, ld_db, x_norm_max, x_resid_max,
-                       s_max, w.eps2, w.lists, xkeys, w.counts, w.flags, w.qsel_n);
-  else
-    hipLaunchKernelGGL(k_filter_topm_i8<768>, dim3(G), dim3(64 * TM_WAVES), 0, st, db_i8, ld_i8,
-                       tile_scales, n, q, nq, ld_q, (int)rpb, db, ld_db, x_norm_max, x_resid_max,
-                       s_max, w.eps2, w.lists, xkeys, w.counts, w.flags, w.qsel_n);
+  // candidate buffers laid out for 4 queries (4x the rows each) or for 8
+  auto kern = ep == 384 ? (nq <= 4 ? k_filter_topm_i8<384, 4> : k_filter_topm_i8<384, TM_NQ_I8>)
+                        : (nq <= 4 ? k_filter_topm_i8<768, 4> : k_filter_topm_i8<768, TM_NQ_I8>);
+  hipLaunchKernelGGL(kern, dim3(G), dim3(64 * TM_WAVES), 0, st, db_i8, ld_i8, tile_scales, n, q,
+                     nq, ld_q, (int)rpb, db, ld_db, x_norm_max, x_resid_max, s_max, w.eps2,
+                     w.lists, xkeys, w.counts, w.flags, w.qsel_n);
   if ((rc = check_launch("k_filter_topm_i8"))) return rc;
   if (ev_stop && hipEventRecord((hipEvent_t)ev_stop, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "hipEventRecord(stop)");

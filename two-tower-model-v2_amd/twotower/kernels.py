@@ -232,7 +232,7 @@ def scan_topk_bf16(db: torch.Tensor, db16: torch.Tensor, n: int, d: int, q: torc
 
 
 I8_DIMS = (384, 768)  # padded dims of the int8 single pass (tt_scan_topk_i8f32)
-I8_NQ_MAX = 4
+I8_NQ_MAX = 8  # nq 5-8: the 8-query buffer layout (still ahead of the multi-level path)
 
 
 def i8_image(x: torch.Tensor, d: int, out3: torch.Tensor = None):
@@ -253,7 +253,7 @@ def i8_image(x: torch.Tensor, d: int, out3: torch.Tensor = None):
 def scan_topk_i8(db: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, n: int, d: int,
                  q: torch.Tensor, k: int, bounds3, row_base: int = 0,
                  workspace: torch.Tensor = None, out=None, events=(None, None)):
-    """Exact top-k (bit-identical to scan_topk) for nq <= 4 through the int8 single pass
+    """Exact top-k (bit-identical to scan_topk) for nq <= 8 through the int8 single pass
     (tt_scan_topk_i8f32): padded dim 384 / 768, k <= 128.  bounds3 = i8_image's out3 as host
     floats."""
     _check_2d(db, "db")
@@ -262,7 +262,7 @@ def scan_topk_i8(db: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, n:
         raise ValueError("codes must be the int8 image [n, ep] of db (i8_image)")
     nq = q.shape[0]
     if not (1 <= k <= min(n, FILTER_KMAX)) or nq > I8_NQ_MAX:
-        raise ValueError(f"scan_topk_i8: need 1 <= k ({k}) <= min(n, 128) and nq <= 4")
+        raise ValueError(f"scan_topk_i8: need 1 <= k ({k}) <= min(n, 128) and nq <= 8")
     if out is None:
         out = (torch.empty((nq, k), dtype=_f32, device=q.device),
                torch.empty((nq, k), dtype=torch.int64, device=q.device))
@@ -291,7 +291,7 @@ class PreparedSearch:
 
     def __init__(self, db: torch.Tensor, db16: torch.Tensor, n: int, d: int, nq: int, k: int,
                  bounds, row_base: int = 0, i8=None):
-        """i8 = (codes, scales, bounds3) from i8_image: nq <= 4 at padded dim 384 / 768 then
+        """i8 = (codes, scales, bounds3) from i8_image: nq <= 8 at padded dim 384 / 768 then
         runs the int8 single pass (tt_scan_topk_i8f32, same results)."""
         _check_2d(db, "db")
         _check_2d(db16, "db16", torch.bfloat16)

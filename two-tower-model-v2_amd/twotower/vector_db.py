@@ -46,7 +46,7 @@ class FlatIPIndex:
         self._bounds_dev = torch.zeros(2, dtype=torch.float32, device=self.device)
         self.bounds = (0.0, 0.0)
         self.ntotal = 0
-        self.i8 = None  # int8 image (codes, tile scales, bounds) for nq <= 4 searches
+        self.i8 = None  # int8 image (codes, tile scales, bounds) for nq <= 8 searches
         self._ws = _lib.StreamWorkspaces(4)  # search_device's workspace, one per HIP stream
         # host searches (the /retrieve path, FlatIPIndex.search_host): serving slots, each with
         # its own HIP stream, device query / output buffers, pinned host staging and filter
@@ -120,7 +120,7 @@ class FlatIPIndex:
     def search_device(self, q: torch.Tensor, k: int, method: str = "auto"):
         """q: [nq, ep] normalised device rows -> (scores [nq,k], labels [nq,k]) on device.
 
-        method "auto": bf16 filter + exact f32 re-rank for k <= 128 (nq <= 4 at padded dim 384 /
+        method "auto": bf16 filter + exact f32 re-rank for k <= 128 (nq <= 8 at padded dim 384 /
         768: the int8 single pass), else exact f32 scores + radix select (k <= 1024); "f32" /
         "bf16" force the f32 scan / the bf16 filter.  All give bit-identical results."""
         if k < 1:
@@ -391,7 +391,7 @@ class _ServingSlot:
         if akey != self.args_key:  # the C arguments, bound once per (state, nq, k)
             vp = ctypes.c_void_p
             qp, st = vp(self.q.data_ptr()), vp(self.stream.cuda_stream)
-            if use8:  # the int8 single pass (one-buyer /retrieve calls, nq <= 4)
+            if use8:  # the int8 single pass (one-buyer /retrieve calls, nq <= 8)
                 codes, scales, (X, R, S) = i8
                 self.fn = _lib.lib().tt_scan_topk_i8f32
                 self.args = (
