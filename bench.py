@@ -189,12 +189,13 @@ def configs1(a, dev, rank):
         # the same batches of 256 with two in flight (alternating streams, each with its own
         # encoder workspace / outputs / search workspace): a batch's GEMMs fill under two
         # rounds of tiles on 256 CUs, the other batch's kernels fill the rest
-        streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+        NS = getattr(a, "configs1_streams", 2)
+        streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(NS - 1)]
         bufs = [(torch.empty((BS, cfg["hidden"]), device=dev), torch.zeros((BS, ep), device=dev),
                  torch.empty_like(ws)) for _ in streams]
 
         def step2(j):
-            pooled_s, qn_s, ws_s = bufs[j % 2]
+            pooled_s, qn_s, ws_s = bufs[j % NS]
             ids, cu, mx = batches[j]
             nt = cu.numel() - 1
             enc.encode_packed(ids, cu, mx, out=pooled_s[:nt])
@@ -203,13 +204,13 @@ def configs1(a, dev, rank):
             kernels.l2norm_rows(y, E, _lib.TT_NORM_ADD_EPS, out=qn_s[:nt])
             kernels.scan_topk_bf16(cat, cat16, 100_000, E, qn_s[:nt], K, bnd, workspace=ws_s)
 
-        for j in range(2):
-            with torch.cuda.stream(streams[j % 2]):
+        for j in range(NS):
+            with torch.cuda.stream(streams[j % NS]):
                 step2(j)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for j in range(nb):
-            with torch.cuda.stream(streams[j % 2]):
+            with torch.cuda.stream(streams[j % NS]):
                 step2(j)
         torch.cuda.synchronize()
         dt2 = time.perf_counter() - t0
@@ -249,16 +250,19 @@ def configs1(a, dev, rank):
     it.head_prec = "x3"
     chunks = [pack_sequences(seqs[i:i + DB], dev) for i in range(0, n_txt, DB)]
     pooled = torch.empty((DB, cfg["hidden"]), device=dev)
+    qc = torch.zeros((DB, ep), device=dev)
+    wsc = torch.empty(kernels.filter_workspace_bytes(100_000, E, DB, K), dtype=torch.uint8,
+                      device=dev)
 
     def chunk_step(c):
         ids, cu, mx = chunks[c]
         nt = cu.numel() - 1
         enc.encode_packed(ids, cu, mx, out=pooled[:nt])
         y = it.head(pooled[:nt], bid[c * DB:c * DB + nt], cid[c * DB:c * DB + nt], use_cat=True)
-        for j in range(0, nt, BS):
-            nb_ = min(BS, nt - j)
-            kernels.l2norm_rows(y[j:j + nb_], E, _lib.TT_NORM_ADD_EPS, out=qn[:nb_])
-            kernels.scan_topk_bf16(cat, cat16, 100_000, E, qn[:nb_], K, bnd, workspace=ws)
+        # the top-100 of the chunk's new embeddings in one batched search (each query's exact
+        # top 100: the same answers as one search per 256)
+        kernels.l2norm_rows(y, E, _lib.TT_NORM_ADD_EPS, out=qc[:nt])
+        kernels.scan_topk_bf16(cat, cat16, 100_000, E, qc[:nt], K, bnd, workspace=wsc)
 
     chunk_step(0)
     torch.cuda.synchronize()
@@ -270,7 +274,8 @@ def configs1(a, dev, rank):
     res["x3_api_chunks"] = {
         "texts_per_s": n_txt / dtc, "device_batch": DB, "texts": n_txt,
         "is": ("ItemTower.encode_batch(texts, batch_size=256)'s device chunking (4096 texts per "
-               "encoder call, x3) + exact top-100 per 256 new embeddings")}
+               "encoder call, x3) + the exact top-100 of each new embedding (one batched search "
+               "per chunk)")}
     del enc
     out.update(res)
     out["value"] = res["x3"]["texts_per_s"]
@@ -621,6 +626,7 @@ def summary(result):
         s["batch_ms"] = {b: _sig(v["ms_per_search"]) for b, v in bs.items()}
     if "configs1" in result:
         s["configs1_texts_per_s"] = _sig(result["configs1"]["value"])
+        s["configs1_api_chunks_texts_per_s"] = _sig(result["configs1"]["x3_api_chunks"]["texts_per_s"])
     if "catalog_10m" in result:
         s["catalog_10m_queries_per_s"] = _sig(result["catalog_10m"]["queries_per_s"])
     if "catalog_10m_768" in result:

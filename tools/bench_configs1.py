@@ -1,30 +1,30 @@
-"""bench.py's configs[1] leg alone (x3 / bf16 / f32 encoders + top-100 per batch of 256).
-
-    python tools/bench_configs1.py [--texts 100000]
-"""
+"""configs[1] leg of bench.py with 2 / 3 / 4 batches in flight (bench.configs1, 25.6k texts
+per run): x3 texts/s on one stream and on NS streams."""
 import argparse
 import json
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
 
-import torch  # noqa: E402
-
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--texts", type=int, default=100_000)
-    a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    out = bench.configs1(argparse.Namespace(configs1_texts=a.texts), dev, 0)
-    keep = {p: {k: out[p][k] for k in ("texts_per_s", "texts_per_s_one_stream",
-                                        "texts_per_s_two_streams", "encode_ms_per_batch",
-                                        "ms_per_batch")} for p in ("x3", "bf16", "f32")}
-    keep["x3_api_chunks"] = out["x3_api_chunks"]["texts_per_s"]
-    print(json.dumps(keep))
+    out = {}
+    for rep in range(2):
+        for ns in (2, 3, 4):
+            a = argparse.Namespace(configs1_texts=25_600, configs1_streams=ns)
+            r = bench.configs1(a, dev, 0)
+            out.setdefault(str(ns), []).append(
+                {"x3_two_streams": round(r["x3"]["texts_per_s_two_streams"]),
+                 "x3_one_stream": round(r["x3"]["texts_per_s_one_stream"]),
+                 "bf16_ns": round(r["bf16"]["texts_per_s_two_streams"])})
+            print(ns, out[str(ns)][-1], flush=True)
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":
