@@ -348,11 +348,16 @@ constexpr int RG_BLOCKS_PER_CU = TT_RING_HALF ? 2 : 1;
 // flight: 1.5x the compute per tile covers the same lead time): 6.26-6.33 -> 5.99-6.02 ms
 // (A/B x2, one box).  Small batches (LVL 2: one-buyer searches are HBM-bound and want 3 tiles
 // in flight) and sample levels keep two blocks per wave.
+#ifndef TT_RING_S3
+#define TT_RING_S3 0  // 1: the large-batch sample level (LVL 3) at E = 384 with 3 query blocks too
+#endif
+TT_CHECK_EXP(TT_RING_S3, "TT_RING_S3");
 template <int EP, int LVL>
 struct RingK {
   static constexpr int QB = TT_RING_W4QB ? (EP == 384 && LVL == 1 ? TT_RING_W4QB
                                                                   : 2 * RingCfg<EP>::QB)
-                            : (EP == 384 && LVL == 1 && !TT_RING_HALF && !TT_RING_QB4)
+                            : (EP == 384 && (LVL == 1 || (LVL == 3 && TT_RING_S3)) &&
+                               !TT_RING_HALF && !TT_RING_QB4)
                                 ? 3
                             : (EP >= 512 && (LVL == 1 || LVL >= 3)) ? TT_RING_QB_WIDE
                                                                      : RingCfg<EP>::QB;
@@ -1314,6 +1319,10 @@ __global__ __launch_bounds__(256) void k_select_wave(const uint64_t* __restrict_
 // register e / 64; every list load of the query is issued before the first use, and the
 // selection runs on registers.  Same outputs as k_select_wave.
 constexpr int SR_GMAX = 16;
+#ifndef TT_SEL_BOUND
+#define TT_SEL_BOUND 1  // k_select_reg: bound + compaction before the bitwise search (0: off)
+#endif
+TT_CHECK_EXP(TT_SEL_BOUND != 1, "TT_SEL_BOUND");
 template <bool GROUPED>
 __global__ __launch_bounds__(256) void k_select_reg(const uint64_t* __restrict__ lists,
                                                     const int* __restrict__ counts, int n_slabs,
@@ -1486,6 +1495,62 @@ __global__ __launch_bounds__(256) void k_select_reg(const uint64_t* __restrict__
     return;
   }
   uint32_t T = 0;
+  // Bound first (TT_SEL_BOUND): the R-th largest of the lanes' top-1 (R <= 64) or top-2
+  // (R <= 128) keys is a lower bound L of the R-th largest key (>= R distinct keys reach it).
+  // The keys >= L (a few dozen above R) are compacted through LDS into <= 4 registers per lane,
+  // and the 32-step search runs there: for cand <= L both sets count >= R, above L they count
+  // alike, so T is the same.  (The search over all PER registers -- 32 x ni ballots -- was
+  // most of the selection's time: the sample level's ~2k keys per query.)
+  __shared__ uint32_t cmp_s[4][256];
+  int nc = -1;  // compacted keys (-1: none)
+  uint32_t ck[4] = {0u, 0u, 0u, 0u};
+  if (TT_SEL_BOUND && R <= 128 && ni > 4) {
+    uint32_t m1 = 0u, m2 = 0u;
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      if (i < ni) {
+        m2 = max(m2, min(m1, hv[i]));
+        m1 = max(m1, hv[i]);
+      }
+    uint32_t L = 0u;
+    for (int bit = 31; bit >= 0; --bit) {
+      const uint32_t cand = L | (1u << bit);
+      int cnt = __popcll(__ballot(m1 >= cand));
+      if (R > 64) cnt += __popcll(__ballot(m2 >= cand));
+      if (cnt >= R) L = cand;
+    }
+    int c = 0;
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      if (i < ni) c += __popcll(__ballot(hv[i] >= L && hv[i] != 0u));
+    if (c <= 256) {
+      int base = 0;
+#pragma unroll
+      for (int i = 0; i < PER; ++i)
+        if (i < ni) {
+          const bool in = hv[i] >= L && hv[i] != 0u;
+          const uint64_t bm = __ballot(in);
+          const int pos = base + (int)__builtin_amdgcn_mbcnt_hi(
+                                     (uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+          if (in) cmp_s[wv][pos] = hv[i];
+          base += __popcll(bm);
+        }
+      wave_sync();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ck[r] = lane + 64 * r < c ? cmp_s[wv][lane + 64 * r] : 0u;
+      nc = c;
+    }
+  }
+  if (nc >= 0) {
+    const int nr = __builtin_amdgcn_readfirstlane((nc + 63) / 64);
+    for (int bit = 31; bit >= 0; --bit) {
+      const uint32_t cand = T | (1u << bit);
+      int cnt = __popcll(__ballot(ck[0] >= cand));
+      if (nr > 1) cnt += __popcll(__ballot(ck[1] >= cand));
+      if (nr > 2) cnt += __popcll(__ballot(ck[2] >= cand)) + __popcll(__ballot(ck[3] >= cand));
+      if (cnt >= R) T = cand;
+    }
+  } else
   for (int bit = 31; bit >= 0; --bit) {
     const uint32_t cand = T | (1u << bit);
     // wave count by ballot + scalar popcount (a 6-step shuffle reduction per bit was a
