@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.join(ROOT, "two-tower-model-v2_amd"))
 from twotower import _lib, kernels  # noqa: E402
 from twotower.vector_db import FlatIPIndex, VectorDatabase  # noqa: E402
 
-VARIANTS = [(0, 8), (2, 8), (2, 4), (4, 4)]  # (LEAD_EXTRA, COALESCE_MAX)
+VARIANTS = [(0, 8), (0, 4), (0, 2), (0, 0)]  # (LEAD_EXTRA, COALESCE_MAX); 0: no coalescing
 
 
 def main():
@@ -59,14 +59,18 @@ def main():
 
     res = {f"lead{le}_max{cm}": {"1": [], "4": [], "8": [], "batch4": [], "batch8": []}
            for le, cm in VARIANTS}
+    def setv(le, cm):
+        idx.LEAD_EXTRA, idx.COALESCE_MAX = le, max(cm, 1)
+        idx.coalesce = cm > 0
+
     for v in VARIANTS:
-        idx.LEAD_EXTRA, idx.COALESCE_MAX = v
+        setv(*v)
         rate(1, 20)
         rate(4, 20)
     for rep in range(5):
         order = VARIANTS[rep % len(VARIANTS):] + VARIANTS[:rep % len(VARIANTS)]
         for le, cm in order:
-            idx.LEAD_EXTRA, idx.COALESCE_MAX = le, cm
+            setv(le, cm)
             r = res[f"lead{le}_max{cm}"]
             r["1"].append(rate(1)[0])
             v4, b4 = rate(4)

@@ -598,8 +598,11 @@ class VectorDatabase:
         # Python ints / floats first (.tolist()): per-element numpy scalars made a k = 1000
         # response cost ~0.25 ms of host time; float(np.float32 x) == the list's float of x
         for query_scores, query_indices in zip(scores.tolist(), indices.tolist()):
-            out.append([(ids[idx], score) for idx, score in zip(query_indices, query_scores)
-                        if idx < n])  # reference :165 (note: -1 would pass, as in the reference)
+            if query_indices and max(query_indices) < n:  # the common case: one C-level pass
+                out.append(list(zip(map(ids.__getitem__, query_indices), query_scores)))
+            else:
+                out.append([(ids[idx], score) for idx, score in zip(query_indices, query_scores)
+                            if idx < n])  # reference :165 (-1 would pass, as in the reference)
         return out
 
     def retrieve(self, query_embedding: np.ndarray, k: int = 10) -> List[Tuple[str, float]]:
