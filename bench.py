@@ -924,6 +924,10 @@ def main():
     else:
         ws_bytes = kernels.scan_workspace_bytes(hi - lo, E, nq, K)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    # the catalog's int8 image (built once with the index, like the bf16 one): the one-buyer
+    # single pass and the batched search's sample level run on it (same results)
+    img8 = (kernels.i8_image(shard, E) if a.method == "bf16" and not staged
+            and ep in kernels.I8_DIMS else None)
     s_shard = torch.empty((nq, K), device=dev)
     i_shard = torch.empty((nq, K), dtype=torch.int64, device=dev)
     L = _lib.lib()
@@ -935,7 +939,8 @@ def main():
             p0.record(stream)
         if a.method == "bf16":
             kernels.scan_topk_bf16(shard, shard16, hi - lo, E, qall, K, bounds, row_base=lo,
-                                   workspace=ws, out=(s_shard, i_shard), events=(e0, e1))
+                                   workspace=ws, out=(s_shard, i_shard), events=(e0, e1),
+                                   i8=img8)
         else:
             _lib.check(L.tt_scan_topk_f32_timed(
                 shard.data_ptr(), hi - lo, E, shard.stride(0), lo,
@@ -1049,6 +1054,8 @@ def main():
             "workload": "configs[2]: 1M x 384 catalog, 10k buyers/rank x 20 events, weighted-avg, "
                         "Mode B (history rows gathered), k=100",
             "catalog_rows": N, "dim": E, "buyers_per_rank": B, "history": S, "k": K,
+            "sample_level": ("int8 image (k_sample_i8; the threshold it places is certified by "
+                             "the exact re-rank)" if img8 is not None and ep == 384 else "bf16"),
             "backend": a.backend if world > 1 else None,
             "parallelism": f"catalog row-shard x{world}" + ((f" + RCCL all-gather(queries, filter stats), all-reduce(probe counts), all-to-all(top-k), {len(pipe.ex)} overlapped query chunks" if staged else " + RCCL all-gather(queries), all-to-all(top-k)") if world > 1 else ""),
         },
@@ -1101,7 +1108,7 @@ def main():
         lvl_ms = statistics.median(lvl)
         # the int8 single pass the serving path takes for nq <= 8 (tt_scan_topk_i8f32, same
         # results): its image is built once per catalog, like the bf16 one
-        i8 = kernels.i8_image(shard, E) if ep in kernels.I8_DIMS else None
+        i8 = img8
         i8_lvl = []
         if i8 is not None:
             for r in range(n1 + 3):

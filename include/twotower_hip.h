@@ -131,6 +131,17 @@ int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n, in
                          float* out_score, int64_t* out_idx,
                          void* workspace, int64_t workspace_bytes, void* stream,
                          void* ev_start, void* ev_stop);
+/* tt_scan_topk_bf16f32 for a catalog that also holds its int8 image (tt_i8_image; db_i8 may be
+ * NULL): a large batch (> 2048 queries) at padded dim 384 runs its first, sampled level on the
+ * int8 image (half the bytes, twice the MFMA rate).  That level only places the full level's
+ * threshold, which the exact re-rank certifies, so the results are the same bits. */
+int tt_scan_topk_bf16f32_i8s(const float* db, const uint16_t* db_bf16, const int8_t* db_i8,
+                             const float* tile_scales, int64_t n, int32_t d, int64_t ld_db,
+                             int64_t ld_i8, int64_t row_base, const float* q, int32_t nq,
+                             int64_t ld_q, int32_t k, float x_norm_max, float x_resid_max,
+                             float* out_score, int64_t* out_idx, void* workspace,
+                             int64_t workspace_bytes, void* stream, void* ev_start,
+                             void* ev_stop);
 
 /* ---------------------------------------------------------------------------------
  * Same results as tt_scan_topk_f32 for the one-buyer serving call (nq <= 8, padded dim 384
@@ -192,6 +203,9 @@ int tt_filter_workspace_layout(int64_t n, int32_t d, int32_t nq, int32_t k, int3
  * k_filter_topm and k_final_topm (the nq <= 4 single pass).  The kernels must then never read
  * that row and flag the query for the exact fallback.  where = 0 clears.  One-shot. */
 int tt_debug_plant_bad_row(int32_t where, int32_t query);
+/* 1 if this thread's last tt_scan_topk_bf16f32[_i8s] call ran its sample level on the int8
+ * image (k_sample_i8), else 0 -- a test diagnostic. */
+int tt_debug_last_sample_i8(void);
 int tt_sharded_filter_begin(const uint16_t* sample_bf16, int64_t n_sample, int32_t d, int64_t ld,
                             const float* q, int32_t nq, int64_t ld_q, int32_t k, float* stats,
                             void* workspace, int64_t workspace_bytes, void* stream);

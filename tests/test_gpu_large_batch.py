@@ -23,12 +23,19 @@ def K():
     return kernels
 
 
-def _bf16_search(K, xd, n, d, qd, k):
+def _bf16_search(K, xd, n, d, qd, k, i8=False):
+    """i8: the catalog also holds its int8 image, so a large batch at padded dim 384 runs its
+    sample level on it (k_sample_i8; tt_scan_topk_bf16f32_i8s) -- asserted taken."""
+    from twotower import _lib
+
     x16 = xd.to(torch.bfloat16)
     ws = torch.empty(K.filter_workspace_bytes(n, d, qd.shape[0], k), dtype=torch.uint8,
                      device="cuda")
-    s, i = K.scan_topk_bf16(xd, x16, n, d, qd, k, bounds(K, xd, x16, d), workspace=ws)
+    img = K.i8_image(xd, d) if i8 else None
+    s, i = K.scan_topk_bf16(xd, x16, n, d, qd, k, bounds(K, xd, x16, d), workspace=ws, i8=img)
     torch.cuda.synchronize()
+    if i8:
+        assert _lib.lib().tt_debug_last_sample_i8() == int(_lib.padded_dim(d) == 384)
     return s, i, K.filter_fallback_count(ws, n, d, qd.shape[0], k)
 
 
@@ -48,21 +55,24 @@ def test_large_batch_threshold_is_crossed():
     assert int(re.search(r"constexpr int RG_SMALL_NQ = (\d+);", src).group(1)) == 2048
 
 
+@pytest.mark.parametrize("i8", [False, True])
 @pytest.mark.parametrize("nq", [2049, 4096])
-def test_large_batch_iid_bit_exact_vs_oracle(K, oracle_mod, nq):
+def test_large_batch_iid_bit_exact_vs_oracle(K, oracle_mod, nq, i8):
     """n = 100k, k = 100: every query bit-exact vs the C oracle (2049 = one query past the
-    threshold, a 1-query ragged last tile; 4096 = 16 full 256-query tiles)."""
+    threshold, a 1-query ragged last tile; 4096 = 16 full 256-query tiles); with and without
+    the int8 sample level."""
     rng = np.random.default_rng(nq)
     n, d, k = 100_000, 384, 100
     x, q = _iid(oracle_mod, rng, n, nq)
-    s, i, fb = _bf16_search(K, dev_rows(x), n, d, dev_rows(q), k)
+    s, i, fb = _bf16_search(K, dev_rows(x), n, d, dev_rows(q), k, i8=i8)
     rs, ri = oracle_mod.scan_topk(x, q, k)
     assert np.array_equal(i.cpu().numpy(), ri)
     assert np.array_equal(s.cpu().numpy(), rs)
     assert fb == 0  # iid data: the optimistic thresholds hold
 
 
-def test_large_batch_clustered_bit_exact(K, oracle_mod):
+@pytest.mark.parametrize("i8", [False, True])
+def test_large_batch_clustered_bit_exact(K, oracle_mod, i8):
     """Near-duplicate clusters (tiny score gaps, band overflow -> exact fallback for some
     queries) and queries that sit on a cluster centre, nq = 4096 (ragged n)."""
     rng = np.random.default_rng(101)
@@ -73,15 +83,16 @@ def test_large_batch_clustered_bit_exact(K, oracle_mod):
     q = rng.standard_normal((nq, d)).astype(np.float32)
     q[::3] = c[rng.integers(0, 200, len(q[::3]))]
     q = oracle_mod.l2norm_rows(q, 0)
-    s, i, fb = _bf16_search(K, dev_rows(x), n, d, dev_rows(q), k)
+    s, i, fb = _bf16_search(K, dev_rows(x), n, d, dev_rows(q), k, i8=i8)
     rs, ri = oracle_mod.scan_topk(x, q, k)
     assert np.array_equal(i.cpu().numpy(), ri)
     assert np.array_equal(s.cpu().numpy(), rs)
 
 
-def test_large_batch_duplicates_and_special_queries(K, oracle_mod):
+@pytest.mark.parametrize("i8", [False, True])
+def test_large_batch_duplicates_and_special_queries(K, oracle_mod, i8):
     """Exact duplicate rows (ties on both scores -> lower row first), zero queries (all scores
-    0: rows 0..k-1), a NaN catalog row, nq = 4096."""
+    0: rows 0..k-1), a NaN catalog row, a NaN query, nq = 4096."""
     rng = np.random.default_rng(102)
     n, d, nq, k = 60_000, 384, 4096, 128
     base = oracle_mod.l2norm_rows(rng.standard_normal((n // 4, d)).astype(np.float32), 0)
@@ -91,7 +102,8 @@ def test_large_batch_duplicates_and_special_queries(K, oracle_mod):
     q[::5] = base[rng.integers(0, n // 4, len(q[::5]))]
     q[17] = 0.0
     q[4095] = 0.0
-    s, i, fb = _bf16_search(K, dev_rows(x), n, d, dev_rows(q), k)
+    q[2222, 3] = np.nan  # every slot (-inf, -1), as the f32 scan
+    s, i, fb = _bf16_search(K, dev_rows(x), n, d, dev_rows(q), k, i8=i8)
     rs, ri = oracle_mod.scan_topk(x, q, k)
     gi = i.cpu().numpy()
     assert np.array_equal(gi, ri)
@@ -113,17 +125,19 @@ def test_large_batch_other_dims(K, oracle_mod, d, k):
 
 
 @pytest.mark.slow
-def test_configs2_full_size_bit_exact(K, oracle_mod):
-    """configs[2] exactly as bench.py runs it: 1M x 384 catalog, 10k queries, k = 100.
-    Every query bit-exact vs the exact f32 MFMA scan; 64 queries (spread over all 40 query
-    tiles, incl. the 16-query last tile) bit-exact vs the C oracle; no fallbacks."""
+@pytest.mark.parametrize("i8", [False, True])
+def test_configs2_full_size_bit_exact(K, oracle_mod, i8):
+    """configs[2] exactly as bench.py runs it: 1M x 384 catalog, 10k queries, k = 100 (with and
+    without the int8 sample level).  Every query bit-exact vs the exact f32 MFMA scan; 64
+    queries (spread over all 40 query tiles, incl. the 16-query last tile) bit-exact vs the C
+    oracle; no fallbacks."""
     n, d, nq, k = 1_000_000, 384, 10_000, 100
     g = torch.Generator(device="cuda").manual_seed(2)
     x = torch.randn((n, d), generator=g, device="cuda")
     K.l2norm_rows(x, d, 0, out=x)
     q = torch.randn((nq, d), generator=g, device="cuda")
     K.l2norm_rows(q, d, 0, out=q)
-    s, i, fb = _bf16_search(K, x, n, d, q, k)
+    s, i, fb = _bf16_search(K, x, n, d, q, k, i8=i8)
     fs, fi = K.scan_topk(x, n, d, q, k)
     assert fb == 0
     assert torch.equal(i, fi), int((i != fi).any(dim=1).sum())

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--dim", type=int, default=384)
     ap.add_argument("--nq", type=int, default=10_000)
     ap.add_argument("--k", type=int, default=100)
+    ap.add_argument("--i8", action="store_true",
+                    help="call tt_scan_topk_bf16f32_i8s with the catalog's int8 image")
     a = ap.parse_args()
     N, E, B, S, K = a.n, a.dim, a.nq, 20, a.k
     dev = torch.device("cuda", 0)
@@ -40,6 +42,7 @@ def main():
     x16 = torch.empty((N, ep), device=dev, dtype=torch.bfloat16)
     kernels.l2norm_rows(table, E, _lib.TT_NORM_ADD_EPS, out=x, out_bf16=x16)
     bnd = kernels.bf16_image_bounds(x, x16, E).tolist()
+    img = kernels.i8_image(x, E) if a.i8 else None
     gb = torch.Generator(device=dev).manual_seed(3)
     hist = torch.randint(0, N, (B, S), generator=gb, device=dev)
     w = torch.ones((B, S), device=dev)
@@ -56,6 +59,14 @@ def main():
             ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32,
             ctypes.c_float, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        if a.i8:
+            L.tt_scan_topk_bf16f32_i8s.restype = ctypes.c_int
+            L.tt_scan_topk_bf16f32_i8s.argtypes = [
+                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, ctypes.c_float,
+                ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.tt_filter_workspace_bytes.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                                 ctypes.c_int32, ctypes.POINTER(ctypes.c_int64)]
         need = ctypes.c_int64(0)
@@ -71,12 +82,18 @@ def main():
     def run(L, ws, out, timed):
         if timed:
             ev[2].record(stream)
-        rc = L.tt_scan_topk_bf16f32(x.data_ptr(), x16.data_ptr(), N, E, x.stride(0), 0,
-                                    q.data_ptr(), B, q.stride(0), K, bnd[0], bnd[1],
-                                    out[0].data_ptr(), out[1].data_ptr(), ws.data_ptr(),
-                                    ws.numel(), stream.cuda_stream,
-                                    ev[0].cuda_event if timed else None,
-                                    ev[1].cuda_event if timed else None)
+        evs = (ev[0].cuda_event if timed else None, ev[1].cuda_event if timed else None)
+        if a.i8:
+            rc = L.tt_scan_topk_bf16f32_i8s(
+                x.data_ptr(), x16.data_ptr(), img[0].data_ptr(), img[1].data_ptr(), N, E,
+                x.stride(0), img[0].stride(0), 0, q.data_ptr(), B, q.stride(0), K, bnd[0],
+                bnd[1], out[0].data_ptr(), out[1].data_ptr(), ws.data_ptr(), ws.numel(),
+                stream.cuda_stream, *evs)
+        else:
+            rc = L.tt_scan_topk_bf16f32(x.data_ptr(), x16.data_ptr(), N, E, x.stride(0), 0,
+                                        q.data_ptr(), B, q.stride(0), K, bnd[0], bnd[1],
+                                        out[0].data_ptr(), out[1].data_ptr(), ws.data_ptr(),
+                                        ws.numel(), stream.cuda_stream, *evs)
         assert rc == 0, rc
         if timed:
             ev[3].record(stream)

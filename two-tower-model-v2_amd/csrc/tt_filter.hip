@@ -3095,6 +3095,204 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_topm_i8(
   band_rank_out<EP>(bl, nb, qid, k, row_base, out_s, out_i);
 }
 
+// ------------------------------------------ the batched sample level on the int8 image
+// The first level of a large batch (a stride-16 sample, theta = -inf: every 32-row tile's
+// maximum is a candidate, k_filter_ring<EP, 3>'s append_tmax) only has to PLACE the full
+// level's threshold: its a_J becomes aref, the full level keeps a >= aref - 1.25 eps and the
+// re-rank certifies from exact scores that s_k >= aref - eps / 8 (full_theta / full_cert), a
+// query failing it takes the exact fallback.  So any estimate of a_J gives exact results; its
+// quality only sets how many candidates the full level keeps.  Here the tile maxima come from
+// the int8 image (tt_i8_image) at twice the bf16 MFMA rate and half the bytes: the coded
+// query (k_query_eps: t m, t = max|q| / 127) against the rows' codes, times the rows' tile
+// scale and t (positive, so they commute with the max).  Same lists / counts layout as the
+// ring level (key = orderable max << 32 | ~first row of the tile); NaN maxima enter as -inf.
+// E = 384, stride 16 (4 consecutive sample rows share one 64-row scale tile): 4 waves x 64
+// queries per block, the slab's 64-row chunks through a 4-slot LDS ring (3 in flight,
+// global_load_lds per lane: the sample rows are 16 catalog rows apart), per chunk and wave
+// 4 row blocks x 4 query blocks x 6 k-steps of v_mfma_i32_16x16x64_i8.
+#ifndef TT_SI_WAVES
+#define TT_SI_WAVES 4  // waves (x 64 queries) per block of k_sample_i8: 4 (1 per SIMD) or 8
+#endif
+TT_CHECK_EXP(TT_SI_WAVES != 4, "TT_SI_WAVES");
+#ifndef TT_SI_PIPE
+#define TT_SI_PIPE 0  // 1: a chunk's epilogue runs between the next chunk's MFMAs (slower: A/B)
+#endif
+TT_CHECK_EXP(TT_SI_PIPE != 0, "TT_SI_PIPE");
+constexpr int SI_NW = TT_SI_WAVES, SI_QPB = 64 * SI_NW, SI_CH = 64, SI_SLOTS = 4;
+constexpr int SI_PD = SI_SLOTS - 1, SI_MAXROWS = 32 * FL_CAP;  // sample rows per slab
+template <int EP>
+__global__ __launch_bounds__(64 * SI_NW, 1) void k_sample_i8(
+    const int8_t* __restrict__ xc, int64_t ldc, const float* __restrict__ scales, int64_t n_rows,
+    int64_t n_sample, int rows_per_slab, int n_slabs, const int8_t* __restrict__ q8,
+    const float* __restrict__ tq8, int nq, uint64_t* __restrict__ lists,
+    int* __restrict__ counts) {
+  static_assert(EP == 384, "int8 sample level: E = 384");
+  constexpr int KS = EP / 64, CPR = EP / 16, TILE_B = SI_CH * EP, PIECES = TILE_B / 1024;
+  constexpr int PPW = PIECES / SI_NW, STRIDE = 16;
+  static_assert(PIECES % SI_NW == 0 && CPR == 24, "chunk layout");
+  __shared__ __attribute__((aligned(16))) char ring[SI_SLOTS * TILE_B];
+  // the slab's row-group scales (4 sample rows = 64 catalog rows = one scale tile), staged once:
+  // a global load per chunk in the epilogue stalled on its latency every chunk
+  __shared__ float ssc[SI_MAXROWS / 4];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int slab = (int)(blockIdx.x % (unsigned)n_slabs), qt = (int)(blockIdx.x / (unsigned)n_slabs);
+  const int64_t j0 = (int64_t)slab * rows_per_slab;  // sample rows; rows_per_slab % 64 == 0
+  const int64_t j1 = j0 + rows_per_slab < n_sample ? j0 + rows_per_slab : n_sample;
+  if (j0 >= j1) return;
+  const int n_ch = (int)((j1 - j0 + SI_CH - 1) / SI_CH);
+  if (tid < SI_QPB) {
+    const int qi = qt * SI_QPB + tid;
+    if (qi < nq) counts[(int64_t)qi * n_slabs + slab] = (int)((j1 - j0 + 31) / 32);
+  }
+  // DMA: piece pp of a chunk = LDS bytes [1024 (w + 4 pp), +1024); lane chunk P = 64 (w + 4 pp)
+  // + lane = (row r, position pos); its source is chunk pos ^ swz(r) of sample row r (clamped
+  // to the slab's last row), so row r's logical chunk c sits at position c ^ swz(r)
+  auto issue = [&](int c) __attribute__((always_inline)) {
+    char* slot = ring + (c % SI_SLOTS) * TILE_B;
+#pragma unroll
+    for (int pp = 0; pp < PPW; ++pp) {
+      const int P = (w + SI_NW * pp) * 64 + lane;
+      const int r = P / CPR;
+      int64_t i = j0 + (int64_t)c * SI_CH + r;
+      i = i < j1 ? i : j1 - 1;
+      const int8_t* src = xc + (i * STRIDE) * ldc + 16 * ((P % CPR) ^ i8_swz<EP>(r));
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)src,
+          (__attribute__((address_space(3))) void*)(slot + (w + SI_NW * pp) * 1024), 16, 0, 0);
+    }
+  };
+  for (int c = 0; c < SI_PD && c < n_ch; ++c) issue(c);
+  for (int gi = tid; gi < n_ch * (SI_CH / 4); gi += 64 * SI_NW) {
+    int64_t i = j0 + 4 * (int64_t)gi;
+    i = i < j1 ? i : j1 - 1;  // clamped rows are copies of the slab's last row
+    ssc[gi] = scales[(i * STRIDE) >> 6];
+  }
+  // this wave's 64 queries as B fragments: lanes (g, col) hold chunk 4 s + g of query 16 qb + col
+  u32x4 qf[4][KS];
+  float tqv[4];
+  const int qbase = qt * SI_QPB + 64 * w;
+#pragma unroll
+  for (int qb = 0; qb < 4; ++qb) {
+    const int qi = qbase + 16 * qb + col;
+    const bool v = qi < nq;
+    const int8_t* qp = q8 + (int64_t)(v ? qi : 0) * EP + 16 * g;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) qf[qb][s] = *(const u32x4*)(qp + 64 * s);
+    tqv[qb] = v ? tq8[qi] : 0.0f;
+  }
+  // A-fragment LDS addresses: row 16 rb + col, logical chunk 4 s + g at position (4 s + g) ^ f,
+  // f = swz(16 rb + col) = (col >> 1) & 7 for every rb
+  const int f = i8_swz<EP>(col);
+  uint32_t lrd[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) lrd[s] = lds_addr(ring) + col * EP + 16 * ((4 * s + g) ^ f);
+  // the tile keys of chunk c from its accumulators: per query the max over each 32-row tile,
+  // scaled by the rows' tile scale (rows 4 g .. 4 g + 3 of row block rb share one: sample row
+  // i -> catalog row 16 i) and the query's t; lane (g, col) then writes query 16 g + col's two
+  // keys (tiles 2 c, 2 c + 1) as one 16-B store
+  auto emit = [&](const i32x4 (&ac)[4][4], int c) __attribute__((always_inline)) {
+    float srb[4];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) srb[rb] = ssc[(SI_CH / 4) * c + 4 * rb + g];
+    float mq[4][2];
+#pragma unroll
+    for (int qb = 0; qb < 4; ++qb)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float m = -__builtin_huge_valf();
+#pragma unroll
+        for (int r2 = 0; r2 < 2; ++r2) {
+          const i32x4 v = ac[2 * h + r2][qb];
+          const int mi = max(max(v[0], v[1]), max(v[2], v[3]));
+          m = fmaxf(m, (float)mi * srb[2 * h + r2]);
+        }
+        const auto x16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m),
+                                                          false, false);
+        m = fmaxf(__uint_as_float(x16[0]), __uint_as_float(x16[1]));
+        const auto x32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m),
+                                                          false, false);
+        m = fmaxf(__uint_as_float(x32[0]), __uint_as_float(x32[1])) * tqv[qb];
+        mq[qb][h] = m == m ? m : -__builtin_huge_valf();
+      }
+    float m0 = mq[0][0], m1 = mq[0][1];
+#pragma unroll
+    for (int qb = 1; qb < 4; ++qb)
+      if (g == qb) {
+        m0 = mq[qb][0];
+        m1 = mq[qb][1];
+      }
+    const int qi = qbase + 16 * g + col;
+    if (qi < nq) {
+      const int64_t t0 = j0 + (int64_t)c * SI_CH;
+      const uint64_t k0 = make_key(m0, (uint32_t)(t0 * STRIDE));
+      const uint64_t k1 = make_key(m1, (uint32_t)((t0 + 32) * STRIDE));
+      *(u32x4*)(lists + ((int64_t)qi * n_slabs + slab) * FL_CAP + 2 * c) =
+          u32x4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32)};
+    }
+  };
+  // chunk c's MFMAs, with chunk c - 1's epilogue (emit) placed after the first k-step: its
+  // VALU work issues between the MFMAs instead of after them (all waves of the block move in
+  // lockstep between barriers, so no other wave would fill the MFMA pipes meanwhile)
+  i32x4 accp[4][4];
+  for (int c = 0; c < n_ch; ++c) {
+    const int younger = n_ch - 1 - c < SI_PD - 1 ? n_ch - 1 - c : SI_PD - 1;
+    if (younger >= 2) wait_vm<2 * PPW>();
+    else if (younger == 1) wait_vm<PPW>();
+    else wait_vm<0>();
+    lds_barrier();  // chunk c landed (every wave's pieces); every wave is done with chunk c - 1
+    if (c + SI_PD < n_ch) issue(c + SI_PD);
+    const uint32_t so = (uint32_t)((c % SI_SLOTS) * TILE_B);
+    i32x4 acc[4][4];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+      for (int qb = 0; qb < 4; ++qb) acc[rb][qb] = i32x4{0, 0, 0, 0};
+    // k-step S's 4 A fragments are read while step S - 1's 16 MFMAs run (one step ahead; with
+    // 8 waves the SIMD's other wave covers the LDS latency and one buffer fits 256 registers)
+    constexpr int AB = SI_NW == 4 ? 2 : 1;
+    u32x4 a[2][4];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) a[0][rb] = lds_read128<0>(lrd[0] + so + rb * 16 * EP);
+    static_for<KS>([&](auto s_) __attribute__((always_inline)) {
+      constexpr int S = decltype(s_)::value;
+      if constexpr (AB == 1) {
+        if constexpr (S > 0) {
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb) a[S & 1][rb] = lds_read128<0>(lrd[S] + so + rb * 16 * EP);
+        }
+        lds_wait<0>();
+      } else if constexpr (S + 1 < KS) {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+          a[(S + 1) & 1][rb] = lds_read128<0>(lrd[S + 1] + so + rb * 16 * EP);
+        lds_wait<4>();
+      } else {
+        lds_wait<0>();
+      }
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        reg_tie(a[S & 1][rb]);
+#pragma unroll
+        for (int qb = 0; qb < 4; ++qb)
+          acc[rb][qb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+              __builtin_bit_cast(i32x4, a[S & 1][rb]), __builtin_bit_cast(i32x4, qf[qb][S]),
+              acc[rb][qb], 0, 0, 0);
+      }
+      if constexpr (S == 0 && TT_SI_PIPE)
+        if (c > 0) emit(accp, c - 1);
+    });
+    if (!TT_SI_PIPE) emit(acc, c);
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+      for (int qb = 0; qb < 4; ++qb) accp[rb][qb] = acc[rb][qb];
+  }
+  if (TT_SI_PIPE && n_ch > 0) emit(accp, n_ch - 1);
+  wait_vm<0>();
+}
+
 // sharded finish: pcount[q][i] = #rows over ALL shards with a >= t_i (all-reduced SUM).
 // pcount[q][0] < k: the sample threshold did not certify -> exact fallback on every shard
 // (identical decision on all ranks).  Else A_k >= t* = the highest probe with >= k rows, so
@@ -3483,9 +3681,27 @@ __global__ __launch_bounds__(256) void k_query_eps(const float* __restrict__ q, 
                                                    float* __restrict__ aref,
                                                    int* __restrict__ flags,
                                                    int* __restrict__ qsel_n,
-                                                   uint16_t* __restrict__ q16) {
+                                                   uint16_t* __restrict__ q16,
+                                                   int8_t* __restrict__ q8 = nullptr,
+                                                   float* __restrict__ tq8 = nullptr) {
   const int qi = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (qi >= nq) return;
+  if (q8) {  // the int8 sample level's coded query t m (k_sample_i8): t = max|q| / 127
+    const float* qr = q + (int64_t)qi * ldq;
+    float mx = 0.0f;
+    for (int i = lane; i < EP; i += 64) mx = fmaxf(mx, fabsf(qr[i]));
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    const float t = mx / 127.0f;
+    for (int i = lane; i < EP; i += 64) {
+      int c = 0;
+      if (t > 0.0f) {
+        c = (int)rintf(qr[i] / t);
+        c = c > 127 ? 127 : c < -127 ? -127 : c;
+      }
+      q8[(int64_t)qi * EP + i] = (int8_t)c;
+    }
+    if (lane == 0) tq8[qi] = t;
+  }
   if (q16) {  // the bf16 image the ring levels load (the conversion k_filter_ring's f32 path does)
     const float* qr = q + (int64_t)qi * ldq;
     for (int c = lane; c < EP / 8; c += 64) {
@@ -3772,6 +3988,8 @@ struct FilterWs {
   int64_t scan_ws_bytes;
   uint16_t* q16;     // [nq][ep] bf16 query image (k_query_eps), for the ring levels
   bool q16_valid;    // written by this search's k_query_eps
+  int8_t* q8;        // [nq][ep] int8-coded queries + tq8[nq] (k_query_eps), for k_sample_i8
+  float* tq8;
   int64_t total;
 };
 
@@ -3807,6 +4025,8 @@ static FilterWs carve(void* base, const FilterPlan& p, int64_t n, int d, int nq,
   w.scan_ws = take(sb);
   w.q16 = (uint16_t*)take((int64_t)nq * tt_padded_dim(d) * 2);
   w.q16_valid = false;
+  w.q8 = (int8_t*)take((int64_t)nq * tt_padded_dim(d));
+  w.tq8 = (float*)take((int64_t)nq * 4);
   w.total = off;
   return w;
 }
@@ -3936,7 +4156,7 @@ int filter_setup(const float* db, const uint16_t* db_bf16, int64_t n, int32_t d,
 // (the tmax-first plan): that launch initialises it (*fold filled in, no launch here).
 int filter_init(FilterWs& w, const float* q, int nq, int64_t ld_q, int ep, float x_norm_max,
                 float x_resid_max, hipStream_t st, const FilterPlan* p = nullptr,
-                QueryInit* fold = nullptr, bool want_q16 = false) {
+                QueryInit* fold = nullptr, bool want_q16 = false, bool want_q8 = false) {
   TT_REQUIRE(x_norm_max >= 0.0f && x_resid_max >= 0.0f,
              "x_norm_max / x_resid_max must be >= 0 (tt_bf16_image_bounds)");
   if (fold) *fold = QueryInit{0.0f, 0.0f, nullptr, nullptr, nullptr, nullptr};
@@ -3951,7 +4171,8 @@ int filter_init(FilterWs& w, const float* q, int nq, int64_t ld_q, int ep, float
   case E:                                                                                     \
     hipLaunchKernelGGL(k_query_eps<E>, dim3(eps_grid), dim3(256), 0, st, q, nq, ld_q,         \
                        x_norm_max, x_resid_max, w.eps2, w.theta, w.aref, w.flags, w.qsel_n,  \
-                       want_q16 ? w.q16 : nullptr);                                          \
+                       want_q16 ? w.q16 : nullptr, want_q8 ? w.q8 : nullptr,                 \
+                       want_q8 ? w.tq8 : nullptr);                                           \
     break;
     TT_QE(64) TT_QE(128) TT_QE(256) TT_QE(384) TT_QE(512) TT_QE(768)
 #undef TT_QE
@@ -3960,13 +4181,35 @@ int filter_init(FilterWs& w, const float* q, int nq, int64_t ld_q, int ep, float
   return check_launch("filter_init");
 }
 
+// whether this thread's last batched search ran its sample level on the int8 image (tests)
+thread_local bool g_last_sample_i8 = false;
+// the int8 image for the batched sample level (k_sample_i8), when the caller has one
+struct I8Sample {
+  const int8_t* x;
+  int64_t ld;
+  const float* scales;
+};
+#ifndef TT_SAMPLE_I8
+#define TT_SAMPLE_I8 1  // 0: the batched sample level stays on the bf16 ring (A/B builds)
+#endif
+TT_CHECK_EXP(TT_SAMPLE_I8 != 1, "TT_SAMPLE_I8");
+// the batched search's first level runs on the int8 image: a large batch at E = 384 whose plan
+// starts with the stride-16 tile-max sample and has the full level after it
+static bool sample_i8_applies(const FilterPlan& p, int nq, int ep, bool q16) {
+  return TT_SAMPLE_I8 && ep == 384 && q16 && nq > RG_SMALL_NQ && !p.small &&
+         p.n_levels == 2 && p.lv[0].tmax && !p.lv[0].dense && p.lv[0].stride == 16 &&
+         p.lv[0].n_slabs_p == 0 && p.lv[0].rows_per_slab % SI_CH == 0 &&
+         (int64_t)p.lv[0].rows_per_slab / 32 <= FL_CAP;
+}
+
 // level li (+ its selection in `mode`); events around the full-catalog level
 int filter_level(const FilterPlan& p, const FilterWs& w, int li, int mode, const uint16_t* db16,
                  int64_t n, int64_t ld_db, const float* q, int nq, int64_t ld_q, int k, int ep,
                  hipStream_t st, void* ev_start, void* ev_stop, const float* stats = nullptr,
                  int* pcount = nullptr, float* smax_out = nullptr, int fin = 0,
                  bool no_select = false,
-                 const QueryInit& qi = QueryInit{0.0f, 0.0f, nullptr, nullptr, nullptr, nullptr}) {
+                 const QueryInit& qi = QueryInit{0.0f, 0.0f, nullptr, nullptr, nullptr, nullptr},
+                 const I8Sample* i8s = nullptr) {
   const Level& L = p.lv[li];
   const bool last = li == p.n_levels - 1;
   // k_filter_ring addresses a tile (TR sample rows) through one buffer resource: < 2 GiB
@@ -3974,6 +4217,12 @@ int filter_level(const FilterPlan& p, const FilterWs& w, int li, int mode, const
     return fail(TT_ERR_UNSUPPORTED, "bf16 filter: catalog sample stride too large");
   if (last && ev_start && hipEventRecord((hipEvent_t)ev_start, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "hipEventRecord(start)");
+  if (i8s && li == 0 && !last) {  // sample_i8_applies checked the shape
+    const int nqt = (nq + SI_QPB - 1) / SI_QPB;
+    hipLaunchKernelGGL(k_sample_i8<384>, dim3((unsigned)(nqt * L.n_slabs)), dim3(64 * SI_NW), 0, st,
+                       i8s->x, i8s->ld, i8s->scales, n, L.n_sample, L.rows_per_slab, L.n_slabs,
+                       w.q8, w.tq8, nq, w.lists, w.counts);
+  } else
   switch (ep) {
     case 64: launch_level<64>(L, db16, n, ld_db, q, nq, ld_q, w, st, qi); break;
     case 128: launch_level<128>(L, db16, n, ld_db, q, nq, ld_q, w, st, qi); break;
@@ -4097,7 +4346,8 @@ int scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n, int32
                       int64_t ld_db, int64_t row_base, const float* q, int32_t nq, int64_t ld_q,
                       int32_t k, float x_norm_max, float x_resid_max, float* out_score,
                       int64_t* out_idx, void* workspace, int64_t workspace_bytes, void* stream,
-                      void* ev_start, void* ev_stop) {
+                      void* ev_start, void* ev_stop, const I8Sample* i8 = nullptr) {
+  g_last_sample_i8 = false;
   TT_REQUIRE(nq >= 0, "nq < 0");
   if (nq == 0) return TT_OK;
   int ep;
@@ -4161,8 +4411,10 @@ int scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n, int32
   // large batches: k_query_eps (one launch) writes the per-query state AND the bf16 query
   // image the ring levels load; smaller ones fold the state into the first level (no launch)
   const bool q16 = nq > RG_SMALL_NQ && q16_enabled();
+  const I8Sample* i8s = i8 && sample_i8_applies(p, nq, ep, q16) ? i8 : nullptr;
+  g_last_sample_i8 = i8s != nullptr;
   if ((rc = filter_init(w, q, nq, ld_q, ep, x_norm_max, x_resid_max, st, &p, q16 ? nullptr : &qinit,
-                        q16)))
+                        q16, i8s != nullptr)))
     return rc;
   if (q16) qinit = QueryInit{0.0f, 0.0f, nullptr, nullptr, nullptr, nullptr};
   // small batches: block-per-query selection (k_select_small) and a fused selection +
@@ -4175,7 +4427,8 @@ int scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n, int32
     const int fin = li == p.n_levels - 2;
     if ((rc = filter_level(p, w, li, last ? 1 : 0, db_bf16, n, ld_db, q, nq, ld_q, k, ep, st,
                            ev_start, ev_stop, nullptr, nullptr, nullptr, fin, small,
-                           li == 0 ? qinit : QueryInit{0.0f, 0.0f, nullptr, nullptr, nullptr, nullptr})))
+                           li == 0 ? qinit : QueryInit{0.0f, 0.0f, nullptr, nullptr, nullptr, nullptr},
+                           i8s)))
       return rc;
     if (small && !last) {
       hipLaunchKernelGGL(k_select_small, dim3(nq), dim3(SM_THREADS), 0, st, w.lists, w.counts,
@@ -4226,6 +4479,26 @@ extern "C" int tt_scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, in
   g_plant_where = 0;
   return rc;
 }
+
+extern "C" int tt_scan_topk_bf16f32_i8s(const float* db, const uint16_t* db_bf16,
+                                        const int8_t* db_i8, const float* tile_scales, int64_t n,
+                                        int32_t d, int64_t ld_db, int64_t ld_i8, int64_t row_base,
+                                        const float* q, int32_t nq, int64_t ld_q, int32_t k,
+                                        float x_norm_max, float x_resid_max, float* out_score,
+                                        int64_t* out_idx, void* workspace, int64_t workspace_bytes,
+                                        void* stream, void* ev_start, void* ev_stop) {
+  TT_REQUIRE(db_i8 == nullptr || (tile_scales != nullptr && ld_i8 >= tt_padded_dim(d) &&
+                                  ld_i8 % 16 == 0 && ((uintptr_t)db_i8 % 16) == 0),
+             "int8 image: tile scales, ld_i8 >= tt_padded_dim(d), multiple of 16, 16-B aligned");
+  const I8Sample i8{db_i8, ld_i8, tile_scales};
+  const int rc = scan_topk_bf16f32(db, db_bf16, n, d, ld_db, row_base, q, nq, ld_q, k, x_norm_max,
+                                   x_resid_max, out_score, out_idx, workspace, workspace_bytes,
+                                   stream, ev_start, ev_stop, db_i8 ? &i8 : nullptr);
+  g_plant_where = 0;
+  return rc;
+}
+
+extern "C" int tt_debug_last_sample_i8(void) { return g_last_sample_i8 ? 1 : 0; }
 
 extern "C" int tt_scan_topk_i8f32(const float* db, const int8_t* db_i8, const float* tile_scales,
                                   int64_t n, int32_t d, int64_t ld_db, int64_t ld_i8,

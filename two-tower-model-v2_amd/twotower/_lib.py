@@ -77,6 +77,10 @@ SIGNATURES = {
     "tt_scan_topk_bf16f32": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _i64, _vp, _i32, _i64,
                                             _i32, ctypes.c_float, ctypes.c_float, _vp, _vp, _vp,
                                             _i64, _vp, _vp, _vp]),
+    "tt_scan_topk_bf16f32_i8s": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _i32, _i64, _i64, _i64,
+                                                _vp, _i32, _i64, _i32, ctypes.c_float,
+                                                ctypes.c_float, _vp, _vp, _vp, _i64, _vp, _vp,
+                                                _vp]),
     "tt_sharded_workspace_bytes": (ctypes.c_int, [_i64, _i32, _i32, _i32, ctypes.POINTER(_i64)]),
     "tt_sharded_fallback_offset": (ctypes.c_int, [_i64, _i32, _i32, _i32, ctypes.POINTER(_i64)]),
     "tt_filter_workspace_layout": (ctypes.c_int, [_i64, _i32, _i32, _i32, _i32,
@@ -113,6 +117,7 @@ SIGNATURES = {
                                    _i32, _i32, _i32, _i32, _vp]),
     "tt_x3_split_weights": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp]),
     "tt_debug_plant_bad_row": (ctypes.c_int, [_i32, _i32]),
+    "tt_debug_last_sample_i8": (ctypes.c_int, []),
     "tt_attention_varlen_x3i": (ctypes.c_int, [_vp, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _i64,
                                                _vp]),
     "tt_x3i_weights": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp]),

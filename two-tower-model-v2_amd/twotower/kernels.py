@@ -201,10 +201,12 @@ def filter_workspace_layout(n: int, d: int, nq: int, k: int, sharded: bool = Fal
 
 def scan_topk_bf16(db: torch.Tensor, db16: torch.Tensor, n: int, d: int, q: torch.Tensor,
                    k: int, bounds, row_base: int = 0, workspace: torch.Tensor = None,
-                   out=None, events=(None, None)):
+                   out=None, events=(None, None), i8=None):
     """Exact top-k (bit-identical to scan_topk) via the bf16 filter + f32 re-rank (k <= 128).
 
-    bounds = (x_norm_max, x_resid_max) host floats, e.g. bf16_image_bounds(...).tolist()."""
+    bounds = (x_norm_max, x_resid_max) host floats, e.g. bf16_image_bounds(...).tolist().
+    i8 = (codes, tile scales[, bounds]) from i8_image: a large batch at padded dim 384 then runs
+    its sample level on the int8 image (tt_scan_topk_bf16f32_i8s; same results)."""
     x_norm_max, x_resid_max = (float(v) for v in bounds)
     _check_2d(db, "db")
     _check_2d(db16, "db16", torch.bfloat16)
@@ -223,11 +225,21 @@ def scan_topk_bf16(db: torch.Tensor, db16: torch.Tensor, n: int, d: int, q: torc
     if workspace is None or workspace.numel() < need:
         workspace = torch.empty(need, dtype=torch.uint8, device=q.device)
     e0, e1 = events
+    ev = (e0.cuda_event if e0 is not None else None, e1.cuda_event if e1 is not None else None)
+    if i8 is not None:
+        codes, scales = i8[0], i8[1]
+        if codes.dtype != torch.int8 or codes.dim() != 2 or codes.shape[0] < n:
+            raise ValueError("i8 codes must be the int8 image [n, ep] of db (i8_image)")
+        check(lib().tt_scan_topk_bf16f32_i8s(
+            _ptr(db), _ptr(db16), _ptr(codes), _ptr(scales), n, d, db.stride(0),
+            codes.stride(0), row_base, _ptr(q), nq, q.stride(0), k, ctypes.c_float(x_norm_max),
+            ctypes.c_float(x_resid_max), _ptr(out[0]), _ptr(out[1]), _ptr(workspace),
+            workspace.numel(), stream_ptr(), *ev), "tt_scan_topk_bf16f32_i8s")
+        return out
     check(lib().tt_scan_topk_bf16f32(
         _ptr(db), _ptr(db16), n, d, db.stride(0), row_base, _ptr(q), nq, q.stride(0), k,
         ctypes.c_float(x_norm_max), ctypes.c_float(x_resid_max), _ptr(out[0]), _ptr(out[1]), _ptr(workspace), workspace.numel(),
-        stream_ptr(), e0.cuda_event if e0 is not None else None,
-        e1.cuda_event if e1 is not None else None), "tt_scan_topk_bf16f32")
+        stream_ptr(), *ev), "tt_scan_topk_bf16f32")
     return out
 
 

@@ -144,9 +144,10 @@ class FlatIPIndex:
                 codes, scales, b3 = self.i8
                 return kernels.scan_topk_i8(self.xb, codes, scales, self.ntotal, self.d, q, k, b3,
                                             row_base=self.row_base, workspace=ws)
-            if use_bf16:
+            if use_bf16:  # (a large batch runs its sample level on the int8 image, if any)
                 return kernels.scan_topk_bf16(self.xb, self.xb16, self.ntotal, self.d, q, k,
-                                              self.bounds, row_base=self.row_base, workspace=ws)
+                                              self.bounds, row_base=self.row_base, workspace=ws,
+                                              i8=self.i8 if method == "auto" else None)
             if use_select:
                 return kernels.scan_topk_select(self.xb, self.ntotal, self.d, q, k,
                                                 row_base=self.row_base, workspace=ws)
@@ -383,7 +384,8 @@ class _ServingSlot:
         nq, d = x.shape
         ws = self._workspace(n, nq, k, "bf16")
         use8 = i8 is not None and nq <= kernels.I8_NQ_MAX
-        akey = (skey, nq, k, ws.data_ptr(), self.s.data_ptr(), bounds, normalize, use8)
+        akey = (skey, nq, k, ws.data_ptr(), self.s.data_ptr(), bounds, normalize, use8,
+                i8[0].data_ptr() if i8 is not None else 0)  # (build_i8 may replace the image)
         if akey != self.args_key and akey in self.bound:  # coalesced batches vary nq
             self.fn, self.args, self.h2d, self.norm, self.d2h = self.bound[akey]
             self.bound.move_to_end(akey)
@@ -400,6 +402,15 @@ class _ServingSlot:
                     ctypes.c_float(X), ctypes.c_float(R), ctypes.c_float(S),
                     vp(self.s.data_ptr()), vp(self.i.data_ptr()), vp(ws.data_ptr()), ws.numel(),
                     st, None, None)
+            elif i8 is not None:  # a large batch's sample level on the int8 image (same results)
+                codes, scales, _ = i8
+                self.fn = _lib.lib().tt_scan_topk_bf16f32_i8s
+                self.args = (
+                    vp(xb.data_ptr()), vp(xb16.data_ptr()), vp(codes.data_ptr()),
+                    vp(scales.data_ptr()), n, d, xb.stride(0), codes.stride(0), ix.row_base, qp,
+                    nq, self.q.stride(0), k, ctypes.c_float(bounds[0]),
+                    ctypes.c_float(bounds[1]), vp(self.s.data_ptr()), vp(self.i.data_ptr()),
+                    vp(ws.data_ptr()), ws.numel(), st, None, None)
             else:
                 self.fn = _lib.lib().tt_scan_topk_bf16f32
                 self.args = (
@@ -427,7 +438,7 @@ class _ServingSlot:
             _lib.check(self.norm_fn(*self.norm), "tt_l2norm_rows_f32")
         rc = self.fn(*self.args)
         if rc:
-            _lib.check(rc, "tt_scan_topk_i8f32" if use8 else "tt_scan_topk_bf16f32")
+            _lib.check(rc, "tt_scan_topk_i8f32" if use8 else "tt_scan_topk_bf16f32[_i8s]")
         for a in self.d2h:
             if hip.hipMemcpyAsync(*a):
                 raise RuntimeError("hipMemcpyAsync (results) failed")
