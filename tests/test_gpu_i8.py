@@ -166,3 +166,26 @@ def test_i8_abi_rejects_more_than_8_queries(K):
         0, q.data_ptr(), 9, q.stride(0), k, X, R, S, out_s.data_ptr(), out_i.data_ptr(),
         ws.data_ptr(), ws.numel(), None, None, None)
     assert rc == _lib.TT_ERR_UNSUPPORTED
+
+
+def test_retrieve_batch_large_takes_the_i8_sample_level(K, oracle_mod):
+    """VectorDatabase.retrieve_batch with 2100 queries at d = 384 (the serving slot's large
+    batch) runs its sample level on the index's int8 image (tt_scan_topk_bf16f32_i8s) and
+    returns the C oracle's exact top k."""
+    from twotower import VectorDatabase, _lib
+
+    rng = np.random.default_rng(33)
+    n, d, k, nq = 40_000, 384, 50, 2100
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    vdb = VectorDatabase(d)
+    vdb.build_index(x, [f"p{j}" for j in range(n)])
+    assert vdb.index.i8 is not None
+    q = rng.standard_normal((nq, d)).astype(np.float32)
+    got = vdb.retrieve_batch(q, k=k)
+    assert _lib.lib().tt_debug_last_sample_i8() == 1
+    xn = oracle_mod.vector_db_normalize(x)
+    qn = oracle_mod.vector_db_normalize(q)
+    rs, ri = oracle_mod.scan_topk(xn, qn, k)
+    for b in (0, 1, 777, 2099):
+        assert [p for p, _ in got[b]] == [f"p{j}" for j in ri[b].tolist()]
+        assert [v for _, v in got[b]] == rs[b].tolist()

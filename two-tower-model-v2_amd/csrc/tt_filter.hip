@@ -3118,7 +3118,12 @@ TT_CHECK_EXP(TT_SI_WAVES != 4, "TT_SI_WAVES");
 #define TT_SI_PIPE 0  // 1: a chunk's epilogue runs between the next chunk's MFMAs (slower: A/B)
 #endif
 TT_CHECK_EXP(TT_SI_PIPE != 0, "TT_SI_PIPE");
-constexpr int SI_NW = TT_SI_WAVES, SI_QPB = 64 * SI_NW, SI_CH = 64, SI_SLOTS = 4;
+#ifndef TT_SI_CH
+#define TT_SI_CH 64  // sample rows per chunk (one barrier each): 64 (4-slot ring) or 128 (3 slots)
+#endif
+TT_CHECK_EXP(TT_SI_CH != 64, "TT_SI_CH");
+constexpr int SI_NW = TT_SI_WAVES, SI_QPB = 64 * SI_NW, SI_CH = TT_SI_CH;
+constexpr int SI_SLOTS = SI_CH == 64 ? 4 : 3, SI_RB = SI_CH / 16, SI_NT = SI_CH / 32;
 constexpr int SI_PD = SI_SLOTS - 1, SI_MAXROWS = 32 * FL_CAP;  // sample rows per slab
 template <int EP>
 __global__ __launch_bounds__(64 * SI_NW, 1) void k_sample_i8(
@@ -3133,7 +3138,7 @@ __global__ __launch_bounds__(64 * SI_NW, 1) void k_sample_i8(
   __shared__ __attribute__((aligned(16))) char ring[SI_SLOTS * TILE_B];
   // the slab's row-group scales (4 sample rows = 64 catalog rows = one scale tile), staged once:
   // a global load per chunk in the epilogue stalled on its latency every chunk
-  __shared__ float ssc[SI_MAXROWS / 4];
+  __shared__ float ssc[(SI_MAXROWS + SI_CH) / 4];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int col = lane & 15, g = lane >> 4;
@@ -3192,15 +3197,16 @@ __global__ __launch_bounds__(64 * SI_NW, 1) void k_sample_i8(
   // scaled by the rows' tile scale (rows 4 g .. 4 g + 3 of row block rb share one: sample row
   // i -> catalog row 16 i) and the query's t; lane (g, col) then writes query 16 g + col's two
   // keys (tiles 2 c, 2 c + 1) as one 16-B store
-  auto emit = [&](const i32x4 (&ac)[4][4], int c) __attribute__((always_inline)) {
-    float srb[4];
+  const int ntiles = (int)((j1 - j0 + 31) / 32);
+  auto emit = [&](const i32x4 (&ac)[SI_RB][4], int c) __attribute__((always_inline)) {
+    float srb[SI_RB];
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb) srb[rb] = ssc[(SI_CH / 4) * c + 4 * rb + g];
-    float mq[4][2];
+    for (int rb = 0; rb < SI_RB; ++rb) srb[rb] = ssc[(SI_CH / 4) * c + 4 * rb + g];
+    float mq[4][SI_NT];
 #pragma unroll
     for (int qb = 0; qb < 4; ++qb)
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < SI_NT; ++h) {
         float m = -__builtin_huge_valf();
 #pragma unroll
         for (int r2 = 0; r2 < 2; ++r2) {
@@ -3216,26 +3222,32 @@ __global__ __launch_bounds__(64 * SI_NW, 1) void k_sample_i8(
         m = fmaxf(__uint_as_float(x32[0]), __uint_as_float(x32[1])) * tqv[qb];
         mq[qb][h] = m == m ? m : -__builtin_huge_valf();
       }
-    float m0 = mq[0][0], m1 = mq[0][1];
+    float mm[SI_NT];
+#pragma unroll
+    for (int h = 0; h < SI_NT; ++h) mm[h] = mq[0][h];
 #pragma unroll
     for (int qb = 1; qb < 4; ++qb)
-      if (g == qb) {
-        m0 = mq[qb][0];
-        m1 = mq[qb][1];
-      }
+      if (g == qb)
+#pragma unroll
+        for (int h = 0; h < SI_NT; ++h) mm[h] = mq[qb][h];
     const int qi = qbase + 16 * g + col;
     if (qi < nq) {
-      const int64_t t0 = j0 + (int64_t)c * SI_CH;
-      const uint64_t k0 = make_key(m0, (uint32_t)(t0 * STRIDE));
-      const uint64_t k1 = make_key(m1, (uint32_t)((t0 + 32) * STRIDE));
-      *(u32x4*)(lists + ((int64_t)qi * n_slabs + slab) * FL_CAP + 2 * c) =
-          u32x4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32)};
+#pragma unroll
+      for (int h = 0; h < SI_NT; h += 2) {
+        const int t = SI_NT * c + h;  // tile within the slab (pairs never cross FL_CAP)
+        if (t >= ntiles) break;
+        const int64_t r0 = j0 + 32 * (int64_t)t;
+        const uint64_t k0 = make_key(mm[h], (uint32_t)(r0 * STRIDE));
+        const uint64_t k1 = make_key(mm[h + 1], (uint32_t)((r0 + 32) * STRIDE));
+        *(u32x4*)(lists + ((int64_t)qi * n_slabs + slab) * FL_CAP + t) =
+            u32x4{(uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32)};
+      }
     }
   };
   // chunk c's MFMAs, with chunk c - 1's epilogue (emit) placed after the first k-step: its
   // VALU work issues between the MFMAs instead of after them (all waves of the block move in
   // lockstep between barriers, so no other wave would fill the MFMA pipes meanwhile)
-  i32x4 accp[4][4];
+  i32x4 accp[SI_RB][4];
   for (int c = 0; c < n_ch; ++c) {
     const int younger = n_ch - 1 - c < SI_PD - 1 ? n_ch - 1 - c : SI_PD - 1;
     if (younger >= 2) wait_vm<2 * PPW>();
@@ -3244,35 +3256,35 @@ __global__ __launch_bounds__(64 * SI_NW, 1) void k_sample_i8(
     lds_barrier();  // chunk c landed (every wave's pieces); every wave is done with chunk c - 1
     if (c + SI_PD < n_ch) issue(c + SI_PD);
     const uint32_t so = (uint32_t)((c % SI_SLOTS) * TILE_B);
-    i32x4 acc[4][4];
+    i32x4 acc[SI_RB][4];
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb)
+    for (int rb = 0; rb < SI_RB; ++rb)
 #pragma unroll
       for (int qb = 0; qb < 4; ++qb) acc[rb][qb] = i32x4{0, 0, 0, 0};
     // k-step S's 4 A fragments are read while step S - 1's 16 MFMAs run (one step ahead; with
     // 8 waves the SIMD's other wave covers the LDS latency and one buffer fits 256 registers)
     constexpr int AB = SI_NW == 4 ? 2 : 1;
-    u32x4 a[2][4];
+    u32x4 a[2][SI_RB];
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb) a[0][rb] = lds_read128<0>(lrd[0] + so + rb * 16 * EP);
+    for (int rb = 0; rb < SI_RB; ++rb) a[0][rb] = lds_read128<0>(lrd[0] + so + rb * 16 * EP);
     static_for<KS>([&](auto s_) __attribute__((always_inline)) {
       constexpr int S = decltype(s_)::value;
       if constexpr (AB == 1) {
         if constexpr (S > 0) {
 #pragma unroll
-          for (int rb = 0; rb < 4; ++rb) a[S & 1][rb] = lds_read128<0>(lrd[S] + so + rb * 16 * EP);
+          for (int rb = 0; rb < SI_RB; ++rb) a[S & 1][rb] = lds_read128<0>(lrd[S] + so + rb * 16 * EP);
         }
         lds_wait<0>();
       } else if constexpr (S + 1 < KS) {
 #pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
+        for (int rb = 0; rb < SI_RB; ++rb)
           a[(S + 1) & 1][rb] = lds_read128<0>(lrd[S + 1] + so + rb * 16 * EP);
-        lds_wait<4>();
+        lds_wait<SI_RB>();
       } else {
         lds_wait<0>();
       }
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb) {
+      for (int rb = 0; rb < SI_RB; ++rb) {
         reg_tie(a[S & 1][rb]);
 #pragma unroll
         for (int qb = 0; qb < 4; ++qb)
@@ -3285,7 +3297,7 @@ __global__ __launch_bounds__(64 * SI_NW, 1) void k_sample_i8(
     });
     if (!TT_SI_PIPE) emit(acc, c);
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb)
+    for (int rb = 0; rb < SI_RB; ++rb)
 #pragma unroll
       for (int qb = 0; qb < 4; ++qb) accp[rb][qb] = acc[rb][qb];
   }
@@ -4198,7 +4210,7 @@ TT_CHECK_EXP(TT_SAMPLE_I8 != 1, "TT_SAMPLE_I8");
 static bool sample_i8_applies(const FilterPlan& p, int nq, int ep, bool q16) {
   return TT_SAMPLE_I8 && ep == 384 && q16 && nq > RG_SMALL_NQ && !p.small &&
          p.n_levels == 2 && p.lv[0].tmax && !p.lv[0].dense && p.lv[0].stride == 16 &&
-         p.lv[0].n_slabs_p == 0 && p.lv[0].rows_per_slab % SI_CH == 0 &&
+         p.lv[0].n_slabs_p == 0 && p.lv[0].rows_per_slab % 64 == 0 &&
          (int64_t)p.lv[0].rows_per_slab / 32 <= FL_CAP;
 }
 
