@@ -3122,11 +3122,22 @@ TT_CHECK_EXP(TT_SI_PIPE != 0, "TT_SI_PIPE");
 #define TT_SI_CH 64  // sample rows per chunk (one barrier each): 64 (4-slot ring) or 128 (3 slots)
 #endif
 TT_CHECK_EXP(TT_SI_CH != 64, "TT_SI_CH");
-constexpr int SI_NW = TT_SI_WAVES, SI_QPB = 64 * SI_NW, SI_CH = TT_SI_CH;
-constexpr int SI_SLOTS = SI_CH == 64 ? 4 : 3, SI_RB = SI_CH / 16, SI_NT = SI_CH / 32;
-constexpr int SI_PD = SI_SLOTS - 1, SI_MAXROWS = 32 * FL_CAP;  // sample rows per slab
+#ifndef TT_SI_OCC2
+#define TT_SI_OCC2 0  // 1: two 4-wave blocks per CU (3-slot rings, slabs <= 2048 sample rows)
+#endif
+TT_CHECK_EXP(TT_SI_OCC2 != 0, "TT_SI_OCC2");
+#ifndef TT_SI_QBW
+#define TT_SI_QBW 4  // 16-query blocks per wave of k_sample_i8 (4: 64 queries; 2: 32)
+#endif
+TT_CHECK_EXP(TT_SI_QBW != 4, "TT_SI_QBW");
+constexpr int SI_NW = TT_SI_WAVES, SI_QBW = TT_SI_QBW, SI_QPB = 16 * SI_QBW * SI_NW;
+constexpr int SI_CH = TT_SI_CH;
+constexpr int SI_SLOTS = (SI_CH == 64 && !TT_SI_OCC2) ? 4 : 3, SI_RB = SI_CH / 16;
+constexpr int SI_NT = SI_CH / 32, SI_BPC = TT_SI_OCC2 ? 2 : 1;
+// sample rows per slab (the plan's FL_CAP tiles of 32; 2048 with two blocks per CU)
+constexpr int SI_PD = SI_SLOTS - 1, SI_MAXROWS = TT_SI_OCC2 ? 2048 : 32 * FL_CAP;
 template <int EP>
-__global__ __launch_bounds__(64 * SI_NW, 1) void k_sample_i8(
+__global__ __launch_bounds__(64 * SI_NW, SI_BPC) void k_sample_i8(
     const int8_t* __restrict__ xc, int64_t ldc, const float* __restrict__ scales, int64_t n_rows,
     int64_t n_sample, int rows_per_slab, int n_slabs, const int8_t* __restrict__ q8,
     const float* __restrict__ tq8, int nq, uint64_t* __restrict__ lists,
@@ -3175,11 +3186,11 @@ __global__ __launch_bounds__(64 * SI_NW, 1) void k_sample_i8(
     ssc[gi] = scales[(i * STRIDE) >> 6];
   }
   // this wave's 64 queries as B fragments: lanes (g, col) hold chunk 4 s + g of query 16 qb + col
-  u32x4 qf[4][KS];
-  float tqv[4];
-  const int qbase = qt * SI_QPB + 64 * w;
+  u32x4 qf[SI_QBW][KS];
+  float tqv[SI_QBW];
+  const int qbase = qt * SI_QPB + 16 * SI_QBW * w;
 #pragma unroll
-  for (int qb = 0; qb < 4; ++qb) {
+  for (int qb = 0; qb < SI_QBW; ++qb) {
     const int qi = qbase + 16 * qb + col;
     const bool v = qi < nq;
     const int8_t* qp = q8 + (int64_t)(v ? qi : 0) * EP + 16 * g;
@@ -3198,13 +3209,13 @@ __global__ __launch_bounds__(64 * SI_NW, 1) void k_sample_i8(
   // i -> catalog row 16 i) and the query's t; lane (g, col) then writes query 16 g + col's two
   // keys (tiles 2 c, 2 c + 1) as one 16-B store
   const int ntiles = (int)((j1 - j0 + 31) / 32);
-  auto emit = [&](const i32x4 (&ac)[SI_RB][4], int c) __attribute__((always_inline)) {
+  auto emit = [&](const i32x4 (&ac)[SI_RB][SI_QBW], int c) __attribute__((always_inline)) {
     float srb[SI_RB];
 #pragma unroll
     for (int rb = 0; rb < SI_RB; ++rb) srb[rb] = ssc[(SI_CH / 4) * c + 4 * rb + g];
-    float mq[4][SI_NT];
+    float mq[SI_QBW][SI_NT];
 #pragma unroll
-    for (int qb = 0; qb < 4; ++qb)
+    for (int qb = 0; qb < SI_QBW; ++qb)
 #pragma unroll
       for (int h = 0; h < SI_NT; ++h) {
         float m = -__builtin_huge_valf();
@@ -3226,12 +3237,12 @@ __global__ __launch_bounds__(64 * SI_NW, 1) void k_sample_i8(
 #pragma unroll
     for (int h = 0; h < SI_NT; ++h) mm[h] = mq[0][h];
 #pragma unroll
-    for (int qb = 1; qb < 4; ++qb)
+    for (int qb = 1; qb < SI_QBW; ++qb)
       if (g == qb)
 #pragma unroll
         for (int h = 0; h < SI_NT; ++h) mm[h] = mq[qb][h];
     const int qi = qbase + 16 * g + col;
-    if (qi < nq) {
+    if (g < SI_QBW && qi < nq) {
 #pragma unroll
       for (int h = 0; h < SI_NT; h += 2) {
         const int t = SI_NT * c + h;  // tile within the slab (pairs never cross FL_CAP)
@@ -3247,7 +3258,7 @@ __global__ __launch_bounds__(64 * SI_NW, 1) void k_sample_i8(
   // chunk c's MFMAs, with chunk c - 1's epilogue (emit) placed after the first k-step: its
   // VALU work issues between the MFMAs instead of after them (all waves of the block move in
   // lockstep between barriers, so no other wave would fill the MFMA pipes meanwhile)
-  i32x4 accp[SI_RB][4];
+  i32x4 accp[SI_RB][SI_QBW];
   for (int c = 0; c < n_ch; ++c) {
     const int younger = n_ch - 1 - c < SI_PD - 1 ? n_ch - 1 - c : SI_PD - 1;
     if (younger >= 2) wait_vm<2 * PPW>();
@@ -3256,14 +3267,14 @@ __global__ __launch_bounds__(64 * SI_NW, 1) void k_sample_i8(
     lds_barrier();  // chunk c landed (every wave's pieces); every wave is done with chunk c - 1
     if (c + SI_PD < n_ch) issue(c + SI_PD);
     const uint32_t so = (uint32_t)((c % SI_SLOTS) * TILE_B);
-    i32x4 acc[SI_RB][4];
+    i32x4 acc[SI_RB][SI_QBW];
 #pragma unroll
     for (int rb = 0; rb < SI_RB; ++rb)
 #pragma unroll
-      for (int qb = 0; qb < 4; ++qb) acc[rb][qb] = i32x4{0, 0, 0, 0};
+      for (int qb = 0; qb < SI_QBW; ++qb) acc[rb][qb] = i32x4{0, 0, 0, 0};
     // k-step S's 4 A fragments are read while step S - 1's 16 MFMAs run (one step ahead; with
     // 8 waves the SIMD's other wave covers the LDS latency and one buffer fits 256 registers)
-    constexpr int AB = SI_NW == 4 ? 2 : 1;
+    constexpr int AB = (SI_NW == 4 && !TT_SI_OCC2) ? 2 : 1;
     u32x4 a[2][SI_RB];
 #pragma unroll
     for (int rb = 0; rb < SI_RB; ++rb) a[0][rb] = lds_read128<0>(lrd[0] + so + rb * 16 * EP);
@@ -3287,7 +3298,7 @@ __global__ __launch_bounds__(64 * SI_NW, 1) void k_sample_i8(
       for (int rb = 0; rb < SI_RB; ++rb) {
         reg_tie(a[S & 1][rb]);
 #pragma unroll
-        for (int qb = 0; qb < 4; ++qb)
+        for (int qb = 0; qb < SI_QBW; ++qb)
           acc[rb][qb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
               __builtin_bit_cast(i32x4, a[S & 1][rb]), __builtin_bit_cast(i32x4, qf[qb][S]),
               acc[rb][qb], 0, 0, 0);
@@ -3299,7 +3310,7 @@ __global__ __launch_bounds__(64 * SI_NW, 1) void k_sample_i8(
 #pragma unroll
     for (int rb = 0; rb < SI_RB; ++rb)
 #pragma unroll
-      for (int qb = 0; qb < 4; ++qb) accp[rb][qb] = acc[rb][qb];
+      for (int qb = 0; qb < SI_QBW; ++qb) accp[rb][qb] = acc[rb][qb];
   }
   if (TT_SI_PIPE && n_ch > 0) emit(accp, n_ch - 1);
   wait_vm<0>();
@@ -4211,7 +4222,7 @@ static bool sample_i8_applies(const FilterPlan& p, int nq, int ep, bool q16) {
   return TT_SAMPLE_I8 && ep == 384 && q16 && nq > RG_SMALL_NQ && !p.small &&
          p.n_levels == 2 && p.lv[0].tmax && !p.lv[0].dense && p.lv[0].stride == 16 &&
          p.lv[0].n_slabs_p == 0 && p.lv[0].rows_per_slab % 64 == 0 &&
-         (int64_t)p.lv[0].rows_per_slab / 32 <= FL_CAP;
+         (int64_t)p.lv[0].rows_per_slab <= SI_MAXROWS;
 }
 
 // level li (+ its selection in `mode`); events around the full-catalog level
