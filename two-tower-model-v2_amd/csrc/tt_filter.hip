@@ -288,9 +288,13 @@ template <> struct RingCfg<768> { static constexpr int TR = 16, QB = 1; };
 // XCC id, logical block) into g_blktime (tt_debug_blktimes): the launch's per-CU timeline
 #define TT_EXP_BLKTIME 0
 #endif
+#ifndef TT_EXP_BLKTIME_LVL
+#define TT_EXP_BLKTIME_LVL 1  // the k_filter_ring level (LVL) whose blocks TT_EXP_BLKTIME records
+#endif
 #if TT_EXP_BLKTIME
 constexpr int BLKTIME_MAX = 8192;
 __device__ unsigned long long g_blktime[BLKTIME_MAX * 4];
+__device__ unsigned long long g_blkph[BLKTIME_MAX * 2];  // k_filter_ring: tile 0 landed, loop end
 #endif
 TT_CHECK_EXP(TT_EXP_NOSEL || TT_EXP_NOWRITE || TT_EXP_MAXONLY ||
                  TT_EXP_SEL_STOP || TT_EXP_SEL_TIMING || TT_EXP_FINAL_STOP ||
@@ -569,10 +573,13 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
   struct BlkTimeEnd {  // end stamp when the block's last wave leaves (any return path)
     unsigned long long t0;
     int lb;
+    unsigned long long ph[2];
     __device__ ~BlkTimeEnd() {
-      if (LVL != 1 || blockIdx.x >= BLKTIME_MAX) return;
+      if (LVL != TT_EXP_BLKTIME_LVL || blockIdx.x >= BLKTIME_MAX) return;
       __syncthreads();
       if (threadIdx.x == 0) {
+        g_blkph[2 * blockIdx.x] = ph[0];
+        g_blkph[2 * blockIdx.x + 1] = ph[1];
         unsigned long long* o = g_blktime + 4 * blockIdx.x;
         o[0] = t0;
         o[1] = wall_clock64();
@@ -581,7 +588,7 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
                (unsigned)__builtin_amdgcn_s_getreg((3 << 11) | 20);            // XCC_ID
       }
     }
-  } blk_end{blk_t0, lb};
+  } blk_end{blk_t0, lb, {0ull, 0ull}};
 #endif
 
   bf16x8 qf[QB][KS];
@@ -853,6 +860,9 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
     for (int t = 0; t < RG_PD && t < n_tiles; ++t) issue(t);
   wait_tiles(n_tiles - 1 < RG_PD - 1 ? n_tiles - 1 : RG_PD - 1);
   lds_barrier();  // tile 0 landed; counters initialised
+#if TT_EXP_BLKTIME
+  blk_end.ph[0] = wall_clock64();
+#endif
   // A wave without a single real query only moves its share of the ring DMA, in lockstep with
   // the block's one barrier per tile: small batches (LVL 2, e.g. one buyer: its MFMAs on
   // padding queries had made the one-buyer full level issue-bound, 8 waves x 48 MFMAs / tile)
@@ -993,6 +1003,9 @@ __global__ __launch_bounds__(64 * RG_WAVES, RG_BLOCKS_PER_CU) void k_filter_ring
       }
     });
   }
+#if TT_EXP_BLKTIME
+  blk_end.ph[1] = wall_clock64();
+#endif
   if (n_tiles > 0 && !TT_EXP_NOSEL) {
     float mx[QB];
     tile_max(accp, mx);
@@ -1980,6 +1993,23 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_small(
   __shared__ BandLds<EP> bl;
   const int qid = blockIdx.x;
   const int tid = threadIdx.x;
+#if TT_EXP_BLKTIME
+  struct BlkTimeEnd {  // TT_EXP_BLKTIME_LVL 9: this kernel's blocks instead of a ring level's
+    unsigned long long t0;
+    __device__ ~BlkTimeEnd() {
+      if (TT_EXP_BLKTIME_LVL != 9 || blockIdx.x >= BLKTIME_MAX) return;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        unsigned long long* o = g_blktime + 4 * blockIdx.x;
+        o[0] = t0;
+        o[1] = wall_clock64();
+        o[2] = (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        o[3] = ((unsigned long long)blockIdx.x << 32) |
+               (unsigned)__builtin_amdgcn_s_getreg((3 << 11) | 20);
+      }
+    }
+  } blk_end{(unsigned long long)wall_clock64()};
+#endif
   if (flags[qid]) return;  // served by the exact fallback
   const int total = small_collect(lists, counts, n_slabs, qid, s);
   if (total < k) {  // overflow (-1) or too few candidates to certify: exact fallback
@@ -4345,6 +4375,10 @@ __global__ void k_debug_plant(uint64_t* keys, uint64_t* xk, const int* counts, i
 }  // namespace
 
 #if TT_EXP_BLKTIME
+extern "C" int tt_debug_blkph(void* host, int32_t n) {  // timing builds only
+  if (n > BLKTIME_MAX) n = BLKTIME_MAX;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_blkph), (size_t)n * 16) == hipSuccess ? n : -1;
+}
 extern "C" int tt_debug_blktimes(void* host, int32_t n) {  // timing builds only
   if (n > BLKTIME_MAX) n = BLKTIME_MAX;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_blktime), (size_t)n * 32) == hipSuccess ? n : -1;
