@@ -1,14 +1,19 @@
-# int8 single pass: tests on the new swizzle, latency A/B (main vs old swizzle vs 5 slots), x2
-set -o pipefail
-mkdir -p gpurun_out/r05j
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_i8.py > gpurun_out/r05j/tests.log 2>&1
-rt=$?; echo "tests rc=$rt"; tail -2 gpurun_out/r05j/tests.log
-[ $rt -eq 0 ] || exit $rt
+#!/bin/bash
+# GPU box: small-batch sample level ring depth (TT_RING_PD_S0 3 / 4 / 5) -- block phases, the
+# one-search latency at 16 / 32 / 256 queries, and the parity suite on the deepest variant.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+V=$PWD/two-tower-model-v2_amd/lib/variants
+for v in s0 s0p5; do
+  TWOTOWER_HIP_LIB=$V/lib_$v.so timeout -k 10 120 python tools/blktime_small.py --nq 32 > gpurun_out/r05j_blk_$v.json 2>&1 || exit 1
+done
 for rep in 1 2; do
-for lib in lib/libtwotower_hip.so lib/variants/lib_swz0.so lib/variants/lib_sl5.so; do
-  TWOTOWER_HIP_LIB=$PWD/two-tower-model-v2_amd/$lib timeout -k 10 120 python -u tools/bench_i8.py > gpurun_out/r05j/b.json 2>/dev/null || exit 1
-  python -c "
-import json,sys; d=json.load(open('gpurun_out/r05j/b.json'))
-print(sys.argv[1], ' '.join('nq%s bf16 %.4f i8 %.4f (stream %.4f) fb %d' % (q[2:], v['bf16']['ms_per_search'], v['i8']['ms_per_search'], v['i8']['stream_ms'], v['i8']['fallbacks_last']) for q, v in d.items() if q.startswith('nq')))" $lib
+  for v in base p4 p5; do
+    for nq in 16 32 256; do
+      echo "$v $nq $(TWOTOWER_HIP_LIB=$V/lib_$v.so timeout -k 10 120 python tools/bench_small_search.py --nq $nq --modeb --reps 100 2>/dev/null | tail -1)" >> gpurun_out/r05j_ab.txt || exit 1
+    done
+  done
 done
-done
+TWOTOWER_HIP_LIB=$V/lib_p5.so timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_vectordb_reference.py -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/r05j_p5_tests.log 2>&1
+tail -2 gpurun_out/r05j_p5_tests.log

@@ -1,11 +1,19 @@
-# int8 stream: which part of the compute costs (timing-only variants) + /retrieve threads A/B
-set -o pipefail
-mkdir -p gpurun_out/r05l
-for lib in lib/libtwotower_hip.so lib/variants/lib_noapp.so lib/variants/lib_nolds.so lib/variants/lib_nomfma.so lib/variants/lib_nocomp.so; do
-  TWOTOWER_HIP_LIB=$PWD/two-tower-model-v2_amd/$lib timeout -k 10 180 python -u tools/bench_i8.py > gpurun_out/r05l/b.json 2>gpurun_out/r05l/b.err || exit 1
-  python -c "
-import json,sys; d=json.load(open('gpurun_out/r05l/b.json'))
-print(sys.argv[1], ' '.join('nq%s i8 stream %.4f' % (q[2:], v['i8']['stream_ms']) for q, v in d.items() if q.startswith('nq')))" $lib
+#!/bin/bash
+# GPU box: small batches through k_query_eps (bf16 query image, TT_Q16_SMALL=1) vs the state
+# folded into the first ring level (0) -- block phases of both ring levels, and the search
+# latency at 16 / 32 / 64 / 256 queries.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+V=$PWD/two-tower-model-v2_amd/lib/variants
+for v in s0 s2; do
+  TWOTOWER_HIP_LIB=$V/lib_$v.so timeout -k 10 120 python tools/blktime_small.py --nq 32 > gpurun_out/r05l_blk_$v.json 2>&1 || exit 1
 done
-timeout -k 10 300 python -u tools/bench_api.py > gpurun_out/r05l/api.json 2>gpurun_out/r05l/api.err || exit 1
-cat gpurun_out/r05l/api.json
+for rep in 1 2; do
+  for v in off on; do
+    for nq in 16 32 64 256; do
+      echo "$v $nq $(TWOTOWER_HIP_LIB=$V/lib_$v.so timeout -k 10 120 python tools/bench_small_search.py --nq $nq --modeb --reps 100 2>/dev/null | tail -1)" >> gpurun_out/r05l_ab.txt || exit 1
+    done
+  done
+done
+echo done

@@ -2727,13 +2727,14 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
       for (int u = 0; u < 4; ++u) {
         const f32x4 v = *(const f32x4*)(qp + 64 * s + 4 * u);
         uint32_t pk = 0u;
+        // (selects, no branch: a branch per element kept these loads from being hoisted, so
+        // they went out one at a time -- ~24 dependent round trips before the ring started)
+        const float tdiv = tq > 0.0f ? tq : 1.0f;
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-          int c = 0;
-          if (tq > 0.0f) {
-            c = (int)rintf(v[b] / tq);
-            c = c > 127 ? 127 : c < -127 ? -127 : c;
-          }
+          int c = (int)rintf(v[b] / tdiv);
+          c = c > 127 ? 127 : c < -127 ? -127 : c;
+          c = tq > 0.0f ? c : 0;
           const double e = (double)v[b] - (double)tq * (double)c;
           sq += (double)v[b] * (double)v[b];
           sd += e * e;
@@ -3804,6 +3805,15 @@ static bool select_reg_disabled() {  // TT_SELECT_REG=0: LDS-staged k_select_wav
   static const bool off = env_switch("TT_SELECT_REG", 1) == 0;
   return off;
 }
+// Small batches too take the k_query_eps launch (bf16 query image + per-query state) instead of
+// folding the state into the first ring level: that fold's f32 query loads went out one k-step
+// at a time (the bf16 conversion's NaN branch splits every step, and a hoisted f32 conversion
+// does not fit the ring kernels' registers) -- ~15 us before the first tile of EVERY ring
+// launch of the search, sample and full level alike (tools/blktime_small.py).
+#ifndef TT_Q16_SMALL
+#define TT_Q16_SMALL 1
+#endif
+TT_CHECK_EXP(TT_Q16_SMALL != 1, "TT_Q16_SMALL");
 static bool q16_enabled() {  // TT_FILTER_Q16=0: ring levels load f32 queries (timing builds)
   static const bool on = env_switch("TT_FILTER_Q16", 1) != 0;
   return on;
@@ -4465,9 +4475,9 @@ int scan_topk_bf16f32(const float* db, const uint16_t* db_bf16, int64_t n, int32
                                  w.done, out_score, out_idx, w.scan_ws, w.scan_ws_bytes, st);
   }
   QueryInit qinit;
-  // large batches: k_query_eps (one launch) writes the per-query state AND the bf16 query
-  // image the ring levels load; smaller ones fold the state into the first level (no launch)
-  const bool q16 = nq > RG_SMALL_NQ && q16_enabled();
+  // k_query_eps (one launch) writes the per-query state AND the bf16 query image the ring
+  // levels load (TT_Q16_SMALL=0 timing builds: small batches fold the state into the first level)
+  const bool q16 = (nq > RG_SMALL_NQ || TT_Q16_SMALL) && q16_enabled();
   const I8Sample* i8s = i8 && sample_i8_applies(p, nq, ep, q16) ? i8 : nullptr;
   g_last_sample_i8 = i8s != nullptr;
   if ((rc = filter_init(w, q, nq, ld_q, ep, x_norm_max, x_resid_max, st, &p, q16 ? nullptr : &qinit,
