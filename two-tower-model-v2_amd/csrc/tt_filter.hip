@@ -1996,10 +1996,13 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_small(
 #if TT_EXP_BLKTIME
   struct BlkTimeEnd {  // TT_EXP_BLKTIME_LVL 9: this kernel's blocks instead of a ring level's
     unsigned long long t0;
+    unsigned long long ph[2];
     __device__ ~BlkTimeEnd() {
       if (TT_EXP_BLKTIME_LVL != 9 || blockIdx.x >= BLKTIME_MAX) return;
       __syncthreads();
       if (threadIdx.x == 0) {
+        g_blkph[2 * blockIdx.x] = ph[0];
+        g_blkph[2 * blockIdx.x + 1] = ph[1];
         unsigned long long* o = g_blktime + 4 * blockIdx.x;
         o[0] = t0;
         o[1] = wall_clock64();
@@ -2008,10 +2011,13 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_small(
                (unsigned)__builtin_amdgcn_s_getreg((3 << 11) | 20);
       }
     }
-  } blk_end{(unsigned long long)wall_clock64()};
+  } blk_end{(unsigned long long)wall_clock64(), {0ull, 0ull}};
 #endif
   if (flags[qid]) return;  // served by the exact fallback
   const int total = small_collect(lists, counts, n_slabs, qid, s);
+#if TT_EXP_BLKTIME
+  blk_end.ph[0] = wall_clock64();
+#endif
   if (total < k) {  // overflow (-1) or too few candidates to certify: exact fallback
     if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
     return;
@@ -2023,6 +2029,9 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_small(
     h[j] = e < total ? (uint32_t)(s.key[e] >> 32) : 0u;
   }
   const float A = key_float(small_radix_select(h, k, s));
+#if TT_EXP_BLKTIME
+  blk_end.ph[1] = wall_clock64();
+#endif
   if (!(A >= aref[qid])) {
     if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
     return;
