@@ -1853,6 +1853,10 @@ __device__ __forceinline__ f32x4 exact16(const float* __restrict__ db, int64_t l
     f32x4 a[TCH];
 #pragma unroll
     for (int t = 0; t < TCH; ++t) a[t] = *(const f32x4*)(xr + 16 * (t0 + t));
+    // every load of the batch issued before the chain: left to itself the scheduler kept two
+    // in flight (1024-thread blocks: a 128-register budget), i.e. ~TCH dependent round trips
+    // per 16 rows -- most of k_final_small's time (tools/blktime_small.py)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < TCH; ++t) {
       const f32x4 b = *(const f32x4*)(qs + 16 * (t0 + t) + 4 * g);
