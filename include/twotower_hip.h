@@ -152,8 +152,13 @@ int tt_scan_topk_bf16f32_i8s(const float* db, const uint16_t* db_bf16, const int
  * score at most its 16th approximate score + eps, eps from x_norm_max, x_resid_max, s_max = the
  * image's bounds).  Uncertified queries take the exact f32 fallback in a following launch.
  * Workspace: tt_filter_workspace_bytes (same n, d, nq, k).  Returns TT_ERR_UNSUPPORTED outside
- * that shape (callers then use tt_scan_topk_bf16f32).
+ * that shape (callers then use tt_scan_topk_bf16f32); tt_i8_single_pass_ok(n, d, nq, k, ld_i8)
+ * answers 1 / 0 for a shape without a launch (the limits: nq <= 8, k <= 128, rows per CU
+ * <= 65536 -- about 16.7M rows on 256 CUs -- and at most 256 CUs).
+ * tt_debug_i8_force_unsupported(1) makes both report "unsupported" (test hook; 0 clears).
  * --------------------------------------------------------------------------------- */
+int tt_i8_single_pass_ok(int64_t n, int32_t d, int32_t nq, int32_t k, int64_t ld_i8);
+int tt_debug_i8_force_unsupported(int32_t on);
 int tt_scan_topk_i8f32(const float* db, const int8_t* db_i8, const float* tile_scales,
                        int64_t n, int32_t d, int64_t ld_db, int64_t ld_i8, int64_t row_base,
                        const float* q, int32_t nq, int64_t ld_q, int32_t k, float x_norm_max,

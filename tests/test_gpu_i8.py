@@ -143,6 +143,50 @@ def test_retrieve_one_buyer_takes_the_i8_pass(K):
         assert [v for _, v in got] == s16[b].tolist()
 
 
+def test_retrieve_falls_back_when_the_i8_pass_is_unsupported(K, oracle_mod):
+    """A shape the int8 single pass refuses (TT_ERR_UNSUPPORTED: > 16.7M rows on 256 CUs, a
+    GPU with more than 256 CUs, TT_FILTER_TOPM=0 -- forced here by the test hook) is served by
+    the bf16 filter on every one-buyer path: retrieve (serving slot), search_device and
+    PreparedSearch, with the oracle's exact answers; the int8 image is built lazily (on the
+    first search after build_index) and add() marks it stale instead of rebuilding it."""
+    from twotower import VectorDatabase, kernels
+
+    rng = np.random.default_rng(41)
+    n, d, k = 30_000, 384, 100
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    vdb = VectorDatabase(d)
+    vdb.build_index(x, [f"p{j}" for j in range(n)])
+    assert vdb.index._i8_stale and vdb.index._i8 is None  # lazy: not built by build_index
+    q = rng.standard_normal((2, d)).astype(np.float32)
+    xn = oracle_mod.vector_db_normalize(x)
+    qn = oracle_mod.vector_db_normalize(q)
+    rs, ri = oracle_mod.scan_topk(xn, qn, k)
+    assert K.i8_single_pass_ok(n, d, 1, k, 384)
+    first = vdb.retrieve(q[0], k=k)  # builds the image, runs the int8 pass
+    assert vdb.index._i8 is not None and not vdb.index._i8_stale
+    try:
+        K.debug_i8_force_unsupported(True)
+        assert not K.i8_single_pass_ok(n, d, 1, k, 384)
+        for b in range(2):
+            got = vdb.retrieve(q[b], k=k)
+            assert [p for p, _ in got] == [f"p{j}" for j in ri[b].tolist()]
+            assert [v for _, v in got] == rs[b].tolist()
+        assert got == vdb.retrieve(q[1], k=k) and first == vdb.retrieve(q[0], k=k)
+        qd = vdb.normalize_queries(torch.from_numpy(q).cuda())
+        s, i = vdb.index.search_device(qd, k)
+        assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
+        ix = vdb.index
+        ps = K.PreparedSearch(ix.xb, ix.xb16, n, d, 2, k, ix.bounds, i8=ix.i8)
+        assert not ps.i8
+        s, i = ps(qd)
+        assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
+    finally:
+        K.debug_i8_force_unsupported(False)
+    assert vdb.retrieve(q[0], k=k) == first  # back on the int8 pass, same answers
+    vdb.index.add(np.zeros((1, d), np.float32))  # add(): image marked stale, not rebuilt
+    assert vdb.index._i8_stale and vdb.index._i8 is None
+
+
 def test_i8_abi_rejects_more_than_8_queries(K):
     """The ABI's batch limit (nq <= 8, the 8-query buffer layout): nq = 9 is refused with
     TT_ERR_UNSUPPORTED before any launch, and the Python wrapper raises."""

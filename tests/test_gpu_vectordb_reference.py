@@ -283,3 +283,78 @@ def test_retrieve_coalesces_concurrent_requests_bit_identical():
     nb, nr = (vdb.index.coalesce_stats[0] - st0[0], vdb.index.coalesce_stats[1] - st0[1])
     assert nr == 240 and 1 <= nb <= 240
     print(f"coalesced 240 requests into {nb} searches")
+
+
+class _Abort(BaseException):
+    """Stands for KeyboardInterrupt / SystemExit raised inside a serving thread."""
+
+
+def test_retrieve_survives_a_base_exception_in_the_coalescing_leader():
+    """A BaseException (KeyboardInterrupt, SystemExit) raised inside the thread that leads the
+    coalesced searches must not leave the lead held: that thread sees the exception, requests
+    queued behind it still get their answers (the lead is handed over), and later retrieve
+    calls return (FlatIPIndex._serve's finally)."""
+    import threading
+
+    from twotower import VectorDatabase
+
+    rng = np.random.default_rng(17)
+    n, d, k = 20000, 384, 10
+    vdb = VectorDatabase(d)
+    vdb.build_index(rng.standard_normal((n, d)).astype(np.float32), [f"p{i}" for i in range(n)])
+    q = rng.standard_normal((4, d)).astype(np.float32)
+    want = [vdb.retrieve(q[b], k=k) for b in range(4)]
+    ix = vdb.index
+    real = ix._run_batch
+    entered, release = threading.Event(), threading.Event()
+    calls = []
+
+    def flaky(xs, kk, normalize, state=None):  # the first batch blocks, then aborts
+        calls.append(xs.shape[0])
+        if len(calls) == 1:
+            entered.set()
+            release.wait(30)
+            raise _Abort()
+        return real(xs, kk, normalize, state)
+
+    ix._run_batch = flaky
+    out = {}
+
+    def lead():
+        try:
+            vdb.retrieve(q[0], k=k)
+            out["lead"] = "returned"
+        except _Abort:
+            out["lead"] = "aborted"
+
+    def follow(b):
+        try:
+            out[b] = vdb.retrieve(q[b], k=k)
+        except Exception as e:  # pragma: no cover - reported by the asserts
+            out[b] = e
+
+    try:
+        t0 = threading.Thread(target=lead)
+        t0.start()
+        assert entered.wait(30)
+        followers = [threading.Thread(target=follow, args=(b,)) for b in (1, 2, 3)]
+        for t in followers:
+            t.start()
+        while len(ix._queue) < 3 and all(t.is_alive() for t in followers):
+            threading.Event().wait(0.01)
+        release.set()
+        for t in [t0] + followers:
+            t.join(60)
+            assert not t.is_alive(), "a retrieve call hung after the leader's BaseException"
+    finally:
+        release.set()
+        ix._run_batch = real
+    assert out["lead"] == "aborted"
+    for b in (1, 2, 3):
+        assert out[b] == want[b], (b, out[b])
+    assert not ix._leading and not ix._queue
+    res = {}
+    th = threading.Thread(target=lambda: res.setdefault("r", vdb.retrieve(q[2], k=k)))
+    th.start()
+    th.join(60)
+    assert not th.is_alive() and res["r"] == want[2]

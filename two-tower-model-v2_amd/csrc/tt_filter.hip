@@ -4580,6 +4580,33 @@ extern "C" int tt_scan_topk_bf16f32_i8s(const float* db, const uint16_t* db_bf16
 
 extern "C" int tt_debug_last_sample_i8(void) { return g_last_sample_i8 ? 1 : 0; }
 
+// Test hook: while set, the int8 single pass reports TT_ERR_UNSUPPORTED for every shape (and
+// tt_i8_single_pass_ok says 0), as it does past its row limit or on a GPU with > 256 CUs.
+static bool g_i8_force_unsupported = false;
+extern "C" int tt_debug_i8_force_unsupported(int32_t on) {
+  g_i8_force_unsupported = on != 0;
+  return TT_OK;
+}
+
+// The shape limits of tt_scan_topk_i8f32 without a launch: the single-pass plan (nq <= 8,
+// device_cus() * TM_M <= TM_CAP, TT_FILTER_TOPM), the per-block scale-tile limit (rows per CU
+// <= 65536) and the 31-bit tile offsets.  1: the call would run, 0: it would return
+// TT_ERR_UNSUPPORTED (the caller then takes tt_scan_topk_bf16f32).
+static bool i8_single_pass_fits(int64_t n, int ep, int nq, int k, int64_t ld_i8) {
+  if (g_i8_force_unsupported || (ep != 384 && ep != 768) || nq < 1 || nq > TM_NQ_I8 || k < 1 ||
+      k > FL_KMAX || k > n || n < 1 || n > 0x7fffffffLL)
+    return false;
+  if (!plan_filter(n, nq, k, ep).topm) return false;
+  const int G = device_cus();
+  const int64_t rpb = ((n + G - 1) / G + 63) / 64 * 64;
+  return rpb / 64 <= I8_MAXTILES && ld_i8 * (24576 / ep) <= 0x7fffffffLL;
+}
+
+extern "C" int tt_i8_single_pass_ok(int64_t n, int32_t d, int32_t nq, int32_t k, int64_t ld_i8) {
+  const int ep = tt_padded_dim(d);
+  return ep > 0 && i8_single_pass_fits(n, ep, nq, k, ld_i8 > 0 ? ld_i8 : ep) ? 1 : 0;
+}
+
 extern "C" int tt_scan_topk_i8f32(const float* db, const int8_t* db_i8, const float* tile_scales,
                                   int64_t n, int32_t d, int64_t ld_db, int64_t ld_i8,
                                   int64_t row_base, const float* q, int32_t nq, int64_t ld_q,
@@ -4598,6 +4625,7 @@ extern "C" int tt_scan_topk_i8f32(const float* db, const int8_t* db_i8, const fl
              "int8 image: ld_i8 >= tt_padded_dim(d), multiple of 16, 16-B aligned");
   TT_REQUIRE(x_norm_max >= 0.0f && x_resid_max >= 0.0f && s_max >= 0.0f,
              "bounds must be >= 0 (tt_i8_image)");
+  if (g_i8_force_unsupported) return fail(TT_ERR_UNSUPPORTED, "int8 single pass: forced (test)");
   int epx;
   FilterPlan p;
   FilterWs w;

@@ -118,6 +118,8 @@ SIGNATURES = {
     "tt_x3_split_weights": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp]),
     "tt_debug_plant_bad_row": (ctypes.c_int, [_i32, _i32]),
     "tt_debug_last_sample_i8": (ctypes.c_int, []),
+    "tt_i8_single_pass_ok": (ctypes.c_int, [_i64, _i32, _i32, _i32, _i64]),
+    "tt_debug_i8_force_unsupported": (ctypes.c_int, [_i32]),
     "tt_attention_varlen_x3i": (ctypes.c_int, [_vp, _i64, _vp, _i32, _i32, _i32, _i32, _vp, _i64,
                                                _vp]),
     "tt_x3i_weights": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp]),

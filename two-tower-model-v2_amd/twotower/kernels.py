@@ -245,6 +245,27 @@ def scan_topk_bf16(db: torch.Tensor, db16: torch.Tensor, n: int, d: int, q: torc
 
 I8_DIMS = (384, 768)  # padded dims of the int8 single pass (tt_scan_topk_i8f32)
 I8_NQ_MAX = 8  # nq 5-8: the 8-query buffer layout (still ahead of the multi-level path)
+_i8_ok_cache = {}
+
+
+def i8_single_pass_ok(n: int, d: int, nq: int, k: int, ld_i8: int = 0) -> bool:
+    """Whether tt_scan_topk_i8f32 runs this shape (tt_i8_single_pass_ok: nq <= 8, k <= 128,
+    padded dim 384 / 768, rows per CU <= 65536, <= 256 CUs) -- else the caller takes the bf16
+    filter (tt_scan_topk_bf16f32), which it would otherwise return TT_ERR_UNSUPPORTED for."""
+    key = (n, d, nq, k, ld_i8)
+    v = _i8_ok_cache.get(key)
+    if v is None:
+        if len(_i8_ok_cache) > 4096:
+            _i8_ok_cache.clear()
+        v = _i8_ok_cache[key] = bool(lib().tt_i8_single_pass_ok(n, d, nq, k, ld_i8))
+    return v
+
+
+def debug_i8_force_unsupported(on: bool) -> None:
+    """Test hook (tt_debug_i8_force_unsupported): make the int8 single pass report every shape
+    unsupported, as on a > 256-CU GPU or past its row limit."""
+    check(lib().tt_debug_i8_force_unsupported(1 if on else 0), "tt_debug_i8_force_unsupported")
+    _i8_ok_cache.clear()
 
 
 def i8_image(x: torch.Tensor, d: int, out3: torch.Tensor = None):
@@ -322,7 +343,8 @@ class PreparedSearch:
         self._head = (_ptr(db), _ptr(db16), n, d, db.stride(0), row_base)
         self._tail = (k, ctypes.c_float(x_norm_max), ctypes.c_float(x_resid_max),
                       _ptr(self.out[0]), _ptr(self.out[1]), _ptr(self.ws), self.ws.numel())
-        self.i8 = i8 is not None and nq <= I8_NQ_MAX and self.ld_q in I8_DIMS
+        self.i8 = (i8 is not None and nq <= I8_NQ_MAX and self.ld_q in I8_DIMS
+                   and i8_single_pass_ok(n, d, nq, k, i8[0].stride(0)))
         if self.i8:
             codes, scales, b3 = i8
             X, R, S = (float(v) for v in b3)

@@ -34,7 +34,7 @@ class FlatIPIndex:
     rows L2-normalised by ``add`` exactly as the reference does before ``index.add``.
     """
 
-    def __init__(self, d: int, device=None, row_base: int = 0):
+    def __init__(self, d: int, device=None, row_base: int = 0, int8_image: bool = True):
         self.d = int(d)
         self.row_base = int(row_base)  # global id of local row 0 (catalog row shard)
         self.ep = _lib.padded_dim(self.d)
@@ -46,7 +46,13 @@ class FlatIPIndex:
         self._bounds_dev = torch.zeros(2, dtype=torch.float32, device=self.device)
         self.bounds = (0.0, 0.0)
         self.ntotal = 0
-        self.i8 = None  # int8 image (codes, tile scales, bounds) for nq <= 8 searches
+        # int8 image (codes, tile scales, bounds) for nq <= 8 searches (and a large batch's
+        # sample level) at padded dim 384 / 768: built lazily, on the first search after an
+        # add() (one O(n) pass per burst of adds, not per add); int8_image=False: never
+        self.int8_image = bool(int8_image)
+        self._i8 = None
+        self._i8_stale = False
+        self.version = 0  # bumped by every catalog / int8-image change (serving-slot caches)
         self._ws = _lib.StreamWorkspaces(4)  # search_device's workspace, one per HIP stream
         # host searches (the /retrieve path, FlatIPIndex.search_host): serving slots, each with
         # its own HIP stream, device query / output buffers, pinned host staging and filter
@@ -75,11 +81,36 @@ class FlatIPIndex:
         if self.ntotal:
             rows = torch.cat([self.xb[: self.ntotal], rows])
             rows16 = torch.cat([self.xb16[: self.ntotal], rows16])
-        i8 = self._i8_image(rows)
         with self._lock:  # searches read (xb, xb16, ntotal, bounds, i8) as one snapshot
             self.xb, self.xb16 = rows, rows16
             self.ntotal = rows.shape[0]
-            self.i8 = i8
+            self._i8 = None
+            self._i8_stale = self.int8_image and self.ep in kernels.I8_DIMS and self.ntotal > 0
+            self.version += 1
+
+    @property
+    def i8(self):
+        """The int8 image (codes, tile scales, (X, R, S)) of the current rows, or None; built
+        here on first use after the rows changed."""
+        if self._i8_stale:
+            with self._lock:
+                if self._i8_stale:
+                    self._i8 = self._i8_image(self.xb[: self.ntotal])
+                    self._i8_stale = False
+                    self.version += 1
+        return self._i8
+
+    @i8.setter
+    def i8(self, value) -> None:
+        with self._lock:
+            self._i8, self._i8_stale = value, False
+            self.version += 1
+
+    def _snapshot(self):
+        """One consistent catalog state for a search: (xb, xb16, ntotal, bounds, i8, version)."""
+        with self._lock:
+            i8 = self.i8
+            return (self.xb, self.xb16, self.ntotal, self.bounds, i8, self.version)
 
     def _i8_image(self, rows: torch.Tensor):
         """(codes, tile scales, bounds) of the int8 single pass for one-buyer searches
@@ -92,8 +123,7 @@ class FlatIPIndex:
     def build_i8(self) -> None:
         """(Re)build the int8 image of the current rows (for an index whose xb was set
         directly rather than through add)."""
-        with self._lock:
-            self.i8 = self._i8_image(self.xb[: self.ntotal])
+        self.i8 = self._i8_image(self.xb[: self.ntotal])
 
     # faiss-style add of ALREADY-normalised float32 rows (host or device)
     def add(self, x) -> None:
@@ -139,15 +169,17 @@ class FlatIPIndex:
             need = kernels.scan_workspace_bytes(self.ntotal, self.d, q.shape[0], k)
         with self._lock:  # the workspace cache is shared; the outputs are fresh per call
             ws = self._ws.get(need, self.device)
-            if (use_bf16 and method == "auto" and self.i8 is not None
-                    and q.shape[0] <= kernels.I8_NQ_MAX):  # one-buyer calls: the int8 pass
-                codes, scales, b3 = self.i8
+            i8 = self.i8 if use_bf16 and method == "auto" else None
+            if (i8 is not None and q.shape[0] <= kernels.I8_NQ_MAX
+                    and kernels.i8_single_pass_ok(self.ntotal, self.d, q.shape[0], k,
+                                                  i8[0].stride(0))):
+                codes, scales, b3 = i8  # one-buyer calls: the int8 single pass
                 return kernels.scan_topk_i8(self.xb, codes, scales, self.ntotal, self.d, q, k, b3,
                                             row_base=self.row_base, workspace=ws)
             if use_bf16:  # (a large batch runs its sample level on the int8 image, if any)
                 return kernels.scan_topk_bf16(self.xb, self.xb16, self.ntotal, self.d, q, k,
                                               self.bounds, row_base=self.row_base, workspace=ws,
-                                              i8=self.i8 if method == "auto" else None)
+                                              i8=i8)
             if use_select:
                 return kernels.scan_topk_select(self.xb, self.ntotal, self.d, q, k,
                                                 row_base=self.row_base, workspace=ws)
@@ -184,8 +216,7 @@ class FlatIPIndex:
         if x.ndim != 2 or x.shape[1] != self.d:
             raise ValueError(f"search: expected [nq, {self.d}] float32 queries")
         nq = x.shape[0]
-        with self._lock:  # one consistent catalog state for this call
-            state = (self.xb, self.xb16, self.ntotal, self.bounds, self.i8)
+        state = self._snapshot()  # one consistent catalog state for this call
         if nq == 0 or not (1 <= k <= state[2]):
             q = torch.zeros((nq, self.ep), dtype=torch.float32, device=self.device)
             q[:, : self.d] = torch.from_numpy(x).to(self.device)
@@ -200,8 +231,7 @@ class FlatIPIndex:
 
     def _run_batch(self, x: np.ndarray, k: int, normalize: bool, state=None):
         if state is None:
-            with self._lock:
-                state = (self.xb, self.xb16, self.ntotal, self.bounds, self.i8)
+            state = self._snapshot()
         slot = self._checkout(x.shape[0])
         try:
             return slot.run(x, k, normalize, state)
@@ -244,44 +274,64 @@ class FlatIPIndex:
 
     def _serve(self, me: "_Request") -> None:
         extra = 0
-        while True:
-            with self._qlock:
-                head = self._queue[0]
-                cls = (head.normalize, self._path(head.k))
-                batch, rest = [], []
-                for r in self._queue:
-                    if len(batch) < self.COALESCE_MAX and (r.normalize, self._path(r.k)) == cls:
-                        batch.append(r)
-                    else:
-                        rest.append(r)
-                self._queue[:] = rest
-            kk = max(r.k for r in batch)
-            self.coalesce_stats[0] += 1
-            self.coalesce_stats[1] += len(batch)
-            try:
-                with self._lock:
-                    state = (self.xb, self.xb16, self.ntotal, self.bounds, self.i8)
-                kk = min(kk, state[2])
-                xs = np.concatenate([r.x for r in batch]) if len(batch) > 1 else batch[0].x
-                s, i = self._run_batch(xs, kk, head.normalize, state)
-                for j, r in enumerate(batch):
-                    r.result = (s[j:j + 1, :r.k], i[j:j + 1, :r.k])
-            except Exception as e:  # every request of the failed batch sees the error
-                for r in batch:
-                    r.error = e
-            for r in batch:
-                r.finished = True
-                if r is not me:
-                    r.event.set()
-            with self._qlock:
-                if me.finished:
-                    if not self._queue:
-                        self._leading = False
-                        return
-                    if extra >= self.LEAD_EXTRA:  # hand the lead to the oldest waiting thread
+        released = False  # the lead was cleared or handed over
+        batch = []
+        try:
+            while True:
+                with self._qlock:
+                    head = self._queue[0]
+                    cls = (head.normalize, self._path(head.k))
+                    batch, rest = [], []
+                    for r in self._queue:
+                        if len(batch) < self.COALESCE_MAX and (r.normalize, self._path(r.k)) == cls:
+                            batch.append(r)
+                        else:
+                            rest.append(r)
+                    self._queue[:] = rest
+                kk = max(r.k for r in batch)
+                self.coalesce_stats[0] += 1
+                self.coalesce_stats[1] += len(batch)
+                try:
+                    state = self._snapshot()
+                    kk = min(kk, state[2])
+                    xs = np.concatenate([r.x for r in batch]) if len(batch) > 1 else batch[0].x
+                    s, i = self._run_batch(xs, kk, head.normalize, state)
+                    for j, r in enumerate(batch):
+                        r.result = (s[j:j + 1, :r.k], i[j:j + 1, :r.k])
+                except Exception as e:  # every request of the failed batch sees the error
+                    for r in batch:
+                        r.error = e
+                except BaseException:  # e.g. KeyboardInterrupt / SystemExit in this thread:
+                    for r in batch:  # the batch's other callers fail, this one re-raises
+                        if r is not me:
+                            r.error = RuntimeError("search aborted: the thread running this "
+                                                   "coalesced batch was interrupted")
+                    raise
+                finally:
+                    for r in batch:
+                        r.finished = True
+                        if r is not me:
+                            r.event.set()
+                    batch = []
+                with self._qlock:
+                    if me.finished:
+                        if not self._queue:
+                            self._leading = False
+                            released = True
+                            return
+                        if extra >= self.LEAD_EXTRA:  # hand the lead to the oldest waiting thread
+                            self._queue[0].event.set()
+                            released = True
+                            return
+                        extra += 1
+        finally:
+            if not released:  # left by an exception: never leave the lead held (later
+                with self._qlock:  # single-query callers would wait for it forever)
+                    me.finished = True
+                    if self._queue:
                         self._queue[0].event.set()
-                        return
-                    extra += 1
+                    else:
+                        self._leading = False
 
     def search(self, x: np.ndarray, k: int):
         """faiss signature: float32 [nq, d] host queries -> (D [nq,k] f32, I [nq,k] i64) host."""
@@ -349,8 +399,7 @@ class _ServingSlot:
         self.fn = _lib.lib().tt_scan_topk_bf16f32
         self.norm_fn = _lib.lib().tt_l2norm_rows_f32
         self.qh_np = self.qh.numpy()
-        self.args, self.args_key = None, None
-        self.bound = collections.OrderedDict()  # akey -> bound C arguments (a few nq / k)
+        self.args = None  # (self.bound / self.args_key: _outs, akey -> bound C arguments)
         index.allocations += 1
 
     def _outs(self, kc: int, pin: bool) -> None:
@@ -358,6 +407,8 @@ class _ServingSlot:
         # call's [nq, k] scores and ids out back to back and copies them in ONE transfer
         dev = self.ix.device
         self.kc = kc
+        self.bound = collections.OrderedDict()  # bound C arguments name the old buffers
+        self.args_key = None
         m = self.bucket * kc
         o = _align256(4 * m)
         self.dout = torch.empty(o + 8 * m, dtype=torch.uint8, device=dev)
@@ -378,6 +429,8 @@ class _ServingSlot:
         if self.ws.numel() < need:
             self.ws = torch.empty(need, dtype=torch.uint8, device=self.ix.device)
             self.ix.allocations += 1
+            self.bound.clear()  # bound C arguments name the old workspace
+            self.args_key = None
         return self.ws
 
     def _fast(self, x: np.ndarray, k: int, normalize: bool, state, skey):
@@ -388,12 +441,14 @@ class _ServingSlot:
         so other serving threads run their host work meanwhile.  ~25% less host time per call
         than the torch-op form."""
         ix = self.ix
-        xb, xb16, n, bounds, i8 = state
+        xb, xb16, n, bounds, i8, _ = state
         nq, d = x.shape
         ws = self._workspace(n, nq, k, "bf16")
-        use8 = i8 is not None and nq <= kernels.I8_NQ_MAX
-        akey = (skey, nq, k, ws.data_ptr(), self.dout.data_ptr(), bounds, normalize, use8,
-                i8[0].data_ptr() if i8 is not None else 0)  # (build_i8 may replace the image)
+        use8 = (i8 is not None and nq <= kernels.I8_NQ_MAX
+                and kernels.i8_single_pass_ok(n, d, nq, k, i8[0].stride(0)))
+        # skey = the catalog state's version (rows, bounds and int8 image); the workspace and
+        # output buffers are fixed while an entry lives (their reallocation clears self.bound)
+        akey = (skey, nq, k, normalize, use8)
         o8 = _align256(nq * k * 4)  # this call's ids follow its scores
         if akey != self.args_key and akey in self.bound:  # coalesced batches vary nq
             self.fn, self.args, self.h2d, self.norm, self.d2h = self.bound[akey]
@@ -455,7 +510,7 @@ class _ServingSlot:
 
     def run(self, x: np.ndarray, k: int, normalize: bool, state):
         ix = self.ix
-        xb, xb16, n, _, _ = state
+        xb, xb16, n, _, _, version = state
         nq, d = x.shape
         if k > self.kc:
             self._outs(k, torch.cuda.is_available())
@@ -463,7 +518,7 @@ class _ServingSlot:
         q = self.q[:nq]
         # ordered after the caller's stream once per catalog state (an add() whose kernels may
         # still run there); later calls on the same state need no cross-stream wait
-        skey = (xb.data_ptr(), xb16.data_ptr(), n)
+        skey = version
         if skey != self.synced:
             self.stream.wait_stream(torch.cuda.current_stream())
             self.synced = skey
