@@ -526,8 +526,11 @@ def train_step_leg(a, dev, steps=20, B=512, N=4, S=20, E=768):
     projection head on the positive / 4 negative text embeddings, buyer-tower attention
     aggregation over S = 20 history rows, InfoNCE (in-batch + explicit negatives, tau 0.07),
     backward, Adam -- twotower.train.TwoTowerTrainStep, every GEMM on HIP MFMA, in bf16 (GEMM
-    operands) and f32.  Reports ms per step, the MFMA fraction of the matching dense peak, and
-    the bf16 step's loss / gradient deviation from the f32 step on the same weights and batch.
+    operands) and f32.  Reports ms per step (ms_per_step: forward + backward replayed as one HIP
+    graph, then the one-launch Adam; eager_ms_per_step: the same launches issued one by one), the
+    MFMA fraction of the matching dense peak, and the bf16 step's loss / gradient deviation from
+    the f32 step on the same weights and batch.  The frozen text encoder is NOT in this leg: the
+    step takes text embeddings (see train_step_e2e for the step with the encoder inside).
     Synthetic batch (random-normal text and history embeddings, event-mix weights), random-init
     weights; projection Dropout active (train mode) in the timed steps, off for the deviation."""
     import copy
@@ -570,21 +573,26 @@ def train_step_leg(a, dev, steps=20, B=512, N=4, S=20, E=768):
         loss, gr = st.forward_backward(*batch)
         grads[prec] = (float(loss), {k: v.detach().clone() for k, v in gr.items()})
         it.train()  # as under the reference Trainer (model.train(), trainer.py:167)
-        for _ in range(3):
-            st.step(*batch)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        torch.cuda.synchronize()
-        ev[0].record(stream)
-        for _ in range(steps):
-            st.step(*batch)
-        ev[1].record(stream)
-        torch.cuda.synchronize()
-        ms = ev[0].elapsed_time(ev[1]) / steps
+        ms = {}
+        for mode in ("eager", "graph"):
+            if mode == "graph":  # the same step captured once in a HIP graph, then replayed
+                st = TwoTowerTrainStep(it, bt, lr=1e-4, prec=prec, graph=True)
+            for _ in range(3):
+                st.step(*batch)
+            torch.cuda.synchronize()
+            ev[0].record(stream)
+            for _ in range(steps):
+                st.step(*batch)
+            ev[1].record(stream)
+            torch.cuda.synchronize()
+            ms[mode] = ev[0].elapsed_time(ev[1]) / steps
         peak = BF16_MFMA_PEAK_TFLOPS if prec == "bf16" else F32_MFMA_PEAK_TFLOPS
-        out[prec] = {"ms_per_step": ms, "samples_per_s": B / (ms * 1e-3),
-                     "tflops": flops / (ms * 1e-3) / 1e12,
-                     "mfma_frac": flops / (ms * 1e-3) / 1e12 / peak, "mfma_peak_tflops": peak,
-                     "loss_after": float(st.last_loss)}
+        out[prec] = {"ms_per_step": ms["graph"], "eager_ms_per_step": ms["eager"],
+                     "samples_per_s": B / (ms["graph"] * 1e-3),
+                     "tflops": flops / (ms["graph"] * 1e-3) / 1e12,
+                     "mfma_frac": flops / (ms["graph"] * 1e-3) / 1e12 / peak,
+                     "mfma_peak_tflops": peak, "loss_after": float(st.last_loss)}
         del st, it, bt
     l16, g16 = grads["bf16"]
     l32, g32 = grads["f32"]
@@ -596,6 +604,130 @@ def train_step_leg(a, dev, steps=20, B=512, N=4, S=20, E=768):
         "is": ("one forward+backward on identical weights and batch, dropout off; relative "
                "Frobenius error per gradient tensor (tests/test_gpu_trainer.py bounds it by 2x "
                "torch autocast-bf16's own error on the same step)")}
+    return out
+
+
+def train_step_e2e(a, dev, steps=3, B=512, N=4, S=20):
+    """configs[4]'s training step as the reference's Trainer runs it, encoder included
+    (trainer.py:93-131 _encode_buyer_sequences_batched + :161-231 train_epoch with
+    forward_simplified, two_tower.py:155-218): per step of B = 512 buyers
+      1. the frozen MiniLM encoder over the B*S = 10,240 history texts (ONE pass, :128-131),
+      2. the frozen MiniLM encoder over the B positive + 4B negative texts (two_tower.py:182,198;
+         2,560 texts, written straight into the step's static text buffer),
+      3. head + attention + InfoNCE forward/backward (HIP graph replay) + Adam (one launch).
+    E = 384 is the reference's composition exactly (history rows = encode_text outputs, 384-d,
+    into a BuyerTower(384)).  At configs[4]'s E = 768 the reference's Trainer cannot run as
+    written (384-d encode_text rows into a Linear(768 -> 128)), so the history rows pass the
+    frozen item-tower head first (no grad, the inference composition of encoder.py:288-292) to
+    become 768-d.  Histories use S = 20 positions (the reference pads to 100 with weight 0:
+    exactly zero contribution after the L2 normalisation).  Pre-tokenized
+    synthetic ids (the tokenizer is host-side, out of scope), random-init weights, the encoder
+    at x3 (the parity class) and bf16 (throughput mode)."""
+    import copy
+
+    from twotower.buyer_tower import BuyerTower
+    from twotower.item_tower import MINILM_L12, BertEncoder, ItemTower, pack_sequences, \
+        random_bert_state_dict
+    from twotower.train import TwoTowerTrainStep
+
+    cfg = MINILM_L12
+    sd = random_bert_state_dict(cfg, 0)
+    rng = np.random.default_rng(400)
+    R = B + B * N
+    nsteps = steps + 1  # one warm-up batch
+    # per step: history texts and positive/negative texts, packed on the device up front
+    batches = []
+    for _ in range(nsteps):
+        hs = synth_text_ids_fast(rng, B * S, cfg["vocab"])
+        ps = synth_text_ids_fast(rng, R, cfg["vocab"])
+        batches.append((pack_sequences(hs, dev), pack_sequences(ps, dev),
+                        [len(x) for x in hs] + [len(x) for x in ps]))
+    g = torch.Generator(device=dev).manual_seed(23)
+    w = event_mix(g, (B, S), dev)
+    hb = rng.integers(0, 501, B * S).tolist()
+    hc = rng.integers(0, 51, B * S).tolist()
+    pb = torch.from_numpy(rng.integers(0, 501, R).astype(np.int32)).to(dev)
+    pc = torch.from_numpy(rng.integers(0, 51, R).astype(np.int32)).to(dev)
+
+    class _Dim:
+        def get_sentence_embedding_dimension(self):
+            return cfg["hidden"]
+
+    out = {"workload": f"configs[4] training step with the frozen text encoder inside: B={B}, "
+                       f"{N} negatives, S={S}; {B * S} history + {R} positive/negative texts "
+                       "per step through the MiniLM-L12 architecture (seeded random weights, "
+                       "synthetic Zipf ids, L ~ U[16,128]), then head + attention + InfoNCE "
+                       "fwd/bwd + Adam",
+           "texts_per_step": B * S + R}
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4 * nsteps)]
+    for E in (768, 384):
+        torch.manual_seed(0)
+        it0 = ItemTower(embedding_dim=E, text_encoder=_Dim())
+        it0.initialize_categorical_embeddings([f"b{i}" for i in range(500)],
+                                              [f"c{i}" for i in range(50)])
+        bt0 = BuyerTower(E, "attention")
+        res_e = {}
+        for prec in ("x3", "bf16"):
+            enc = BertEncoder(sd, cfg, device=dev, prec=prec)
+            it, bt = copy.deepcopy(it0).to(dev), copy.deepcopy(bt0).to(dev)
+            it.head_prec = "x3"
+            st = TwoTowerTrainStep(it, bt, lr=1e-4, prec="bf16", graph=True)
+            it.train()
+            items, wbuf, text, bids, cids = st.input_buffers(B, S, N)
+            wbuf.copy_(w)
+            bids.copy_(pb)
+            cids.copy_(pc)
+            args = (items, wbuf, text[:B], text[B:].view(B, N, -1), bids[:B], cids[:B],
+                    bids[B:].view(B, N), cids[B:].view(B, N))
+            pooled = torch.empty((B * S, cfg["hidden"]), device=dev)
+
+            def step(j, timed):
+                (hi, hcu, hmx), (pi, pcu, pmx), _ = batches[j]
+                if timed:
+                    ev[4 * j].record()
+                with torch.no_grad():
+                    if E == cfg["hidden"]:  # the reference's rows: encode_text outputs
+                        enc.encode_packed(hi, hcu, hmx, out=items.view(B * S, E))
+                    else:  # 768-d rows: the frozen head after the encoder (see docstring)
+                        enc.encode_packed(hi, hcu, hmx, out=pooled)
+                        it.eval()
+                        items.view(B * S, E).copy_(it.head(pooled, hb, hc, use_cat=True))
+                        it.train()
+                    enc.encode_packed(pi, pcu, pmx, out=text)
+                if timed:
+                    ev[4 * j + 1].record()
+                loss = st.step(*args)
+                if timed:
+                    ev[4 * j + 2].record()
+                return loss
+
+            step(0, False)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for j in range(1, nsteps):
+                loss = step(j, True)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / steps
+            enc_ms = sum(ev[4 * j].elapsed_time(ev[4 * j + 1]) for j in range(1, nsteps)) / steps
+            post_ms = sum(ev[4 * j + 1].elapsed_time(ev[4 * j + 2])
+                          for j in range(1, nsteps)) / steps
+            lens = [L for j in range(1, nsteps) for L in batches[j][2]]
+            fl_enc = encoder_flops(lens) / steps
+            fl_step = 3.0 * (2 * B * (1 + N) * (512 * 256 + 256 * E) + 2 * B * S * E * 128
+                             + 2 * B * B * E)
+            mf = 3.0 if prec == "x3" else 1.0
+            res_e[prec] = {"ms_per_step": dt * 1e3, "samples_per_s": B / dt,
+                           "texts_per_s": (B * S + R) / dt, "encode_ms": enc_ms,
+                           "post_encode_ms": post_ms, "encoder_share": enc_ms / (dt * 1e3),
+                           "tflops": (fl_enc + fl_step) / dt / 1e12,
+                           "mfma_frac": (mf * fl_enc + fl_step) / dt / 1e12 / BF16_MFMA_PEAK_TFLOPS,
+                           "loss_last": float(loss)}
+            del enc, st, it, bt
+            torch.cuda.empty_cache()
+        out[f"E{E}"] = res_e
+    out["is"] = ("E768 = configs[4]; E384 = the reference Trainer's exact composition. "
+                 "mfma_frac counts x3's three bf16 products per encoder flop; the step's GEMMs "
+                 "are bf16 (TwoTowerTrainStep prec='bf16', HIP graph)")
     return out
 
 
@@ -647,6 +779,11 @@ def summary(result):
         s["train_ms"] = {p: _sig(t[p]["ms_per_step"]) for p in ("bf16", "f32")}
         s["train_mfma_frac"] = {p: _sig(t[p]["mfma_frac"]) for p in ("bf16", "f32")}
         s["train_bf16_grad_rel"] = _sig(t["bf16_vs_f32"]["grad_max_rel_l2"])
+    if "train_step_e2e" in result:
+        t = result["train_step_e2e"]
+        s["train_e2e_ms"] = {f"{e}_{p}": _sig(t[e][p]["ms_per_step"])
+                             for e in ("E768", "E384") for p in ("x3", "bf16")}
+        s["train_e2e_encoder_share"] = _sig(t["E768"]["x3"]["encoder_share"])
     cb = result.get("cpu_baseline")
     if cb:
         s["cpu_buyers_per_s"] = _sig(cb["value"])
@@ -1189,6 +1326,8 @@ def main():
         result["catalog_10m_768"] = catalog_10m_768(a, dev)
         torch.cuda.empty_cache()
         result["train_step"] = train_step_leg(a, dev)
+        torch.cuda.empty_cache()
+        result["train_step_e2e"] = train_step_e2e(a, dev)
         torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         sys.path.insert(0, ROOT)

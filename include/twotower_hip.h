@@ -472,6 +472,53 @@ int tt_attn_pool_bwd_f32(const float* dz, int64_t lddz, const float* z, int64_t 
 /* nn.Embedding(padding_idx=0) backward: table_grad[ids[r]] += g[r] (ids <= 0 skipped). */
 int tt_embedding_backward_f32(const float* g, int64_t ldg, const int32_t* ids, int64_t n,
                               int32_t C, float* table_grad, void* stream);
+/* tt_attn_pool_fwd_f32 with the bias b2 read from device memory (a step captured in a HIP
+ * graph replays without a host read of the parameter). */
+int tt_attn_pool_fwd_f32_dev(const float* H, int32_t Hd, const float* W2, const float* b2,
+                             const float* w, const float* x, int64_t B, int32_t S, int32_t E,
+                             float* alpha, float* onorm, float* z, int64_t ldz, void* stream);
+/* tt_attn_pool_bwd_f32 with the ReLU backward of H fused into dH (dH = 0 where H <= 0). */
+int tt_attn_pool_bwd_relu_f32(const float* dz, int64_t lddz, const float* z, int64_t ldz,
+                              const float* onorm, const float* alpha, const float* w,
+                              const float* x, int64_t B, int32_t S, int32_t E, const float* H,
+                              const float* W2, int32_t Hd, float* dW2, float* db2, float* dH,
+                              float* da_ws, void* stream);
+/* Weight gradients without transposed copies: C [N, K] = A^T B for row-major A [M, N] (dY),
+ * B [M, K] (X), f32 in; prec TT_PREC_BF16 rounds the operands to bf16 (bf16 MFMA, f32
+ * accumulate), TT_PREC_F32 keeps f32 (f32 MFMA).  db (may be NULL) = column sums of A (the bias
+ * gradient, f32).  The rows are split over blocks (partial tiles in the workspace) and a
+ * second launch sums the splits in a fixed order (deterministic).  Workspace:
+ * tt_gemm_tn_workspace_bytes (0 when the rows are not split); one workspace may serve calls
+ * of different shapes in stream order. */
+int tt_gemm_tn_workspace_bytes(int64_t M, int32_t N, int32_t K, int64_t* bytes);
+int tt_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t N,
+               int32_t K, int32_t prec, float* C, int64_t ldc, float* db, void* workspace,
+               int64_t workspace_bytes, void* stream);
+/* nn.Dropout forward with a keep mask (tt_dropout_apply_f32) plus a bf16 copy (may be NULL). */
+int tt_dropout_apply_ex(float* x, const uint8_t* keep, float scale, int64_t n, uint16_t* x_bf16,
+                        void* stream);
+/* ReLU (+ Dropout) backward on the post-activation h: dh = h > 0 ? dh * scale : 0 (scale =
+ * 1/(1-p) with dropout, 1 without), plus a bf16 copy (may be NULL). */
+int tt_relu_dropout_backward_f32(float* dh, const float* h, float scale, int64_t n,
+                                 uint16_t* dh_bf16, void* stream);
+/* tt_l2norm_backward_f32 plus a bf16 copy of dy (may be NULL). */
+int tt_l2norm_backward_ex(const float* y, int64_t ldy, const float* z, int64_t ldz,
+                          const float* dz, int64_t lddz, int64_t n, int32_t d, float* dy,
+                          int64_t lddy, uint16_t* dy_bf16, int64_t lddy16, void* stream);
+/* Batched operand preparation, ONE launch: job j writes src [rows, cols] f32 to dst as f32 or
+ * bf16 (to_bf16), transposed (dst [cols, ld_dst], columns rows..ld_dst-1 zero) or not.  The
+ * training step's weight-derived GEMM operands (bf16 weights, transposed weights) and bf16
+ * copies of its inputs, once per step. */
+#define TT_CONVERT_MAX_JOBS 8
+typedef struct tt_convert_job {
+  const float* src;
+  int64_t ld_src;
+  int32_t rows, cols;
+  void* dst;
+  int64_t ld_dst;
+  int32_t transpose, to_bf16;
+} tt_convert_job;
+int tt_convert_batch(const tt_convert_job* jobs, int32_t njobs, void* stream);
 /* torch.optim.Adam step (weight_decay 0): step is the 1-based step count after increment. */
 int tt_adam_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                 float beta2, float eps, int32_t step, void* stream);

@@ -27,15 +27,17 @@ def _ln(x, g, b, eps):
     return F.layer_norm(x, (x.shape[-1],), g, b, eps)
 
 
-def bert_mean_pool(sd, cfg, ids, cu_seqlens, dtype=torch.float32):
-    """sd: HF BertModel state dict; ids [T] int; cu_seqlens [n+1] -> pooled [n, H]."""
+def bert_mean_pool(sd, cfg, ids, cu_seqlens, dtype=torch.float32, device="cpu"):
+    """sd: HF BertModel state dict; ids [T] int; cu_seqlens [n+1] -> pooled [n, H] (computed on
+    `device`: a float64 run of a 12-layer configs[1] batch is minutes on the CPU, a second on a
+    GPU's torch -- still this restatement, not the product path)."""
     H, nh = cfg["hidden"], cfg["heads"]
     dh = H // nh
-    ids = torch.as_tensor(ids, dtype=torch.long)
+    ids = torch.as_tensor(ids, dtype=torch.long).to(device)
     cu = [int(v) for v in cu_seqlens]
     n = len(cu) - 1
-    W = {k: v.to(dtype) for k, v in sd.items()}
-    pos = torch.cat([torch.arange(cu[i + 1] - cu[i]) for i in range(n)])
+    W = {k: v.to(device=device, dtype=dtype) for k, v in sd.items()}
+    pos = torch.cat([torch.arange(cu[i + 1] - cu[i]) for i in range(n)]).to(device)
     x = (W["embeddings.word_embeddings.weight"][ids]
          + W["embeddings.token_type_embeddings.weight"][0]) \
         + W["embeddings.position_embeddings.weight"][pos]

@@ -275,3 +275,147 @@ def test_modules_train_under_torch_autograd():
         scale = v.abs().max().item() + 1e-12
         assert (g.cpu().reshape(v.shape) - v).abs().max().item() <= 1e-4 * scale + 1e-6, k
     torch.optim.Adam(model.parameters(), lr=1e-3).step()  # torch's own optimizer on top
+
+
+@pytest.mark.parametrize("M,N,K", [(2560, 768, 256), (2560, 256, 512), (10240, 128, 768),
+                                   (512, 512, 768), (37, 70, 33), (64, 64, 64), (1000, 5, 300),
+                                   (0, 16, 16)])
+@pytest.mark.parametrize("prec", ["f32", "bf16"])
+@pytest.mark.parametrize("with_db", [True, False])
+def test_gemm_tn_vs_float64(M, N, K, prec, with_db):
+    """tt_gemm_tn (the weight-gradient GEMM C = A^T B without transposed copies, bias column
+    sums fused): vs float64 of the same (bf16-rounded for prec bf16) operands.  f32 MFMA: only
+    the summation order differs (relative 1e-5 of the |A|^T |B| scale); bf16: operands rounded
+    RNE, f32 accumulation.  Deterministic: two calls give the same bits."""
+    import ctypes
+
+    from twotower import _lib
+
+    L = _lib.lib()
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N * 3 + K)
+    A = torch.randn((M, N), generator=g, device="cuda")
+    Bm = torch.randn((M, K), generator=g, device="cuda")
+    C = torch.full((N, K), float("nan"), device="cuda")
+    db = torch.full((N,), float("nan"), device="cuda") if with_db else None
+    need = ctypes.c_int64(0)
+    _lib.check(L.tt_gemm_tn_workspace_bytes(M, N, K, ctypes.byref(need)), "ws")
+    ws = torch.zeros(max(need.value, 256), dtype=torch.uint8, device="cuda")
+    pr = _lib.TT_PREC_BF16 if prec == "bf16" else _lib.TT_PREC_F32
+
+    def run():
+        _lib.check(L.tt_gemm_tn(A.data_ptr(), N, Bm.data_ptr(), K, M, N, K, pr, C.data_ptr(), K,
+                                db.data_ptr() if with_db else None, ws.data_ptr(), ws.numel(),
+                                _lib.stream_ptr()), "tt_gemm_tn")
+        return C.clone(), (db.clone() if with_db else None)
+
+    c1, d1 = run()
+    c2, d2 = run()  # deterministic: the same bits again
+    assert torch.equal(c1, c2) and (not with_db or torch.equal(d1, d2))
+    a64, b64 = A.double(), Bm.double()
+    if prec == "bf16":
+        a64, b64 = A.bfloat16().double(), Bm.bfloat16().double()
+    ref = (a64.T @ b64) if M else torch.zeros((N, K), dtype=torch.float64, device="cuda")
+    scale = (a64.abs().T @ b64.abs()) if M else torch.ones((N, K), dtype=torch.float64,
+                                                           device="cuda")
+    err = ((c1.double() - ref).abs() / (scale + 1e-30)).max().item()
+    assert err <= 1e-5, err
+    if with_db:
+        rdb = A.double().sum(0) if M else torch.zeros(N, dtype=torch.float64, device="cuda")
+        dscale = A.double().abs().sum(0) + 1e-30 if M else torch.ones(N, dtype=torch.float64,
+                                                                       device="cuda")
+        assert ((d1.double() - rdb).abs() / dscale).max().item() <= 1e-5
+
+
+@pytest.mark.parametrize("prec", ["f32", "bf16"])
+@pytest.mark.parametrize("use_cat", [True, False])
+def test_graph_step_matches_eager_step(prec, use_cat):
+    """TwoTowerTrainStep(graph=True) (forward + backward captured once per step shape in a HIP
+    graph, then replayed) trains like the eager launch sequence: same losses and parameters over
+    6 Adam steps within float-reordering noise (the embedding / attention-bias gradient sums use
+    atomics), and inputs written in place through input_buffers give the same step."""
+    from twotower.train import TwoTowerTrainStep
+
+    B, N, S, E = 128, 4, 20, 768
+    it0, bt0 = _setup(E, use_cat, seed=9)
+    rng = np.random.default_rng(9)
+    cu = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    items = cu(rng.standard_normal((B, S, E)).astype(np.float32))
+    w = cu(rng.integers(1, 11, (B, S)).astype(np.float32))
+    pos = cu(rng.standard_normal((B, 384)).astype(np.float32))
+    neg = cu(rng.standard_normal((B, N, 384)).astype(np.float32))
+    nv = (len(gi.BRANDS) + 1, len(gi.CATEGORIES) + 1)  # vocab sizes incl. <UNK> = 0
+    ids = [cu(rng.integers(0, nv[j % 2], s).astype(np.int32))
+           for j, s in enumerate(((B,), (B,), (B, N), (B, N)))]  # brand, cat, brand, cat
+    batch = (items, w, pos, neg, *ids) if use_cat else (items, w, pos, neg)
+    res = {}
+    for mode in ("eager", "graph"):
+        it, bt = copy.deepcopy(it0).cuda().eval(), copy.deepcopy(bt0).cuda()
+        st = TwoTowerTrainStep(it, bt, lr=1e-3, prec=prec, graph=mode == "graph")
+        l0, g0 = st.forward_backward(*batch)  # graph: warm-up, capture, replay
+        g0 = {k: v.clone() for k, v in g0.items()}
+        losses = [float(l0)] + [float(st.step(*batch)) for _ in range(6)]
+        res[mode] = (losses, g0, st)
+    (le, ge, _), (lg, gg, st) = res["eager"], res["graph"]
+    assert len(st._graphs) == 1
+    # the first forward + backward: same gradients up to float reordering (embedding-row and
+    # attention-bias gradient sums use atomics); then the loss trajectory over 6 Adam steps
+    # (parameters are not compared: Adam's first step is lr x sign(g), which an ulp of
+    # reordering flips for near-zero gradient elements)
+    for k in ge:
+        d = (gg[k] - ge[k]).abs().max().item()
+        assert d <= 1e-5 * max(ge[k].abs().max().item(), 1e-12), (k, d)
+    np.testing.assert_allclose(lg, le, rtol=1e-4, atol=0)
+    # inputs written in place: the same next step as the copying call
+    if use_cat:
+        bi = st.input_buffers(B, S, N)
+        bi[0].copy_(items)
+        bi[1].copy_(w)
+        bi[2][:B].copy_(pos)
+        bi[2][B:].copy_(neg.reshape(B * N, -1))
+        bi[3][:B].copy_(ids[0])
+        bi[3][B:].copy_(ids[2].reshape(-1))
+        bi[4][:B].copy_(ids[1])
+        bi[4][B:].copy_(ids[3].reshape(-1))
+        l1, g1 = st.forward_backward(*batch)
+        l1, g1 = float(l1), {k: v.clone() for k, v in g1.items()}
+        l2, g2 = st.forward_backward(bi[0], bi[1], bi[2][:B], bi[2][B:].view(B, N, -1),
+                                     bi[3][:B], bi[4][:B], bi[3][B:].view(B, N),
+                                     bi[4][B:].view(B, N))
+        assert abs(float(l2) - l1) <= 1e-6 * abs(l1)
+        for k in g1:
+            assert torch.allclose(g2[k], g1[k], rtol=1e-5, atol=1e-7), k
+
+
+def test_gemm_tn_one_workspace_many_shapes():
+    """One workspace serves tt_gemm_tn calls of different shapes in stream order (the training
+    step's dW3 / dW0 / dWa0): each result is complete."""
+    import ctypes
+
+    from twotower import _lib
+
+    L = _lib.lib()
+    shapes = [(2560, 768, 256), (2560, 256, 512), (10240, 128, 768), (2560, 768, 256),
+              (300, 40, 700)]
+    need = 0
+    for M, N, K in shapes:
+        v = ctypes.c_int64(0)
+        _lib.check(L.tt_gemm_tn_workspace_bytes(M, N, K, ctypes.byref(v)), "ws")
+        need = max(need, v.value)
+    ws = torch.empty(need, dtype=torch.uint8, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(3)
+    outs = []
+    for M, N, K in shapes:
+        A = torch.randn((M, N), generator=g, device="cuda")
+        Bm = torch.randn((M, K), generator=g, device="cuda")
+        C = torch.full((N, K), float("nan"), device="cuda")
+        db = torch.full((N,), float("nan"), device="cuda")
+        _lib.check(L.tt_gemm_tn(A.data_ptr(), N, Bm.data_ptr(), K, M, N, K, _lib.TT_PREC_F32,
+                                C.data_ptr(), K, db.data_ptr(), ws.data_ptr(), ws.numel(),
+                                _lib.stream_ptr()), "tt_gemm_tn")
+        outs.append((A, Bm, C, db))
+    for A, Bm, C, db in outs:
+        ref = A.double().T @ Bm.double()
+        scale = A.double().abs().T @ Bm.double().abs()
+        assert ((C.double() - ref).abs() / scale).max().item() <= 1e-5
+        assert ((db.double() - A.double().sum(0)).abs()
+                / A.double().abs().sum(0)).max().item() <= 1e-5

@@ -9,8 +9,10 @@
 //   dL/db_i  = c [ (P0_i - 1) p_i + sum_j Pn_ij n_ij + (Pb p)_i ]
 //   dL/dp_k  = c [ (P0_k - 1) b_k + (Pb^T b)_k ]
 //   dL/dn_ij = c Pn_ij b_i
-// GEMMs use tt_gemm_f32 / tt_gemm_bf16 (prec): S, Pb . p, Pb^T . b.  The row kernel
-// (logits, softmax, per-row loss) and the gradient assembly are HBM/latency-bound and tiny.
+// GEMMs (prec f32 / bf16 MFMA): S = b p^T on tt_gemm_f32 / tt_gemm_bf16; the backward's
+// Pb . p = (Pb^T)^T p and Pb^T . b on tt_gemm_tn (A^T B from the row-major Pb^T / Pb the row
+// kernel writes: no transposed or bf16 operand copies).  The row kernel (logits, softmax,
+// per-row loss) and the gradient assembly are HBM/latency-bound and tiny.
 #include "tt_common.hpp"
 
 extern "C" int tt_gemm_f32(const float* A, int64_t lda, const float* W, int64_t ldw,
@@ -21,6 +23,10 @@ extern "C" int tt_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, i
                             const float* bias, const float* residual, int64_t ldr, float* C,
                             int64_t ldc, uint16_t* C_bf16, int64_t ldc16, int32_t M, int32_t N,
                             int32_t K, int32_t act, void* stream);
+extern "C" int tt_gemm_tn_workspace_bytes(int64_t M, int32_t N, int32_t K, int64_t* bytes);
+extern "C" int tt_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M,
+                          int32_t N, int32_t K, int32_t prec, float* C, int64_t ldc, float* db,
+                          void* workspace, int64_t workspace_bytes, void* stream);
 
 namespace tt {
 
@@ -43,28 +49,6 @@ __device__ __forceinline__ float block_max(float v, float* red) {
   float s = -__builtin_huge_valf();
   for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s = fmaxf(s, red[i]);
   return s;
-}
-
-// [rows, E] (ld) -> transposed [E, ldt] f32 and/or bf16, columns >= rows zero (K padding).
-__global__ __launch_bounds__(256) void k_transpose_pad(const float* __restrict__ x, int64_t ldx,
-                                                       int rows, int E, float* __restrict__ t,
-                                                       uint16_t* __restrict__ t16, int ldt) {
-  __shared__ float tile[32][33];
-  const int r0 = blockIdx.x * 32, e0 = blockIdx.y * 32;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
-  for (int j = ty; j < 32; j += 8) {
-    const int r = r0 + j, e = e0 + tx;
-    tile[j][tx] = (r < rows && e < E) ? x[(int64_t)r * ldx + e] : 0.0f;
-  }
-  __syncthreads();
-  for (int j = ty; j < 32; j += 8) {
-    const int e = e0 + j, r = r0 + tx;
-    if (e < E && r < ldt) {
-      const float v = tile[tx][j];
-      if (t) t[(int64_t)e * ldt + r] = v;
-      if (t16) t16[(int64_t)e * ldt + r] = f32_to_bf16_rne(v);
-    }
-  }
 }
 
 __global__ __launch_bounds__(256) void k_to_bf16(const float* __restrict__ x, int64_t ldx,
@@ -125,16 +109,6 @@ __global__ __launch_bounds__(256) void k_infonce_rows(
     }
 }
 
-// padding columns [B, ldp) of P^T rows (written once; rows k < B only get columns i < B)
-__global__ void k_zero_cols(float* __restrict__ x, uint16_t* __restrict__ x16, int rows, int c0,
-                            int ld) {
-  const int r = blockIdx.x;
-  for (int c = c0 + threadIdx.x; c < ld; c += blockDim.x) {
-    if (x) x[(int64_t)r * ld + c] = 0.0f;
-    if (x16) x16[(int64_t)r * ld + c] = 0;
-  }
-}
-
 __global__ __launch_bounds__(256) void k_mean(const float* __restrict__ v, int n, float* out) {
   __shared__ float red[8];
   float s = 0.0f;
@@ -176,8 +150,10 @@ using namespace tt;
 namespace {
 size_t al(size_t b) { return (b + 255) / 256 * 256; }
 struct NceWs {
-  float *S, *row_loss, *P0, *Pn, *Pb, *PbT, *bT, *pT, *G1, *G2;
-  uint16_t *b16, *p16, *Pb16, *PbT16, *bT16, *pT16;
+  float *S, *row_loss, *P0, *Pn, *Pb, *PbT, *G1, *G2;
+  uint16_t *b16, *p16;
+  char* tn;
+  int64_t tn_bytes;
   size_t total;
 };
 NceWs nce_carve(char* base, int B, int N, int E, bool bf, bool grads) {
@@ -200,17 +176,12 @@ NceWs nce_carve(char* base, int B, int N, int E, bool bf, bool grads) {
     w.Pn = (float*)take((size_t)B * (N > 0 ? N : 1) * 4);
     w.G1 = (float*)take((size_t)B * E * 4);
     w.G2 = (float*)take((size_t)B * E * 4);
-    if (bf) {
-      w.Pb16 = (uint16_t*)take((size_t)B * Bp * 2);
-      w.PbT16 = (uint16_t*)take((size_t)B * Bp * 2);
-      w.bT16 = (uint16_t*)take((size_t)E * Bp * 2);
-      w.pT16 = (uint16_t*)take((size_t)E * Bp * 2);
-    } else {
-      w.Pb = (float*)take((size_t)B * Bp * 4);
-      w.PbT = (float*)take((size_t)B * Bp * 4);
-      w.bT = (float*)take((size_t)E * Bp * 4);
-      w.pT = (float*)take((size_t)E * Bp * 4);
-    }
+    w.Pb = (float*)take((size_t)B * Bp * 4);
+    w.PbT = (float*)take((size_t)B * Bp * 4);
+    int64_t tb = 0;
+    tt_gemm_tn_workspace_bytes(B, B, E, &tb);
+    w.tn_bytes = tb;
+    w.tn = take((size_t)tb);
   }
   w.total = off;
   return w;
@@ -256,28 +227,16 @@ extern "C" int tt_infonce_f32(const float* b, int64_t ldb, const float* p, int64
   if (rc) return rc;
   hipLaunchKernelGGL(k_infonce_rows, dim3(B), dim3(256), 0, st, b, ldb, p, ldp, n, ldn_row,
                      ldn_item, w.S, (int64_t)B, B, N, E, inv_tau, w.row_loss, w.P0,
-                     N > 0 ? w.Pn : nullptr, w.Pb, w.PbT, w.Pb16, w.PbT16, Bp);
+                     N > 0 ? w.Pn : nullptr, w.Pb, w.PbT, (uint16_t*)nullptr,
+                     (uint16_t*)nullptr, Bp);
   if ((rc = check_launch("k_infonce_rows"))) return rc;
   hipLaunchKernelGGL(k_mean, dim3(1), dim3(256), 0, st, w.row_loss, B, loss);
   if ((rc = check_launch("k_mean"))) return rc;
   if (!grads) return TT_OK;
-  if (Bp > B) {
-    hipLaunchKernelGGL(k_zero_cols, dim3(B), dim3(64), 0, st, w.PbT, w.PbT16, B, B, Bp);
-    if ((rc = check_launch("k_zero_cols"))) return rc;
-  }
-  // b^T, p^T [E, Bp] (zero-padded K)
-  const dim3 tg((unsigned)((Bp + 31) / 32), (unsigned)((E + 31) / 32));
-  hipLaunchKernelGGL(k_transpose_pad, tg, dim3(256), 0, st, b, ldb, B, E, w.bT, w.bT16, Bp);
-  hipLaunchKernelGGL(k_transpose_pad, tg, dim3(256), 0, st, p, ldp, B, E, w.pT, w.pT16, Bp);
-  if ((rc = check_launch("k_transpose_pad"))) return rc;
-  // G1 = Pb . p  (A = Pb [B, Bp], W = p^T [E, Bp]);  G2 = Pb^T . b
-  if (bf) {
-    rc = tt_gemm_bf16(w.Pb16, Bp, w.pT16, Bp, nullptr, nullptr, 0, w.G1, E, nullptr, 0, B, E, Bp, 0, stream);
-    if (!rc) rc = tt_gemm_bf16(w.PbT16, Bp, w.bT16, Bp, nullptr, nullptr, 0, w.G2, E, nullptr, 0, B, E, Bp, 0, stream);
-  } else {
-    rc = tt_gemm_f32(w.Pb, Bp, w.pT, Bp, nullptr, nullptr, 0, w.G1, E, nullptr, 0, B, E, Bp, 0, stream);
-    if (!rc) rc = tt_gemm_f32(w.PbT, Bp, w.bT, Bp, nullptr, nullptr, 0, w.G2, E, nullptr, 0, B, E, Bp, 0, stream);
-  }
+  // G1 = Pb . p = (Pb^T)^T p;  G2 = Pb^T . b   (row-major Pb^T / Pb as the A^T operands)
+  rc = tt_gemm_tn(w.PbT, Bp, p, ldp, B, B, E, prec, w.G1, E, nullptr, w.tn, w.tn_bytes, stream);
+  if (!rc)
+    rc = tt_gemm_tn(w.Pb, Bp, b, ldb, B, B, E, prec, w.G2, E, nullptr, w.tn, w.tn_bytes, stream);
   if (rc) return rc;
   hipLaunchKernelGGL(k_infonce_grads, dim3(B), dim3(256), 0, st, b, ldb, p, ldp, n, ldn_row,
                      ldn_item, B, N, E, inv_tau / (float)B, w.P0, w.Pn, w.G1, w.G2, (int64_t)E,

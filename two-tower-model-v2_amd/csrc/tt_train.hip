@@ -29,7 +29,9 @@ __global__ __launch_bounds__(256) void k_l2norm_bwd(const float* __restrict__ y,
                                                     const float* __restrict__ z, int64_t ldz,
                                                     const float* __restrict__ dz, int64_t lddz,
                                                     int64_t n, int d, float* __restrict__ dy,
-                                                    int64_t lddy) {
+                                                    int64_t lddy,
+                                                    uint16_t* __restrict__ dy16 = nullptr,
+                                                    int64_t lddy16 = 0) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int64_t r = (int64_t)blockIdx.x * 4 + w; r < n; r += (int64_t)gridDim.x * 4) {
     float ss = 0.0f, zd = 0.0f;
@@ -43,7 +45,9 @@ __global__ __launch_bounds__(256) void k_l2norm_bwd(const float* __restrict__ y,
     const float nrm = sqrtf(ss);
     for (int e = lane; e < d; e += 64) {
       const float g = dz[r * lddz + e];
-      dy[r * lddy + e] = nrm > 1e-12f ? (g - z[r * ldz + e] * zd) / nrm : g / 1e-12f;
+      const float v = nrm > 1e-12f ? (g - z[r * ldz + e] * zd) / nrm : g / 1e-12f;
+      dy[r * lddy + e] = v;
+      if (dy16) dy16[r * lddy16 + e] = f32_to_bf16_rne(v);
     }
   }
 }
@@ -109,11 +113,13 @@ __global__ void k_dropout(float* __restrict__ x, const uint8_t* __restrict__ kee
 //   z = o / max(||o||, 1e-12).  Saves alpha [B, S] and ||o|| [B] for the backward.
 __global__ __launch_bounds__(256) void k_attn_pool_fwd(
     const float* __restrict__ H, int Hd, const float* __restrict__ W2, float b2,
-    const float* __restrict__ w, const float* __restrict__ x, int S, int E,
-    float* __restrict__ alpha, float* __restrict__ onorm, float* __restrict__ z, int64_t ldz) {
+    const float* __restrict__ b2p, const float* __restrict__ w, const float* __restrict__ x,
+    int S, int E, float* __restrict__ alpha, float* __restrict__ onorm, float* __restrict__ z,
+    int64_t ldz) {
   __shared__ float cs[128];
   __shared__ float red[4];
   const int b = blockIdx.x, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  if (b2p) b2 = *b2p;  // the bias read on the device (a graph-captured step: no host sync)
   for (int s = wv; s < S; s += 4) {  // wave per position
     const float* h = H + ((int64_t)b * S + s) * Hd;
     float a = 0.0f;
@@ -160,7 +166,8 @@ __global__ __launch_bounds__(256) void k_attn_pool_bwd(
     const float* __restrict__ dz, int64_t lddz, const float* __restrict__ z, int64_t ldz,
     const float* __restrict__ onorm, const float* __restrict__ alpha,
     const float* __restrict__ w, const float* __restrict__ x, int S, int E,
-    const float* __restrict__ W2, int Hd, float* __restrict__ da, float* __restrict__ dH) {
+    const float* __restrict__ W2, int Hd, float* __restrict__ da, float* __restrict__ dH,
+    const float* __restrict__ Hmask) {
   __shared__ float dov[1024];
   __shared__ float dal[128];
   __shared__ float red[4];
@@ -191,7 +198,10 @@ __global__ __launch_bounds__(256) void k_attn_pool_bwd(
     const float al = alpha[(int64_t)b * S + s];
     const float das = al * (dal[s] - adot) * w[(int64_t)b * S + s];
     if (tid == 0) da[(int64_t)b * S + s] = das;
-    for (int j = tid; j < Hd; j += 256) dH[((int64_t)b * S + s) * Hd + j] = das * W2[j];
+    for (int j = tid; j < Hd; j += 256) {
+      const int64_t o = ((int64_t)b * S + s) * Hd + j;
+      dH[o] = Hmask && !(Hmask[o] > 0.0f) ? 0.0f : das * W2[j];  // (ReLU backward, fused)
+    }
   }
 }
 
@@ -252,6 +262,291 @@ __global__ void k_adam(float* __restrict__ p, const float* __restrict__ g, float
 unsigned grid_for(int64_t n) {
   const int64_t b = (n + 255) / 256;
   return (unsigned)(b < 8192 ? (b > 0 ? b : 1) : 8192);
+}
+
+// ------------------------------------------------------------- C = A^T B  (weight gradients)
+// dW [N, K] = dY^T X for row-major dY [M, N], X [M, K] f32: the reduction runs over the batch
+// rows M (2.5k-10k) while N, K <= 768, so a tile grid over the output alone has 24-96 blocks.
+// Each block takes one 64 x 64 output tile and one split of the rows and writes its partial
+// tile to the workspace; k_tn_reduce then sums the splits of every output element in split
+// order (deterministic; one thread per element, so the tail is parallel, not one block's).  No
+// transposed copies: a 64-row chunk of dY and X is staged in LDS with m contiguous (a lane's
+// coalesced column loads land as one 16-B write), and the next chunk's loads are in flight
+// while this chunk's MFMAs run.  BF: operands rounded to bf16 (RNE) in registers,
+// v_mfma_f32_16x16x32_bf16; else v_mfma_f32_16x16x4_f32.  Optional db [N] = column sums of
+// dY (the bias gradient, from the same loads; f32, fixed order).
+typedef __bf16 tn_bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int TN_T = 64;
+constexpr int TN_SMAX = 32;  // row splits per tile
+__host__ __device__ constexpr int tn_pitch(bool bf) { return bf ? 64 + 8 : 64 + 4; }
+
+template <bool BF>
+__global__ __launch_bounds__(256) void k_gemm_tn(const float* __restrict__ A, int64_t lda,
+                                                 const float* __restrict__ B, int64_t ldb, int M,
+                                                 int N, int K, int mc, float* __restrict__ C,
+                                                 int64_t ldc, float* __restrict__ db,
+                                                 float* __restrict__ parts,
+                                                 float* __restrict__ dbparts) {
+  using E = typename std::conditional<BF, uint16_t, float>::type;
+  constexpr int P = tn_pitch(BF);
+  __shared__ __attribute__((aligned(16))) E sA[TN_T * P];
+  __shared__ __attribute__((aligned(16))) E sB[TN_T * P];
+  __shared__ float sdb[4][TN_T];
+  const int kt = blockIdx.x, nt = blockIdx.y, s = blockIdx.z, S = gridDim.z;
+  const int KT = gridDim.x, tile = nt * KT + kt;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int col = tid & 63, grp = tid >> 6;  // staging: column col, m-groups grp and grp + 4
+  const int n0 = nt * TN_T, k0 = kt * TN_T;
+  const int m_beg = s * mc, m_end = min(M, m_beg + mc);
+  const bool na = n0 + col < N, kb = k0 + col < K;
+  const bool want_db = db != nullptr && kt == 0;
+  const int wn = w & 1, wk = w >> 1, r = lane & 15, q = lane >> 4;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float dbs = 0.0f;
+  float av[2][8], bv[2][8];
+  auto load = [&](int mc0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int g8 = 8 * (grp + 4 * h);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = mc0 + g8 + j;
+        const bool mv = m < m_end;
+        av[h][j] = mv && na ? A[(int64_t)m * lda + n0 + col] : 0.0f;
+        bv[h][j] = mv && kb ? B[(int64_t)m * ldb + k0 + col] : 0.0f;
+      }
+    }
+  };
+  if (m_beg < m_end) load(m_beg);
+  for (int mc0 = m_beg; mc0 < m_end; mc0 += TN_T) {
+    if (want_db) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dbs += av[h][j];
+    }
+    __syncthreads();  // the previous chunk's fragment reads are done
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int g8 = 8 * (grp + 4 * h);
+      if constexpr (BF) {
+        uint32_t pa[4], pb[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pa[j] = (uint32_t)f32_to_bf16_rne(av[h][2 * j]) |
+                  ((uint32_t)f32_to_bf16_rne(av[h][2 * j + 1]) << 16);
+          pb[j] = (uint32_t)f32_to_bf16_rne(bv[h][2 * j]) |
+                  ((uint32_t)f32_to_bf16_rne(bv[h][2 * j + 1]) << 16);
+        }
+        *(u32x4_t*)&sA[col * P + g8] = u32x4_t{pa[0], pa[1], pa[2], pa[3]};
+        *(u32x4_t*)&sB[col * P + g8] = u32x4_t{pb[0], pb[1], pb[2], pb[3]};
+      } else {
+        *(f32x4*)&sA[col * P + g8] = f32x4{av[h][0], av[h][1], av[h][2], av[h][3]};
+        *(f32x4*)&sA[col * P + g8 + 4] = f32x4{av[h][4], av[h][5], av[h][6], av[h][7]};
+        *(f32x4*)&sB[col * P + g8] = f32x4{bv[h][0], bv[h][1], bv[h][2], bv[h][3]};
+        *(f32x4*)&sB[col * P + g8 + 4] = f32x4{bv[h][4], bv[h][5], bv[h][6], bv[h][7]};
+      }
+    }
+    __syncthreads();
+    if (mc0 + TN_T < m_end) load(mc0 + TN_T);  // next chunk in flight during the MFMAs
+    if constexpr (BF) {
+#pragma unroll
+      for (int kk = 0; kk < TN_T; kk += 32) {
+        tn_bf16x8 fa[2], fb[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          fa[i] = *(const tn_bf16x8*)&sA[(32 * wn + 16 * i + r) * P + kk + 8 * q];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          fb[j] = *(const tn_bf16x8*)&sB[(32 * wk + 16 * j + r) * P + kk + 8 * q];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < TN_T; kk += 4) {
+        float fa[2], fb[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) fa[i] = sA[(32 * wn + 16 * i + r) * P + kk + q];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb[j] = sB[(32 * wk + 16 * j + r) * P + kk + q];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  // D lane layout: acc[i][j][v] = tile[n = 32 wn + 16 i + 4 q + v][k = 32 wk + 16 j + r]
+  if (want_db) {
+    sdb[grp][col] = dbs;
+    __syncthreads();
+  }
+  if (S == 1) {  // no split: straight to C (and db)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int n = n0 + 32 * wn + 16 * i + 4 * q + v, k = k0 + 32 * wk + 16 * j + r;
+          if (n < N && k < K) C[(int64_t)n * ldc + k] = acc[i][j][v];
+        }
+    if (want_db && tid < TN_T && n0 + tid < N)
+      db[n0 + tid] = ((sdb[0][tid] + sdb[1][tid]) + sdb[2][tid]) + sdb[3][tid];
+    return;
+  }
+  const int T = gridDim.x * gridDim.y;
+  float* pt = parts + ((int64_t)s * T + tile) * (TN_T * TN_T);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        pt[(32 * wn + 16 * i + 4 * q + v) * TN_T + 32 * wk + 16 * j + r] = acc[i][j][v];
+  if (want_db && tid < TN_T)
+    dbparts[(int64_t)s * gridDim.y * TN_T + n0 + tid] =
+        ((sdb[0][tid] + sdb[1][tid]) + sdb[2][tid]) + sdb[3][tid];
+}
+
+// The splits' sum, one thread per output element (and per bias-gradient entry), in split
+// order; the S loads of a thread are independent, so they are all in flight at once.
+__global__ __launch_bounds__(256) void k_tn_reduce(const float* __restrict__ parts,
+                                                   const float* __restrict__ dbparts, int S,
+                                                   int T, int KT, int NT, int N, int K,
+                                                   float* __restrict__ C, int64_t ldc,
+                                                   float* __restrict__ db) {
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t ne = (int64_t)T * TN_T * TN_T;
+  if (gid < ne) {
+    const int tile = (int)(gid / (TN_T * TN_T)), e = (int)(gid % (TN_T * TN_T));
+    const int n = (tile / KT) * TN_T + e / TN_T, k = (tile % KT) * TN_T + e % TN_T;
+    if (n >= N || k >= K) return;
+    float v[TN_SMAX];
+#pragma unroll
+    for (int u = 0; u < TN_SMAX; ++u) v[u] = u < S ? parts[(int64_t)u * ne + gid] : 0.0f;
+    float sum = v[0];
+#pragma unroll
+    for (int u = 1; u < TN_SMAX; ++u)
+      if (u < S) sum += v[u];
+    C[(int64_t)n * ldc + k] = sum;
+    return;
+  }
+  const int64_t i = gid - ne;  // bias gradient entries
+  if (db == nullptr || i >= N) return;
+  float v[TN_SMAX];
+#pragma unroll
+  for (int u = 0; u < TN_SMAX; ++u) v[u] = u < S ? dbparts[(int64_t)u * NT * TN_T + i] : 0.0f;
+  float sum = v[0];
+#pragma unroll
+  for (int u = 1; u < TN_SMAX; ++u)
+    if (u < S) sum += v[u];
+  db[i] = sum;
+}
+
+struct TnPlan {
+  int NT, KT, S, mc;
+  size_t parts, dbparts, total;
+};
+TnPlan tn_plan(int64_t M, int N, int K) {
+  TnPlan p{};
+  p.NT = (N + TN_T - 1) / TN_T;
+  p.KT = (K + TN_T - 1) / TN_T;
+  const int T = p.NT * p.KT;
+  int64_t S = (512 + T - 1) / T;  // ~2 blocks per CU
+  const int64_t maxS = (M + TN_T - 1) / TN_T;
+  if (S > maxS) S = maxS;
+  if (S > TN_SMAX) S = TN_SMAX;
+  if (S < 1) S = 1;
+  int64_t mc = (M + S - 1) / S;
+  mc = (mc + TN_T - 1) / TN_T * TN_T;
+  if (mc < TN_T) mc = TN_T;
+  p.mc = (int)mc;
+  p.S = (int)((M + mc - 1) / mc);
+  if (p.S < 1) p.S = 1;
+  auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+  p.parts = 0;
+  p.dbparts = p.S > 1 ? al((size_t)p.S * T * TN_T * TN_T * 4) : 0;
+  p.total = p.S > 1 ? p.dbparts + al((size_t)p.S * p.NT * TN_T * 4) : 0;
+  return p;
+}
+
+// ------------------------------------------------- fused elementwise pieces of the step
+// nn.Dropout forward with a given keep mask plus the bf16 copy the next GEMM reads
+__global__ void k_dropout_ex(float* __restrict__ x, const uint8_t* __restrict__ keep, float scale,
+                             int64_t n, uint16_t* __restrict__ x16) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = keep[i] ? x[i] * scale : 0.0f;
+    x[i] = v;
+    if (x16) x16[i] = f32_to_bf16_rne(v);
+  }
+}
+
+// ReLU (+ Dropout) backward on the post-activation h: h > 0 iff the unit was kept and active,
+// so dh = h > 0 ? dh * scale : 0 covers both (scale = 1 / (1 - p), 1 without dropout)
+__global__ void k_relu_drop_bwd(float* __restrict__ dh, const float* __restrict__ h, float scale,
+                                int64_t n, uint16_t* __restrict__ dh16) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = h[i] > 0.0f ? dh[i] * scale : 0.0f;
+    dh[i] = v;
+    if (dh16) dh16[i] = f32_to_bf16_rne(v);
+  }
+}
+
+struct tt_convert_batch_args {
+  tt_convert_job jobs[TT_CONVERT_MAX_JOBS];
+  int tile_off[TT_CONVERT_MAX_JOBS];
+  int njobs;
+};
+
+// Batched operand preparation (one launch per step for all weight-derived GEMM operands and
+// the bf16 copies of f32 inputs): job j copies src [rows, cols] to dst as f32 or bf16,
+// optionally transposed (dst [cols, ld_dst], columns rows..ld_dst-1 zero-filled).
+__global__ __launch_bounds__(256) void k_convert_batch(tt_convert_batch_args a) {
+  int j = 0;
+  while (j + 1 < a.njobs && (int)blockIdx.x >= a.tile_off[j + 1]) ++j;
+  const tt_convert_job& jb = a.jobs[j];
+  const int t = (int)blockIdx.x - a.tile_off[j];
+  const int rr = jb.transpose ? (int)(jb.ld_dst > jb.rows ? jb.ld_dst : jb.rows) : jb.rows;
+  const int ct = (jb.cols + 31) / 32;
+  const int r0 = (t / ct) * 32, c0 = (t % ct) * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  if (!jb.transpose) {
+    for (int y = ty; y < 32; y += 8) {
+      const int r = r0 + y, c = c0 + tx;
+      if (r < jb.rows && c < jb.cols) {
+        const float v = jb.src[(int64_t)r * jb.ld_src + c];
+        if (jb.to_bf16) ((uint16_t*)jb.dst)[(int64_t)r * jb.ld_dst + c] = f32_to_bf16_rne(v);
+        else ((float*)jb.dst)[(int64_t)r * jb.ld_dst + c] = v;
+      }
+    }
+    return;
+  }
+  __shared__ float tl[32][33];
+  for (int y = ty; y < 32; y += 8) {
+    const int r = r0 + y, c = c0 + tx;
+    tl[y][tx] = (r < jb.rows && c < jb.cols) ? jb.src[(int64_t)r * jb.ld_src + c] : 0.0f;
+  }
+  __syncthreads();
+  for (int y = ty; y < 32; y += 8) {
+    const int c = c0 + y, r = r0 + tx;
+    if (c < jb.cols && r < rr) {
+      const float v = tl[tx][y];
+      if (jb.to_bf16) ((uint16_t*)jb.dst)[(int64_t)c * jb.ld_dst + r] = f32_to_bf16_rne(v);
+      else ((float*)jb.dst)[(int64_t)c * jb.ld_dst + r] = v;
+    }
+  }
 }
 
 }  // namespace tt
@@ -321,15 +616,28 @@ extern "C" int tt_attn_pool_fwd_f32(const float* H, int32_t Hd, const float* W2,
   if (B == 0) return TT_OK;
   TT_REQUIRE(H && W2 && w && x && alpha && onorm && z, "null pointer");
   hipLaunchKernelGGL(k_attn_pool_fwd, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, H, Hd,
-                     W2, b2, w, x, S, E, alpha, onorm, z, ldz);
+                     W2, b2, (const float*)nullptr, w, x, S, E, alpha, onorm, z, ldz);
   return check_launch("tt_attn_pool_fwd_f32");
 }
 
-extern "C" int tt_attn_pool_bwd_f32(const float* dz, int64_t lddz, const float* z, int64_t ldz,
-                                    const float* onorm, const float* alpha, const float* w,
-                                    const float* x, int64_t B, int32_t S, int32_t E,
-                                    const float* H, const float* W2, int32_t Hd, float* dW2,
-                                    float* db2, float* dH, float* da_ws, void* stream) {
+extern "C" int tt_attn_pool_fwd_f32_dev(const float* H, int32_t Hd, const float* W2,
+                                        const float* b2, const float* w, const float* x, int64_t B,
+                                        int32_t S, int32_t E, float* alpha, float* onorm, float* z,
+                                        int64_t ldz, void* stream) {
+  TT_REQUIRE(B >= 0 && S >= 1 && S <= 128 && E >= 1 && E <= 1024 && Hd >= 1,
+             "need 1 <= S <= 128, 1 <= E <= 1024");
+  if (B == 0) return TT_OK;
+  TT_REQUIRE(H && W2 && b2 && w && x && alpha && onorm && z, "null pointer");
+  hipLaunchKernelGGL(k_attn_pool_fwd, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, H, Hd,
+                     W2, 0.0f, b2, w, x, S, E, alpha, onorm, z, ldz);
+  return check_launch("tt_attn_pool_fwd_f32_dev");
+}
+
+namespace {
+int attn_pool_bwd(const float* dz, int64_t lddz, const float* z, int64_t ldz, const float* onorm,
+                  const float* alpha, const float* w, const float* x, int64_t B, int32_t S,
+                  int32_t E, const float* H, const float* W2, int32_t Hd, float* dW2, float* db2,
+                  float* dH, float* da_ws, bool relu_mask, void* stream) {
   TT_REQUIRE(B >= 0 && S >= 1 && S <= 128 && E >= 1 && E <= 1024 && Hd >= 1,
              "need 1 <= S <= 128, 1 <= E <= 1024");
   if (B == 0) return TT_OK;
@@ -337,7 +645,8 @@ extern "C" int tt_attn_pool_bwd_f32(const float* dz, int64_t lddz, const float* 
              "null pointer");
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_attn_pool_bwd, dim3((unsigned)B), dim3(256), 0, st, dz, lddz, z, ldz,
-                     onorm, alpha, w, x, S, E, W2, Hd, da_ws, dH);
+                     onorm, alpha, w, x, S, E, W2, Hd, da_ws, dH,
+                     relu_mask ? H : (const float*)nullptr);
   int rc = check_launch("k_attn_pool_bwd");
   if (rc) return rc;
   if (hipMemsetAsync(dW2, 0, (size_t)Hd * 4, st) != hipSuccess ||
@@ -349,6 +658,26 @@ extern "C" int tt_attn_pool_bwd_f32(const float* dz, int64_t lddz, const float* 
                      dim3(256), 0, st, H, Hd, da_ws, B * S, dW2, db2);
   return check_launch("k_weighted_col_sum");
 }
+}  // namespace
+
+extern "C" int tt_attn_pool_bwd_f32(const float* dz, int64_t lddz, const float* z, int64_t ldz,
+                                    const float* onorm, const float* alpha, const float* w,
+                                    const float* x, int64_t B, int32_t S, int32_t E,
+                                    const float* H, const float* W2, int32_t Hd, float* dW2,
+                                    float* db2, float* dH, float* da_ws, void* stream) {
+  return attn_pool_bwd(dz, lddz, z, ldz, onorm, alpha, w, x, B, S, E, H, W2, Hd, dW2, db2, dH,
+                       da_ws, false, stream);
+}
+
+extern "C" int tt_attn_pool_bwd_relu_f32(const float* dz, int64_t lddz, const float* z,
+                                         int64_t ldz, const float* onorm, const float* alpha,
+                                         const float* w, const float* x, int64_t B, int32_t S,
+                                         int32_t E, const float* H, const float* W2, int32_t Hd,
+                                         float* dW2, float* db2, float* dH, float* da_ws,
+                                         void* stream) {
+  return attn_pool_bwd(dz, lddz, z, ldz, onorm, alpha, w, x, B, S, E, H, W2, Hd, dW2, db2, dH,
+                       da_ws, true, stream);
+}
 
 extern "C" int tt_embedding_backward_f32(const float* g, int64_t ldg, const int32_t* ids,
                                          int64_t n, int32_t C, float* table_grad, void* stream) {
@@ -358,6 +687,105 @@ extern "C" int tt_embedding_backward_f32(const float* g, int64_t ldg, const int3
   hipLaunchKernelGGL(k_embedding_bwd, dim3((unsigned)n), dim3(64), 0, (hipStream_t)stream, g, ldg,
                      ids, n, C, table_grad);
   return check_launch("tt_embedding_backward_f32");
+}
+
+extern "C" int tt_gemm_tn_workspace_bytes(int64_t M, int32_t N, int32_t K, int64_t* bytes) {
+  TT_REQUIRE(bytes && M >= 0 && N >= 0 && K >= 0, "bad arguments");
+  *bytes = (int64_t)tn_plan(M, N, K).total;
+  return TT_OK;
+}
+
+extern "C" int tt_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M,
+                          int32_t N, int32_t K, int32_t prec, float* C, int64_t ldc, float* db,
+                          void* workspace, int64_t workspace_bytes, void* stream) {
+  TT_REQUIRE(M >= 0 && N >= 0 && K >= 0 && M <= 0x7fffffffLL, "bad sizes");
+  TT_REQUIRE(prec == TT_PREC_F32 || prec == TT_PREC_BF16, "prec must be TT_PREC_F32 / BF16");
+  if (N == 0 || K == 0) return TT_OK;
+  TT_REQUIRE(C && ldc >= K && lda >= N && ldb >= K, "null C or ld too small");
+  hipStream_t st = (hipStream_t)stream;
+  if (M == 0) {  // empty reduction: zeros
+    if (hipMemset2DAsync(C, (size_t)ldc * 4, 0, (size_t)K * 4, (size_t)N, st) != hipSuccess ||
+        (db && hipMemsetAsync(db, 0, (size_t)N * 4, st) != hipSuccess))
+      return fail(TT_ERR_LAUNCH, "tt_gemm_tn: hipMemset");
+    return TT_OK;
+  }
+  TT_REQUIRE(A && B, "null operand");
+  const TnPlan p = tn_plan(M, N, K);
+  TT_REQUIRE(p.NT <= 65535, "N too large");
+  if (p.S > 1 && (!workspace || workspace_bytes < (int64_t)p.total))
+    return fail(TT_ERR_WORKSPACE, "tt_gemm_tn: workspace too small (tt_gemm_tn_workspace_bytes)");
+  char* ws = (char*)workspace;
+  float* parts = p.S > 1 ? (float*)(ws + p.parts) : nullptr;
+  float* dbparts = p.S > 1 ? (float*)(ws + p.dbparts) : nullptr;
+  const dim3 grid((unsigned)p.KT, (unsigned)p.NT, (unsigned)p.S);
+  if (prec == TT_PREC_BF16)
+    hipLaunchKernelGGL(k_gemm_tn<true>, grid, dim3(256), 0, st, A, lda, B, ldb, (int)M, N, K,
+                       p.mc, C, ldc, db, parts, dbparts);
+  else
+    hipLaunchKernelGGL(k_gemm_tn<false>, grid, dim3(256), 0, st, A, lda, B, ldb, (int)M, N, K,
+                       p.mc, C, ldc, db, parts, dbparts);
+  int rc = check_launch("k_gemm_tn");
+  if (rc || p.S == 1) return rc;
+  const int T = p.NT * p.KT;
+  const int64_t items = (int64_t)T * TN_T * TN_T + (db ? N : 0);
+  hipLaunchKernelGGL(k_tn_reduce, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, parts,
+                     dbparts, p.S, T, p.KT, p.NT, N, K, C, ldc, db);
+  return check_launch("k_tn_reduce");
+}
+
+extern "C" int tt_dropout_apply_ex(float* x, const uint8_t* keep, float scale, int64_t n,
+                                   uint16_t* x_bf16, void* stream) {
+  TT_REQUIRE(n >= 0, "n < 0");
+  if (n == 0) return TT_OK;
+  TT_REQUIRE(x && keep, "null pointer");
+  hipLaunchKernelGGL(k_dropout_ex, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, keep,
+                     scale, n, x_bf16);
+  return check_launch("tt_dropout_apply_ex");
+}
+
+extern "C" int tt_relu_dropout_backward_f32(float* dh, const float* h, float scale, int64_t n,
+                                            uint16_t* dh_bf16, void* stream) {
+  TT_REQUIRE(n >= 0, "n < 0");
+  if (n == 0) return TT_OK;
+  TT_REQUIRE(dh && h, "null pointer");
+  hipLaunchKernelGGL(k_relu_drop_bwd, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, dh, h,
+                     scale, n, dh_bf16);
+  return check_launch("tt_relu_dropout_backward_f32");
+}
+
+extern "C" int tt_convert_batch(const tt_convert_job* jobs, int32_t njobs, void* stream) {
+  TT_REQUIRE(jobs && njobs >= 0 && njobs <= TT_CONVERT_MAX_JOBS, "need 0 <= njobs <= 8");
+  tt_convert_batch_args a{};
+  int tiles = 0, nj = 0;
+  for (int j = 0; j < njobs; ++j) {
+    const tt_convert_job& jb = jobs[j];
+    TT_REQUIRE(jb.src && jb.dst && jb.rows >= 0 && jb.cols >= 0 && jb.ld_src >= jb.cols,
+               "bad job");
+    TT_REQUIRE(jb.transpose ? jb.ld_dst >= jb.rows : jb.ld_dst >= jb.cols, "bad job ld_dst");
+    if (jb.rows == 0 || jb.cols == 0) continue;
+    const int64_t rr = jb.transpose && jb.ld_dst > jb.rows ? jb.ld_dst : jb.rows;
+    a.jobs[nj] = jb;
+    a.tile_off[nj] = tiles;
+    tiles += (int)(((rr + 31) / 32) * ((jb.cols + 31) / 32));
+    ++nj;
+  }
+  a.njobs = nj;
+  if (tiles == 0) return TT_OK;
+  hipLaunchKernelGGL(k_convert_batch, dim3((unsigned)tiles), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("tt_convert_batch");
+}
+
+extern "C" int tt_l2norm_backward_ex(const float* y, int64_t ldy, const float* z, int64_t ldz,
+                                     const float* dz, int64_t lddz, int64_t n, int32_t d,
+                                     float* dy, int64_t lddy, uint16_t* dy_bf16, int64_t lddy16,
+                                     void* stream) {
+  TT_REQUIRE(n >= 0 && d >= 1, "bad sizes");
+  if (n == 0) return TT_OK;
+  TT_REQUIRE(y && z && dz && dy, "null pointer");
+  hipLaunchKernelGGL(k_l2norm_bwd, dim3(grid_for((n + 3) / 4 * 256)), dim3(256), 0,
+                     (hipStream_t)stream, y, ldy, z, ldz, dz, lddz, n, d, dy, lddy, dy_bf16,
+                     lddy16);
+  return check_launch("tt_l2norm_backward_ex");
 }
 
 extern "C" int tt_adam_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr,

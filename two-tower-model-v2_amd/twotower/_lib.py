@@ -54,6 +54,12 @@ class BertModel(ctypes.Structure):
                 ("emb_ln_b", _vp), ("layer", ctypes.POINTER(BertLayer))]
 
 
+class ConvertJob(ctypes.Structure):
+    """tt_convert_job (include/twotower_hip.h): one operand copy of tt_convert_batch."""
+    _fields_ = [("src", _vp), ("ld_src", _i64), ("rows", _i32), ("cols", _i32), ("dst", _vp),
+                ("ld_dst", _i64), ("transpose", _i32), ("to_bf16", _i32)]
+
+
 # name -> (restype, argtypes); mirrors include/twotower_hip.h
 SIGNATURES = {
     "tt_version": (ctypes.c_int, []),
@@ -157,6 +163,19 @@ SIGNATURES = {
     "tt_adam_f32": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float,
                                    ctypes.c_float, ctypes.c_float, _i32, _vp]),
     "tt_f32_to_bf16": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp]),
+    "tt_attn_pool_fwd_f32_dev": (ctypes.c_int, [_vp, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32,
+                                                _vp, _vp, _vp, _i64, _vp]),
+    "tt_attn_pool_bwd_relu_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i64,
+                                                 _i32, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _vp,
+                                                 _vp]),
+    "tt_gemm_tn_workspace_bytes": (ctypes.c_int, [_i64, _i32, _i32, ctypes.POINTER(_i64)]),
+    "tt_gemm_tn": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32, _vp, _i64, _vp,
+                                  _vp, _i64, _vp]),
+    "tt_dropout_apply_ex": (ctypes.c_int, [_vp, _vp, ctypes.c_float, _i64, _vp, _vp]),
+    "tt_relu_dropout_backward_f32": (ctypes.c_int, [_vp, _vp, ctypes.c_float, _i64, _vp, _vp]),
+    "tt_l2norm_backward_ex": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _vp,
+                                             _i64, _vp, _i64, _vp]),
+    "tt_convert_batch": (ctypes.c_int, [ctypes.POINTER(ConvertJob), _i32, _vp]),
     "tt_item_concat": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _i32, _i64, _vp, _i64,
                                       _vp, _vp]),
 }

@@ -14,6 +14,7 @@ Python only sequences the launches and owns the buffers.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Dict, List, Optional
 
 import torch
@@ -97,11 +98,38 @@ class GemmOps:
         return out
 
 
+def _vp(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class _Bufs:
+    """Every intermediate of one step shape (preallocated once: a replayed HIP graph and the
+    eager launch sequence read and write the same addresses)."""
+
+
 class TwoTowerTrainStep:
-    """One optimizer step of the item head + buyer attention under InfoNCE (Adam)."""
+    """One optimizer step of the item head + buyer attention under InfoNCE (Adam).
+
+    Layout: the trained parameters live in ONE flat f32 buffer (the modules' parameters are
+    views of it), beside flat gradient / Adam-moment buffers, so Adam is one launch and the
+    data-parallel gradient average one all-reduce.  Every intermediate of a step shape is
+    preallocated; the launch sequence per step is:
+
+      forward   concat(+bf16 copy) | operand prep (ONE tt_convert_batch: bf16 weights,
+                transposed weights, bf16 history rows) | head GEMM + ReLU | dropout (+bf16) |
+                head GEMM | F.normalize | attention GEMM + ReLU | attention pooling | InfoNCE
+      backward  F.normalize bwd (+bf16) | dW3, db3 (tt_gemm_tn: A^T B, bias fused) | dh GEMM |
+                ReLU + dropout bwd (+bf16) | dW0, db0 (tt_gemm_tn) | embedding-row grads |
+                attention pooling bwd (+ReLU) | dWa0, dba0 (tt_gemm_tn)
+      then      all-reduce (multi-GPU) | Adam (one launch over the flat buffers)
+
+    ``graph=True`` captures forward + backward of each step shape in a HIP graph (torch's
+    CUDAGraph over the same launches) after one eager warm-up call, and replays it: the ~35
+    launches cost one graph launch of host time.  Inputs are copied into the graph's static
+    buffers (``input_buffers`` hands them out to write in place instead)."""
 
     def __init__(self, item_tower, buyer_tower, temperature: float = 0.07, lr: float = 1e-4,
-                 betas=(0.9, 0.999), eps: float = 1e-8, prec: str = "f32"):
+                 betas=(0.9, 0.999), eps: float = 1e-8, prec: str = "f32", graph: bool = False):
         if buyer_tower.aggregation_method not in ("attention", "weighted_avg"):
             raise ValueError(f"Unknown aggregation method: {buyer_tower.aggregation_method}")
         self.attention = buyer_tower.aggregation_method == "attention"
@@ -113,16 +141,19 @@ class TwoTowerTrainStep:
         self.ops = GemmOps(prec, self.dev)
         self.it.to(self.dev)
         self.bt.to(self.dev)
-        self.params = self._params()
-        self.m = {k: torch.zeros_like(v) for k, v in self.params.items()}
-        self.v = {k: torch.zeros_like(v) for k, v in self.params.items()}
+        self._flatten()
         self.t = 0
         self.last_loss = None
         # nn.Dropout(0.1) of the projection (item_tower.py:61): active when the item tower is
         # in train mode, as under the reference Trainer (model.train(), trainer.py:167)
         self.keep_fn = dropout_keep
+        self.graph = graph
+        self._bufs = {}    # shape key -> _Bufs
+        self._graphs = {}  # shape key -> torch.cuda.CUDAGraph (graph=True)
+        self._pool = None
 
-    def _params(self) -> Dict[str, torch.Tensor]:
+    # ------------------------------------------------------------------ flat parameters
+    def _param_objs(self) -> Dict[str, torch.nn.Parameter]:
         it, bt = self.it, self.bt
         p = {"proj0.w": it.projection[0].weight, "proj0.b": it.projection[0].bias,
              "proj3.w": it.projection[3].weight, "proj3.b": it.projection[3].bias}
@@ -130,27 +161,149 @@ class TwoTowerTrainStep:
             p.update({"att0.w": bt.attention[0].weight, "att0.b": bt.attention[0].bias,
                       "att2.w": bt.attention[2].weight, "att2.b": bt.attention[2].bias})
         if it.use_categorical_features and it.brand_embedding is not None:
-            p["brand"] = it.brand_embedding.weight
+            p["brand"] = it.brand_embedding.weight  # brand and cat adjacent: one zero-fill
             p["cat"] = it.category_embedding.weight
-        for v in p.values():
-            if not v.is_contiguous():
-                raise ValueError("parameters must be contiguous")
-        return {k: v.data for k, v in p.items()}
+        return p
 
+    def _flatten(self) -> None:
+        """Move the trained parameters into one flat buffer (module parameters become views)
+        and lay out the matching gradient / moment buffers.  Moments carry over by name."""
+        objs = self._param_objs()
+        total = sum(v.numel() for v in objs.values())
+        flat = torch.empty(total, dtype=torch.float32, device=self.dev)
+        old_m, old_v = getattr(self, "m", None), getattr(self, "v", None)
+        fm = torch.zeros(total, dtype=torch.float32, device=self.dev)
+        fv = torch.zeros(total, dtype=torch.float32, device=self.dev)
+        self.flat_g = torch.zeros(total, dtype=torch.float32, device=self.dev)
+        self.params, self.m, self.v, self.g, self._span = {}, {}, {}, {}, {}
+        off = 0
+        for k, prm in objs.items():
+            n = prm.numel()
+            view = flat[off:off + n].view(prm.shape)
+            view.copy_(prm.data)
+            prm.data = view
+            self.params[k] = prm.data
+            self.m[k] = fm[off:off + n].view(prm.shape)
+            self.v[k] = fv[off:off + n].view(prm.shape)
+            self.g[k] = self.flat_g[off:off + n].view(prm.shape)
+            if old_m is not None and k in old_m:
+                self.m[k].copy_(old_m[k])
+                self.v[k].copy_(old_v[k])
+            self._span[k] = (off, n)
+            off += n
+        self.flat_p, self.flat_m, self.flat_v = flat, fm, fv
+        self._objs = objs
+        self._bufs = {}
+        self._graphs = {}
+
+    def _check_layout(self) -> None:
+        # model.to() / parameter re-assignment after construction: rebuild the flat layout
+        for k, prm in self._objs.items():
+            if prm.data.data_ptr() != self.params[k].data_ptr():
+                self._flatten()
+                return
+
+    # kept for autograd_ops-style callers
     def _gemm(self, A, W, bias=None, act=0, res=None):
         return self.ops.gemm(A, W, bias, act, res)
 
-    def _kpad(self, k):
-        return self.ops.kpad(k)
+    # ------------------------------------------------------------------ buffers
+    def _key(self, B, S, N, E, Ht, use_cat, has_b, has_c, pdrop):
+        return (B, S, N, E, Ht, use_cat, has_b, has_c, pdrop)
 
-    def _T(self, x, ld=None):
-        return self.ops.T(x, ld)
+    def _alloc(self, key) -> "_Bufs":
+        B, S, N, E, Ht, use_cat, has_b, has_c, pdrop = key
+        dev, f32, bf = self.dev, torch.float32, torch.bfloat16
+        P = self.params
+        b = _Bufs()
+        R = B + B * N
+        C = self.it.categorical_embedding_dim if use_cat else 0
+        width = Ht + 2 * C
+        hid = P["proj0.w"].shape[0]
+        b.R, b.C, b.width, b.hid = R, C, width, hid
+        e = lambda *shape, dt=f32: torch.empty(shape, dtype=dt, device=dev)  # noqa: E731
+        # inputs (static in graph mode)
+        b.items, b.w = e(B, S, E), e(B, S)
+        b.text = e(R, Ht)
+        b.bids = torch.zeros(R, dtype=torch.int32, device=dev) if has_b else None
+        b.cids = torch.zeros(R, dtype=torch.int32, device=dev) if has_c else None
+        bf16 = self.prec == "bf16"
+        b.x = e(R, width)
+        b.x16 = e(R, width, dt=bf) if bf16 else None
+        b.h = e(R, hid)
+        b.h16 = e(R, hid, dt=bf) if bf16 else None
+        b.y, b.z = e(R, E), e(R, E)
+        b.zb = e(B, E)
+        if self.attention:
+            Hd = P["att0.w"].shape[0]
+            b.Hd = Hd
+            b.Hb = e(B * S, Hd)
+            b.X16 = e(B * S, E, dt=bf) if bf16 else None
+            b.alpha, b.onorm = e(B, S), e(B)
+            b.dHb, b.da = e(B * S, Hd), e(B * S)
+        b.loss = torch.empty((), dtype=f32, device=dev)
+        need = ctypes.c_int64(0)
+        check(lib().tt_infonce_workspace_bytes(B, N, E, _lib.TT_PREC_BF16 if bf16 else
+                                               _lib.TT_PREC_F32, 1, ctypes.byref(need)),
+              "tt_infonce_workspace_bytes")
+        b.nce_ws = torch.empty(need.value, dtype=torch.uint8, device=dev)
+        b.gb = e(B, E)
+        b.dz = e(R, E)        # [gp; gn]: InfoNCE writes the item rows' gradient in place
+        b.dy = e(R, E)
+        b.dy16 = e(R, E, dt=bf) if bf16 else None
+        b.dh = e(R, hid)
+        b.dh16 = e(R, hid, dt=bf) if (bf16 and use_cat) else None
+        b.dxc = e(R, 2 * C) if use_cat else None
+        tn = 0
+        for M_, N_, K_ in ((R, E, hid), (R, hid, width)) + (((B * S, b.Hd, E),)
+                                                           if self.attention else ()):
+            v = ctypes.c_int64(0)
+            check(lib().tt_gemm_tn_workspace_bytes(M_, N_, K_, ctypes.byref(v)), "tn ws")
+            tn = max(tn, v.value)
+        b.tn_ws = torch.empty(max(tn, 256), dtype=torch.uint8, device=dev)
+        # weight-derived GEMM operands, refreshed by ONE tt_convert_batch per step
+        W0, W3 = P["proj0.w"], P["proj3.w"]
+        jobs = []
 
-    def _dW(self, dY, X):
-        return self.ops.dW(dY, X)
+        def job(src, rows, cols, ld_src, dst, ld_dst, transpose, to_bf16):
+            jobs.append(_lib.ConvertJob(ctypes.c_void_p(src), ld_src, rows, cols,
+                                        ctypes.c_void_p(dst.data_ptr()), ld_dst, transpose,
+                                        to_bf16))
+        b.W3T = e(hid, E, dt=bf if bf16 else f32)
+        job(W3.data_ptr(), E, hid, hid, b.W3T, E, 1, int(bf16))
+        b.W0cT = e(2 * C, hid, dt=bf if bf16 else f32) if use_cat else None
+        if use_cat:
+            job(W0.data_ptr() + 4 * Ht, hid, 2 * C, width, b.W0cT, hid, 1, int(bf16))
+        if bf16:
+            b.W0_16, b.W3_16 = e(hid, width, dt=bf), e(E, hid, dt=bf)
+            job(W0.data_ptr(), hid, width, width, b.W0_16, width, 0, 1)
+            job(W3.data_ptr(), E, hid, hid, b.W3_16, hid, 0, 1)
+            if self.attention:
+                Wa = P["att0.w"]
+                b.Wa16 = e(b.Hd, E, dt=bf)
+                job(Wa.data_ptr(), b.Hd, E, E, b.Wa16, E, 0, 1)
+                job(b.items.data_ptr(), B * S, E, E, b.X16, E, 0, 1)
+            if not use_cat:
+                job(b.text.data_ptr(), R, Ht, Ht, b.x16, width, 0, 1)
+        b.jobs = (_lib.ConvertJob * len(jobs))(*jobs)
+        b.njobs = len(jobs)
+        return b
 
-    def _colsum(self, x):
-        return self.ops.colsum(x)
+    def input_buffers(self, B, S, N, E=None, Ht=None, use_cat=None, has_b=True, has_c=True):
+        """The static input buffers of a step shape (graph mode): (items [B,S,E], w [B,S],
+        text [B + B N, Ht] = positives then negatives row-major, brand ids [B + B N] int32,
+        cat ids [B + B N] int32).  Write a batch there and call step(...) with the SAME tensors
+        to skip the copies."""
+        E = E or self.params["proj3.w"].shape[0]
+        Ht = Ht or (self.params["proj0.w"].shape[1] - 2 * (self.it.categorical_embedding_dim
+                    if "brand" in self.params else 0))
+        use_cat = "brand" in self.params if use_cat is None else use_cat
+        pdrop = self.it.projection[2].p if self.it.training else 0.0
+        key = self._key(B, S, N, E, Ht, use_cat, has_b and use_cat, has_c and use_cat, pdrop)
+        if key not in self._bufs:
+            self._bufs[key] = self._alloc(key)
+        bb = self._bufs[key]
+        return bb.items, bb.w, bb.text, bb.bids, bb.cids
 
     # ------------------------------------------------------------------ the step
     def forward_loss(self, *args, **kw) -> torch.Tensor:
@@ -162,103 +315,183 @@ class TwoTowerTrainStep:
                          pos_cat=None, neg_brand=None, neg_cat=None, grads: bool = True):
         """buyer_items [B,S,E], weights [B,S], pos_text [B,Ht], neg_text [B,N,Ht] (device f32);
         *_brand / *_cat: int32 id tensors (vocab ids, 0 = <UNK>) or None.
-        Returns (loss tensor, grads dict keyed like self.params; {} when grads=False)."""
+        Returns (loss tensor, grads dict keyed like self.params; {} when grads=False).  The
+        returned tensors are this step shape's buffers: read them before the next call."""
+        self._check_layout()
         P = self.params
         B, S, E = buyer_items.shape
         N = neg_text.shape[1]
         Ht = pos_text.shape[1]
-        R = B + B * N
         use_cat = "brand" in P
-        C = self.it.categorical_embedding_dim if use_cat else 0
-        text = torch.cat([pos_text, neg_text.reshape(B * N, Ht)]).contiguous()
-        width = Ht + 2 * C
-        x = torch.empty((R, width), dtype=torch.float32, device=self.dev)
-        bids = cids = None
-        if use_cat:
-            def ids(a, b_):
-                if a is None and b_ is None:
-                    return None
-                a = a if a is not None else torch.zeros(B, dtype=torch.int32, device=self.dev)
-                b_ = b_ if b_ is not None else torch.zeros(B * N, dtype=torch.int32, device=self.dev)
-                return torch.cat([a.reshape(-1), b_.reshape(-1)]).to(torch.int32).contiguous()
-            bids, cids = ids(pos_brand, neg_brand), ids(pos_cat, neg_cat)
-            check(lib().tt_item_concat(text.data_ptr(), Ht, Ht, _p(bids),
-                                       _p(P["brand"]) if bids is not None else None, _p(cids),
-                                       _p(P["cat"]) if cids is not None else None, C, R,
-                                       x.data_ptr(), width, None, stream_ptr()), "concat")
-        else:
-            x.copy_(text)
-        # item head forward (Linear -> ReLU -> Dropout -> Linear)
-        h = self._gemm(x, P["proj0.w"], P["proj0.b"], _lib.TT_ACT_RELU)
+        has_b = use_cat and (pos_brand is not None or neg_brand is not None)
+        has_c = use_cat and (pos_cat is not None or neg_cat is not None)
         pdrop = self.it.projection[2].p if self.it.training else 0.0
-        keep = self.keep_fn(h.shape, pdrop, self.dev) if pdrop > 0 else None
-        if keep is not None:
-            apply_dropout(h, keep, pdrop)
-        y = self._gemm(h, P["proj3.w"], P["proj3.b"])
-        z = kernels.l2norm_rows(y, E, _lib.TT_NORM_MAX_EPS, out=torch.empty_like(y))
-        w = weights.contiguous().to(torch.float32)
-        if not self.attention:  # weighted average + F.normalize: no trainable parameters
-            zb = kernels.weighted_avg_l2(buyer_items, w)
-        else:  # buyer attention forward
-            X = buyer_items.reshape(B * S, E).contiguous()
-            Hb = self._gemm(X, P["att0.w"], P["att0.b"], _lib.TT_ACT_RELU)
-            Hd = Hb.shape[1]
-            alpha = torch.empty((B, S), dtype=torch.float32, device=self.dev)
-            onorm = torch.empty(B, dtype=torch.float32, device=self.dev)
-            zb = torch.empty((B, E), dtype=torch.float32, device=self.dev)
-            b2 = float(P["att2.b"].item())
-            check(lib().tt_attn_pool_fwd_f32(Hb.data_ptr(), Hd, P["att2.w"].data_ptr(), b2,
-                                             w.data_ptr(), X.data_ptr(), B, S, E,
-                                             alpha.data_ptr(), onorm.data_ptr(), zb.data_ptr(),
-                                             E, stream_ptr()), "attn_pool_fwd")
-        # InfoNCE forward + backward
+        key = self._key(B, S, N, E, Ht, use_cat, has_b, has_c, pdrop)
+        bb = self._bufs.get(key)
+        if bb is None:
+            bb = self._bufs[key] = self._alloc(key)
+        # inputs into the static buffers (no-ops when the caller wrote them in place)
+        bb_R = bb.R
+
+        def put(dst, src):
+            if src is not None and src.data_ptr() != dst.data_ptr():
+                dst.copy_(src.reshape(dst.shape))
+        put(bb.items, buyer_items.to(torch.float32))
+        put(bb.w, weights.to(torch.float32))
+        if pos_text.data_ptr() != bb.text.data_ptr():
+            bb.text[:B].copy_(pos_text)
+            bb.text[B:].copy_(neg_text.reshape(B * N, Ht))
+        for buf, a, c in ((bb.bids, pos_brand, neg_brand), (bb.cids, pos_cat, neg_cat)):
+            if buf is None or (a is not None and a.data_ptr() == buf.data_ptr()):
+                continue
+            if a is not None:
+                buf[:B].copy_(a.reshape(-1))
+            else:
+                buf[:B].zero_()
+            if c is not None:
+                buf[B:].copy_(c.reshape(-1))
+            else:
+                buf[B:].zero_()
+        del bb_R
         if not grads:
-            return infonce(zb, z[:B], z[B:].view(B, N, E), self.tau, self.prec, grads=False)[0], {}
-        loss, (gb, gp, gn) = infonce(zb, z[:B], z[B:].view(B, N, E), self.tau, self.prec)
-        g = {}
-        # item head backward
-        dz = torch.cat([gp, gn.reshape(B * N, E)]).contiguous()
-        dy = torch.empty_like(y)
-        check(lib().tt_l2norm_backward_f32(y.data_ptr(), E, z.data_ptr(), E, dz.data_ptr(), E,
-                                           R, E, dy.data_ptr(), E, stream_ptr()), "norm_bwd")
-        g["proj3.b"] = self._colsum(dy)
-        g["proj3.w"] = self._dW(dy, h)
-        dh = self._gemm(dy, self._T(P["proj3.w"], self._kpad(E)))       # dy W3
-        if keep is not None:  # dropout backward; h is post-dropout (dropped entries 0)
-            apply_dropout(dh, keep, pdrop)
-        check(lib().tt_relu_backward_f32(dh.data_ptr(), h.data_ptr(), dh.numel(), stream_ptr()),
-              "relu_bwd")
-        g["proj0.b"] = self._colsum(dh)
-        g["proj0.w"] = self._dW(dh, x)
+            self._launch(bb, key, grads=False)
+            return bb.loss, {}
+        if self.graph:
+            g = self._graphs.get(key)
+            if g is None:
+                self._launch(bb, key, grads=True)  # eager warm-up (lazy inits, pool sizes)
+                torch.cuda.current_stream().synchronize()
+                g = torch.cuda.CUDAGraph()
+                if self._pool is None:
+                    self._pool = torch.cuda.graph_pool_handle()
+                with torch.cuda.graph(g, pool=self._pool):
+                    self._launch(bb, key, grads=True)
+                self._graphs[key] = g
+            g.replay()
+        else:
+            self._launch(bb, key, grads=True)
+        return bb.loss, {k: self.g[k] for k in P}
+
+    def _launch(self, bb: "_Bufs", key, grads: bool) -> None:
+        B, S, N, E, Ht, use_cat, has_b, has_c, pdrop = key
+        P, L, st = self.params, lib(), stream_ptr()
+        bf16 = self.prec == "bf16"
+        R, C, width, hid = bb.R, bb.C, bb.width, bb.hid
+        # forward: [text | brand | cat] (+ bf16 copy for the bf16 GEMM)
         if use_cat:
-            W0cat = P["proj0.w"][:, Ht:].contiguous()                     # [hid, 2C]
-            dxc = self._gemm(dh, self._T(W0cat, self._kpad(dh.shape[1])))  # [R, 2C]
-            for key, idsv, off in (("brand", bids, 0), ("cat", cids, C)):
-                gt = torch.zeros_like(P[key])
-                if idsv is not None:
-                    check(lib().tt_embedding_backward_f32(dxc[:, off:].data_ptr(), dxc.stride(0),
-                                                          idsv.data_ptr(), R, C, gt.data_ptr(),
-                                                          stream_ptr()), "emb_bwd")
-                g[key] = gt
+            check(L.tt_item_concat(bb.text.data_ptr(), Ht, Ht, _p(bb.bids),
+                                   _p(P["brand"]) if has_b else None, _p(bb.cids),
+                                   _p(P["cat"]) if has_c else None, C, R, bb.x.data_ptr(),
+                                   width, _p(bb.x16), st), "concat")
+            x_in = bb.x
+        else:
+            x_in = bb.text
+        if bb.njobs:
+            check(L.tt_convert_batch(bb.jobs, bb.njobs, st), "convert_batch")
+        keep = self.keep_fn((R, hid), pdrop, self.dev) if pdrop > 0 else None
+        h16 = bb.h16 if keep is None else None
+        if bf16:
+            xa = bb.x16
+            check(L.tt_gemm_bf16(xa.data_ptr(), width, bb.W0_16.data_ptr(), width,
+                                 _p(P["proj0.b"]), None, 0, bb.h.data_ptr(), hid, _p(h16), hid,
+                                 R, hid, width, _lib.TT_ACT_RELU, st), "gemm h")
+        else:
+            check(L.tt_gemm_f32(x_in.data_ptr(), x_in.stride(0), P["proj0.w"].data_ptr(), width,
+                                _p(P["proj0.b"]), None, 0, bb.h.data_ptr(), hid, None, 0, R, hid,
+                                width, _lib.TT_ACT_RELU, st), "gemm h")
+        scale = 1.0
+        if keep is not None:
+            scale = 1.0 / (1.0 - pdrop)
+            check(L.tt_dropout_apply_ex(bb.h.data_ptr(), keep.data_ptr(), scale, bb.h.numel(),
+                                        _p(bb.h16), st), "dropout")
+        if bf16:
+            check(L.tt_gemm_bf16(bb.h16.data_ptr(), hid, bb.W3_16.data_ptr(), hid,
+                                 _p(P["proj3.b"]), None, 0, bb.y.data_ptr(), E, None, 0, R, E,
+                                 hid, 0, st), "gemm y")
+        else:
+            check(L.tt_gemm_f32(bb.h.data_ptr(), hid, P["proj3.w"].data_ptr(), hid,
+                                _p(P["proj3.b"]), None, 0, bb.y.data_ptr(), E, None, 0, R, E,
+                                hid, 0, st), "gemm y")
+        check(L.tt_l2norm_rows_f32(bb.y.data_ptr(), R, E, E, bb.z.data_ptr(), E, None,
+                                   _lib.TT_NORM_MAX_EPS, st), "normalize")
+        X = bb.items.view(B * S, E)
+        if not self.attention:  # weighted average + F.normalize: no trainable parameters
+            check(L.tt_weighted_avg_l2_f32(bb.items.data_ptr(), B, S, E, bb.w.data_ptr(),
+                                           bb.zb.data_ptr(), E, st), "weighted_avg")
+        else:
+            Hd = bb.Hd
+            if bf16:
+                check(L.tt_gemm_bf16(bb.X16.data_ptr(), E, bb.Wa16.data_ptr(), E,
+                                     _p(P["att0.b"]), None, 0, bb.Hb.data_ptr(), Hd, None, 0,
+                                     B * S, Hd, E, _lib.TT_ACT_RELU, st), "gemm att")
+            else:
+                check(L.tt_gemm_f32(X.data_ptr(), E, P["att0.w"].data_ptr(), E, _p(P["att0.b"]),
+                                    None, 0, bb.Hb.data_ptr(), Hd, None, 0, B * S, Hd, E,
+                                    _lib.TT_ACT_RELU, st), "gemm att")
+            check(L.tt_attn_pool_fwd_f32_dev(bb.Hb.data_ptr(), Hd, P["att2.w"].data_ptr(),
+                                             P["att2.b"].data_ptr(), bb.w.data_ptr(),
+                                             X.data_ptr(), B, S, E, bb.alpha.data_ptr(),
+                                             bb.onorm.data_ptr(), bb.zb.data_ptr(), E, st),
+                  "attn_pool_fwd")
+        # InfoNCE forward (+ backward): item-row gradients straight into dz = [gp; gn]
+        pr = _lib.TT_PREC_BF16 if bf16 else _lib.TT_PREC_F32
+        zp, zn = bb.z.data_ptr(), bb.z.data_ptr() + 4 * B * E
+        dzp, dzn = bb.dz.data_ptr(), bb.dz.data_ptr() + 4 * B * E
+        check(L.tt_infonce_f32(bb.zb.data_ptr(), E, zp, E, zn if N else None, N * E, E, B, N, E,
+                               ctypes.c_float(self.tau), pr, bb.loss.data_ptr(),
+                               bb.gb.data_ptr() if grads else None, dzp if grads else None,
+                               (dzn if N else None) if grads else None, bb.nce_ws.data_ptr(),
+                               bb.nce_ws.numel(), st), "tt_infonce_f32")
+        if not grads:
+            return
+        G, ws = self.g, bb.tn_ws
+        # item head backward
+        check(L.tt_l2norm_backward_ex(bb.y.data_ptr(), E, bb.z.data_ptr(), E, dzp, E, R, E,
+                                      bb.dy.data_ptr(), E, _p(bb.dy16), E, st), "norm_bwd")
+        check(L.tt_gemm_tn(bb.dy.data_ptr(), E, bb.h.data_ptr(), hid, R, E, hid, pr,
+                           G["proj3.w"].data_ptr(), hid, G["proj3.b"].data_ptr(), ws.data_ptr(),
+                           ws.numel(), st), "dW3")
+        if bf16:  # dh = dy W3 (A W^T form with W = W3^T)
+            check(L.tt_gemm_bf16(bb.dy16.data_ptr(), E, bb.W3T.data_ptr(), E, None, None, 0,
+                                 bb.dh.data_ptr(), hid, None, 0, R, hid, E, 0, st), "gemm dh")
+        else:
+            check(L.tt_gemm_f32(bb.dy.data_ptr(), E, bb.W3T.data_ptr(), E, None, None, 0,
+                                bb.dh.data_ptr(), hid, None, 0, R, hid, E, 0, st), "gemm dh")
+        check(L.tt_relu_dropout_backward_f32(bb.dh.data_ptr(), bb.h.data_ptr(), scale,
+                                             bb.dh.numel(), _p(bb.dh16), st), "relu_bwd")
+        check(L.tt_gemm_tn(bb.dh.data_ptr(), hid, x_in.data_ptr(), x_in.stride(0), R, hid,
+                           width, pr, G["proj0.w"].data_ptr(), width, G["proj0.b"].data_ptr(),
+                           ws.data_ptr(), ws.numel(), st), "dW0")
+        if use_cat:  # embedding-row gradients through dxc = dh W0[:, Ht:]
+            if bf16:
+                check(L.tt_gemm_bf16(bb.dh16.data_ptr(), hid, bb.W0cT.data_ptr(), hid, None,
+                                     None, 0, bb.dxc.data_ptr(), 2 * C, None, 0, R, 2 * C, hid,
+                                     0, st), "gemm dxc")
+            else:
+                check(L.tt_gemm_f32(bb.dh.data_ptr(), hid, bb.W0cT.data_ptr(), hid, None, None,
+                                    0, bb.dxc.data_ptr(), 2 * C, None, 0, R, 2 * C, hid, 0, st),
+                      "gemm dxc")
+            o0 = self._span["brand"][0]
+            o1 = self._span["cat"][0] + self._span["cat"][1]
+            self.flat_g[o0:o1].zero_()
+            for k_, ids, off in (("brand", bb.bids, 0), ("cat", bb.cids, C)):
+                if ids is not None:
+                    check(L.tt_embedding_backward_f32(bb.dxc.data_ptr() + 4 * off, 2 * C,
+                                                      ids.data_ptr(), R, C,
+                                                      G[k_].data_ptr(), st), "emb_bwd")
         if not self.attention:
-            return loss, g
-        # buyer attention backward
-        dW2 = torch.empty(Hd, dtype=torch.float32, device=self.dev)
-        db2 = torch.empty(1, dtype=torch.float32, device=self.dev)
-        dHb = torch.empty_like(Hb)
-        da = torch.empty(B * S, dtype=torch.float32, device=self.dev)
-        check(lib().tt_attn_pool_bwd_f32(gb.data_ptr(), E, zb.data_ptr(), E, onorm.data_ptr(),
-                                         alpha.data_ptr(), w.data_ptr(), X.data_ptr(), B, S, E,
-                                         Hb.data_ptr(), P["att2.w"].data_ptr(), Hd,
-                                         dW2.data_ptr(), db2.data_ptr(), dHb.data_ptr(),
-                                         da.data_ptr(), stream_ptr()), "attn_pool_bwd")
-        check(lib().tt_relu_backward_f32(dHb.data_ptr(), Hb.data_ptr(), dHb.numel(),
-                                         stream_ptr()), "relu_bwd")
-        g["att2.w"] = dW2.view_as(P["att2.w"])
-        g["att2.b"] = db2.view_as(P["att2.b"])
-        g["att0.b"] = self._colsum(dHb)
-        g["att0.w"] = self._dW(dHb, X)
-        return loss, g
+            return
+        Hd = bb.Hd
+        check(L.tt_attn_pool_bwd_relu_f32(bb.gb.data_ptr(), E, bb.zb.data_ptr(), E,
+                                          bb.onorm.data_ptr(), bb.alpha.data_ptr(),
+                                          bb.w.data_ptr(), X.data_ptr(), B, S, E,
+                                          bb.Hb.data_ptr(), P["att2.w"].data_ptr(), Hd,
+                                          G["att2.w"].data_ptr(), G["att2.b"].data_ptr(),
+                                          bb.dHb.data_ptr(), bb.da.data_ptr(), st),
+              "attn_pool_bwd")
+        check(L.tt_gemm_tn(bb.dHb.data_ptr(), Hd, X.data_ptr(), E, B * S, Hd, E, pr,
+                           G["att0.w"].data_ptr(), E, G["att0.b"].data_ptr(), ws.data_ptr(),
+                           ws.numel(), st), "dWa0")
 
     # torch.optim.Adam state dict (the reference saves optimizer.state_dict(), trainer.py:330):
     # 'state' indexed by the position of the parameter in model.parameters(), 'param_groups'
@@ -319,13 +552,18 @@ class TwoTowerTrainStep:
         self.eps = g.get("eps", self.eps)
 
     def adam(self, grads: Dict[str, torch.Tensor]) -> None:
+        """One Adam launch over the flat parameter / gradient / moment buffers (gradients not
+        already in the flat gradient buffer are copied there first)."""
+        self._check_layout()
         self.t += 1
         b1, b2 = self.betas
-        for k, p in self.params.items():
-            gk = grads[k].contiguous()
-            check(lib().tt_adam_f32(p.data_ptr(), gk.data_ptr(), self.m[k].data_ptr(),
-                                    self.v[k].data_ptr(), p.numel(), self.lr, b1, b2, self.eps,
-                                    self.t, stream_ptr()), "adam")
+        for k in self.params:
+            if grads[k].data_ptr() != self.g[k].data_ptr():
+                self.g[k].copy_(grads[k].reshape(self.g[k].shape))
+        check(lib().tt_adam_f32(self.flat_p.data_ptr(), self.flat_g.data_ptr(),
+                                self.flat_m.data_ptr(), self.flat_v.data_ptr(),
+                                self.flat_p.numel(), self.lr, b1, b2, self.eps, self.t,
+                                stream_ptr()), "adam")
 
     def step(self, *args, group=None, **kw) -> torch.Tensor:
         """One optimiser step.  With an initialised process group (one process per GPU, the
@@ -333,22 +571,28 @@ class TwoTowerTrainStep:
         over ranks before Adam (data parallel, like DistributedDataParallel around the
         reference's model)."""
         loss, g = self.forward_backward(*args, **kw)
-        allreduce_mean(g, group)
+        allreduce_mean(g, group, flat=self.flat_g)
         self.adam(g)
         self.last_loss = loss
         return loss
 
 
-def allreduce_mean(grads: Dict[str, torch.Tensor], group=None) -> None:
+def allreduce_mean(grads: Dict[str, torch.Tensor], group=None, flat: torch.Tensor = None) -> None:
     """Average gradient tensors over the ranks of ``group`` in place with ONE all-reduce of a
     flat bucket (the parameters of the trainable towers are ~0.5 M floats: one RCCL call over
-    xGMI instead of one per tensor).  No-op without an initialised multi-rank group."""
+    xGMI instead of one per tensor).  ``flat``: a buffer the gradients already are views of
+    (TwoTowerTrainStep.flat_g) -- reduced in place, no packing.  No-op without an initialised
+    multi-rank group."""
     import torch.distributed as dist
 
     if not (dist.is_available() and dist.is_initialized()):
         return
     world = dist.get_world_size(group)
     if world == 1:
+        return
+    if flat is not None:
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+        flat.mul_(1.0 / world)
         return
     keys = sorted(grads)  # same order on every rank
     flat = torch.cat([grads[k].reshape(-1) for k in keys])
