@@ -473,11 +473,15 @@ int tt_attn_pool_bwd_f32(const float* dz, int64_t lddz, const float* z, int64_t 
 int tt_embedding_backward_f32(const float* g, int64_t ldg, const int32_t* ids, int64_t n,
                               int32_t C, float* table_grad, void* stream);
 /* tt_attn_pool_fwd_f32 with the bias b2 read from device memory (a step captured in a HIP
- * graph replays without a host read of the parameter). */
+ * graph replays without a host read of the parameter), plus a bf16 copy of z (may be NULL; ld
+ * = ldz) for the bf16 InfoNCE GEMM. */
 int tt_attn_pool_fwd_f32_dev(const float* H, int32_t Hd, const float* W2, const float* b2,
                              const float* w, const float* x, int64_t B, int32_t S, int32_t E,
-                             float* alpha, float* onorm, float* z, int64_t ldz, void* stream);
-/* tt_attn_pool_bwd_f32 with the ReLU backward of H fused into dH (dH = 0 where H <= 0). */
+                             float* alpha, float* onorm, float* z, int64_t ldz, uint16_t* z_bf16,
+                             void* stream);
+/* tt_attn_pool_bwd_f32 with the ReLU backward of H fused into dH (dH = 0 where H <= 0) and
+ * dW2 / db2 ACCUMULATED (atomics) by the same launch: the caller zeroes them first (e.g. a
+ * zero-fill job of the step's tt_convert_batch). */
 int tt_attn_pool_bwd_relu_f32(const float* dz, int64_t lddz, const float* z, int64_t ldz,
                               const float* onorm, const float* alpha, const float* w,
                               const float* x, int64_t B, int32_t S, int32_t E, const float* H,
@@ -494,6 +498,25 @@ int tt_gemm_tn_workspace_bytes(int64_t M, int32_t N, int32_t K, int64_t* bytes);
 int tt_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t N,
                int32_t K, int32_t prec, float* C, int64_t ldc, float* db, void* workspace,
                int64_t workspace_bytes, void* stream);
+/* nn.Dropout forward with the keep mask drawn in the kernel: element i is kept iff
+ * hash(seed, *counter, i) >= p 2^32 (splitmix64, counter-based: a graph-replayed step draws a
+ * fresh mask when the caller advances *counter, a device int64), kept values scaled by
+ * 1/(1-p); plus a bf16 copy (may be NULL).  No mask is stored (the backward is
+ * tt_relu_dropout_backward_f32 on the post-dropout activation). */
+int tt_dropout_rng_f32(float* x, int64_t n, float p, uint64_t seed, const int64_t* counter,
+                       uint16_t* x_bf16, void* stream);
+/* Both item-tower embedding tables' row gradients in one launch: grad0[ids0[r]] += g[r][0:C],
+ * grad1[ids1[r]] += g[r][C:2C] (ids <= 0 skipped; a NULL id array skips its table). */
+int tt_embedding_backward2_f32(const float* g, int64_t ldg, const int32_t* ids0,
+                               const int32_t* ids1, int64_t n, int32_t C, float* grad0,
+                               float* grad1, void* stream);
+/* tt_infonce_f32 with the caller's bf16 copies of b and p (either may be NULL: converted
+ * inside) for the prec = TT_PREC_BF16 logits GEMM. */
+int tt_infonce_ex(const float* b, int64_t ldb, const float* p, int64_t ldp, const float* n,
+                  int64_t ldn_row, int64_t ldn_item, int32_t B, int32_t N, int32_t E,
+                  float temperature, int32_t prec, float* loss, float* grad_b, float* grad_p,
+                  float* grad_n, void* workspace, int64_t workspace_bytes, const uint16_t* b_bf16,
+                  int64_t ldb16, const uint16_t* p_bf16, int64_t ldp16, void* stream);
 /* nn.Dropout forward with a keep mask (tt_dropout_apply_f32) plus a bf16 copy (may be NULL). */
 int tt_dropout_apply_ex(float* x, const uint8_t* keep, float scale, int64_t n, uint16_t* x_bf16,
                         void* stream);
@@ -506,9 +529,10 @@ int tt_l2norm_backward_ex(const float* y, int64_t ldy, const float* z, int64_t l
                           const float* dz, int64_t lddz, int64_t n, int32_t d, float* dy,
                           int64_t lddy, uint16_t* dy_bf16, int64_t lddy16, void* stream);
 /* Batched operand preparation, ONE launch: job j writes src [rows, cols] f32 to dst as f32 or
- * bf16 (to_bf16), transposed (dst [cols, ld_dst], columns rows..ld_dst-1 zero) or not.  The
- * training step's weight-derived GEMM operands (bf16 weights, transposed weights) and bf16
- * copies of its inputs, once per step. */
+ * bf16 (to_bf16), transposed (dst [cols, ld_dst], columns rows..ld_dst-1 zero) or not; src
+ * NULL zero-fills dst [rows, cols] (not transposed).  The training step's weight-derived GEMM
+ * operands (bf16 weights, transposed weights), bf16 copies of its inputs and the zeroing of
+ * its accumulated gradients, once per step. */
 #define TT_CONVERT_MAX_JOBS 8
 typedef struct tt_convert_job {
   const float* src;

@@ -195,11 +195,40 @@ extern "C" int tt_infonce_workspace_bytes(int32_t B, int32_t N, int32_t E, int32
   return TT_OK;
 }
 
+namespace {
+int infonce(const float* b, int64_t ldb, const float* p, int64_t ldp, const float* n,
+            int64_t ldn_row, int64_t ldn_item, int32_t B, int32_t N, int32_t E, float temperature,
+            int32_t prec, float* loss, float* grad_b, float* grad_p, float* grad_n,
+            void* workspace, int64_t workspace_bytes, const uint16_t* b16_in, int64_t ldb16,
+            const uint16_t* p16_in, int64_t ldp16, void* stream);
+}
+
 extern "C" int tt_infonce_f32(const float* b, int64_t ldb, const float* p, int64_t ldp,
                               const float* n, int64_t ldn_row, int64_t ldn_item, int32_t B,
                               int32_t N, int32_t E, float temperature, int32_t prec,
                               float* loss, float* grad_b, float* grad_p, float* grad_n,
                               void* workspace, int64_t workspace_bytes, void* stream) {
+  return infonce(b, ldb, p, ldp, n, ldn_row, ldn_item, B, N, E, temperature, prec, loss, grad_b,
+                 grad_p, grad_n, workspace, workspace_bytes, nullptr, 0, nullptr, 0, stream);
+}
+
+extern "C" int tt_infonce_ex(const float* b, int64_t ldb, const float* p, int64_t ldp,
+                             const float* n, int64_t ldn_row, int64_t ldn_item, int32_t B,
+                             int32_t N, int32_t E, float temperature, int32_t prec, float* loss,
+                             float* grad_b, float* grad_p, float* grad_n, void* workspace,
+                             int64_t workspace_bytes, const uint16_t* b_bf16, int64_t ldb16,
+                             const uint16_t* p_bf16, int64_t ldp16, void* stream) {
+  return infonce(b, ldb, p, ldp, n, ldn_row, ldn_item, B, N, E, temperature, prec, loss, grad_b,
+                 grad_p, grad_n, workspace, workspace_bytes, b_bf16, ldb16, p_bf16, ldp16,
+                 stream);
+}
+
+namespace {
+int infonce(const float* b, int64_t ldb, const float* p, int64_t ldp, const float* n,
+            int64_t ldn_row, int64_t ldn_item, int32_t B, int32_t N, int32_t E, float temperature,
+            int32_t prec, float* loss, float* grad_b, float* grad_p, float* grad_n,
+            void* workspace, int64_t workspace_bytes, const uint16_t* b16_in, int64_t ldb16,
+            const uint16_t* p16_in, int64_t ldp16, void* stream) {
   TT_REQUIRE(B >= 1 && N >= 0 && N <= 64 && E >= 1, "need B >= 1, 0 <= N <= 64, E >= 1");
   TT_REQUIRE(temperature > 0.0f, "temperature must be > 0");
   TT_REQUIRE(prec == TT_PREC_F32 || prec == TT_PREC_BF16, "bad precision");
@@ -216,11 +245,19 @@ extern "C" int tt_infonce_f32(const float* b, int64_t ldb, const float* p, int64
   const int Bp = (B + 63) / 64 * 64;
   int rc;
   // S = b p^T  [B, B]
-  if (bf) {
+  if (bf) {  // bf16 operands: the caller's copies (tt_infonce_ex) or converted here
     const unsigned g = (unsigned)(((int64_t)B * E + 255) / 256 < 4096 ? ((int64_t)B * E + 255) / 256 : 4096);
-    hipLaunchKernelGGL(k_to_bf16, dim3(g), dim3(256), 0, st, b, ldb, B, E, w.b16, (int64_t)E);
-    hipLaunchKernelGGL(k_to_bf16, dim3(g), dim3(256), 0, st, p, ldp, B, E, w.p16, (int64_t)E);
-    rc = tt_gemm_bf16(w.b16, E, w.p16, E, nullptr, nullptr, 0, w.S, B, nullptr, 0, B, B, E, 0, stream);
+    const uint16_t *b16 = b16_in, *p16 = p16_in;
+    if (!b16) {
+      hipLaunchKernelGGL(k_to_bf16, dim3(g), dim3(256), 0, st, b, ldb, B, E, w.b16, (int64_t)E);
+      b16 = w.b16, ldb16 = E;
+    }
+    if (!p16) {
+      hipLaunchKernelGGL(k_to_bf16, dim3(g), dim3(256), 0, st, p, ldp, B, E, w.p16, (int64_t)E);
+      p16 = w.p16, ldp16 = E;
+    }
+    rc = tt_gemm_bf16(b16, ldb16, p16, ldp16, nullptr, nullptr, 0, w.S, B, nullptr, 0, B, B, E, 0,
+                      stream);
   } else {
     rc = tt_gemm_f32(b, ldb, p, ldp, nullptr, nullptr, 0, w.S, B, nullptr, 0, B, B, E, 0, stream);
   }
@@ -243,6 +280,8 @@ extern "C" int tt_infonce_f32(const float* b, int64_t ldb, const float* p, int64
                      grad_b, (int64_t)E, grad_p, (int64_t)E, grad_n, (int64_t)N * E, (int64_t)E);
   return check_launch("k_infonce_grads");
 }
+
+}  // namespace
 
 extern "C" int tt_f32_to_bf16(const float* x, int64_t ldx, int32_t rows, int32_t cols, uint16_t* y,
                               int64_t ldy, void* stream) {

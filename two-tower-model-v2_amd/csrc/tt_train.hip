@@ -19,6 +19,9 @@
 
 namespace tt {
 
+typedef __bf16 tn_bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t tn_u32x2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
@@ -33,6 +36,48 @@ __global__ __launch_bounds__(256) void k_l2norm_bwd(const float* __restrict__ y,
                                                     uint16_t* __restrict__ dy16 = nullptr,
                                                     int64_t lddy16 = 0) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool vec = d % 256 == 0 && d <= 1024 && ldy % 4 == 0 && ldz % 4 == 0 && lddz % 4 == 0 &&
+                   lddy % 4 == 0 && (!dy16 || lddy16 % 4 == 0) && ((uintptr_t)y % 16) == 0 &&
+                   ((uintptr_t)z % 16) == 0 && ((uintptr_t)dz % 16) == 0 &&
+                   ((uintptr_t)dy % 16) == 0 && ((uintptr_t)dy16 % 8) == 0;
+  if (vec) {  // a lane holds 4 consecutive columns per 256: one 16-B load per operand
+    for (int64_t r = (int64_t)blockIdx.x * 4 + w; r < n; r += (int64_t)gridDim.x * 4) {
+      f32x4 zv[4], gv[4];
+      float ss = 0.0f, zd = 0.0f;
+      const int nc = d / 256;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (c >= nc) break;
+        const int e = 256 * c + 4 * lane;
+        const f32x4 yv = *(const f32x4*)(y + r * ldy + e);
+        zv[c] = *(const f32x4*)(z + r * ldz + e);
+        gv[c] = *(const f32x4*)(dz + r * lddz + e);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          ss = fmaf(yv[u], yv[u], ss);
+          zd = fmaf(zv[c][u], gv[c][u], zd);
+        }
+      }
+      ss = wave_sum(ss);
+      zd = wave_sum(zd);
+      const float nrm = sqrtf(ss);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (c >= nc) break;
+        const int e = 256 * c + 4 * lane;
+        f32x4 o;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          o[u] = nrm > 1e-12f ? (gv[c][u] - zv[c][u] * zd) / nrm : gv[c][u] / 1e-12f;
+        *(f32x4*)(dy + r * lddy + e) = o;
+        if (dy16)
+          *(tn_u32x2*)(dy16 + r * lddy16 + e) = tn_u32x2{
+              (uint32_t)f32_to_bf16_rne(o[0]) | ((uint32_t)f32_to_bf16_rne(o[1]) << 16),
+              (uint32_t)f32_to_bf16_rne(o[2]) | ((uint32_t)f32_to_bf16_rne(o[3]) << 16)};
+      }
+    }
+    return;
+  }
   for (int64_t r = (int64_t)blockIdx.x * 4 + w; r < n; r += (int64_t)gridDim.x * 4) {
     float ss = 0.0f, zd = 0.0f;
     for (int e = lane; e < d; e += 64) {
@@ -115,7 +160,7 @@ __global__ __launch_bounds__(256) void k_attn_pool_fwd(
     const float* __restrict__ H, int Hd, const float* __restrict__ W2, float b2,
     const float* __restrict__ b2p, const float* __restrict__ w, const float* __restrict__ x,
     int S, int E, float* __restrict__ alpha, float* __restrict__ onorm, float* __restrict__ z,
-    int64_t ldz) {
+    int64_t ldz, uint16_t* __restrict__ z16 = nullptr) {
   __shared__ float cs[128];
   __shared__ float red[4];
   const int b = blockIdx.x, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
@@ -154,7 +199,10 @@ __global__ __launch_bounds__(256) void k_attn_pool_fwd(
   const float den = fmaxf(nrm, 1e-12f);
   for (int i = 0; i < 4; ++i) {
     const int e = tid + 256 * i;
-    if (e < E) z[(int64_t)b * ldz + e] = ov[i] / den;
+    if (e < E) {
+      z[(int64_t)b * ldz + e] = ov[i] / den;
+      if (z16) z16[(int64_t)b * ldz + e] = f32_to_bf16_rne(ov[i] / den);
+    }
   }
 }
 
@@ -167,11 +215,16 @@ __global__ __launch_bounds__(256) void k_attn_pool_bwd(
     const float* __restrict__ onorm, const float* __restrict__ alpha,
     const float* __restrict__ w, const float* __restrict__ x, int S, int E,
     const float* __restrict__ W2, int Hd, float* __restrict__ da, float* __restrict__ dH,
-    const float* __restrict__ Hmask) {
+    const float* __restrict__ H, bool relu_mask, float* __restrict__ dW2_acc,
+    float* __restrict__ db2_acc) {
   __shared__ float dov[1024];
-  __shared__ float dal[128];
+  __shared__ float dal[128], sal[128], sw[128], sdas[128];
   __shared__ float red[4];
   const int b = blockIdx.x, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  if (tid < S) {  // the buyer's alpha and weights, loaded once (not per position in a loop)
+    sal[tid] = alpha[(int64_t)b * S + tid];
+    sw[tid] = w[(int64_t)b * S + tid];
+  }
   const float nrm = onorm[b];
   float zd = 0.0f;
   for (int e = tid; e < E; e += 256) zd = fmaf(z[(int64_t)b * ldz + e], dz[(int64_t)b * lddz + e], zd);
@@ -193,14 +246,28 @@ __global__ __launch_bounds__(256) void k_attn_pool_bwd(
   }
   __syncthreads();
   float adot = 0.0f;
-  for (int s = 0; s < S; ++s) adot = fmaf(alpha[(int64_t)b * S + s], dal[s], adot);
-  for (int s = 0; s < S; ++s) {
-    const float al = alpha[(int64_t)b * S + s];
-    const float das = al * (dal[s] - adot) * w[(int64_t)b * S + s];
-    if (tid == 0) da[(int64_t)b * S + s] = das;
+  for (int s = 0; s < S; ++s) adot = fmaf(sal[s], dal[s], adot);
+  if (tid < S) {
+    const float das = sal[tid] * (dal[tid] - adot) * sw[tid];
+    sdas[tid] = das;
+    da[(int64_t)b * S + tid] = das;
+  }
+  __syncthreads();
+  const int64_t o0 = (int64_t)b * S * Hd;
+  for (int i = tid; i < S * Hd; i += 256) {  // dH = da W2 (ReLU backward of H fused)
+    const float v = sdas[i / Hd] * W2[i % Hd];
+    dH[o0 + i] = relu_mask && !(H[o0 + i] > 0.0f) ? 0.0f : v;
+  }
+  if (dW2_acc) {  // this buyer's part of dW2 = da^T H and db2 = sum da, accumulated
     for (int j = tid; j < Hd; j += 256) {
-      const int64_t o = ((int64_t)b * S + s) * Hd + j;
-      dH[o] = Hmask && !(Hmask[o] > 0.0f) ? 0.0f : das * W2[j];  // (ReLU backward, fused)
+      float acc = 0.0f;
+      for (int s2 = 0; s2 < S; ++s2) acc = fmaf(sdas[s2], H[o0 + (int64_t)s2 * Hd + j], acc);
+      atomicAdd(dW2_acc + j, acc);
+    }
+    if (tid == 0) {
+      float sd = 0.0f;
+      for (int s2 = 0; s2 < S; ++s2) sd += sdas[s2];
+      atomicAdd(db2_acc, sd);
     }
   }
 }
@@ -275,7 +342,6 @@ unsigned grid_for(int64_t n) {
 // while this chunk's MFMAs run.  BF: operands rounded to bf16 (RNE) in registers,
 // v_mfma_f32_16x16x32_bf16; else v_mfma_f32_16x16x4_f32.  Optional db [N] = column sums of
 // dY (the bias gradient, from the same loads; f32, fixed order).
-typedef __bf16 tn_bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int TN_T = 64;
 constexpr int TN_SMAX = 32;  // row splits per tile
 __host__ __device__ constexpr int tn_pitch(bool bf) { return bf ? 64 + 8 : 64 + 4; }
@@ -492,6 +558,45 @@ __global__ void k_dropout_ex(float* __restrict__ x, const uint8_t* __restrict__ 
   }
 }
 
+// nn.Dropout forward with the keep mask drawn in the kernel: element i of draw c is kept iff
+// u(seed, c, i) >= p * 2^32, u = the high 32 bits of splitmix64(seed + (c << 40) + i) -- a
+// counter-based generator, so a step replayed from a HIP graph draws fresh masks by reading
+// the draw counter c from device memory (the caller advances it each step).  No mask is
+// stored: the backward needs only h > 0 (k_relu_drop_bwd).
+__device__ __forceinline__ uint32_t drop_u32(uint64_t seed, uint64_t c, uint64_t i) {
+  uint64_t zz = seed + (c << 40) + i + 0x9e3779b97f4a7c15ull;
+  zz = (zz ^ (zz >> 30)) * 0xbf58476d1ce4e5b9ull;
+  zz = (zz ^ (zz >> 27)) * 0x94d049bb133111ebull;
+  return (uint32_t)((zz ^ (zz >> 31)) >> 32);
+}
+__global__ void k_dropout_rng(float* __restrict__ x, int64_t n, uint32_t thresh, float scale,
+                              uint64_t seed, const int64_t* __restrict__ ctr,
+                              uint16_t* __restrict__ x16) {
+  const uint64_t c = (uint64_t)*ctr;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = drop_u32(seed, c, (uint64_t)i) >= thresh ? x[i] * scale : 0.0f;
+    x[i] = v;
+    if (x16) x16[i] = f32_to_bf16_rne(v);
+  }
+}
+
+// both embedding tables' row gradients in one launch: blocks [0, n) brand, [n, 2n) category
+__global__ void k_embedding_bwd2(const float* __restrict__ g, int64_t ldg,
+                                 const int32_t* __restrict__ ids0,
+                                 const int32_t* __restrict__ ids1, int64_t n, int C,
+                                 float* __restrict__ grad0, float* __restrict__ grad1) {
+  const bool second = blockIdx.x >= n;
+  const int64_t r = second ? blockIdx.x - n : blockIdx.x;
+  const int32_t* ids = second ? ids1 : ids0;
+  if (ids == nullptr) return;
+  const int id = ids[r];
+  if (id <= 0) return;  // padding_idx 0 gets no gradient
+  float* tg = second ? grad1 : grad0;
+  const float* gr = g + r * ldg + (second ? C : 0);
+  for (int c = threadIdx.x; c < C; c += blockDim.x) atomicAdd(&tg[(int64_t)id * C + c], gr[c]);
+}
+
 // ReLU (+ Dropout) backward on the post-activation h: h > 0 iff the unit was kept and active,
 // so dh = h > 0 ? dh * scale : 0 covers both (scale = 1 / (1 - p), 1 without dropout)
 __global__ void k_relu_drop_bwd(float* __restrict__ dh, const float* __restrict__ h, float scale,
@@ -518,21 +623,47 @@ __global__ __launch_bounds__(256) void k_convert_batch(tt_convert_batch_args a) 
   while (j + 1 < a.njobs && (int)blockIdx.x >= a.tile_off[j + 1]) ++j;
   const tt_convert_job& jb = a.jobs[j];
   const int t = (int)blockIdx.x - a.tile_off[j];
-  const int rr = jb.transpose ? (int)(jb.ld_dst > jb.rows ? jb.ld_dst : jb.rows) : jb.rows;
-  const int ct = (jb.cols + 31) / 32;
-  const int r0 = (t / ct) * 32, c0 = (t % ct) * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  if (!jb.transpose) {
-    for (int y = ty; y < 32; y += 8) {
-      const int r = r0 + y, c = c0 + tx;
-      if (r < jb.rows && c < jb.cols) {
-        const float v = jb.src[(int64_t)r * jb.ld_src + c];
-        if (jb.to_bf16) ((uint16_t*)jb.dst)[(int64_t)r * jb.ld_dst + c] = f32_to_bf16_rne(v);
-        else ((float*)jb.dst)[(int64_t)r * jb.ld_dst + c] = v;
+  if (!jb.transpose) {  // 8 x 128 tiles, 4 consecutive elements per thread
+    const int ct = (jb.cols + 127) / 128;
+    const int r = (t / ct) * 8 + ty, c = (t % ct) * 128 + 4 * tx;
+    if (r >= jb.rows || c >= jb.cols) return;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    const bool full = c + 4 <= jb.cols;
+    if (jb.src) {
+      const float* sp = jb.src + (int64_t)r * jb.ld_src + c;
+      if (full && ((uintptr_t)sp % 16) == 0) {
+        const f32x4 q = *(const f32x4*)sp;
+        v[0] = q[0], v[1] = q[1], v[2] = q[2], v[3] = q[3];
+      } else {
+        for (int u = 0; u < 4; ++u)
+          if (c + u < jb.cols) v[u] = sp[u];
+      }
+    }
+    if (jb.to_bf16) {
+      uint16_t* dp = (uint16_t*)jb.dst + (int64_t)r * jb.ld_dst + c;
+      if (full && ((uintptr_t)dp % 8) == 0) {
+        *(tn_u32x2*)dp = tn_u32x2{
+            (uint32_t)f32_to_bf16_rne(v[0]) | ((uint32_t)f32_to_bf16_rne(v[1]) << 16),
+            (uint32_t)f32_to_bf16_rne(v[2]) | ((uint32_t)f32_to_bf16_rne(v[3]) << 16)};
+      } else {
+        for (int u = 0; u < 4; ++u)
+          if (c + u < jb.cols) dp[u] = f32_to_bf16_rne(v[u]);
+      }
+    } else {
+      float* dp = (float*)jb.dst + (int64_t)r * jb.ld_dst + c;
+      if (full && ((uintptr_t)dp % 16) == 0) {
+        *(f32x4*)dp = f32x4{v[0], v[1], v[2], v[3]};
+      } else {
+        for (int u = 0; u < 4; ++u)
+          if (c + u < jb.cols) dp[u] = v[u];
       }
     }
     return;
   }
+  const int rr = (int)(jb.ld_dst > jb.rows ? jb.ld_dst : jb.rows);
+  const int ct = (jb.cols + 31) / 32;
+  const int r0 = (t / ct) * 32, c0 = (t % ct) * 32;
   __shared__ float tl[32][33];
   for (int y = ty; y < 32; y += 8) {
     const int r = r0 + y, c = c0 + tx;
@@ -623,13 +754,13 @@ extern "C" int tt_attn_pool_fwd_f32(const float* H, int32_t Hd, const float* W2,
 extern "C" int tt_attn_pool_fwd_f32_dev(const float* H, int32_t Hd, const float* W2,
                                         const float* b2, const float* w, const float* x, int64_t B,
                                         int32_t S, int32_t E, float* alpha, float* onorm, float* z,
-                                        int64_t ldz, void* stream) {
+                                        int64_t ldz, uint16_t* z_bf16, void* stream) {
   TT_REQUIRE(B >= 0 && S >= 1 && S <= 128 && E >= 1 && E <= 1024 && Hd >= 1,
              "need 1 <= S <= 128, 1 <= E <= 1024");
   if (B == 0) return TT_OK;
   TT_REQUIRE(H && W2 && b2 && w && x && alpha && onorm && z, "null pointer");
   hipLaunchKernelGGL(k_attn_pool_fwd, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, H, Hd,
-                     W2, 0.0f, b2, w, x, S, E, alpha, onorm, z, ldz);
+                     W2, 0.0f, b2, w, x, S, E, alpha, onorm, z, ldz, z_bf16);
   return check_launch("tt_attn_pool_fwd_f32_dev");
 }
 
@@ -637,7 +768,7 @@ namespace {
 int attn_pool_bwd(const float* dz, int64_t lddz, const float* z, int64_t ldz, const float* onorm,
                   const float* alpha, const float* w, const float* x, int64_t B, int32_t S,
                   int32_t E, const float* H, const float* W2, int32_t Hd, float* dW2, float* db2,
-                  float* dH, float* da_ws, bool relu_mask, void* stream) {
+                  float* dH, float* da_ws, bool relu_mask, bool fused, void* stream) {
   TT_REQUIRE(B >= 0 && S >= 1 && S <= 128 && E >= 1 && E <= 1024 && Hd >= 1,
              "need 1 <= S <= 128, 1 <= E <= 1024");
   if (B == 0) return TT_OK;
@@ -645,10 +776,10 @@ int attn_pool_bwd(const float* dz, int64_t lddz, const float* z, int64_t ldz, co
              "null pointer");
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_attn_pool_bwd, dim3((unsigned)B), dim3(256), 0, st, dz, lddz, z, ldz,
-                     onorm, alpha, w, x, S, E, W2, Hd, da_ws, dH,
-                     relu_mask ? H : (const float*)nullptr);
+                     onorm, alpha, w, x, S, E, W2, Hd, da_ws, dH, H, relu_mask,
+                     fused ? dW2 : (float*)nullptr, fused ? db2 : (float*)nullptr);
   int rc = check_launch("k_attn_pool_bwd");
-  if (rc) return rc;
+  if (rc || fused) return rc;
   if (hipMemsetAsync(dW2, 0, (size_t)Hd * 4, st) != hipSuccess ||
       hipMemsetAsync(db2, 0, 4, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "tt_attn_pool_bwd_f32: hipMemsetAsync");
@@ -666,7 +797,7 @@ extern "C" int tt_attn_pool_bwd_f32(const float* dz, int64_t lddz, const float* 
                                     const float* H, const float* W2, int32_t Hd, float* dW2,
                                     float* db2, float* dH, float* da_ws, void* stream) {
   return attn_pool_bwd(dz, lddz, z, ldz, onorm, alpha, w, x, B, S, E, H, W2, Hd, dW2, db2, dH,
-                       da_ws, false, stream);
+                       da_ws, false, false, stream);
 }
 
 extern "C" int tt_attn_pool_bwd_relu_f32(const float* dz, int64_t lddz, const float* z,
@@ -676,7 +807,7 @@ extern "C" int tt_attn_pool_bwd_relu_f32(const float* dz, int64_t lddz, const fl
                                          float* dW2, float* db2, float* dH, float* da_ws,
                                          void* stream) {
   return attn_pool_bwd(dz, lddz, z, ldz, onorm, alpha, w, x, B, S, E, H, W2, Hd, dW2, db2, dH,
-                       da_ws, true, stream);
+                       da_ws, true, true, stream);
 }
 
 extern "C" int tt_embedding_backward_f32(const float* g, int64_t ldg, const int32_t* ids,
@@ -743,6 +874,29 @@ extern "C" int tt_dropout_apply_ex(float* x, const uint8_t* keep, float scale, i
   return check_launch("tt_dropout_apply_ex");
 }
 
+extern "C" int tt_dropout_rng_f32(float* x, int64_t n, float p, uint64_t seed,
+                                  const int64_t* counter, uint16_t* x_bf16, void* stream) {
+  TT_REQUIRE(n >= 0 && p >= 0.0f && p < 1.0f, "need n >= 0, 0 <= p < 1");
+  if (n == 0) return TT_OK;
+  TT_REQUIRE(x && counter, "null pointer");
+  const double th = (double)p * 4294967296.0;
+  const uint32_t thresh = th >= 4294967295.0 ? 0xffffffffu : (uint32_t)th;
+  hipLaunchKernelGGL(k_dropout_rng, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, n,
+                     thresh, 1.0f / (1.0f - p), seed, counter, x_bf16);
+  return check_launch("tt_dropout_rng_f32");
+}
+
+extern "C" int tt_embedding_backward2_f32(const float* g, int64_t ldg, const int32_t* ids0,
+                                          const int32_t* ids1, int64_t n, int32_t C,
+                                          float* grad0, float* grad1, void* stream) {
+  TT_REQUIRE(n >= 0 && C >= 1, "bad sizes");
+  if (n == 0 || (!ids0 && !ids1)) return TT_OK;
+  TT_REQUIRE(g && (!ids0 || grad0) && (!ids1 || grad1) && ldg >= 2 * C, "null pointer / ldg");
+  hipLaunchKernelGGL(k_embedding_bwd2, dim3((unsigned)(2 * n)), dim3(64), 0, (hipStream_t)stream,
+                     g, ldg, ids0, ids1, n, C, grad0, grad1);
+  return check_launch("tt_embedding_backward2_f32");
+}
+
 extern "C" int tt_relu_dropout_backward_f32(float* dh, const float* h, float scale, int64_t n,
                                             uint16_t* dh_bf16, void* stream) {
   TT_REQUIRE(n >= 0, "n < 0");
@@ -759,14 +913,19 @@ extern "C" int tt_convert_batch(const tt_convert_job* jobs, int32_t njobs, void*
   int tiles = 0, nj = 0;
   for (int j = 0; j < njobs; ++j) {
     const tt_convert_job& jb = jobs[j];
-    TT_REQUIRE(jb.src && jb.dst && jb.rows >= 0 && jb.cols >= 0 && jb.ld_src >= jb.cols,
+    TT_REQUIRE(jb.dst && jb.rows >= 0 && jb.cols >= 0 && (!jb.src || jb.ld_src >= jb.cols),
                "bad job");
+    TT_REQUIRE(jb.src || !jb.transpose, "a zero-fill job (src NULL) cannot transpose");
     TT_REQUIRE(jb.transpose ? jb.ld_dst >= jb.rows : jb.ld_dst >= jb.cols, "bad job ld_dst");
     if (jb.rows == 0 || jb.cols == 0) continue;
-    const int64_t rr = jb.transpose && jb.ld_dst > jb.rows ? jb.ld_dst : jb.rows;
     a.jobs[nj] = jb;
     a.tile_off[nj] = tiles;
-    tiles += (int)(((rr + 31) / 32) * ((jb.cols + 31) / 32));
+    if (jb.transpose) {
+      const int64_t rr = jb.ld_dst > jb.rows ? jb.ld_dst : jb.rows;
+      tiles += (int)(((rr + 31) / 32) * ((jb.cols + 31) / 32));
+    } else {
+      tiles += (int)(((jb.rows + 7) / 8) * ((jb.cols + 127) / 128));
+    }
     ++nj;
   }
   a.njobs = nj;

@@ -164,7 +164,14 @@ SIGNATURES = {
                                    ctypes.c_float, ctypes.c_float, _i32, _vp]),
     "tt_f32_to_bf16": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _i64, _vp]),
     "tt_attn_pool_fwd_f32_dev": (ctypes.c_int, [_vp, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32,
-                                                _vp, _vp, _vp, _i64, _vp]),
+                                                _vp, _vp, _vp, _i64, _vp, _vp]),
+    "tt_dropout_rng_f32": (ctypes.c_int, [_vp, _i64, ctypes.c_float, ctypes.c_uint64, _vp, _vp,
+                                          _vp]),
+    "tt_embedding_backward2_f32": (ctypes.c_int, [_vp, _i64, _vp, _vp, _i64, _i32, _vp, _vp,
+                                                  _vp]),
+    "tt_infonce_ex": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32,
+                                     ctypes.c_float, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
+                                     _i64, _vp, _i64, _vp]),
     "tt_attn_pool_bwd_relu_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i64,
                                                  _i32, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _vp,
                                                  _vp]),

@@ -148,6 +148,10 @@ class TwoTowerTrainStep:
         # in train mode, as under the reference Trainer (model.train(), trainer.py:167)
         self.keep_fn = dropout_keep
         self.graph = graph
+        # projection dropout drawn in-kernel (tt_dropout_rng_f32) from (seed, draw counter): the
+        # counter lives on the device and advances every step, so graph replays draw new masks
+        self._drop_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        self._drop_ctr = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self._bufs = {}    # shape key -> _Bufs
         self._graphs = {}  # shape key -> torch.cuda.CUDAGraph (graph=True)
         self._pool = None
@@ -234,6 +238,8 @@ class TwoTowerTrainStep:
         b.h16 = e(R, hid, dt=bf) if bf16 else None
         b.y, b.z = e(R, E), e(R, E)
         b.zb = e(B, E)
+        b.z16 = e(R, E, dt=bf) if bf16 else None  # the bf16 InfoNCE GEMM's operand copies
+        b.zb16 = e(B, E, dt=bf) if (bf16 and self.attention) else None
         if self.attention:
             Hd = P["att0.w"].shape[0]
             b.Hd = Hd
@@ -285,6 +291,15 @@ class TwoTowerTrainStep:
                 job(b.items.data_ptr(), B * S, E, E, b.X16, E, 0, 1)
             if not use_cat:
                 job(b.text.data_ptr(), R, Ht, Ht, b.x16, width, 0, 1)
+        # gradients the step accumulates with atomics, zeroed by the same launch
+        if use_cat:
+            o0, o1 = self._span["brand"][0], self._span["cat"][0] + self._span["cat"][1]
+            jobs.append(_lib.ConvertJob(None, 0, 1, o1 - o0, ctypes.c_void_p(
+                self.flat_g.data_ptr() + 4 * o0), o1 - o0, 0, 0))
+        if self.attention:
+            o0, o1 = self._span["att2.w"][0], self._span["att2.b"][0] + self._span["att2.b"][1]
+            jobs.append(_lib.ConvertJob(None, 0, 1, o1 - o0, ctypes.c_void_p(
+                self.flat_g.data_ptr() + 4 * o0), o1 - o0, 0, 0))
         b.jobs = (_lib.ConvertJob * len(jobs))(*jobs)
         b.njobs = len(jobs)
         return b
@@ -388,8 +403,9 @@ class TwoTowerTrainStep:
             x_in = bb.text
         if bb.njobs:
             check(L.tt_convert_batch(bb.jobs, bb.njobs, st), "convert_batch")
-        keep = self.keep_fn((R, hid), pdrop, self.dev) if pdrop > 0 else None
-        h16 = bb.h16 if keep is None else None
+        rng_drop = pdrop > 0 and self.keep_fn is dropout_keep  # (a custom keep_fn: its mask)
+        keep = self.keep_fn((R, hid), pdrop, self.dev) if pdrop > 0 and not rng_drop else None
+        h16 = bb.h16 if pdrop == 0 else None
         if bf16:
             xa = bb.x16
             check(L.tt_gemm_bf16(xa.data_ptr(), width, bb.W0_16.data_ptr(), width,
@@ -400,7 +416,13 @@ class TwoTowerTrainStep:
                                 _p(P["proj0.b"]), None, 0, bb.h.data_ptr(), hid, None, 0, R, hid,
                                 width, _lib.TT_ACT_RELU, st), "gemm h")
         scale = 1.0
-        if keep is not None:
+        if rng_drop:
+            scale = 1.0 / (1.0 - pdrop)
+            check(L.tt_dropout_rng_f32(bb.h.data_ptr(), bb.h.numel(), ctypes.c_float(pdrop),
+                                       self._drop_seed, self._drop_ctr.data_ptr(), _p(bb.h16),
+                                       st), "dropout")
+            self._drop_ctr.add_(1)
+        elif keep is not None:
             scale = 1.0 / (1.0 - pdrop)
             check(L.tt_dropout_apply_ex(bb.h.data_ptr(), keep.data_ptr(), scale, bb.h.numel(),
                                         _p(bb.h16), st), "dropout")
@@ -412,7 +434,7 @@ class TwoTowerTrainStep:
             check(L.tt_gemm_f32(bb.h.data_ptr(), hid, P["proj3.w"].data_ptr(), hid,
                                 _p(P["proj3.b"]), None, 0, bb.y.data_ptr(), E, None, 0, R, E,
                                 hid, 0, st), "gemm y")
-        check(L.tt_l2norm_rows_f32(bb.y.data_ptr(), R, E, E, bb.z.data_ptr(), E, None,
+        check(L.tt_l2norm_rows_f32(bb.y.data_ptr(), R, E, E, bb.z.data_ptr(), E, _p(bb.z16),
                                    _lib.TT_NORM_MAX_EPS, st), "normalize")
         X = bb.items.view(B * S, E)
         if not self.attention:  # weighted average + F.normalize: no trainable parameters
@@ -431,17 +453,18 @@ class TwoTowerTrainStep:
             check(L.tt_attn_pool_fwd_f32_dev(bb.Hb.data_ptr(), Hd, P["att2.w"].data_ptr(),
                                              P["att2.b"].data_ptr(), bb.w.data_ptr(),
                                              X.data_ptr(), B, S, E, bb.alpha.data_ptr(),
-                                             bb.onorm.data_ptr(), bb.zb.data_ptr(), E, st),
-                  "attn_pool_fwd")
+                                             bb.onorm.data_ptr(), bb.zb.data_ptr(), E,
+                                             _p(bb.zb16), st), "attn_pool_fwd")
         # InfoNCE forward (+ backward): item-row gradients straight into dz = [gp; gn]
         pr = _lib.TT_PREC_BF16 if bf16 else _lib.TT_PREC_F32
         zp, zn = bb.z.data_ptr(), bb.z.data_ptr() + 4 * B * E
         dzp, dzn = bb.dz.data_ptr(), bb.dz.data_ptr() + 4 * B * E
-        check(L.tt_infonce_f32(bb.zb.data_ptr(), E, zp, E, zn if N else None, N * E, E, B, N, E,
-                               ctypes.c_float(self.tau), pr, bb.loss.data_ptr(),
-                               bb.gb.data_ptr() if grads else None, dzp if grads else None,
-                               (dzn if N else None) if grads else None, bb.nce_ws.data_ptr(),
-                               bb.nce_ws.numel(), st), "tt_infonce_f32")
+        check(L.tt_infonce_ex(bb.zb.data_ptr(), E, zp, E, zn if N else None, N * E, E, B, N, E,
+                              ctypes.c_float(self.tau), pr, bb.loss.data_ptr(),
+                              bb.gb.data_ptr() if grads else None, dzp if grads else None,
+                              (dzn if N else None) if grads else None, bb.nce_ws.data_ptr(),
+                              bb.nce_ws.numel(), _p(bb.zb16), E, _p(bb.z16), E, st),
+              "tt_infonce_ex")
         if not grads:
             return
         G, ws = self.g, bb.tn_ws
@@ -471,14 +494,10 @@ class TwoTowerTrainStep:
                 check(L.tt_gemm_f32(bb.dh.data_ptr(), hid, bb.W0cT.data_ptr(), hid, None, None,
                                     0, bb.dxc.data_ptr(), 2 * C, None, 0, R, 2 * C, hid, 0, st),
                       "gemm dxc")
-            o0 = self._span["brand"][0]
-            o1 = self._span["cat"][0] + self._span["cat"][1]
-            self.flat_g[o0:o1].zero_()
-            for k_, ids, off in (("brand", bb.bids, 0), ("cat", bb.cids, C)):
-                if ids is not None:
-                    check(L.tt_embedding_backward_f32(bb.dxc.data_ptr() + 4 * off, 2 * C,
-                                                      ids.data_ptr(), R, C,
-                                                      G[k_].data_ptr(), st), "emb_bwd")
+            # (brand / cat gradients zeroed by the step's tt_convert_batch)
+            check(L.tt_embedding_backward2_f32(bb.dxc.data_ptr(), 2 * C, _p(bb.bids), _p(bb.cids),
+                                               R, C, G["brand"].data_ptr(), G["cat"].data_ptr(),
+                                               st), "emb_bwd")
         if not self.attention:
             return
         Hd = bb.Hd
