@@ -480,8 +480,8 @@ int tt_attn_pool_fwd_f32_dev(const float* H, int32_t Hd, const float* W2, const 
                              float* alpha, float* onorm, float* z, int64_t ldz, uint16_t* z_bf16,
                              void* stream);
 /* tt_attn_pool_bwd_f32 with the ReLU backward of H fused into dH (dH = 0 where H <= 0) and
- * dW2 / db2 ACCUMULATED (atomics) by the same launch: the caller zeroes them first (e.g. a
- * zero-fill job of the step's tt_convert_batch). */
+ * dW2 / db2 from per-buyer parts summed in a fixed order by a second launch (deterministic, no
+ * atomics, no memsets).  da_ws holds B*S + 64 + B*(Hd+1) floats (da, then the parts). */
 int tt_attn_pool_bwd_relu_f32(const float* dz, int64_t lddz, const float* z, int64_t ldz,
                               const float* onorm, const float* alpha, const float* w,
                               const float* x, int64_t B, int32_t S, int32_t E, const float* H,
@@ -521,9 +521,11 @@ int tt_infonce_ex(const float* b, int64_t ldb, const float* p, int64_t ldp, cons
 int tt_dropout_apply_ex(float* x, const uint8_t* keep, float scale, int64_t n, uint16_t* x_bf16,
                         void* stream);
 /* ReLU (+ Dropout) backward on the post-activation h: dh = h > 0 ? dh * scale : 0 (scale =
- * 1/(1-p) with dropout, 1 without), plus a bf16 copy (may be NULL). */
+ * 1/(1-p) with dropout, 1 without), plus a bf16 copy (may be NULL).  counter_advance (may be
+ * NULL): a tt_dropout_rng_f32 draw counter this launch increments by one (the step's last use
+ * of the mask is its forward, so the next step draws a new one). */
 int tt_relu_dropout_backward_f32(float* dh, const float* h, float scale, int64_t n,
-                                 uint16_t* dh_bf16, void* stream);
+                                 uint16_t* dh_bf16, int64_t* counter_advance, void* stream);
 /* tt_l2norm_backward_f32 plus a bf16 copy of dy (may be NULL). */
 int tt_l2norm_backward_ex(const float* y, int64_t ldy, const float* z, int64_t ldz,
                           const float* dz, int64_t lddz, int64_t n, int32_t d, float* dy,

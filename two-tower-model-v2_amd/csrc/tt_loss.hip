@@ -74,14 +74,34 @@ __global__ __launch_bounds__(256) void k_infonce_rows(
   __shared__ float lg[1 + 64];  // positive + up to 64 explicit negatives
   const int i = blockIdx.x, tid = threadIdx.x;
   const float* bi = b + (int64_t)i * ldb;
-  for (int j = 0; j <= N; ++j) {
-    const float* y = j == 0 ? p + (int64_t)i * ldp_in : n + (int64_t)i * ldn_row + (int64_t)(j - 1) * ldn_item;
-    float s = 0.0f;
-    for (int e = tid; e < E; e += 256) s = fmaf(bi[e], y[e], s);
-    s = block_sum(s, red);
-    if (tid == 0) lg[j] = s * inv_tau;
+  // the positive and the explicit negatives' logits, 8 dot products per pass (one reduction
+  // round for all 8: their loads in flight together)
+  __shared__ float red8[8][8];
+  for (int j0 = 0; j0 <= N; j0 += 8) {
+    float sv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + u;
+      float acc = 0.0f;
+      if (j <= N) {
+        const float* y = j == 0 ? p + (int64_t)i * ldp_in
+                                : n + (int64_t)i * ldn_row + (int64_t)(j - 1) * ldn_item;
+        for (int e = tid; e < E; e += 256) acc = fmaf(bi[e], y[e], acc);
+      }
+      for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+      sv[u] = acc;
+    }
+    if ((tid & 63) == 0)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) red8[tid >> 6][u] = sv[u];
+    __syncthreads();
+    if (tid < 8 && j0 + tid <= N) {
+      float t = 0.0f;
+      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red8[w][tid];
+      lg[j0 + tid] = t * inv_tau;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   const float* Si = S + (int64_t)i * lds;
   float mx = -__builtin_huge_valf();
   for (int j = tid; j <= N; j += 256) mx = fmaxf(mx, lg[j]);
@@ -124,8 +144,15 @@ __global__ __launch_bounds__(256) void k_infonce_grads(
     const float* __restrict__ P0, const float* __restrict__ Pn, const float* __restrict__ G1,
     const float* __restrict__ G2, int64_t ldg, float* __restrict__ gb, int64_t ldgb,
     float* __restrict__ gp, int64_t ldgp, float* __restrict__ gn, int64_t ldgn_row,
-    int64_t ldgn_item) {
+    int64_t ldgn_item, const float* __restrict__ row_loss, float* __restrict__ loss) {
   const int i = blockIdx.x;
+  if (i == 0 && loss) {  // the mean loss (k_mean's sum, in the same order), no launch of its own
+    __shared__ float red[8];
+    float sl = 0.0f;
+    for (int r = threadIdx.x; r < B; r += 256) sl += row_loss[r];
+    sl = block_sum(sl, red);
+    if (threadIdx.x == 0) *loss = sl / (float)B;
+  }
   const float a0 = P0[i] - 1.0f;
   const float* bi = b + (int64_t)i * ldb;
   const float* pi = p + (int64_t)i * ldp_in;
@@ -267,9 +294,10 @@ int infonce(const float* b, int64_t ldb, const float* p, int64_t ldp, const floa
                      N > 0 ? w.Pn : nullptr, w.Pb, w.PbT, (uint16_t*)nullptr,
                      (uint16_t*)nullptr, Bp);
   if ((rc = check_launch("k_infonce_rows"))) return rc;
-  hipLaunchKernelGGL(k_mean, dim3(1), dim3(256), 0, st, w.row_loss, B, loss);
-  if ((rc = check_launch("k_mean"))) return rc;
-  if (!grads) return TT_OK;
+  if (!grads) {
+    hipLaunchKernelGGL(k_mean, dim3(1), dim3(256), 0, st, w.row_loss, B, loss);
+    return check_launch("k_mean");
+  }
   // G1 = Pb . p = (Pb^T)^T p;  G2 = Pb^T . b   (row-major Pb^T / Pb as the A^T operands)
   rc = tt_gemm_tn(w.PbT, Bp, p, ldp, B, B, E, prec, w.G1, E, nullptr, w.tn, w.tn_bytes, stream);
   if (!rc)
@@ -277,7 +305,8 @@ int infonce(const float* b, int64_t ldb, const float* p, int64_t ldp, const floa
   if (rc) return rc;
   hipLaunchKernelGGL(k_infonce_grads, dim3(B), dim3(256), 0, st, b, ldb, p, ldp, n, ldn_row,
                      ldn_item, B, N, E, inv_tau / (float)B, w.P0, w.Pn, w.G1, w.G2, (int64_t)E,
-                     grad_b, (int64_t)E, grad_p, (int64_t)E, grad_n, (int64_t)N * E, (int64_t)E);
+                     grad_b, (int64_t)E, grad_p, (int64_t)E, grad_n, (int64_t)N * E, (int64_t)E,
+                     w.row_loss, loss);
   return check_launch("k_infonce_grads");
 }
 

@@ -156,21 +156,30 @@ __global__ void k_dropout(float* __restrict__ x, const uint8_t* __restrict__ kee
 // Attention pooling, one block per buyer (S <= 128, hidden Hd <= 256, E <= 1024):
 //   a_s = H_s . W2 + b2 ; c_s = a_s * w_s ; alpha = softmax(c) ; o = sum_s alpha_s x_s ;
 //   z = o / max(||o||, 1e-12).  Saves alpha [B, S] and ||o|| [B] for the backward.
-__global__ __launch_bounds__(256) void k_attn_pool_fwd(
+template <int NT>
+__global__ __launch_bounds__(NT) void k_attn_pool_fwd(
     const float* __restrict__ H, int Hd, const float* __restrict__ W2, float b2,
     const float* __restrict__ b2p, const float* __restrict__ w, const float* __restrict__ x,
     int S, int E, float* __restrict__ alpha, float* __restrict__ onorm, float* __restrict__ z,
     int64_t ldz, uint16_t* __restrict__ z16 = nullptr) {
-  __shared__ float cs[128];
-  __shared__ float red[4];
+  constexpr int NW = NT / 64, PER = (1024 + NT - 1) / NT;
+  __shared__ float cs[128], pal[128];
+  __shared__ float red[NW];
   const int b = blockIdx.x, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   if (b2p) b2 = *b2p;  // the bias read on the device (a graph-captured step: no host sync)
-  for (int s = wv; s < S; s += 4) {  // wave per position
-    const float* h = H + ((int64_t)b * S + s) * Hd;
+  // a_s = H_s . W2: 16 lanes per position, 16 positions per pass (the loads of all positions
+  // in flight together; was one wave per position, five dependent rounds per wave)
+  const int pl = tid & 15, pg = tid >> 4;
+  for (int s0 = 0; s0 < S; s0 += NT / 16) {
+    const int s = s0 + pg;
     float a = 0.0f;
-    for (int j = lane; j < Hd; j += 64) a = fmaf(h[j], W2[j], a);
-    a = wave_sum(a);
-    if (lane == 0) cs[s] = (a + b2) * w[(int64_t)b * S + s];
+    if (s < S) {
+      const float* h = H + ((int64_t)b * S + s) * Hd;
+      for (int j = pl; j < Hd; j += 16) a = fmaf(h[j], W2[j], a);
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) a += __shfl_xor(a, o, 16);
+    if (pl == 0 && s < S) cs[s] = (a + b2) * w[(int64_t)b * S + s];
   }
   __syncthreads();
   float m = -__builtin_huge_valf();
@@ -178,27 +187,37 @@ __global__ __launch_bounds__(256) void k_attn_pool_fwd(
   float sum = 0.0f;
   for (int s = 0; s < S; ++s) sum += expf(cs[s] - m);
   const float inv = 1.0f / sum;
-  if (tid < S) alpha[(int64_t)b * S + tid] = expf(cs[tid] - m) * inv;
+  if (tid < S) {
+    const float al = expf(cs[tid] - m) * inv;
+    pal[tid] = al;
+    alpha[(int64_t)b * S + tid] = al;
+  }
+  __syncthreads();
   // o = sum alpha x ; ||o||
   const float* xb = x + (int64_t)b * S * E;
   float ss = 0.0f;
-  float ov[4];
-  for (int i = 0; i < 4; ++i) {
-    const int e = tid + 256 * i;
+  float ov[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = tid + NT * i;
     float o = 0.0f;
     if (e < E)
-      for (int s = 0; s < S; ++s) o = fmaf(expf(cs[s] - m) * inv, xb[(int64_t)s * E + e], o);
+      for (int s = 0; s < S; ++s) o = fmaf(pal[s], xb[(int64_t)s * E + e], o);
     ov[i] = o;
     ss = fmaf(o, o, ss);
   }
   ss = wave_sum(ss);
   if (lane == 0) red[wv] = ss;
   __syncthreads();
-  const float nrm = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
+  float ssum = 0.0f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) ssum += red[i];
+  const float nrm = sqrtf(ssum);
   if (tid == 0) onorm[b] = nrm;
   const float den = fmaxf(nrm, 1e-12f);
-  for (int i = 0; i < 4; ++i) {
-    const int e = tid + 256 * i;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = tid + NT * i;
     if (e < E) {
       z[(int64_t)b * ldz + e] = ov[i] / den;
       if (z16) z16[(int64_t)b * ldz + e] = f32_to_bf16_rne(ov[i] / den);
@@ -210,16 +229,17 @@ __global__ __launch_bounds__(256) void k_attn_pool_fwd(
 // dalpha_s = do . x_s ; dc_s = alpha_s (dalpha_s - sum_t alpha_t dalpha_t) ; da_s = dc_s w_s.
 // Writes da [B*S] (dW2 = da^T H and db2 = sum da are reductions done after) and
 // dH[bs][j] = da_bs * W2[j] (the ReLU mask is applied by tt_relu_backward_f32).
-__global__ __launch_bounds__(256) void k_attn_pool_bwd(
+template <int NT>
+__global__ __launch_bounds__(NT) void k_attn_pool_bwd(
     const float* __restrict__ dz, int64_t lddz, const float* __restrict__ z, int64_t ldz,
     const float* __restrict__ onorm, const float* __restrict__ alpha,
     const float* __restrict__ w, const float* __restrict__ x, int S, int E,
     const float* __restrict__ W2, int Hd, float* __restrict__ da, float* __restrict__ dH,
-    const float* __restrict__ H, bool relu_mask, float* __restrict__ dW2_acc,
-    float* __restrict__ db2_acc) {
+    const float* __restrict__ H, bool relu_mask, float* __restrict__ part) {
   __shared__ float dov[1024];
   __shared__ float dal[128], sal[128], sw[128], sdas[128];
-  __shared__ float red[4];
+  constexpr int NW = NT / 64;
+  __shared__ float red[NW];
   const int b = blockIdx.x, tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   if (tid < S) {  // the buyer's alpha and weights, loaded once (not per position in a loop)
     sal[tid] = alpha[(int64_t)b * S + tid];
@@ -227,22 +247,29 @@ __global__ __launch_bounds__(256) void k_attn_pool_bwd(
   }
   const float nrm = onorm[b];
   float zd = 0.0f;
-  for (int e = tid; e < E; e += 256) zd = fmaf(z[(int64_t)b * ldz + e], dz[(int64_t)b * lddz + e], zd);
+  for (int e = tid; e < E; e += NT) zd = fmaf(z[(int64_t)b * ldz + e], dz[(int64_t)b * lddz + e], zd);
   zd = wave_sum(zd);
   if (lane == 0) red[wv] = zd;
   __syncthreads();
-  zd = (red[0] + red[1]) + (red[2] + red[3]);
-  for (int e = tid; e < E; e += 256) {
+  zd = 0.0f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) zd += red[i];
+  for (int e = tid; e < E; e += NT) {
     const float g = dz[(int64_t)b * lddz + e];
     dov[e] = nrm > 1e-12f ? (g - z[(int64_t)b * ldz + e] * zd) / nrm : g / 1e-12f;
   }
   __syncthreads();
   const float* xb = x + (int64_t)b * S * E;
-  for (int s = wv; s < S; s += 4) {
+  // dalpha_s = do . x_s: 16 lanes per position, 16 positions per pass (all loads in flight)
+  const int pl = tid & 15, pg = tid >> 4;
+  for (int s0 = 0; s0 < S; s0 += NT / 16) {
+    const int s = s0 + pg;
     float d = 0.0f;
-    for (int e = lane; e < E; e += 64) d = fmaf(dov[e], xb[(int64_t)s * E + e], d);
-    d = wave_sum(d);
-    if (lane == 0) dal[s] = d;
+    if (s < S)
+      for (int e = pl; e < E; e += 16) d = fmaf(dov[e], xb[(int64_t)s * E + e], d);
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) d += __shfl_xor(d, o, 16);
+    if (pl == 0 && s < S) dal[s] = d;
   }
   __syncthreads();
   float adot = 0.0f;
@@ -254,21 +281,55 @@ __global__ __launch_bounds__(256) void k_attn_pool_bwd(
   }
   __syncthreads();
   const int64_t o0 = (int64_t)b * S * Hd;
-  for (int i = tid; i < S * Hd; i += 256) {  // dH = da W2 (ReLU backward of H fused)
+  for (int i = tid; i < S * Hd; i += NT) {  // dH = da W2 (ReLU backward of H fused)
     const float v = sdas[i / Hd] * W2[i % Hd];
     dH[o0 + i] = relu_mask && !(H[o0 + i] > 0.0f) ? 0.0f : v;
   }
-  if (dW2_acc) {  // this buyer's part of dW2 = da^T H and db2 = sum da, accumulated
-    for (int j = tid; j < Hd; j += 256) {
+  if (part) {  // this buyer's part of dW2 = da^T H and db2 = sum da (k_attn_bwd_reduce sums)
+    float* pb = part + (int64_t)b * (Hd + 1);
+    for (int j = tid; j < Hd; j += NT) {
       float acc = 0.0f;
       for (int s2 = 0; s2 < S; ++s2) acc = fmaf(sdas[s2], H[o0 + (int64_t)s2 * Hd + j], acc);
-      atomicAdd(dW2_acc + j, acc);
+      pb[j] = acc;
     }
     if (tid == 0) {
       float sd = 0.0f;
       for (int s2 = 0; s2 < S; ++s2) sd += sdas[s2];
-      atomicAdd(db2_acc, sd);
+      pb[Hd] = sd;
     }
+  }
+}
+
+// dW2 [Hd] and db2 from the per-buyer parts [B][Hd + 1]: a block of 8 row groups x 128
+// columns (a wave reads 64 consecutive columns of one row), each group a fixed contiguous
+// range of buyers with all its loads in flight, then the 8 groups summed in order
+// (deterministic; one launch, where 512 blocks' atomics on the same 129 addresses had
+// serialised at the L2)
+__global__ __launch_bounds__(1024) void k_attn_bwd_reduce(const float* __restrict__ part, int B,
+                                                          int Hd, float* __restrict__ dW2,
+                                                          float* __restrict__ db2) {
+  __shared__ float gs[8][128];
+  const int g = threadIdx.x >> 7, cl = threadIdx.x & 127;
+  const int c = blockIdx.x * 128 + cl;
+  const int per = (B + 7) / 8, r0 = g * per, r1 = min(B, r0 + per);
+  float sacc = 0.0f;
+  if (c <= Hd) {
+    for (int rb = r0; rb < r1; rb += 32) {  // 32 loads in flight, then summed in row order
+      float v[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) v[u] = rb + u < r1 ? part[(int64_t)(rb + u) * (Hd + 1) + c] : 0.0f;
+#pragma unroll
+      for (int u = 0; u < 32; ++u) sacc += v[u];
+    }
+  }
+  gs[g][cl] = sacc;
+  __syncthreads();
+  if (g == 0 && c <= Hd) {
+    float t = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += gs[i][cl];
+    if (c < Hd) dW2[c] = t;
+    else *db2 = t;
   }
 }
 
@@ -343,7 +404,7 @@ unsigned grid_for(int64_t n) {
 // v_mfma_f32_16x16x32_bf16; else v_mfma_f32_16x16x4_f32.  Optional db [N] = column sums of
 // dY (the bias gradient, from the same loads; f32, fixed order).
 constexpr int TN_T = 64;
-constexpr int TN_SMAX = 32;  // row splits per tile
+constexpr int TN_SMAX = 64;  // row splits per tile
 __host__ __device__ constexpr int tn_pitch(bool bf) { return bf ? 64 + 8 : 64 + 4; }
 
 template <bool BF>
@@ -528,7 +589,7 @@ TnPlan tn_plan(int64_t M, int N, int K) {
   p.NT = (N + TN_T - 1) / TN_T;
   p.KT = (K + TN_T - 1) / TN_T;
   const int T = p.NT * p.KT;
-  int64_t S = (512 + T - 1) / T;  // ~2 blocks per CU
+  int64_t S = (1024 + T - 1) / T;  // ~4 blocks per CU: the k-loop is latency-bound
   const int64_t maxS = (M + TN_T - 1) / TN_T;
   if (S > maxS) S = maxS;
   if (S > TN_SMAX) S = TN_SMAX;
@@ -600,7 +661,10 @@ __global__ void k_embedding_bwd2(const float* __restrict__ g, int64_t ldg,
 // ReLU (+ Dropout) backward on the post-activation h: h > 0 iff the unit was kept and active,
 // so dh = h > 0 ? dh * scale : 0 covers both (scale = 1 / (1 - p), 1 without dropout)
 __global__ void k_relu_drop_bwd(float* __restrict__ dh, const float* __restrict__ h, float scale,
-                                int64_t n, uint16_t* __restrict__ dh16) {
+                                int64_t n, uint16_t* __restrict__ dh16,
+                                int64_t* __restrict__ ctr_advance) {
+  // (advances the dropout draw counter of tt_dropout_rng_f32 after this step's last use)
+  if (ctr_advance && blockIdx.x == 0 && threadIdx.x == 0) *ctr_advance += 1;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const float v = h[i] > 0.0f ? dh[i] * scale : 0.0f;
@@ -746,8 +810,9 @@ extern "C" int tt_attn_pool_fwd_f32(const float* H, int32_t Hd, const float* W2,
              "need 1 <= S <= 128, 1 <= E <= 1024");
   if (B == 0) return TT_OK;
   TT_REQUIRE(H && W2 && w && x && alpha && onorm && z, "null pointer");
-  hipLaunchKernelGGL(k_attn_pool_fwd, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, H, Hd,
-                     W2, b2, (const float*)nullptr, w, x, S, E, alpha, onorm, z, ldz);
+  hipLaunchKernelGGL(k_attn_pool_fwd<256>, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, H,
+                     Hd, W2, b2, (const float*)nullptr, w, x, S, E, alpha, onorm, z, ldz,
+                     (uint16_t*)nullptr);
   return check_launch("tt_attn_pool_fwd_f32");
 }
 
@@ -759,8 +824,8 @@ extern "C" int tt_attn_pool_fwd_f32_dev(const float* H, int32_t Hd, const float*
              "need 1 <= S <= 128, 1 <= E <= 1024");
   if (B == 0) return TT_OK;
   TT_REQUIRE(H && W2 && b2 && w && x && alpha && onorm && z, "null pointer");
-  hipLaunchKernelGGL(k_attn_pool_fwd, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, H, Hd,
-                     W2, 0.0f, b2, w, x, S, E, alpha, onorm, z, ldz, z_bf16);
+  hipLaunchKernelGGL(k_attn_pool_fwd<512>, dim3((unsigned)B), dim3(512), 0, (hipStream_t)stream, H,
+                     Hd, W2, 0.0f, b2, w, x, S, E, alpha, onorm, z, ldz, z_bf16);
   return check_launch("tt_attn_pool_fwd_f32_dev");
 }
 
@@ -775,11 +840,16 @@ int attn_pool_bwd(const float* dz, int64_t lddz, const float* z, int64_t ldz, co
   TT_REQUIRE(dz && z && onorm && alpha && w && x && H && W2 && dW2 && db2 && dH && da_ws,
              "null pointer");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_attn_pool_bwd, dim3((unsigned)B), dim3(256), 0, st, dz, lddz, z, ldz,
-                     onorm, alpha, w, x, S, E, W2, Hd, da_ws, dH, H, relu_mask,
-                     fused ? dW2 : (float*)nullptr, fused ? db2 : (float*)nullptr);
+  float* part = fused ? da_ws + (B * S + 63) / 64 * 64 : nullptr;  // [B][Hd + 1] after da
+  hipLaunchKernelGGL(k_attn_pool_bwd<512>, dim3((unsigned)B), dim3(512), 0, st, dz, lddz, z, ldz,
+                     onorm, alpha, w, x, S, E, W2, Hd, da_ws, dH, H, relu_mask, part);
   int rc = check_launch("k_attn_pool_bwd");
-  if (rc || fused) return rc;
+  if (rc) return rc;
+  if (fused) {
+    hipLaunchKernelGGL(k_attn_bwd_reduce, dim3((unsigned)((Hd + 1 + 127) / 128)), dim3(1024), 0,
+                       st, part, (int)B, Hd, dW2, db2);
+    return check_launch("k_attn_bwd_reduce");
+  }
   if (hipMemsetAsync(dW2, 0, (size_t)Hd * 4, st) != hipSuccess ||
       hipMemsetAsync(db2, 0, 4, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "tt_attn_pool_bwd_f32: hipMemsetAsync");
@@ -898,12 +968,13 @@ extern "C" int tt_embedding_backward2_f32(const float* g, int64_t ldg, const int
 }
 
 extern "C" int tt_relu_dropout_backward_f32(float* dh, const float* h, float scale, int64_t n,
-                                            uint16_t* dh_bf16, void* stream) {
+                                            uint16_t* dh_bf16, int64_t* counter_advance,
+                                            void* stream) {
   TT_REQUIRE(n >= 0, "n < 0");
   if (n == 0) return TT_OK;
   TT_REQUIRE(dh && h, "null pointer");
   hipLaunchKernelGGL(k_relu_drop_bwd, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, dh, h,
-                     scale, n, dh_bf16);
+                     scale, n, dh_bf16, counter_advance);
   return check_launch("tt_relu_dropout_backward_f32");
 }
 

@@ -179,7 +179,8 @@ SIGNATURES = {
     "tt_gemm_tn": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32, _vp, _i64, _vp,
                                   _vp, _i64, _vp]),
     "tt_dropout_apply_ex": (ctypes.c_int, [_vp, _vp, ctypes.c_float, _i64, _vp, _vp]),
-    "tt_relu_dropout_backward_f32": (ctypes.c_int, [_vp, _vp, ctypes.c_float, _i64, _vp, _vp]),
+    "tt_relu_dropout_backward_f32": (ctypes.c_int, [_vp, _vp, ctypes.c_float, _i64, _vp, _vp,
+                                                    _vp]),
     "tt_l2norm_backward_ex": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _vp,
                                              _i64, _vp, _i64, _vp]),
     "tt_convert_batch": (ctypes.c_int, [ctypes.POINTER(ConvertJob), _i32, _vp]),

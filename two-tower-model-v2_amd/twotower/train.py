@@ -246,7 +246,8 @@ class TwoTowerTrainStep:
             b.Hb = e(B * S, Hd)
             b.X16 = e(B * S, E, dt=bf) if bf16 else None
             b.alpha, b.onorm = e(B, S), e(B)
-            b.dHb, b.da = e(B * S, Hd), e(B * S)
+            b.dHb = e(B * S, Hd)
+            b.da = e((B * S + 63) // 64 * 64 + B * (Hd + 1))  # da, then per-buyer dW2 parts
         b.loss = torch.empty((), dtype=f32, device=dev)
         need = ctypes.c_int64(0)
         check(lib().tt_infonce_workspace_bytes(B, N, E, _lib.TT_PREC_BF16 if bf16 else
@@ -294,10 +295,6 @@ class TwoTowerTrainStep:
         # gradients the step accumulates with atomics, zeroed by the same launch
         if use_cat:
             o0, o1 = self._span["brand"][0], self._span["cat"][0] + self._span["cat"][1]
-            jobs.append(_lib.ConvertJob(None, 0, 1, o1 - o0, ctypes.c_void_p(
-                self.flat_g.data_ptr() + 4 * o0), o1 - o0, 0, 0))
-        if self.attention:
-            o0, o1 = self._span["att2.w"][0], self._span["att2.b"][0] + self._span["att2.b"][1]
             jobs.append(_lib.ConvertJob(None, 0, 1, o1 - o0, ctypes.c_void_p(
                 self.flat_g.data_ptr() + 4 * o0), o1 - o0, 0, 0))
         b.jobs = (_lib.ConvertJob * len(jobs))(*jobs)
@@ -421,7 +418,6 @@ class TwoTowerTrainStep:
             check(L.tt_dropout_rng_f32(bb.h.data_ptr(), bb.h.numel(), ctypes.c_float(pdrop),
                                        self._drop_seed, self._drop_ctr.data_ptr(), _p(bb.h16),
                                        st), "dropout")
-            self._drop_ctr.add_(1)
         elif keep is not None:
             scale = 1.0 / (1.0 - pdrop)
             check(L.tt_dropout_apply_ex(bb.h.data_ptr(), keep.data_ptr(), scale, bb.h.numel(),
@@ -481,7 +477,9 @@ class TwoTowerTrainStep:
             check(L.tt_gemm_f32(bb.dy.data_ptr(), E, bb.W3T.data_ptr(), E, None, None, 0,
                                 bb.dh.data_ptr(), hid, None, 0, R, hid, E, 0, st), "gemm dh")
         check(L.tt_relu_dropout_backward_f32(bb.dh.data_ptr(), bb.h.data_ptr(), scale,
-                                             bb.dh.numel(), _p(bb.dh16), st), "relu_bwd")
+                                             bb.dh.numel(), _p(bb.dh16),
+                                             _p(self._drop_ctr) if rng_drop else None, st),
+              "relu_bwd")
         check(L.tt_gemm_tn(bb.dh.data_ptr(), hid, x_in.data_ptr(), x_in.stride(0), R, hid,
                            width, pr, G["proj0.w"].data_ptr(), width, G["proj0.b"].data_ptr(),
                            ws.data_ptr(), ws.numel(), st), "dW0")
