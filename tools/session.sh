@@ -41,6 +41,10 @@ for s in "$@"; do
     debug_graph) step debug_graph 200 python3 -u tools/debug_graph_step.py ;;
     trainer_tests_nograph) step trainer_tests_nograph 600 $PYT -m gpu tests/test_gpu_trainer.py tests/test_gpu_train.py tests/test_gpu_loss.py -k "not graph_step" ;;
     enc_batch) step enc_batch 400 $PYT -s -m gpu tests/test_gpu_encoder.py -k large_batch ;;
+    enc_prof) step enc_prof_5120 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$OUT/enc5120" -o run -- python3 tools/bench_encoder.py --prec x3 --batch 5120 --batches 3 &&
+              step enc_prof_256 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$OUT/enc256" -o run -- python3 tools/bench_encoder.py --prec x3 --batch 256 --batches 20 ;;
     bench) step bench 600 python3 bench.py --steps 20 --warmup 5 ;;
     smoke) step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $s"; exit 2 ;;
