@@ -142,8 +142,9 @@ def test_bf16_step_vs_f32_step_configs4_shape():
     print("bf16 rel grad error (ours, torch autocast):", report)
 
 
+@pytest.mark.parametrize("graph", [False, True])
 @pytest.mark.parametrize("aggregation", ["attention", "weighted_avg"])
-def test_trainer_epochs_reference_batches(tmp_path, aggregation):
+def test_trainer_epochs_reference_batches(tmp_path, aggregation, graph):
     from twotower.config import DEFAULT_CONFIG
     from twotower.trainer import Trainer
 
@@ -175,12 +176,14 @@ def test_trainer_epochs_reference_batches(tmp_path, aggregation):
     cp = tmp_path / "config.yaml"
     cp.write_text(yaml.safe_dump(cfg, allow_unicode=True))
     model = _model(aggregation=aggregation, seed=1)
-    tr = Trainer(model, train, val, config_path=str(cp), pad_to_batch_max=True)
+    tr = Trainer(model, train, val, config_path=str(cp), pad_to_batch_max=True, graph=graph)
     tr.set_product_metadata(meta)
     v0 = tr.validate()
     assert v0 == tr.validate()  # eval mode: deterministic
     losses = [tr.train_epoch() for _ in range(3)]
     assert all(np.isfinite(losses)) and losses[-1] < losses[0]
+    if graph:  # one captured HIP graph per batch shape (histories padded to the batch max)
+        assert 1 <= len(tr.step._graphs) <= len(train)
     tr.train()
     assert (tmp_path / "best_model.pt").exists()
     ck = torch.load(tmp_path / "checkpoint_epoch_4.pt", weights_only=True)

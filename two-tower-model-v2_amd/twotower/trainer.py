@@ -9,6 +9,8 @@ weights) and loop structure:
       MiniLM encoder) -> per buyer [max_interaction_history, H] zero-padded with weight 0;
       empty histories fall back to the positive text with weight 1; the last
       max_interaction_history items are kept.
+  graph=True: each batch shape's forward + backward is captured once in a HIP graph and
+      replayed (TwoTowerTrainStep(graph=True)).
   train_epoch (:161-243)  model.train(); per batch: the sequence encode above, brand /
       category lookups from the product metadata (:190-209), then ONE fused HIP step
       (twotower.train.TwoTowerTrainStep: item head incl. its train-mode Dropout + buyer
@@ -44,7 +46,7 @@ class Trainer:
 
     def __init__(self, model, train_loader, val_loader=None,
                  config_path: Optional[str] = "configs/config.yaml", prec: str = "f32",
-                 pad_to_batch_max: bool = False):
+                 pad_to_batch_max: bool = False, graph: bool = False):
         self.model = model
         self.train_loader = train_loader
         self.val_loader = val_loader
@@ -54,7 +56,7 @@ class Trainer:
         tc = self.config["training"]
         self.step = TwoTowerTrainStep(model.item_tower, model.buyer_tower,
                                       temperature=tc["temperature"], lr=tc["learning_rate"],
-                                      prec=prec)
+                                      prec=prec, graph=graph)
         self.optimizer = self.step  # Adam lives in the fused step (moments resident in HBM)
         self.current_epoch = 0
         self.start_epoch = 0  # first epoch train() runs (load_checkpoint: saved epoch + 1)
