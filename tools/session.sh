@@ -45,6 +45,18 @@ for s in "$@"; do
                 -d "$OUT/enc5120" -o run -- python3 tools/bench_encoder.py --prec x3 --batch 5120 --batches 3 &&
               step enc_prof_256 300 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d "$OUT/enc256" -o run -- python3 tools/bench_encoder.py --prec x3 --batch 256 --batches 20 ;;
+    # A/B of a timing-switch (AB_ENV=NAME, values 0 / 1) on the timing build lib_tb.so: the
+    # encoder's x3 tests under the switch, then bench_encoder alternating x2 at 5120 and 256
+    enc_ab) L=$PWD/two-tower-model-v2_amd/lib/variants/lib_tb.so
+        env TWOTOWER_HIP_LIB=$L $AB_ENV=1 timeout -k 10 400 $PYT -m gpu tests/test_gpu_encoder.py \
+          -k "x3 or attention or large_batch" > "$OUT/enc_ab_tests.log" 2>&1 || { tail -5 "$OUT/enc_ab_tests.log"; exit 1; }
+        tail -1 "$OUT/enc_ab_tests.log"
+        for rep in 1 2; do for v in 0 1; do for b in 5120 256; do
+          nb=$([ $b = 5120 ] && echo 3 || echo 20)
+          env TWOTOWER_HIP_LIB=$L $AB_ENV=$v timeout -k 10 200 python3 tools/bench_encoder.py --prec x3 \
+            --batch $b --batches $nb > "$OUT/ab_${v}_${b}_$rep.json" 2>/dev/null || exit 1
+          echo "$AB_ENV=$v b=$b rep=$rep $(tail -1 $OUT/ab_${v}_${b}_$rep.json | cut -c1-120)"
+        done; done; done ;;
     bench) step bench 600 python3 bench.py --steps 20 --warmup 5 ;;
     smoke) step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $s"; exit 2 ;;
