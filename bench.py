@@ -1083,6 +1083,8 @@ def main():
     # single pass and the batched search's sample level run on it (same results)
     img8 = (kernels.i8_image(shard, E) if a.method == "bf16" and not staged
             and ep in kernels.I8_DIMS else None)
+    if img8 is not None:  # + the tiled copy the register-fed stream reads (padded dim 384)
+        img8 = (*img8, kernels.i8_tile(img8[0], hi - lo, E) if ep in kernels.I8T_DIMS else None)
     s_shard = torch.empty((nq, K), device=dev)
     i_shard = torch.empty((nq, K), dtype=torch.int64, device=dev)
     L = _lib.lib()
@@ -1264,15 +1266,20 @@ def main():
         # the int8 single pass the serving path takes for nq <= 8 (tt_scan_topk_i8f32, same
         # results): its image is built once per catalog, like the bf16 one
         i8 = img8
-        i8_lvl = []
+        i8_lvl, ring_lvl = [], []
         if i8 is not None:
+            # the stream the serving path takes (the register-fed one over the tiled image at
+            # padded dim 384), and the LDS-ring stream over the row-major image beside it
             for r in range(n1 + 3):
-                kernels.scan_topk_i8(shard, i8[0], i8[1], hi - lo, E, q1, K, i8[2].tolist(),
-                                     row_base=lo, workspace=ws1, events=(ev[0], ev[1]))
-                torch.cuda.synchronize()
-                if r >= 3:
-                    i8_lvl.append(ev[0].elapsed_time(ev[1]))
-            i8_fb = kernels.filter_fallback_count(ws1, hi - lo, E, 1, K)
+                for tl, acc in ((i8[3], i8_lvl), (None, ring_lvl)):
+                    kernels.scan_topk_i8(shard, i8[0], i8[1], hi - lo, E, q1, K, i8[2].tolist(),
+                                         row_base=lo, workspace=ws1, events=(ev[0], ev[1]),
+                                         tiled=tl)
+                    torch.cuda.synchronize()
+                    if r >= 3:
+                        acc.append(ev[0].elapsed_time(ev[1]))
+                    if tl is not None:
+                        i8_fb = kernels.filter_fallback_count(ws1, hi - lo, E, 1, K)
 
         # the device search as the serving path binds it (kernels.PreparedSearch: one C call per
         # buyer, outputs / workspace bound once); median of 21 synchronised calls
@@ -1299,10 +1306,16 @@ def main():
         if i8 is not None:
             i8_ms = statistics.median(i8_lvl)
             i8_bytes = float((hi - lo) * ep + 4 * ((hi - lo + 63) // 64))
+            ring_ms = statistics.median(ring_lvl)
             i8_info = {"bf16_pass_ms_per_search": bf16_ms, "int8_stream_ms": i8_ms,
+                       "int8_stream_kernel": ("k_filter_topm_i8r<384, 4> (tiled image, "
+                                              "register-fed)" if i8[3] is not None else
+                                              f"k_filter_topm_i8<{ep}, 4> (LDS ring)"),
                        "int8_stream_bytes": i8_bytes,
                        "int8_stream_gbps": i8_bytes / (i8_ms * 1e-3) / 1e9,
                        "int8_stream_frac": i8_bytes / (i8_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                       "int8_ring_stream_ms": ring_ms,
+                       "int8_ring_stream_frac": i8_bytes / (ring_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                        "int8_fallback_queries": int(i8_fb),
                        "int8_same_as_bf16_pass": True}
         result["single_buyer_search"] = {

@@ -165,6 +165,17 @@ int tt_scan_topk_i8f32(const float* db, const int8_t* db_i8, const float* tile_s
                        float x_resid_max, float s_max, float* out_score, int64_t* out_idx,
                        void* workspace, int64_t workspace_bytes, void* stream, void* ev_start,
                        void* ev_stop);
+/* The same search over the TILED int8 image (tt_i8_tile; padded dim 384 only): each of a
+ * block's 8 waves streams its own 16-row blocks straight into MFMA operands (1 KB contiguous per
+ * load instruction, no LDS staging, no block barrier).  Same results bit for bit as
+ * tt_scan_topk_i8f32 and tt_scan_topk_f32; same workspace, limits and fallback;
+ * TT_ERR_UNSUPPORTED at other padded dims (callers then take tt_scan_topk_i8f32). */
+int tt_scan_topk_i8t_f32(const float* db, const int8_t* db_i8t, const float* tile_scales,
+                         int64_t n, int32_t d, int64_t ld_db, int64_t row_base, const float* q,
+                         int32_t nq, int64_t ld_q, int32_t k, float x_norm_max,
+                         float x_resid_max, float s_max, float* out_score, int64_t* out_idx,
+                         void* workspace, int64_t workspace_bytes, void* stream, void* ev_start,
+                         void* ev_stop);
 
 /* ---------------------------------------------------------------------------------
  * Row-sharded (multi-GPU) form of tt_scan_topk_bf16f32 (faiss IndexFlatIP.search,
@@ -237,6 +248,14 @@ int tt_i8_image(const float* x, int64_t n, int32_t d, int64_t ld, int8_t* codes,
                 int64_t ld_codes, float* tile_scales, float* out3, void* stream);
 int tt_bf16_image_bounds(const float* x, const uint16_t* x_bf16, int64_t n, int32_t d,
                          int64_t ld, float* out2, void* stream);
+/* The tiled int8 image for tt_scan_topk_i8t_f32, from tt_i8_image's codes [n, ld_codes]:
+ * per 16-row block b, E / 64 pieces of 1 KB (E = tt_padded_dim(d)); piece s holds, at byte
+ * 16 l (l = 16 g + col), row 16 b + col's codes 64 s + 16 g .. + 15 (rows past n zero).
+ * tt_i8_tiled_bytes(n, d) = ceil(n / 16) * 16 * E (-1 when E % 64 != 0).  Buffers 16-B
+ * aligned, ld_codes a multiple of 16.  The tile scales and bounds stay tt_i8_image's. */
+int64_t tt_i8_tiled_bytes(int64_t n, int32_t d);
+int tt_i8_tile(const int8_t* codes, int64_t ld_codes, int64_t n, int32_t d, int8_t* tiled,
+               void* stream);
 
 /* Merge n_lists per-shard top-k lists [n_lists, nq, k_in] (each sorted, global row ids)
  * into [nq, k]; same ordering rule.  Used after the RCCL all-gather of per-shard top-k

@@ -148,6 +148,20 @@ def vector_db_normalize(x: np.ndarray) -> np.ndarray:
     return (x / (norms + 1e-8)).astype(np.float32)
 
 
+def i8_tile(codes: np.ndarray, n: int) -> np.ndarray:
+    """numpy restatement of tt_i8_tile (test infrastructure; the layout is this framework's,
+    not the reference's): codes [n, E] int8 (E % 64 == 0) -> per 16-row block b, E / 64 pieces
+    of 1 KB, piece s holding at byte 16 l (l = 16 g + col) row 16 b + col's codes
+    64 s + 16 g .. + 15; rows past n zero.  Flat int8 [ceil(n / 16) * 16 * E]."""
+    e = codes.shape[1]
+    nb = (n + 15) // 16
+    c = np.zeros((nb * 16, e), np.int8)
+    c[:n] = codes[:n]
+    # [b, col, s, g, 16] -> [b, s, g, col, 16]
+    t = c.reshape(nb, 16, e // 64, 4, 16).transpose(0, 2, 3, 1, 4)
+    return np.ascontiguousarray(t).reshape(-1)
+
+
 def i8_image(x: np.ndarray):
     """numpy restatement of tt_i8_image (test infrastructure): per 64-row tile s = max|x| / 127
     over finite values (float32 division), codes rint(x / s) clamped to [-127, 127] (0 where

@@ -68,6 +68,81 @@ def test_scan_topk_i8_bit_exact_vs_oracle(K, oracle_mod, n, d, nq, k):
     assert np.array_equal(s.cpu().numpy(), rs)
 
 
+@pytest.mark.parametrize("n,d", [(1000, 384), (37, 300), (16, 384), (129, 768)])
+def test_i8_tile_vs_numpy(K, oracle_mod, n, d):
+    """The tiled int8 image (tt_i8_tile) is the numpy restatement's permutation of the codes:
+    per 16-row block, piece s, lane l = 16 g + col -> row col's bytes 64 s + 16 g .. + 15."""
+    from oracle import oracle as O
+
+    rng = np.random.default_rng(n * 3 + d)
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
+    db = dev_rows(x)
+    codes, _, _ = K.i8_image(db, d)
+    tiled = K.i8_tile(codes, n, d)
+    ref = O.i8_tile(codes.cpu().numpy(), n)
+    assert tiled.numel() == ref.size
+    assert np.array_equal(tiled.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("n,nq,k", [(100_000, 1, 100), (300_001, 4, 128), (1000, 2, 10),
+                                    (5, 1, 3), (257, 1, 128), (70_001, 3, 1),
+                                    (1_000_000, 1, 100), (200_000, 5, 100), (1_000_000, 8, 100)])
+def test_scan_topk_i8_tiled_bit_exact(K, oracle_mod, n, nq, k):
+    """The register-fed stream over the tiled image (tt_scan_topk_i8t_f32, padded dim 384):
+    bit-exact against the oracle and identical to the LDS-ring stream over the row-major
+    image, fallback counts included; tiny catalogs leave most waves without a block (n = 5:
+    one block in one wave of the whole grid) and at 1M rows the last slabs hold no rows."""
+    d = 384
+    rng = np.random.default_rng(n + 7 * nq + k)
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
+    q = oracle_mod.l2norm_rows(rng.standard_normal((nq, d)).astype(np.float32), 0)
+    db, qd = dev_rows(x), dev_rows(q)
+    codes, scales, b3 = K.i8_image(db, d)
+    tiled = K.i8_tile(codes, n, d)
+    ws = torch.empty(K.filter_workspace_bytes(n, d, nq, k), dtype=torch.uint8, device="cuda")
+    out = {}
+    for name, t in (("tiled", tiled), ("ring", None)):
+        s, i = K.scan_topk_i8(db, codes, scales, n, d, qd, k, b3.tolist(), workspace=ws, tiled=t)
+        out[name] = (s.cpu().numpy(), i.cpu().numpy(), K.filter_fallback_count(ws, n, d, nq, k))
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    assert np.array_equal(out["tiled"][1], ri) and np.array_equal(out["tiled"][0], rs)
+    assert out["tiled"][2] == out["ring"][2]
+    assert np.array_equal(out["tiled"][1], out["ring"][1])
+    assert np.array_equal(out["tiled"][0], out["ring"][0])
+
+
+def test_scan_topk_i8_tiled_nan_and_clustered(K, oracle_mod):
+    """The tiled stream on the adversarial cases: a NaN row and a NaN query (bit-exact), and a
+    clustered slab the final cannot certify (falls back, bit-exact)."""
+    d, k = 384, 100
+    rng = np.random.default_rng(11)
+    n = 20_000
+    x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
+    x[77, 5] = np.nan
+    q = oracle_mod.l2norm_rows(rng.standard_normal((2, d)).astype(np.float32), 0)
+    q[1, 0] = np.nan
+    db = dev_rows(x)
+    codes, scales, b3 = K.i8_image(db, d)
+    s, i = K.scan_topk_i8(db, codes, scales, n, d, dev_rows(q), 50, b3.tolist(),
+                          tiled=K.i8_tile(codes, n, d))
+    rs, ri = oracle_mod.scan_topk(x, q, 50)
+    assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
+    n = 200_000
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    q = rng.standard_normal((1, d)).astype(np.float32)
+    x[1000:1400] = q + 0.05 * rng.standard_normal((400, d)).astype(np.float32)
+    x = oracle_mod.l2norm_rows(x, 0)
+    q = oracle_mod.l2norm_rows(q, 0)
+    db = dev_rows(x)
+    codes, scales, b3 = K.i8_image(db, d)
+    ws = torch.empty(K.filter_workspace_bytes(n, d, 1, k), dtype=torch.uint8, device="cuda")
+    s, i = K.scan_topk_i8(db, codes, scales, n, d, dev_rows(q), k, b3.tolist(), workspace=ws,
+                          tiled=K.i8_tile(codes, n, d))
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
+    assert K.filter_fallback_count(ws, n, d, 1, k) == 1
+
+
 def test_scan_topk_i8_mode_b_buyers_no_fallback(K, oracle_mod):
     """Mode B buyers (weighted averages of 20 catalog rows, as bench.py's) over 1M x 384: every
     result bit-exact, and the certification holds (no query falls back)."""

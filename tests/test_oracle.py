@@ -139,3 +139,23 @@ def test_event_weights_match_reference(golden):
         table = json.load(f)
     for name, wgt in table.items():
         assert get_event_weight(name, DEFAULT_CONFIG) == wgt, name
+
+
+def test_oracle_i8_tile_layout():
+    """oracle.i8_tile against the layout's definition chunk by chunk (the tiled int8 image of
+    tt_i8_tile: piece s of 16-row block b holds, at byte 16 l, row 16 b + l % 16's codes
+    64 s + 16 (l // 16) .. + 15; rows past n zero)."""
+    from oracle import oracle as O
+
+    rng = np.random.default_rng(0)
+    for n, e in ((37, 384), (16, 768), (1, 64)):
+        c = rng.integers(-127, 128, (n, e)).astype(np.int8)
+        t = O.i8_tile(c, n)
+        nb = (n + 15) // 16
+        assert t.size == nb * 16 * e
+        for ch in range(nb * e):
+            b, wi = divmod(ch, e)
+            s, lane = wi >> 6, wi & 63
+            row, off = 16 * b + (lane & 15), 64 * s + 16 * (lane >> 4)
+            exp = c[row, off:off + 16] if row < n else np.zeros(16, np.int8)
+            assert np.array_equal(t[16 * ch:16 * ch + 16], exp), (n, e, ch)

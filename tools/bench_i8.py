@@ -1,6 +1,9 @@
 """One-buyer / small-batch latency (env NQS = batch sizes, default 1,2,4): bf16 single pass vs the int8 single pass (1M x 384, k=100),
 kernels.PreparedSearch device calls, median of 51 synchronised calls (HIP events), plus the
-stream kernel alone (ev_start/ev_stop around k_filter_topm / k_filter_topm_i8)."""
+stream kernel alone (ev_start/ev_stop around k_filter_topm / k_filter_topm_i8[r]).  I8VS = the
+int8 streams to time in turn (ring: k_filter_topm_i8 over the row-major image; tiled:
+k_filter_topm_i8r over kernels.i8_tile's image; default "ring,tiled,ring,tiled": an A/B x2 in
+one process)."""
 import json
 import os
 import statistics
@@ -25,6 +28,7 @@ def main():
     kernels.l2norm_rows(x, E, _lib.TT_NORM_ADD_EPS, out=x, out_bf16=x16)
     bnd = kernels.bf16_image_bounds(x, x16, E).tolist()
     codes, scales, b3 = kernels.i8_image(x, E)
+    tiled = kernels.i8_tile(codes, N, E) if ep in kernels.I8T_DIMS else None
     out = {"config": f"{N} x {E}, k={K}", "i8_bounds": b3.tolist()}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     st = torch.cuda.current_stream()
@@ -37,11 +41,18 @@ def main():
         kernels.l2norm_rows(q, E, _lib.TT_NORM_ADD_EPS, out=q)
         res = {}
         ref = None
-        for name, i8 in (("bf16", None), ("i8", (codes, scales, b3))):
-            if name == "i8" and nq > kernels.I8_NQ_MAX:
+        runs = [("bf16", None, None)]
+        for r, v in enumerate(os.environ.get("I8VS", "ring,tiled,ring,tiled").split(",")):
+            if v == "tiled" and tiled is None:
+                continue
+            runs.append((f"i8_{v}" + ("" if r < 2 else f"_{r // 2 + 1}"),
+                         (codes, scales, b3) + ((tiled,) if v == "tiled" else ()),
+                         tiled if v == "tiled" else None))
+        for name, i8, tl in runs:
+            if i8 is not None and nq > kernels.I8_NQ_MAX:
                 continue
             ps = kernels.PreparedSearch(x, x16, N, E, nq, K, bnd, i8=i8)
-            assert ps.i8 == (name == "i8")
+            assert ps.i8 == (i8 is not None)
             for _ in range(5):
                 ps(q)
             t = []
@@ -61,9 +72,9 @@ def main():
             lv = []
             for _ in range(21):
                 torch.cuda.synchronize()
-                if name == "i8":
+                if i8 is not None:
                     kernels.scan_topk_i8(x, codes, scales, N, E, q, K, b3.tolist(), workspace=ws,
-                                         events=(ev[0], ev[1]))
+                                         events=(ev[0], ev[1]), tiled=tl)
                 else:
                     kernels.scan_topk_bf16(x, x16, N, E, q, K, bnd, workspace=ws,
                                            events=(ev[0], ev[1]))

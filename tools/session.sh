@@ -57,6 +57,26 @@ for s in "$@"; do
             --batch $b --batches $nb > "$OUT/ab_${v}_${b}_$rep.json" 2>/dev/null || exit 1
           echo "$AB_ENV=$v b=$b rep=$rep $(tail -1 $OUT/ab_${v}_${b}_$rep.json | cut -c1-120)"
         done; done; done ;;
+    probe) step probe 120 ./tools/bin/stream_probe ;;
+    i8r_tests) step i8r_tests 500 $PYT -m gpu tests/test_gpu_i8.py tests/test_gpu_vectordb_reference.py ;;
+    i8r_bench) step i8r_bench 300 python3 -u tools/bench_i8.py ;;
+    # the tiled stream's timing builds (tools/exp_build2.sh; VARS = names under lib/variants)
+    i8r_ab) for v in ${VARS:-noapp nomfma d2 d3 d5}; do
+        TWOTOWER_HIP_LIB=$PWD/two-tower-model-v2_amd/lib/variants/lib_$v.so NQS=1 I8VS=tiled,ring \
+          step i8r_ab_$v 120 python3 -u tools/bench_i8.py
+        python3 -c "import json,sys; t=open('$OUT/i8r_ab_$v.log').read(); d=json.loads(t[t.index('{'):]); print('$v', {k: round(r['stream_ms'], 4) for k, r in d['nq1'].items()})"
+      done ;;
+    # fixed costs vs bytes: the int8 streams at 4 catalog sizes (a linear fit of stream_ms)
+    i8r_sizes) for nn in 16384 131072 500000 1000000; do
+        N=$nn NQS=1 I8VS=tiled,ring,tiled,ring step i8r_size_$nn 120 python3 -u tools/bench_i8.py
+        python3 -c "import json,sys; t=open('$OUT/i8r_size_$nn.log').read(); d=json.loads(t[t.index('{'):]); print('$nn', {k: round(r['stream_ms'], 4) for k, r in d['nq1'].items()})"
+      done ;;
+    i8r_clk) for nn in 1000000 16384; do
+        N=$nn TWOTOWER_HIP_LIB=$PWD/two-tower-model-v2_amd/lib/variants/lib_clk.so \
+          step i8r_clk_$nn 120 python3 -u tools/i8r_clk.py; cat "$OUT/i8r_clk_$nn.log"
+      done ;;
+    i8r_prof) step i8r_prof 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$OUT/i8r_prof" -o run -- python3 tools/bench_i8.py ;;
     bench) step bench 600 python3 bench.py --steps 20 --warmup 5 ;;
     smoke) step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -3051,6 +3051,431 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8(
   }
 }
 
+// The int8 single pass over the TILED int8 image (round 6).  k_filter_topm_i8 stages 64-row
+// tiles of the row-major image through an LDS ring with one block barrier per tile: every wave
+// waits for the slowest wave's appends and the DMA waves' counted waits each tile, and the
+// stream ran at 0.61 of 8 TB/s (its DMA-only floor: 0.78).  Here each of the 8 waves streams
+// its OWN 16-row blocks (block b = w, w + 8, ... of the slab) straight into VGPRs, D blocks in
+// flight, and runs the per-block work (KS i8 MFMAs, the tile scale, the appends and tile-max
+// bound of the previous block) with no barrier in the loop: a slow block delays only its wave.
+// Loads straight into MFMA operands need the tiled image (tt_i8_tile): a 16-row block is KS
+// 1-KB pieces, piece s holding lane (g, col)'s 16 B = row col's bytes 64 s + 16 g .. + 15, so
+// each load instruction reads 1 KB contiguous (tools/stream_probe.hip on MI355X: 7.0 TB/s into
+// registers; the row-major image read in the same lane order: 5.5, and 2.5 TB/s with 96
+// contiguous bytes per lane).  The query is coded in k_filter_topm_i8's chunk order.
+// The loads are inline asm with explicit counted waits (vmcnt((D - 1) KS) before a block is
+// consumed) so the compiler neither reorders nor flushes them; blocks past the slab read 0
+// from the bounded buffer resource (rows past its end: masked).  Candidate buffers per (wave,
+// query): TM_NQ TM_BUF / QB / 8 keys (128 at QB = 4).  The slab's merged top-16 and its exact
+// keys are k_filter_topm_i8's, so k_final_topm_i8 is unchanged.
+#ifndef TT_I8R_D
+#define TT_I8R_D 4  // row blocks in flight per wave (timing builds: other depths)
+#endif
+TT_CHECK_EXP(TT_I8R_D != 4, "TT_I8R_D");
+#ifndef TT_I8R_EXP
+#define TT_I8R_EXP 0  // timing only (results WRONG): 1 no appends, 2 no appends and no MFMA
+#endif
+TT_CHECK_EXP(TT_I8R_EXP, "TT_I8R_EXP");
+#ifndef TT_I8R_CLK
+#define TT_I8R_CLK 0  // timing only: per-block phase stamps (s_memrealtime, 100 MHz) of the stream
+#endif
+TT_CHECK_EXP(TT_I8R_CLK, "TT_I8R_CLK");
+#if TT_I8R_CLK
+__device__ unsigned long long g_i8rclk[256 * 8];
+extern "C" int tt_debug_i8r_clk(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_i8rclk), sizeof(g_i8rclk)) == hipSuccess ? 0 : -2;
+}
+#define I8R_STAMP(i)                                                               \
+  do {                                                                             \
+    if (tid == 0 && blk < 256) g_i8rclk[blk * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define I8R_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+template <int EP>
+struct I8RegCfg {
+  static constexpr int D = TT_I8R_D;  // row blocks in flight per wave (E = 384: 96 VGPRs)
+  static_assert(EP == 384, "E = 768 would need 12 loads per block: D = 2 spills");
+};
+typedef int32_t i8r_v4i __attribute__((ext_vector_type(4)));
+
+template <int EP, int QB>
+__global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8r(
+    const int8_t* __restrict__ xt, int64_t /*unused*/, const float* __restrict__ scales,
+    int64_t n, const float* __restrict__ q, int nq, int64_t ldq, int rows_per_blk,
+    const float* __restrict__ db, int64_t ld, float X, float R, float S,
+    float* __restrict__ eps1, uint64_t* __restrict__ lists, uint64_t* __restrict__ xkeys,
+    int* __restrict__ counts, int* __restrict__ flags, int* __restrict__ qsel_n) {
+  constexpr int KS = EP / 64, NW = TM_WAVES, D = I8RegCfg<EP>::D, BLK = 16 * EP;
+  constexpr int TMB = TM_NQ * TM_BUF / QB / NW, CPER = TMB / 64;
+  static_assert(TMB % 64 == 0 && TMB >= 2 * TM_M && QB <= 16, "top-m buffer shape");
+  __shared__ __attribute__((aligned(16))) uint64_t tbuf[TM_NQ * TM_BUF];  // [NW][QB][TMB]
+  __shared__ int ncs[TM_NQ];
+  __shared__ int ncw[NW][TM_NQ];
+  __shared__ float ssc[I8_MAXTILES];
+  __shared__ __attribute__((aligned(16))) float tau_sh[QB][NW];
+  __shared__ int next_blk;  // the next unclaimed 16-row block of the slab
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 15, g = lane >> 4;
+  const int G = gridDim.x, blk = blockIdx.x;
+  I8R_STAMP(0);
+  if (tid == 0) next_blk = NW * I8RegCfg<EP>::D;
+  if (blk == 0 && tid < nq) {  // per-query fallback state (FilterWs: flags, qsel, qsel_n, done)
+    flags[tid] = 0;
+    qsel_n[1 + tid] = 0;
+    if (tid == 0) *qsel_n = 0;
+  }
+  const int64_t j0 = (int64_t)blk * rows_per_blk;  // rows_per_blk: a multiple of 64
+  const int64_t j1 = (j0 + rows_per_blk < n) ? j0 + rows_per_blk : n;
+  const int nb = j0 < j1 ? (int)((j1 - j0 + 15) / 16) : 0;  // 16-row blocks of the slab
+  for (int i = tid; i < (rows_per_blk >> 6); i += 64 * NW) {
+    const int64_t st = (j0 >> 6) + i;
+    ssc[i] = st < ((n + 63) >> 6) ? scales[st] : 0.0f;
+  }
+  if (lane < QB) tau_sh[lane][w] = -__builtin_huge_valf();
+  uint64_t* wbuf = tbuf + w * QB * TMB;  // [QB][TMB] of this wave
+  const bool qv = col < nq;
+  float tau = qv ? -__builtin_huge_valf() : __builtin_huge_valf();
+  int cnt = 0;
+  float tm[16];  // the tile-max bound's set, ascending (k_filter_topm_i8)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) tm[i] = -__builtin_huge_valf();
+  auto tm_insert = [&](float m) __attribute__((always_inline)) {
+    m = m == m ? m : -__builtin_huge_valf();
+#pragma unroll
+    for (int i = 0; i < 15; ++i) tm[i] = __builtin_amdgcn_fmed3f(tm[i], m, tm[i + 1]);
+    tm[15] = fmaxf(tm[15], m);
+  };
+  auto read_shtau = [&]() __attribute__((always_inline)) {
+    const f32x4* p = (const f32x4*)&tau_sh[col < QB ? col : 0][0];
+    const f32x4 a = p[0], b = p[1];
+    return fmaxf(fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])),
+                 fmaxf(fmaxf(b[0], b[1]), fmaxf(b[2], b[3])));
+  };
+  // the query (column col) coded as t m, lane (g, col) holding dims 64 s + 16 g .. + 15 for
+  // MFMA step s: the bytes the lane loads of every row (the tiled image's piece s).  The 24
+  // 16-B units su = 4 s + u of a lane are split over the 8 waves (3 each) and the codes meet in
+  // LDS: the prologue's code is fetched cold on every launch (the I-cache), so it is kept short
+  // (the fully unrolled per-wave form was 10.7 us of the 77 us launch, TT_I8R_CLK)
+  static_assert(KS * 4 == 3 * NW, "three 16-B query units per wave");
+  __shared__ __attribute__((aligned(16))) float qmx[16][NW];
+  __shared__ double qsq[16][NW], qsd[16][NW];
+  __shared__ uint32_t qcode[KS * 4][64];
+  float tq;
+  {
+    const float* qp = q + (int64_t)(qv ? col : 0) * ldq + 16 * g;
+    f32x4 v[3];
+    float mx = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int su = 3 * w + j;
+      v[j] = *(const f32x4*)(qp + 64 * (su >> 2) + 4 * (su & 3));
+      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[j][0]), fabsf(v[j][1])),
+                           fmaxf(fabsf(v[j][2]), fabsf(v[j][3]))));
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    if (g == 0) qmx[col][w] = mx;
+    __syncthreads();
+    {
+      const f32x4* p = (const f32x4*)&qmx[col][0];
+      const f32x4 a = p[0], b = p[1];
+      mx = fmaxf(fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])),
+                 fmaxf(fmaxf(b[0], b[1]), fmaxf(b[2], b[3])));
+    }
+    tq = mx / 127.0f;
+    double sq = 0.0, sd = 0.0;
+    const float tdiv = tq > 0.0f ? tq : 1.0f;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      uint32_t pk = 0u;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {  // (selects, no branch: see k_filter_topm_i8)
+        int c = (int)rintf(v[j][b] / tdiv);
+        c = c > 127 ? 127 : c < -127 ? -127 : c;
+        c = tq > 0.0f ? c : 0;
+        const double e = (double)v[j][b] - (double)tq * (double)c;
+        sq += (double)v[j][b] * (double)v[j][b];
+        sd += e * e;
+        pk |= ((uint32_t)(c & 0xff)) << (8 * b);
+      }
+      qcode[3 * w + j][lane] = pk;
+    }
+    sq += __shfl_xor(sq, 16, 64);
+    sd += __shfl_xor(sd, 16, 64);
+    sq += __shfl_xor(sq, 32, 64);
+    sd += __shfl_xor(sd, 32, 64);
+    if (g == 0) {
+      qsq[col][w] = sq;
+      qsd[col][w] = sd;
+    }
+  }
+  wait_vm<0>();     // every compiler-issued load retired: the loop's counted waits see only its own
+  __syncthreads();  // ssc, tau_sh, the query codes
+  u32x4 qf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+    qf[s] = u32x4{qcode[4 * s][lane], qcode[4 * s + 1][lane], qcode[4 * s + 2][lane],
+                  qcode[4 * s + 3][lane]};
+  if (blk == 0 && w == 0 && g == 0 && qv) {
+    double sq = 0.0, sd = 0.0;
+#pragma unroll
+    for (int wb = 0; wb < NW; ++wb) {
+      sq += qsq[col][wb];
+      sd += qsd[col][wb];
+    }
+    const double nq2 = sqrt(sq) * 1.000001, nd = sqrt(sd) * 1.000001;
+    const double e = 1.001 * ((double)R * nq2 + (double)S * nd +
+                              1.1920928955078125e-07 * (double)S * (nq2 + nd) +
+                              1.01 * EP * 5.9604644775390625e-08 * (double)X * nq2);
+    eps1[col] = e == e ? f64_up(e) : __builtin_huge_valf();
+  }
+  wait_vm<0>();  // (the eps store retired: the loop's counted waits see only its own loads)
+  I8R_STAMP(1);
+
+  // the slab's blocks as a bounded buffer resource (the tiled image pads the last block)
+  const uint64_t sbase = (uint64_t)(uintptr_t)(xt + j0 * EP);
+  i8r_v4i rs;
+  rs[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)sbase);
+  rs[1] = __builtin_amdgcn_readfirstlane((int)((uint32_t)(sbase >> 32) & 0xffffu));
+  // (slabs past the catalog end -- j0 >= n at 1M rows over 256 CUs -- get 0 records: every load
+  // of theirs reads 0 and touches no memory)
+  rs[2] = __builtin_amdgcn_readfirstlane(nb * BLK);
+  rs[3] = 0x00020000;
+  u32x4 buf[D][KS];
+  auto issue = [&](int slot, int b) __attribute__((always_inline)) {  // 16-row block b
+    // (piece s at bo + 4096 (s / 4) + immediate 1024 (s % 4): the immediate is 12 bits)
+    const uint32_t bo = (uint32_t)(b * BLK + 16 * lane), bo4 = bo + 4096u;
+    static_assert(KS == 6, "six pieces per block");
+#define TT_I8R_LD(S)                                                          \
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3 nt"         \
+               : "=v"(buf[slot][S])                                           \
+               : "v"((S) < 4 ? bo : bo4), "s"(rs), "n"(1024 * ((S) % 4))      \
+               : "memory")
+    TT_I8R_LD(0);
+    TT_I8R_LD(1);
+    TT_I8R_LD(2);
+    TT_I8R_LD(3);
+    TT_I8R_LD(4);
+    TT_I8R_LD(5);
+#undef TT_I8R_LD
+  };
+
+  static_assert(TM_M == 16, "wave_top16 keeps 16");
+  auto compact = [&](int c) __attribute__((always_inline)) {
+    uint64_t* b = wbuf + c * TMB;
+    const int cc = __shfl(cnt, c, 64);
+    uint64_t key[CPER];
+#pragma unroll
+    for (int r = 0; r < CPER; ++r) {
+      const int e = lane * CPER + r;
+      key[r] = e < cc ? b[e] : 0ull;
+    }
+    int nc;
+    const uint64_t k = wave_top16<CPER>(key, lane, b, &nc);
+    if (lane < nc) b[lane] = k;
+    const uint32_t hk = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(k >> 32), TM_M - 1);
+    if (col == c) {
+      cnt = nc;
+      if (nc == TM_M) tau = fmaxf(tau, key_float(hk));
+    }
+    wave_sync();
+  };
+  // appends of block bl (first: the wave's first block) and the tile-max bound:
+  // k_filter_topm_i8's
+  auto appends = [&](f32x4 acc, int bl, bool first, float shtau) __attribute__((always_inline)) {
+    const int64_t jt = j0 + 16 * (int64_t)bl;
+    if (qv) tau = fmaxf(tau, shtau);
+    if (jt + 16 > j1) {  // (wave-uniform) the slab's last block: rows past its end score -inf
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        if (jt + 4 * g + jj >= j1) acc[jj] = -__builtin_huge_valf();
+    }
+    const bool any = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])) >= tau;
+    if (__ballot(any) != 0ull) {
+      const int lr0 = 16 * bl + 4 * g, nloc = (int)(j1 - j0);  // slab-local rows
+      bool pass[4];
+      int np = 0;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        pass[jj] = lr0 + jj < nloc && acc[jj] >= tau;
+        np += pass[jj] ? 1 : 0;
+      }
+      const auto x16 = __builtin_amdgcn_permlane16_swap((uint32_t)np, (uint32_t)np, false, false);
+      const int b = (int)((g & 1) ? x16[0] : x16[1]);  // lane ^ 16
+      const int s2 = np + b;
+      const auto x32 = __builtin_amdgcn_permlane32_swap((uint32_t)s2, (uint32_t)s2, false, false);
+      const int s2x = (int)(lane < 32 ? x32[1] : x32[0]);  // lane ^ 32
+      int pos = cnt + ((g & 1) ? b : 0) + ((g & 2) ? s2x : 0);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        if (pass[jj]) {
+          lds_write64(lds_addr(wbuf + col * TMB + pos), make_key(acc[jj], (uint32_t)(j0 + lr0 + jj)));
+          ++pos;
+        }
+      cnt += s2 + s2x;
+    }
+    if (first) {  // the wave's first block: its 16 rows (every lane of the column gathers all 16)
+      float v16[16];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        v16[jj] = acc[jj];
+        const auto x16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[jj]),
+                                                          __float_as_uint(acc[jj]), false, false);
+        v16[4 + jj] = __uint_as_float((g & 1) ? x16[0] : x16[1]);
+      }
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const auto x32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v16[jj]),
+                                                          __float_as_uint(v16[jj]), false, false);
+        v16[8 + jj] = __uint_as_float(lane < 32 ? x32[1] : x32[0]);
+      }
+#pragma unroll
+      for (int k2 = 0; k2 < 16; ++k2) tm_insert(v16[k2]);
+    } else {
+      float m = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3]));
+      const auto x16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m),
+                                                        false, false);
+      m = fmaxf(__uint_as_float(x16[0]), __uint_as_float(x16[1]));
+      const auto x32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m),
+                                                        false, false);
+      tm_insert(fmaxf(__uint_as_float(x32[0]), __uint_as_float(x32[1])));  // the block max
+    }
+    tau = fmaxf(tau, qv ? tm[0] : tau);
+    const uint64_t need = __ballot(lane < 16 && cnt > TMB - 16);
+    if (need != 0ull) {
+      lds_wait<0>();
+      uint64_t nd = need;
+      while (nd) {
+        const int c = __builtin_ctzll(nd);
+        nd &= nd - 1;
+        compact(c);
+      }
+    }
+    if (qv && g == 0) tau_sh[col][w] = tau;  // published for the other waves
+  };
+
+  // Blocks are handed out dynamically: slot d of wave w starts on block w + NW d, and every
+  // consumed slot claims the next block from a block-wide LDS counter, so a wave whose loads
+  // come back early takes more of the slab and all 8 keep D blocks in flight to the end (with
+  // the static round-robin split, wave 0 left the loop ~14 us before the block's last wave:
+  // TT_I8R_CLK at 1M rows).  Claims are made in processing order and only grow, so the first
+  // slot holding a block >= nb ends the wave's loop; its later slots hold larger blocks.
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  int bid[D];
+  static_for<D>([&](auto d_) __attribute__((always_inline)) {
+    constexpr int d = decltype(d_)::value;
+    bid[d] = w + NW * d;
+    issue(d, bid[d]);
+  });
+  int prev = -1;  // the block whose scores acc holds (its appends run one block later)
+  bool first = true, more = nb > 0;
+  while (more) {
+    static_for<D>([&](auto d_) __attribute__((always_inline)) {
+      constexpr int d = decltype(d_)::value;
+      if (more && bid[d] >= nb) more = false;  // (wave-uniform)
+      if (more) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * KS) : "memory");
+#pragma unroll
+        for (int s = 0; s < KS; ++s) reg_tie(buf[d][s]);
+        const int b = bid[d];
+        const float shtau = read_shtau();
+        const float st = ssc[b >> 2] * tq;  // the block's 64-row scale tile x t
+        i32x4 ai = {0, 0, 0, 0};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          if (TT_I8R_EXP == 2)
+            ai += __builtin_bit_cast(i32x4, buf[d][s]);
+          else
+            ai = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, buf[d][s]),
+                                                       __builtin_bit_cast(i32x4, qf[s]), ai, 0,
+                                                       0, 0);
+        }
+        if (prev >= 0 && TT_I8R_EXP == 0) {
+          appends(acc, prev, first, shtau);
+          first = false;
+        }
+        if (TT_I8R_EXP && acc[0] == 1.2345f) tau_sh[0][w] = acc[1];  // keeps the work live
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) acc[jj] = (float)ai[jj] * st;
+        prev = b;
+        // the next block for this slot (past nb: reads 0 and ends the loop when reached)
+        int nx = 0;
+        if (lane == 0) nx = __hip_atomic_fetch_add(&next_blk, 1, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+        bid[d] = __builtin_amdgcn_readfirstlane(nx);
+        __builtin_amdgcn_sched_barrier(0);
+        issue(d, bid[d]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    });
+  }
+  if (prev >= 0 && TT_I8R_EXP == 0) appends(acc, prev, first, read_shtau());
+  // every load retired before its registers are given back
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) reg_tie(buf[d][s]);
+  // each wave cuts its own lists to their top 16 (in parallel), so the block's merge below
+  // selects from 8 x 16 keys per query instead of 8 full buffers
+  {
+    const uint64_t need = __ballot(lane < 16 && cnt > TM_M);
+    if (need != 0ull) {
+      lds_wait<0>();
+      uint64_t nd = need;
+      while (nd) {
+        const int c = __builtin_ctzll(nd);
+        nd &= nd - 1;
+        compact(c);
+      }
+    }
+  }
+  I8R_STAMP(2);
+  if (lane < nq && g == 0) ncw[w][lane] = cnt;
+  lds_wait<0>();
+  __syncthreads();
+  I8R_STAMP(3);
+  static_assert(NW * TM_M == 128, "the merge holds 2 keys per lane");
+  for (int c = w; c < nq; c += NW) {
+    uint64_t key[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {  // key e = 2 lane + r: wave e / 16's e % 16-th
+      const int e = 2 * lane + r, wb = e >> 4, idx = e & 15;
+      key[r] = idx < ncw[wb][c] ? tbuf[(wb * QB + c) * TMB + idx] : 0ull;
+    }
+    int nc;
+    const uint64_t k = wave_top16<2>(key, lane, tbuf + c * TMB, &nc);
+    if (lane < nc) {
+      tbuf[c * TMB + lane] = k;
+      lists[((int64_t)c * G + blk) * TM_M + lane] = k;
+    }
+    if (lane == 0) {
+      counts[(int64_t)c * G + blk] = nc;
+      ncs[c] = nc;
+    }
+  }
+  __syncthreads();
+  for (int c = w; c < nq; c += NW) {
+    const int nc = ncs[c], r16 = lane & 15, g4 = 4 * (lane >> 4);
+    if (nc == 0) continue;
+    const uint64_t* tb = tbuf + c * TMB;
+    const f32x4 ex =
+        exact16<EP>(db, ld, key_row(tb[r16 < nc ? r16 : 0]), q + (int64_t)c * ldq, lane);
+    if (r16 == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (g4 + j < nc)
+          xkeys[((int64_t)c * G + blk) * TM_M + g4 + j] =
+              ex[j] != ex[j] ? 0ull : make_key(ex[j], key_row(tb[g4 + j]));
+    }
+  }
+  I8R_STAMP(4);
+}
+
 // Final of the int8 single pass, one block per query: the union U of the G slab lists' exact
 // keys; S_k = the k-th best exact score of U (radix select on the exact keys); certified when
 // every full list's tau_b (its 16th approximate score) has tau_b + eps < S_k (see above);
@@ -4587,7 +5012,6 @@ extern "C" int tt_debug_i8_force_unsupported(int32_t on) {
   g_i8_force_unsupported = on != 0;
   return TT_OK;
 }
-
 // The shape limits of tt_scan_topk_i8f32 without a launch: the single-pass plan (nq <= 8,
 // device_cus() * TM_M <= TM_CAP, TT_FILTER_TOPM), the per-block scale-tile limit (rows per CU
 // <= 65536) and the 31-bit tile offsets.  1: the call would run, 0: it would return
@@ -4607,21 +5031,26 @@ extern "C" int tt_i8_single_pass_ok(int64_t n, int32_t d, int32_t nq, int32_t k,
   return ep > 0 && i8_single_pass_fits(n, ep, nq, k, ld_i8 > 0 ? ld_i8 : ep) ? 1 : 0;
 }
 
-extern "C" int tt_scan_topk_i8f32(const float* db, const int8_t* db_i8, const float* tile_scales,
-                                  int64_t n, int32_t d, int64_t ld_db, int64_t ld_i8,
-                                  int64_t row_base, const float* q, int32_t nq, int64_t ld_q,
-                                  int32_t k, float x_norm_max, float x_resid_max, float s_max,
-                                  float* out_score, int64_t* out_idx, void* workspace,
-                                  int64_t workspace_bytes, void* stream, void* ev_start,
-                                  void* ev_stop) {
+namespace {
+// tt_scan_topk_i8f32 (row-major image, LDS-ring stream k_filter_topm_i8) and
+// tt_scan_topk_i8t_f32 (tiled image, register-fed stream k_filter_topm_i8r): the same plan,
+// workspace, final and fallback
+int i8_single_pass(const float* db, const int8_t* img, bool tiled, const float* tile_scales,
+                   int64_t n, int32_t d, int64_t ld_db, int64_t ld_i8, int64_t row_base,
+                   const float* q, int32_t nq, int64_t ld_q, int32_t k, float x_norm_max,
+                   float x_resid_max, float s_max, float* out_score, int64_t* out_idx,
+                   void* workspace, int64_t workspace_bytes, void* stream, void* ev_start,
+                   void* ev_stop) {
   TT_REQUIRE(nq >= 0, "nq < 0");
   if (nq == 0) return TT_OK;
-  TT_REQUIRE(db != nullptr && db_i8 != nullptr && tile_scales != nullptr && out_score &&
+  TT_REQUIRE(db != nullptr && img != nullptr && tile_scales != nullptr && out_score &&
                  out_idx, "null pointer");
   const int ep = tt_padded_dim(d);
   if (ep != 384 && ep != 768) return fail(TT_ERR_UNSUPPORTED, "int8 single pass: E 384 / 768");
+  if (tiled && ep != 384) return fail(TT_ERR_UNSUPPORTED, "tiled int8 single pass: E 384");
   if (nq > TM_NQ_I8) return fail(TT_ERR_UNSUPPORTED, "int8 single pass: nq <= 8");
-  TT_REQUIRE(ld_i8 >= ep && ld_i8 % 16 == 0 && ((uintptr_t)db_i8 % 16) == 0,
+  if (tiled) ld_i8 = ep;
+  TT_REQUIRE(ld_i8 >= ep && ld_i8 % 16 == 0 && ((uintptr_t)img % 16) == 0,
              "int8 image: ld_i8 >= tt_padded_dim(d), multiple of 16, 16-B aligned");
   TT_REQUIRE(x_norm_max >= 0.0f && x_resid_max >= 0.0f && s_max >= 0.0f,
              "bounds must be >= 0 (tt_i8_image)");
@@ -4629,7 +5058,7 @@ extern "C" int tt_scan_topk_i8f32(const float* db, const int8_t* db_i8, const fl
   int epx;
   FilterPlan p;
   FilterWs w;
-  int rc = filter_setup(db, (const uint16_t*)db_i8, n, d, ld_db, q, nq, ld_q, k, workspace,
+  int rc = filter_setup(db, (const uint16_t*)img, n, d, ld_db, q, nq, ld_q, k, workspace,
                         workspace_bytes, &epx, &p, &w);
   if (rc) return rc;
   if (!p.topm) return fail(TT_ERR_UNSUPPORTED, "int8 single pass: not a single-pass plan");
@@ -4645,10 +5074,12 @@ extern "C" int tt_scan_topk_i8f32(const float* db, const int8_t* db_i8, const fl
   // candidate buffers laid out for 4 queries (4x the rows each) or for 8
   auto kern = ep == 384 ? (nq <= 4 ? k_filter_topm_i8<384, 4> : k_filter_topm_i8<384, TM_NQ_I8>)
                         : (nq <= 4 ? k_filter_topm_i8<768, 4> : k_filter_topm_i8<768, TM_NQ_I8>);
-  hipLaunchKernelGGL(kern, dim3(G), dim3(64 * TM_WAVES), 0, st, db_i8, ld_i8, tile_scales, n, q,
+  if (tiled)  // (rpb <= 65536 rows: a slab's tiled bytes fit the buffer resource's record count)
+    kern = nq <= 4 ? k_filter_topm_i8r<384, 4> : k_filter_topm_i8r<384, TM_NQ_I8>;
+  hipLaunchKernelGGL(kern, dim3(G), dim3(64 * TM_WAVES), 0, st, img, ld_i8, tile_scales, n, q,
                      nq, ld_q, (int)rpb, db, ld_db, x_norm_max, x_resid_max, s_max, w.eps2,
                      w.lists, xkeys, w.counts, w.flags, w.qsel_n);
-  if ((rc = check_launch("k_filter_topm_i8"))) return rc;
+  if ((rc = check_launch(tiled ? "k_filter_topm_i8r" : "k_filter_topm_i8"))) return rc;
   if (ev_stop && hipEventRecord((hipEvent_t)ev_stop, st) != hipSuccess)
     return fail(TT_ERR_LAUNCH, "hipEventRecord(stop)");
   if (ep == 384)
@@ -4662,6 +5093,31 @@ extern "C" int tt_scan_topk_i8f32(const float* db, const int8_t* db_i8, const fl
   if ((rc = check_launch("k_final_topm_i8"))) return rc;
   return scan_f32_select_fused(db, n, d, ld_db, row_base, q, nq, ld_q, k, w.qsel, w.qsel_n,
                                w.done, out_score, out_idx, w.scan_ws, w.scan_ws_bytes, st);
+}
+}  // namespace
+
+extern "C" int tt_scan_topk_i8f32(const float* db, const int8_t* db_i8, const float* tile_scales,
+                                  int64_t n, int32_t d, int64_t ld_db, int64_t ld_i8,
+                                  int64_t row_base, const float* q, int32_t nq, int64_t ld_q,
+                                  int32_t k, float x_norm_max, float x_resid_max, float s_max,
+                                  float* out_score, int64_t* out_idx, void* workspace,
+                                  int64_t workspace_bytes, void* stream, void* ev_start,
+                                  void* ev_stop) {
+  return i8_single_pass(db, db_i8, false, tile_scales, n, d, ld_db, ld_i8, row_base, q, nq, ld_q,
+                        k, x_norm_max, x_resid_max, s_max, out_score, out_idx, workspace,
+                        workspace_bytes, stream, ev_start, ev_stop);
+}
+
+extern "C" int tt_scan_topk_i8t_f32(const float* db, const int8_t* db_i8t,
+                                    const float* tile_scales, int64_t n, int32_t d, int64_t ld_db,
+                                    int64_t row_base, const float* q, int32_t nq, int64_t ld_q,
+                                    int32_t k, float x_norm_max, float x_resid_max, float s_max,
+                                    float* out_score, int64_t* out_idx, void* workspace,
+                                    int64_t workspace_bytes, void* stream, void* ev_start,
+                                    void* ev_stop) {
+  return i8_single_pass(db, db_i8t, true, tile_scales, n, d, ld_db, 0, row_base, q, nq, ld_q, k,
+                        x_norm_max, x_resid_max, s_max, out_score, out_idx, workspace,
+                        workspace_bytes, stream, ev_start, ev_stop);
 }
 
 // ------------------------------------------------------------------ sharded (multi-GPU)

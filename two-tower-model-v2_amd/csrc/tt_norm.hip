@@ -186,7 +186,47 @@ __global__ __launch_bounds__(256) void k_i8_image(const float* __restrict__ x, i
     atomicMax((unsigned int*)&out3[2], __float_as_uint(f64_up(sqrt(bs) * 1.000001)));
   }
 }
+
+// The tiled int8 image (tt_i8_tile) for the register-fed single pass (k_filter_topm_i8r): per
+// 16-row block KS = E / 64 pieces of 1 KB, piece s holding, for lane l = 16 g + col, row
+// 16 b + col's bytes 64 s + 16 g .. + 15 -- one MFMA operand per 16-B load, 1 KB contiguous
+// per wave instruction.  One thread per 16-B chunk; rows past n are zero.
+__global__ __launch_bounds__(256) void k_i8_tile(const int8_t* __restrict__ codes, int64_t ldc,
+                                                 int64_t n, int ep, int64_t chunks,
+                                                 int8_t* __restrict__ tiled) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= chunks) return;
+  const int64_t b = c / ep;  // 16-row block (ep chunks of 16 B each)
+  const int wi = (int)(c - b * ep), s = wi >> 6, l = wi & 63;
+  const int64_t row = 16 * b + (l & 15);
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (row < n) v = *(const uint4*)(codes + row * ldc + 64 * s + 16 * (l >> 4));
+  *(uint4*)(tiled + 16 * c) = v;
+}
 }  // namespace tt
+
+extern "C" int64_t tt_i8_tiled_bytes(int64_t n, int32_t d) {
+  const int ep = tt_padded_dim(d);
+  if (n < 0 || ep <= 0 || ep % 64 != 0) return -1;
+  return (n + 15) / 16 * 16 * (int64_t)ep;
+}
+
+extern "C" int tt_i8_tile(const int8_t* codes, int64_t ld_codes, int64_t n, int32_t d,
+                          int8_t* tiled, void* stream) {
+  using namespace tt;
+  const int ep = tt_padded_dim(d);
+  TT_REQUIRE(n >= 0 && ep > 0 && ep % 64 == 0, "need n >= 0 and tt_padded_dim(d) % 64 == 0");
+  if (n == 0) return TT_OK;
+  TT_REQUIRE(codes != nullptr && tiled != nullptr, "null pointer");
+  TT_REQUIRE(ld_codes >= ep && ld_codes % 16 == 0 && (uintptr_t)codes % 16 == 0 &&
+                 (uintptr_t)tiled % 16 == 0,
+             "ld_codes >= tt_padded_dim(d), multiple of 16; 16-B aligned buffers");
+  const int64_t chunks = (n + 15) / 16 * ep;
+  TT_REQUIRE((chunks + 255) / 256 < (1ll << 31), "too many rows");
+  hipLaunchKernelGGL(k_i8_tile, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, codes, ld_codes, n, ep, chunks, tiled);
+  return check_launch("tt_i8_tile");
+}
 
 extern "C" int tt_i8_image(const float* x, int64_t n, int32_t d, int64_t ld, int8_t* codes,
                            int64_t ld_codes, float* tile_scales, float* out3, void* stream) {

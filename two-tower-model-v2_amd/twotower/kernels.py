@@ -283,12 +283,30 @@ def i8_image(x: torch.Tensor, d: int, out3: torch.Tensor = None):
     return codes, scales, out3
 
 
+I8T_DIMS = (384,)  # padded dims of the tiled int8 image's register-fed stream
+
+
+def i8_tile(codes: torch.Tensor, n: int, d: int) -> torch.Tensor:
+    """The tiled int8 image (tt_i8_tile) of i8_image's codes: per 16-row block E / 64 pieces of
+    1 KB in MFMA operand order, for scan_topk_i8(tiled=...) / PreparedSearch at padded dim 384."""
+    if codes.dtype != torch.int8 or codes.dim() != 2 or codes.shape[0] < n:
+        raise ValueError("codes must be the int8 image [n, ep] (i8_image)")
+    nbytes = lib().tt_i8_tiled_bytes(n, d)
+    if nbytes < 0:
+        raise ValueError(f"i8_tile: padded dim of d = {d} is not a multiple of 64")
+    tiled = torch.empty(max(nbytes, 16), dtype=torch.int8, device=codes.device)
+    check(lib().tt_i8_tile(_ptr(codes), codes.stride(0), n, d, _ptr(tiled), stream_ptr()),
+          "tt_i8_tile")
+    return tiled
+
+
 def scan_topk_i8(db: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, n: int, d: int,
                  q: torch.Tensor, k: int, bounds3, row_base: int = 0,
-                 workspace: torch.Tensor = None, out=None, events=(None, None)):
+                 workspace: torch.Tensor = None, out=None, events=(None, None), tiled=None):
     """Exact top-k (bit-identical to scan_topk) for nq <= 8 through the int8 single pass
     (tt_scan_topk_i8f32): padded dim 384 / 768, k <= 128.  bounds3 = i8_image's out3 as host
-    floats."""
+    floats.  tiled = i8_tile(codes, ...) at padded dim 384: the register-fed stream over the
+    tiled image (tt_scan_topk_i8t_f32, same results)."""
     _check_2d(db, "db")
     _check_2d(q, "q")
     if codes.dtype != torch.int8 or codes.dim() != 2 or codes.shape[0] < n:
@@ -306,11 +324,20 @@ def scan_topk_i8(db: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, n:
         workspace = torch.empty(need, dtype=torch.uint8, device=q.device)
     X, R, S = (float(v) for v in bounds3)
     e0, e1 = events
+    ev = (e0.cuda_event if e0 is not None else None, e1.cuda_event if e1 is not None else None)
+    if tiled is not None and _lib.padded_dim(d) in I8T_DIMS:
+        if tiled.dtype != torch.int8 or tiled.numel() < lib().tt_i8_tiled_bytes(n, d):
+            raise ValueError("tiled must be i8_tile(codes, n, d)")
+        check(lib().tt_scan_topk_i8t_f32(
+            _ptr(db), _ptr(tiled), _ptr(scales), n, d, db.stride(0), row_base, _ptr(q), nq,
+            q.stride(0), k, ctypes.c_float(X), ctypes.c_float(R), ctypes.c_float(S),
+            _ptr(out[0]), _ptr(out[1]), _ptr(workspace), workspace.numel(), stream_ptr(), *ev),
+            "tt_scan_topk_i8t_f32")
+        return out
     check(lib().tt_scan_topk_i8f32(
         _ptr(db), _ptr(codes), _ptr(scales), n, d, db.stride(0), codes.stride(0), row_base,
         _ptr(q), nq, q.stride(0), k, ctypes.c_float(X), ctypes.c_float(R), ctypes.c_float(S),
-        _ptr(out[0]), _ptr(out[1]), _ptr(workspace), workspace.numel(), stream_ptr(),
-        e0.cuda_event if e0 is not None else None, e1.cuda_event if e1 is not None else None),
+        _ptr(out[0]), _ptr(out[1]), _ptr(workspace), workspace.numel(), stream_ptr(), *ev),
         "tt_scan_topk_i8f32")
     return out
 
@@ -324,8 +351,9 @@ class PreparedSearch:
 
     def __init__(self, db: torch.Tensor, db16: torch.Tensor, n: int, d: int, nq: int, k: int,
                  bounds, row_base: int = 0, i8=None):
-        """i8 = (codes, scales, bounds3) from i8_image: nq <= 8 at padded dim 384 / 768 then
-        runs the int8 single pass (tt_scan_topk_i8f32, same results)."""
+        """i8 = (codes, scales, bounds3[, tiled]) from i8_image (+ i8_tile): nq <= 8 at padded
+        dim 384 / 768 then runs the int8 single pass (tt_scan_topk_i8f32; with the tiled image
+        at 384, tt_scan_topk_i8t_f32 -- same results)."""
         _check_2d(db, "db")
         _check_2d(db16, "db16", torch.bfloat16)
         if db16.shape[0] < n or db16.stride(0) != db.stride(0):
@@ -346,12 +374,17 @@ class PreparedSearch:
         self.i8 = (i8 is not None and nq <= I8_NQ_MAX and self.ld_q in I8_DIMS
                    and i8_single_pass_ok(n, d, nq, k, i8[0].stride(0)))
         if self.i8:
-            codes, scales, b3 = i8
+            codes, scales, b3 = i8[:3]
+            tiled = i8[3] if len(i8) > 3 else None
             X, R, S = (float(v) for v in b3)
-            self._keep = (codes, scales)
-            self._fn = lib().tt_scan_topk_i8f32
-            self._head = (_ptr(db), _ptr(codes), _ptr(scales), n, d, db.stride(0),
-                          codes.stride(0), row_base)
+            self._keep = (codes, scales, tiled)
+            if tiled is not None and self.ld_q in I8T_DIMS:
+                self._fn = lib().tt_scan_topk_i8t_f32
+                self._head = (_ptr(db), _ptr(tiled), _ptr(scales), n, d, db.stride(0), row_base)
+            else:
+                self._fn = lib().tt_scan_topk_i8f32
+                self._head = (_ptr(db), _ptr(codes), _ptr(scales), n, d, db.stride(0),
+                              codes.stride(0), row_base)
             self._tail = (k, ctypes.c_float(X), ctypes.c_float(R), ctypes.c_float(S),
                           _ptr(self.out[0]), _ptr(self.out[1]), _ptr(self.ws), self.ws.numel())
 

@@ -113,12 +113,15 @@ class FlatIPIndex:
             return (self.xb, self.xb16, self.ntotal, self.bounds, i8, self.version)
 
     def _i8_image(self, rows: torch.Tensor):
-        """(codes, tile scales, bounds) of the int8 single pass for one-buyer searches
-        (kernels.i8_image; padded dims 384 / 768), or None."""
+        """(codes, tile scales, bounds, tiled) of the int8 single pass for one-buyer searches
+        (kernels.i8_image; padded dims 384 / 768), or None.  tiled = the MFMA-ordered copy of
+        the codes (kernels.i8_tile) the register-fed stream reads at padded dim 384, else None."""
         if self.ep not in kernels.I8_DIMS or rows.shape[0] == 0:
             return None
+        n = rows.shape[0]
         codes, scales, b3 = kernels.i8_image(rows, self.d)
-        return codes, scales, tuple(b3.tolist())
+        tiled = kernels.i8_tile(codes, n, self.d) if self.ep in kernels.I8T_DIMS else None
+        return codes, scales, tuple(b3.tolist()), tiled
 
     def build_i8(self) -> None:
         """(Re)build the int8 image of the current rows (for an index whose xb was set
@@ -173,9 +176,9 @@ class FlatIPIndex:
             if (i8 is not None and q.shape[0] <= kernels.I8_NQ_MAX
                     and kernels.i8_single_pass_ok(self.ntotal, self.d, q.shape[0], k,
                                                   i8[0].stride(0))):
-                codes, scales, b3 = i8  # one-buyer calls: the int8 single pass
+                codes, scales, b3, tiled = i8  # one-buyer calls: the int8 single pass
                 return kernels.scan_topk_i8(self.xb, codes, scales, self.ntotal, self.d, q, k, b3,
-                                            row_base=self.row_base, workspace=ws)
+                                            row_base=self.row_base, workspace=ws, tiled=tiled)
             if use_bf16:  # (a large batch runs its sample level on the int8 image, if any)
                 return kernels.scan_topk_bf16(self.xb, self.xb16, self.ntotal, self.d, q, k,
                                               self.bounds, row_base=self.row_base, workspace=ws,
@@ -459,15 +462,23 @@ class _ServingSlot:
             qp, st = vp(self.q.data_ptr()), vp(self.stream.cuda_stream)
             sp, ip = vp(self.dout.data_ptr()), vp(self.dout.data_ptr() + o8)
             if use8:  # the int8 single pass (one-buyer /retrieve calls, nq <= 8)
-                codes, scales, (X, R, S) = i8
-                self.fn = _lib.lib().tt_scan_topk_i8f32
-                self.args = (
-                    vp(xb.data_ptr()), vp(codes.data_ptr()), vp(scales.data_ptr()), n, d,
-                    xb.stride(0), codes.stride(0), ix.row_base, qp, nq, self.q.stride(0), k,
-                    ctypes.c_float(X), ctypes.c_float(R), ctypes.c_float(S), sp, ip,
-                    vp(ws.data_ptr()), ws.numel(), st, None, None)
+                codes, scales, (X, R, S), tiled = i8
+                if tiled is not None:  # padded dim 384: the register-fed stream, tiled image
+                    self.fn = _lib.lib().tt_scan_topk_i8t_f32
+                    self.args = (
+                        vp(xb.data_ptr()), vp(tiled.data_ptr()), vp(scales.data_ptr()), n, d,
+                        xb.stride(0), ix.row_base, qp, nq, self.q.stride(0), k,
+                        ctypes.c_float(X), ctypes.c_float(R), ctypes.c_float(S), sp, ip,
+                        vp(ws.data_ptr()), ws.numel(), st, None, None)
+                else:
+                    self.fn = _lib.lib().tt_scan_topk_i8f32
+                    self.args = (
+                        vp(xb.data_ptr()), vp(codes.data_ptr()), vp(scales.data_ptr()), n, d,
+                        xb.stride(0), codes.stride(0), ix.row_base, qp, nq, self.q.stride(0), k,
+                        ctypes.c_float(X), ctypes.c_float(R), ctypes.c_float(S), sp, ip,
+                        vp(ws.data_ptr()), ws.numel(), st, None, None)
             elif i8 is not None:  # a large batch's sample level on the int8 image (same results)
-                codes, scales, _ = i8
+                codes, scales = i8[0], i8[1]
                 self.fn = _lib.lib().tt_scan_topk_bf16f32_i8s
                 self.args = (
                     vp(xb.data_ptr()), vp(xb16.data_ptr()), vp(codes.data_ptr()),
