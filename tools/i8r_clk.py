@@ -27,13 +27,15 @@ def main():
     q = torch.randn((1, E), generator=g, device=dev)
     kernels.l2norm_rows(q, E, _lib.TT_NORM_ADD_EPS, out=q)
     L = _lib.lib()
-    buf = (ctypes.c_ulonglong * (256 * 8))()
+    buf = (ctypes.c_ulonglong * (256 * 8 + 8))()
     out = {}
     for rep in range(5):
         kernels.scan_topk_i8(x, codes, scales, N, E, q, K, b3.tolist(), tiled=tiled)
         torch.cuda.synchronize()
     assert L.tt_debug_i8r_clk(buf) == 0
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 8)[:, :5].astype(np.float64)
+    allv = np.frombuffer(buf, dtype=np.uint64)
+    a = allv[:256 * 8].reshape(256, 8)[:, :5].astype(np.float64)
+    f = allv[256 * 8:256 * 8 + 5].astype(np.float64)
     t0 = a[:, 0].min()
     us = (a - t0) / 100.0  # 100 MHz -> us
     for i, name in enumerate(("start", "prologue_done", "loop_done", "merge_barrier", "end")):
@@ -44,6 +46,10 @@ def main():
     for i, name in enumerate(("prologue", "loop", "merge_wait", "epilogue")):
         out["dur_" + name] = {"median": round(float(np.median(d[:, i])), 2),
                               "max": round(float(d[:, i].max()), 2)}
+    fd = np.diff(f) / 100.0
+    out["final"] = {"start_after_stream_end_max_us": round((f[0] - a[:, 4].max()) / 100.0, 2),
+                    "load_reduce": round(fd[0], 2), "select": round(fd[1], 2),
+                    "cert_band": round(fd[2], 2), "rank_out": round(fd[3], 2)}
     print(json.dumps(out, indent=1))
 
 

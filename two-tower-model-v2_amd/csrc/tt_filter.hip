@@ -3082,15 +3082,27 @@ TT_CHECK_EXP(TT_I8R_EXP, "TT_I8R_EXP");
 TT_CHECK_EXP(TT_I8R_CLK, "TT_I8R_CLK");
 #if TT_I8R_CLK
 __device__ unsigned long long g_i8rclk[256 * 8];
+__device__ unsigned long long g_i8fclk[8];  // k_final_topm_i8, query 0
 extern "C" int tt_debug_i8r_clk(unsigned long long* host) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_i8rclk), sizeof(g_i8rclk)) == hipSuccess ? 0 : -2;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_i8rclk), sizeof(g_i8rclk)) == hipSuccess &&
+                 hipMemcpyFromSymbol(host + 256 * 8, HIP_SYMBOL(g_i8fclk), sizeof(g_i8fclk)) ==
+                     hipSuccess
+             ? 0
+             : -2;
 }
+#define I8F_STAMP(i)                                                               \
+  do {                                                                             \
+    if (tid == 0 && qid == 0) g_i8fclk[i] = __builtin_amdgcn_s_memrealtime();      \
+  } while (0)
 #define I8R_STAMP(i)                                                               \
   do {                                                                             \
     if (tid == 0 && blk < 256) g_i8rclk[blk * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
 #define I8R_STAMP(i) \
+  do {               \
+  } while (0)
+#define I8F_STAMP(i) \
   do {               \
   } while (0)
 #endif
@@ -3131,6 +3143,34 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8r(
   const int64_t j0 = (int64_t)blk * rows_per_blk;  // rows_per_blk: a multiple of 64
   const int64_t j1 = (j0 + rows_per_blk < n) ? j0 + rows_per_blk : n;
   const int nb = j0 < j1 ? (int)((j1 - j0 + 15) / 16) : 0;  // 16-row blocks of the slab
+  // the slab's blocks as a bounded buffer resource (the tiled image pads the last block)
+  const uint64_t sbase = (uint64_t)(uintptr_t)(xt + j0 * EP);
+  i8r_v4i rs;
+  rs[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)sbase);
+  rs[1] = __builtin_amdgcn_readfirstlane((int)((uint32_t)(sbase >> 32) & 0xffffu));
+  // (slabs past the catalog end -- j0 >= n at 1M rows over 256 CUs -- get 0 records: every load
+  // of theirs reads 0 and touches no memory)
+  rs[2] = __builtin_amdgcn_readfirstlane(nb * BLK);
+  rs[3] = 0x00020000;
+  u32x4 buf[D][KS];
+  auto issue = [&](int slot, int b) __attribute__((always_inline)) {  // 16-row block b
+    // (piece s at bo + 4096 (s / 4) + immediate 1024 (s % 4): the immediate is 12 bits)
+    const uint32_t bo = (uint32_t)(b * BLK + 16 * lane), bo4 = bo + 4096u;
+    static_assert(KS == 6, "six pieces per block");
+#define TT_I8R_LD(S)                                                          \
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3 nt"         \
+               : "=v"(buf[slot][S])                                           \
+               : "v"((S) < 4 ? bo : bo4), "s"(rs), "n"(1024 * ((S) % 4))      \
+               : "memory")
+    TT_I8R_LD(0);
+    TT_I8R_LD(1);
+    TT_I8R_LD(2);
+    TT_I8R_LD(3);
+    TT_I8R_LD(4);
+    TT_I8R_LD(5);
+#undef TT_I8R_LD
+  };
+
   for (int i = tid; i < (rows_per_blk >> 6); i += 64 * NW) {
     const int64_t st = (j0 >> 6) + i;
     ssc[i] = st < ((n + 63) >> 6) ? scales[st] : 0.0f;
@@ -3236,34 +3276,6 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8r(
   wait_vm<0>();  // (the eps store retired: the loop's counted waits see only its own loads)
   I8R_STAMP(1);
 
-  // the slab's blocks as a bounded buffer resource (the tiled image pads the last block)
-  const uint64_t sbase = (uint64_t)(uintptr_t)(xt + j0 * EP);
-  i8r_v4i rs;
-  rs[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)sbase);
-  rs[1] = __builtin_amdgcn_readfirstlane((int)((uint32_t)(sbase >> 32) & 0xffffu));
-  // (slabs past the catalog end -- j0 >= n at 1M rows over 256 CUs -- get 0 records: every load
-  // of theirs reads 0 and touches no memory)
-  rs[2] = __builtin_amdgcn_readfirstlane(nb * BLK);
-  rs[3] = 0x00020000;
-  u32x4 buf[D][KS];
-  auto issue = [&](int slot, int b) __attribute__((always_inline)) {  // 16-row block b
-    // (piece s at bo + 4096 (s / 4) + immediate 1024 (s % 4): the immediate is 12 bits)
-    const uint32_t bo = (uint32_t)(b * BLK + 16 * lane), bo4 = bo + 4096u;
-    static_assert(KS == 6, "six pieces per block");
-#define TT_I8R_LD(S)                                                          \
-  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3 nt"         \
-               : "=v"(buf[slot][S])                                           \
-               : "v"((S) < 4 ? bo : bo4), "s"(rs), "n"(1024 * ((S) % 4))      \
-               : "memory")
-    TT_I8R_LD(0);
-    TT_I8R_LD(1);
-    TT_I8R_LD(2);
-    TT_I8R_LD(3);
-    TT_I8R_LD(4);
-    TT_I8R_LD(5);
-#undef TT_I8R_LD
-  };
-
   static_assert(TM_M == 16, "wave_top16 keeps 16");
   auto compact = [&](int c) __attribute__((always_inline)) {
     uint64_t* b = wbuf + c * TMB;
@@ -3365,6 +3377,8 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8r(
   // TT_I8R_CLK at 1M rows).  Claims are made in processing order and only grow, so the first
   // slot holding a block >= nb ends the wave's loop; its later slots hold larger blocks.
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  // (issuing these before the prologue, so their round trip overlaps the query's, measured
+  // neutral: prologue 2.5 -> 7.7 us, loop 52.8 -> 47.8 us -- the stream is HBM-bound throughout)
   int bid[D];
   static_for<D>([&](auto d_) __attribute__((always_inline)) {
     constexpr int d = decltype(d_)::value;
@@ -3491,6 +3505,7 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_topm_i8(
   __shared__ BandLds<EP> bl;
   __shared__ uint32_t taus[SM_WAVES];
   const int qid = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  I8F_STAMP(0);
   uint32_t h[PER];
   uint64_t xk[PER];
   {
@@ -3538,7 +3553,9 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_topm_i8(
     if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
     return;
   }
+  I8F_STAMP(1);
   const float Sk = key_float(small_radix_select(h, k, s, hmax));
+  I8F_STAMP(2);
   // certification: a row dropped by slab b has exact score <= tau_b + eps (strictly below S_k)
   if (tau_max != 0u && !(key_float(tau_max) + eps1[qid] < Sk)) {
     if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
@@ -3561,7 +3578,9 @@ __global__ __launch_bounds__(SM_THREADS) void k_final_topm_i8(
     if (tid == 0) flag_query(qid, flags, qsel, qsel_n);
     return;
   }
+  I8F_STAMP(3);
   band_rank_out<EP>(bl, nb, qid, k, row_base, out_s, out_i);
+  I8F_STAMP(4);
 }
 
 // ------------------------------------------ the batched sample level on the int8 image
