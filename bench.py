@@ -325,8 +325,8 @@ def batch_sweep(a, shard, shard16, n, E, K, bounds, dev, i8=None):
             tot.append(ev[2].elapsed_time(ev[3]))
             lvl.append(ev[0].elapsed_time(ev[1]))
         tw, l_ = float(np.median(tot)), float(np.median(lvl))
-        # end to end through the serving path (one PreparedSearch call per batch; nq <= 8 takes
-        # the int8 single pass when the catalog has its image, same results)
+        # end to end through the serving path (one PreparedSearch call per batch; nq <= 32
+        # takes the int8 single pass over the tiled image when the catalog has it, same results)
         def prepared(i8_):
             ps = kernels.PreparedSearch(shard, shard16, n, E, B, K, bounds, i8=i8_)
             for _ in range(3):
@@ -343,7 +343,7 @@ def batch_sweep(a, shard, shard16, n, E, K, bounds, dev, i8=None):
 
         t16, _, o16 = prepared(None)
         t, extra = t16, {}
-        if i8 is not None and B <= kernels.I8_NQ_MAX:
+        if kernels.i8_pass_ok(n, E, B, K, i8):
             t8, used, o8 = prepared(i8)
             if used:
                 assert torch.equal(o8[0], o16[0]) and torch.equal(o8[1], o16[1])

@@ -165,11 +165,14 @@ int tt_scan_topk_i8f32(const float* db, const int8_t* db_i8, const float* tile_s
                        float x_resid_max, float s_max, float* out_score, int64_t* out_idx,
                        void* workspace, int64_t workspace_bytes, void* stream, void* ev_start,
                        void* ev_stop);
-/* The same search over the TILED int8 image (tt_i8_tile; padded dim 384 only): each of a
- * block's 8 waves streams its own 16-row blocks straight into MFMA operands (1 KB contiguous per
- * load instruction, no LDS staging, no block barrier).  Same results bit for bit as
- * tt_scan_topk_i8f32 and tt_scan_topk_f32; same workspace, limits and fallback;
- * TT_ERR_UNSUPPORTED at other padded dims (callers then take tt_scan_topk_i8f32). */
+/* The same search over the TILED int8 image (tt_i8_tile; padded dim 384 only), for nq <= 32:
+ * each of a block's 8 waves streams its own 16-row blocks straight into MFMA operands (1 KB
+ * contiguous per load instruction, no LDS staging, no block barrier), 9-32 queries as two
+ * 16-query MFMA blocks per row block.  Same results bit for bit as tt_scan_topk_i8f32 and
+ * tt_scan_topk_f32; same workspace (tt_filter_workspace_bytes), certification and fallback;
+ * TT_ERR_UNSUPPORTED outside the shape tt_i8t_single_pass_ok(n, d, nq, k) accepts (callers
+ * then take tt_scan_topk_i8f32 or tt_scan_topk_bf16f32). */
+int tt_i8t_single_pass_ok(int64_t n, int32_t d, int32_t nq, int32_t k);
 int tt_scan_topk_i8t_f32(const float* db, const int8_t* db_i8t, const float* tile_scales,
                          int64_t n, int32_t d, int64_t ld_db, int64_t row_base, const float* q,
                          int32_t nq, int64_t ld_q, int32_t k, float x_norm_max,

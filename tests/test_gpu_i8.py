@@ -86,12 +86,15 @@ def test_i8_tile_vs_numpy(K, oracle_mod, n, d):
 
 @pytest.mark.parametrize("n,nq,k", [(100_000, 1, 100), (300_001, 4, 128), (1000, 2, 10),
                                     (5, 1, 3), (257, 1, 128), (70_001, 3, 1),
-                                    (1_000_000, 1, 100), (200_000, 5, 100), (1_000_000, 8, 100)])
+                                    (1_000_000, 1, 100), (200_000, 5, 100), (1_000_000, 8, 100),
+                                    (100_000, 9, 100), (1_000_000, 16, 100), (33_333, 17, 64),
+                                    (1_000_000, 32, 100), (4097, 31, 128), (20, 32, 20)])
 def test_scan_topk_i8_tiled_bit_exact(K, oracle_mod, n, nq, k):
     """The register-fed stream over the tiled image (tt_scan_topk_i8t_f32, padded dim 384):
-    bit-exact against the oracle and identical to the LDS-ring stream over the row-major
-    image, fallback counts included; tiny catalogs leave most waves without a block (n = 5:
-    one block in one wave of the whole grid) and at 1M rows the last slabs hold no rows."""
+    bit-exact against the oracle and, for nq <= 8, identical to the LDS-ring stream over the
+    row-major image, fallback counts included; tiny catalogs leave most waves without a block
+    (n = 5: one block in one wave of the whole grid), at 1M rows the last slabs hold no rows,
+    and 9-32 queries run as one or two 16-query MFMA blocks."""
     d = 384
     rng = np.random.default_rng(n + 7 * nq + k)
     x = oracle_mod.l2norm_rows(rng.standard_normal((n, d)).astype(np.float32), 0)
@@ -102,13 +105,44 @@ def test_scan_topk_i8_tiled_bit_exact(K, oracle_mod, n, nq, k):
     ws = torch.empty(K.filter_workspace_bytes(n, d, nq, k), dtype=torch.uint8, device="cuda")
     out = {}
     for name, t in (("tiled", tiled), ("ring", None)):
+        if t is None and nq > K.I8_NQ_MAX:
+            continue
         s, i = K.scan_topk_i8(db, codes, scales, n, d, qd, k, b3.tolist(), workspace=ws, tiled=t)
         out[name] = (s.cpu().numpy(), i.cpu().numpy(), K.filter_fallback_count(ws, n, d, nq, k))
     rs, ri = oracle_mod.scan_topk(x, q, k)
     assert np.array_equal(out["tiled"][1], ri) and np.array_equal(out["tiled"][0], rs)
-    assert out["tiled"][2] == out["ring"][2]
-    assert np.array_equal(out["tiled"][1], out["ring"][1])
-    assert np.array_equal(out["tiled"][0], out["ring"][0])
+    if "ring" in out:
+        assert out["tiled"][2] == out["ring"][2]
+        assert np.array_equal(out["tiled"][1], out["ring"][1])
+        assert np.array_equal(out["tiled"][0], out["ring"][0])
+    if n >= 100_000:  # iid rows: every query certifies
+        assert out["tiled"][2] == 0
+
+
+def test_scan_topk_i8_tiled_32_queries_nan_clustered_mode_b(K, oracle_mod):
+    """32 queries over the tiled image (two 16-query blocks) on the hard cases at once: Mode B
+    buyers, a NaN query in the second block, and one query with 400 near-copies in one slab
+    (cannot certify: falls back alone); every result bit-exact."""
+    n, d, k = 300_000, 384, 100
+    rng = np.random.default_rng(21)
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    q = np.empty((32, d), np.float32)
+    h = rng.integers(0, n, (32, 20))
+    w = np.where(rng.random((32, 20)) < 0.75, 1.0, 5.0).astype(np.float32)
+    xn = oracle_mod.l2norm_rows(x, 0)
+    q[:] = oracle_mod.weighted_avg_l2(xn[h], w)
+    x[5000:5400] = q[7] + 0.05 * rng.standard_normal((400, d)).astype(np.float32)
+    x = oracle_mod.l2norm_rows(x, 0)
+    q = oracle_mod.l2norm_rows(q, 0)
+    q[20, 3] = np.nan
+    db = dev_rows(x)
+    codes, scales, b3 = K.i8_image(db, d)
+    ws = torch.empty(K.filter_workspace_bytes(n, d, 32, k), dtype=torch.uint8, device="cuda")
+    s, i = K.scan_topk_i8(db, codes, scales, n, d, dev_rows(q), k, b3.tolist(), workspace=ws,
+                          tiled=K.i8_tile(codes, n, d))
+    rs, ri = oracle_mod.scan_topk(x, q, k)
+    assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(s.cpu().numpy(), rs)
+    assert 1 <= K.filter_fallback_count(ws, n, d, 32, k) <= 2  # query 7 (and the NaN query)
 
 
 def test_scan_topk_i8_tiled_nan_and_clustered(K, oracle_mod):

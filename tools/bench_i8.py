@@ -49,7 +49,7 @@ def main():
                          (codes, scales, b3) + ((tiled,) if v == "tiled" else ()),
                          tiled if v == "tiled" else None))
         for name, i8, tl in runs:
-            if i8 is not None and nq > kernels.I8_NQ_MAX:
+            if i8 is not None and nq > (kernels.I8T_NQ_MAX if tl is not None else kernels.I8_NQ_MAX):
                 continue
             ps = kernels.PreparedSearch(x, x16, N, E, nq, K, bnd, i8=i8)
             assert ps.i8 == (i8 is not None)

@@ -24,7 +24,8 @@ def main():
     kernels.l2norm_rows(x, E, _lib.TT_NORM_ADD_EPS, out=x)
     codes, scales, b3 = kernels.i8_image(x, E)
     tiled = kernels.i8_tile(codes, N, E)
-    q = torch.randn((1, E), generator=g, device=dev)
+    NQ = int(os.environ.get("NQ", 1))
+    q = torch.randn((NQ, E), generator=g, device=dev)
     kernels.l2norm_rows(q, E, _lib.TT_NORM_ADD_EPS, out=q)
     L = _lib.lib()
     buf = (ctypes.c_ulonglong * (256 * 8 + 8))()
@@ -35,6 +36,7 @@ def main():
     assert L.tt_debug_i8r_clk(buf) == 0
     allv = np.frombuffer(buf, dtype=np.uint64)
     a = allv[:256 * 8].reshape(256, 8)[:, :5].astype(np.float64)
+    cnts = allv[:256 * 8].reshape(256, 8)[:, 5:7]
     f = allv[256 * 8:256 * 8 + 5].astype(np.float64)
     t0 = a[:, 0].min()
     us = (a - t0) / 100.0  # 100 MHz -> us
@@ -46,6 +48,11 @@ def main():
     for i, name in enumerate(("prologue", "loop", "merge_wait", "epilogue")):
         out["dur_" + name] = {"median": round(float(np.median(d[:, i])), 2),
                               "max": round(float(d[:, i].max()), 2)}
+    t7 = allv[:256 * 8].reshape(256, 8)[:, 7].astype(np.float64)
+    out["dur_merge"] = {"median": round(float(np.median((t7 - a[:, 3]) / 100.0)), 2)}
+    out["dur_exact16"] = {"median": round(float(np.median((a[:, 4] - t7) / 100.0)), 2)}
+    out["wave0_compactions_median"] = float(np.median(cnts[:, 0]))
+    out["wave0_append_blocks_median"] = float(np.median(cnts[:, 1]))
     fd = np.diff(f) / 100.0
     out["final"] = {"start_after_stream_end_max_us": round((f[0] - a[:, 4].max()) / 100.0, 2),
                     "load_reduce": round(fd[0], 2), "select": round(fd[1], 2),

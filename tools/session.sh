@@ -75,6 +75,10 @@ for s in "$@"; do
         N=$nn TWOTOWER_HIP_LIB=$PWD/two-tower-model-v2_amd/lib/variants/lib_clk.so \
           step i8r_clk_$nn 120 python3 -u tools/i8r_clk.py; cat "$OUT/i8r_clk_$nn.log"
       done ;;
+    i8r_clk_nq) for nq in 1 16 32; do
+        NQ=$nq TWOTOWER_HIP_LIB=$PWD/two-tower-model-v2_amd/lib/variants/lib_clk.so \
+          step i8r_clk_nq$nq 120 python3 -u tools/i8r_clk.py
+      done ;;
     i8r_prof) step i8r_prof 300 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d "$OUT/i8r_prof" -o run -- python3 tools/bench_i8.py ;;
     bench) step bench 600 python3 bench.py --steps 20 --warmup 5 ;;

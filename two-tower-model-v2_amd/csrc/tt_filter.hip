@@ -3113,7 +3113,16 @@ struct I8RegCfg {
 };
 typedef int32_t i8r_v4i __attribute__((ext_vector_type(4)));
 
-template <int EP, int QB>
+// Up to 32 queries (round 6): NQB = 2 runs two 16-query MFMA blocks on every row block (12
+// MFMAs), each with its own tau / tile-max state and candidate lists; with no LDS ring the
+// candidate buffers get 128 KB (QB = 16 / 32: 128 / 64 keys per wave and query), so 9-32
+// queries stay off the multi-level ladder too.
+constexpr int TM_NQ_I8T = 32;  // queries of the tiled int8 single pass
+template <int QB>
+constexpr int i8r_keys() {  // candidate-buffer keys of k_filter_topm_i8r
+  return QB <= 8 ? TM_NQ * TM_BUF : 16384;
+}
+template <int EP, int QB, int NQB>
 __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8r(
     const int8_t* __restrict__ xt, int64_t /*unused*/, const float* __restrict__ scales,
     int64_t n, const float* __restrict__ q, int nq, int64_t ldq, int rows_per_blk,
@@ -3121,13 +3130,18 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8r(
     float* __restrict__ eps1, uint64_t* __restrict__ lists, uint64_t* __restrict__ xkeys,
     int* __restrict__ counts, int* __restrict__ flags, int* __restrict__ qsel_n) {
   constexpr int KS = EP / 64, NW = TM_WAVES, D = I8RegCfg<EP>::D, BLK = 16 * EP;
-  constexpr int TMB = TM_NQ * TM_BUF / QB / NW, CPER = TMB / 64;
-  static_assert(TMB % 64 == 0 && TMB >= 2 * TM_M && QB <= 16, "top-m buffer shape");
-  __shared__ __attribute__((aligned(16))) uint64_t tbuf[TM_NQ * TM_BUF];  // [NW][QB][TMB]
-  __shared__ int ncs[TM_NQ];
-  __shared__ int ncw[NW][TM_NQ];
+  constexpr int TMB = i8r_keys<QB>() / QB / NW, CPER = TMB / 64, NQ16 = 16 * NQB;
+  // a query's buffer every CS keys: the 2-key pad puts the 16 columns' appends (one ds_write
+  // per row of the lane) on 16 different bank pairs instead of one bank (TMB * 8 B = 0 mod 256)
+  constexpr int CS = TMB + 2;
+  static_assert(TMB % 64 == 0 && TMB >= 2 * TM_M && QB <= NQ16 && NQ16 <= QB * 4,
+                "top-m buffer shape");
+  __shared__ __attribute__((aligned(16))) uint64_t tbuf[NW * QB * CS];  // [NW][QB][CS]
+  __shared__ int ncs[QB];
+  __shared__ int ncw[NW][QB];
   __shared__ float ssc[I8_MAXTILES];
   __shared__ __attribute__((aligned(16))) float tau_sh[QB][NW];
+  __shared__ __attribute__((aligned(16))) float t2_sh[QB][NW];  // each wave's 2nd-largest tm
   __shared__ int next_blk;  // the next unclaimed 16-row block of the slab
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -3175,111 +3189,148 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8r(
     const int64_t st = (j0 >> 6) + i;
     ssc[i] = st < ((n + 63) >> 6) ? scales[st] : 0.0f;
   }
-  if (lane < QB) tau_sh[lane][w] = -__builtin_huge_valf();
-  uint64_t* wbuf = tbuf + w * QB * TMB;  // [QB][TMB] of this wave
-  const bool qv = col < nq;
-  float tau = qv ? -__builtin_huge_valf() : __builtin_huge_valf();
-  int cnt = 0;
-  float tm[16];  // the tile-max bound's set, ascending (k_filter_topm_i8)
+  if (lane < QB) {
+    tau_sh[lane][w] = -__builtin_huge_valf();
+    t2_sh[lane][w] = -__builtin_huge_valf();
+  }
+  uint64_t* wbuf = tbuf + w * QB * CS;  // [QB][CS] of this wave
+  // per query block qb (queries 16 qb + col): validity, tau, count, the tile-max set
+  bool qv[NQB];
+  float tau[NQB];
+  int cnt[NQB];
+  float tm[NQB][16];  // the tile-max bound's sets, ascending (k_filter_topm_i8)
 #pragma unroll
-  for (int i = 0; i < 16; ++i) tm[i] = -__builtin_huge_valf();
-  auto tm_insert = [&](float m) __attribute__((always_inline)) {
+  for (int qb = 0; qb < NQB; ++qb) {
+    qv[qb] = 16 * qb + col < nq;
+    tau[qb] = qv[qb] ? -__builtin_huge_valf() : __builtin_huge_valf();
+    cnt[qb] = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) tm[qb][i] = -__builtin_huge_valf();
+  }
+  auto tm_insert = [&](int qb, float m) __attribute__((always_inline)) {
     m = m == m ? m : -__builtin_huge_valf();
 #pragma unroll
-    for (int i = 0; i < 15; ++i) tm[i] = __builtin_amdgcn_fmed3f(tm[i], m, tm[i + 1]);
-    tm[15] = fmaxf(tm[15], m);
+    for (int i = 0; i < 15; ++i) tm[qb][i] = __builtin_amdgcn_fmed3f(tm[qb][i], m, tm[qb][i + 1]);
+    tm[qb][15] = fmaxf(tm[qb][15], m);
   };
-  auto read_shtau = [&]() __attribute__((always_inline)) {
-    const f32x4* p = (const f32x4*)&tau_sh[col < QB ? col : 0][0];
+  // The block's shared bound for query c: the largest of the waves' taus, and the smallest of
+  // the waves' second-largest tile-max entries -- the 8 waves' two largest entries are the
+  // scores of 16 distinct rows of the slab (disjoint blocks per wave, distinct rows within a
+  // set), all >= that minimum, so the slab's 16th best is too.  (Each wave's own 16th of ~46
+  // entries sat near the rows' 85th percentile: ~80 appends per wave and query, and at 32
+  // queries 56 compactions per wave; TT_I8R_CLK.)
+  static_assert(2 * NW == TM_M, "the waves' two largest entries make 16 rows");
+  auto read_shtau = [&](int qb) __attribute__((always_inline)) {
+    const int c = 16 * qb + col < QB ? 16 * qb + col : 0;
+    const f32x4* p = (const f32x4*)&tau_sh[c][0];
     const f32x4 a = p[0], b = p[1];
-    return fmaxf(fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])),
-                 fmaxf(fmaxf(b[0], b[1]), fmaxf(b[2], b[3])));
+    const f32x4* p2 = (const f32x4*)&t2_sh[c][0];
+    const f32x4 a2 = p2[0], b2 = p2[1];
+    return fmaxf(fmaxf(fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])),
+                       fmaxf(fmaxf(b[0], b[1]), fmaxf(b[2], b[3]))),
+                 fminf(fminf(fminf(a2[0], a2[1]), fminf(a2[2], a2[3])),
+                       fminf(fminf(b2[0], b2[1]), fminf(b2[2], b2[3]))));
   };
-  // the query (column col) coded as t m, lane (g, col) holding dims 64 s + 16 g .. + 15 for
-  // MFMA step s: the bytes the lane loads of every row (the tiled image's piece s).  The 24
-  // 16-B units su = 4 s + u of a lane are split over the 8 waves (3 each) and the codes meet in
-  // LDS: the prologue's code is fetched cold on every launch (the I-cache), so it is kept short
-  // (the fully unrolled per-wave form was 10.7 us of the 77 us launch, TT_I8R_CLK)
+  // the queries (column col of block qb) coded as t m, lane (g, col) holding dims 64 s + 16 g ..
+  // + 15 for MFMA step s: the bytes the lane loads of every row (the tiled image's piece s).
+  // The 24 16-B units su = 4 s + u of a lane are split over the 8 waves (3 each) and the codes
+  // meet in LDS: the fully unrolled per-wave form (2,660 ISA lines before the first load) made
+  // the prologue 10.7 of the 77 us launch (TT_I8R_CLK); this one is 2.5 us
   static_assert(KS * 4 == 3 * NW, "three 16-B query units per wave");
-  __shared__ __attribute__((aligned(16))) float qmx[16][NW];
-  __shared__ double qsq[16][NW], qsd[16][NW];
-  __shared__ uint32_t qcode[KS * 4][64];
-  float tq;
+  __shared__ __attribute__((aligned(16))) float qmx[NQ16][NW];
+  __shared__ double qsq[NQ16][NW], qsd[NQ16][NW];
+  __shared__ uint32_t qcode[NQB][KS * 4][64];
+  float tq[NQB];
   {
-    const float* qp = q + (int64_t)(qv ? col : 0) * ldq + 16 * g;
-    f32x4 v[3];
-    float mx = 0.0f;
+    f32x4 v[NQB][3];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int su = 3 * w + j;
-      v[j] = *(const f32x4*)(qp + 64 * (su >> 2) + 4 * (su & 3));
-      mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[j][0]), fabsf(v[j][1])),
-                           fmaxf(fabsf(v[j][2]), fabsf(v[j][3]))));
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    if (g == 0) qmx[col][w] = mx;
-    __syncthreads();
-    {
-      const f32x4* p = (const f32x4*)&qmx[col][0];
-      const f32x4 a = p[0], b = p[1];
-      mx = fmaxf(fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])),
-                 fmaxf(fmaxf(b[0], b[1]), fmaxf(b[2], b[3])));
-    }
-    tq = mx / 127.0f;
-    double sq = 0.0, sd = 0.0;
-    const float tdiv = tq > 0.0f ? tq : 1.0f;
+    for (int qb = 0; qb < NQB; ++qb) {
+      const float* qp = q + (int64_t)(qv[qb] ? 16 * qb + col : 0) * ldq + 16 * g;
+      float mx = 0.0f;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      uint32_t pk = 0u;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {  // (selects, no branch: see k_filter_topm_i8)
-        int c = (int)rintf(v[j][b] / tdiv);
-        c = c > 127 ? 127 : c < -127 ? -127 : c;
-        c = tq > 0.0f ? c : 0;
-        const double e = (double)v[j][b] - (double)tq * (double)c;
-        sq += (double)v[j][b] * (double)v[j][b];
-        sd += e * e;
-        pk |= ((uint32_t)(c & 0xff)) << (8 * b);
+      for (int j = 0; j < 3; ++j) {
+        const int su = 3 * w + j;
+        v[qb][j] = *(const f32x4*)(qp + 64 * (su >> 2) + 4 * (su & 3));
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v[qb][j][0]), fabsf(v[qb][j][1])),
+                             fmaxf(fabsf(v[qb][j][2]), fabsf(v[qb][j][3]))));
       }
-      qcode[3 * w + j][lane] = pk;
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (g == 0) qmx[16 * qb + col][w] = mx;
     }
-    sq += __shfl_xor(sq, 16, 64);
-    sd += __shfl_xor(sd, 16, 64);
-    sq += __shfl_xor(sq, 32, 64);
-    sd += __shfl_xor(sd, 32, 64);
-    if (g == 0) {
-      qsq[col][w] = sq;
-      qsd[col][w] = sd;
+    __syncthreads();
+#pragma unroll
+    for (int qb = 0; qb < NQB; ++qb) {
+      const f32x4* p = (const f32x4*)&qmx[16 * qb + col][0];
+      const f32x4 a = p[0], b = p[1];
+      const float mx = fmaxf(fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3])),
+                             fmaxf(fmaxf(b[0], b[1]), fmaxf(b[2], b[3])));
+      tq[qb] = mx / 127.0f;
+      double sq = 0.0, sd = 0.0;
+      const float tdiv = tq[qb] > 0.0f ? tq[qb] : 1.0f;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        uint32_t pk = 0u;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {  // (selects, no branch: see k_filter_topm_i8)
+          const float x = v[qb][j][b];
+          int c = (int)rintf(x / tdiv);
+          c = c > 127 ? 127 : c < -127 ? -127 : c;
+          c = tq[qb] > 0.0f ? c : 0;
+          const double e = (double)x - (double)tq[qb] * (double)c;
+          sq += (double)x * (double)x;
+          sd += e * e;
+          pk |= ((uint32_t)(c & 0xff)) << (8 * b);
+        }
+        qcode[qb][3 * w + j][lane] = pk;
+      }
+      sq += __shfl_xor(sq, 16, 64);
+      sd += __shfl_xor(sd, 16, 64);
+      sq += __shfl_xor(sq, 32, 64);
+      sd += __shfl_xor(sd, 32, 64);
+      if (g == 0) {
+        qsq[16 * qb + col][w] = sq;
+        qsd[16 * qb + col][w] = sd;
+      }
     }
   }
   wait_vm<0>();     // every compiler-issued load retired: the loop's counted waits see only its own
   __syncthreads();  // ssc, tau_sh, the query codes
-  u32x4 qf[KS];
+  u32x4 qf[NQB][KS];
 #pragma unroll
-  for (int s = 0; s < KS; ++s)
-    qf[s] = u32x4{qcode[4 * s][lane], qcode[4 * s + 1][lane], qcode[4 * s + 2][lane],
-                  qcode[4 * s + 3][lane]};
-  if (blk == 0 && w == 0 && g == 0 && qv) {
+  for (int qb = 0; qb < NQB; ++qb)
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      qf[qb][s] = u32x4{qcode[qb][4 * s][lane], qcode[qb][4 * s + 1][lane],
+                        qcode[qb][4 * s + 2][lane], qcode[qb][4 * s + 3][lane]};
+  if (blk == 0 && w < NQB && g == 0 && 16 * w + col < nq) {  // eps of query 16 w + col
     double sq = 0.0, sd = 0.0;
 #pragma unroll
     for (int wb = 0; wb < NW; ++wb) {
-      sq += qsq[col][wb];
-      sd += qsd[col][wb];
+      sq += qsq[16 * w + col][wb];
+      sd += qsd[16 * w + col][wb];
     }
     const double nq2 = sqrt(sq) * 1.000001, nd = sqrt(sd) * 1.000001;
     const double e = 1.001 * ((double)R * nq2 + (double)S * nd +
                               1.1920928955078125e-07 * (double)S * (nq2 + nd) +
                               1.01 * EP * 5.9604644775390625e-08 * (double)X * nq2);
-    eps1[col] = e == e ? f64_up(e) : __builtin_huge_valf();
+    eps1[16 * w + col] = e == e ? f64_up(e) : __builtin_huge_valf();
   }
-  wait_vm<0>();  // (the eps store retired: the loop's counted waits see only its own loads)
+  wait_vm<0>();  // (the eps stores retired: the loop's counted waits see only its own loads)
   I8R_STAMP(1);
 
   static_assert(TM_M == 16, "wave_top16 keeps 16");
-  auto compact = [&](int c) __attribute__((always_inline)) {
-    uint64_t* b = wbuf + c * TMB;
-    const int cc = __shfl(cnt, c, 64);
+  // compaction of query c's buffer (of this wave) to its top 16
+#if TT_I8R_CLK
+  unsigned long long n_cmp = 0, n_any = 0;
+#endif
+  auto compact = [&](int qb, int c16) __attribute__((always_inline)) {
+#if TT_I8R_CLK
+    ++n_cmp;
+#endif
+    const int c = 16 * qb + c16;
+    uint64_t* b = wbuf + c * CS;
+    const int cc = __shfl(cnt[qb], c16, 64);
     uint64_t key[CPER];
 #pragma unroll
     for (int r = 0; r < CPER; ++r) {
@@ -3290,30 +3341,78 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8r(
     const uint64_t k = wave_top16<CPER>(key, lane, b, &nc);
     if (lane < nc) b[lane] = k;
     const uint32_t hk = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(k >> 32), TM_M - 1);
-    if (col == c) {
-      cnt = nc;
-      if (nc == TM_M) tau = fmaxf(tau, key_float(hk));
+    if (col == c16) {
+      cnt[qb] = nc;
+      if (nc == TM_M) tau[qb] = fmaxf(tau[qb], key_float(hk));
     }
     wave_sync();
   };
-  // appends of block bl (first: the wave's first block) and the tile-max bound:
-  // k_filter_topm_i8's
-  auto appends = [&](f32x4 acc, int bl, bool first, float shtau) __attribute__((always_inline)) {
+  // Cutting query c's buffer: first drop its keys below the query's current tau (a valid lower
+  // bound of the slab's 16th best, so nothing it drops can be in the slab's top 16 -- early
+  // appends fall below it once tau has risen): one ballot pass.  Only a buffer that is still
+  // longer than lim is compacted to its top 16 (wave_top16, ~1 us).  (Compacting every full
+  // buffer: 30 compactions per wave at 32 queries, ~1/4 of that launch; TT_I8R_CLK.)
+  auto cut = [&](int qb, int c16, int lim) __attribute__((always_inline)) {
+    const int c = 16 * qb + c16;
+    uint64_t* bb = wbuf + c * CS;
+    const int cc = __shfl(cnt[qb], c16, 64);
+    const float tc = __shfl(tau[qb], c16, 64);
+    uint64_t key[CPER];
+#pragma unroll
+    for (int r = 0; r < CPER; ++r) {
+      const int e = lane * CPER + r;
+      key[r] = e < cc ? bb[e] : 0ull;
+    }
+    wave_sync();
+    int base = 0;
+#pragma unroll
+    for (int r = 0; r < CPER; ++r) {
+      const bool keep = key[r] != 0ull && key_float((uint32_t)(key[r] >> 32)) >= tc;
+      const uint64_t bm = __ballot(keep);
+      const int pos = base + (int)__builtin_amdgcn_mbcnt_hi(
+                                 (uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+      if (keep) bb[pos] = key[r];
+      base += __popcll(bm);
+    }
+    wave_sync();
+    if (col == c16) cnt[qb] = base;
+    if (base > lim) compact(qb, c16);  // (wave-uniform)
+  };
+  auto compact_over = [&](int qb, int lim) __attribute__((always_inline)) {
+    const uint64_t need = __ballot(lane < 16 && cnt[qb] > lim);
+    if (need != 0ull) {
+      lds_wait<0>();
+      uint64_t nd = need;
+      while (nd) {
+        const int c16 = __builtin_ctzll(nd);
+        nd &= nd - 1;
+        cut(qb, c16, lim);
+      }
+    }
+  };
+  // appends of block bl for query block qb (first: the wave's first block) and the tile-max
+  // bound: k_filter_topm_i8's
+  auto appends = [&](int qb, f32x4 acc, int bl, bool first,
+                     float shtau) __attribute__((always_inline)) {
     const int64_t jt = j0 + 16 * (int64_t)bl;
-    if (qv) tau = fmaxf(tau, shtau);
+    const int c = 16 * qb + col;
+    if (qv[qb]) tau[qb] = fmaxf(tau[qb], shtau);
     if (jt + 16 > j1) {  // (wave-uniform) the slab's last block: rows past its end score -inf
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj)
         if (jt + 4 * g + jj >= j1) acc[jj] = -__builtin_huge_valf();
     }
-    const bool any = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])) >= tau;
+    const bool any = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])) >= tau[qb];
     if (__ballot(any) != 0ull) {
+#if TT_I8R_CLK
+      ++n_any;
+#endif
       const int lr0 = 16 * bl + 4 * g, nloc = (int)(j1 - j0);  // slab-local rows
       bool pass[4];
       int np = 0;
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
-        pass[jj] = lr0 + jj < nloc && acc[jj] >= tau;
+        pass[jj] = lr0 + jj < nloc && acc[jj] >= tau[qb];
         np += pass[jj] ? 1 : 0;
       }
       const auto x16 = __builtin_amdgcn_permlane16_swap((uint32_t)np, (uint32_t)np, false, false);
@@ -3321,14 +3420,15 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8r(
       const int s2 = np + b;
       const auto x32 = __builtin_amdgcn_permlane32_swap((uint32_t)s2, (uint32_t)s2, false, false);
       const int s2x = (int)(lane < 32 ? x32[1] : x32[0]);  // lane ^ 32
-      int pos = cnt + ((g & 1) ? b : 0) + ((g & 2) ? s2x : 0);
+      int pos = cnt[qb] + ((g & 1) ? b : 0) + ((g & 2) ? s2x : 0);
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj)
         if (pass[jj]) {
-          lds_write64(lds_addr(wbuf + col * TMB + pos), make_key(acc[jj], (uint32_t)(j0 + lr0 + jj)));
+          lds_write64(lds_addr(wbuf + (c < QB ? c : 0) * CS + pos),
+                      make_key(acc[jj], (uint32_t)(j0 + lr0 + jj)));
           ++pos;
         }
-      cnt += s2 + s2x;
+      cnt[qb] += s2 + s2x;
     }
     if (first) {  // the wave's first block: its 16 rows (every lane of the column gathers all 16)
       float v16[16];
@@ -3346,7 +3446,7 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8r(
         v16[8 + jj] = __uint_as_float(lane < 32 ? x32[1] : x32[0]);
       }
 #pragma unroll
-      for (int k2 = 0; k2 < 16; ++k2) tm_insert(v16[k2]);
+      for (int k2 = 0; k2 < 16; ++k2) tm_insert(qb, v16[k2]);
     } else {
       float m = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3]));
       const auto x16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m),
@@ -3354,20 +3454,14 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8r(
       m = fmaxf(__uint_as_float(x16[0]), __uint_as_float(x16[1]));
       const auto x32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m),
                                                         false, false);
-      tm_insert(fmaxf(__uint_as_float(x32[0]), __uint_as_float(x32[1])));  // the block max
+      tm_insert(qb, fmaxf(__uint_as_float(x32[0]), __uint_as_float(x32[1])));  // the block max
     }
-    tau = fmaxf(tau, qv ? tm[0] : tau);
-    const uint64_t need = __ballot(lane < 16 && cnt > TMB - 16);
-    if (need != 0ull) {
-      lds_wait<0>();
-      uint64_t nd = need;
-      while (nd) {
-        const int c = __builtin_ctzll(nd);
-        nd &= nd - 1;
-        compact(c);
-      }
+    tau[qb] = fmaxf(tau[qb], qv[qb] ? tm[qb][0] : tau[qb]);
+    compact_over(qb, TMB - 16);
+    if (qv[qb] && g == 0) {  // published for the other waves
+      tau_sh[c][w] = tau[qb];
+      t2_sh[c][w] = tm[qb][14];
     }
-    if (qv && g == 0) tau_sh[col][w] = tau;  // published for the other waves
   };
 
   // Blocks are handed out dynamically: slot d of wave w starts on block w + NW d, and every
@@ -3376,80 +3470,114 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8r(
   // the static round-robin split, wave 0 left the loop ~14 us before the block's last wave:
   // TT_I8R_CLK at 1M rows).  Claims are made in processing order and only grow, so the first
   // slot holding a block >= nb ends the wave's loop; its later slots hold larger blocks.
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  // (issuing these before the prologue, so their round trip overlaps the query's, measured
-  // neutral: prologue 2.5 -> 7.7 us, loop 52.8 -> 47.8 us -- the stream is HBM-bound throughout)
+  // (Issuing the first blocks before the prologue, so their round trip overlaps the query's,
+  // measured neutral: prologue 2.5 -> 7.7 us, loop 52.8 -> 47.8 us -- HBM-bound throughout.)
+  f32x4 acc[NQB];
   int bid[D];
   static_for<D>([&](auto d_) __attribute__((always_inline)) {
     constexpr int d = decltype(d_)::value;
     bid[d] = w + NW * d;
     issue(d, bid[d]);
   });
+  // The slot is a run-time (wave-uniform) index: only the per-slot pieces (the wait-and-MFMA
+  // of a slot's registers, its next issue) are switched over, and the appends -- the bulk of
+  // the loop's code -- appear once.  (Unrolling the loop over the D slots put D copies of them
+  // in the loop: 10.5k instructions at 32 queries, and that build ran 0.27 ms per search.)
   int prev = -1;  // the block whose scores acc holds (its appends run one block later)
-  bool first = true, more = nb > 0;
-  while (more) {
+  bool first = true;
+  for (int dcur = 0;;) {
+    int b = 0;
+    static_for<D>([&](auto d_) __attribute__((always_inline)) {
+      if (dcur == decltype(d_)::value) b = bid[decltype(d_)::value];
+    });
+    const bool live = b < nb;  // (wave-uniform; the first slot at or past nb ends the loop)
+    i32x4 ai[NQB];
+    float sb = 0.0f;
+    float shtau[NQB];
+#pragma unroll
+    for (int qb = 0; qb < NQB; ++qb) shtau[qb] = read_shtau(qb);
+    if (live) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * KS) : "memory");
+      sb = ssc[b >> 2];  // the block's 64-row scale tile
+      static_for<D>([&](auto d_) __attribute__((always_inline)) {
+        constexpr int d = decltype(d_)::value;
+        if (dcur == d) {
+#pragma unroll
+          for (int s = 0; s < KS; ++s) reg_tie(buf[d][s]);
+#pragma unroll
+          for (int qb = 0; qb < NQB; ++qb) {
+            ai[qb] = i32x4{0, 0, 0, 0};
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+              if (TT_I8R_EXP == 2)
+                ai[qb] += __builtin_bit_cast(i32x4, buf[d][s]);
+              else
+                ai[qb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                    __builtin_bit_cast(i32x4, buf[d][s]), __builtin_bit_cast(i32x4, qf[qb][s]),
+                    ai[qb], 0, 0, 0);
+            }
+          }
+        }
+      });
+    }
+    if (prev >= 0 && TT_I8R_EXP == 0) {
+#pragma unroll
+      for (int qb = 0; qb < NQB; ++qb) appends(qb, acc[qb], prev, first, shtau[qb]);
+      first = false;
+    }
+    if (!live) break;
+    if (TT_I8R_EXP && acc[0][0] == 1.2345f) tau_sh[0][w] = acc[0][1];  // keeps the work live
+#pragma unroll
+    for (int qb = 0; qb < NQB; ++qb)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) acc[qb][jj] = (float)ai[qb][jj] * (sb * tq[qb]);
+    prev = b;
+    // the next block for this slot (past nb: reads 0 and ends the loop when reached); issued
+    // after acc is converted, i.e. after the MFMAs that read the slot's registers completed
+    int nx = 0;
+    if (lane == 0) nx = __hip_atomic_fetch_add(&next_blk, 1, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    nx = __builtin_amdgcn_readfirstlane(nx);
+    __builtin_amdgcn_sched_barrier(0);
     static_for<D>([&](auto d_) __attribute__((always_inline)) {
       constexpr int d = decltype(d_)::value;
-      if (more && bid[d] >= nb) more = false;  // (wave-uniform)
-      if (more) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * KS) : "memory");
-#pragma unroll
-        for (int s = 0; s < KS; ++s) reg_tie(buf[d][s]);
-        const int b = bid[d];
-        const float shtau = read_shtau();
-        const float st = ssc[b >> 2] * tq;  // the block's 64-row scale tile x t
-        i32x4 ai = {0, 0, 0, 0};
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          if (TT_I8R_EXP == 2)
-            ai += __builtin_bit_cast(i32x4, buf[d][s]);
-          else
-            ai = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(i32x4, buf[d][s]),
-                                                       __builtin_bit_cast(i32x4, qf[s]), ai, 0,
-                                                       0, 0);
-        }
-        if (prev >= 0 && TT_I8R_EXP == 0) {
-          appends(acc, prev, first, shtau);
-          first = false;
-        }
-        if (TT_I8R_EXP && acc[0] == 1.2345f) tau_sh[0][w] = acc[1];  // keeps the work live
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) acc[jj] = (float)ai[jj] * st;
-        prev = b;
-        // the next block for this slot (past nb: reads 0 and ends the loop when reached)
-        int nx = 0;
-        if (lane == 0) nx = __hip_atomic_fetch_add(&next_blk, 1, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-        bid[d] = __builtin_amdgcn_readfirstlane(nx);
-        __builtin_amdgcn_sched_barrier(0);
-        issue(d, bid[d]);
-        __builtin_amdgcn_sched_barrier(0);
+      if (dcur == d) {
+        bid[d] = nx;
+        issue(d, nx);
       }
     });
+    __builtin_amdgcn_sched_barrier(0);
+    dcur = dcur + 1 == D ? 0 : dcur + 1;
   }
-  if (prev >= 0 && TT_I8R_EXP == 0) appends(acc, prev, first, read_shtau());
   // every load retired before its registers are given back
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
   for (int d = 0; d < D; ++d)
 #pragma unroll
     for (int s = 0; s < KS; ++s) reg_tie(buf[d][s]);
-  // each wave cuts its own lists to their top 16 (in parallel), so the block's merge below
-  // selects from 8 x 16 keys per query instead of 8 full buffers
-  {
-    const uint64_t need = __ballot(lane < 16 && cnt > TM_M);
-    if (need != 0ull) {
-      lds_wait<0>();
-      uint64_t nd = need;
-      while (nd) {
-        const int c = __builtin_ctzll(nd);
-        nd &= nd - 1;
-        compact(c);
-      }
-    }
+#if TT_I8R_CLK
+  if (tid == 0 && blk < 256) {
+    g_i8rclk[blk * 8 + 5] = n_cmp;
+    g_i8rclk[blk * 8 + 6] = n_any;
+  }
+#endif
+  // Each wave cuts its own lists for the merge (8 x at most 16 keys per query) by the block's
+  // final shared bound (every wave's last tau and second-largest entry is published), which
+  // leaves a few keys per wave and query; a list still longer than 16 is compacted.
+  // (Compacting every list to 16 cost ~1 us per query and wave: 18.6 us of epilogue at 16
+  // queries, 37 at 32.)
+  lds_wait<0>();
+  __syncthreads();
+#pragma unroll
+  for (int qb = 0; qb < NQB; ++qb) {
+    const float bnd = read_shtau(qb);
+    if (qv[qb]) tau[qb] = fmaxf(tau[qb], bnd);
+    compact_over(qb, TM_M);
   }
   I8R_STAMP(2);
-  if (lane < nq && g == 0) ncw[w][lane] = cnt;
+#pragma unroll
+  for (int qb = 0; qb < NQB; ++qb)
+    if (lane < 16 && 16 * qb + lane < nq) ncw[w][16 * qb + lane] = cnt[qb];
   lds_wait<0>();
   __syncthreads();
   I8R_STAMP(3);
@@ -3459,12 +3587,12 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8r(
 #pragma unroll
     for (int r = 0; r < 2; ++r) {  // key e = 2 lane + r: wave e / 16's e % 16-th
       const int e = 2 * lane + r, wb = e >> 4, idx = e & 15;
-      key[r] = idx < ncw[wb][c] ? tbuf[(wb * QB + c) * TMB + idx] : 0ull;
+      key[r] = idx < ncw[wb][c] ? tbuf[(wb * QB + c) * CS + idx] : 0ull;
     }
     int nc;
-    const uint64_t k = wave_top16<2>(key, lane, tbuf + c * TMB, &nc);
+    const uint64_t k = wave_top16<2>(key, lane, tbuf + c * CS, &nc);
     if (lane < nc) {
-      tbuf[c * TMB + lane] = k;
+      tbuf[c * CS + lane] = k;
       lists[((int64_t)c * G + blk) * TM_M + lane] = k;
     }
     if (lane == 0) {
@@ -3473,10 +3601,11 @@ __global__ __launch_bounds__(64 * TM_WAVES, 1) void k_filter_topm_i8r(
     }
   }
   __syncthreads();
+  I8R_STAMP(7);
   for (int c = w; c < nq; c += NW) {
     const int nc = ncs[c], r16 = lane & 15, g4 = 4 * (lane >> 4);
     if (nc == 0) continue;
-    const uint64_t* tb = tbuf + c * TMB;
+    const uint64_t* tb = tbuf + c * CS;
     const f32x4 ex =
         exact16<EP>(db, ld, key_row(tb[r16 < nc ? r16 : 0]), q + (int64_t)c * ldq, lane);
     if (r16 == 0) {
@@ -4459,8 +4588,9 @@ static FilterPlan plan_filter_uncached(int64_t n, int nq, int k, int ep) {
   for (int i = 0; i < nl; ++i) p.small = p.small && p.lv[i].n_slabs <= SM_THREADS;
   // single pass for the smallest batches: lists [nq][G][TM_M] and counts [nq][G] fit the
   // level workspace once max_slabs >= G (FL_CAP >= TM_M)
-  // (the bf16 single pass runs for nq <= TM_NQ_RUN; the int8 one up to TM_NQ_I8)
-  p.topm = nq <= TM_NQ_I8 && !topm_disabled() && device_cus() * TM_M <= TM_CAP &&
+  // (the bf16 single pass runs for nq <= TM_NQ_RUN; the int8 ones up to TM_NQ_I8 (ring) and
+  // TM_NQ_I8T (tiled image))
+  p.topm = nq <= TM_NQ_I8T && !topm_disabled() && device_cus() * TM_M <= TM_CAP &&
            device_cus() <= SM_THREADS;
   if (p.topm && p.max_slabs < device_cus()) p.max_slabs = device_cus();
   return p;
@@ -5035,9 +5165,11 @@ extern "C" int tt_debug_i8_force_unsupported(int32_t on) {
 // device_cus() * TM_M <= TM_CAP, TT_FILTER_TOPM), the per-block scale-tile limit (rows per CU
 // <= 65536) and the 31-bit tile offsets.  1: the call would run, 0: it would return
 // TT_ERR_UNSUPPORTED (the caller then takes tt_scan_topk_bf16f32).
-static bool i8_single_pass_fits(int64_t n, int ep, int nq, int k, int64_t ld_i8) {
-  if (g_i8_force_unsupported || (ep != 384 && ep != 768) || nq < 1 || nq > TM_NQ_I8 || k < 1 ||
-      k > FL_KMAX || k > n || n < 1 || n > 0x7fffffffLL)
+static bool i8_single_pass_fits(int64_t n, int ep, int nq, int k, int64_t ld_i8,
+                                bool tiled = false) {
+  if (g_i8_force_unsupported || (ep != 384 && ep != 768) || (tiled && ep != 384) || nq < 1 ||
+      nq > (tiled ? TM_NQ_I8T : TM_NQ_I8) || k < 1 || k > FL_KMAX || k > n || n < 1 ||
+      n > 0x7fffffffLL)
     return false;
   if (!plan_filter(n, nq, k, ep).topm) return false;
   const int G = device_cus();
@@ -5048,6 +5180,11 @@ static bool i8_single_pass_fits(int64_t n, int ep, int nq, int k, int64_t ld_i8)
 extern "C" int tt_i8_single_pass_ok(int64_t n, int32_t d, int32_t nq, int32_t k, int64_t ld_i8) {
   const int ep = tt_padded_dim(d);
   return ep > 0 && i8_single_pass_fits(n, ep, nq, k, ld_i8 > 0 ? ld_i8 : ep) ? 1 : 0;
+}
+
+extern "C" int tt_i8t_single_pass_ok(int64_t n, int32_t d, int32_t nq, int32_t k) {
+  const int ep = tt_padded_dim(d);
+  return ep > 0 && i8_single_pass_fits(n, ep, nq, k, ep, true) ? 1 : 0;
 }
 
 namespace {
@@ -5067,7 +5204,9 @@ int i8_single_pass(const float* db, const int8_t* img, bool tiled, const float* 
   const int ep = tt_padded_dim(d);
   if (ep != 384 && ep != 768) return fail(TT_ERR_UNSUPPORTED, "int8 single pass: E 384 / 768");
   if (tiled && ep != 384) return fail(TT_ERR_UNSUPPORTED, "tiled int8 single pass: E 384");
-  if (nq > TM_NQ_I8) return fail(TT_ERR_UNSUPPORTED, "int8 single pass: nq <= 8");
+  if (nq > (tiled ? TM_NQ_I8T : TM_NQ_I8))
+    return fail(TT_ERR_UNSUPPORTED, tiled ? "tiled int8 single pass: nq <= 32"
+                                          : "int8 single pass: nq <= 8");
   if (tiled) ld_i8 = ep;
   TT_REQUIRE(ld_i8 >= ep && ld_i8 % 16 == 0 && ((uintptr_t)img % 16) == 0,
              "int8 image: ld_i8 >= tt_padded_dim(d), multiple of 16, 16-B aligned");
@@ -5094,7 +5233,10 @@ int i8_single_pass(const float* db, const int8_t* img, bool tiled, const float* 
   auto kern = ep == 384 ? (nq <= 4 ? k_filter_topm_i8<384, 4> : k_filter_topm_i8<384, TM_NQ_I8>)
                         : (nq <= 4 ? k_filter_topm_i8<768, 4> : k_filter_topm_i8<768, TM_NQ_I8>);
   if (tiled)  // (rpb <= 65536 rows: a slab's tiled bytes fit the buffer resource's record count)
-    kern = nq <= 4 ? k_filter_topm_i8r<384, 4> : k_filter_topm_i8r<384, TM_NQ_I8>;
+    kern = nq <= 4    ? k_filter_topm_i8r<384, 4, 1>
+           : nq <= 8  ? k_filter_topm_i8r<384, 8, 1>
+           : nq <= 16 ? k_filter_topm_i8r<384, 16, 1>
+                      : k_filter_topm_i8r<384, 32, 2>;
   hipLaunchKernelGGL(kern, dim3(G), dim3(64 * TM_WAVES), 0, st, img, ld_i8, tile_scales, n, q,
                      nq, ld_q, (int)rpb, db, ld_db, x_norm_max, x_resid_max, s_max, w.eps2,
                      w.lists, xkeys, w.counts, w.flags, w.qsel_n);

@@ -107,6 +107,7 @@ SIGNATURES = {
                                             _i64, _i32, ctypes.c_float, ctypes.c_float,
                                             ctypes.c_float, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
     "tt_i8_tiled_bytes": (ctypes.c_int64, [_i64, _i32]),
+    "tt_i8t_single_pass_ok": (ctypes.c_int, [_i64, _i32, _i32, _i32]),
     "tt_i8_tile": (ctypes.c_int, [_vp, _i64, _i64, _i32, _vp, _vp]),
     "tt_topk_merge_f32": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp]),
     "tt_weighted_avg_l2_f32": (ctypes.c_int, [_vp, _i64, _i32, _i32, _vp, _vp, _i64, _vp]),

@@ -266,6 +266,7 @@ def debug_i8_force_unsupported(on: bool) -> None:
     unsupported, as on a > 256-CU GPU or past its row limit."""
     check(lib().tt_debug_i8_force_unsupported(1 if on else 0), "tt_debug_i8_force_unsupported")
     _i8_ok_cache.clear()
+    _i8t_ok_cache.clear()
 
 
 def i8_image(x: torch.Tensor, d: int, out3: torch.Tensor = None):
@@ -284,6 +285,30 @@ def i8_image(x: torch.Tensor, d: int, out3: torch.Tensor = None):
 
 
 I8T_DIMS = (384,)  # padded dims of the tiled int8 image's register-fed stream
+I8T_NQ_MAX = 32  # queries of the tiled int8 single pass (two 16-query MFMA blocks)
+_i8t_ok_cache = {}
+
+
+def i8t_single_pass_ok(n: int, d: int, nq: int, k: int) -> bool:
+    """Whether tt_scan_topk_i8t_f32 (the tiled image, nq <= 32) runs this shape."""
+    key = (n, d, nq, k)
+    v = _i8t_ok_cache.get(key)
+    if v is None:
+        if len(_i8t_ok_cache) > 4096:
+            _i8t_ok_cache.clear()
+        v = _i8t_ok_cache[key] = bool(lib().tt_i8t_single_pass_ok(n, d, nq, k))
+    return v
+
+
+def i8_pass_ok(n: int, d: int, nq: int, k: int, i8) -> bool:
+    """Whether an int8 single pass serves nq queries with this int8 image tuple (codes, scales,
+    bounds[, tiled]): the tiled stream for nq <= 32 at padded dim 384, else the ring one for
+    nq <= 8 at 384 / 768."""
+    if i8 is None:
+        return False
+    if len(i8) > 3 and i8[3] is not None and _lib.padded_dim(d) in I8T_DIMS:
+        return nq <= I8T_NQ_MAX and i8t_single_pass_ok(n, d, nq, k)
+    return nq <= I8_NQ_MAX and i8_single_pass_ok(n, d, nq, k, i8[0].stride(0))
 
 
 def i8_tile(codes: torch.Tensor, n: int, d: int) -> torch.Tensor:
@@ -312,8 +337,9 @@ def scan_topk_i8(db: torch.Tensor, codes: torch.Tensor, scales: torch.Tensor, n:
     if codes.dtype != torch.int8 or codes.dim() != 2 or codes.shape[0] < n:
         raise ValueError("codes must be the int8 image [n, ep] of db (i8_image)")
     nq = q.shape[0]
-    if not (1 <= k <= min(n, FILTER_KMAX)) or nq > I8_NQ_MAX:
-        raise ValueError(f"scan_topk_i8: need 1 <= k ({k}) <= min(n, 128) and nq <= 8")
+    nq_max = I8T_NQ_MAX if tiled is not None and _lib.padded_dim(d) in I8T_DIMS else I8_NQ_MAX
+    if not (1 <= k <= min(n, FILTER_KMAX)) or nq > nq_max:
+        raise ValueError(f"scan_topk_i8: need 1 <= k ({k}) <= min(n, 128) and nq <= {nq_max}")
     if out is None:
         out = (torch.empty((nq, k), dtype=_f32, device=q.device),
                torch.empty((nq, k), dtype=torch.int64, device=q.device))
@@ -371,8 +397,7 @@ class PreparedSearch:
         self._head = (_ptr(db), _ptr(db16), n, d, db.stride(0), row_base)
         self._tail = (k, ctypes.c_float(x_norm_max), ctypes.c_float(x_resid_max),
                       _ptr(self.out[0]), _ptr(self.out[1]), _ptr(self.ws), self.ws.numel())
-        self.i8 = (i8 is not None and nq <= I8_NQ_MAX and self.ld_q in I8_DIMS
-                   and i8_single_pass_ok(n, d, nq, k, i8[0].stride(0)))
+        self.i8 = self.ld_q in I8_DIMS and i8_pass_ok(n, d, nq, k, i8)
         if self.i8:
             codes, scales, b3 = i8[:3]
             tiled = i8[3] if len(i8) > 3 else None

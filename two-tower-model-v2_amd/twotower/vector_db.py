@@ -173,9 +173,7 @@ class FlatIPIndex:
         with self._lock:  # the workspace cache is shared; the outputs are fresh per call
             ws = self._ws.get(need, self.device)
             i8 = self.i8 if use_bf16 and method == "auto" else None
-            if (i8 is not None and q.shape[0] <= kernels.I8_NQ_MAX
-                    and kernels.i8_single_pass_ok(self.ntotal, self.d, q.shape[0], k,
-                                                  i8[0].stride(0))):
+            if kernels.i8_pass_ok(self.ntotal, self.d, q.shape[0], k, i8):
                 codes, scales, b3, tiled = i8  # one-buyer calls: the int8 single pass
                 return kernels.scan_topk_i8(self.xb, codes, scales, self.ntotal, self.d, q, k, b3,
                                             row_base=self.row_base, workspace=ws, tiled=tiled)
@@ -447,8 +445,7 @@ class _ServingSlot:
         xb, xb16, n, bounds, i8, _ = state
         nq, d = x.shape
         ws = self._workspace(n, nq, k, "bf16")
-        use8 = (i8 is not None and nq <= kernels.I8_NQ_MAX
-                and kernels.i8_single_pass_ok(n, d, nq, k, i8[0].stride(0)))
+        use8 = kernels.i8_pass_ok(n, d, nq, k, i8)
         # skey = the catalog state's version (rows, bounds and int8 image); the workspace and
         # output buffers are fixed while an entry lives (their reallocation clears self.bound)
         akey = (skey, nq, k, normalize, use8)
