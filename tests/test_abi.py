@@ -49,6 +49,14 @@ def test_version_and_padded_dim(L):
         [64, 64, 128, 128, 384, 512, 768, -1]
 
 
+def test_i8_tiled_bytes(L):
+    """tt_i8_tiled_bytes: whole 16-row blocks of the padded dim (host arithmetic only)."""
+    assert [L.tt_i8_tiled_bytes(n, 384) for n in (1, 16, 17, 1_000_000)] == \
+        [16 * 384, 16 * 384, 32 * 384, 1_000_000 * 384]
+    assert L.tt_i8_tiled_bytes(5, 768) == 16 * 768
+    assert L.tt_i8_tiled_bytes(5, 900) == -1 and L.tt_i8_tiled_bytes(-1, 384) == -1
+
+
 def test_invalid_arguments_rejected_without_device(L):
     from twotower._lib import check
 
