@@ -1321,7 +1321,8 @@ def main():
         result["single_buyer_search"] = {
             "nq": 1, "ms_per_search": one_ms,
             "ms_per_search_is": ("kernels.PreparedSearch device call (no host copies); the int8 "
-                                 "single pass (nq <= 8), bit-identical to the bf16 pass"
+                                 "single pass (tiled image at padded dim 384: nq <= 32; else "
+                                 "nq <= 8), bit-identical to the bf16 pass"
                                  if i8 is not None else
                                  "kernels.PreparedSearch device call (no host copies)"),
             **i8_info,
