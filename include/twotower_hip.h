@@ -509,6 +509,13 @@ int tt_attn_pool_bwd_relu_f32(const float* dz, int64_t lddz, const float* z, int
                               const float* x, int64_t B, int32_t S, int32_t E, const float* H,
                               const float* W2, int32_t Hd, float* dW2, float* db2, float* dH,
                               float* da_ws, void* stream);
+/* tt_attn_pool_bwd_relu_f32 without its second launch: the per-buyer dW2 / db2 parts stay in
+ * da_ws (after the B*S da values, at a 64-float boundary) for tt_train_bwd_tail. */
+int tt_attn_pool_bwd_relu_parts_f32(const float* dz, int64_t lddz, const float* z, int64_t ldz,
+                                    const float* onorm, const float* alpha, const float* w,
+                                    const float* x, int64_t B, int32_t S, int32_t E,
+                                    const float* H, const float* W2, int32_t Hd, float* dH,
+                                    float* da_ws, void* stream);
 /* Weight gradients without transposed copies: C [N, K] = A^T B for row-major A [M, N] (dY),
  * B [M, K] (X), f32 in; prec TT_PREC_BF16 rounds the operands to bf16 (bf16 MFMA, f32
  * accumulate), TT_PREC_F32 keeps f32 (f32 MFMA).  db (may be NULL) = column sums of A (the bias
@@ -520,6 +527,32 @@ int tt_gemm_tn_workspace_bytes(int64_t M, int32_t N, int32_t K, int64_t* bytes);
 int tt_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int32_t N,
                int32_t K, int32_t prec, float* C, int64_t ldc, float* db, void* workspace,
                int64_t workspace_bytes, void* stream);
+/* tt_gemm_tn without its second launch: the split sums stay in `workspace` (which must not be
+ * reused until they are reduced) and tt_gemm_tn_reduce_many sums up to 8 such GEMMs in ONE
+ * launch, same order and bits as tt_gemm_tn.  A plan with one split writes C / db directly
+ * (its job is then skipped).  The training step defers its weight-gradient reduces to one
+ * launch and InfoNCE reduces its two products together. */
+typedef struct tt_tn_pending {
+  const void* workspace;  /* the workspace given to tt_gemm_tn_partial */
+  int64_t M;
+  int32_t N, K;
+  float* C;
+  int64_t ldc;
+  float* db; /* may be NULL */
+} tt_tn_pending;
+int tt_gemm_tn_partial(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M,
+                       int32_t N, int32_t K, int32_t prec, float* C, int64_t ldc, float* db,
+                       void* workspace, int64_t workspace_bytes, void* stream);
+int tt_gemm_tn_reduce_many(const tt_tn_pending* jobs, int32_t n, void* stream);
+/* The training step's backward tail in ONE launch: the deferred weight-gradient reduces (as
+ * tt_gemm_tn_reduce_many), the attention pooling's dW2 / db2 from the per-buyer parts that
+ * tt_attn_pool_bwd_relu_parts_f32 left at attn_parts (same order and bits as
+ * tt_attn_pool_bwd_relu_f32's second launch; attn_parts NULL: none), and the embedding-row
+ * gradients of tt_embedding_backward2_f32 (g_emb NULL: none). */
+int tt_train_bwd_tail(const tt_tn_pending* jobs, int32_t njobs, const float* attn_parts,
+                      int64_t B, int32_t Hd, float* dW2, float* db2, const float* g_emb,
+                      int64_t ldg, const int32_t* ids0, const int32_t* ids1, int64_t n_emb,
+                      int32_t C, float* grad0, float* grad1, void* stream);
 /* nn.Dropout forward with the keep mask drawn in the kernel: element i is kept iff
  * hash(seed, *counter, i) >= p 2^32 (splitmix64, counter-based: a graph-replayed step draws a
  * fresh mask when the caller advances *counter, a device int64), kept values scaled by
@@ -556,8 +589,10 @@ int tt_l2norm_backward_ex(const float* y, int64_t ldy, const float* z, int64_t l
  * bf16 (to_bf16), transposed (dst [cols, ld_dst], columns rows..ld_dst-1 zero) or not; src
  * NULL zero-fills dst [rows, cols] (not transposed).  The training step's weight-derived GEMM
  * operands (bf16 weights, transposed weights), bf16 copies of its inputs and the zeroing of
- * its accumulated gradients, once per step. */
-#define TT_CONVERT_MAX_JOBS 8
+ * its accumulated gradients, once per step.  row_ids (may be NULL; not with transpose): dst
+ * row r takes src row row_ids[r], zeros for a negative id -- the [text | brand | cat]
+ * concatenation of the item head's input as jobs of the same launch. */
+#define TT_CONVERT_MAX_JOBS 16
 typedef struct tt_convert_job {
   const float* src;
   int64_t ld_src;
@@ -565,6 +600,7 @@ typedef struct tt_convert_job {
   void* dst;
   int64_t ld_dst;
   int32_t transpose, to_bf16;
+  const int32_t* row_ids;
 } tt_convert_job;
 int tt_convert_batch(const tt_convert_job* jobs, int32_t njobs, void* stream);
 /* torch.optim.Adam step (weight_decay 0): step is the 1-based step count after increment. */

@@ -36,6 +36,12 @@ for s in "$@"; do
           step bench_i8_$v 180 python3 -u tools/bench_i8.py; done ;;
     train_prof) step train_prof 300 rocprofv3 --kernel-trace --stats --output-format csv \
                   -d "$OUT/train_prof" -o train -- python3 tools/train_step_prof.py ;;
+    # the training step under timing builds (VARS = names under lib/variants), product lib first
+    train_ab) for rep in 1 2; do for v in base ${VARS:-b512 b256 b2048}; do
+        L=$PWD/two-tower-model-v2_amd/lib/variants/lib_$v.so; [ $v = base ] && L=$PWD/two-tower-model-v2_amd/lib/libtwotower_hip.so
+        TWOTOWER_HIP_LIB=$L step train_ab_${v}_$rep 200 python3 tools/train_step_prof.py --json "$OUT/ab_${v}_$rep.json"
+        python3 -c "import json; d=json.load(open('$OUT/ab_${v}_$rep.json')); print('$v $rep', round(d['bf16']['graph_inplace_inputs_ms'],4), round(d['f32']['graph_inplace_inputs_ms'],4))"
+      done; done ;;
     train_bench) step train_bench 300 python3 tools/train_step_prof.py --json "$OUT/train.json" ;;
     trainer_tests) step trainer_tests 600 $PYT -m gpu tests/test_gpu_trainer.py tests/test_gpu_train.py tests/test_gpu_loss.py ;;
     debug_graph) step debug_graph 200 python3 -u tools/debug_graph_step.py ;;

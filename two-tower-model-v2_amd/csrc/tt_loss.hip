@@ -179,7 +179,7 @@ size_t al(size_t b) { return (b + 255) / 256 * 256; }
 struct NceWs {
   float *S, *row_loss, *P0, *Pn, *Pb, *PbT, *G1, *G2;
   uint16_t *b16, *p16;
-  char* tn;
+  char *tn, *tn2;
   int64_t tn_bytes;
   size_t total;
 };
@@ -209,6 +209,7 @@ NceWs nce_carve(char* base, int B, int N, int E, bool bf, bool grads) {
     tt_gemm_tn_workspace_bytes(B, B, E, &tb);
     w.tn_bytes = tb;
     w.tn = take((size_t)tb);
+    w.tn2 = take((size_t)tb);  // G2's splits (both products are reduced in one launch)
   }
   w.total = off;
   return w;
@@ -299,9 +300,17 @@ int infonce(const float* b, int64_t ldb, const float* p, int64_t ldp, const floa
     return check_launch("k_mean");
   }
   // G1 = Pb . p = (Pb^T)^T p;  G2 = Pb^T . b   (row-major Pb^T / Pb as the A^T operands)
-  rc = tt_gemm_tn(w.PbT, Bp, p, ldp, B, B, E, prec, w.G1, E, nullptr, w.tn, w.tn_bytes, stream);
+  // (the two products' split sums reduced by one launch)
+  rc = tt_gemm_tn_partial(w.PbT, Bp, p, ldp, B, B, E, prec, w.G1, E, nullptr, w.tn, w.tn_bytes,
+                          stream);
   if (!rc)
-    rc = tt_gemm_tn(w.Pb, Bp, b, ldb, B, B, E, prec, w.G2, E, nullptr, w.tn, w.tn_bytes, stream);
+    rc = tt_gemm_tn_partial(w.Pb, Bp, b, ldb, B, B, E, prec, w.G2, E, nullptr, w.tn2, w.tn_bytes,
+                            stream);
+  if (!rc) {
+    const tt_tn_pending jobs[2] = {{w.tn, B, B, E, w.G1, E, nullptr},
+                                   {w.tn2, B, B, E, w.G2, E, nullptr}};
+    rc = tt_gemm_tn_reduce_many(jobs, 2, stream);
+  }
   if (rc) return rc;
   hipLaunchKernelGGL(k_infonce_grads, dim3(B), dim3(256), 0, st, b, ldb, p, ldp, n, ldn_row,
                      ldn_item, B, N, E, inv_tau / (float)B, w.P0, w.Pn, w.G1, w.G2, (int64_t)E,

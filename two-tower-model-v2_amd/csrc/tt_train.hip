@@ -547,12 +547,11 @@ __global__ __launch_bounds__(256) void k_gemm_tn(const float* __restrict__ A, in
 
 // The splits' sum, one thread per output element (and per bias-gradient entry), in split
 // order; the S loads of a thread are independent, so they are all in flight at once.
-__global__ __launch_bounds__(256) void k_tn_reduce(const float* __restrict__ parts,
-                                                   const float* __restrict__ dbparts, int S,
-                                                   int T, int KT, int NT, int N, int K,
-                                                   float* __restrict__ C, int64_t ldc,
-                                                   float* __restrict__ db) {
-  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void tn_reduce_item(const float* __restrict__ parts,
+                                               const float* __restrict__ dbparts, int S, int T,
+                                               int KT, int NT, int N, int K,
+                                               float* __restrict__ C, int64_t ldc,
+                                               float* __restrict__ db, int64_t gid) {
   const int64_t ne = (int64_t)T * TN_T * TN_T;
   if (gid < ne) {
     const int tile = (int)(gid / (TN_T * TN_T)), e = (int)(gid % (TN_T * TN_T));
@@ -580,6 +579,118 @@ __global__ __launch_bounds__(256) void k_tn_reduce(const float* __restrict__ par
   db[i] = sum;
 }
 
+__global__ __launch_bounds__(256) void k_tn_reduce(const float* __restrict__ parts,
+                                                   const float* __restrict__ dbparts, int S,
+                                                   int T, int KT, int NT, int N, int K,
+                                                   float* __restrict__ C, int64_t ldc,
+                                                   float* __restrict__ db) {
+  tn_reduce_item(parts, dbparts, S, T, KT, NT, N, K, C, ldc, db,
+                 (int64_t)blockIdx.x * 256 + threadIdx.x);
+}
+
+// Several GEMMs' split sums in one launch (tt_gemm_tn_reduce_many): job i owns the global
+// items [start_i, start_{i+1}); the same per-item code and order as k_tn_reduce.
+constexpr int TN_RED_MAX = 8;
+struct TnRedJob {
+  const float* parts;
+  const float* dbparts;
+  float* C;
+  float* db;
+  int64_t ldc, start;
+  int S, T, KT, NT, N, K;
+};
+struct TnRedArgs {
+  TnRedJob j[TN_RED_MAX];
+  int n;
+};
+__global__ __launch_bounds__(256) void k_tn_reduce_many(TnRedArgs a) {
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int i = 0;
+#pragma unroll
+  for (int u = 1; u < TN_RED_MAX; ++u)
+    if (u < a.n && gid >= a.j[u].start) i = u;
+  const TnRedJob& J = a.j[i];
+  tn_reduce_item(J.parts, J.dbparts, J.S, J.T, J.KT, J.NT, J.N, J.K, J.C, J.ldc, J.db,
+                 gid - J.start);
+}
+
+// The training step's backward tail in ONE launch (tt_train_bwd_tail): blocks [0, nA) sum the
+// deferred weight-gradient splits (k_tn_reduce_many's items), the next nB blocks the attention
+// pooling's per-buyer dW2 / db2 parts (k_attn_bwd_reduce's order: 8 row groups, each summed in
+// row order, then the groups in order -- the same bits), the rest scatter the embedding-row
+// gradients (k_embedding_bwd2, one wave per row, atomics).
+struct TailArgs {
+  TnRedArgs tn;
+  int64_t tn_items;
+  int nA, nB;
+  const float* part;  // attention parts [B][Hd + 1]
+  int B, Hd;
+  float *dW2, *db2;
+  const float* g;  // embedding rows' gradients [n][ldg]: brand at 0, cat at C
+  int64_t ldg, n;
+  const int32_t *ids0, *ids1;
+  int C;
+  float *grad0, *grad1;
+};
+__global__ __launch_bounds__(256) void k_train_tail(TailArgs a) {
+  const int bx = blockIdx.x, tid = threadIdx.x;
+  if (bx < a.nA) {
+    const int64_t gid = (int64_t)bx * 256 + tid;
+    if (gid >= a.tn_items) return;
+    int i = 0;
+#pragma unroll
+    for (int u = 1; u < TN_RED_MAX; ++u)
+      if (u < a.tn.n && gid >= a.tn.j[u].start) i = u;
+    const TnRedJob& J = a.tn.j[i];
+    tn_reduce_item(J.parts, J.dbparts, J.S, J.T, J.KT, J.NT, J.N, J.K, J.C, J.ldc, J.db,
+                   gid - J.start);
+    return;
+  }
+  if (bx < a.nA + a.nB) {
+    __shared__ float gs[8][32];
+    const int g = tid >> 5, cl = tid & 31;
+    const int c = (bx - a.nA) * 32 + cl, Hd = a.Hd, B = a.B;
+    const int per = (B + 7) / 8, r0 = g * per, r1 = min(B, r0 + per);
+    float sacc = 0.0f;
+    if (c <= Hd) {
+      for (int rb = r0; rb < r1; rb += 32) {
+        float v[32];
+#pragma unroll
+        for (int u = 0; u < 32; ++u)
+          v[u] = rb + u < r1 ? a.part[(int64_t)(rb + u) * (Hd + 1) + c] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < 32; ++u) sacc += v[u];
+      }
+    }
+    gs[g][cl] = sacc;
+    __syncthreads();
+    if (g == 0 && c <= Hd) {
+      float t = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t += gs[i][cl];
+      if (c < Hd) a.dW2[c] = t;
+      else *a.db2 = t;
+    }
+    return;
+  }
+  const int64_t rr = (int64_t)(bx - a.nA - a.nB) * 4 + (tid >> 6), lane = tid & 63;
+  if (rr >= 2 * a.n) return;
+  const bool second = rr >= a.n;
+  const int64_t r = second ? rr - a.n : rr;
+  const int32_t* ids = second ? a.ids1 : a.ids0;
+  if (ids == nullptr) return;
+  const int id = ids[r];
+  if (id <= 0) return;  // padding_idx 0 gets no gradient
+  float* tg = second ? a.grad1 : a.grad0;
+  const float* gr = a.g + r * a.ldg + (second ? a.C : 0);
+  for (int c = (int)lane; c < a.C; c += 64) atomicAdd(&tg[(int64_t)id * a.C + c], gr[c]);
+}
+
+#ifndef TT_TN_BLOCKS
+#define TT_TN_BLOCKS 1024  // blocks a split plan aims at (~4 per CU: the k-loop is latency-bound)
+#endif
+TT_CHECK_EXP(TT_TN_BLOCKS != 1024, "TT_TN_BLOCKS");
+constexpr int TN_TARGET_BLOCKS = TT_TN_BLOCKS;
 struct TnPlan {
   int NT, KT, S, mc;
   size_t parts, dbparts, total;
@@ -589,7 +700,7 @@ TnPlan tn_plan(int64_t M, int N, int K) {
   p.NT = (N + TN_T - 1) / TN_T;
   p.KT = (K + TN_T - 1) / TN_T;
   const int T = p.NT * p.KT;
-  int64_t S = (1024 + T - 1) / T;  // ~4 blocks per CU: the k-loop is latency-bound
+  int64_t S = (TN_TARGET_BLOCKS + T - 1) / T;
   const int64_t maxS = (M + TN_T - 1) / TN_T;
   if (S > maxS) S = maxS;
   if (S > TN_SMAX) S = TN_SMAX;
@@ -673,6 +784,7 @@ __global__ void k_relu_drop_bwd(float* __restrict__ dh, const float* __restrict_
   }
 }
 
+constexpr int CV_RG = 4;  // row groups of 8 per non-transposed convert tile (32 rows)
 struct tt_convert_batch_args {
   tt_convert_job jobs[TT_CONVERT_MAX_JOBS];
   int tile_off[TT_CONVERT_MAX_JOBS];
@@ -688,39 +800,45 @@ __global__ __launch_bounds__(256) void k_convert_batch(tt_convert_batch_args a) 
   const tt_convert_job& jb = a.jobs[j];
   const int t = (int)blockIdx.x - a.tile_off[j];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  if (!jb.transpose) {  // 8 x 128 tiles, 4 consecutive elements per thread
+  if (!jb.transpose) {  // 32 x 128 tiles: 4 row groups of 8, 4 consecutive elements per thread
     const int ct = (jb.cols + 127) / 128;
-    const int r = (t / ct) * 8 + ty, c = (t % ct) * 128 + 4 * tx;
-    if (r >= jb.rows || c >= jb.cols) return;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    const int c = (t % ct) * 128 + 4 * tx;
+    if (c >= jb.cols) return;
     const bool full = c + 4 <= jb.cols;
-    if (jb.src) {
-      const float* sp = jb.src + (int64_t)r * jb.ld_src + c;
-      if (full && ((uintptr_t)sp % 16) == 0) {
-        const f32x4 q = *(const f32x4*)sp;
-        v[0] = q[0], v[1] = q[1], v[2] = q[2], v[3] = q[3];
-      } else {
-        for (int u = 0; u < 4; ++u)
-          if (c + u < jb.cols) v[u] = sp[u];
+#pragma unroll
+    for (int k = 0; k < CV_RG; ++k) {
+      const int r = (t / ct) * (8 * CV_RG) + 8 * k + ty;
+      if (r >= jb.rows) break;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      const int sr = jb.row_ids ? jb.row_ids[r] : r;  // (gathered rows: a negative id is zeros)
+      if (jb.src && sr >= 0) {
+        const float* sp = jb.src + (int64_t)sr * jb.ld_src + c;
+        if (full && ((uintptr_t)sp % 16) == 0) {
+          const f32x4 q = *(const f32x4*)sp;
+          v[0] = q[0], v[1] = q[1], v[2] = q[2], v[3] = q[3];
+        } else {
+          for (int u = 0; u < 4; ++u)
+            if (c + u < jb.cols) v[u] = sp[u];
+        }
       }
-    }
-    if (jb.to_bf16) {
-      uint16_t* dp = (uint16_t*)jb.dst + (int64_t)r * jb.ld_dst + c;
-      if (full && ((uintptr_t)dp % 8) == 0) {
-        *(tn_u32x2*)dp = tn_u32x2{
-            (uint32_t)f32_to_bf16_rne(v[0]) | ((uint32_t)f32_to_bf16_rne(v[1]) << 16),
-            (uint32_t)f32_to_bf16_rne(v[2]) | ((uint32_t)f32_to_bf16_rne(v[3]) << 16)};
+      if (jb.to_bf16) {
+        uint16_t* dp = (uint16_t*)jb.dst + (int64_t)r * jb.ld_dst + c;
+        if (full && ((uintptr_t)dp % 8) == 0) {
+          *(tn_u32x2*)dp = tn_u32x2{
+              (uint32_t)f32_to_bf16_rne(v[0]) | ((uint32_t)f32_to_bf16_rne(v[1]) << 16),
+              (uint32_t)f32_to_bf16_rne(v[2]) | ((uint32_t)f32_to_bf16_rne(v[3]) << 16)};
+        } else {
+          for (int u = 0; u < 4; ++u)
+            if (c + u < jb.cols) dp[u] = f32_to_bf16_rne(v[u]);
+        }
       } else {
-        for (int u = 0; u < 4; ++u)
-          if (c + u < jb.cols) dp[u] = f32_to_bf16_rne(v[u]);
-      }
-    } else {
-      float* dp = (float*)jb.dst + (int64_t)r * jb.ld_dst + c;
-      if (full && ((uintptr_t)dp % 16) == 0) {
-        *(f32x4*)dp = f32x4{v[0], v[1], v[2], v[3]};
-      } else {
-        for (int u = 0; u < 4; ++u)
-          if (c + u < jb.cols) dp[u] = v[u];
+        float* dp = (float*)jb.dst + (int64_t)r * jb.ld_dst + c;
+        if (full && ((uintptr_t)dp % 16) == 0) {
+          *(f32x4*)dp = f32x4{v[0], v[1], v[2], v[3]};
+        } else {
+          for (int u = 0; u < 4; ++u)
+            if (c + u < jb.cols) dp[u] = v[u];
+        }
       }
     }
     return;
@@ -833,18 +951,20 @@ namespace {
 int attn_pool_bwd(const float* dz, int64_t lddz, const float* z, int64_t ldz, const float* onorm,
                   const float* alpha, const float* w, const float* x, int64_t B, int32_t S,
                   int32_t E, const float* H, const float* W2, int32_t Hd, float* dW2, float* db2,
-                  float* dH, float* da_ws, bool relu_mask, bool fused, void* stream) {
+                  float* dH, float* da_ws, bool relu_mask, bool fused, void* stream,
+                  bool parts_only = false) {
   TT_REQUIRE(B >= 0 && S >= 1 && S <= 128 && E >= 1 && E <= 1024 && Hd >= 1,
              "need 1 <= S <= 128, 1 <= E <= 1024");
   if (B == 0) return TT_OK;
-  TT_REQUIRE(dz && z && onorm && alpha && w && x && H && W2 && dW2 && db2 && dH && da_ws,
+  TT_REQUIRE(dz && z && onorm && alpha && w && x && H && W2 && (parts_only || (dW2 && db2)) &&
+                 dH && da_ws,
              "null pointer");
   hipStream_t st = (hipStream_t)stream;
   float* part = fused ? da_ws + (B * S + 63) / 64 * 64 : nullptr;  // [B][Hd + 1] after da
   hipLaunchKernelGGL(k_attn_pool_bwd<512>, dim3((unsigned)B), dim3(512), 0, st, dz, lddz, z, ldz,
                      onorm, alpha, w, x, S, E, W2, Hd, da_ws, dH, H, relu_mask, part);
   int rc = check_launch("k_attn_pool_bwd");
-  if (rc) return rc;
+  if (rc || parts_only) return rc;
   if (fused) {
     hipLaunchKernelGGL(k_attn_bwd_reduce, dim3((unsigned)((Hd + 1 + 127) / 128)), dim3(1024), 0,
                        st, part, (int)B, Hd, dW2, db2);
@@ -880,6 +1000,16 @@ extern "C" int tt_attn_pool_bwd_relu_f32(const float* dz, int64_t lddz, const fl
                        da_ws, true, true, stream);
 }
 
+extern "C" int tt_attn_pool_bwd_relu_parts_f32(const float* dz, int64_t lddz, const float* z,
+                                               int64_t ldz, const float* onorm,
+                                               const float* alpha, const float* w,
+                                               const float* x, int64_t B, int32_t S, int32_t E,
+                                               const float* H, const float* W2, int32_t Hd,
+                                               float* dH, float* da_ws, void* stream) {
+  return attn_pool_bwd(dz, lddz, z, ldz, onorm, alpha, w, x, B, S, E, H, W2, Hd, nullptr,
+                       nullptr, dH, da_ws, true, true, stream, true);
+}
+
 extern "C" int tt_embedding_backward_f32(const float* g, int64_t ldg, const int32_t* ids,
                                          int64_t n, int32_t C, float* table_grad, void* stream) {
   TT_REQUIRE(n >= 0 && C >= 1, "bad sizes");
@@ -896,9 +1026,12 @@ extern "C" int tt_gemm_tn_workspace_bytes(int64_t M, int32_t N, int32_t K, int64
   return TT_OK;
 }
 
-extern "C" int tt_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M,
-                          int32_t N, int32_t K, int32_t prec, float* C, int64_t ldc, float* db,
-                          void* workspace, int64_t workspace_bytes, void* stream) {
+namespace {
+// the GEMM launch of tt_gemm_tn; *pending = 1 when its split sums still have to be reduced
+int gemm_tn_launch(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M,
+                   int32_t N, int32_t K, int32_t prec, float* C, int64_t ldc, float* db,
+                   void* workspace, int64_t workspace_bytes, void* stream, int* pending) {
+  *pending = 0;
   TT_REQUIRE(M >= 0 && N >= 0 && K >= 0 && M <= 0x7fffffffLL, "bad sizes");
   TT_REQUIRE(prec == TT_PREC_F32 || prec == TT_PREC_BF16, "prec must be TT_PREC_F32 / BF16");
   if (N == 0 || K == 0) return TT_OK;
@@ -926,12 +1059,107 @@ extern "C" int tt_gemm_tn(const float* A, int64_t lda, const float* B, int64_t l
     hipLaunchKernelGGL(k_gemm_tn<false>, grid, dim3(256), 0, st, A, lda, B, ldb, (int)M, N, K,
                        p.mc, C, ldc, db, parts, dbparts);
   int rc = check_launch("k_gemm_tn");
-  if (rc || p.S == 1) return rc;
+  if (!rc) *pending = p.S > 1;
+  return rc;
+}
+}  // namespace
+
+extern "C" int tt_gemm_tn(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M,
+                          int32_t N, int32_t K, int32_t prec, float* C, int64_t ldc, float* db,
+                          void* workspace, int64_t workspace_bytes, void* stream) {
+  int pending = 0;
+  int rc = gemm_tn_launch(A, lda, B, ldb, M, N, K, prec, C, ldc, db, workspace, workspace_bytes,
+                          stream, &pending);
+  if (rc || !pending) return rc;
+  const TnPlan p = tn_plan(M, N, K);
   const int T = p.NT * p.KT;
   const int64_t items = (int64_t)T * TN_T * TN_T + (db ? N : 0);
-  hipLaunchKernelGGL(k_tn_reduce, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, parts,
-                     dbparts, p.S, T, p.KT, p.NT, N, K, C, ldc, db);
+  char* ws = (char*)workspace;
+  hipLaunchKernelGGL(k_tn_reduce, dim3((unsigned)((items + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, (const float*)(ws + p.parts),
+                     (const float*)(ws + p.dbparts), p.S, T, p.KT, p.NT, N, K, C, ldc, db);
   return check_launch("k_tn_reduce");
+}
+
+extern "C" int tt_gemm_tn_partial(const float* A, int64_t lda, const float* B, int64_t ldb,
+                                  int64_t M, int32_t N, int32_t K, int32_t prec, float* C,
+                                  int64_t ldc, float* db, void* workspace,
+                                  int64_t workspace_bytes, void* stream) {
+  int pending = 0;
+  return gemm_tn_launch(A, lda, B, ldb, M, N, K, prec, C, ldc, db, workspace, workspace_bytes,
+                        stream, &pending);
+}
+
+namespace {
+int fill_tn_jobs(const tt_tn_pending* jobs, int32_t n, TnRedArgs& a, int64_t* total_out) {
+  TT_REQUIRE(n >= 0 && n <= TN_RED_MAX && (n == 0 || jobs), "0 <= n <= 8 jobs");
+  int64_t total = 0;
+  for (int i = 0; i < n; ++i) {
+    const tt_tn_pending& q = jobs[i];
+    TT_REQUIRE(q.M >= 0 && q.N >= 0 && q.K >= 0, "bad sizes");
+    if (q.M == 0 || q.N == 0 || q.K == 0) continue;
+    const TnPlan p = tn_plan(q.M, q.N, q.K);
+    if (p.S == 1) continue;  // (that GEMM wrote C directly)
+    TT_REQUIRE(q.workspace && q.C, "null workspace / C");
+    TnRedJob& J = a.j[a.n++];
+    const char* ws = (const char*)q.workspace;
+    J.parts = (const float*)(ws + p.parts);
+    J.dbparts = (const float*)(ws + p.dbparts);
+    J.C = q.C;
+    J.db = q.db;
+    J.ldc = q.ldc;
+    J.start = total;
+    J.S = p.S;
+    J.T = p.NT * p.KT;
+    J.KT = p.KT;
+    J.NT = p.NT;
+    J.N = q.N;
+    J.K = q.K;
+    total += (int64_t)J.T * TN_T * TN_T + (q.db ? q.N : 0);
+  }
+  *total_out = total;
+  return TT_OK;
+}
+}  // namespace
+
+extern "C" int tt_gemm_tn_reduce_many(const tt_tn_pending* jobs, int32_t n, void* stream) {
+  TnRedArgs a{};
+  int64_t total = 0;
+  int rc = fill_tn_jobs(jobs, n, a, &total);
+  if (rc) return rc;
+  if (a.n == 0) return TT_OK;
+  hipLaunchKernelGGL(k_tn_reduce_many, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, a);
+  return check_launch("k_tn_reduce_many");
+}
+
+extern "C" int tt_train_bwd_tail(const tt_tn_pending* jobs, int32_t njobs,
+                                 const float* attn_parts, int64_t B, int32_t Hd, float* dW2,
+                                 float* db2, const float* g_emb, int64_t ldg,
+                                 const int32_t* ids0, const int32_t* ids1, int64_t n_emb,
+                                 int32_t C, float* grad0, float* grad1, void* stream) {
+  TailArgs a{};
+  int rc = fill_tn_jobs(jobs, njobs, a.tn, &a.tn_items);
+  if (rc) return rc;
+  a.nA = (int)((a.tn_items + 255) / 256);
+  TT_REQUIRE(B >= 0 && Hd >= 0 && n_emb >= 0 && C >= 0, "bad sizes");
+  if (attn_parts && B > 0) {
+    TT_REQUIRE(dW2 && db2 && Hd >= 1, "attention: null dW2 / db2");
+    a.part = attn_parts, a.B = (int)B, a.Hd = Hd, a.dW2 = dW2, a.db2 = db2;
+    a.nB = (Hd + 1 + 31) / 32;
+  }
+  int nC = 0;
+  if (g_emb && n_emb > 0 && (ids0 || ids1)) {
+    TT_REQUIRE(C >= 1 && ldg >= 2 * C && (!ids0 || grad0) && (!ids1 || grad1),
+               "embedding: bad ldg / null grads");
+    a.g = g_emb, a.ldg = ldg, a.n = n_emb, a.ids0 = ids0, a.ids1 = ids1, a.C = C;
+    a.grad0 = grad0, a.grad1 = grad1;
+    nC = (int)((2 * n_emb + 3) / 4);
+  }
+  const int64_t blocks = (int64_t)a.nA + a.nB + nC;
+  if (blocks == 0) return TT_OK;
+  hipLaunchKernelGGL(k_train_tail, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("k_train_tail");
 }
 
 extern "C" int tt_dropout_apply_ex(float* x, const uint8_t* keep, float scale, int64_t n,
@@ -979,7 +1207,7 @@ extern "C" int tt_relu_dropout_backward_f32(float* dh, const float* h, float sca
 }
 
 extern "C" int tt_convert_batch(const tt_convert_job* jobs, int32_t njobs, void* stream) {
-  TT_REQUIRE(jobs && njobs >= 0 && njobs <= TT_CONVERT_MAX_JOBS, "need 0 <= njobs <= 8");
+  TT_REQUIRE(jobs && njobs >= 0 && njobs <= TT_CONVERT_MAX_JOBS, "need 0 <= njobs <= 16");
   tt_convert_batch_args a{};
   int tiles = 0, nj = 0;
   for (int j = 0; j < njobs; ++j) {
@@ -987,6 +1215,7 @@ extern "C" int tt_convert_batch(const tt_convert_job* jobs, int32_t njobs, void*
     TT_REQUIRE(jb.dst && jb.rows >= 0 && jb.cols >= 0 && (!jb.src || jb.ld_src >= jb.cols),
                "bad job");
     TT_REQUIRE(jb.src || !jb.transpose, "a zero-fill job (src NULL) cannot transpose");
+    TT_REQUIRE(!jb.row_ids || !jb.transpose, "a gather job (row_ids) cannot transpose");
     TT_REQUIRE(jb.transpose ? jb.ld_dst >= jb.rows : jb.ld_dst >= jb.cols, "bad job ld_dst");
     if (jb.rows == 0 || jb.cols == 0) continue;
     a.jobs[nj] = jb;
@@ -995,7 +1224,7 @@ extern "C" int tt_convert_batch(const tt_convert_job* jobs, int32_t njobs, void*
       const int64_t rr = jb.ld_dst > jb.rows ? jb.ld_dst : jb.rows;
       tiles += (int)(((rr + 31) / 32) * ((jb.cols + 31) / 32));
     } else {
-      tiles += (int)(((jb.rows + 7) / 8) * ((jb.cols + 127) / 128));
+      tiles += (int)(((jb.rows + 8 * CV_RG - 1) / (8 * CV_RG)) * ((jb.cols + 127) / 128));
     }
     ++nj;
   }

@@ -57,7 +57,13 @@ class BertModel(ctypes.Structure):
 class ConvertJob(ctypes.Structure):
     """tt_convert_job (include/twotower_hip.h): one operand copy of tt_convert_batch."""
     _fields_ = [("src", _vp), ("ld_src", _i64), ("rows", _i32), ("cols", _i32), ("dst", _vp),
-                ("ld_dst", _i64), ("transpose", _i32), ("to_bf16", _i32)]
+                ("ld_dst", _i64), ("transpose", _i32), ("to_bf16", _i32), ("row_ids", _vp)]
+
+
+class TnPending(ctypes.Structure):
+    """tt_tn_pending (include/twotower_hip.h): one deferred tt_gemm_tn_partial reduce."""
+    _fields_ = [("workspace", _vp), ("M", _i64), ("N", _i32), ("K", _i32), ("C", _vp),
+                ("ldc", _i64), ("db", _vp)]
 
 
 # name -> (restype, argtypes); mirrors include/twotower_hip.h
@@ -182,6 +188,14 @@ SIGNATURES = {
                                                  _i32, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _vp,
                                                  _vp]),
     "tt_gemm_tn_workspace_bytes": (ctypes.c_int, [_i64, _i32, _i32, ctypes.POINTER(_i64)]),
+    "tt_gemm_tn_partial": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32, _vp,
+                                          _i64, _vp, _vp, _i64, _vp]),
+    "tt_gemm_tn_reduce_many": (ctypes.c_int, [_vp, _i32, _vp]),
+    "tt_train_bwd_tail": (ctypes.c_int, [_vp, _i32, _vp, _i64, _i32, _vp, _vp, _vp, _i64, _vp,
+                                         _vp, _i64, _i32, _vp, _vp, _vp]),
+    "tt_attn_pool_bwd_relu_parts_f32": (ctypes.c_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp,
+                                                       _i64, _i32, _i32, _vp, _vp, _i32, _vp,
+                                                       _vp, _vp]),
     "tt_gemm_tn": (ctypes.c_int, [_vp, _i64, _vp, _i64, _i64, _i32, _i32, _i32, _vp, _i64, _vp,
                                   _vp, _i64, _vp]),
     "tt_dropout_apply_ex": (ctypes.c_int, [_vp, _vp, ctypes.c_float, _i64, _vp, _vp]),

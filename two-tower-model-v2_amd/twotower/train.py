@@ -261,21 +261,40 @@ class TwoTowerTrainStep:
         b.dh = e(R, hid)
         b.dh16 = e(R, hid, dt=bf) if (bf16 and use_cat) else None
         b.dxc = e(R, 2 * C) if use_cat else None
-        tn = 0
-        for M_, N_, K_ in ((R, E, hid), (R, hid, width)) + (((B * S, b.Hd, E),)
-                                                           if self.attention else ()):
+        # one workspace per weight-gradient GEMM: their split sums wait for ONE reduce launch
+        # at the end of the backward (tt_gemm_tn_partial + tt_gemm_tn_reduce_many)
+        G = self.g
+        tn_jobs = [((R, E, hid), "proj3"), ((R, hid, width), "proj0")]
+        if self.attention:
+            tn_jobs.append(((B * S, b.Hd, E), "att0"))
+        b.tn_ws, pend = [], []
+        for (M_, N_, K_), name in tn_jobs:
             v = ctypes.c_int64(0)
             check(lib().tt_gemm_tn_workspace_bytes(M_, N_, K_, ctypes.byref(v)), "tn ws")
-            tn = max(tn, v.value)
-        b.tn_ws = torch.empty(max(tn, 256), dtype=torch.uint8, device=dev)
+            ws_ = torch.empty(max(v.value, 256), dtype=torch.uint8, device=dev)
+            b.tn_ws.append(ws_)
+            pend.append(_lib.TnPending(ctypes.c_void_p(ws_.data_ptr()), M_, N_, K_,
+                                       ctypes.c_void_p(G[name + ".w"].data_ptr()), K_,
+                                       ctypes.c_void_p(G[name + ".b"].data_ptr())))
+        b.tn_pend = (_lib.TnPending * len(pend))(*pend)
+        b.n_pend = len(pend)
         # weight-derived GEMM operands, refreshed by ONE tt_convert_batch per step
         W0, W3 = P["proj0.w"], P["proj3.w"]
         jobs = []
 
-        def job(src, rows, cols, ld_src, dst, ld_dst, transpose, to_bf16):
+        def job(src, rows, cols, ld_src, dst, ld_dst, transpose, to_bf16, ids=None, dst_off=0):
             jobs.append(_lib.ConvertJob(ctypes.c_void_p(src), ld_src, rows, cols,
-                                        ctypes.c_void_p(dst.data_ptr()), ld_dst, transpose,
-                                        to_bf16))
+                                        ctypes.c_void_p(dst.data_ptr() + dst_off), ld_dst,
+                                        transpose, to_bf16,
+                                        ctypes.c_void_p(ids.data_ptr()) if ids is not None
+                                        else None))
+        if use_cat:  # the item head's input [text | brand[bid] | cat[cid]] (+ its bf16 copy)
+            for dst, sz, bf_ in ((b.x, 4, 0),) + (((b.x16, 2, 1),) if bf16 else ()):
+                job(b.text.data_ptr(), R, Ht, Ht, dst, width, 0, bf_)
+                job(P["brand"].data_ptr() if has_b else None, R, C, C, dst, width, 0, bf_,
+                    ids=b.bids, dst_off=sz * Ht)
+                job(P["cat"].data_ptr() if has_c else None, R, C, C, dst, width, 0, bf_,
+                    ids=b.cids, dst_off=sz * (Ht + C))
         b.W3T = e(hid, E, dt=bf if bf16 else f32)
         job(W3.data_ptr(), E, hid, hid, b.W3T, E, 1, int(bf16))
         b.W0cT = e(2 * C, hid, dt=bf if bf16 else f32) if use_cat else None
@@ -389,15 +408,9 @@ class TwoTowerTrainStep:
         P, L, st = self.params, lib(), stream_ptr()
         bf16 = self.prec == "bf16"
         R, C, width, hid = bb.R, bb.C, bb.width, bb.hid
-        # forward: [text | brand | cat] (+ bf16 copy for the bf16 GEMM)
-        if use_cat:
-            check(L.tt_item_concat(bb.text.data_ptr(), Ht, Ht, _p(bb.bids),
-                                   _p(P["brand"]) if has_b else None, _p(bb.cids),
-                                   _p(P["cat"]) if has_c else None, C, R, bb.x.data_ptr(),
-                                   width, _p(bb.x16), st), "concat")
-            x_in = bb.x
-        else:
-            x_in = bb.text
+        # forward: [text | brand | cat] (+ bf16 copy for the bf16 GEMM) -- jobs of the step's
+        # one tt_convert_batch launch, with the weight-derived GEMM operands
+        x_in = bb.x if use_cat else bb.text
         if bb.njobs:
             check(L.tt_convert_batch(bb.jobs, bb.njobs, st), "convert_batch")
         rng_drop = pdrop > 0 and self.keep_fn is dropout_keep  # (a custom keep_fn: its mask)
@@ -463,13 +476,13 @@ class TwoTowerTrainStep:
               "tt_infonce_ex")
         if not grads:
             return
-        G, ws = self.g, bb.tn_ws
+        G, ws3, ws0 = self.g, bb.tn_ws[0], bb.tn_ws[1]
         # item head backward
         check(L.tt_l2norm_backward_ex(bb.y.data_ptr(), E, bb.z.data_ptr(), E, dzp, E, R, E,
                                       bb.dy.data_ptr(), E, _p(bb.dy16), E, st), "norm_bwd")
-        check(L.tt_gemm_tn(bb.dy.data_ptr(), E, bb.h.data_ptr(), hid, R, E, hid, pr,
-                           G["proj3.w"].data_ptr(), hid, G["proj3.b"].data_ptr(), ws.data_ptr(),
-                           ws.numel(), st), "dW3")
+        check(L.tt_gemm_tn_partial(bb.dy.data_ptr(), E, bb.h.data_ptr(), hid, R, E, hid, pr,
+                                   G["proj3.w"].data_ptr(), hid, G["proj3.b"].data_ptr(),
+                                   ws3.data_ptr(), ws3.numel(), st), "dW3")
         if bf16:  # dh = dy W3 (A W^T form with W = W3^T)
             check(L.tt_gemm_bf16(bb.dy16.data_ptr(), E, bb.W3T.data_ptr(), E, None, None, 0,
                                  bb.dh.data_ptr(), hid, None, 0, R, hid, E, 0, st), "gemm dh")
@@ -480,9 +493,10 @@ class TwoTowerTrainStep:
                                              bb.dh.numel(), _p(bb.dh16),
                                              _p(self._drop_ctr) if rng_drop else None, st),
               "relu_bwd")
-        check(L.tt_gemm_tn(bb.dh.data_ptr(), hid, x_in.data_ptr(), x_in.stride(0), R, hid,
-                           width, pr, G["proj0.w"].data_ptr(), width, G["proj0.b"].data_ptr(),
-                           ws.data_ptr(), ws.numel(), st), "dW0")
+        check(L.tt_gemm_tn_partial(bb.dh.data_ptr(), hid, x_in.data_ptr(), x_in.stride(0), R,
+                                   hid, width, pr, G["proj0.w"].data_ptr(), width,
+                                   G["proj0.b"].data_ptr(), ws0.data_ptr(), ws0.numel(), st),
+              "dW0")
         if use_cat:  # embedding-row gradients through dxc = dh W0[:, Ht:]
             if bf16:
                 check(L.tt_gemm_bf16(bb.dh16.data_ptr(), hid, bb.W0cT.data_ptr(), hid, None,
@@ -492,23 +506,31 @@ class TwoTowerTrainStep:
                 check(L.tt_gemm_f32(bb.dh.data_ptr(), hid, bb.W0cT.data_ptr(), hid, None, None,
                                     0, bb.dxc.data_ptr(), 2 * C, None, 0, R, 2 * C, hid, 0, st),
                       "gemm dxc")
-            # (brand / cat gradients zeroed by the step's tt_convert_batch)
-            check(L.tt_embedding_backward2_f32(bb.dxc.data_ptr(), 2 * C, _p(bb.bids), _p(bb.cids),
-                                               R, C, G["brand"].data_ptr(), G["cat"].data_ptr(),
-                                               st), "emb_bwd")
-        if not self.attention:
+            # (brand / cat gradients zeroed by the step's tt_convert_batch; scattered by the
+            # backward tail below)
+        emb = ((bb.dxc.data_ptr(), 2 * C, _p(bb.bids), _p(bb.cids), R, C, G["brand"].data_ptr(),
+                G["cat"].data_ptr()) if use_cat else (None, 0, None, None, 0, 0, None, None))
+        if not self.attention:  # the backward tail: weight-gradient reduces + embedding rows
+            check(L.tt_train_bwd_tail(bb.tn_pend, bb.n_pend, None, 0, 0, None, None, *emb, st),
+                  "bwd tail")
             return
         Hd = bb.Hd
-        check(L.tt_attn_pool_bwd_relu_f32(bb.gb.data_ptr(), E, bb.zb.data_ptr(), E,
-                                          bb.onorm.data_ptr(), bb.alpha.data_ptr(),
-                                          bb.w.data_ptr(), X.data_ptr(), B, S, E,
-                                          bb.Hb.data_ptr(), P["att2.w"].data_ptr(), Hd,
-                                          G["att2.w"].data_ptr(), G["att2.b"].data_ptr(),
-                                          bb.dHb.data_ptr(), bb.da.data_ptr(), st),
+        check(L.tt_attn_pool_bwd_relu_parts_f32(bb.gb.data_ptr(), E, bb.zb.data_ptr(), E,
+                                                bb.onorm.data_ptr(), bb.alpha.data_ptr(),
+                                                bb.w.data_ptr(), X.data_ptr(), B, S, E,
+                                                bb.Hb.data_ptr(), P["att2.w"].data_ptr(), Hd,
+                                                bb.dHb.data_ptr(), bb.da.data_ptr(), st),
               "attn_pool_bwd")
-        check(L.tt_gemm_tn(bb.dHb.data_ptr(), Hd, X.data_ptr(), E, B * S, Hd, E, pr,
-                           G["att0.w"].data_ptr(), E, G["att0.b"].data_ptr(), ws.data_ptr(),
-                           ws.numel(), st), "dWa0")
+        wsa = bb.tn_ws[2]
+        check(L.tt_gemm_tn_partial(bb.dHb.data_ptr(), Hd, X.data_ptr(), E, B * S, Hd, E, pr,
+                                   G["att0.w"].data_ptr(), E, G["att0.b"].data_ptr(),
+                                   wsa.data_ptr(), wsa.numel(), st), "dWa0")
+        # the backward tail, one launch: the three weight gradients' split sums, dW2 / db2
+        # from the attention pooling's per-buyer parts, the embedding-row gradients
+        parts = bb.da.data_ptr() + 4 * ((B * S + 63) // 64 * 64)
+        check(L.tt_train_bwd_tail(bb.tn_pend, bb.n_pend, ctypes.c_void_p(parts), B, Hd,
+                                  G["att2.w"].data_ptr(), G["att2.b"].data_ptr(), *emb, st),
+              "bwd tail")
 
     # torch.optim.Adam state dict (the reference saves optimizer.state_dict(), trainer.py:330):
     # 'state' indexed by the position of the parameter in model.parameters(), 'param_groups'
